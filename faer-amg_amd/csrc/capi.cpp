@@ -1,0 +1,622 @@
+// capi.cpp -- extern "C" boundary (include/amg.h).  Converts library
+// exceptions to amg_status + a thread-local message; handles are thin boxes
+// around shared_ptr<LinOp> so operators keep what they reference alive (the
+// reference's Arc<dyn LinOp> ownership, core.rs:9-17).
+#include <cmath>
+#include <cstring>
+#include <string>
+
+#include "famg.hpp"
+
+using namespace famg;
+
+struct amg_ctx {
+    Ctx ctx;
+    DevBuf<double> stage_in, stage_out;  // host-memory staging
+};
+
+struct amg_linop {
+    LinOpPtr op;
+};
+
+namespace {
+thread_local std::string g_last_error;
+
+amg_status set_err(amg_status s, const std::string &m) {
+    g_last_error = m;
+    return s;
+}
+
+template <typename F> amg_status guard(F &&f) {
+    try {
+        f();
+        g_last_error.clear();
+        return AMG_OK;
+    } catch (const AmgError &e) {
+        return set_err(e.status, e.what());
+    } catch (const std::bad_alloc &) {
+        return set_err(AMG_ERR_OOM, "host allocation failed");
+    } catch (const std::exception &e) {
+        return set_err(AMG_ERR_INVALID, e.what());
+    }
+}
+
+amg_linop *box(LinOpPtr p) { return new amg_linop{std::move(p)}; }
+
+LinOp &need(const amg_linop *h) {
+    FAMG_REQUIRE(h && h->op, AMG_ERR_INVALID, "null amg_linop handle");
+    return *h->op;
+}
+
+CsrPtr need_csr(const amg_linop *h) {
+    need(h);
+    auto p = std::dynamic_pointer_cast<CsrOp>(h->op);
+    FAMG_REQUIRE(p, AMG_ERR_INVALID, "operator is not a CSR matrix");
+    return p;
+}
+
+std::shared_ptr<MultigridOp> need_mg(const amg_linop *h) {
+    need(h);
+    auto p = std::dynamic_pointer_cast<MultigridOp>(h->op);
+    FAMG_REQUIRE(p, AMG_ERR_INVALID, "operator is not a multigrid");
+    return p;
+}
+
+amg_ctx *ctx_of(const LinOp &op) {
+    // Ctx is the first member of amg_ctx
+    return reinterpret_cast<amg_ctx *>(op.ctx);
+}
+
+// Run f(out_col, rhs_col) for each of k columns, staging host memory.
+template <typename F>
+void for_columns(LinOp &op, double *out, int64_t ld_out, const double *rhs, int64_t ld_rhs,
+                 int64_t k, amg_mem mem, int64_t out_rows, int64_t rhs_rows, F &&f) {
+    FAMG_REQUIRE(k >= 0, AMG_ERR_INVALID, "negative column count");
+    if (k == 0) return;
+    FAMG_REQUIRE(out && rhs, AMG_ERR_INVALID, "null vector");
+    FAMG_REQUIRE(ld_out >= out_rows && ld_rhs >= rhs_rows, AMG_ERR_INVALID, "leading dimension too small");
+    Ctx &ctx = *op.ctx;
+    ctx.set_device();
+    if (mem == AMG_MEM_DEVICE) {
+        for (int64_t c = 0; c < k; c++) f(out + c * ld_out, rhs + c * ld_rhs);
+        return;
+    }
+    FAMG_REQUIRE(mem == AMG_MEM_HOST, AMG_ERR_INVALID, "bad amg_mem");
+    amg_ctx *ac = ctx_of(op);
+    if (ac->stage_in.size() < (size_t)rhs_rows) ac->stage_in.resize(rhs_rows);
+    if (ac->stage_out.size() < (size_t)out_rows) ac->stage_out.resize(out_rows);
+    for (int64_t c = 0; c < k; c++) {
+        FAMG_CHECK_HIP(hipMemcpyAsync(ac->stage_in.get(), rhs + c * ld_rhs, rhs_rows * sizeof(double),
+                                      hipMemcpyHostToDevice, ctx.stream));
+        f(ac->stage_out.get(), ac->stage_in.get());
+        FAMG_CHECK_HIP(hipMemcpyAsync(out + c * ld_out, ac->stage_out.get(), out_rows * sizeof(double),
+                                      hipMemcpyDeviceToHost, ctx.stream));
+        FAMG_CHECK_HIP(hipStreamSynchronize(ctx.stream));
+    }
+}
+
+}  // namespace
+
+extern "C" {
+
+const char *amg_last_error(void) { return g_last_error.c_str(); }
+const char *amg_version(void) { return "faer-amg_amd 0.1.0 (gfx950)"; }
+
+amg_status amg_ctx_create(int device, void *hip_stream, amg_ctx **out) {
+    return guard([&] {
+        FAMG_REQUIRE(out, AMG_ERR_INVALID, "null output pointer");
+        int ndev = 0;
+        FAMG_CHECK_HIP(hipGetDeviceCount(&ndev));
+        FAMG_REQUIRE(device >= 0 && device < ndev, AMG_ERR_INVALID, "device index out of range");
+        auto *c = new amg_ctx();
+        c->ctx.device = device;
+        try {
+            c->ctx.set_device();
+            if (hip_stream) {
+                c->ctx.stream = static_cast<hipStream_t>(hip_stream);
+            } else {
+                FAMG_CHECK_HIP(hipStreamCreateWithFlags(&c->ctx.stream, hipStreamNonBlocking));
+                c->ctx.own_stream = true;
+            }
+            hipDeviceProp_t prop;
+            FAMG_CHECK_HIP(hipGetDeviceProperties(&prop, device));
+            c->ctx.num_cus = prop.multiProcessorCount;
+        } catch (...) {
+            delete c;
+            throw;
+        }
+        *out = c;
+    });
+}
+
+amg_status amg_ctx_destroy(amg_ctx *ctx) {
+    return guard([&] {
+        if (!ctx) return;
+        ctx->ctx.set_device();
+        if (ctx->ctx.stream) (void)hipStreamSynchronize(ctx->ctx.stream);
+        delete ctx;
+    });
+}
+
+amg_status amg_ctx_synchronize(amg_ctx *ctx) {
+    return guard([&] {
+        FAMG_REQUIRE(ctx, AMG_ERR_INVALID, "null context");
+        ctx->ctx.set_device();
+        FAMG_CHECK_HIP(hipStreamSynchronize(ctx->ctx.stream));
+    });
+}
+
+amg_status amg_ctx_stream(amg_ctx *ctx, void **hip_stream) {
+    return guard([&] {
+        FAMG_REQUIRE(ctx && hip_stream, AMG_ERR_INVALID, "null argument");
+        *hip_stream = ctx->ctx.stream;
+    });
+}
+
+// ------------------------------------------------------------------ CSR
+
+amg_status amg_csr_create(amg_ctx *ctx, int64_t nrows, int64_t ncols, const int64_t *rowptr,
+                          const int64_t *colidx, const double *vals, amg_linop **out) {
+    return guard([&] {
+        FAMG_REQUIRE(ctx && out, AMG_ERR_INVALID, "null argument");
+        FAMG_REQUIRE(nrows >= 0 && ncols >= 0, AMG_ERR_INVALID, "negative dimension");
+        ctx->ctx.set_device();
+        auto p = make_csr(&ctx->ctx);
+        csr_from_host(p->m, &ctx->ctx, nrows, ncols, rowptr, colidx, vals);
+        p->nrows = nrows;
+        p->ncols = ncols;
+        *out = box(p);
+    });
+}
+
+__attribute__((visibility("default"))) amg_status amg_csr_create_device_i32(
+    amg_ctx *ctx, int64_t nrows, int64_t ncols, const int32_t *rowptr, const int32_t *colidx,
+    const double *vals, amg_linop **out) {
+    return guard([&] {
+        FAMG_REQUIRE(ctx && out && rowptr, AMG_ERR_INVALID, "null argument");
+        ctx->ctx.set_device();
+        hipStream_t s = ctx->ctx.stream;
+        std::vector<int32_t> rp32(nrows + 1);
+        FAMG_CHECK_HIP(hipMemcpyAsync(rp32.data(), rowptr, (nrows + 1) * sizeof(int32_t), hipMemcpyDeviceToHost, s));
+        FAMG_CHECK_HIP(hipStreamSynchronize(s));
+        std::vector<int64_t> rp(rp32.begin(), rp32.end());
+        const int64_t nnz = rp[nrows];
+        auto p = make_csr(&ctx->ctx);
+        csr_alloc(p->m, &ctx->ctx, nrows, ncols, nnz);
+        FAMG_CHECK_HIP(hipMemcpyAsync(p->m.rp64.get(), rp.data(), (nrows + 1) * sizeof(int64_t), hipMemcpyHostToDevice, s));
+        if (nnz) {
+            FAMG_CHECK_HIP(hipMemcpyAsync(p->m.col.get(), colidx, nnz * sizeof(int32_t), hipMemcpyDeviceToDevice, s));
+            FAMG_CHECK_HIP(hipMemcpyAsync(p->m.val.get(), vals, nnz * sizeof(double), hipMemcpyDeviceToDevice, s));
+        }
+        FAMG_CHECK_HIP(hipStreamSynchronize(s));
+        csr_finalize(p->m);
+        p->nrows = nrows;
+        p->ncols = ncols;
+        *out = box(p);
+    });
+}
+
+amg_status amg_csr_nnz(const amg_linop *op, int64_t *nnz) {
+    return guard([&] {
+        FAMG_REQUIRE(nnz, AMG_ERR_INVALID, "null argument");
+        *nnz = need_csr(op)->m.nnz;
+    });
+}
+
+amg_status amg_csr_download(const amg_linop *op, int64_t *rowptr, int64_t *colidx, double *vals) {
+    return guard([&] {
+        auto p = need_csr(op);
+        FAMG_REQUIRE(rowptr && (p->m.nnz == 0 || (colidx && vals)), AMG_ERR_INVALID, "null array");
+        p->ctx->set_device();
+        csr_to_host(p->m, rowptr, colidx, vals);
+    });
+}
+
+amg_status amg_gen_laplace3d_7pt(amg_ctx *ctx, int64_t nx, int64_t ny, int64_t nz, amg_linop **out) {
+    return guard([&] {
+        FAMG_REQUIRE(ctx && out, AMG_ERR_INVALID, "null argument");
+        ctx->ctx.set_device();
+        static const int offs[21] = {0, 0, -1, 0, -1, 0, -1, 0, 0, 0, 0, 0, 1, 0, 0, 0, 1, 0, 0, 0, 1};
+        static const double coef[7] = {-1.0, -1.0, -1.0, 6.0, -1.0, -1.0, -1.0};
+        auto p = make_csr(&ctx->ctx);
+        gen_stencil(p->m, &ctx->ctx, nx, ny, nz, offs, coef, 7);
+        p->nrows = p->ncols = p->m.nrows;
+        *out = box(p);
+    });
+}
+
+amg_status amg_gen_aniso27(amg_ctx *ctx, int64_t nx, int64_t ny, int64_t nz, double ex, double ey,
+                           double ez, amg_linop **out) {
+    return guard([&] {
+        FAMG_REQUIRE(ctx && out, AMG_ERR_INVALID, "null argument");
+        ctx->ctx.set_device();
+        const double T[3] = {-1.0, 2.0, -1.0};
+        const double M[3] = {1.0 / 6.0, 4.0 / 6.0, 1.0 / 6.0};
+        int offs[81];
+        double coef[27];
+        int k = 0;
+        for (int dz = 0; dz < 3; dz++)
+            for (int dy = 0; dy < 3; dy++)
+                for (int dx = 0; dx < 3; dx++, k++) {
+                    offs[3 * k] = dx - 1;
+                    offs[3 * k + 1] = dy - 1;
+                    offs[3 * k + 2] = dz - 1;
+                    coef[k] = ex * (T[dx] * M[dy] * M[dz]) + ey * (M[dx] * T[dy] * M[dz]) +
+                              ez * (M[dx] * M[dy] * T[dz]);
+                }
+        auto p = make_csr(&ctx->ctx);
+        gen_stencil(p->m, &ctx->ctx, nx, ny, nz, offs, coef, 27);
+        p->nrows = p->ncols = p->m.nrows;
+        *out = box(p);
+    });
+}
+
+// ------------------------------------------------------------ generic ops
+
+amg_status amg_linop_kind_of(const amg_linop *op, int32_t *kind) {
+    return guard([&] {
+        FAMG_REQUIRE(kind, AMG_ERR_INVALID, "null argument");
+        *kind = static_cast<int32_t>(need(op).kind());
+    });
+}
+
+amg_status amg_linop_dims(const amg_linop *op, int64_t *nrows, int64_t *ncols) {
+    return guard([&] {
+        const LinOp &o = need(op);
+        if (nrows) *nrows = o.nrows;
+        if (ncols) *ncols = o.ncols;
+    });
+}
+
+amg_status amg_linop_apply(amg_linop *op, double *out, int64_t ld_out, const double *rhs,
+                           int64_t ld_rhs, int64_t k, amg_mem mem) {
+    return guard([&] {
+        LinOp &o = need(op);
+        for_columns(o, out, ld_out, rhs, ld_rhs, k, mem, o.nrows, o.ncols,
+                    [&](double *y, const double *x) { o.apply(y, x); });
+    });
+}
+
+amg_status amg_linop_transpose_apply(amg_linop *op, double *out, int64_t ld_out, const double *rhs,
+                                     int64_t ld_rhs, int64_t k, amg_mem mem) {
+    return guard([&] {
+        LinOp &o = need(op);
+        for_columns(o, out, ld_out, rhs, ld_rhs, k, mem, o.ncols, o.nrows,
+                    [&](double *y, const double *x) { o.transpose_apply(y, x); });
+    });
+}
+
+amg_status amg_precond_apply_in_place(amg_linop *op, double *rhs, int64_t ld, int64_t k, amg_mem mem) {
+    return guard([&] {
+        LinOp &o = need(op);
+        FAMG_REQUIRE(o.nrows == o.ncols, AMG_ERR_DIM, "apply_in_place needs a square operator");
+        if (mem == AMG_MEM_DEVICE) {
+            o.ctx->set_device();
+            FAMG_REQUIRE(k >= 0 && (k == 0 || rhs) && ld >= o.nrows, AMG_ERR_INVALID, "bad vector");
+            for (int64_t c = 0; c < k; c++) o.apply_in_place(rhs + c * ld);
+        } else {
+            for_columns(o, rhs, ld, rhs, ld, k, mem, o.nrows, o.ncols,
+                        [&](double *y, const double *x) { o.apply(y, x); });
+        }
+    });
+}
+
+amg_status amg_precond_transpose_apply_in_place(amg_linop *op, double *rhs, int64_t ld, int64_t k,
+                                                amg_mem mem) {
+    // every preconditioner of this library is symmetric (BiPrecond impls of the
+    // reference forward transpose to apply: coarse_solvers.rs:266-276)
+    return amg_precond_apply_in_place(op, rhs, ld, k, mem);
+}
+
+amg_status amg_linop_destroy(amg_linop *op) {
+    return guard([&] {
+        if (!op) return;
+        if (op->op && op->op->ctx) op->op->ctx->set_device();
+        delete op;
+    });
+}
+
+// ------------------------------------------------------------- smoothers
+
+amg_status amg_jacobi_create(const amg_linop *A, double omega, amg_linop **out) {
+    return guard([&] {
+        FAMG_REQUIRE(out, AMG_ERR_INVALID, "null output");
+        auto a = need_csr(A);
+        a->ctx->set_device();
+        *out = box(make_jacobi(*a, omega));
+    });
+}
+
+amg_status amg_l1_create(const amg_linop *A, amg_linop **out) {
+    return guard([&] {
+        FAMG_REQUIRE(out, AMG_ERR_INVALID, "null output");
+        auto a = need_csr(A);
+        a->ctx->set_device();
+        *out = box(make_l1(*a));
+    });
+}
+
+amg_status amg_l2_create(const amg_linop *A, amg_linop **out) {
+    return guard([&] {
+        FAMG_REQUIRE(out, AMG_ERR_INVALID, "null output");
+        auto a = need_csr(A);
+        a->ctx->set_device();
+        *out = box(make_l2(*a));
+    });
+}
+
+amg_status amg_diag_create(amg_ctx *ctx, int64_t n, const double *d, amg_linop **out) {
+    return guard([&] {
+        FAMG_REQUIRE(ctx && out && (n == 0 || d) && n >= 0, AMG_ERR_INVALID, "bad argument");
+        ctx->ctx.set_device();
+        auto p = std::make_shared<DiagOp>();
+        p->ctx = &ctx->ctx;
+        p->nrows = p->ncols = n;
+        p->d.resize(n);
+        if (n) {
+            FAMG_CHECK_HIP(hipMemcpyAsync(p->d.get(), d, n * sizeof(double), hipMemcpyHostToDevice, ctx->ctx.stream));
+            FAMG_CHECK_HIP(hipStreamSynchronize(ctx->ctx.stream));
+        }
+        *out = box(p);
+    });
+}
+
+amg_status amg_sgs_create(const amg_linop *A, const int32_t *colors, amg_linop **out) {
+    return guard([&] {
+        FAMG_REQUIRE(out, AMG_ERR_INVALID, "null output");
+        auto a = need_csr(A);
+        a->ctx->set_device();
+        *out = box(make_sgs(a, colors));
+    });
+}
+
+amg_status amg_sgs_ncolors(const amg_linop *op, int64_t *ncolors) {
+    return guard([&] {
+        FAMG_REQUIRE(ncolors, AMG_ERR_INVALID, "null output");
+        auto p = std::dynamic_pointer_cast<SgsOp>(need(op).shared_from_this());
+        FAMG_REQUIRE(p, AMG_ERR_INVALID, "operator is not an SGS smoother");
+        *ncolors = p->ncolors;
+    });
+}
+
+amg_status amg_coarse_chol_create(const amg_linop *A, amg_linop **out) {
+    return guard([&] {
+        FAMG_REQUIRE(out, AMG_ERR_INVALID, "null output");
+        auto a = need_csr(A);
+        a->ctx->set_device();
+        *out = box(make_coarse_chol(*a));
+    });
+}
+
+// -------------------------------------------------------------- multigrid
+
+amg_status amg_multigrid_create(amg_linop *op, amg_linop *smoother, amg_linop **out) {
+    return guard([&] {
+        FAMG_REQUIRE(out, AMG_ERR_INVALID, "null output");
+        LinOp &A = need(op);
+        LinOp &S = need(smoother);
+        FAMG_REQUIRE(A.nrows == A.ncols, AMG_ERR_DIM, "multigrid: op must be square");
+        FAMG_REQUIRE(S.nrows == A.nrows && S.ncols == A.ncols, AMG_ERR_DIM, "multigrid: smoother size");
+        auto mg = std::make_shared<MultigridOp>();
+        mg->ctx = A.ctx;
+        mg->nrows = mg->ncols = A.nrows;
+        MgLevel L;
+        L.A = op->op;
+        L.S = smoother->op;
+        mg->levels.push_back(std::move(L));
+        *out = box(mg);
+    });
+}
+
+amg_status amg_multigrid_add_level(amg_linop *mg, amg_linop *op, amg_linop *smoother, amg_linop *r,
+                                   amg_linop *p) {
+    return guard([&] {
+        auto m = need_mg(mg);
+        need(op); need(smoother); need(r); need(p);
+        std::lock_guard<std::mutex> lk(m->mtx);
+        m->add_level(op->op, smoother->op, r->op, p->op);
+    });
+}
+
+amg_status amg_multigrid_set(amg_linop *mg, int64_t mu, int64_t steps) {
+    return guard([&] {
+        auto m = need_mg(mg);
+        FAMG_REQUIRE(mu > 0 && steps > 0, AMG_ERR_INVALID, "mu and steps must be > 0");
+        std::lock_guard<std::mutex> lk(m->mtx);
+        m->mu = mu;
+        m->steps = steps;
+        m->invalidate_graphs();
+    });
+}
+
+amg_status amg_multigrid_levels(const amg_linop *mg, int64_t *levels) {
+    return guard([&] {
+        FAMG_REQUIRE(levels, AMG_ERR_INVALID, "null output");
+        *levels = (int64_t)need_mg(mg)->levels.size();
+    });
+}
+
+amg_status amg_multigrid_set_graph(amg_linop *mg, int32_t enable) {
+    return guard([&] {
+        auto m = need_mg(mg);
+        std::lock_guard<std::mutex> lk(m->mtx);
+        m->use_graph = enable != 0;
+        m->invalidate_graphs();
+    });
+}
+
+amg_status amg_multigrid_apply(amg_linop *mg, double *out, int64_t ld_out, const double *rhs,
+                               int64_t ld_rhs, int64_t k, amg_mem mem) {
+    return guard([&] {
+        auto m = need_mg(mg);
+        for_columns(*m, out, ld_out, rhs, ld_rhs, k, mem, m->nrows, m->ncols,
+                    [&](double *y, const double *x) { m->apply(y, x); });
+    });
+}
+
+amg_status amg_multigrid_get_level(const amg_linop *mg, int64_t level, amg_linop **A, amg_linop **S,
+                                   amg_linop **R, amg_linop **P) {
+    return guard([&] {
+        auto m = need_mg(mg);
+        FAMG_REQUIRE(level >= 0 && level < (int64_t)m->levels.size(), AMG_ERR_INVALID, "level out of range");
+        const MgLevel &L = m->levels[level];
+        if (A) *A = box(L.A);
+        if (S) *S = box(L.S);
+        if (R) *R = L.R ? box(L.R) : nullptr;
+        if (P) *P = L.P ? box(L.P) : nullptr;
+    });
+}
+
+// ------------------------------------------------------------------ setup
+
+amg_status amg_spgemm(const amg_linop *A, const amg_linop *B, amg_linop **out) {
+    return guard([&] {
+        FAMG_REQUIRE(out, AMG_ERR_INVALID, "null output");
+        auto a = need_csr(A), b = need_csr(B);
+        FAMG_REQUIRE(a->ctx == b->ctx, AMG_ERR_INVALID, "operands on different contexts");
+        a->ctx->set_device();
+        *out = box(spgemm_op(*a, *b));
+    });
+}
+
+amg_status amg_transpose(const amg_linop *P, amg_linop **out) {
+    return guard([&] {
+        FAMG_REQUIRE(out, AMG_ERR_INVALID, "null output");
+        auto p = need_csr(P);
+        p->ctx->set_device();
+        *out = box(transpose_op(*p));
+    });
+}
+
+amg_status amg_galerkin_rap(const amg_linop *R, const amg_linop *A, const amg_linop *P, amg_linop **out) {
+    return guard([&] {
+        FAMG_REQUIRE(out, AMG_ERR_INVALID, "null output");
+        auto r = need_csr(R), a = need_csr(A), p = need_csr(P);
+        a->ctx->set_device();
+        *out = box(galerkin_rap(*r, *a, *p));
+    });
+}
+
+amg_status amg_smooth_interpolation(const amg_linop *A, const amg_linop *P, double omega, amg_linop **out) {
+    return guard([&] {
+        FAMG_REQUIRE(out, AMG_ERR_INVALID, "null output");
+        auto a = need_csr(A), p = need_csr(P);
+        a->ctx->set_device();
+        *out = box(smooth_interpolation(*a, *p, omega));
+    });
+}
+
+amg_status amg_sa_tentative(amg_ctx *ctx, int64_t n, const int64_t *agg_of, int64_t naggs,
+                            const double *near_null, amg_linop **P, double *coarse_nn) {
+    return guard([&] {
+        FAMG_REQUIRE(ctx && P && coarse_nn && (n == 0 || (agg_of && near_null)), AMG_ERR_INVALID, "null argument");
+        FAMG_REQUIRE(n >= 0 && naggs > 0, AMG_ERR_INVALID, "bad sizes");
+        ctx->ctx.set_device();
+        *P = box(sa_tentative(&ctx->ctx, n, agg_of, naggs, near_null, coarse_nn));
+    });
+}
+
+amg_status amg_nn_stationary_l1(const amg_linop *A, int64_t iters, double *x) {
+    return guard([&] {
+        auto a = need_csr(A);
+        FAMG_REQUIRE(x && iters >= 1, AMG_ERR_INVALID, "bad argument");
+        a->ctx->set_device();
+        nn_stationary_l1(*a, iters, x);
+    });
+}
+
+amg_status amg_sa_build_box(amg_linop *A, int64_t nx, int64_t ny, int64_t nz, int64_t bx, int64_t by,
+                            int64_t bz, int64_t coarsest_dim, int64_t max_levels, double omega,
+                            int32_t smoother, amg_linop **mg_out) {
+    return guard([&] {
+        FAMG_REQUIRE(mg_out, AMG_ERR_INVALID, "null output");
+        auto a = need_csr(A);
+        a->ctx->set_device();
+        *mg_out = box(sa_build_box(a, nx, ny, nz, bx, by, bz, coarsest_dim, max_levels, omega, smoother));
+    });
+}
+
+// ------------------------------------------------------------ solve drivers
+
+amg_status amg_stationary_solve(amg_linop *A, amg_linop *M, const double *b, double *x, int64_t max_iter,
+                                double rel_tol, double *hist, int64_t *iters) {
+    return guard([&] {
+        LinOp &a = need(A);
+        LinOp &m = need(M);
+        FAMG_REQUIRE(b && x && iters && max_iter > 0, AMG_ERR_INVALID, "bad argument");
+        FAMG_REQUIRE(a.nrows == a.ncols && m.nrows == a.nrows, AMG_ERR_DIM, "solver dims");
+        Ctx &ctx = *a.ctx;
+        ctx.set_device();
+        hipStream_t s = ctx.stream;
+        const int64_t n = a.nrows;
+        DevBuf<double> r(n), z(n);
+        const double bn = std::sqrt(vec_dot(b, b, n, ctx));
+        auto *ac = dynamic_cast<CsrOp *>(&a);
+        int64_t it = 0;
+        for (;;) {
+            if (ac) {
+                SpmvEpi epi;
+                epi.b = b;
+                spmv(ac->m, x, r.get(), SPMV_RESID, epi, s);
+            } else {
+                a.apply(r.get(), x);
+                vec_sub(r.get(), b, r.get(), n, s);
+            }
+            const double rel = std::sqrt(vec_dot(r.get(), r.get(), n, ctx)) / bn;
+            it++;
+            if (hist) hist[it - 1] = rel;
+            if (rel < rel_tol || it >= max_iter) break;
+            m.apply(z.get(), r.get());
+            vec_add_inplace(x, z.get(), n, s);
+        }
+        FAMG_CHECK_HIP(hipStreamSynchronize(s));
+        *iters = it;
+    });
+}
+
+amg_status amg_pcg_solve(amg_linop *A, amg_linop *M, const double *b, double *x, int64_t max_iter,
+                         double rel_tol, double abs_tol, double *hist, int64_t *iters) {
+    return guard([&] {
+        LinOp &a = need(A);
+        FAMG_REQUIRE(b && x && iters && max_iter >= 0, AMG_ERR_INVALID, "bad argument");
+        LinOp *m = M ? &need(M) : nullptr;
+        FAMG_REQUIRE(a.nrows == a.ncols && (!m || m->nrows == a.nrows), AMG_ERR_DIM, "solver dims");
+        Ctx &ctx = *a.ctx;
+        ctx.set_device();
+        hipStream_t s = ctx.stream;
+        const int64_t n = a.nrows;
+        DevBuf<double> r(n), z(n), p(n), Ap(n);
+        a.apply(Ap.get(), x);
+        vec_sub(r.get(), b, Ap.get(), n, s);
+        const double bn = std::sqrt(vec_dot(b, b, n, ctx));
+        const double tol = std::max(rel_tol * bn, abs_tol);
+        int64_t it = 0;
+        if (std::sqrt(vec_dot(r.get(), r.get(), n, ctx)) > tol) {
+            auto pc = [&](double *dst, const double *src) {
+                if (m) m->apply(dst, src);
+                else vec_copy(dst, src, n, s);
+            };
+            pc(z.get(), r.get());
+            vec_copy(p.get(), z.get(), n, s);
+            double rz = vec_dot(r.get(), z.get(), n, ctx);
+            for (it = 1; it <= max_iter; it++) {
+                a.apply(Ap.get(), p.get());
+                const double alpha = rz / vec_dot(p.get(), Ap.get(), n, ctx);
+                vec_axpy(x, alpha, p.get(), n, s);
+                vec_axpy(r.get(), -alpha, Ap.get(), n, s);
+                const double rn = std::sqrt(vec_dot(r.get(), r.get(), n, ctx));
+                if (hist) hist[it - 1] = rn / bn;
+                if (rn <= tol) break;
+                pc(z.get(), r.get());
+                const double rzn = vec_dot(r.get(), z.get(), n, ctx);
+                const double beta = rzn / rz;
+                rz = rzn;
+                vec_xpay(p.get(), beta, z.get(), n, s);
+            }
+        }
+        FAMG_CHECK_HIP(hipStreamSynchronize(s));
+        *iters = it;
+    });
+}
+
+}  // extern "C"

@@ -1,0 +1,99 @@
+// common.hpp -- runtime plumbing shared by the MI355X AMG library: status and
+// error propagation, device buffers, the per-process device context.
+//
+// Errors are C++ exceptions inside the library (AmgError carrying an
+// amg_status) and are converted to status codes + a thread-local message at the
+// C ABI boundary (capi.cpp).  The reference panics instead.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <cstdio>
+#include <memory>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "../../include/amg.h"
+
+namespace famg {
+
+struct AmgError : std::runtime_error {
+    amg_status status;
+    AmgError(amg_status s, const std::string &msg) : std::runtime_error(msg), status(s) {}
+};
+
+[[noreturn]] inline void fail(amg_status s, const std::string &msg) { throw AmgError(s, msg); }
+
+#define FAMG_CHECK_HIP(expr)                                                               \
+    do {                                                                                   \
+        hipError_t e_ = (expr);                                                            \
+        if (e_ != hipSuccess) {                                                            \
+            ::famg::fail(e_ == hipErrorOutOfMemory ? AMG_ERR_OOM : AMG_ERR_HIP,            \
+                         std::string(#expr) + ": " + hipGetErrorString(e_) + " at " +      \
+                             __FILE__ + ":" + std::to_string(__LINE__));                   \
+        }                                                                                  \
+    } while (0)
+
+#define FAMG_REQUIRE(cond, status, msg)                                                    \
+    do {                                                                                   \
+        if (!(cond)) ::famg::fail(status, msg);                                            \
+    } while (0)
+
+// Owning device allocation.  Sizes are in elements.  Allocation and free are
+// synchronous (setup-time only; nothing in an apply path allocates).
+template <typename T> class DevBuf {
+  public:
+    DevBuf() = default;
+    explicit DevBuf(size_t n) { resize(n); }
+    DevBuf(const DevBuf &) = delete;
+    DevBuf &operator=(const DevBuf &) = delete;
+    DevBuf(DevBuf &&o) noexcept : p_(o.p_), n_(o.n_) { o.p_ = nullptr; o.n_ = 0; }
+    DevBuf &operator=(DevBuf &&o) noexcept {
+        if (this != &o) { release(); p_ = o.p_; n_ = o.n_; o.p_ = nullptr; o.n_ = 0; }
+        return *this;
+    }
+    ~DevBuf() { release(); }
+    // pad: extra elements allocated past n (vector loads may read up to 16 B past the end)
+    void resize(size_t n, size_t pad = 0) {
+        release();
+        if (n + pad) {
+            void *p = nullptr;
+            FAMG_CHECK_HIP(hipMalloc(&p, (n + pad) * sizeof(T)));
+            p_ = static_cast<T *>(p);
+        }
+        n_ = n;
+    }
+    void release() {
+        if (p_) (void)hipFree(p_);
+        p_ = nullptr;
+        n_ = 0;
+    }
+    T *get() const { return p_; }
+    size_t size() const { return n_; }
+    size_t bytes() const { return n_ * sizeof(T); }
+
+  private:
+    T *p_ = nullptr;
+    size_t n_ = 0;
+};
+
+// One per process / device (one process per GPU).  All work of the handles
+// created under a context is ordered on `stream`.
+struct Ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    bool own_stream = false;
+    int num_cus = 256;
+    // scratch used by host-memory staging and reductions
+    DevBuf<double> red_partials;   // block partial sums for deterministic reductions
+    DevBuf<double> red_result;     // reduction results
+    double *host_red = nullptr;    // pinned host mirror of red_result
+    void set_device() const { FAMG_CHECK_HIP(hipSetDevice(device)); }
+    ~Ctx();
+};
+
+inline int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
+
+}  // namespace famg

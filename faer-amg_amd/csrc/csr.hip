@@ -1,0 +1,217 @@
+// csr.hip -- device CSR storage: upload/download, 32-bit index view, SpMV
+// schedule, diagonal extraction and the structured-grid generators.
+//
+// The reference stores SparseRowMat<usize, f64> (8-byte indices, core.rs:12-17)
+// and, for parallel apply, a second copy cut into 8192x8192 CSC tiles
+// (par_spmm.rs:31-96).  Here one CSR copy lives in HBM with 32-bit row pointers
+// and column indices (12 B per entry instead of 16-24), plus an int64 row
+// pointer array used only by setup kernels.
+#include <algorithm>
+#include <cstring>
+
+#include "famg.hpp"
+
+namespace famg {
+
+void build_schedule(const std::vector<int64_t> &rp, const std::vector<int64_t> &seg_bounds,
+                    std::vector<int32_t> &sched, std::vector<int64_t> &seg_blocks);
+
+void csr_alloc(GpuCsr &m, Ctx *ctx, int64_t nrows, int64_t ncols, int64_t nnz) {
+    FAMG_REQUIRE(nrows >= 0 && ncols >= 0 && nnz >= 0, AMG_ERR_INVALID, "negative CSR size");
+    FAMG_REQUIRE(nrows < (int64_t(1) << 31) && ncols < (int64_t(1) << 31), AMG_ERR_UNSUPPORTED,
+                 "CSR dimensions must be < 2^31");
+    m.ctx = ctx;
+    m.nrows = nrows;
+    m.ncols = ncols;
+    m.nnz = nnz;
+    m.rp64.resize(nrows + 1);
+    m.col.resize(nnz, 4);
+    m.val.resize(nnz, 2);
+    m.rp32.release();
+    m.sched.release();
+    m.nblocks = 0;
+}
+
+__global__ void k_narrow_rp(const int64_t *rp64, int32_t *rp32, int64_t n1) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i < n1) rp32[i] = static_cast<int32_t>(rp64[i]);
+}
+
+void csr_finalize(GpuCsr &m) {
+    Ctx &ctx = *m.ctx;
+    if (m.nnz >= (int64_t(1) << 31)) {  // setup-only matrix: no SpMV view
+        m.rp32.release();
+        m.sched.release();
+        m.nblocks = 0;
+        return;
+    }
+    m.rp32.resize(m.nrows + 1);
+    hipLaunchKernelGGL(k_narrow_rp, dim3((unsigned)ceil_div(m.nrows + 1, 256)), dim3(256), 0,
+                       ctx.stream, m.rp64.get(), m.rp32.get(), m.nrows + 1);
+    FAMG_CHECK_HIP(hipGetLastError());
+    std::vector<int64_t> rp(m.nrows + 1);
+    FAMG_CHECK_HIP(hipMemcpyAsync(rp.data(), m.rp64.get(), (m.nrows + 1) * sizeof(int64_t),
+                                  hipMemcpyDeviceToHost, ctx.stream));
+    FAMG_CHECK_HIP(hipStreamSynchronize(ctx.stream));
+    std::vector<int32_t> sched;
+    std::vector<int64_t> segb;
+    build_schedule(rp, {0, m.nrows}, sched, segb);
+    m.nblocks = static_cast<int64_t>(sched.size()) - 1;
+    m.sched.resize(sched.size());
+    FAMG_CHECK_HIP(hipMemcpyAsync(m.sched.get(), sched.data(), sched.size() * sizeof(int32_t),
+                                  hipMemcpyHostToDevice, ctx.stream));
+    FAMG_CHECK_HIP(hipStreamSynchronize(ctx.stream));
+}
+
+void csr_from_host(GpuCsr &m, Ctx *ctx, int64_t nrows, int64_t ncols, const int64_t *rowptr,
+                   const int64_t *col, const double *val) {
+    FAMG_REQUIRE(rowptr != nullptr, AMG_ERR_INVALID, "null rowptr");
+    const int64_t nnz = rowptr[nrows];
+    FAMG_REQUIRE(rowptr[0] == 0, AMG_ERR_INVALID, "rowptr[0] must be 0");
+    FAMG_REQUIRE(nnz == 0 || (col && val), AMG_ERR_INVALID, "null column/value array");
+    // validate structure (sorted, in range) -- the reference relies on faer's
+    // invariants for SparseRowMat
+    for (int64_t i = 0; i < nrows; i++) {
+        FAMG_REQUIRE(rowptr[i + 1] >= rowptr[i], AMG_ERR_INVALID, "rowptr not monotone");
+        for (int64_t e = rowptr[i]; e < rowptr[i + 1]; e++) {
+            FAMG_REQUIRE(col[e] >= 0 && col[e] < ncols, AMG_ERR_INVALID, "column index out of range");
+            FAMG_REQUIRE(e == rowptr[i] || col[e] > col[e - 1], AMG_ERR_INVALID,
+                         "column indices must be strictly ascending within a row");
+        }
+    }
+    csr_alloc(m, ctx, nrows, ncols, nnz);
+    FAMG_REQUIRE(nnz < (int64_t(1) << 31), AMG_ERR_UNSUPPORTED, "nnz must be < 2^31");
+    std::vector<int32_t> c32(nnz);
+    for (int64_t e = 0; e < nnz; e++) c32[e] = static_cast<int32_t>(col[e]);
+    hipStream_t s = ctx->stream;
+    FAMG_CHECK_HIP(hipMemcpyAsync(m.rp64.get(), rowptr, (nrows + 1) * sizeof(int64_t), hipMemcpyHostToDevice, s));
+    if (nnz) {
+        FAMG_CHECK_HIP(hipMemcpyAsync(m.col.get(), c32.data(), nnz * sizeof(int32_t), hipMemcpyHostToDevice, s));
+        FAMG_CHECK_HIP(hipMemcpyAsync(m.val.get(), val, nnz * sizeof(double), hipMemcpyHostToDevice, s));
+    }
+    FAMG_CHECK_HIP(hipStreamSynchronize(s));
+    csr_finalize(m);
+}
+
+void csr_to_host(const GpuCsr &m, int64_t *rowptr, int64_t *col, double *val) {
+    hipStream_t s = m.ctx->stream;
+    std::vector<int32_t> c32(m.nnz);
+    FAMG_CHECK_HIP(hipMemcpyAsync(rowptr, m.rp64.get(), (m.nrows + 1) * sizeof(int64_t), hipMemcpyDeviceToHost, s));
+    if (m.nnz) {
+        FAMG_CHECK_HIP(hipMemcpyAsync(c32.data(), m.col.get(), m.nnz * sizeof(int32_t), hipMemcpyDeviceToHost, s));
+        FAMG_CHECK_HIP(hipMemcpyAsync(val, m.val.get(), m.nnz * sizeof(double), hipMemcpyDeviceToHost, s));
+    }
+    FAMG_CHECK_HIP(hipStreamSynchronize(s));
+    for (int64_t e = 0; e < m.nnz; e++) col[e] = c32[e];
+}
+
+// a_ii by binary search in each row; missing diagonal -> *missing = 1
+__global__ void k_diag(const int64_t *rp, const int32_t *col, const double *val, int64_t n,
+                       double *d, int *missing) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    int64_t lo = rp[i], hi = rp[i + 1];
+    while (lo < hi) {
+        const int64_t mid = (lo + hi) >> 1;
+        if (col[mid] < i) lo = mid + 1;
+        else hi = mid;
+    }
+    if (lo < rp[i + 1] && col[lo] == i) d[i] = val[lo];
+    else { d[i] = 0.0; *missing = 1; }
+}
+
+void csr_diagonal(const GpuCsr &m, double *d_out) {
+    FAMG_REQUIRE(m.nrows == m.ncols, AMG_ERR_DIM, "diagonal of a non-square matrix");
+    DevBuf<int> flag(1);
+    hipStream_t s = m.ctx->stream;
+    FAMG_CHECK_HIP(hipMemsetAsync(flag.get(), 0, sizeof(int), s));
+    if (m.nrows)
+        hipLaunchKernelGGL(k_diag, dim3((unsigned)ceil_div(m.nrows, 256)), dim3(256), 0, s,
+                           m.rp64.get(), m.col.get(), m.val.get(), m.nrows, d_out, flag.get());
+    int h = 0;
+    FAMG_CHECK_HIP(hipMemcpyAsync(&h, flag.get(), sizeof(int), hipMemcpyDeviceToHost, s));
+    FAMG_CHECK_HIP(hipStreamSynchronize(s));
+    FAMG_REQUIRE(h == 0, AMG_ERR_INVALID, "matrix has a missing diagonal entry");
+}
+
+__global__ void k_abs_row_sums(const int64_t *rp, const double *val, int64_t n, double *out) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    double s = 0.0;
+    for (int64_t e = rp[i]; e < rp[i + 1]; e++) s += fabs(val[e]);
+    out[i] = s;
+}
+
+void csr_abs_row_sums(const GpuCsr &m, double *out) {
+    if (!m.nrows) return;
+    hipLaunchKernelGGL(k_abs_row_sums, dim3((unsigned)ceil_div(m.nrows, 256)), dim3(256), 0,
+                       m.ctx->stream, m.rp64.get(), m.val.get(), m.nrows, out);
+    FAMG_CHECK_HIP(hipGetLastError());
+}
+
+// ------------------------------------------------------------ generators
+
+struct Stencil {
+    int dx[27], dy[27], dz[27];
+    double c[27];
+    int n;
+};
+
+__global__ void k_sten_count(Stencil st, int64_t nx, int64_t ny, int64_t nz, int64_t *cnt) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    const int64_t n = nx * ny * nz;
+    if (i >= n) return;
+    const int64_t x = i % nx, y = (i / nx) % ny, z = i / (nx * ny);
+    int64_t c = 0;
+    for (int k = 0; k < st.n; k++) {
+        const int64_t xx = x + st.dx[k], yy = y + st.dy[k], zz = z + st.dz[k];
+        c += (xx >= 0 && yy >= 0 && zz >= 0 && xx < nx && yy < ny && zz < nz);
+    }
+    cnt[i] = c;
+}
+
+__global__ void k_sten_fill(Stencil st, int64_t nx, int64_t ny, int64_t nz, const int64_t *rp,
+                            int32_t *col, double *val) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    const int64_t n = nx * ny * nz;
+    if (i >= n) return;
+    const int64_t x = i % nx, y = (i / nx) % ny, z = i / (nx * ny);
+    int64_t e = rp[i];
+    for (int k = 0; k < st.n; k++) {
+        const int64_t xx = x + st.dx[k], yy = y + st.dy[k], zz = z + st.dz[k];
+        if (xx >= 0 && yy >= 0 && zz >= 0 && xx < nx && yy < ny && zz < nz) {
+            col[e] = static_cast<int32_t>(xx + nx * (yy + ny * zz));
+            val[e] = st.c[k];
+            e++;
+        }
+    }
+}
+
+// offs: nsten triples (dx,dy,dz) in ascending linear-offset order (dz, dy, dx).
+void gen_stencil(GpuCsr &m, Ctx *ctx, int64_t nx, int64_t ny, int64_t nz, const int *offs,
+                 const double *coef, int nsten) {
+    FAMG_REQUIRE(nx > 0 && ny > 0 && nz > 0, AMG_ERR_INVALID, "grid dims must be positive");
+    const int64_t n = nx * ny * nz;
+    Stencil st;
+    st.n = nsten;
+    for (int k = 0; k < nsten; k++) {
+        st.dx[k] = offs[3 * k];
+        st.dy[k] = offs[3 * k + 1];
+        st.dz[k] = offs[3 * k + 2];
+        st.c[k] = coef[k];
+    }
+    DevBuf<int64_t> cnt(n);
+    hipStream_t s = ctx->stream;
+    const unsigned g = (unsigned)ceil_div(n, 256);
+    hipLaunchKernelGGL(k_sten_count, dim3(g), dim3(256), 0, s, st, nx, ny, nz, cnt.get());
+    DevBuf<int64_t> rp(n + 1);
+    const int64_t nnz = scan_counts(cnt.get(), rp.get(), n, *ctx);
+    csr_alloc(m, ctx, n, n, nnz);
+    m.rp64 = std::move(rp);
+    hipLaunchKernelGGL(k_sten_fill, dim3(g), dim3(256), 0, s, st, nx, ny, nz, m.rp64.get(),
+                       m.col.get(), m.val.get());
+    FAMG_CHECK_HIP(hipGetLastError());
+    csr_finalize(m);
+}
+
+}  // namespace famg

@@ -1,0 +1,234 @@
+// famg.hpp -- host-side object model of the MI355X AMG library.
+//
+// The classes mirror the reference's operator surface (faer matrix_free
+// LinOp / Precond / BiPrecond as used by aujxn/faer-amg):
+//   LinOp            <- faer::matrix_free::LinOp<f64>        (trait object)
+//   CsrOp            <- SparseMatOp / ParSpmmOp / SparseRowMat (core.rs, par_spmm.rs)
+//   DiagOp           <- Diag<f64> from new_jacobi/new_l1/new_l2 (smoothers.rs:43-86)
+//   SgsOp            <- SmootherKind::SymGaussSeidel (smoothers.rs:20, unimplemented there)
+//   CoarseCholOp     <- SparseCholeskySolve (coarse_solvers.rs:164-276)
+//   MultigridOp      <- Multigrid (preconditioners/multigrid.rs:171-518)
+// All operator data lives in HBM; apply() works on device pointers and is
+// asynchronous on the context stream.
+#pragma once
+
+#include <memory>
+#include <mutex>
+#include <vector>
+
+#include "common.hpp"
+
+namespace famg {
+
+// ------------------------------------------------------------------ CSR data
+
+// A CSR matrix resident on the device.  rp64 (int64 row pointers) always
+// exists and is what setup kernels (SpGEMM, transpose, extraction) read;
+// rp32 + the stream schedule exist when nnz < 2^31 and are what SpMV reads
+// (12 B per entry + 4 B per row of index/value traffic).
+struct GpuCsr {
+    Ctx *ctx = nullptr;
+    int64_t nrows = 0, ncols = 0, nnz = 0;
+    DevBuf<int64_t> rp64;
+    DevBuf<int32_t> rp32;
+    DevBuf<int32_t> col;   // padded by 4 entries (16-B vector loads)
+    DevBuf<double> val;    // padded by 2 entries
+    DevBuf<int32_t> sched; // stream-SpMV row blocks: nblocks+1 row starts
+    int64_t nblocks = 0;
+    bool spmv_ready() const { return rp32.get() != nullptr && sched.get() != nullptr; }
+    int64_t index_bytes() const { return 12 * nnz + 4 * (nrows + 1); }
+};
+
+// Allocate a CSR with the given shape/nnz (arrays uninitialised).
+void csr_alloc(GpuCsr &m, Ctx *ctx, int64_t nrows, int64_t ncols, int64_t nnz);
+// Build rp32 (if nnz < 2^31) and the stream schedule from rp64.  Host pass over
+// the row pointers (setup only).
+void csr_finalize(GpuCsr &m);
+// Host upload from usize-compatible arrays.
+void csr_from_host(GpuCsr &m, Ctx *ctx, int64_t nrows, int64_t ncols, const int64_t *rowptr,
+                   const int64_t *col, const double *val);
+void csr_to_host(const GpuCsr &m, int64_t *rowptr, int64_t *col, double *val);
+// Diagonal a_ii per row (device, n); throws if a diagonal entry is missing.
+void csr_diagonal(const GpuCsr &m, double *d_out);
+void csr_abs_row_sums(const GpuCsr &m, double *d_out);
+
+// ------------------------------------------------------------------ kernels
+
+enum SpmvMode : int {
+    SPMV_SET = 0,    // y = A x
+    SPMV_ADD = 1,    // y = y + A x
+    SPMV_RESID = 2,  // y = b - A x
+    SPMV_JACOBI = 3, // y = x + d (b - A x)   (x != y)
+    SPMV_SGS = 4     // e[perm p] = e[perm p] + d_p (b[perm p] - (A e)_p)
+};
+
+struct SpmvEpi {
+    const double *b = nullptr;
+    const double *d = nullptr;
+    const int32_t *perm = nullptr;
+};
+
+// Stream (LDS-staged) CSR SpMV over blocks [blk_begin, blk_end) of m's schedule.
+void spmv(const GpuCsr &m, const double *x, double *y, SpmvMode mode, const SpmvEpi &epi,
+          hipStream_t s, int64_t blk_begin = 0, int64_t blk_end = -1,
+          const int32_t *sched_override = nullptr);
+
+// BLAS-1 (n-vectors, device pointers)
+void vec_fill(double *x, double v, int64_t n, hipStream_t s);
+void vec_copy(double *dst, const double *src, int64_t n, hipStream_t s);
+void vec_sub(double *out, const double *a, const double *b, int64_t n, hipStream_t s);  // a-b
+void vec_add_inplace(double *x, const double *y, int64_t n, hipStream_t s);           // x+=y
+void vec_mul(double *out, const double *d, const double *a, int64_t n, hipStream_t s); // d*a
+void vec_axpy(double *y, double alpha, const double *x, int64_t n, hipStream_t s);      // y+=a x
+void vec_xpay(double *y, double beta, const double *x, int64_t n, hipStream_t s);       // y=x+b y
+void vec_scale(double *x, double alpha, int64_t n, hipStream_t s);                      // x*=a
+// x = x + d*(x - r)   (StationaryIteration quirk step, smoothers.rs:153-156)
+void vec_nn_step(double *x, const double *d, const double *r, int64_t n, hipStream_t s);
+// Deterministic dot product; result left on device in *res (fixed reduction tree).
+void vec_dot_dev(const double *x, const double *y, int64_t n, double *res, Ctx &ctx);
+double vec_dot(const double *x, const double *y, int64_t n, Ctx &ctx);  // syncs
+
+// dense row-major GEMV: out = M * x (M n x n)
+void dense_gemv(const double *M, const double *x, double *out, int64_t n, hipStream_t s);
+
+// exclusive scan of int64 counts (n entries) into out (n+1 entries); returns total
+int64_t scan_counts(const int64_t *counts, int64_t *out, int64_t n, Ctx &ctx);
+
+// sparse products / setup
+void spgemm(const GpuCsr &A, const GpuCsr &B, GpuCsr &C);
+void transpose(const GpuCsr &A, GpuCsr &T);
+void smooth_interp_fixup(GpuCsr &S, const GpuCsr &P, const double *diag, double omega);
+void gen_stencil(GpuCsr &m, Ctx *ctx, int64_t nx, int64_t ny, int64_t nz, const int *offs,
+                 const double *coef, int nsten);
+
+// ------------------------------------------------------------------ operators
+
+enum class Kind : int {
+    Csr = AMG_KIND_CSR,
+    Diag = AMG_KIND_DIAG,
+    Sgs = AMG_KIND_SGS,
+    Coarse = AMG_KIND_COARSE,
+    Multigrid = AMG_KIND_MULTIGRID,
+    DistCsr = AMG_KIND_DIST_CSR,
+    DistMultigrid = AMG_KIND_DIST_MULTIGRID
+};
+
+struct LinOp : std::enable_shared_from_this<LinOp> {
+    Ctx *ctx = nullptr;
+    int64_t nrows = 0, ncols = 0;
+    virtual ~LinOp() = default;
+    virtual Kind kind() const = 0;
+    // LinOp::apply -- out = M rhs (device, one column), out overwritten.
+    virtual void apply(double *out, const double *rhs) = 0;
+    // BiLinOp::transpose_apply -- symmetric operators reuse apply.
+    virtual void transpose_apply(double *out, const double *rhs) { apply(out, rhs); }
+    // Precond::apply_in_place -- default: copy to scratch, then apply.
+    virtual void apply_in_place(double *rhs);
+    virtual bool is_precond() const { return false; }
+
+  protected:
+    DevBuf<double> inplace_scratch_;
+};
+using LinOpPtr = std::shared_ptr<LinOp>;
+
+struct CsrOp : LinOp {
+    GpuCsr m;
+    DevBuf<double> diag_;  // cached a_ii (lazy)
+    std::shared_ptr<CsrOp> transpose_;  // lazy, for transpose_apply
+    Kind kind() const override { return Kind::Csr; }
+    void apply(double *out, const double *rhs) override;
+    void transpose_apply(double *out, const double *rhs) override;
+    const double *diagonal();
+};
+using CsrPtr = std::shared_ptr<CsrOp>;
+
+struct DiagOp : LinOp {
+    DevBuf<double> d;
+    Kind kind() const override { return Kind::Diag; }
+    bool is_precond() const override { return true; }
+    void apply(double *out, const double *rhs) override;
+    void apply_in_place(double *rhs) override;
+};
+
+struct SgsOp : LinOp {
+    CsrPtr A;              // original operator
+    GpuCsr Ap;             // rows grouped by color (columns in original numbering)
+    DevBuf<int32_t> perm;  // permuted row p -> original row
+    DevBuf<double> dinv;   // 1/a_ii at permuted rows
+    std::vector<int64_t> color_ptr;   // rows of color c: [color_ptr[c], color_ptr[c+1])
+    std::vector<int64_t> color_blk;   // schedule blocks of color c
+    std::vector<int32_t> host_colors;
+    int64_t ncolors = 0;
+    DevBuf<double> e_;     // scratch correction
+    Kind kind() const override { return Kind::Sgs; }
+    bool is_precond() const override { return true; }
+    // e = SGS(r) from e = 0 (device pointers, e != r)
+    void sweep(double *e, const double *r);
+    void apply(double *out, const double *rhs) override;
+    void apply_in_place(double *rhs) override;
+};
+
+struct CoarseCholOp : LinOp {
+    DevBuf<double> inv;  // dense A^{-1}, row-major
+    Kind kind() const override { return Kind::Coarse; }
+    bool is_precond() const override { return true; }
+    void apply(double *out, const double *rhs) override;
+};
+
+struct MgLevel {
+    LinOpPtr A, S, R, P;  // R, P: transfer to the next-coarser level (null on the coarsest)
+    // device workspaces (allocated lazily at first apply)
+    DevBuf<double> v, f, t, r;
+};
+
+struct MultigridOp : LinOp {
+    std::vector<MgLevel> levels;
+    int64_t mu = 1, steps = 1;
+    bool use_graph = true;
+    std::mutex mtx;
+    Kind kind() const override { return Kind::Multigrid; }
+    bool is_precond() const override { return true; }
+    void apply(double *out, const double *rhs) override;
+    void add_level(LinOpPtr A, LinOpPtr S, LinOpPtr R, LinOpPtr P);
+    void ensure_workspace();
+    void invalidate_graphs();
+    ~MultigridOp() override;
+
+    // V-cycle building blocks (also used by the distributed multigrid)
+    void cycle(int64_t l, double *v, const double *f, bool v_zero, double *out_final);
+    void smooth(int64_t l, double *&v, double *&t, const double *f, bool v_zero);
+
+  private:
+    struct GraphEntry {
+        double *out;
+        const double *rhs;
+        hipGraphExec_t exec;
+    };
+    std::vector<GraphEntry> graphs_;
+    bool workspace_ready_ = false;
+};
+
+// ---------------------------------------------------------------- factories
+
+CsrPtr make_csr(Ctx *ctx);
+std::shared_ptr<DiagOp> make_jacobi(CsrOp &A, double omega);
+std::shared_ptr<DiagOp> make_l1(CsrOp &A);
+std::shared_ptr<DiagOp> make_l2(CsrOp &A);
+std::shared_ptr<SgsOp> make_sgs(const CsrPtr &A, const int32_t *colors);
+std::shared_ptr<CoarseCholOp> make_coarse_chol(CsrOp &A);
+
+// SA setup pieces
+CsrPtr sa_tentative(Ctx *ctx, int64_t n, const int64_t *agg_of, int64_t naggs,
+                    const double *nn, double *coarse_nn);
+CsrPtr smooth_interpolation(CsrOp &A, const CsrOp &P, double omega);
+CsrPtr galerkin_rap(const CsrOp &R, const CsrOp &A, const CsrOp &P);
+CsrPtr transpose_op(const CsrOp &P);
+CsrPtr spgemm_op(const CsrOp &A, const CsrOp &B);
+void nn_stationary_l1(CsrOp &A, int64_t iters, double *x_host);
+int64_t greedy_coloring(const GpuCsr &A, std::vector<int32_t> &color);
+std::shared_ptr<MultigridOp> sa_build_box(const CsrPtr &A, int64_t nx, int64_t ny, int64_t nz,
+                                          int64_t bx, int64_t by, int64_t bz,
+                                          int64_t coarsest_dim, int64_t max_levels,
+                                          double omega, int smoother);
+
+}  // namespace famg

@@ -1,0 +1,661 @@
+// ops.hip -- LinOp implementations: CSR, diagonal smoothers, multicolor SGS,
+// coarse solve, and the multigrid V-cycle (reference
+// src/preconditioners/{smoothers,coarse_solvers,multigrid}.rs).
+//
+// The V-cycle keeps the reference's order of operations exactly
+// (multigrid.rs:269-380): pre-smooth, r = f - A v, f_c = R r, mu coarse cycles
+// from v_c = 0, v += P v_c, post-smooth; the coarsest level applies its
+// smoother (the coarse solve).  What changes is where the work runs and how it
+// is fused: every level's vectors are preallocated in HBM, `smooth`'s four
+// passes (A x, b - Ax, D r, x + r) are one SpMV with a Jacobi epilogue, the
+// residual and the interpolation-correction are SpMV epilogues, the first
+// smoothing step from v = 0 skips the SpMV (A 0 = 0 exactly), and a whole
+// V-cycle is captured once into a hipGraph and replayed.
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <numeric>
+
+#include "famg.hpp"
+
+namespace famg {
+
+void build_schedule(const std::vector<int64_t> &rp, const std::vector<int64_t> &seg_bounds,
+                    std::vector<int32_t> &sched, std::vector<int64_t> &seg_blocks);
+
+Ctx::~Ctx() {
+    if (host_red) (void)hipHostFree(host_red);
+    if (own_stream && stream) (void)hipStreamDestroy(stream);
+}
+
+// ------------------------------------------------------------------ LinOp
+
+void LinOp::apply_in_place(double *rhs) {
+    if (inplace_scratch_.size() < (size_t)nrows) inplace_scratch_.resize(nrows);
+    vec_copy(inplace_scratch_.get(), rhs, nrows, ctx->stream);
+    apply(rhs, inplace_scratch_.get());
+}
+
+CsrPtr make_csr(Ctx *ctx) {
+    auto p = std::make_shared<CsrOp>();
+    p->ctx = ctx;
+    return p;
+}
+
+void CsrOp::apply(double *out, const double *rhs) {
+    spmv(m, rhs, out, SPMV_SET, SpmvEpi{}, ctx->stream);
+}
+
+void CsrOp::transpose_apply(double *out, const double *rhs) {
+    if (!transpose_) transpose_ = transpose_op(*this);
+    transpose_->apply(out, rhs);
+}
+
+const double *CsrOp::diagonal() {
+    if (!diag_.get()) {
+        diag_.resize(m.nrows);
+        csr_diagonal(m, diag_.get());
+    }
+    return diag_.get();
+}
+
+// ------------------------------------------------------------- diagonal
+
+void DiagOp::apply(double *out, const double *rhs) { vec_mul(out, d.get(), rhs, nrows, ctx->stream); }
+void DiagOp::apply_in_place(double *rhs) { vec_mul(rhs, d.get(), rhs, nrows, ctx->stream); }
+
+__global__ void k_jacobi_diag(const double *aii, double omega, double *d, int64_t n) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i < n) d[i] = omega / aii[i];
+}
+__global__ void k_recip(double *d, int64_t n) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i < n) d[i] = 1.0 / d[i];
+}
+
+static std::shared_ptr<DiagOp> new_diag(Ctx *ctx, int64_t n) {
+    auto p = std::make_shared<DiagOp>();
+    p->ctx = ctx;
+    p->nrows = p->ncols = n;
+    p->d.resize(n);
+    return p;
+}
+
+// new_jacobi (smoothers.rs:78-86): d_i = omega / a_ii
+std::shared_ptr<DiagOp> make_jacobi(CsrOp &A, double omega) {
+    FAMG_REQUIRE(A.nrows == A.ncols, AMG_ERR_DIM, "jacobi: matrix must be square");
+    auto p = new_diag(A.ctx, A.nrows);
+    if (A.nrows)
+        hipLaunchKernelGGL(k_jacobi_diag, dim3((unsigned)ceil_div(A.nrows, 256)), dim3(256), 0,
+                           A.ctx->stream, A.diagonal(), omega, p->d.get(), A.nrows);
+    FAMG_CHECK_HIP(hipGetLastError());
+    return p;
+}
+
+// new_l1 (smoothers.rs:63-76): d_i = 1 / sum_j |a_ij|
+std::shared_ptr<DiagOp> make_l1(CsrOp &A) {
+    FAMG_REQUIRE(A.nrows == A.ncols, AMG_ERR_DIM, "l1: matrix must be square");
+    auto p = new_diag(A.ctx, A.nrows);
+    csr_abs_row_sums(A.m, p->d.get());
+    if (A.nrows)
+        hipLaunchKernelGGL(k_recip, dim3((unsigned)ceil_div(A.nrows, 256)), dim3(256), 0,
+                           A.ctx->stream, p->d.get(), A.nrows);
+    FAMG_CHECK_HIP(hipGetLastError());
+    return p;
+}
+
+// new_l2 (smoothers.rs:43-61): d_i = 1 / sum_j |a_ij| sqrt(a_ii)/sqrt(a_jj)
+__global__ void k_l2(const int64_t *rp, const int32_t *col, const double *val, const double *aii,
+                     double *d, int64_t n) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    const double si = sqrt(aii[i]);
+    double s = 0.0;
+    for (int64_t e = rp[i]; e < rp[i + 1]; e++) {
+        const double scale = si / sqrt(aii[col[e]]);
+        s += fabs(val[e]) * scale;
+    }
+    d[i] = 1.0 / s;
+}
+
+std::shared_ptr<DiagOp> make_l2(CsrOp &A) {
+    FAMG_REQUIRE(A.nrows == A.ncols, AMG_ERR_DIM, "l2: matrix must be square");
+    auto p = new_diag(A.ctx, A.nrows);
+    if (A.nrows)
+        hipLaunchKernelGGL(k_l2, dim3((unsigned)ceil_div(A.nrows, 256)), dim3(256), 0, A.ctx->stream,
+                           A.m.rp64.get(), A.m.col.get(), A.m.val.get(), A.diagonal(), p->d.get(),
+                           A.nrows);
+    FAMG_CHECK_HIP(hipGetLastError());
+    return p;
+}
+
+// --------------------------------------------------------- multicolor SGS
+
+int64_t greedy_coloring(const GpuCsr &A, std::vector<int32_t> &color) {
+    std::vector<int64_t> rp(A.nrows + 1), col(A.nnz);
+    std::vector<double> val(A.nnz);
+    csr_to_host(A, rp.data(), col.data(), val.data());
+    color.assign(A.nrows, 0);
+    std::vector<int64_t> mark(64, -1);
+    int64_t nc = 0;
+    for (int64_t i = 0; i < A.nrows; i++) {
+        for (int64_t e = rp[i]; e < rp[i + 1]; e++) {
+            const int64_t j = col[e];
+            if (j < i) {
+                const int32_t c = color[j];
+                if ((size_t)c >= mark.size()) mark.resize(2 * (c + 1), -1);
+                mark[c] = i;
+            }
+        }
+        int32_t c = 0;
+        while ((size_t)c < mark.size() && mark[c] == i) c++;
+        if ((size_t)c >= mark.size()) mark.resize(2 * mark.size(), -1);
+        color[i] = c;
+        nc = std::max<int64_t>(nc, c + 1);
+    }
+    return nc;
+}
+
+__global__ void k_perm_counts(const int64_t *rp, const int32_t *perm, int64_t n, int64_t *cnt) {
+    const int64_t p = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (p < n) cnt[p] = rp[perm[p] + 1] - rp[perm[p]];
+}
+__global__ void k_perm_rows(const int64_t *rp, const int32_t *col, const double *val,
+                            const int32_t *perm, int64_t n, const int64_t *prp, int32_t *pcol,
+                            double *pval, const double *aii, double *dinv) {
+    const int64_t p = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (p >= n) return;
+    const int32_t i = perm[p];
+    int64_t o = prp[p];
+    for (int64_t e = rp[i]; e < rp[i + 1]; e++, o++) {
+        pcol[o] = col[e];
+        pval[o] = val[e];
+    }
+    dinv[p] = 1.0 / aii[i];
+}
+// first forward color from e = 0: e_i = 0 + dinv (r_i - 0) = dinv r_i
+__global__ void k_sgs_first(const int32_t *perm, const double *dinv, const double *r, double *e,
+                            int64_t p0, int64_t p1) {
+    const int64_t p = p0 + (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (p < p1) {
+        const int32_t i = perm[p];
+        e[i] = dinv[p] * r[i];
+    }
+}
+
+std::shared_ptr<SgsOp> make_sgs(const CsrPtr &A, const int32_t *colors) {
+    FAMG_REQUIRE(A->nrows == A->ncols, AMG_ERR_DIM, "sgs: matrix must be square");
+    Ctx *ctx = A->ctx;
+    hipStream_t s = ctx->stream;
+    auto op = std::make_shared<SgsOp>();
+    op->ctx = ctx;
+    op->A = A;
+    op->nrows = op->ncols = A->nrows;
+    const int64_t n = A->nrows;
+    std::vector<int32_t> color;
+    if (colors) {
+        color.assign(colors, colors + n);
+        op->ncolors = 0;
+        for (int64_t i = 0; i < n; i++) {
+            FAMG_REQUIRE(color[i] >= 0, AMG_ERR_INVALID, "negative color");
+            op->ncolors = std::max<int64_t>(op->ncolors, color[i] + 1);
+        }
+        // validate: no two coupled rows share a color
+        std::vector<int64_t> rp(n + 1), col(A->m.nnz);
+        std::vector<double> val(A->m.nnz);
+        csr_to_host(A->m, rp.data(), col.data(), val.data());
+        for (int64_t i = 0; i < n; i++)
+            for (int64_t e = rp[i]; e < rp[i + 1]; e++)
+                FAMG_REQUIRE(col[e] == i || color[col[e]] != color[i], AMG_ERR_INVALID,
+                             "coloring couples two rows of the same color");
+    } else {
+        op->ncolors = greedy_coloring(A->m, color);
+    }
+    op->host_colors = color;
+    // stable counting sort of rows by color
+    op->color_ptr.assign(op->ncolors + 1, 0);
+    for (int64_t i = 0; i < n; i++) op->color_ptr[color[i] + 1]++;
+    for (int64_t c = 0; c < op->ncolors; c++) op->color_ptr[c + 1] += op->color_ptr[c];
+    std::vector<int32_t> perm(n);
+    {
+        std::vector<int64_t> pos(op->color_ptr.begin(), op->color_ptr.end() - 1);
+        for (int64_t i = 0; i < n; i++) perm[pos[color[i]]++] = (int32_t)i;
+    }
+    op->perm.resize(n);
+    FAMG_CHECK_HIP(hipMemcpyAsync(op->perm.get(), perm.data(), n * sizeof(int32_t), hipMemcpyHostToDevice, s));
+    DevBuf<int64_t> cnt(n);
+    const unsigned g = (unsigned)std::max<int64_t>(1, ceil_div(n, 256));
+    if (n) hipLaunchKernelGGL(k_perm_counts, dim3(g), dim3(256), 0, s, A->m.rp64.get(), op->perm.get(), n, cnt.get());
+    DevBuf<int64_t> prp(n + 1);
+    const int64_t nnz = scan_counts(cnt.get(), prp.get(), n, *ctx);
+    csr_alloc(op->Ap, ctx, n, n, nnz);
+    op->Ap.rp64 = std::move(prp);
+    op->dinv.resize(n);
+    if (n)
+        hipLaunchKernelGGL(k_perm_rows, dim3(g), dim3(256), 0, s, A->m.rp64.get(), A->m.col.get(),
+                           A->m.val.get(), op->perm.get(), n, op->Ap.rp64.get(), op->Ap.col.get(),
+                           op->Ap.val.get(), A->diagonal(), op->dinv.get());
+    FAMG_CHECK_HIP(hipGetLastError());
+    csr_finalize(op->Ap);  // rp32 (the generic schedule is replaced below)
+    FAMG_REQUIRE(op->Ap.spmv_ready(), AMG_ERR_UNSUPPORTED, "sgs: nnz must be < 2^31");
+    std::vector<int64_t> rp(n + 1);
+    FAMG_CHECK_HIP(hipMemcpyAsync(rp.data(), op->Ap.rp64.get(), (n + 1) * sizeof(int64_t), hipMemcpyDeviceToHost, s));
+    FAMG_CHECK_HIP(hipStreamSynchronize(s));
+    std::vector<int32_t> sched;
+    build_schedule(rp, op->color_ptr, sched, op->color_blk);
+    op->Ap.nblocks = (int64_t)sched.size() - 1;
+    op->Ap.sched.resize(sched.size());
+    FAMG_CHECK_HIP(hipMemcpyAsync(op->Ap.sched.get(), sched.data(), sched.size() * sizeof(int32_t), hipMemcpyHostToDevice, s));
+    FAMG_CHECK_HIP(hipStreamSynchronize(s));
+    op->e_.resize(n);
+    return op;
+}
+
+// e = SGS(r) from e = 0: forward colors 0..C-1, backward C-2..0.
+void SgsOp::sweep(double *e, const double *r) {
+    hipStream_t s = ctx->stream;
+    const int64_t n = nrows;
+    if (!n) return;
+    vec_fill(e, 0.0, n, s);
+    const int64_t p0 = color_ptr[0], p1 = color_ptr[1];
+    if (p1 > p0)
+        hipLaunchKernelGGL(k_sgs_first, dim3((unsigned)ceil_div(p1 - p0, 256)), dim3(256), 0, s,
+                           perm.get(), dinv.get(), r, e, p0, p1);
+    SpmvEpi epi;
+    epi.b = r;
+    epi.d = dinv.get();
+    epi.perm = perm.get();
+    for (int64_t c = 1; c < ncolors; c++) spmv(Ap, e, e, SPMV_SGS, epi, s, color_blk[c], color_blk[c + 1]);
+    for (int64_t c = ncolors - 2; c >= 0; c--) spmv(Ap, e, e, SPMV_SGS, epi, s, color_blk[c], color_blk[c + 1]);
+}
+
+void SgsOp::apply(double *out, const double *rhs) {
+    if (out == rhs) { apply_in_place(out); return; }
+    sweep(out, rhs);
+}
+
+void SgsOp::apply_in_place(double *rhs) {
+    sweep(e_.get(), rhs);
+    vec_copy(rhs, e_.get(), nrows, ctx->stream);
+}
+
+// ------------------------------------------------------------ coarse solve
+
+// Dense Cholesky on the host (setup) and the explicit inverse; the solve on the
+// device is one GEMV (8 n^2 bytes, L2/MALL resident for n <= ~2000).
+std::shared_ptr<CoarseCholOp> make_coarse_chol(CsrOp &A) {
+    FAMG_REQUIRE(A.nrows == A.ncols, AMG_ERR_DIM, "coarse solve: matrix must be square");
+    const int64_t n = A.nrows;
+    FAMG_REQUIRE(n <= 8192, AMG_ERR_UNSUPPORTED, "coarse Cholesky limited to 8192 rows (dense)");
+    std::vector<int64_t> rp(n + 1), col(A.m.nnz);
+    std::vector<double> val(A.m.nnz);
+    csr_to_host(A.m, rp.data(), col.data(), val.data());
+    std::vector<double> L((size_t)n * n, 0.0);
+    for (int64_t i = 0; i < n; i++)
+        for (int64_t e = rp[i]; e < rp[i + 1]; e++) L[(size_t)i * n + col[e]] += val[e];
+    // in-place lower Cholesky (row-major), left-looking
+    for (int64_t j = 0; j < n; j++) {
+        double sjj = L[(size_t)j * n + j];
+        for (int64_t k = 0; k < j; k++) sjj -= L[(size_t)j * n + k] * L[(size_t)j * n + k];
+        FAMG_REQUIRE(sjj > 0.0, AMG_ERR_NOT_SPD, "coarse matrix is not SPD (Cholesky pivot <= 0)");
+        const double ljj = std::sqrt(sjj);
+        L[(size_t)j * n + j] = ljj;
+#pragma omp parallel for schedule(static)
+        for (int64_t i = j + 1; i < n; i++) {
+            double t = L[(size_t)i * n + j];
+            for (int64_t k = 0; k < j; k++) t -= L[(size_t)i * n + k] * L[(size_t)j * n + k];
+            L[(size_t)i * n + j] = t / ljj;
+        }
+    }
+    // inverse: column j = L^-T L^-1 e_j ; stored row-major (symmetric)
+    std::vector<double> inv((size_t)n * n, 0.0);
+#pragma omp parallel for schedule(dynamic, 8)
+    for (int64_t j = 0; j < n; j++) {
+        std::vector<double> y(n, 0.0);
+        y[j] = 1.0;
+        for (int64_t i = j; i < n; i++) {
+            double t = y[i];
+            for (int64_t k = j; k < i; k++) t -= L[(size_t)i * n + k] * y[k];
+            y[i] = t / L[(size_t)i * n + i];
+        }
+        for (int64_t i = n - 1; i >= 0; i--) {
+            double t = y[i];
+            for (int64_t k = i + 1; k < n; k++) t -= L[(size_t)k * n + i] * y[k];
+            y[i] = t / L[(size_t)i * n + i];
+        }
+        for (int64_t i = 0; i < n; i++) inv[(size_t)i * n + j] = y[i];
+    }
+    auto op = std::make_shared<CoarseCholOp>();
+    op->ctx = A.ctx;
+    op->nrows = op->ncols = n;
+    op->inv.resize((size_t)n * n);
+    FAMG_CHECK_HIP(hipMemcpyAsync(op->inv.get(), inv.data(), inv.size() * sizeof(double),
+                                  hipMemcpyHostToDevice, A.ctx->stream));
+    FAMG_CHECK_HIP(hipStreamSynchronize(A.ctx->stream));
+    return op;
+}
+
+void CoarseCholOp::apply(double *out, const double *rhs) {
+    if (out == rhs) { LinOp::apply_in_place(out); return; }
+    dense_gemv(inv.get(), rhs, out, nrows, ctx->stream);
+}
+
+// --------------------------------------------------------------- multigrid
+
+MultigridOp::~MultigridOp() { invalidate_graphs(); }
+
+void MultigridOp::invalidate_graphs() {
+    for (auto &g : graphs_) (void)hipGraphExecDestroy(g.exec);
+    graphs_.clear();
+}
+
+void MultigridOp::add_level(LinOpPtr A, LinOpPtr S, LinOpPtr R, LinOpPtr P) {
+    FAMG_REQUIRE(!levels.empty(), AMG_ERR_INVALID, "add_level on an empty multigrid");
+    FAMG_REQUIRE(A && S && R && P, AMG_ERR_INVALID, "add_level: null operator");
+    const int64_t nf = levels.back().A->nrows, nc = A->nrows;
+    FAMG_REQUIRE(A->nrows == A->ncols, AMG_ERR_DIM, "add_level: op must be square");
+    FAMG_REQUIRE(S->nrows == nc && S->ncols == nc, AMG_ERR_DIM, "add_level: smoother size != op size");
+    FAMG_REQUIRE(P->nrows == nf && P->ncols == nc, AMG_ERR_DIM, "add_level: p must be n_fine x n_coarse");
+    FAMG_REQUIRE(R->nrows == nc && R->ncols == nf, AMG_ERR_DIM, "add_level: r must be n_coarse x n_fine");
+    levels.back().R = R;
+    levels.back().P = P;
+    MgLevel L;
+    L.A = A;
+    L.S = S;
+    levels.push_back(std::move(L));
+    workspace_ready_ = false;
+    invalidate_graphs();
+}
+
+void MultigridOp::ensure_workspace() {
+    if (workspace_ready_) return;
+    for (size_t l = 0; l < levels.size(); l++) {
+        const int64_t n = levels[l].A->nrows;
+        MgLevel &L = levels[l];
+        if (l > 0) { L.v.resize(n); L.f.resize(n); }
+        L.t.resize(n);
+        L.r.resize(n);
+    }
+    // make sure smoothers' own scratch exists before any graph capture
+    for (auto &L : levels) {
+        if (auto *sg = dynamic_cast<SgsOp *>(L.S.get())) (void)sg;
+    }
+    workspace_ready_ = true;
+}
+
+// smooth (multigrid.rs:407-424), `steps` times: x <- x + S (b - A x).
+// Fused forms per smoother; the first step from x = 0 needs no SpMV.
+// v/t are the two buffers of the level; Jacobi ping-pongs between them.
+void MultigridOp::smooth(int64_t l, double *&v, double *&t, const double *f, bool v_zero) {
+    MgLevel &L = levels[l];
+    const int64_t n = L.A->nrows;
+    hipStream_t s = ctx->stream;
+    auto *A = dynamic_cast<CsrOp *>(L.A.get());
+    auto *D = dynamic_cast<DiagOp *>(L.S.get());
+    auto *G = dynamic_cast<SgsOp *>(L.S.get());
+    for (int64_t it = 0; it < steps; it++) {
+        const bool zero = v_zero && it == 0;
+        if (A && D) {
+            if (zero) {
+                vec_mul(t, D->d.get(), f, n, s);  // 0 + d (f - A 0)
+            } else {
+                SpmvEpi epi;
+                epi.b = f;
+                epi.d = D->d.get();
+                spmv(A->m, v, t, SPMV_JACOBI, epi, s);
+            }
+            std::swap(v, t);
+        } else if (A && G) {
+            if (zero) {
+                G->sweep(v, f);  // e = SGS(f - A 0); v = 0 + e
+            } else {
+                SpmvEpi epi;
+                epi.b = f;
+                spmv(A->m, v, L.r.get(), SPMV_RESID, epi, s);
+                G->sweep(t, L.r.get());
+                vec_add_inplace(v, t, n, s);
+            }
+        } else {
+            if (zero) {
+                L.S->apply(v, f);
+            } else {
+                L.A->apply(t, v);
+                vec_sub(L.r.get(), f, t, n, s);
+                L.S->apply_in_place(L.r.get());
+                vec_add_inplace(v, L.r.get(), n, s);
+            }
+        }
+    }
+}
+
+// cycle (multigrid.rs:269-380).  The result ends in the buffer v points to on
+// entry (Jacobi ping-pong flips an even number of times: 2*steps).
+void MultigridOp::cycle(int64_t l, double *v, const double *f, bool v_zero, double *) {
+    MgLevel &L = levels[l];
+    hipStream_t s = ctx->stream;
+    const int64_t n = L.A->nrows;
+    if (l == (int64_t)levels.size() - 1) {
+        L.S->apply(v, f);  // smoother.apply(v, f) (:291)
+        return;
+    }
+    double *v0 = v;
+    double *t = (v == L.t.get()) ? L.v.get() : L.t.get();
+    smooth(l, v, t, f, v_zero);
+    auto *A = dynamic_cast<CsrOp *>(L.A.get());
+    if (A) {
+        SpmvEpi epi;
+        epi.b = f;
+        spmv(A->m, v, L.r.get(), SPMV_RESID, epi, s);  // work = f - A v (:341-342)
+    } else {
+        L.A->apply(L.r.get(), v);
+        vec_sub(L.r.get(), f, L.r.get(), n, s);
+    }
+    MgLevel &C = levels[l + 1];
+    L.R->apply(C.f.get(), L.r.get());  // f_c = R work (:343)
+    for (int64_t k = 0; k < mu; k++) cycle(l + 1, C.v.get(), C.f.get(), k == 0, nullptr);
+    auto *P = dynamic_cast<CsrOp *>(L.P.get());
+    if (P) {
+        spmv(P->m, C.v.get(), v, SPMV_ADD, SpmvEpi{}, s);  // v += P v_c (:349-350)
+    } else {
+        L.P->apply(L.r.get(), C.v.get());
+        vec_add_inplace(v, L.r.get(), n, s);
+    }
+    smooth(l, v, t, f, false);  // post-smoothing (:361-369)
+    if (v != v0) vec_copy(v0, v, n, s);
+}
+
+// LinOp::apply for Multigrid (multigrid.rs:469-473 / init_cycle :251-267):
+// out = V-cycle(rhs) from a zero guess.
+void MultigridOp::apply(double *out, const double *rhs) {
+    std::lock_guard<std::mutex> lk(mtx);
+    FAMG_REQUIRE(!levels.empty(), AMG_ERR_INVALID, "empty multigrid");
+    FAMG_REQUIRE(out != rhs, AMG_ERR_INVALID, "multigrid apply: out must not alias rhs");
+    for (size_t l = 0; l + 1 < levels.size(); l++)
+        FAMG_REQUIRE(levels[l].R && levels[l].P, AMG_ERR_INVALID, "multigrid level without R/P");
+    ensure_workspace();
+    hipStream_t s = ctx->stream;
+    auto run = [&]() { cycle(0, out, rhs, true, out); };
+    if (!use_graph || s == nullptr) {
+        run();
+        return;
+    }
+    for (auto &g : graphs_)
+        if (g.out == out && g.rhs == rhs) {
+            FAMG_CHECK_HIP(hipGraphLaunch(g.exec, s));
+            return;
+        }
+    hipGraph_t graph = nullptr;
+    FAMG_CHECK_HIP(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
+    try {
+        run();
+    } catch (...) {
+        (void)hipStreamEndCapture(s, &graph);
+        if (graph) (void)hipGraphDestroy(graph);
+        throw;
+    }
+    FAMG_CHECK_HIP(hipStreamEndCapture(s, &graph));
+    hipGraphExec_t exec = nullptr;
+    FAMG_CHECK_HIP(hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0));
+    (void)hipGraphDestroy(graph);
+    if (graphs_.size() >= 8) {
+        (void)hipGraphExecDestroy(graphs_.front().exec);
+        graphs_.erase(graphs_.begin());
+    }
+    graphs_.push_back({out, rhs, exec});
+    FAMG_CHECK_HIP(hipGraphLaunch(exec, s));
+}
+
+// ------------------------------------------------------------------- setup
+
+// Tentative SA interpolation, one candidate (interpolation/mod.rs:754-805).
+CsrPtr sa_tentative(Ctx *ctx, int64_t n, const int64_t *agg_of, int64_t naggs, const double *nn,
+                    double *coarse_nn) {
+    std::vector<double> ss(naggs, 0.0);
+    for (int64_t i = 0; i < n; i++) {
+        const int64_t J = agg_of[i];
+        FAMG_REQUIRE(J >= 0 && J < naggs, AMG_ERR_INVALID, "node not aggregated");
+        ss[J] = ss[J] + nn[i] * nn[i];
+    }
+    for (int64_t J = 0; J < naggs; J++) {
+        coarse_nn[J] = std::sqrt(ss[J]);
+        FAMG_REQUIRE(coarse_nn[J] > 0.0, AMG_ERR_INVALID, "aggregate with a zero candidate");
+    }
+    std::vector<int64_t> rp(n + 1), col(n);
+    std::vector<double> val(n);
+    for (int64_t i = 0; i < n; i++) {
+        rp[i] = i;
+        col[i] = agg_of[i];
+        val[i] = nn[i] / coarse_nn[agg_of[i]];
+    }
+    rp[n] = n;
+    auto P = make_csr(ctx);
+    csr_from_host(P->m, ctx, n, naggs, rp.data(), col.data(), val.data());
+    P->nrows = n;
+    P->ncols = naggs;
+    return P;
+}
+
+static CsrPtr wrap(Ctx *ctx, GpuCsr &&m) {
+    auto p = make_csr(ctx);
+    p->m = std::move(m);
+    p->nrows = p->m.nrows;
+    p->ncols = p->m.ncols;
+    return p;
+}
+
+CsrPtr spgemm_op(const CsrOp &A, const CsrOp &B) {
+    GpuCsr C;
+    spgemm(A.m, B.m, C);
+    return wrap(A.ctx, std::move(C));
+}
+
+CsrPtr transpose_op(const CsrOp &P) {
+    GpuCsr T;
+    transpose(P.m, T);
+    return wrap(P.ctx, std::move(T));
+}
+
+// smooth_interpolation (interpolation/mod.rs:927-946)
+CsrPtr smooth_interpolation(CsrOp &A, const CsrOp &P, double omega) {
+    FAMG_REQUIRE(A.nrows == A.ncols && A.ncols == P.nrows, AMG_ERR_DIM, "smooth_interpolation dims");
+    GpuCsr S;
+    spgemm(A.m, P.m, S);
+    smooth_interp_fixup(S, P.m, A.diagonal(), omega);
+    return wrap(A.ctx, std::move(S));
+}
+
+// A_c = R (A P) (interpolation/mod.rs:828)
+CsrPtr galerkin_rap(const CsrOp &R, const CsrOp &A, const CsrOp &P) {
+    FAMG_REQUIRE(R.ncols == A.nrows && A.ncols == P.nrows && R.nrows == P.ncols, AMG_ERR_DIM,
+                 "galerkin_rap dims");
+    GpuCsr AP, C;
+    spgemm(A.m, P.m, AP);
+    spgemm(R.m, AP, C);
+    return wrap(A.ctx, std::move(C));
+}
+
+__global__ void k_divs(double *x, double s, int64_t n) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i < n) x[i] = x[i] / s;
+}
+
+// hierarchy.rs:219-228 + smoothers.rs:146-158 (r = x - A x quirk) + thin QR
+void nn_stationary_l1(CsrOp &A, int64_t iters, double *x_host) {
+    Ctx &ctx = *A.ctx;
+    hipStream_t s = ctx.stream;
+    const int64_t n = A.nrows;
+    auto d = make_l1(A);
+    DevBuf<double> x(n), xin(n), r(n);
+    FAMG_CHECK_HIP(hipMemcpyAsync(xin.get(), x_host, n * sizeof(double), hipMemcpyHostToDevice, s));
+    vec_mul(x.get(), d->d.get(), xin.get(), n, s);
+    for (int64_t it = 1; it < iters; it++) {
+        spmv(A.m, x.get(), r.get(), SPMV_SET, SpmvEpi{}, s);
+        vec_nn_step(x.get(), d->d.get(), r.get(), n, s);
+    }
+    const double nrm = std::sqrt(vec_dot(x.get(), x.get(), n, ctx));
+    if (n) hipLaunchKernelGGL(k_divs, dim3((unsigned)ceil_div(n, 256)), dim3(256), 0, s, x.get(), nrm, n);
+    FAMG_CHECK_HIP(hipMemcpyAsync(x_host, x.get(), n * sizeof(double), hipMemcpyDeviceToHost, s));
+    FAMG_CHECK_HIP(hipStreamSynchronize(s));
+}
+
+// Hierarchy::coarsen (hierarchy.rs:190-248) with box aggregates, then a
+// Multigrid assembled as Multigrid::new / add_level (multigrid.rs:190-239).
+std::shared_ptr<MultigridOp> sa_build_box(const CsrPtr &A, int64_t nx, int64_t ny, int64_t nz,
+                                          int64_t bx, int64_t by, int64_t bz,
+                                          int64_t coarsest_dim, int64_t max_levels,
+                                          double omega, int smoother) {
+    FAMG_REQUIRE(nx * ny * nz == A->nrows, AMG_ERR_DIM, "grid dims do not match the matrix");
+    FAMG_REQUIRE(bx > 0 && by > 0 && bz > 0, AMG_ERR_INVALID, "box sizes must be positive");
+    Ctx *ctx = A->ctx;
+    if (max_levels <= 0) max_levels = INT64_MAX;
+    std::vector<CsrPtr> As{A}, Rs, Ps;
+    std::vector<double> nn(A->nrows, 1.0);
+    int64_t cx = nx, cy = ny, cz = nz;
+    int64_t level = 1, coarse_dim = -1;
+    while ((coarse_dim < 0 || coarse_dim > coarsest_dim) && level < max_levels) {
+        CsrPtr cur = As.back();
+        const int64_t n = cur->nrows;
+        const int64_t ncx = ceil_div(cx, bx), ncy = ceil_div(cy, by), ncz = ceil_div(cz, bz);
+        std::vector<int64_t> agg(n);
+        for (int64_t z = 0; z < cz; z++)
+            for (int64_t y = 0; y < cy; y++)
+                for (int64_t x = 0; x < cx; x++)
+                    agg[x + cx * (y + cy * z)] = x / bx + ncx * (y / by + ncy * (z / bz));
+        const int64_t na = ncx * ncy * ncz;
+        std::vector<double> cnn(na);
+        CsrPtr Pt = sa_tentative(ctx, n, agg.data(), na, nn.data(), cnn.data());
+        CsrPtr P = smooth_interpolation(*cur, *Pt, omega);
+        CsrPtr R = transpose_op(*P);
+        CsrPtr Ac = galerkin_rap(*R, *cur, *P);
+        nn_stationary_l1(*Ac, 3, cnn.data());
+        Rs.push_back(R);
+        Ps.push_back(P);
+        As.push_back(Ac);
+        nn.swap(cnn);
+        cx = ncx; cy = ncy; cz = ncz;
+        coarse_dim = Ac->nrows;
+        level++;
+    }
+    auto make_smoother = [&](const CsrPtr &M) -> LinOpPtr {
+        switch (smoother) {
+        case 0: return make_jacobi(*M, omega);
+        case 1: return make_l1(*M);
+        case 2: return make_sgs(M, nullptr);
+        default: fail(AMG_ERR_INVALID, "unknown smoother kind");
+        }
+    };
+    auto mg = std::make_shared<MultigridOp>();
+    mg->ctx = ctx;
+    mg->nrows = mg->ncols = A->nrows;
+    MgLevel L0;
+    L0.A = A;
+    L0.S = As.size() == 1 ? LinOpPtr(make_coarse_chol(*A)) : make_smoother(A);
+    mg->levels.push_back(std::move(L0));
+    for (size_t l = 1; l < As.size(); l++) {
+        LinOpPtr S = (l + 1 == As.size()) ? LinOpPtr(make_coarse_chol(*As[l])) : make_smoother(As[l]);
+        mg->add_level(As[l], S, Rs[l - 1], Ps[l - 1]);
+    }
+    return mg;
+}
+
+}  // namespace famg

@@ -1,0 +1,248 @@
+/*
+ * amg.h -- C ABI of the MI355X-native faer-amg V-cycle path (libfaer_amg_amd.so).
+ *
+ * One handle type, amg_linop, stands for the reference's `Arc<dyn LinOp<f64>>`
+ * (faer matrix_free::{LinOp, Precond, BiLinOp, BiPrecond}); every constructor
+ * returns one.  Handles are reference counted: amg_linop_destroy drops the
+ * caller's reference, and operators that hold other operators (a multigrid
+ * holding its A/S/R/P) keep their own.  Each entry point below names the
+ * reference interface it replaces (paths relative to the reference root).
+ *
+ * Errors: every function returns amg_status; AMG_OK is 0.  The message of the
+ * last failure on the calling thread is amg_last_error().  The reference
+ * panics instead; its binding panics on non-zero status.
+ *
+ * Memory: vectors are column-major n x k blocks with a leading dimension, as
+ * faer MatRef/MatMut.  AMG_MEM_DEVICE pointers are read/written
+ * asynchronously on the context's HIP stream (synchronise with
+ * amg_ctx_synchronize); AMG_MEM_HOST pointers are staged through the device
+ * and the call returns after the result is back on the host.
+ *
+ * Threading: handles are immutable after construction except through the
+ * amg_multigrid_add_level / amg_multigrid_set builders; apply calls on one
+ * handle must not run concurrently (workspaces are preallocated).
+ */
+#ifndef FAER_AMG_AMD_AMG_H
+#define FAER_AMG_AMD_AMG_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef enum amg_status {
+    AMG_OK = 0,
+    AMG_ERR_INVALID = 1,     /* bad argument (null handle, negative size, ...) */
+    AMG_ERR_DIM = 2,         /* dimension mismatch (the reference's assert_eq! panics) */
+    AMG_ERR_UNSUPPORTED = 3, /* valid input the library does not handle (e.g. nnz >= 2^31) */
+    AMG_ERR_NOT_SPD = 4,     /* Cholesky factorization failed */
+    AMG_ERR_HIP = 5,         /* HIP runtime error / no device */
+    AMG_ERR_RCCL = 6,        /* RCCL error */
+    AMG_ERR_OOM = 7          /* device allocation failed */
+} amg_status;
+
+typedef enum amg_mem { AMG_MEM_HOST = 0, AMG_MEM_DEVICE = 1 } amg_mem;
+
+typedef enum amg_linop_kind {
+    AMG_KIND_CSR = 0,       /* sparse matrix (SparseMatOp / ParSpmmOp / SparseRowMat) */
+    AMG_KIND_DIAG = 1,      /* Diag<f64> smoother: Jacobi, L1, L2 */
+    AMG_KIND_SGS = 2,       /* multicolor symmetric Gauss-Seidel */
+    AMG_KIND_COARSE = 3,    /* coarse Cholesky solve */
+    AMG_KIND_MULTIGRID = 4, /* Multigrid */
+    AMG_KIND_DIST_CSR = 5,  /* row-block distributed sparse matrix */
+    AMG_KIND_DIST_MULTIGRID = 6
+} amg_linop_kind;
+
+typedef struct amg_ctx amg_ctx;
+typedef struct amg_linop amg_linop;
+
+/* ---- errors, context ------------------------------------------------------ */
+
+/* Thread-local message of the last non-OK status on this thread ("" if none). */
+const char *amg_last_error(void);
+/* Library version string. */
+const char *amg_version(void);
+
+/* Bind device `device` (one process per GPU).  `hip_stream` may be NULL (the
+ * library creates its own non-blocking stream) or an existing hipStream_t to
+ * order work with the caller's (e.g. torch.cuda.current_stream()). */
+amg_status amg_ctx_create(int device, void *hip_stream, amg_ctx **out);
+amg_status amg_ctx_destroy(amg_ctx *ctx);
+amg_status amg_ctx_synchronize(amg_ctx *ctx);
+amg_status amg_ctx_stream(amg_ctx *ctx, void **hip_stream);
+
+/* ---- sparse matrices (replaces SparseMatOp::new core.rs:56-74, ParSpmmOp::new
+ *      par_spmm.rs:31-96, and the SparseRowMat<usize,f64> LinOp used at
+ *      multigrid.rs:137-158) -------------------------------------------------- */
+
+/* Copy a host CSR with usize-compatible (int64) row pointers and column indices
+ * and fp64 values to the device.  Columns must be sorted ascending within each
+ * row and in [0, ncols).  Stored internally with 32-bit indices: returns
+ * AMG_ERR_UNSUPPORTED if nrows, ncols or nnz >= 2^31. */
+amg_status amg_csr_create(amg_ctx *ctx, int64_t nrows, int64_t ncols, const int64_t *rowptr,
+                          const int64_t *colidx, const double *vals, amg_linop **out);
+/* Same from device arrays with 32-bit indices (copied). */
+amg_status amg_csr_create_device_i32(amg_ctx *ctx, int64_t nrows, int64_t ncols,
+                                     const int32_t *rowptr, const int32_t *colidx,
+                                     const double *vals, amg_linop **out);
+/* Number of stored entries of a CSR operator. */
+amg_status amg_csr_nnz(const amg_linop *op, int64_t *nnz);
+/* Copy a CSR operator back to host arrays (rowptr: nrows+1, colidx/vals: nnz). */
+amg_status amg_csr_download(const amg_linop *op, int64_t *rowptr, int64_t *colidx, double *vals);
+/* Device-side generators for the benchmark operators:
+ * 3-D 7-point Laplacian (6 / -1) and 3-D 27-point anisotropic Q1 diffusion on an
+ * nx*ny*nz Dirichlet interior grid; row = x + nx*(y + ny*z). */
+amg_status amg_gen_laplace3d_7pt(amg_ctx *ctx, int64_t nx, int64_t ny, int64_t nz,
+                                 amg_linop **out);
+amg_status amg_gen_aniso27(amg_ctx *ctx, int64_t nx, int64_t ny, int64_t nz, double ex,
+                           double ey, double ez, amg_linop **out);
+
+/* ---- generic LinOp / Precond / BiPrecond (faer matrix_free traits) -------- */
+
+amg_status amg_linop_kind_of(const amg_linop *op, int32_t *kind);
+/* LinOp::nrows / ncols */
+amg_status amg_linop_dims(const amg_linop *op, int64_t *nrows, int64_t *ncols);
+/* LinOp::apply: out = M * rhs, out overwritten (par_spmm.rs:117,151; multigrid.rs:469).
+ * out: nrows x k (ld_out), rhs: ncols x k (ld_rhs). */
+amg_status amg_linop_apply(amg_linop *op, double *out, int64_t ld_out, const double *rhs,
+                           int64_t ld_rhs, int64_t k, amg_mem mem);
+/* BiLinOp::transpose_apply.  Supported for the symmetric operators (smoothers,
+ * coarse solve, multigrid -- multigrid.rs:487-502) and for CSR matrices. */
+amg_status amg_linop_transpose_apply(amg_linop *op, double *out, int64_t ld_out,
+                                     const double *rhs, int64_t ld_rhs, int64_t k, amg_mem mem);
+/* Precond::apply_in_place: rhs <- M * rhs (coarse_solvers.rs:254; faer Diag). */
+amg_status amg_precond_apply_in_place(amg_linop *op, double *rhs, int64_t ld, int64_t k,
+                                      amg_mem mem);
+/* BiPrecond::transpose_apply_in_place (coarse_solvers.rs:270). */
+amg_status amg_precond_transpose_apply_in_place(amg_linop *op, double *rhs, int64_t ld,
+                                                int64_t k, amg_mem mem);
+/* Drop the caller's reference. */
+amg_status amg_linop_destroy(amg_linop *op);
+
+/* ---- smoothers (smoothers.rs:24-86) and coarse solver (coarse_solvers.rs) -- */
+
+/* new_jacobi: d_i = omega / a_ii (smoothers.rs:78-86). */
+amg_status amg_jacobi_create(const amg_linop *A, double omega, amg_linop **out);
+/* new_l1: d_i = 1 / sum_j |a_ij| (smoothers.rs:63-76). */
+amg_status amg_l1_create(const amg_linop *A, amg_linop **out);
+/* new_l2 (smoothers.rs:43-61). */
+amg_status amg_l2_create(const amg_linop *A, amg_linop **out);
+/* Diag from explicit host values (faer Diag<f64>). */
+amg_status amg_diag_create(amg_ctx *ctx, int64_t n, const double *d, amg_linop **out);
+/* SmootherKind::SymGaussSeidel (smoothers.rs:20,26 -- unimplemented! in the
+ * reference; definition in DESIGN.md): multicolor SGS on A e = r from e = 0.
+ * colors: host array of nrows colors in [0, ncolors) or NULL for greedy
+ * first-fit coloring in row order. */
+amg_status amg_sgs_create(const amg_linop *A, const int32_t *colors, amg_linop **out);
+/* Number of colors of an SGS smoother. */
+amg_status amg_sgs_ncolors(const amg_linop *op, int64_t *ncolors);
+/* CoarseSolverKind::Cholesky (coarse_solvers.rs:21-33, SparseCholeskySolve
+ * :172-181): exact coarse solve.  Returns AMG_ERR_NOT_SPD if A is not SPD and
+ * AMG_ERR_UNSUPPORTED above 16384 rows (dense factor). */
+amg_status amg_coarse_chol_create(const amg_linop *A, amg_linop **out);
+
+/* ---- multigrid (multigrid.rs:171-424) -------------------------------------- */
+
+/* Multigrid::new(op, smoother) (multigrid.rs:190-199): mu = 1, steps = 1. */
+amg_status amg_multigrid_create(amg_linop *op, amg_linop *smoother, amg_linop **out);
+/* Multigrid::add_level(op, smoother, r, p) (multigrid.rs:228-239).  r: n_c x n_f,
+ * p: n_f x n_c where n_f is the previous level's size and n_c = op's size;
+ * AMG_ERR_DIM otherwise (hierarchy.rs:258-264 asserts). */
+amg_status amg_multigrid_add_level(amg_linop *mg, amg_linop *op, amg_linop *smoother,
+                                   amg_linop *r, amg_linop *p);
+/* with_cycle_type(mu) / with_smoothing_steps(steps) (multigrid.rs:204-214); both > 0. */
+amg_status amg_multigrid_set(amg_linop *mg, int64_t mu, int64_t steps);
+amg_status amg_multigrid_levels(const amg_linop *mg, int64_t *levels);
+/* Enable/disable hipGraph capture of whole V-cycles (default on). */
+amg_status amg_multigrid_set_graph(amg_linop *mg, int32_t enable);
+/* Multigrid::apply == amg_linop_apply on a multigrid handle. */
+amg_status amg_multigrid_apply(amg_linop *mg, double *out, int64_t ld_out, const double *rhs,
+                               int64_t ld_rhs, int64_t k, amg_mem mem);
+
+/* ---- Galerkin setup kernels (interpolation/mod.rs:716-720, 824-828, 927-946) - */
+
+/* C = A * B (faer sparse x sparse). */
+amg_status amg_spgemm(const amg_linop *A, const amg_linop *B, amg_linop **out);
+/* R = P^T as a CSR (interpolation/mod.rs:824-827). */
+amg_status amg_transpose(const amg_linop *P, amg_linop **out);
+/* A_c = R * (A * P) (interpolation/mod.rs:828). */
+amg_status amg_galerkin_rap(const amg_linop *R, const amg_linop *A, const amg_linop *P,
+                            amg_linop **out);
+/* smooth_interpolation: P_s = A P scaled by -(omega/a_ii) per row, plus P
+ * (interpolation/mod.rs:927-946). */
+amg_status amg_smooth_interpolation(const amg_linop *A, const amg_linop *P, double omega,
+                                    amg_linop **out);
+/* Tentative SA interpolation for one candidate (interpolation/mod.rs:754-805):
+ * agg_of[i] in [0,naggs) (host), near_null (host, n); coarse_nn (host, naggs) out. */
+amg_status amg_sa_tentative(amg_ctx *ctx, int64_t n, const int64_t *agg_of, int64_t naggs,
+                            const double *near_null, amg_linop **P, double *coarse_nn);
+/* Coarse near-null post-processing (hierarchy.rs:219-228): L1 StationaryIteration
+ * (`iters` steps, smoothers.rs:146-158) then normalization; x is host, in/out. */
+amg_status amg_nn_stationary_l1(const amg_linop *A, int64_t iters, double *x);
+
+/* Smoothed-aggregation hierarchy on a structured nx*ny*nz grid with bx*by*bz box
+ * aggregates and one constant candidate (Hierarchy::coarsen, hierarchy.rs:190-248,
+ * box aggregates standing in for the modularity partitioner -- DESIGN.md).
+ * Coarsens until the coarse size <= coarsest_dim or max_levels (0 = unlimited).
+ * smoother: 0 Jacobi(omega), 1 L1, 2 SGS (greedy coloring) on every level but
+ * the coarsest, which gets the Cholesky coarse solve.  Returns the multigrid. */
+amg_status amg_sa_build_box(amg_linop *A, int64_t nx, int64_t ny, int64_t nz, int64_t bx,
+                            int64_t by, int64_t bz, int64_t coarsest_dim, int64_t max_levels,
+                            double omega, int32_t smoother, amg_linop **mg_out);
+/* Level accessors of a multigrid: A_l, R_l, P_l (l < levels-1), smoother S_l.
+ * Returned handles are new references. */
+amg_status amg_multigrid_get_level(const amg_linop *mg, int64_t level, amg_linop **A,
+                                   amg_linop **S, amg_linop **R, amg_linop **P);
+
+/* ---- solve drivers (the callers of the hot path) ------- */
+
+/* Stationary solver of examples/simple_geometric.rs:117-158 on device vectors:
+ * loop { r = b - A x; rho = ||r||/||b||; hist[it] = rho; stop if rho < rel_tol or
+ * it+1 >= max_iter; x += M r }.  b, x device pointers (n); hist host (max_iter).
+ * *iters = number of residual evaluations. */
+amg_status amg_stationary_solve(amg_linop *A, amg_linop *M, const double *b, double *x,
+                                int64_t max_iter, double rel_tol, double *hist, int64_t *iters);
+/* Preconditioned CG (faer conjugate_gradient caller, utils.rs:600): stops when
+ * ||r|| <= max(abs_tol, rel_tol ||b||); M may be NULL (identity).
+ * *iters = iterations (max_iter+1 if not converged); hist host (max_iter) gets
+ * ||r_k||/||b||. */
+amg_status amg_pcg_solve(amg_linop *A, amg_linop *M, const double *b, double *x,
+                         int64_t max_iter, double rel_tol, double abs_tol, double *hist,
+                         int64_t *iters);
+
+/* ---- multi-GPU (row-block partition + RCCL halo exchange) ------- */
+
+typedef struct amg_comm amg_comm;
+/* ncclUniqueId size in bytes (128). */
+int32_t amg_comm_unique_id_size(void);
+/* Fill `id` (amg_comm_unique_id_size() bytes) on rank 0; broadcast it out of band. */
+amg_status amg_comm_get_unique_id(void *id);
+/* One RCCL communicator per process (one process per GPU). */
+amg_status amg_comm_create(amg_ctx *ctx, int32_t nranks, int32_t rank, const void *id,
+                           amg_comm **out);
+amg_status amg_comm_destroy(amg_comm *comm);
+amg_status amg_comm_barrier(amg_comm *comm);
+/* Max over ranks of a host double (allreduce on the device). */
+amg_status amg_comm_allreduce_max(amg_comm *comm, double *value);
+
+/* Partition plan for rows [row_begin, row_end) of a global operator: given the
+ * global CSR (on this rank's device), extract the owned rows with the column
+ * space split into owned + ghost entries and the halo exchange plan.  Host logic
+ * exposed for tests: amg_dist_plan_info reports (n_owned, n_ghost, n_neighbors). */
+amg_status amg_dist_csr_create(amg_comm *comm, const amg_linop *A_global,
+                               const int64_t *row_splits, const int64_t *col_splits,
+                               amg_linop **out);
+amg_status amg_dist_plan_info(const amg_linop *dist, int64_t *info3);
+/* Distributed SA multigrid: every level row-block partitioned by the given
+ * global multigrid's sizes and z-slab splits; levels with fewer than
+ * agglomerate_rows global rows run redundantly on every rank. */
+amg_status amg_dist_multigrid_create(amg_comm *comm, const amg_linop *mg_global,
+                                     int64_t agglomerate_rows, amg_linop **out);
+/* Row range [begin, end) of this rank at the finest level. */
+amg_status amg_dist_local_rows(const amg_linop *dist, int64_t *begin, int64_t *end);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,361 @@
+"""GPU parity tests: the HIP path (through the C ABI) against the CPU oracle on
+the same inputs.  Tolerances (DESIGN.md "Parity"):
+  SpMV            |y - y_ref|_i <= 2 nnz_i u sum_j |a_ij x_j|   (bitwise for <=128-nnz rows)
+  one V-cycle     ||z - z_ref|| / ||z_ref|| <= 1e-11
+  residual hist   |rho_k - rho_ref_k| <= 1e-8 rho_ref_k + eps ||A||_inf ||x||_inf / ||b||_inf
+  RAP / SpGEMM    identical pattern, values bitwise (ascending-k fma in both)
+  PCG iterations  equal or +-1
+"""
+import os
+
+import numpy as np
+import pytest
+import scipy.sparse as sp
+
+import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+EPS = np.finfo(float).eps
+
+
+def load(name):
+    return np.load(os.path.join(GOLD, name), allow_pickle=False)
+
+
+def T(x):
+    import torch
+    return torch.as_tensor(np.ascontiguousarray(x, np.float64), device="cuda:0")
+
+
+def H(t):
+    import torch
+    torch.cuda.synchronize()
+    return t.detach().cpu().numpy()
+
+
+def fa():
+    import faer_amg_amd
+    return faer_amg_amd
+
+
+def gpu_csr(ctx, Ocsr):
+    m, n, _ = Ocsr.dims()
+    rp, ci, va = Ocsr.arrays()
+    return fa().SparseMatOp.from_arrays(ctx, m, n, rp, ci, va)
+
+
+def spmv_bound(S, x):
+    absx = abs(S) @ np.abs(x)
+    return 2 * np.diff(S.indptr) * 2.0**-53 * absx + 1e-300
+
+
+def apply_dev(ctx, op, x, nout):
+    xd = T(x)
+    yd = T(np.full(nout, np.nan))
+    op.apply(yd, xd)
+    ctx.synchronize()
+    return H(yd)
+
+
+# ------------------------------------------------------------------ SpMV
+
+def test_generators_bitwise(ctx):
+    A = fa().SparseMatOp.laplace3d_7pt(ctx, 9, 7, 5)
+    rp, ci, va = A.arrays()
+    orp, oci, ova = O.laplace3d_7pt(9, 7, 5).arrays()
+    assert np.array_equal(rp, orp) and np.array_equal(ci, oci) and np.array_equal(va, ova)
+    B = fa().SparseMatOp.aniso27(ctx, 6, 5, 7, 1.0, 1.0, 0.01)
+    rp, ci, va = B.arrays()
+    orp, oci, ova = O.aniso27(6, 5, 7).arrays()
+    assert np.array_equal(rp, orp) and np.array_equal(ci, oci) and np.array_equal(va, ova)
+
+
+def test_spmv_7pt_bitwise(ctx):
+    A = fa().SparseMatOp.laplace3d_7pt(ctx, 40, 33, 17)
+    OA = O.laplace3d_7pt(40, 33, 17)
+    x = np.random.default_rng(0).standard_normal(OA.ncols)
+    y = apply_dev(ctx, A, x, OA.nrows)
+    assert np.array_equal(y, OA.spmv(x))
+
+
+def test_spmv_27pt(ctx):
+    A = fa().SparseMatOp.aniso27(ctx, 20, 17, 11, 1.0, 1.0, 0.01)
+    OA = O.aniso27(20, 17, 11)
+    x = np.random.default_rng(1).standard_normal(OA.ncols)
+    y = apply_dev(ctx, A, x, OA.nrows)
+    assert np.all(np.abs(y - OA.spmv(x)) <= spmv_bound(OA.to_scipy(), x))
+
+
+def test_spmv_irregular_golden(ctx):
+    """Empty rows, 1-nnz rows, a 300-nnz row, a 3000-nnz row (whole-workgroup path)."""
+    g = load("g5_spmv_irregular.npz")
+    m, n = g["shape"]
+    A = fa().SparseMatOp.from_arrays(ctx, m, n, g["rowptr"], g["col"], g["val"])
+    y = apply_dev(ctx, A, g["x"], m)
+    S = sp.csr_matrix((g["val"], g["col"], g["rowptr"]), shape=(m, n))
+    assert np.all(np.abs(y - g["y"]) <= spmv_bound(S, g["x"]))
+    assert np.all(y[np.diff(g["rowptr"]) == 0] == 0)
+
+
+def test_spmv_host_memory_and_multicolumn(ctx):
+    OA = O.laplace3d_7pt(10, 10, 10)
+    A = gpu_csr(ctx, OA)
+    X = np.asfortranarray(np.random.default_rng(2).standard_normal((1000, 3)))
+    Y = np.asfortranarray(np.zeros((1000, 3)))
+    A.apply(Y, X)  # AMG_MEM_HOST, k = 3
+    for c in range(3):
+        assert np.array_equal(Y[:, c], OA.spmv(X[:, c]))
+
+
+def test_transpose_apply(ctx):
+    g = load("g3_sa7pt16.npz")
+    m, n = g["P0_shape"]
+    P = fa().SparseMatOp.from_arrays(ctx, m, n, g["P0_rowptr"], g["P0_col"], g["P0_val"])
+    x = np.random.default_rng(3).standard_normal(m)
+    out = np.zeros(n)
+    P.transpose_apply(out, x)
+    Ps = sp.csr_matrix((g["P0_val"], g["P0_col"], g["P0_rowptr"]), shape=(m, n))
+    assert np.allclose(out, Ps.T @ x, rtol=1e-13, atol=1e-13)
+
+
+def test_large_spmv_property(ctx):
+    """Full-size-style property check: A 1 == boundary-row deficits (integer exact)."""
+    import torch
+    nx = ny = nz = 96
+    A = fa().SparseMatOp.laplace3d_7pt(ctx, nx, ny, nz)
+    ones = torch.ones(nx * ny * nz, dtype=torch.float64, device="cuda:0")
+    y = torch.empty_like(ones)
+    A.apply(y, ones)
+    ctx.synchronize()
+    z, yy, x = np.meshgrid(np.arange(nz), np.arange(ny), np.arange(nx), indexing="ij")
+    expect = ((x == 0).astype(float) + (x == nx - 1) + (yy == 0) + (yy == ny - 1) + (z == 0)
+              + (z == nz - 1)).ravel()
+    assert np.array_equal(H(y), expect)
+
+
+# ------------------------------------------------------------- smoothers
+
+def test_diag_smoothers(ctx):
+    OA = O.aniso27(7, 6, 5)
+    A = gpu_csr(ctx, OA)
+    r = np.random.default_rng(4).standard_normal(OA.nrows)
+    for mk, ref in [(lambda: fa().new_jacobi(A, 0.66), O.jacobi_diag(OA, 0.66)),
+                    (lambda: fa().new_l1(A), O.l1_diag(OA)),
+                    (lambda: fa().new_l2(A), O.l2_diag(OA))]:
+        S = mk()
+        out = apply_dev(ctx, S, r, OA.nrows)
+        assert np.allclose(out, ref * r, rtol=2e-16 * 4, atol=0)
+        rd = T(r)
+        S.apply_in_place(rd)
+        assert np.allclose(H(rd), ref * r, rtol=8e-16, atol=0)
+
+
+def test_sgs_matches_oracle(ctx):
+    OA = O.aniso27(9, 8, 7)
+    A = gpu_csr(ctx, OA)
+    S = fa().SymGaussSeidel(A)
+    color, nc = O.greedy_coloring(OA)
+    assert S.ncolors == nc == 8
+    r = np.random.default_rng(5).standard_normal(OA.nrows)
+    e = apply_dev(ctx, S, r, OA.nrows)
+    eref = O.sgs_apply(OA, color, nc, r)
+    assert np.linalg.norm(e - eref) <= 1e-13 * np.linalg.norm(eref)
+    # explicit coloring, 7-pt red-black
+    OB = O.laplace3d_7pt(8, 8, 8)
+    B = gpu_csr(ctx, OB)
+    cb, ncb = O.greedy_coloring(OB)
+    SB = fa().SymGaussSeidel(B, colors=cb)
+    assert SB.ncolors == 2
+    r = np.random.default_rng(6).standard_normal(OB.nrows)
+    e = apply_dev(ctx, SB, r, OB.nrows)
+    assert np.array_equal(e, O.sgs_apply(OB, cb, ncb, r))  # 7-pt rows: bitwise
+    with pytest.raises(fa().AmgError):
+        fa().SymGaussSeidel(B, colors=np.zeros(OB.nrows, np.int32))  # invalid coloring
+
+
+def test_coarse_cholesky(ctx):
+    OA = O.laplace3d_7pt(8, 8, 8)
+    A = gpu_csr(ctx, OA)
+    C = fa().CoarseCholesky(A)
+    b = np.random.default_rng(7).standard_normal(OA.nrows)
+    x = apply_dev(ctx, C, b, OA.nrows)
+    assert np.linalg.norm(OA.to_scipy() @ x - b) <= 1e-12 * np.linalg.norm(b)
+    # not SPD -> AMG_ERR_NOT_SPD
+    neg = O.Csr.from_scipy(-OA.to_scipy())
+    with pytest.raises(fa().AmgError) as ei:
+        fa().CoarseCholesky(gpu_csr(ctx, neg))
+    assert ei.value.status == 4
+
+
+# ------------------------------------------------------------------- setup
+
+def csr_equal(G, Oc, exact=True, rtol=0.0):
+    rp, ci, va = G.arrays()
+    orp, oci, ova = Oc.arrays()
+    assert np.array_equal(rp, orp)
+    assert np.array_equal(ci, oci)
+    if exact:
+        assert np.array_equal(va, ova)
+    else:
+        assert np.max(np.abs(va - ova)) <= rtol * np.max(np.abs(ova))
+
+
+def test_spgemm_transpose_rap_bitwise(ctx):
+    OA = O.aniso27(10, 9, 8)
+    A = gpu_csr(ctx, OA)
+    agg, na, _ = O.box_aggregates((10, 9, 8), (2, 2, 2))
+    nn = 1.0 + 0.1 * np.random.default_rng(8).standard_normal(OA.nrows)
+    OPt, ocnn = O.sa_tentative(agg, na, nn)
+    Pt, cnn = fa().sa_tentative(ctx, agg, na, nn)
+    assert np.array_equal(cnn, ocnn)
+    csr_equal(Pt, OPt)
+    csr_equal(fa().spgemm(A, Pt), O.spgemm(OA, OPt))
+    OP = O.smooth_interpolation(OA, OPt, 0.66)
+    P = fa().smooth_interpolation(A, Pt, 0.66)
+    csr_equal(P, OP)
+    R = fa().transpose(P)
+    OR = O.transpose(OP)
+    csr_equal(R, OR)
+    csr_equal(fa().galerkin_rap(R, A, P), O.rap(OR, OA, OP))
+
+
+def test_spgemm_wide_rows(ctx):
+    """Products with > 512 distinct columns per row (larger LDS hash tables)."""
+    rng = np.random.default_rng(9)
+    M = sp.random(300, 2000, density=0.02, random_state=rng, format="csr")
+    N_ = sp.random(2000, 3000, density=0.03, random_state=rng, format="csr")
+    OM, ON = O.Csr.from_scipy(M), O.Csr.from_scipy(N_)
+    G = fa().spgemm(gpu_csr(ctx, OM), gpu_csr(ctx, ON))
+    csr_equal(G, O.spgemm(OM, ON))
+
+
+def test_sa_hierarchy_matches_oracle(ctx):
+    """sa_build_box (GPU SpGEMM setup) vs the oracle hierarchy driver."""
+    dims = (20, 18, 16)
+    OA = O.laplace3d_7pt(*dims)
+    A = fa().SparseMatOp.laplace3d_7pt(ctx, *dims)
+    mg = fa().sa_build_box(A, dims, (2, 2, 2), coarsest_dim=100)
+    olev = O.sa_hierarchy_box(OA, dims, (2, 2, 2), coarsest_dim=100)
+    assert mg.levels() == len(olev)
+    for l in range(mg.levels()):
+        Al, Sl, Rl, Pl = mg.level(l)
+        # level 0/1 exact; deeper levels see the near-null post-processing, which
+        # uses a tree-reduced norm on the GPU (rounding-level differences)
+        csr_equal(Al, olev[l]["A"], exact=False, rtol=1e-12)
+        if Rl is not None:
+            csr_equal(Pl, olev[l]["P"], exact=False, rtol=1e-12)
+            csr_equal(Rl, olev[l]["R"], exact=False, rtol=1e-12)
+
+
+# --------------------------------------------------------------- V-cycle
+
+def oracle_levels_from_gpu(mg, smoother):
+    levels = []
+    nl = mg.levels()
+    for l in range(nl):
+        Al, Sl, Rl, Pl = mg.level(l)
+        m, n = Al.dims()
+        d = {"A": O.Csr.from_arrays(m, n, *Al.arrays()),
+             "smoother": "chol" if l == nl - 1 else smoother}
+        if Rl is not None:
+            d["R"] = O.Csr.from_arrays(*Rl.dims(), *Rl.arrays())
+            d["P"] = O.Csr.from_arrays(*Pl.dims(), *Pl.arrays())
+        levels.append(d)
+    return levels
+
+
+@pytest.mark.parametrize("gen,dims,smoother", [
+    ("7pt", (24, 20, 18), "jacobi"),
+    ("27pt", (14, 12, 16), "sgs"),
+    ("27pt", (12, 12, 12), "l1"),
+])
+def test_vcycle_parity(ctx, gen, dims, smoother):
+    if gen == "7pt":
+        A = fa().SparseMatOp.laplace3d_7pt(ctx, *dims)
+    else:
+        A = fa().SparseMatOp.aniso27(ctx, *dims, 1.0, 1.0, 0.01)
+    mg = fa().sa_build_box(A, dims, (2, 2, 2), coarsest_dim=200, smoother=smoother)
+    levels = oracle_levels_from_gpu(mg, smoother)
+    import sys
+    sys.path.insert(0, GOLD)
+    from make_golden import splitmix_uniform
+    b = splitmix_uniform(A.nrows, 42)
+    for mu, steps in [(1, 1), (2, 2)]:
+        mg.with_cycle_type(mu).with_smoothing_steps(steps)
+        zref = O.Multigrid(levels, mu=mu, steps=steps).apply(b)
+        for graph in (True, False):
+            mg.set_graph(graph)
+            z = apply_dev(ctx, mg, b, A.nrows)
+            assert np.linalg.norm(z - zref) <= 1e-11 * np.linalg.norm(zref), (mu, steps, graph)
+    mg.with_cycle_type(1).with_smoothing_steps(1)
+    mg.set_graph(True)
+
+
+def test_vcycle_golden_fixtures(ctx):
+    """G3/G4 hierarchies uploaded as-is (Multigrid::new + add_level by hand)."""
+    for name, sm in [("g3_sa7pt16.npz", "jacobi"), ("g4_sa27pt12_sgs.npz", "sgs")]:
+        g = load(name)
+        nl = int(g["nlevels"][0])
+        ops = []
+        for l in range(nl):
+            m, n = g[f"A{l}_shape"]
+            ops.append(fa().SparseMatOp.from_arrays(ctx, m, n, g[f"A{l}_rowptr"], g[f"A{l}_col"], g[f"A{l}_val"]))
+        def smoother(A, l):
+            if l == nl - 1:
+                return fa().CoarseCholesky(A)
+            return fa().new_jacobi(A, 0.66) if sm == "jacobi" else fa().SymGaussSeidel(A)
+        mg = fa().Multigrid(ops[0], smoother(ops[0], 0))
+        for l in range(1, nl):
+            Rs, Ps = g[f"R{l - 1}_shape"], g[f"P{l - 1}_shape"]
+            R = fa().SparseMatOp.from_arrays(ctx, *Rs, g[f"R{l-1}_rowptr"], g[f"R{l-1}_col"], g[f"R{l-1}_val"])
+            P = fa().SparseMatOp.from_arrays(ctx, *Ps, g[f"P{l-1}_rowptr"], g[f"P{l-1}_col"], g[f"P{l-1}_val"])
+            mg.add_level(ops[l], smoother(ops[l], l), R, P)
+        z = apply_dev(ctx, mg, g["b"], len(g["b"]))
+        assert np.linalg.norm(z - g["z"]) <= 1e-11 * np.linalg.norm(g["z"])
+        import torch
+        x = torch.zeros(len(g["b"]), dtype=torch.float64, device="cuda:0")
+        it, hist = fa().stationary_solve(ops[0], mg, T(g["b"]), x, max_iter=len(g["hist"]), rel_tol=1e-300)
+        assert it == len(g["hist"])
+        OA = O.Csr.from_arrays(*g["A0_shape"], g["A0_rowptr"], g["A0_col"], g["A0_val"])
+        floor = EPS * abs(OA.to_scipy()).sum(axis=1).max() * np.max(np.abs(H(x))) / np.max(np.abs(g["b"]))
+        assert np.all(np.abs(hist - g["hist"]) <= 1e-8 * g["hist"] + floor)
+
+
+def test_add_level_dimension_errors(ctx):
+    A = fa().SparseMatOp.laplace3d_7pt(ctx, 4, 4, 4)
+    mg = fa().Multigrid(A, fa().new_jacobi(A))
+    B = fa().SparseMatOp.laplace3d_7pt(ctx, 2, 2, 2)
+    with pytest.raises(fa().AmgError) as ei:
+        mg.add_level(B, fa().new_jacobi(B), A, A)  # R/P with wrong shapes
+    assert ei.value.status == 2
+
+
+# ------------------------------------------------------------ solve drivers
+
+def test_c1_gmg2d_stationary_and_pcg(ctx):
+    """Config C1 (2-D 5-pt 127^2, 2-level, Jacobi 0.66, Cholesky coarsest)."""
+    import torch
+    g = load("g2_gmg2d_c1.npz")
+    ops = {}
+    for key in ("A0", "R0", "P0", "A1"):
+        m, n = g[f"{key}_shape"]
+        ops[key] = fa().SparseMatOp.from_arrays(ctx, m, n, g[f"{key}_rowptr"], g[f"{key}_col"], g[f"{key}_val"])
+    mg = fa().Multigrid(ops["A0"], fa().new_jacobi(ops["A0"], 0.66))
+    mg.add_level(ops["A1"], fa().CoarseCholesky(ops["A1"]), ops["R0"], ops["P0"])
+    n = ops["A0"].nrows
+    b = torch.ones(n, dtype=torch.float64, device="cuda:0")
+    z = torch.empty_like(b)
+    mg.apply(z, b)
+    ctx.synchronize()
+    assert np.linalg.norm(H(z) - g["z"]) <= 1e-11 * np.linalg.norm(g["z"])
+    x = torch.zeros_like(b)
+    it, hist = fa().stationary_solve(ops["A0"], mg, b, x, max_iter=30, rel_tol=1e-30)
+    OA = O.Csr.from_arrays(*g["A0_shape"], g["A0_rowptr"], g["A0_col"], g["A0_val"])
+    floor = EPS * abs(OA.to_scipy()).sum(axis=1).max() * np.max(np.abs(H(x)))
+    assert it == 30
+    assert np.all(np.abs(hist - g["hist"]) <= 1e-8 * g["hist"] + floor)
+    x.zero_()
+    it, _ = fa().pcg_solve(ops["A0"], mg, b, x, max_iter=6000, rel_tol=1e-8)
+    assert abs(it - int(g["pcg_iters"][0])) <= 1
