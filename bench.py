@@ -1,21 +1,23 @@
 """Benchmark: AMG V-cycle apply on MI355X (BASELINE.json metric).
 
   python bench.py [--gpus N] [--steps K] [--warmup W]
+  python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
 
-Step = one V-cycle (Multigrid::apply, multigrid.rs:469) of the smoothed-
-aggregation hierarchy of the 3-D 7-point Laplacian, 256^3 per GPU (config
-C2: 2^3 box aggregates, one constant candidate, weighted Jacobi omega=0.66,
-s=1, mu=1, Cholesky coarsest), b ~ U(-1,1) from splitmix64 seed 42, x0 = 0.
-Inputs are generated on the device and resident in HBM before timing.
+Step = one V-cycle (Multigrid::apply, reference multigrid.rs:469) of the
+smoothed-aggregation hierarchy of the 3-D 7-point Laplacian (config C2:
+2^3 box aggregates, one constant candidate, weighted Jacobi omega = 0.66,
+s = 1, mu = 1, Cholesky coarsest), b ~ U(-1,1) from splitmix64 seed 42,
+x0 = 0.  Matrices and vectors are generated on the device and resident in
+HBM before timing.
+
+N = 1: the 256^3 problem on one GPU.
+N > 1: weak scaling -- the global grid has N x 256^3 rows (N = 2: 256x256x512,
+4: 256x512x512, 8: 512^3 = config C4), every level is cut into N z-slabs
+(one per rank, RCCL halo exchange over xGMI before each SpMV), levels below
+--agglomerate rows are gathered and cycled redundantly on every rank.
+value = global V-cycles/s x N  (= 256^3-equivalent V-cycles/s, whole job).
 
 Prints ONE JSON line on rank 0 (stdout); diagnostics go to stderr.
-  value        V-cycles/s of the whole job (for N > 1: weak scaling, N z-slabs
-               of 256^3 -> reported as 256^3-equivalent V-cycles/s)
-  roofline     fine-level CSR SpMV kernel: algorithmic bytes / measured kernel
-               time (HIP events on the library stream) vs 8 TB/s HBM peak
-  cpu_baseline the oracle's restatement of the reference's rayon path
-               (ParSpmmOp 8192x8192 CSC tiles, usize indices, per-call
-               temporaries) on the same hierarchy, host threads stated
 """
 import argparse
 import json
@@ -27,6 +29,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "faer-amg_amd"))
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+METRIC = "V-cycles/s + fine-level SpMV GB/s vs HBM peak, 3D 7-pt Laplacian 256³"
 
 
 def log(*a):
@@ -34,6 +37,7 @@ def log(*a):
 
 
 def splitmix_uniform(n, seed=42):
+    """b ~ U(-1,1): z_i = splitmix64(seed + (i+1)*golden), u = (z>>11)*2^-53, b = 2u-1."""
     import numpy as np
     with np.errstate(over="ignore"):
         i = np.arange(1, n + 1, dtype=np.uint64)
@@ -61,8 +65,23 @@ def time_kernel(fn, iters, stream):
     return e0.elapsed_time(e1) / iters  # ms
 
 
+def weak_dims(n, N):
+    """N x n^3 rows: double z, then y, then x for powers of two; z-stack otherwise."""
+    d = [n, n, n]
+    if N & (N - 1) == 0:
+        k, ax = N, 2
+        while k > 1:
+            d[ax] *= 2
+            ax = (ax - 1) % 3
+            k //= 2
+    else:
+        d[2] *= N
+    return tuple(d)
+
+
 def cpu_baseline(mg, b, threads, budget_s=12.0, max_cycles=40):
-    """Reference-path restatement on the host (oracle ParSpmm + per-call temporaries)."""
+    """The reference's rayon path restated (oracle: ParSpmmOp 8192x8192 CSC tiles,
+    usize indices, per-call temporaries) on the same hierarchy."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import numpy as np
     import oracle as O
@@ -86,53 +105,57 @@ def cpu_baseline(mg, b, threads, budget_s=12.0, max_cycles=40):
         O.lib().orc_mg_apply(omg.h, b, out)
         cycles += 1
     dt = time.perf_counter() - t0
-    return cycles / dt, cycles, dt, out
+    return cycles / dt, cycles, dt
 
 
-def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=50)
-    ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--n", type=int, default=256, help="grid edge per GPU")
-    ap.add_argument("--box", type=int, default=2)
-    ap.add_argument("--smoother", default="jacobi", choices=["jacobi", "l1", "sgs"])
-    ap.add_argument("--problem", default="7pt", choices=["7pt", "27pt"])
-    ap.add_argument("--cpu-threads", type=int, default=int(os.environ.get("OMP_NUM_THREADS", "16")))
-    ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--no-graph", action="store_true")
-    args = ap.parse_args()
+def build_problem(fa, ctx, args, dims):
+    if args.problem == "7pt":
+        A = fa.SparseMatOp.laplace3d_7pt(ctx, *dims)
+    else:
+        A = fa.SparseMatOp.aniso27(ctx, *dims, 1.0, 1.0, 0.01)
+    mg = fa.sa_build_box(A, dims, (args.box,) * 3, coarsest_dim=1000, smoother=args.smoother)
+    return A, mg
 
+
+def vcycle_bytes(mg):
+    """Algorithmic bytes of one V-cycle (s = 1, mu = 1, zero initial guess) from the
+    per-kernel formulas of SURVEY.md 8(d)."""
+    tot = 0
+    nl = mg.levels()
+    for l in range(nl):
+        A, _, R, P = mg.level(l)
+        n, nnz = A.nrows, A.nnz
+        bA = 12 * nnz + 4 * (n + 1)
+        if l == nl - 1:
+            tot += 8 * n * n + 16 * n
+            continue
+        nc = R.nrows
+        tot += 24 * n                                  # first smoothing step from 0
+        tot += bA + 24 * n                             # residual
+        tot += 12 * R.nnz + 4 * (nc + 1) + 8 * n + 8 * nc   # restrict
+        tot += 12 * P.nnz + 4 * (n + 1) + 8 * nc + 16 * n   # interpolate + add
+        tot += bA + 32 * n                             # post-smoothing Jacobi
+    return tot
+
+
+def run_single(args):
     import numpy as np
     import torch
 
     import faer_amg_amd as fa
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    if world > 1 or args.gpus > 1:
-        raise SystemExit("multi-GPU bench: see bench_dist (not yet wired)")
-
     torch.cuda.set_device(0)
     stream = torch.cuda.Stream()
     torch.cuda.set_stream(stream)
     ctx = fa.Context(0, stream=stream.cuda_stream)
-    nx = ny = nz = args.n
+    dims = (args.edge,) * 3
     t0 = time.perf_counter()
-    if args.problem == "7pt":
-        A = fa.SparseMatOp.laplace3d_7pt(ctx, nx, ny, nz)
-    else:
-        A = fa.SparseMatOp.aniso27(ctx, nx, ny, nz, 1.0, 1.0, 0.01)
-    mg = fa.sa_build_box(A, (nx, ny, nz), (args.box,) * 3, coarsest_dim=1000,
-                         smoother=args.smoother)
+    A, mg = build_problem(fa, ctx, args, dims)
     mg.set_graph(not args.no_graph)
     torch.cuda.synchronize()
     setup_s = time.perf_counter() - t0
     n = A.nrows
-    levels = []
-    for l in range(mg.levels()):
-        Al, _, _, _ = mg.level(l)
-        levels.append({"n": Al.nrows, "nnz": Al.nnz})
+    levels = [{"n": mg.level(l)[0].nrows, "nnz": mg.level(l)[0].nnz} for l in range(mg.levels())]
     log(f"setup {setup_s:.2f}s levels={levels}")
 
     b_host = splitmix_uniform(n, 42)
@@ -142,7 +165,6 @@ def main():
         mg.apply(z, b)
     torch.cuda.synchronize()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    torch.cuda.synchronize()
     t_wall0 = time.perf_counter()
     e0.record(stream)
     for _ in range(args.steps):
@@ -151,9 +173,9 @@ def main():
     torch.cuda.synchronize()
     t_wall = time.perf_counter() - t_wall0
     ms_per_cycle = e0.elapsed_time(e1) / args.steps
-    cycles_per_s = 1000.0 / ms_per_cycle
 
-    # fine-level SpMV kernel, timed on the library stream with HIP events
+    # fine-level SpMV kernel (the one the V-cycle's fine smoothing/residual use),
+    # timed with HIP events on the library stream
     x = torch.as_tensor(splitmix_uniform(n, 7), device="cuda:0")
     y = torch.empty_like(x)
     for _ in range(3):
@@ -163,25 +185,43 @@ def main():
     bytes_spmv = spmv_bytes(n, n, nnz)
     achieved = bytes_spmv / (spmv_ms * 1e-3) / 1e9
 
-    # residual reduction of one V-cycle as a sanity figure
+    if args.ab:
+        ops = {}
+        for fmt in ("csr", "sell"):
+            fa.set_spmv_format(fmt)
+            ops[fmt] = (fa.SparseMatOp.laplace3d_7pt(ctx, *dims) if args.problem == "7pt"
+                        else fa.SparseMatOp.aniso27(ctx, *dims, 1.0, 1.0, 0.01))
+        fa.set_spmv_format("auto")
+        res = {k: [] for k in ops}
+        for _ in range(5):
+            for fmt, op in ops.items():
+                res[fmt].append(time_kernel(lambda: op.apply(y, x), 20, stream))
+        for fmt, v in res.items():
+            log(f"A/B fine SpMV {fmt}: median {np.median(v)*1e3:.1f} us  min {min(v)*1e3:.1f} us  "
+                f"-> {bytes_spmv / (min(v) * 1e-3) / 1e9:.0f} GB/s")
+        del ops
+
     r = torch.empty_like(b)
     A.apply(r, z)
     torch.cuda.synchronize()
     rho1 = float(torch.linalg.norm(b - r) / torch.linalg.norm(b))
+    vbytes = vcycle_bytes(mg)
 
     cpu = None
     if not args.no_cpu_baseline:
         try:
-            v, cyc, dt, _ = cpu_baseline(mg, b_host, args.cpu_threads)
+            v, cyc, dt = cpu_baseline(mg, b_host, args.cpu_threads)
             cpu = {"value": round(v, 4), "unit": "V-cycles/s", "cores": args.cpu_threads,
                    "kind": "port",
-                   "sample": f"{cyc} V-cycles of the same {nx}^3 hierarchy in {dt:.1f}s "
-                             f"(oracle ParSpmmOp restatement, OpenMP {args.cpu_threads} threads)"}
-        except Exception as e:  # baseline must not kill the GPU measurement
+                   "sample": f"{cyc} V-cycles of the same {args.edge}^3 hierarchy in {dt:.1f}s "
+                             f"(oracle restatement of the rayon path: ParSpmmOp 8192x8192 CSC "
+                             f"tiles, usize indices; OpenMP {args.cpu_threads} threads)"}
+        except Exception as e:  # the baseline must not kill the GPU measurement
             log(f"cpu baseline failed: {e!r}")
 
-    out = {
-        "metric": "V-cycles/s + fine-level SpMV GB/s vs HBM peak, 3D 7-pt Laplacian 256³",
+    cycles_per_s = 1000.0 / ms_per_cycle
+    return {
+        "metric": METRIC,
         "value": round(cycles_per_s, 3),
         "unit": "V-cycles/s",
         "n_gpus": 1,
@@ -192,23 +232,154 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "f64",
-        "data": "synthetic (device-generated 7-pt Laplacian, splitmix64 rhs seed 42)",
-        "config": {"workload": f"SA V-cycle, 3D {args.problem} {nx}^3, box {args.box}^3, "
+        "data": "synthetic (device-generated operator, splitmix64 rhs seed 42)",
+        "config": {"workload": f"SA V-cycle, 3D {args.problem} {args.edge}^3, box {args.box}^3, "
                                f"{args.smoother} s=1 mu=1, Cholesky coarsest",
                    "levels": len(levels), "fine_rows": n, "fine_nnz": nnz,
                    "hierarchy": levels, "setup_s": round(setup_s, 2),
                    "wall_ms_per_step": round(1000 * t_wall / args.steps, 4),
+                   "vcycle_algorithmic_GB": round(vbytes / 1e9, 3),
+                   "vcycle_GBs": round(vbytes / (ms_per_cycle * 1e-3) / 1e9, 1),
                    "rel_residual_after_1_cycle": rho1,
                    "parallelism": "single GPU"},
         "fine_spmv_gbs": round(achieved, 1),
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
-                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                     "traffic": None,
-                     "kernel": "spmv_stream_kernel<SET> on A_0",
+                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                     "kernel": "spmv_sell_kernel<SET> on A_0 (SELL-64)",
                      "bytes_per_launch": bytes_spmv, "ms_per_launch": round(spmv_ms, 5)},
         "cpu_baseline": cpu,
     }
-    print(json.dumps(out), flush=True)
+
+
+def run_dist(args, world, rank, local_rank):
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    import faer_amg_amd as fa
+
+    dist.init_process_group("gloo")
+    local_rank = local_rank % max(1, torch.cuda.device_count())
+    torch.cuda.set_device(local_rank)
+    stream = torch.cuda.Stream()
+    torch.cuda.set_stream(stream)
+    ctx = fa.Context(local_rank, stream=stream.cuda_stream)
+    dims = weak_dims(args.edge, world)
+    t0 = time.perf_counter()
+    fa.set_spmv_format("csr")  # global (setup) copy: no SELL needed
+    A, mg = build_problem(fa, ctx, args, dims)
+    fa.set_spmv_format("auto")
+    nl = mg.levels()
+    splits = fa.slab_splits(fa.box_level_dims(dims, (args.box,) * 3, nl), world)
+    obj = [fa.unique_id() if rank == 0 else None]
+    dist.broadcast_object_list(obj, src=0)
+    comm = fa.Comm(ctx, nranks=world, rank=rank, uid=obj[0])
+    dm = fa.DistMultigrid(comm, mg, splits, agglomerate_rows=args.agglomerate)
+    infos = [dm.level_info(l) for l in range(nl)]
+    del mg, A  # global fine levels are no longer needed on this rank
+    torch.cuda.synchronize()
+    setup_s = time.perf_counter() - t0
+    r0, r1 = dm.local_rows()
+    n_glob = int(np.prod(dims))
+    b = torch.as_tensor(splitmix_uniform(n_glob, 42)[r0:r1].copy(), device=f"cuda:{local_rank}")
+    z = torch.empty_like(b)
+    for _ in range(args.warmup):
+        dm.apply(z, b)
+    torch.cuda.synchronize()
+    dist.barrier()
+    t_start = time.perf_counter()
+    for _ in range(args.steps):
+        dm.apply(z, b)
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t_start
+    dist.barrier()
+    tmax = torch.tensor([el], dtype=torch.float64)
+    dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
+    el = float(tmax[0])
+    ms_per_cycle = 1000.0 * el / args.steps
+
+    # local fine SpMV kernel on this rank (owned rows, [owned|ghost] columns)
+    Al = dm.level_matrix(0, "A")
+    nloc, ncl = Al.dims()
+    xl = torch.as_tensor(splitmix_uniform(ncl, 7), device=f"cuda:{local_rank}")
+    yl = torch.empty(nloc, dtype=torch.float64, device=f"cuda:{local_rank}")
+    for _ in range(3):
+        Al.apply(yl, xl)
+    spmv_ms = time_kernel(lambda: Al.apply(yl, xl), 20, stream)
+    bytes_spmv = spmv_bytes(nloc, nloc, Al.nnz)
+    achieved = bytes_spmv / (spmv_ms * 1e-3) / 1e9
+    # distributed fine SpMV including the halo exchange
+    Ad = dm.level_operator(0)
+    for _ in range(3):
+        Ad.apply(yl, b)
+    dist.barrier()
+    halo_ms = time_kernel(lambda: Ad.apply(yl, b), 20, stream)
+
+    # residual after one cycle (global)
+    x = torch.zeros_like(b)
+    it, hist = dm.stationary_solve(b, x, max_iter=2, rel_tol=1e-300)
+    ga = torch.tensor([achieved], dtype=torch.float64)
+    dist.all_reduce(ga, op=dist.ReduceOp.MIN)
+    cycles_per_s = 1000.0 / ms_per_cycle
+    out = {
+        "metric": METRIC,
+        "value": round(cycles_per_s * world, 3),
+        "unit": "V-cycles/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(ms_per_cycle, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic (device-generated operator, splitmix64 rhs seed 42)",
+        "config": {"workload": f"SA V-cycle, 3D {args.problem} {dims[0]}x{dims[1]}x{dims[2]} "
+                               f"({world} x {args.edge}^3 rows), box {args.box}^3, {args.smoother} "
+                               f"s=1 mu=1, Cholesky coarsest; value = global V-cycles/s x {world}",
+                   "global_vcycles_per_s": round(cycles_per_s, 3),
+                   "levels": nl, "level_plan_rank0": infos, "setup_s": round(setup_s, 2),
+                   "fine_spmv_with_halo_ms": round(halo_ms, 4),
+                   "rel_residual_after_1_cycle": float(hist[1]) if len(hist) > 1 else None,
+                   "agglomerate_rows": args.agglomerate,
+                   "parallelism": f"row-block z-slabs x{world}, RCCL halo exchange"},
+        "fine_spmv_gbs": round(float(ga[0]), 1),
+        "roofline": {"bound": "hbm", "achieved": round(float(ga[0]), 1), "peak": HBM_PEAK_GBS,
+                     "unit": "GB/s", "frac": round(float(ga[0]) / HBM_PEAK_GBS, 4), "traffic": None,
+                     "kernel": "spmv_sell_kernel<SET> on the rank-local A_0 (min over ranks)",
+                     "bytes_per_launch": bytes_spmv, "ms_per_launch": round(spmv_ms, 5)},
+        "cpu_baseline": None,
+    }
+    dist.destroy_process_group()
+    return out if rank == 0 else None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--edge", type=int, default=256, help="grid edge per GPU")
+    ap.add_argument("--box", type=int, default=2)
+    ap.add_argument("--smoother", default="jacobi", choices=["jacobi", "l1", "sgs"])
+    ap.add_argument("--problem", default="7pt", choices=["7pt", "27pt"])
+    ap.add_argument("--agglomerate", type=int, default=8192,
+                    help="levels with fewer global rows run redundantly on every rank")
+    ap.add_argument("--cpu-threads", type=int, default=int(os.environ.get("OMP_NUM_THREADS", "16")))
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--ab", action="store_true", help="A/B the SpMV storage formats (stderr)")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        out = run_dist(args, world, rank, local_rank)
+    else:
+        out = run_single(args)
+    if out is not None:
+        print(json.dumps(out), flush=True)
 
 
 if __name__ == "__main__":

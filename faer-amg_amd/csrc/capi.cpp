@@ -6,41 +6,20 @@
 #include <cstring>
 #include <string>
 
-#include "famg.hpp"
+#include "handles.hpp"
 
 using namespace famg;
 
-struct amg_ctx {
-    Ctx ctx;
-    DevBuf<double> stage_in, stage_out;  // host-memory staging
-};
-
-struct amg_linop {
-    LinOpPtr op;
-};
-
 namespace {
 thread_local std::string g_last_error;
+}
 
-amg_status set_err(amg_status s, const std::string &m) {
-    g_last_error = m;
+amg_status famg::set_last_error(amg_status s, const char *msg) {
+    g_last_error = msg;
     return s;
 }
 
-template <typename F> amg_status guard(F &&f) {
-    try {
-        f();
-        g_last_error.clear();
-        return AMG_OK;
-    } catch (const AmgError &e) {
-        return set_err(e.status, e.what());
-    } catch (const std::bad_alloc &) {
-        return set_err(AMG_ERR_OOM, "host allocation failed");
-    } catch (const std::exception &e) {
-        return set_err(AMG_ERR_INVALID, e.what());
-    }
-}
-
+namespace {
 amg_linop *box(LinOpPtr p) { return new amg_linop{std::move(p)}; }
 
 LinOp &need(const amg_linop *h) {
@@ -150,6 +129,30 @@ amg_status amg_ctx_stream(amg_ctx *ctx, void **hip_stream) {
     return guard([&] {
         FAMG_REQUIRE(ctx && hip_stream, AMG_ERR_INVALID, "null argument");
         *hip_stream = ctx->ctx.stream;
+    });
+}
+
+amg_status amg_ctx_join_stream(amg_ctx *ctx, void *other, int32_t ctx_waits) {
+    return guard([&] {
+        FAMG_REQUIRE(ctx, AMG_ERR_INVALID, "null context");
+        hipStream_t o = static_cast<hipStream_t>(other);
+        if (o == ctx->ctx.stream) return;
+        ctx->ctx.set_device();
+        if (!ctx->join_event) FAMG_CHECK_HIP(hipEventCreateWithFlags(&ctx->join_event, hipEventDisableTiming));
+        if (ctx_waits) {
+            FAMG_CHECK_HIP(hipEventRecord(ctx->join_event, o));
+            FAMG_CHECK_HIP(hipStreamWaitEvent(ctx->ctx.stream, ctx->join_event, 0));
+        } else {
+            FAMG_CHECK_HIP(hipEventRecord(ctx->join_event, ctx->ctx.stream));
+            FAMG_CHECK_HIP(hipStreamWaitEvent(o, ctx->join_event, 0));
+        }
+    });
+}
+
+amg_status amg_set_spmv_format(int32_t policy) {
+    return guard([&] {
+        FAMG_REQUIRE(policy >= 0 && policy <= 2, AMG_ERR_INVALID, "policy must be 0, 1 or 2");
+        g_spmv_format_policy = policy;
     });
 }
 

@@ -61,6 +61,7 @@ void csr_finalize(GpuCsr &m) {
     FAMG_CHECK_HIP(hipMemcpyAsync(m.sched.get(), sched.data(), sched.size() * sizeof(int32_t),
                                   hipMemcpyHostToDevice, ctx.stream));
     FAMG_CHECK_HIP(hipStreamSynchronize(ctx.stream));
+    build_sell(m, rp);
 }
 
 void csr_from_host(GpuCsr &m, Ctx *ctx, int64_t nrows, int64_t ncols, const int64_t *rowptr,

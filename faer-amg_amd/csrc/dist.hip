@@ -1,0 +1,818 @@
+// dist.hip -- multi-GPU V-cycle: row-block partition of every level, halo
+// exchange before each SpMV, agglomeration of the coarse levels.
+//
+// The reference is shared-memory only (rayon), so this
+// layer is new.  One process per GPU; rank p owns a contiguous row range of
+// every level.  Per level the rank's vector space is laid out [owned | ghost]
+// with the ghosts sorted by global index (so grouped by owner rank): a local
+// matrix row keeps its global column order, which keeps every row sum in the
+// same order as the single-GPU path (bitwise equal for short rows).
+// The ghost set of level l is the union of the columns referenced by A_l, R_l
+// (fine columns) and P_{l-1} (coarse columns) rows owned here, so one halo
+// exchange per vector refresh serves all three.  The exchange packs the
+// requested owned entries into a send buffer and runs grouped point-to-point
+// sends/receives straight into the ghost region of the peer's vector.
+// Levels below `agglomerate_rows` are all-gathered and cycled redundantly by
+// every rank with the single-GPU MultigridOp (the global coarse operators).
+//
+// Transports: RCCL (ncclSend/ncclRecv/ncclAllGather/ncclAllReduce on the
+// context stream, over xGMI) and a loopback hub (virtual ranks as host threads
+// of one process sharing one GPU) that validates the whole algorithm on a
+// single device.
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <condition_variable>
+#include <cstring>
+#include <mutex>
+
+#include "handles.hpp"
+
+using namespace famg;
+
+namespace famg {
+
+// ------------------------------------------------------------- transports
+
+struct Peer {
+    int rank;
+    const void *sbuf;
+    int64_t sbytes;
+    void *rbuf;
+    int64_t rbytes;
+};
+
+struct Transport {
+    int nranks = 1, rank = 0;
+    virtual ~Transport() = default;
+    virtual void exchange(const std::vector<Peer> &peers, hipStream_t s) = 0;
+    virtual void allgather(const void *sbuf, void *rbuf, int64_t bytes, hipStream_t s) = 0;
+    virtual void allreduce(double *buf, int64_t count, bool is_max, hipStream_t s) = 0;
+    virtual void barrier(hipStream_t s) = 0;
+};
+
+#define FAMG_CHECK_NCCL(expr)                                                              \
+    do {                                                                                   \
+        ncclResult_t r_ = (expr);                                                          \
+        if (r_ != ncclSuccess)                                                             \
+            ::famg::fail(AMG_ERR_RCCL, std::string(#expr) + ": " + ncclGetErrorString(r_)); \
+    } while (0)
+
+struct RcclTransport : Transport {
+    ncclComm_t comm = nullptr;
+    DevBuf<double> one;
+    ~RcclTransport() override {
+        if (comm) ncclCommDestroy(comm);
+    }
+    void exchange(const std::vector<Peer> &peers, hipStream_t s) override {
+        if (peers.empty()) return;
+        FAMG_CHECK_NCCL(ncclGroupStart());
+        for (const Peer &p : peers) {
+            if (p.sbytes) FAMG_CHECK_NCCL(ncclSend(p.sbuf, p.sbytes, ncclUint8, p.rank, comm, s));
+            if (p.rbytes) FAMG_CHECK_NCCL(ncclRecv(p.rbuf, p.rbytes, ncclUint8, p.rank, comm, s));
+        }
+        FAMG_CHECK_NCCL(ncclGroupEnd());
+    }
+    void allgather(const void *sbuf, void *rbuf, int64_t bytes, hipStream_t s) override {
+        FAMG_CHECK_NCCL(ncclAllGather(sbuf, rbuf, bytes, ncclUint8, comm, s));
+    }
+    void allreduce(double *buf, int64_t count, bool is_max, hipStream_t s) override {
+        FAMG_CHECK_NCCL(ncclAllReduce(buf, buf, count, ncclDouble, is_max ? ncclMax : ncclSum, comm, s));
+    }
+    void barrier(hipStream_t s) override {
+        if (one.size() < 1) one.resize(1);
+        FAMG_CHECK_NCCL(ncclAllReduce(one.get(), one.get(), 1, ncclDouble, ncclSum, comm, s));
+        FAMG_CHECK_HIP(hipStreamSynchronize(s));
+    }
+};
+
+// Virtual ranks in one process: every collective is a rendezvous of the rank
+// threads; data moves with device-to-device copies issued by the receiver.
+struct LoopbackHub {
+    int nranks;
+    std::mutex mu;
+    std::condition_variable cv;
+    int arrived = 0;
+    uint64_t generation = 0;
+    std::vector<const std::vector<Peer> *> posted;
+    std::vector<const void *> gptr;
+    explicit LoopbackHub(int n) : nranks(n), posted(n), gptr(n) {}
+    void wait() {
+        std::unique_lock<std::mutex> lk(mu);
+        const uint64_t g = generation;
+        if (++arrived == nranks) {
+            arrived = 0;
+            generation++;
+            cv.notify_all();
+        } else {
+            cv.wait(lk, [&] { return generation != g; });
+        }
+    }
+};
+
+struct LoopbackTransport : Transport {
+    std::shared_ptr<LoopbackHub> hub;
+    void exchange(const std::vector<Peer> &peers, hipStream_t s) override {
+        FAMG_CHECK_HIP(hipStreamSynchronize(s));
+        hub->posted[rank] = &peers;
+        hub->wait();
+        for (const Peer &p : peers) {
+            if (!p.rbytes) continue;
+            const Peer *src = nullptr;
+            for (const Peer &q : *hub->posted[p.rank])
+                if (q.rank == rank) src = &q;
+            FAMG_REQUIRE(src && src->sbytes == p.rbytes, AMG_ERR_INVALID, "loopback: unmatched exchange");
+            FAMG_CHECK_HIP(hipMemcpyAsync(p.rbuf, src->sbuf, p.rbytes, hipMemcpyDeviceToDevice, s));
+        }
+        FAMG_CHECK_HIP(hipStreamSynchronize(s));
+        hub->wait();
+    }
+    void allgather(const void *sbuf, void *rbuf, int64_t bytes, hipStream_t s) override {
+        FAMG_CHECK_HIP(hipStreamSynchronize(s));
+        hub->gptr[rank] = sbuf;
+        hub->wait();
+        for (int q = 0; q < nranks; q++)
+            FAMG_CHECK_HIP(hipMemcpyAsync(static_cast<char *>(rbuf) + q * bytes, hub->gptr[q], bytes,
+                                          hipMemcpyDeviceToDevice, s));
+        FAMG_CHECK_HIP(hipStreamSynchronize(s));
+        hub->wait();
+    }
+    void allreduce(double *buf, int64_t count, bool is_max, hipStream_t s) override {
+        FAMG_CHECK_HIP(hipStreamSynchronize(s));
+        hub->gptr[rank] = buf;
+        hub->wait();
+        std::vector<double> acc(count), tmp(count);
+        for (int q = 0; q < nranks; q++) {
+            FAMG_CHECK_HIP(hipMemcpy(tmp.data(), hub->gptr[q], count * sizeof(double), hipMemcpyDeviceToHost));
+            for (int64_t i = 0; i < count; i++)
+                acc[i] = q == 0 ? tmp[i] : (is_max ? std::max(acc[i], tmp[i]) : acc[i] + tmp[i]);
+        }
+        hub->wait();  // everyone has read before anyone writes
+        FAMG_CHECK_HIP(hipMemcpy(buf, acc.data(), count * sizeof(double), hipMemcpyHostToDevice));
+        hub->wait();
+    }
+    void barrier(hipStream_t s) override {
+        FAMG_CHECK_HIP(hipStreamSynchronize(s));
+        hub->wait();
+    }
+};
+
+}  // namespace famg
+
+struct amg_loopback_hub {
+    std::shared_ptr<LoopbackHub> hub;
+};
+
+struct amg_comm {
+    Ctx *ctx;
+    std::shared_ptr<Transport> tr;
+};
+
+namespace famg {
+
+// --------------------------------------------------------------- kernels
+
+__global__ void k_extract_rp(const int64_t *rp, int64_t r0, int64_t n, int64_t *out) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i <= n) out[i] = rp[r0 + i] - rp[r0];
+}
+
+// mark[c] = 1 for every referenced column outside [c0, c1)
+__global__ void k_mark_ghost(const int32_t *col, int64_t nnz, int64_t c0, int64_t c1, int64_t *mark) {
+    const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (e < nnz) {
+        const int64_t c = col[e];
+        if (c < c0 || c >= c1) mark[c] = 1;
+    }
+}
+
+__global__ void k_compact_ghost(const int64_t *mark, const int64_t *scan, int64_t n, int64_t *ids) {
+    const int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (j < n && mark[j]) ids[scan[j]] = j;
+}
+
+__global__ void k_remap_cols(int32_t *col, int64_t nnz, int64_t c0, int64_t c1, int64_t n_own,
+                             const int64_t *scan) {
+    const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (e < nnz) {
+        const int64_t c = col[e];
+        col[e] = (c >= c0 && c < c1) ? (int32_t)(c - c0) : (int32_t)(n_own + scan[c]);
+    }
+}
+
+__global__ void k_gather_idx(const double *x, const int32_t *idx, int64_t n, double *out) {
+    const int64_t k = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (k < n) out[k] = x[idx[k]];
+}
+
+static unsigned g1(int64_t n) { return (unsigned)std::max<int64_t>(1, ceil_div(n, 256)); }
+
+// -------------------------------------------------------- vector spaces
+
+struct Space {
+    bool redundant = false;
+    int64_t n_glob = 0, r0 = 0, r1 = 0, n_own = 0, n_ghost = 0;
+    std::vector<int64_t> splits;          // nranks+1
+    DevBuf<int64_t> mark, scan;           // setup only (global length)
+    std::vector<int64_t> ghost_ids;
+    // halo plan
+    std::vector<int> nbr;
+    std::vector<int64_t> soff, scnt, roff, rcnt;
+    DevBuf<int32_t> send_idx;
+    DevBuf<double> sendbuf;
+    std::vector<Peer> peers;              // rebuilt per vector (rbuf differs)
+    int64_t nsend = 0;
+    int owner(int64_t g) const {
+        return int(std::upper_bound(splits.begin(), splits.end(), g) - splits.begin()) - 1;
+    }
+};
+
+// Local copy of rows [r0, r1) of M with global column ids.
+static void extract_rows(const GpuCsr &M, int64_t r0, int64_t r1, GpuCsr &out, Ctx *ctx) {
+    hipStream_t s = ctx->stream;
+    const int64_t n = r1 - r0;
+    int64_t e0 = 0, e1 = 0;
+    FAMG_CHECK_HIP(hipMemcpyAsync(&e0, M.rp64.get() + r0, sizeof(int64_t), hipMemcpyDeviceToHost, s));
+    FAMG_CHECK_HIP(hipMemcpyAsync(&e1, M.rp64.get() + r1, sizeof(int64_t), hipMemcpyDeviceToHost, s));
+    FAMG_CHECK_HIP(hipStreamSynchronize(s));
+    csr_alloc(out, ctx, n, M.ncols, e1 - e0);
+    hipLaunchKernelGGL(k_extract_rp, dim3(g1(n + 1)), dim3(256), 0, s, M.rp64.get(), r0, n, out.rp64.get());
+    if (e1 > e0) {
+        FAMG_CHECK_HIP(hipMemcpyAsync(out.col.get(), M.col.get() + e0, (e1 - e0) * sizeof(int32_t), hipMemcpyDeviceToDevice, s));
+        FAMG_CHECK_HIP(hipMemcpyAsync(out.val.get(), M.val.get() + e0, (e1 - e0) * sizeof(double), hipMemcpyDeviceToDevice, s));
+    }
+    FAMG_CHECK_HIP(hipGetLastError());
+}
+
+static void space_mark(Space &sp, const GpuCsr &local, Ctx *ctx) {
+    if (local.nnz)
+        hipLaunchKernelGGL(k_mark_ghost, dim3(g1(local.nnz)), dim3(256), 0, ctx->stream, local.col.get(),
+                           local.nnz, sp.r0, sp.r1, sp.mark.get());
+    FAMG_CHECK_HIP(hipGetLastError());
+}
+
+// After all matrices of the space are marked: ghost list, halo plan (request
+// exchange through the transport), scan kept for the column remap.
+static void space_plan(Space &sp, Transport &tr, Ctx *ctx) {
+    hipStream_t s = ctx->stream;
+    sp.scan.resize(sp.n_glob + 1);
+    sp.n_ghost = scan_counts(sp.mark.get(), sp.scan.get(), sp.n_glob, *ctx);
+    DevBuf<int64_t> ids(sp.n_ghost);
+    hipLaunchKernelGGL(k_compact_ghost, dim3(g1(sp.n_glob)), dim3(256), 0, s, sp.mark.get(), sp.scan.get(),
+                       sp.n_glob, ids.get());
+    sp.ghost_ids.resize(sp.n_ghost);
+    if (sp.n_ghost)
+        FAMG_CHECK_HIP(hipMemcpyAsync(sp.ghost_ids.data(), ids.get(), sp.n_ghost * sizeof(int64_t), hipMemcpyDeviceToHost, s));
+    FAMG_CHECK_HIP(hipStreamSynchronize(s));
+    const int P = tr.nranks;
+    // requests per owner
+    std::vector<int64_t> req_cnt(P, 0), req_off(P + 1, 0);
+    for (int64_t g : sp.ghost_ids) req_cnt[sp.owner(g)]++;
+    for (int q = 0; q < P; q++) req_off[q + 1] = req_off[q] + req_cnt[q];
+    // all-to-all counts
+    DevBuf<int64_t> dsend(P), drecv(P);
+    FAMG_CHECK_HIP(hipMemcpyAsync(dsend.get(), req_cnt.data(), P * sizeof(int64_t), hipMemcpyHostToDevice, s));
+    FAMG_CHECK_HIP(hipMemsetAsync(drecv.get(), 0, P * sizeof(int64_t), s));
+    std::vector<Peer> cp;
+    for (int q = 0; q < P; q++)
+        if (q != tr.rank) cp.push_back({q, dsend.get() + q, 8, drecv.get() + q, 8});
+    tr.exchange(cp, s);
+    std::vector<int64_t> got(P);
+    FAMG_CHECK_HIP(hipMemcpyAsync(got.data(), drecv.get(), P * sizeof(int64_t), hipMemcpyDeviceToHost, s));
+    FAMG_CHECK_HIP(hipStreamSynchronize(s));
+    got[tr.rank] = 0;
+    std::vector<int64_t> got_off(P + 1, 0);
+    for (int q = 0; q < P; q++) got_off[q + 1] = got_off[q] + got[q];
+    // exchange the requested ids
+    DevBuf<int64_t> req_ids(std::max<int64_t>(1, sp.n_ghost)), in_ids(std::max<int64_t>(1, got_off[P]));
+    if (sp.n_ghost)
+        FAMG_CHECK_HIP(hipMemcpyAsync(req_ids.get(), sp.ghost_ids.data(), sp.n_ghost * sizeof(int64_t), hipMemcpyHostToDevice, s));
+    std::vector<Peer> ip;
+    for (int q = 0; q < P; q++) {
+        if (q == tr.rank || (req_cnt[q] == 0 && got[q] == 0)) continue;
+        ip.push_back({q, req_ids.get() + req_off[q], req_cnt[q] * 8, in_ids.get() + got_off[q], got[q] * 8});
+    }
+    tr.exchange(ip, s);
+    std::vector<int64_t> inh(got_off[P]);
+    if (got_off[P])
+        FAMG_CHECK_HIP(hipMemcpyAsync(inh.data(), in_ids.get(), got_off[P] * sizeof(int64_t), hipMemcpyDeviceToHost, s));
+    FAMG_CHECK_HIP(hipStreamSynchronize(s));
+    std::vector<int32_t> sidx(got_off[P]);
+    for (int64_t k = 0; k < got_off[P]; k++) {
+        FAMG_REQUIRE(inh[k] >= sp.r0 && inh[k] < sp.r1, AMG_ERR_INVALID, "halo request for a row not owned");
+        sidx[k] = (int32_t)(inh[k] - sp.r0);
+    }
+    sp.nsend = got_off[P];
+    sp.send_idx.resize(std::max<int64_t>(1, sp.nsend));
+    sp.sendbuf.resize(std::max<int64_t>(1, sp.nsend));
+    if (sp.nsend)
+        FAMG_CHECK_HIP(hipMemcpyAsync(sp.send_idx.get(), sidx.data(), sp.nsend * sizeof(int32_t), hipMemcpyHostToDevice, s));
+    sp.nbr.clear(); sp.soff.clear(); sp.scnt.clear(); sp.roff.clear(); sp.rcnt.clear();
+    for (int q = 0; q < P; q++) {
+        if (q == tr.rank || (req_cnt[q] == 0 && got[q] == 0)) continue;
+        sp.nbr.push_back(q);
+        sp.soff.push_back(got_off[q]);
+        sp.scnt.push_back(got[q]);
+        sp.roff.push_back(req_off[q]);
+        sp.rcnt.push_back(req_cnt[q]);
+    }
+    FAMG_CHECK_HIP(hipStreamSynchronize(s));
+}
+
+static void space_remap(const Space &sp, GpuCsr &local, Ctx *ctx) {
+    if (local.nnz)
+        hipLaunchKernelGGL(k_remap_cols, dim3(g1(local.nnz)), dim3(256), 0, ctx->stream, local.col.get(),
+                           local.nnz, sp.r0, sp.r1, sp.n_own, sp.scan.get());
+    FAMG_CHECK_HIP(hipGetLastError());
+    local.ncols = sp.n_own + sp.n_ghost;
+    csr_finalize(local);
+}
+
+// refresh the ghost region of x (x has n_own + n_ghost entries)
+static void halo(Space &sp, double *x, Transport &tr, hipStream_t s) {
+    if (sp.redundant || sp.nbr.empty()) return;
+    if (sp.nsend)
+        hipLaunchKernelGGL(k_gather_idx, dim3(g1(sp.nsend)), dim3(256), 0, s, x, sp.send_idx.get(), sp.nsend,
+                           sp.sendbuf.get());
+    sp.peers.clear();
+    for (size_t k = 0; k < sp.nbr.size(); k++)
+        sp.peers.push_back({sp.nbr[k], sp.sendbuf.get() + sp.soff[k], sp.scnt[k] * 8,
+                            x + sp.n_own + sp.roff[k], sp.rcnt[k] * 8});
+    tr.exchange(sp.peers, s);
+}
+
+// ---------------------------------------------------------- multigrid
+
+struct DLevel {
+    Space sp;
+    CsrPtr A, R, P;  // local: A rows own(l) cols space l; R rows own(l+1) cols space l;
+                     // P rows own(l) cols space l+1 (global ids when l+1 is redundant)
+    std::shared_ptr<DiagOp> S;
+    DevBuf<double> v, t, f, r;
+};
+
+struct DistMultigridOp : LinOp {
+    std::shared_ptr<Transport> tr;
+    std::vector<DLevel> L;                 // distributed levels [0, La)
+    std::shared_ptr<MultigridOp> tail;     // global levels [La, end)
+    int64_t La = 0, nlevels = 0;
+    int64_t mu = 1, steps = 1;
+    std::vector<int64_t> tail_splits;      // row splits of level La
+    int64_t tail_max = 0;
+    DevBuf<double> fc_own, gather, fc_full, vc_full;
+    std::mutex mtx;
+    Kind kind() const override { return Kind::DistMultigrid; }
+    bool is_precond() const override { return true; }
+
+    void smooth(int64_t l, double *&v, double *&t, const double *f, bool zero) {
+        DLevel &D = L[l];
+        hipStream_t s = ctx->stream;
+        for (int64_t it = 0; it < steps; it++) {
+            if (zero && it == 0) {
+                vec_mul(t, D.S->d.get(), f, D.sp.n_own, s);
+            } else {
+                halo(D.sp, v, *tr, s);
+                SpmvEpi epi;
+                epi.b = f;
+                epi.d = D.S->d.get();
+                spmv(D.A->m, v, t, SPMV_JACOBI, epi, s);
+            }
+            std::swap(v, t);
+        }
+    }
+
+    // gather the owned part of level La into the full vector on every rank
+    void gather_tail(const double *own) {
+        hipStream_t s = ctx->stream;
+        const int P = tr->nranks;
+        const int64_t cnt = tail_splits[tr->rank + 1] - tail_splits[tr->rank];
+        if (cnt) vec_copy(fc_own.get(), own, cnt, s);
+        tr->allgather(fc_own.get(), gather.get(), tail_max * 8, s);
+        for (int q = 0; q < P; q++) {
+            const int64_t c = tail_splits[q + 1] - tail_splits[q];
+            if (c) vec_copy(fc_full.get() + tail_splits[q], gather.get() + q * tail_max, c, s);
+        }
+    }
+
+    void cycle(int64_t l, double *v, const double *f, bool zero) {
+        DLevel &D = L[l];
+        hipStream_t s = ctx->stream;
+        double *v0 = v;
+        double *t = (v == D.t.get()) ? D.v.get() : D.t.get();
+        smooth(l, v, t, f, zero);
+        halo(D.sp, v, *tr, s);
+        SpmvEpi epi;
+        epi.b = f;
+        spmv(D.A->m, v, D.r.get(), SPMV_RESID, epi, s);
+        halo(D.sp, D.r.get(), *tr, s);
+        if (l + 1 < La) {
+            DLevel &C = L[l + 1];
+            spmv(D.R->m, D.r.get(), C.f.get(), SPMV_SET, SpmvEpi{}, s);
+            for (int64_t k = 0; k < mu; k++) cycle(l + 1, C.v.get(), C.f.get(), k == 0);
+            halo(C.sp, C.v.get(), *tr, s);
+            spmv(D.P->m, C.v.get(), v, SPMV_ADD, SpmvEpi{}, s);
+        } else {
+            const int64_t cnt = tail_splits[tr->rank + 1] - tail_splits[tr->rank];
+            if (cnt) spmv(D.R->m, D.r.get(), gather.get() + tr->rank * tail_max, SPMV_SET, SpmvEpi{}, s);
+            gather_tail(gather.get() + tr->rank * tail_max);
+            for (int64_t k = 0; k < mu; k++) tail->cycle(0, vc_full.get(), fc_full.get(), k == 0, nullptr);
+            spmv(D.P->m, vc_full.get(), v, SPMV_ADD, SpmvEpi{}, s);
+        }
+        smooth(l, v, t, f, false);
+        if (v != v0) vec_copy(v0, v, D.sp.n_own, s);
+    }
+
+    // r_own = b_own - (A_0 x)_own for the finest level, distributed or not
+    DevBuf<double> xg_, rfull_;
+    void residual0(const double *b, const double *x, double *r) {
+        hipStream_t s = ctx->stream;
+        SpmvEpi epi;
+        epi.b = b;
+        if (La > 0) {
+            DLevel &D = L[0];
+            if (xg_.size() < (size_t)(D.sp.n_own + D.sp.n_ghost + 1)) xg_.resize(D.sp.n_own + D.sp.n_ghost + 1);
+            vec_copy(xg_.get(), x, D.sp.n_own, s);
+            halo(D.sp, xg_.get(), *tr, s);
+            spmv(D.A->m, xg_.get(), r, SPMV_RESID, epi, s);
+            return;
+        }
+        // everything replicated: gather x, global SpMV, keep the owned rows
+        auto *A = dynamic_cast<CsrOp *>(tail->levels[0].A.get());
+        FAMG_REQUIRE(A, AMG_ERR_UNSUPPORTED, "finest operator is not CSR");
+        const int64_t r0 = tail_splits[tr->rank], cnt = tail_splits[tr->rank + 1] - r0;
+        if (rfull_.size() < (size_t)A->nrows) rfull_.resize(A->nrows);
+        gather_tail(x);
+        spmv(A->m, fc_full.get(), rfull_.get(), SPMV_SET, SpmvEpi{}, s);
+        if (cnt) vec_sub(r, b, rfull_.get() + r0, cnt, s);
+    }
+
+    void apply(double *out, const double *rhs) override {
+        std::lock_guard<std::mutex> lk(mtx);
+        hipStream_t s = ctx->stream;
+        tail->ensure_workspace();
+        if (La == 0) {
+            gather_tail(rhs);
+            tail->cycle(0, vc_full.get(), fc_full.get(), true, nullptr);
+            const int64_t r0 = tail_splits[tr->rank], cnt = tail_splits[tr->rank + 1] - r0;
+            if (cnt) vec_copy(out, vc_full.get() + r0, cnt, s);
+            return;
+        }
+        cycle(0, L[0].v.get(), rhs, true);
+        vec_copy(out, L[0].v.get(), L[0].sp.n_own, s);
+    }
+};
+
+// Distributed A_l as a LinOp: out_own = A (x_own with halo)
+struct DistLevelOp : LinOp {
+    std::shared_ptr<DistMultigridOp> mg;
+    int64_t level = 0;
+    DevBuf<double> x;
+    Kind kind() const override { return Kind::DistCsr; }
+    void apply(double *out, const double *rhs) override {
+        DLevel &D = mg->L[level];
+        hipStream_t s = ctx->stream;
+        vec_copy(x.get(), rhs, D.sp.n_own, s);
+        halo(D.sp, x.get(), *mg->tr, s);
+        spmv(D.A->m, x.get(), out, SPMV_SET, SpmvEpi{}, s);
+    }
+};
+
+static std::shared_ptr<DistMultigridOp> build_dist(amg_comm *comm, const MultigridOp &g,
+                                                   const int64_t *splits, int64_t agglo) {
+    Ctx *ctx = comm->ctx;
+    Transport &tr = *comm->tr;
+    const int P = tr.nranks, me = tr.rank;
+    auto d = std::make_shared<DistMultigridOp>();
+    d->ctx = ctx;
+    d->tr = comm->tr;
+    d->mu = g.mu;
+    d->steps = g.steps;
+    d->nlevels = (int64_t)g.levels.size();
+    d->La = d->nlevels - 1;  // the coarsest level is always redundant
+    for (int64_t l = 0; l < d->nlevels - 1; l++)
+        if (g.levels[l].A->nrows < agglo) { d->La = l; break; }
+    auto sp_of = [&](int64_t l) {
+        std::vector<int64_t> s(splits + l * (P + 1), splits + (l + 1) * (P + 1));
+        FAMG_REQUIRE(s[0] == 0 && s[P] == g.levels[l].A->nrows, AMG_ERR_DIM, "level splits must cover the level");
+        for (int q = 0; q < P; q++) FAMG_REQUIRE(s[q + 1] >= s[q], AMG_ERR_INVALID, "splits must be monotone");
+        return s;
+    };
+    d->L.resize(d->La);
+    for (int64_t l = 0; l < d->La; l++) {
+        DLevel &D = d->L[l];
+        auto *A = dynamic_cast<CsrOp *>(g.levels[l].A.get());
+        auto *R = dynamic_cast<CsrOp *>(g.levels[l].R.get());
+        auto *Pm = dynamic_cast<CsrOp *>(g.levels[l].P.get());
+        auto *S = dynamic_cast<DiagOp *>(g.levels[l].S.get());
+        FAMG_REQUIRE(A && R && Pm, AMG_ERR_UNSUPPORTED, "distributed levels need CSR operators");
+        FAMG_REQUIRE(S, AMG_ERR_UNSUPPORTED, "distributed levels need a diagonal (Jacobi/L1/L2) smoother");
+        D.sp.splits = sp_of(l);
+        D.sp.n_glob = A->nrows;
+        D.sp.r0 = D.sp.splits[me];
+        D.sp.r1 = D.sp.splits[me + 1];
+        D.sp.n_own = D.sp.r1 - D.sp.r0;
+    }
+    // local matrices with global columns
+    for (int64_t l = 0; l < d->La; l++) {
+        DLevel &D = d->L[l];
+        auto *A = dynamic_cast<CsrOp *>(g.levels[l].A.get());
+        auto *R = dynamic_cast<CsrOp *>(g.levels[l].R.get());
+        auto *Pm = dynamic_cast<CsrOp *>(g.levels[l].P.get());
+        D.A = make_csr(ctx);
+        extract_rows(A->m, D.sp.r0, D.sp.r1, D.A->m, ctx);
+        D.P = make_csr(ctx);
+        extract_rows(Pm->m, D.sp.r0, D.sp.r1, D.P->m, ctx);
+        const std::vector<int64_t> cs = (l + 1 < d->La) ? std::vector<int64_t>() : sp_of(l + 1);
+        const int64_t cr0 = (l + 1 < d->La) ? 0 : cs[me], cr1 = (l + 1 < d->La) ? 0 : cs[me + 1];
+        D.R = make_csr(ctx);
+        if (l + 1 < d->La) {
+            // rows of R: coarse rows owned at level l+1 (its space is set up below)
+            const std::vector<int64_t> c2 = sp_of(l + 1);
+            extract_rows(R->m, c2[me], c2[me + 1], D.R->m, ctx);
+        } else {
+            extract_rows(R->m, cr0, cr1, D.R->m, ctx);
+        }
+        // smoother slice
+        auto *S = dynamic_cast<DiagOp *>(g.levels[l].S.get());
+        D.S = std::make_shared<DiagOp>();
+        D.S->ctx = ctx;
+        D.S->nrows = D.S->ncols = D.sp.n_own;
+        D.S->d.resize(D.sp.n_own);
+        if (D.sp.n_own) vec_copy(D.S->d.get(), S->d.get() + D.sp.r0, D.sp.n_own, ctx->stream);
+    }
+    // ghost sets: space l collects A_l, R_l (fine columns) and P_{l-1} (coarse columns)
+    for (int64_t l = 0; l < d->La; l++) {
+        Space &sp = d->L[l].sp;
+        sp.mark.resize(sp.n_glob);
+        FAMG_CHECK_HIP(hipMemsetAsync(sp.mark.get(), 0, sp.n_glob * sizeof(int64_t), ctx->stream));
+        space_mark(sp, d->L[l].A->m, ctx);
+        space_mark(sp, d->L[l].R->m, ctx);
+        if (l > 0) space_mark(sp, d->L[l - 1].P->m, ctx);
+        space_plan(sp, tr, ctx);
+        space_remap(sp, d->L[l].A->m, ctx);
+        space_remap(sp, d->L[l].R->m, ctx);
+        if (l > 0) space_remap(sp, d->L[l - 1].P->m, ctx);
+        sp.mark.release();
+        sp.scan.release();
+        for (auto *op : {d->L[l].A.get(), d->L[l].R.get()}) {
+            op->nrows = op->m.nrows;
+            op->ncols = op->m.ncols;
+        }
+    }
+    // the last distributed level's P references the replicated level La by global id
+    if (d->La > 0) {
+        DLevel &D = d->L[d->La - 1];
+        csr_finalize(D.P->m);
+    }
+    for (int64_t l = 0; l < d->La; l++) {
+        d->L[l].P->nrows = d->L[l].P->m.nrows;
+        d->L[l].P->ncols = d->L[l].P->m.ncols;
+    }
+    // workspaces
+    for (int64_t l = 0; l < d->La; l++) {
+        DLevel &D = d->L[l];
+        const int64_t nv = D.sp.n_own + D.sp.n_ghost;
+        D.v.resize(std::max<int64_t>(1, nv));
+        D.t.resize(std::max<int64_t>(1, nv));
+        D.r.resize(std::max<int64_t>(1, nv));
+        D.f.resize(std::max<int64_t>(1, D.sp.n_own));
+        FAMG_CHECK_HIP(hipMemsetAsync(D.v.get(), 0, std::max<int64_t>(1, nv) * 8, ctx->stream));
+        FAMG_CHECK_HIP(hipMemsetAsync(D.t.get(), 0, std::max<int64_t>(1, nv) * 8, ctx->stream));
+        FAMG_CHECK_HIP(hipMemsetAsync(D.r.get(), 0, std::max<int64_t>(1, nv) * 8, ctx->stream));
+    }
+    // redundant tail
+    d->tail = std::make_shared<MultigridOp>();
+    d->tail->ctx = ctx;
+    d->tail->mu = g.mu;
+    d->tail->steps = g.steps;
+    for (int64_t l = d->La; l < d->nlevels; l++) d->tail->levels.push_back(MgLevel{g.levels[l].A, g.levels[l].S, g.levels[l].R, g.levels[l].P});
+    d->tail->nrows = d->tail->ncols = g.levels[d->La].A->nrows;
+    d->tail_splits = sp_of(d->La);
+    for (int q = 0; q < P; q++) d->tail_max = std::max(d->tail_max, d->tail_splits[q + 1] - d->tail_splits[q]);
+    const int64_t nt = g.levels[d->La].A->nrows;
+    d->fc_own.resize(std::max<int64_t>(1, d->tail_max));
+    d->gather.resize(std::max<int64_t>(1, d->tail_max * P));
+    d->fc_full.resize(std::max<int64_t>(1, nt));
+    d->vc_full.resize(std::max<int64_t>(1, nt));
+    FAMG_CHECK_HIP(hipMemsetAsync(d->gather.get(), 0, std::max<int64_t>(1, d->tail_max * P) * 8, ctx->stream));
+    d->nrows = d->ncols = d->La > 0 ? d->L[0].sp.n_own : (d->tail_splits[me + 1] - d->tail_splits[me]);
+    FAMG_CHECK_HIP(hipStreamSynchronize(ctx->stream));
+    tr.barrier(ctx->stream);
+    return d;
+}
+
+}  // namespace famg
+
+// ------------------------------------------------------------------ C ABI
+
+#define dguard guard
+
+static std::shared_ptr<DistMultigridOp> need_dist(const amg_linop *h) {
+    FAMG_REQUIRE(h && h->op, AMG_ERR_INVALID, "null amg_linop handle");
+    auto p = std::dynamic_pointer_cast<DistMultigridOp>(h->op);
+    FAMG_REQUIRE(p, AMG_ERR_INVALID, "operator is not a distributed multigrid");
+    return p;
+}
+
+extern "C" {
+
+int32_t amg_comm_unique_id_size(void) { return (int32_t)sizeof(ncclUniqueId); }
+
+amg_status amg_comm_get_unique_id(void *id) {
+    return dguard([&] {
+        FAMG_REQUIRE(id, AMG_ERR_INVALID, "null id buffer");
+        ncclUniqueId u;
+        FAMG_CHECK_NCCL(ncclGetUniqueId(&u));
+        std::memcpy(id, &u, sizeof(u));
+    });
+}
+
+amg_status amg_comm_create(amg_ctx *ctx, int32_t nranks, int32_t rank, const void *id, amg_comm **out) {
+    return dguard([&] {
+        FAMG_REQUIRE(ctx && id && out && nranks > 0 && rank >= 0 && rank < nranks, AMG_ERR_INVALID, "bad argument");
+        Ctx *c = reinterpret_cast<Ctx *>(ctx);
+        c->set_device();
+        auto t = std::make_shared<RcclTransport>();
+        t->nranks = nranks;
+        t->rank = rank;
+        ncclUniqueId u;
+        std::memcpy(&u, id, sizeof(u));
+        FAMG_CHECK_NCCL(ncclCommInitRank(&t->comm, nranks, u, rank));
+        *out = new amg_comm{c, t};
+    });
+}
+
+amg_status amg_loopback_hub_create(int32_t nranks, amg_loopback_hub **out) {
+    return dguard([&] {
+        FAMG_REQUIRE(out && nranks > 0, AMG_ERR_INVALID, "bad argument");
+        *out = new amg_loopback_hub{std::make_shared<LoopbackHub>(nranks)};
+    });
+}
+
+amg_status amg_loopback_hub_destroy(amg_loopback_hub *hub) {
+    return dguard([&] { delete hub; });
+}
+
+amg_status amg_comm_create_loopback(amg_ctx *ctx, amg_loopback_hub *hub, int32_t rank, amg_comm **out) {
+    return dguard([&] {
+        FAMG_REQUIRE(ctx && hub && out && rank >= 0 && rank < hub->hub->nranks, AMG_ERR_INVALID, "bad argument");
+        auto t = std::make_shared<LoopbackTransport>();
+        t->hub = hub->hub;
+        t->nranks = hub->hub->nranks;
+        t->rank = rank;
+        *out = new amg_comm{reinterpret_cast<Ctx *>(ctx), t};
+    });
+}
+
+amg_status amg_comm_destroy(amg_comm *comm) {
+    return dguard([&] {
+        if (comm) comm->ctx->set_device();
+        delete comm;
+    });
+}
+
+amg_status amg_comm_rank(const amg_comm *comm, int32_t *rank, int32_t *nranks) {
+    return dguard([&] {
+        FAMG_REQUIRE(comm, AMG_ERR_INVALID, "null comm");
+        if (rank) *rank = comm->tr->rank;
+        if (nranks) *nranks = comm->tr->nranks;
+    });
+}
+
+amg_status amg_comm_barrier(amg_comm *comm) {
+    return dguard([&] {
+        FAMG_REQUIRE(comm, AMG_ERR_INVALID, "null comm");
+        comm->ctx->set_device();
+        comm->tr->barrier(comm->ctx->stream);
+    });
+}
+
+static void reduce_host(amg_comm *comm, double *value, bool is_max) {
+    FAMG_REQUIRE(comm && value, AMG_ERR_INVALID, "null argument");
+    comm->ctx->set_device();
+    DevBuf<double> b(1);
+    hipStream_t s = comm->ctx->stream;
+    FAMG_CHECK_HIP(hipMemcpyAsync(b.get(), value, 8, hipMemcpyHostToDevice, s));
+    comm->tr->allreduce(b.get(), 1, is_max, s);
+    FAMG_CHECK_HIP(hipMemcpyAsync(value, b.get(), 8, hipMemcpyDeviceToHost, s));
+    FAMG_CHECK_HIP(hipStreamSynchronize(s));
+}
+
+amg_status amg_comm_allreduce_max(amg_comm *comm, double *value) {
+    return dguard([&] { reduce_host(comm, value, true); });
+}
+
+amg_status amg_comm_allreduce_sum(amg_comm *comm, double *value) {
+    return dguard([&] { reduce_host(comm, value, false); });
+}
+
+amg_status amg_dist_multigrid_create(amg_comm *comm, const amg_linop *mg_global, const int64_t *level_splits,
+                                     int64_t agglomerate_rows, amg_linop **out) {
+    return dguard([&] {
+        FAMG_REQUIRE(comm && mg_global && mg_global->op && level_splits && out, AMG_ERR_INVALID, "null argument");
+        auto g = std::dynamic_pointer_cast<MultigridOp>(mg_global->op);
+        FAMG_REQUIRE(g, AMG_ERR_INVALID, "mg_global is not a multigrid");
+        FAMG_REQUIRE(g->ctx == comm->ctx, AMG_ERR_INVALID, "multigrid and comm on different contexts");
+        comm->ctx->set_device();
+        *out = new amg_linop{build_dist(comm, *g, level_splits, agglomerate_rows)};
+    });
+}
+
+amg_status amg_dist_local_rows(const amg_linop *dist, int64_t *begin, int64_t *end) {
+    return dguard([&] {
+        auto d = need_dist(dist);
+        FAMG_REQUIRE(begin && end, AMG_ERR_INVALID, "null output");
+        if (d->La > 0) {
+            *begin = d->L[0].sp.r0;
+            *end = d->L[0].sp.r1;
+        } else {
+            *begin = d->tail_splits[d->tr->rank];
+            *end = d->tail_splits[d->tr->rank + 1];
+        }
+    });
+}
+
+amg_status amg_dist_level_info(const amg_linop *dist, int64_t level, int64_t *info) {
+    return dguard([&] {
+        auto d = need_dist(dist);
+        FAMG_REQUIRE(info && level >= 0 && level < d->nlevels, AMG_ERR_INVALID, "bad level");
+        if (level < d->La) {
+            const Space &sp = d->L[level].sp;
+            info[0] = sp.n_own;
+            info[1] = sp.n_ghost;
+            info[2] = (int64_t)sp.nbr.size();
+            info[3] = 0;
+            int64_t rc = 0;
+            for (int64_t c : sp.rcnt) rc += c;
+            info[4] = rc;
+            info[5] = sp.n_glob;
+        } else {
+            const int64_t n = d->tail->levels[level - d->La].A->nrows;
+            info[0] = n; info[1] = 0; info[2] = 0; info[3] = 1; info[4] = 0; info[5] = n;
+        }
+    });
+}
+
+amg_status amg_dist_level_operator(const amg_linop *dist, int64_t level, amg_linop **out) {
+    return dguard([&] {
+        auto d = need_dist(dist);
+        FAMG_REQUIRE(out && level >= 0 && level < d->La, AMG_ERR_INVALID, "level must be distributed");
+        auto op = std::make_shared<DistLevelOp>();
+        op->ctx = d->ctx;
+        op->mg = d;
+        op->level = level;
+        op->nrows = op->ncols = d->L[level].sp.n_own;
+        op->x.resize(std::max<int64_t>(1, d->L[level].sp.n_own + d->L[level].sp.n_ghost));
+        FAMG_CHECK_HIP(hipMemset(op->x.get(), 0, op->x.bytes()));
+        *out = new amg_linop{op};
+    });
+}
+
+amg_status amg_dist_level_matrix(const amg_linop *dist, int64_t level, int32_t which, amg_linop **out) {
+    return dguard([&] {
+        auto d = need_dist(dist);
+        FAMG_REQUIRE(out && level >= 0 && level < d->La && which >= 0 && which <= 2, AMG_ERR_INVALID,
+                     "level must be distributed, which in {0,1,2}");
+        const DLevel &D = d->L[level];
+        *out = new amg_linop{which == 0 ? D.A : which == 1 ? D.R : D.P};
+    });
+}
+
+amg_status amg_dist_stationary_solve(amg_linop *dist_mg, const double *b, double *x, int64_t max_iter,
+                                     double rel_tol, double *hist, int64_t *iters) {
+    return dguard([&] {
+        auto d = need_dist(dist_mg);
+        FAMG_REQUIRE(b && x && iters && max_iter > 0, AMG_ERR_INVALID, "bad argument");
+        Ctx &ctx = *d->ctx;
+        ctx.set_device();
+        hipStream_t s = ctx.stream;
+        const int64_t n = d->nrows;
+        DevBuf<double> r(std::max<int64_t>(1, n)), z(std::max<int64_t>(1, n)), red(1);
+        auto gdot = [&](const double *u, const double *w) {
+            vec_dot_dev(u, w, n, red.get(), ctx);
+            d->tr->allreduce(red.get(), 1, false, s);
+            double h = 0;
+            FAMG_CHECK_HIP(hipMemcpyAsync(&h, red.get(), 8, hipMemcpyDeviceToHost, s));
+            FAMG_CHECK_HIP(hipStreamSynchronize(s));
+            return h;
+        };
+        const double bn = std::sqrt(gdot(b, b));
+        int64_t it = 0;
+        for (;;) {
+            {
+                std::lock_guard<std::mutex> lk(d->mtx);
+                d->residual0(b, x, r.get());
+            }
+            const double rel = std::sqrt(gdot(r.get(), r.get())) / bn;
+            it++;
+            if (hist) hist[it - 1] = rel;
+            if (rel < rel_tol || it >= max_iter) break;
+            d->apply(z.get(), r.get());
+            vec_add_inplace(x, z.get(), n, s);
+        }
+        FAMG_CHECK_HIP(hipStreamSynchronize(s));
+        *iters = it;
+    });
+}
+
+}  // extern "C"

@@ -35,15 +35,26 @@ struct GpuCsr {
     DevBuf<double> val;    // padded by 2 entries
     DevBuf<int32_t> sched; // stream-SpMV row blocks: nblocks+1 row starts
     int64_t nblocks = 0;
+    // SELL-64 copy for short, regular rows: slice s holds rows [64s, 64s+64),
+    // width w_s = max row length in the slice, entries column-major
+    // (entry k of lane l at sell_off[s] + 64 k + l); padding = 0.0 * x[c_last].
+    DevBuf<int32_t> sell_off;
+    DevBuf<int32_t> sell_col;
+    DevBuf<double> sell_val;
+    int64_t nslices = 0, sell_padded = 0;
     bool spmv_ready() const { return rp32.get() != nullptr && sched.get() != nullptr; }
+    bool has_sell() const { return sell_off.get() != nullptr; }
     int64_t index_bytes() const { return 12 * nnz + 4 * (nrows + 1); }
 };
 
 // Allocate a CSR with the given shape/nnz (arrays uninitialised).
 void csr_alloc(GpuCsr &m, Ctx *ctx, int64_t nrows, int64_t ncols, int64_t nnz);
-// Build rp32 (if nnz < 2^31) and the stream schedule from rp64.  Host pass over
-// the row pointers (setup only).
+// Build rp32 (if nnz < 2^31), the stream schedule and, for short regular rows,
+// the SELL-64 copy.  Host pass over the row pointers (setup only).
 void csr_finalize(GpuCsr &m);
+// Format policy (tests/bench can force a path): 0 auto, 1 CSR-stream only, 2 SELL when valid
+extern int g_spmv_format_policy;
+void build_sell(GpuCsr &m, const std::vector<int64_t> &rp);
 // Host upload from usize-compatible arrays.
 void csr_from_host(GpuCsr &m, Ctx *ctx, int64_t nrows, int64_t ncols, const int64_t *rowptr,
                    const int64_t *col, const double *val);

@@ -1,0 +1,37 @@
+// handles.hpp -- definitions of the opaque C-ABI handle types and the shared
+// error plumbing of the extern "C" layer (capi.cpp, dist.hip).
+#pragma once
+
+#include "famg.hpp"
+
+struct amg_ctx {
+    famg::Ctx ctx;  // must stay the first member (Ctx* <-> amg_ctx* casts)
+    famg::DevBuf<double> stage_in, stage_out;  // host-memory staging
+    hipEvent_t join_event = nullptr;            // amg_ctx_join_stream
+    ~amg_ctx() {
+        if (join_event) (void)hipEventDestroy(join_event);
+    }
+};
+
+struct amg_linop {
+    famg::LinOpPtr op;
+};
+
+namespace famg {
+// record the thread-local message returned by amg_last_error(); returns s
+amg_status set_last_error(amg_status s, const char *msg);
+
+template <typename F> amg_status guard(F &&f) {
+    try {
+        f();
+        set_last_error(AMG_OK, "");
+        return AMG_OK;
+    } catch (const AmgError &e) {
+        return set_last_error(e.status, e.what());
+    } catch (const std::bad_alloc &) {
+        return set_last_error(AMG_ERR_OOM, "host allocation failed");
+    } catch (const std::exception &e) {
+        return set_last_error(AMG_ERR_INVALID, e.what());
+    }
+}
+}  // namespace famg

@@ -35,15 +35,19 @@ __global__ void k_spgemm_ub(const int64_t *arp, const int32_t *acol, const int64
     if ((threadIdx.x & 63) == 0) atomicMax(maxub, s);
 }
 
+// Linear-probing insert; returns 1 if newly inserted, 0 if present, -1 if the
+// table is full (only possible in the symbolic pass when the distinct count was
+// not bounded in advance).
 template <int TBL>
 __device__ __forceinline__ int hash_insert(int32_t *keys, int32_t j, int *slot_out) {
     unsigned h = hash32(j) & (TBL - 1);
-    for (;;) {
+    for (int probe = 0; probe < TBL; probe++) {
         const int32_t old = atomicCAS(&keys[h], -1, j);
         if (old == -1) { *slot_out = (int)h; return 1; }
         if (old == j) { *slot_out = (int)h; return 0; }
         h = (h + 1) & (TBL - 1);
     }
+    return -1;
 }
 
 template <int TBL>
@@ -56,20 +60,31 @@ __device__ __forceinline__ int hash_find(const int32_t *keys, int32_t j) {
 template <int TBL>
 __global__ __launch_bounds__(64) void k_spgemm_symbolic(const int64_t *arp, const int32_t *acol,
                                                         const int64_t *brp, const int32_t *bcol,
-                                                        int64_t m, int64_t *cnt) {
+                                                        int64_t m, int64_t *cnt,
+                                                        unsigned long long *maxcnt, int *overflow) {
     __shared__ int32_t keys[TBL];
     const int lane = threadIdx.x;
     for (int64_t row = blockIdx.x; row < m; row += gridDim.x) {
         for (int t = lane; t < TBL; t += 64) keys[t] = -1;
         __syncthreads();
-        int local = 0, slot;
+        int local = 0, full = 0, slot;
         for (int64_t e = arp[row]; e < arp[row + 1]; e++) {
             const int32_t k = acol[e];
-            for (int64_t f = brp[k] + lane; f < brp[k + 1]; f += 64)
-                local += hash_insert<TBL>(keys, bcol[f], &slot);
+            for (int64_t f = brp[k] + lane; f < brp[k + 1]; f += 64) {
+                const int ins = hash_insert<TBL>(keys, bcol[f], &slot);
+                if (ins < 0) full = 1;
+                else local += ins;
+            }
         }
-        for (int off = 32; off > 0; off >>= 1) local += __shfl_xor(local, off);
-        if (lane == 0) cnt[row] = local;
+        for (int off = 32; off > 0; off >>= 1) {
+            local += __shfl_xor(local, off);
+            full |= __shfl_xor(full, off);
+        }
+        if (lane == 0) {
+            cnt[row] = local;
+            atomicMax(maxcnt, (unsigned long long)local);
+            if (full || 2 * local > TBL) *overflow = 1;
+        }
         __syncthreads();
     }
 }
@@ -94,7 +109,7 @@ __global__ __launch_bounds__(64) void k_spgemm_numeric(const int64_t *arp, const
             const int32_t k = acol[e];
             for (int64_t f = brp[k] + lane; f < brp[k + 1]; f += 64) {
                 int slot;
-                if (hash_insert<TBL>(keys, bcol[f], &slot)) list[atomicAdd(&cntsh, 1)] = bcol[f];
+                if (hash_insert<TBL>(keys, bcol[f], &slot) == 1) list[atomicAdd(&cntsh, 1)] = bcol[f];
             }
         }
         __syncthreads();
@@ -124,26 +139,41 @@ __global__ __launch_bounds__(64) void k_spgemm_numeric(const int64_t *arp, const
     }
 }
 
+static unsigned spgemm_grid(int64_t m) {
+    return (unsigned)std::max<int64_t>(1, std::min<int64_t>(m, 256 * 16));
+}
+
+// symbolic pass with a TBL-entry table: per-row distinct counts; returns the
+// max count, or -1 if some row did not fit (count > TBL/2)
 template <int TBL>
-static void spgemm_launch(const GpuCsr &A, const GpuCsr &B, GpuCsr &C, Ctx &ctx) {
+static int64_t spgemm_symbolic(const GpuCsr &A, const GpuCsr &B, int64_t *cnt, Ctx &ctx) {
     const int64_t m = A.nrows;
     hipStream_t s = ctx.stream;
-    const unsigned grid = (unsigned)std::max<int64_t>(1, std::min<int64_t>(m, 256 * 16));
-    DevBuf<int64_t> cnt(m + 1);
+    DevBuf<unsigned long long> mx(1);
+    DevBuf<int> of(1);
+    FAMG_CHECK_HIP(hipMemsetAsync(mx.get(), 0, sizeof(unsigned long long), s));
+    FAMG_CHECK_HIP(hipMemsetAsync(of.get(), 0, sizeof(int), s));
     if (m)
-        hipLaunchKernelGGL(k_spgemm_symbolic<TBL>, dim3(grid), dim3(64), 0, s, A.rp64.get(),
-                           A.col.get(), B.rp64.get(), B.col.get(), m, cnt.get());
+        hipLaunchKernelGGL(k_spgemm_symbolic<TBL>, dim3(spgemm_grid(m)), dim3(64), 0, s,
+                           A.rp64.get(), A.col.get(), B.rp64.get(), B.col.get(), m, cnt, mx.get(),
+                           of.get());
     FAMG_CHECK_HIP(hipGetLastError());
-    DevBuf<int64_t> rp(m + 1);
-    const int64_t nnz = scan_counts(cnt.get(), rp.get(), m, ctx);
-    csr_alloc(C, &ctx, m, B.ncols, nnz);
-    C.rp64 = std::move(rp);
+    unsigned long long hmx = 0;
+    int hof = 0;
+    FAMG_CHECK_HIP(hipMemcpyAsync(&hmx, mx.get(), sizeof(hmx), hipMemcpyDeviceToHost, s));
+    FAMG_CHECK_HIP(hipMemcpyAsync(&hof, of.get(), sizeof(hof), hipMemcpyDeviceToHost, s));
+    FAMG_CHECK_HIP(hipStreamSynchronize(s));
+    return hof ? -1 : (int64_t)hmx;
+}
+
+template <int TBL>
+static void spgemm_numeric(const GpuCsr &A, const GpuCsr &B, GpuCsr &C, Ctx &ctx) {
+    const int64_t m = A.nrows;
     if (m)
-        hipLaunchKernelGGL(k_spgemm_numeric<TBL>, dim3(grid), dim3(64), 0, s, A.rp64.get(),
-                           A.col.get(), A.val.get(), B.rp64.get(), B.col.get(), B.val.get(), m,
-                           C.rp64.get(), C.col.get(), C.val.get());
+        hipLaunchKernelGGL(k_spgemm_numeric<TBL>, dim3(spgemm_grid(m)), dim3(64), 0, ctx.stream,
+                           A.rp64.get(), A.col.get(), A.val.get(), B.rp64.get(), B.col.get(),
+                           B.val.get(), m, C.rp64.get(), C.col.get(), C.val.get());
     FAMG_CHECK_HIP(hipGetLastError());
-    csr_finalize(C);
 }
 
 void spgemm(const GpuCsr &A, const GpuCsr &B, GpuCsr &C) {
@@ -158,13 +188,28 @@ void spgemm(const GpuCsr &A, const GpuCsr &B, GpuCsr &C) {
     unsigned long long maxub = 0;
     FAMG_CHECK_HIP(hipMemcpyAsync(&maxub, mx.get(), sizeof(maxub), hipMemcpyDeviceToHost, s));
     FAMG_CHECK_HIP(hipStreamSynchronize(s));
+    // symbolic table: sized from the product bound when it is small, otherwise
+    // the largest table with overflow detection; numeric table: from the true
+    // per-row maximum of distinct columns.
     const int64_t bound = std::min<int64_t>((int64_t)maxub, B.ncols);
-    if (bound <= 32) spgemm_launch<64>(A, B, C, ctx);
-    else if (bound <= 128) spgemm_launch<256>(A, B, C, ctx);
-    else if (bound <= 512) spgemm_launch<1024>(A, B, C, ctx);
-    else if (bound <= 2048) spgemm_launch<4096>(A, B, C, ctx);
-    else if (bound <= 4096) spgemm_launch<8192>(A, B, C, ctx);
-    else fail(AMG_ERR_UNSUPPORTED, "spgemm: a product row may exceed 4096 distinct columns");
+    const int64_t m = A.nrows;
+    DevBuf<int64_t> cnt(m + 1);
+    int64_t maxc;
+    if (bound <= 32) maxc = spgemm_symbolic<64>(A, B, cnt.get(), ctx);
+    else if (bound <= 128) maxc = spgemm_symbolic<256>(A, B, cnt.get(), ctx);
+    else if (bound <= 512) maxc = spgemm_symbolic<1024>(A, B, cnt.get(), ctx);
+    else maxc = spgemm_symbolic<8192>(A, B, cnt.get(), ctx);
+    FAMG_REQUIRE(maxc >= 0, AMG_ERR_UNSUPPORTED, "spgemm: a product row exceeds 4096 distinct columns");
+    DevBuf<int64_t> rp(m + 1);
+    const int64_t nnz = scan_counts(cnt.get(), rp.get(), m, ctx);
+    csr_alloc(C, &ctx, m, B.ncols, nnz);
+    C.rp64 = std::move(rp);
+    if (maxc <= 32) spgemm_numeric<64>(A, B, C, ctx);
+    else if (maxc <= 128) spgemm_numeric<256>(A, B, C, ctx);
+    else if (maxc <= 512) spgemm_numeric<1024>(A, B, C, ctx);
+    else if (maxc <= 2048) spgemm_numeric<4096>(A, B, C, ctx);
+    else spgemm_numeric<8192>(A, B, C, ctx);
+    csr_finalize(C);
 }
 
 // ------------------------------------------------------------- transpose
@@ -185,10 +230,10 @@ __global__ void k_t_fill(const int64_t *rp, const int32_t *col, const double *va
     }
 }
 
-constexpr int TSORT_CAP = 2048;
-
-// per-row sort by column (wave per row): rank sort in LDS, insertion sort fallback
-__global__ __launch_bounds__(64) void k_row_sort(const int64_t *rp, int64_t m, int32_t *col, double *val) {
+// per-row sort by column (workgroup per row): rank sort of distinct keys in
+// LDS; rows longer than TSORT_CAP fall back to a serial insertion sort
+template <int TSORT_CAP, int TSORT_BS>
+__global__ __launch_bounds__(TSORT_BS) void k_row_sort(const int64_t *rp, int64_t m, int32_t *col, double *val) {
     __shared__ int32_t sk[TSORT_CAP];
     __shared__ double sv[TSORT_CAP];
     const int lane = threadIdx.x;
@@ -196,9 +241,9 @@ __global__ __launch_bounds__(64) void k_row_sort(const int64_t *rp, int64_t m, i
         const int64_t s0 = rp[row], len = rp[row + 1] - s0;
         if (len <= 1) continue;
         if (len <= TSORT_CAP) {
-            for (int u = lane; u < len; u += 64) { sk[u] = col[s0 + u]; sv[u] = val[s0 + u]; }
+            for (int u = lane; u < len; u += TSORT_BS) { sk[u] = col[s0 + u]; sv[u] = val[s0 + u]; }
             __syncthreads();
-            for (int u = lane; u < len; u += 64) {
+            for (int u = lane; u < len; u += TSORT_BS) {
                 const int32_t key = sk[u];
                 int r = 0;
                 for (int v = 0; v < len; v++) r += sk[v] < key;
@@ -219,6 +264,16 @@ __global__ __launch_bounds__(64) void k_row_sort(const int64_t *rp, int64_t m, i
     }
 }
 
+__global__ void k_max_len(const int64_t *rp, int64_t n, unsigned long long *out) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    unsigned long long v = i < n ? (unsigned long long)(rp[i + 1] - rp[i]) : 0ull;
+    for (int off = 32; off > 0; off >>= 1) {
+        const unsigned long long o = __shfl_xor(v, off);
+        v = v > o ? v : o;
+    }
+    if ((threadIdx.x & 63) == 0) atomicMax(out, v);
+}
+
 void transpose(const GpuCsr &A, GpuCsr &T) {
     Ctx &ctx = *A.ctx;
     hipStream_t s = ctx.stream;
@@ -234,13 +289,25 @@ void transpose(const GpuCsr &A, GpuCsr &T) {
     csr_alloc(T, &ctx, n, A.nrows, nnz);
     T.rp64 = std::move(rp);
     FAMG_CHECK_HIP(hipMemcpyAsync(cnt.get(), T.rp64.get(), n * sizeof(int64_t), hipMemcpyDeviceToDevice, s));
+    FAMG_CHECK_HIP(hipMemsetAsync(cnt.get() + n, 0, sizeof(unsigned long long), s));
     if (A.nrows)
         hipLaunchKernelGGL(k_t_fill, dim3((unsigned)ceil_div(A.nrows, 256)), dim3(256), 0, s,
                            A.rp64.get(), A.col.get(), A.val.get(), A.nrows, cnt.get(), T.col.get(),
                            T.val.get());
-    if (n)
-        hipLaunchKernelGGL(k_row_sort, dim3((unsigned)std::min<int64_t>(n, 4096)), dim3(64), 0, s,
-                           T.rp64.get(), n, T.col.get(), T.val.get());
+    if (n) {
+        hipLaunchKernelGGL(k_max_len, dim3((unsigned)ceil_div(n, 256)), dim3(256), 0, s,
+                           T.rp64.get(), n, cnt.get() + n);
+        unsigned long long maxlen = 0;
+        FAMG_CHECK_HIP(hipMemcpyAsync(&maxlen, cnt.get() + n, sizeof(maxlen), hipMemcpyDeviceToHost, s));
+        FAMG_CHECK_HIP(hipStreamSynchronize(s));
+        const unsigned g = (unsigned)std::min<int64_t>(n, 4096);
+        if (maxlen <= 2048)
+            hipLaunchKernelGGL((k_row_sort<2048, 64>), dim3(g), dim3(64), 0, s, T.rp64.get(), n,
+                               T.col.get(), T.val.get());
+        else
+            hipLaunchKernelGGL((k_row_sort<8192, 256>), dim3(g), dim3(256), 0, s, T.rp64.get(), n,
+                               T.col.get(), T.val.get());
+    }
     FAMG_CHECK_HIP(hipGetLastError());
     csr_finalize(T);
 }
@@ -287,6 +354,8 @@ void smooth_interp_fixup(GpuCsr &S, const GpuCsr &P, const double *diag, double 
     FAMG_CHECK_HIP(hipStreamSynchronize(s));
     FAMG_REQUIRE(h != 1, AMG_ERR_INVALID, "smooth_interpolation: diagonal nearly zero");
     FAMG_REQUIRE(h != 2, AMG_ERR_INVALID, "smooth_interpolation: P pattern not within A*P");
+    // the values changed in place: rebuild the derived SpMV storage (SELL copy)
+    csr_finalize(S);
 }
 
 }  // namespace famg

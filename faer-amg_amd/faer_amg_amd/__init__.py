@@ -48,6 +48,8 @@ SIGNATURES = {
     "amg_ctx_destroy": (i32, [vp]),
     "amg_ctx_synchronize": (i32, [vp]),
     "amg_ctx_stream": (i32, [vp, P(vp)]),
+    "amg_set_spmv_format": (i32, [i32]),
+    "amg_ctx_join_stream": (i32, [vp, vp, i32]),
     "amg_csr_create": (i32, [vp, i64, i64, vp, vp, vp, P(vp)]),
     "amg_csr_create_device_i32": (i32, [vp, i64, i64, vp, vp, vp, P(vp)]),
     "amg_csr_nnz": (i32, [vp, P(i64)]),
@@ -87,13 +89,20 @@ SIGNATURES = {
     "amg_comm_unique_id_size": (i32, []),
     "amg_comm_get_unique_id": (i32, [vp]),
     "amg_comm_create": (i32, [vp, i32, i32, vp, P(vp)]),
+    "amg_loopback_hub_create": (i32, [i32, P(vp)]),
+    "amg_loopback_hub_destroy": (i32, [vp]),
+    "amg_comm_create_loopback": (i32, [vp, vp, i32, P(vp)]),
     "amg_comm_destroy": (i32, [vp]),
+    "amg_comm_rank": (i32, [vp, P(i32), P(i32)]),
     "amg_comm_barrier": (i32, [vp]),
     "amg_comm_allreduce_max": (i32, [vp, P(dbl)]),
-    "amg_dist_csr_create": (i32, [vp, vp, vp, vp, P(vp)]),
-    "amg_dist_plan_info": (i32, [vp, vp]),
-    "amg_dist_multigrid_create": (i32, [vp, vp, i64, P(vp)]),
+    "amg_comm_allreduce_sum": (i32, [vp, P(dbl)]),
+    "amg_dist_multigrid_create": (i32, [vp, vp, vp, i64, P(vp)]),
     "amg_dist_local_rows": (i32, [vp, P(i64), P(i64)]),
+    "amg_dist_level_info": (i32, [vp, i64, vp]),
+    "amg_dist_level_operator": (i32, [vp, i64, P(vp)]),
+    "amg_dist_level_matrix": (i32, [vp, i64, i32, P(vp)]),
+    "amg_dist_stationary_solve": (i32, [vp, vp, vp, i64, dbl, vp, P(i64)]),
 }
 
 for _name, (_res, _args) in SIGNATURES.items():
@@ -121,6 +130,14 @@ def lib():
 
 def version():
     return _lib.amg_version().decode()
+
+
+SPMV_FORMATS = {"auto": 0, "csr": 1, "sell": 2}
+
+
+def set_spmv_format(policy):
+    """SpMV storage for matrices built afterwards: 'auto', 'csr' or 'sell'."""
+    _ck(_lib.amg_set_spmv_format(SPMV_FORMATS[policy]))
 
 
 def _dptr(x):
@@ -155,27 +172,55 @@ def _dptr(x):
 
 
 class Context:
-    """One device per process (amg_ctx).  `stream` may be a raw hipStream_t int."""
+    """One device per process (amg_ctx).  `stream` may be a raw hipStream_t int.
+
+    Device-memory calls made through this module are ordered against the
+    caller's torch.cuda.current_stream() automatically (amg_ctx_join_stream)."""
 
     def __init__(self, device=0, stream=None):
         h = vp()
         _ck(_lib.amg_ctx_create(device, vp(stream) if stream else None, C.byref(h)))
         self.h = h
         self.device = device
+        s = vp()
+        _ck(_lib.amg_ctx_stream(self.h, C.byref(s)))
+        self._stream = s.value or 0
 
     def synchronize(self):
         _ck(_lib.amg_ctx_synchronize(self.h))
 
     @property
     def stream(self):
-        s = vp()
-        _ck(_lib.amg_ctx_stream(self.h, C.byref(s)))
-        return s.value
+        return self._stream
 
-    def __del__(self):
+    def join_torch(self, ctx_waits):
+        """Order the library stream with torch's current stream (see amg_ctx_join_stream)."""
+        import torch
+        cur = torch.cuda.current_stream(self.device).cuda_stream
+        if cur != self._stream:
+            _ck(_lib.amg_ctx_join_stream(self.h, vp(cur) if cur else None, 1 if ctx_waits else 0))
+
+    def __del__(self, _destroy=_lib.amg_ctx_destroy):
         if getattr(self, "h", None):
-            _lib.amg_ctx_destroy(self.h)
+            _destroy(self.h)
             self.h = None
+
+
+class _ordered:
+    """Context manager: library stream waits for torch's stream before a device
+    call, torch's stream waits for the library stream after it."""
+
+    def __init__(self, ctx, mem):
+        self.ctx, self.on = ctx, (mem == AMG_MEM_DEVICE and ctx is not None)
+
+    def __enter__(self):
+        if self.on:
+            self.ctx.join_torch(True)
+
+    def __exit__(self, *exc):
+        if self.on:
+            self.ctx.join_torch(False)
+        return False
 
 
 class LinOp:
@@ -186,9 +231,9 @@ class LinOp:
         self.ctx = ctx
         self._refs = refs  # python-side references (the C side holds its own)
 
-    def __del__(self):
+    def __del__(self, _destroy=_lib.amg_linop_destroy):
         if getattr(self, "h", None):
-            _lib.amg_linop_destroy(self.h)
+            _destroy(self.h)
             self.h = None
 
     @property
@@ -216,24 +261,28 @@ class LinOp:
         pr, mr, nr, kr, lr = _dptr(rhs)
         if mo != mr or ko != kr:
             raise ValueError("out and rhs must live in the same memory with equal columns")
-        _ck(_lib.amg_linop_apply(self.h, po, lo, pr, lr, ko, mo))
+        with _ordered(self.ctx, mo):
+            _ck(_lib.amg_linop_apply(self.h, po, lo, pr, lr, ko, mo))
         return out
 
     def transpose_apply(self, out, rhs):
         po, mo, no, ko, lo = _dptr(out)
         pr, mr, nr, kr, lr = _dptr(rhs)
-        _ck(_lib.amg_linop_transpose_apply(self.h, po, lo, pr, lr, ko, mo))
+        with _ordered(self.ctx, mo):
+            _ck(_lib.amg_linop_transpose_apply(self.h, po, lo, pr, lr, ko, mo))
         return out
 
     def apply_in_place(self, rhs):
         """Precond::apply_in_place: rhs <- M rhs."""
         p, m, n, k, ld = _dptr(rhs)
-        _ck(_lib.amg_precond_apply_in_place(self.h, p, ld, k, m))
+        with _ordered(self.ctx, m):
+            _ck(_lib.amg_precond_apply_in_place(self.h, p, ld, k, m))
         return rhs
 
     def transpose_apply_in_place(self, rhs):
         p, m, n, k, ld = _dptr(rhs)
-        _ck(_lib.amg_precond_transpose_apply_in_place(self.h, p, ld, k, m))
+        with _ordered(self.ctx, m):
+            _ck(_lib.amg_precond_transpose_apply_in_place(self.h, p, ld, k, m))
         return rhs
 
     def __matmul__(self, x):
@@ -358,7 +407,7 @@ class Multigrid(LinOp):
             _ck(_lib.amg_multigrid_create(op.h, smoother.h, C.byref(h)))
         else:
             h = _handle
-        super().__init__(h, op.ctx if op is not None else smoother)
+        super().__init__(h, op.ctx)
 
     @classmethod
     def _from_handle(cls, h, ctx):
@@ -453,14 +502,141 @@ def stationary_solve(A, M, b, x, max_iter=100, rel_tol=1e-8):
     """examples/simple_geometric.rs:117-158 on device vectors; returns (iters, hist)."""
     hist = np.zeros(max_iter)
     it = i64()
-    _ck(_lib.amg_stationary_solve(A.h, M.h, vp(b.data_ptr()), vp(x.data_ptr()), max_iter,
-                                  rel_tol, hist.ctypes.data_as(vp), C.byref(it)))
+    with _ordered(A.ctx, AMG_MEM_DEVICE):
+        _ck(_lib.amg_stationary_solve(A.h, M.h, vp(b.data_ptr()), vp(x.data_ptr()), max_iter,
+                                      rel_tol, hist.ctypes.data_as(vp), C.byref(it)))
     return it.value, hist[:it.value]
 
 
 def pcg_solve(A, M, b, x, max_iter=1000, rel_tol=1e-8, abs_tol=0.0):
     hist = np.zeros(max(max_iter, 1))
     it = i64()
-    _ck(_lib.amg_pcg_solve(A.h, None if M is None else M.h, vp(b.data_ptr()), vp(x.data_ptr()),
-                           max_iter, rel_tol, abs_tol, hist.ctypes.data_as(vp), C.byref(it)))
+    with _ordered(A.ctx, AMG_MEM_DEVICE):
+        _ck(_lib.amg_pcg_solve(A.h, None if M is None else M.h, vp(b.data_ptr()),
+                               vp(x.data_ptr()), max_iter, rel_tol, abs_tol,
+                               hist.ctypes.data_as(vp), C.byref(it)))
     return it.value, hist[:min(it.value, max_iter)]
+
+
+# ------------------------------------------------------------------ multi-GPU
+
+def unique_id():
+    """ncclUniqueId bytes (create on rank 0, broadcast out of band)."""
+    n = _lib.amg_comm_unique_id_size()
+    buf = (C.c_char * n)()
+    _ck(_lib.amg_comm_get_unique_id(buf))
+    return bytes(buf)
+
+
+class LoopbackHub:
+    """In-process transport hub: `nranks` virtual ranks driven by host threads."""
+
+    def __init__(self, nranks):
+        h = vp()
+        _ck(_lib.amg_loopback_hub_create(nranks, C.byref(h)))
+        self.h = h
+        self.nranks = nranks
+
+    def __del__(self, _destroy=_lib.amg_loopback_hub_destroy):
+        if getattr(self, "h", None):
+            _destroy(self.h)
+            self.h = None
+
+
+class Comm:
+    """Per-process communicator: RCCL (`uid` from unique_id()) or loopback (`hub`)."""
+
+    def __init__(self, ctx, nranks=None, rank=0, uid=None, hub=None):
+        h = vp()
+        if hub is not None:
+            _ck(_lib.amg_comm_create_loopback(ctx.h, hub.h, rank, C.byref(h)))
+            self._hub = hub
+        else:
+            buf = (C.c_char * len(uid)).from_buffer_copy(uid)
+            _ck(_lib.amg_comm_create(ctx.h, nranks, rank, buf, C.byref(h)))
+        self.h = h
+        self.ctx = ctx
+        r, n = i32(), i32()
+        _ck(_lib.amg_comm_rank(h, C.byref(r), C.byref(n)))
+        self.rank, self.nranks = r.value, n.value
+
+    def barrier(self):
+        _ck(_lib.amg_comm_barrier(self.h))
+
+    def allreduce_max(self, v):
+        d = dbl(v)
+        _ck(_lib.amg_comm_allreduce_max(self.h, C.byref(d)))
+        return d.value
+
+    def allreduce_sum(self, v):
+        d = dbl(v)
+        _ck(_lib.amg_comm_allreduce_sum(self.h, C.byref(d)))
+        return d.value
+
+    def __del__(self, _destroy=_lib.amg_comm_destroy):
+        if getattr(self, "h", None):
+            _destroy(self.h)
+            self.h = None
+
+
+class DistMultigrid(LinOp):
+    """Row-block distributed V-cycle built from a global multigrid on this rank.
+
+    level_splits: list (one per level) of nranks+1 row splits."""
+
+    def __init__(self, comm, mg_global, level_splits, agglomerate_rows=1 << 16):
+        s = np.ascontiguousarray(np.concatenate([np.asarray(x, np.int64) for x in level_splits]))
+        h = vp()
+        _ck(_lib.amg_dist_multigrid_create(comm.h, mg_global.h, s.ctypes.data_as(vp),
+                                           int(agglomerate_rows), C.byref(h)))
+        super().__init__(h, comm.ctx)
+        self.comm = comm
+        self.nlevels = len(level_splits)
+
+    def local_rows(self):
+        b, e = i64(), i64()
+        _ck(_lib.amg_dist_local_rows(self.h, C.byref(b), C.byref(e)))
+        return b.value, e.value
+
+    def level_info(self, l):
+        info = np.zeros(6, np.int64)
+        _ck(_lib.amg_dist_level_info(self.h, l, info.ctypes.data_as(vp)))
+        keys = ("n_own", "n_ghost", "n_neighbors", "redundant", "halo_recv", "n_global")
+        return dict(zip(keys, (int(v) for v in info)))
+
+    def level_operator(self, l):
+        h = vp()
+        _ck(_lib.amg_dist_level_operator(self.h, l, C.byref(h)))
+        return LinOp(h, self.ctx, refs=(self,))
+
+    def level_matrix(self, l, which="A"):
+        """This rank's local CSR of level l (owned rows, [owned | ghost] columns)."""
+        h = vp()
+        _ck(_lib.amg_dist_level_matrix(self.h, l, {"A": 0, "R": 1, "P": 2}[which], C.byref(h)))
+        return SparseMatOp(h, self.ctx, refs=(self,))
+
+    def stationary_solve(self, b, x, max_iter=100, rel_tol=1e-8):
+        hist = np.zeros(max_iter)
+        it = i64()
+        with _ordered(self.ctx, AMG_MEM_DEVICE):
+            _ck(_lib.amg_dist_stationary_solve(self.h, vp(b.data_ptr()), vp(x.data_ptr()),
+                                               max_iter, rel_tol, hist.ctypes.data_as(vp),
+                                               C.byref(it)))
+        return it.value, hist[:it.value]
+
+
+def slab_splits(level_dims, nranks):
+    """Row splits per level for a z-slab partition of box-coarsened grids:
+    rank p owns planes [floor(p*nz/P), floor((p+1)*nz/P)) of every level."""
+    out = []
+    for (nx, ny, nz) in level_dims:
+        planes = [(p * nz) // nranks for p in range(nranks + 1)]
+        out.append([z * nx * ny for z in planes])
+    return out
+
+
+def box_level_dims(dims, box, nlevels):
+    d = [tuple(dims)]
+    for _ in range(nlevels - 1):
+        d.append(tuple(-(-a // b) for a, b in zip(d[-1], box)))
+    return d

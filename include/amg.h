@@ -71,6 +71,16 @@ amg_status amg_ctx_create(int device, void *hip_stream, amg_ctx **out);
 amg_status amg_ctx_destroy(amg_ctx *ctx);
 amg_status amg_ctx_synchronize(amg_ctx *ctx);
 amg_status amg_ctx_stream(amg_ctx *ctx, void **hip_stream);
+/* Order the context stream against another stream (e.g. the caller's
+ * torch.cuda.current_stream()): ctx_waits != 0 makes the context stream wait
+ * for the work already queued on `other`; ctx_waits == 0 makes `other` wait for
+ * the context stream.  Event-based, no host synchronisation. */
+amg_status amg_ctx_join_stream(amg_ctx *ctx, void *other, int32_t ctx_waits);
+/* SpMV storage policy for matrices built after the call (process-wide):
+ * 0 auto (SELL-64 for short regular rows, CSR-stream otherwise), 1 CSR-stream
+ * only, 2 SELL-64 whenever rows are <= 256 long.  Results are identical up to
+ * the summation order of rows longer than 128 entries. */
+amg_status amg_set_spmv_format(int32_t policy);
 
 /* ---- sparse matrices (replaces SparseMatOp::new core.rs:56-74, ParSpmmOp::new
  *      par_spmm.rs:31-96, and the SparseRowMat<usize,f64> LinOp used at
@@ -213,7 +223,14 @@ amg_status amg_pcg_solve(amg_linop *A, amg_linop *M, const double *b, double *x,
 
 /* ---- multi-GPU (row-block partition + RCCL halo exchange) ------- */
 
+/* The reference has no distributed backend (rayon only).  Here the
+ * V-cycle is row-block partitioned: rank p owns a contiguous row range of
+ * every level; before each SpMV the ghost entries its rows reference are
+ * refreshed by a halo exchange (grouped RCCL send/recv over xGMI); levels with
+ * fewer than `agglomerate_rows` rows are gathered (ncclAllGather) and solved
+ * redundantly on every rank. */
 typedef struct amg_comm amg_comm;
+typedef struct amg_loopback_hub amg_loopback_hub;
 /* ncclUniqueId size in bytes (128). */
 int32_t amg_comm_unique_id_size(void);
 /* Fill `id` (amg_comm_unique_id_size() bytes) on rank 0; broadcast it out of band. */
@@ -221,26 +238,44 @@ amg_status amg_comm_get_unique_id(void *id);
 /* One RCCL communicator per process (one process per GPU). */
 amg_status amg_comm_create(amg_ctx *ctx, int32_t nranks, int32_t rank, const void *id,
                            amg_comm **out);
+/* In-process transport for validation: `nranks` virtual ranks, each driven by
+ * its own host thread with its own context, exchange through device copies. */
+amg_status amg_loopback_hub_create(int32_t nranks, amg_loopback_hub **out);
+amg_status amg_loopback_hub_destroy(amg_loopback_hub *hub);
+amg_status amg_comm_create_loopback(amg_ctx *ctx, amg_loopback_hub *hub, int32_t rank,
+                                    amg_comm **out);
 amg_status amg_comm_destroy(amg_comm *comm);
+amg_status amg_comm_rank(const amg_comm *comm, int32_t *rank, int32_t *nranks);
 amg_status amg_comm_barrier(amg_comm *comm);
-/* Max over ranks of a host double (allreduce on the device). */
+/* Max / sum over ranks of a host double (reduced on the device). */
 amg_status amg_comm_allreduce_max(amg_comm *comm, double *value);
+amg_status amg_comm_allreduce_sum(amg_comm *comm, double *value);
 
-/* Partition plan for rows [row_begin, row_end) of a global operator: given the
- * global CSR (on this rank's device), extract the owned rows with the column
- * space split into owned + ghost entries and the halo exchange plan.  Host logic
- * exposed for tests: amg_dist_plan_info reports (n_owned, n_ghost, n_neighbors). */
-amg_status amg_dist_csr_create(amg_comm *comm, const amg_linop *A_global,
-                               const int64_t *row_splits, const int64_t *col_splits,
-                               amg_linop **out);
-amg_status amg_dist_plan_info(const amg_linop *dist, int64_t *info3);
-/* Distributed SA multigrid: every level row-block partitioned by the given
- * global multigrid's sizes and z-slab splits; levels with fewer than
- * agglomerate_rows global rows run redundantly on every rank. */
+/* Distributed multigrid from a global multigrid held by every rank (identical
+ * on all ranks, e.g. built redundantly by amg_sa_build_box).  level_splits:
+ * nlevels x (nranks+1) row splits (row range of rank p at level l is
+ * [s[l*(nranks+1)+p], s[l*(nranks+1)+p+1])).  Levels from the first one with
+ * fewer than agglomerate_rows rows down are run redundantly on every rank.
+ * Every distributed level must be smoothed by a diagonal smoother.  apply()
+ * maps the rank's owned rows of rhs (n_own) to its owned rows of out. */
 amg_status amg_dist_multigrid_create(amg_comm *comm, const amg_linop *mg_global,
-                                     int64_t agglomerate_rows, amg_linop **out);
+                                     const int64_t *level_splits, int64_t agglomerate_rows,
+                                     amg_linop **out);
 /* Row range [begin, end) of this rank at the finest level. */
 amg_status amg_dist_local_rows(const amg_linop *dist, int64_t *begin, int64_t *end);
+/* Per-level plan: info[0..5] = n_owned, n_ghost, n_neighbors, redundant (0/1),
+ * halo doubles received per exchange, global rows. */
+amg_status amg_dist_level_info(const amg_linop *dist, int64_t level, int64_t *info6);
+/* The distributed A_l as a LinOp (owned rows in, owned rows out; halo inside). */
+amg_status amg_dist_level_operator(const amg_linop *dist, int64_t level, amg_linop **out);
+/* This rank's local CSR of a distributed level (which: 0 A_l, 1 R_l, 2 P_l):
+ * owned rows, columns in the level's [owned | ghost] numbering. */
+amg_status amg_dist_level_matrix(const amg_linop *dist, int64_t level, int32_t which,
+                                 amg_linop **out);
+/* Distributed stationary solve / PCG (dots all-reduced over ranks): local vectors. */
+amg_status amg_dist_stationary_solve(amg_linop *dist_mg, const double *b, double *x,
+                                     int64_t max_iter, double rel_tol, double *hist,
+                                     int64_t *iters);
 
 #ifdef __cplusplus
 }

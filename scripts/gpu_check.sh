@@ -1,0 +1,28 @@
+#!/bin/bash
+# GPU-box check: each GPU step under its own time limit; stop at the first
+# step that faults, aborts or times out (exit codes other than 0/1).
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out
+step() {  # step NAME SECONDS CMD...
+    local name=$1 secs=$2; shift 2
+    echo "== $name" >&2
+    timeout -k 10 "$secs" "$@" > "gpurun_out/$name.log" 2>&1
+    local rc=$?
+    echo "$name rc=$rc"
+    tail -5 "gpurun_out/$name.log"
+    if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "stopping after $name (rc=$rc)"; exit $rc; fi
+    return 0
+}
+for s in "$@"; do
+    case $s in
+        tests) step pytest_gpu 900 python -m pytest tests -m gpu -q ;;
+        smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
+        bench) step bench 600 python bench.py --steps 20 --warmup 3 ;;
+        benchq) step bench 400 python bench.py --steps 20 --warmup 3 --no-cpu-baseline --ab ;;
+        dist2) step dist2 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
+                  --master-addr 127.0.0.1 --master-port 29511 bench.py --gpus 2 --edge 64 --steps 5 --warmup 1 ;;
+        prof) export TMPDIR=/tmp; R=$(pwd)
+              step prof 600 rocprofv3 --kernel-trace --stats -d "$R/gpurun_out/prof" -o run \
+                  --output-format csv -- python3 "$R/bench.py" --steps 20 --warmup 3 --no-cpu-baseline ;;
+    esac
+done

@@ -1,0 +1,159 @@
+"""Distributed V-cycle on one GPU: N virtual ranks (host threads, each with its
+own context/stream) over the loopback transport run the same row-block
+partitioned code as the RCCL path; results must equal the single-GPU V-cycle
+(tolerance 1e-13 relative: long rows may be reduced with a different lane
+split in the local blocks) and the oracle (1e-11)."""
+import threading
+
+import numpy as np
+import pytest
+
+import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+
+def fa():
+    import faer_amg_amd
+    return faer_amg_amd
+
+
+def run_ranks(nranks, fn):
+    """Run fn(rank) in nranks threads; re-raise the first failure."""
+    out, errs = [None] * nranks, []
+
+    def body(r):
+        try:
+            out[r] = fn(r)
+        except BaseException as e:  # noqa: BLE001
+            errs.append(e)
+
+    th = [threading.Thread(target=body, args=(r,)) for r in range(nranks)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(600)
+    if errs:
+        raise errs[0]
+    return out
+
+
+def global_reference(dims, coarsest, b, problem="7pt"):
+    import torch
+    ctx = fa().Context(0)
+    A = (fa().SparseMatOp.laplace3d_7pt(ctx, *dims) if problem == "7pt"
+         else fa().SparseMatOp.aniso27(ctx, *dims, 1.0, 1.0, 0.01))
+    mg = fa().sa_build_box(A, dims, (2, 2, 2), coarsest_dim=coarsest)
+    bd = torch.as_tensor(b, device="cuda:0")
+    z = torch.empty_like(bd)
+    mg.apply(z, bd)
+    ctx.synchronize()
+    levels = []
+    for l in range(mg.levels()):
+        Al, _, Rl, Pl = mg.level(l)
+        d = {"A": O.Csr.from_arrays(*Al.dims(), *Al.arrays()),
+             "smoother": "chol" if l == mg.levels() - 1 else "jacobi"}
+        if Rl is not None:
+            d["R"] = O.Csr.from_arrays(*Rl.dims(), *Rl.arrays())
+            d["P"] = O.Csr.from_arrays(*Pl.dims(), *Pl.arrays())
+        levels.append(d)
+    zref = O.Multigrid(levels).apply(b)
+    return z.cpu().numpy(), zref, mg.levels()
+
+
+def dist_apply(nranks, dims, coarsest, b, agglo, split_kind="slab", problem="7pt"):
+    import torch
+    hub = fa().LoopbackHub(nranks)
+
+    def rank_fn(r):
+        ctx = fa().Context(0)
+        A = (fa().SparseMatOp.laplace3d_7pt(ctx, *dims) if problem == "7pt"
+             else fa().SparseMatOp.aniso27(ctx, *dims, 1.0, 1.0, 0.01))
+        mg = fa().sa_build_box(A, dims, (2, 2, 2), coarsest_dim=coarsest)
+        nl = mg.levels()
+        if split_kind == "slab":
+            splits = fa().slab_splits(fa().box_level_dims(dims, (2, 2, 2), nl), nranks)
+        else:  # arbitrary (unaligned) equal row splits
+            splits = []
+            for l in range(nl):
+                n = mg.level(l)[0].nrows
+                splits.append([(p * n) // nranks for p in range(nranks + 1)])
+        comm = fa().Comm(ctx, hub=hub, rank=r)
+        dm = fa().DistMultigrid(comm, mg, splits, agglomerate_rows=agglo)
+        r0, r1 = dm.local_rows()
+        bl = torch.as_tensor(np.ascontiguousarray(b[r0:r1]), device="cuda:0")
+        zl = torch.empty_like(bl)
+        dm.apply(zl, bl)
+        ctx.synchronize()
+        infos = [dm.level_info(l) for l in range(nl)]
+        # distributed stationary solve (3 cycles) as well
+        x = torch.zeros_like(bl)
+        it, hist = dm.stationary_solve(bl, x, max_iter=4, rel_tol=1e-300)
+        return r0, r1, zl.cpu().numpy(), infos, hist
+
+    res = run_ranks(nranks, rank_fn)
+    z = np.zeros(len(b))
+    for r0, r1, zl, _, _ in res:
+        z[r0:r1] = zl
+    return z, res
+
+
+@pytest.mark.parametrize("nranks,split_kind,agglo", [
+    (2, "slab", 1000),
+    (3, "equal", 1000),
+    (4, "slab", 1 << 30),   # everything agglomerated (La = 0)
+    (4, "equal", 200),
+])
+def test_dist_vcycle_matches_single_gpu(nranks, split_kind, agglo):
+    dims = (16, 12, 24)
+    b = np.random.default_rng(nranks).uniform(-1, 1, int(np.prod(dims)))
+    zg, zref, nl = global_reference(dims, 60, b)
+    z, res = dist_apply(nranks, dims, 60, b, agglo, split_kind)
+    assert np.linalg.norm(z - zg) <= 1e-13 * np.linalg.norm(zg)
+    assert np.linalg.norm(z - zref) <= 1e-11 * np.linalg.norm(zref)
+    # every rank computes the same residual history
+    h0 = res[0][4]
+    for r in res[1:]:
+        assert np.allclose(r[4], h0, rtol=1e-12, atol=0)
+    assert h0[1] < h0[0]
+
+
+def test_dist_plan_is_consistent():
+    dims = (12, 12, 16)
+    b = np.ones(int(np.prod(dims)))
+    _, res = dist_apply(2, dims, 60, b, 100)
+    infos = [r[3] for r in res]
+    # z-slab partition of a 7-pt operator: each rank receives one 12x12 plane
+    assert infos[0][0]["halo_recv"] == 144 and infos[1][0]["halo_recv"] == 144
+    assert infos[0][0]["n_own"] + infos[1][0]["n_own"] == 12 * 12 * 16
+    assert all(i[-1]["redundant"] == 1 for i in infos)
+
+
+def test_dist_27pt():
+    dims = (10, 10, 16)
+    b = np.random.default_rng(9).uniform(-1, 1, 1600)
+    zg, zref, _ = global_reference(dims, 60, b, problem="27pt")
+    z, _ = dist_apply(2, dims, 60, b, 100, "slab", problem="27pt")
+    assert np.linalg.norm(z - zref) <= 1e-11 * np.linalg.norm(zref)
+
+
+def test_rccl_single_rank():
+    """RCCL communicator with one rank: unique id, barrier, allreduce, and a
+    distributed multigrid whose only rank owns everything."""
+    import torch
+    ctx = fa().Context(0)
+    comm = fa().Comm(ctx, nranks=1, rank=0, uid=fa().unique_id())
+    comm.barrier()
+    assert comm.allreduce_max(3.5) == 3.5
+    assert comm.allreduce_sum(2.0) == 2.0
+    dims = (12, 12, 12)
+    A = fa().SparseMatOp.laplace3d_7pt(ctx, *dims)
+    mg = fa().sa_build_box(A, dims, (2, 2, 2), coarsest_dim=60)
+    splits = fa().slab_splits(fa().box_level_dims(dims, (2, 2, 2), mg.levels()), 1)
+    dm = fa().DistMultigrid(comm, mg, splits, agglomerate_rows=100)
+    b = torch.as_tensor(np.random.default_rng(1).uniform(-1, 1, 1728), device="cuda:0")
+    z1, z2 = torch.empty_like(b), torch.empty_like(b)
+    dm.apply(z1, b)
+    mg.apply(z2, b)
+    ctx.synchronize()
+    assert torch.allclose(z1, z2, rtol=1e-13, atol=0)

@@ -99,6 +99,52 @@ def test_spmv_irregular_golden(ctx):
     assert np.all(y[np.diff(g["rowptr"]) == 0] == 0)
 
 
+@pytest.mark.parametrize("fmt", ["csr", "sell"])
+def test_spmv_formats(ctx, fmt):
+    """Both storage paths (CSR-stream and SELL-64) on short, long, empty and
+    rectangular rows.  SELL sums every row sequentially in one lane (bitwise
+    equal to the oracle); CSR-stream does so when a block holds >= 128 rows
+    (rows of <= 16 entries) and splits longer rows over lanes (bounded)."""
+    fa().set_spmv_format(fmt)
+    try:
+        OA = O.laplace3d_7pt(33, 17, 9)
+        x = np.random.default_rng(10).standard_normal(OA.ncols)
+        assert np.array_equal(apply_dev(ctx, gpu_csr(ctx, OA), x, OA.nrows), OA.spmv(x))
+        g = load("g3_sa7pt16.npz")
+        for key in ("P0", "R0", "A1"):
+            m, n = g[f"{key}_shape"]
+            OM = O.Csr.from_arrays(m, n, g[f"{key}_rowptr"], g[f"{key}_col"], g[f"{key}_val"])
+            xx = np.random.default_rng(11).standard_normal(n)
+            y = apply_dev(ctx, gpu_csr(ctx, OM), xx, m)
+            if fmt == "sell" or key == "P0":
+                assert np.array_equal(y, OM.spmv(xx)), key
+            else:
+                assert np.all(np.abs(y - OM.spmv(xx)) <= spmv_bound(OM.to_scipy(), xx)), key
+        g5 = load("g5_spmv_irregular.npz")
+        m, n = g5["shape"]
+        A = fa().SparseMatOp.from_arrays(ctx, m, n, g5["rowptr"], g5["col"], g5["val"])
+        y = apply_dev(ctx, A, g5["x"], m)
+        S = sp.csr_matrix((g5["val"], g5["col"], g5["rowptr"]), shape=(m, n))
+        assert np.all(np.abs(y - g5["y"]) <= spmv_bound(S, g5["x"]))
+    finally:
+        fa().set_spmv_format("auto")
+
+
+def test_vcycle_forced_sell(ctx):
+    fa().set_spmv_format("sell")
+    try:
+        dims = (20, 16, 12)
+        A = fa().SparseMatOp.laplace3d_7pt(ctx, *dims)
+        mg = fa().sa_build_box(A, dims, (2, 2, 2), coarsest_dim=200)
+        levels = oracle_levels_from_gpu(mg, "jacobi")
+        b = np.random.default_rng(12).uniform(-1, 1, A.nrows)
+        zref = O.Multigrid(levels).apply(b)
+        z = apply_dev(ctx, mg, b, A.nrows)
+        assert np.linalg.norm(z - zref) <= 1e-11 * np.linalg.norm(zref)
+    finally:
+        fa().set_spmv_format("auto")
+
+
 def test_spmv_host_memory_and_multicolumn(ctx):
     OA = O.laplace3d_7pt(10, 10, 10)
     A = gpu_csr(ctx, OA)
