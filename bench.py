@@ -49,6 +49,21 @@ def splitmix_uniform(n, seed=42):
     return 2.0 * u - 1.0
 
 
+def measured_traffic(edge, problem):
+    """HBM bytes per fine-SpMV launch from the committed rocprofv3 PMC passes
+    (scripts/pmc_fine_spmv.py + scripts/pmc_summary.py; FETCH_SIZE calibrated on
+    a diagonal matrix through the same kernel).  None if not measured for this
+    workload."""
+    if edge != 256 or problem != "7pt":
+        return None, None
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "fine_spmv_traffic.json")))
+    if not files:
+        return None, None
+    d = json.load(open(files[-1]))
+    return d["hbm_bytes_per_launch"], os.path.relpath(files[-1], ROOT)
+
+
 def spmv_bytes(nrows, ncols, nnz):
     """Algorithmic bytes of y = A x with 32-bit indices."""
     return 12 * nnz + 4 * (nrows + 1) + 8 * ncols + 8 * nrows
@@ -220,6 +235,7 @@ def run_single(args):
             log(f"cpu baseline failed: {e!r}")
 
     cycles_per_s = 1000.0 / ms_per_cycle
+    traffic, traffic_src = measured_traffic(args.edge, args.problem)
     return {
         "metric": METRIC,
         "value": round(cycles_per_s, 3),
@@ -244,7 +260,8 @@ def run_single(args):
                    "parallelism": "single GPU"},
         "fine_spmv_gbs": round(achieved, 1),
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
-                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                     "traffic_source": traffic_src,
                      "kernel": "spmv_sell_kernel<SET> on A_0 (SELL-64)",
                      "bytes_per_launch": bytes_spmv, "ms_per_launch": round(spmv_ms, 5)},
         "cpu_baseline": cpu,

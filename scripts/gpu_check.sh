@@ -21,6 +21,11 @@ for s in "$@"; do
         benchq) step bench 400 python bench.py --steps 20 --warmup 3 --no-cpu-baseline --ab ;;
         dist2) step dist2 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
                   --master-addr 127.0.0.1 --master-port 29511 bench.py --gpus 2 --edge 64 --steps 5 --warmup 1 ;;
+        pmc) export TMPDIR=/tmp; R=$(pwd)
+              step pmc_fetch 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d "$R/gpurun_out/pmc_fetch" -o run \
+                  --output-format csv -- python3 "$R/scripts/pmc_fine_spmv.py"
+              step pmc_write 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d "$R/gpurun_out/pmc_write" -o run \
+                  --output-format csv -- python3 "$R/scripts/pmc_fine_spmv.py" ;;
         prof) export TMPDIR=/tmp; R=$(pwd)
               step prof 600 rocprofv3 --kernel-trace --stats -d "$R/gpurun_out/prof" -o run \
                   --output-format csv -- python3 "$R/bench.py" --steps 20 --warmup 3 --no-cpu-baseline ;;

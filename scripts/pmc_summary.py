@@ -1,0 +1,52 @@
+"""Fine-SpMV HBM traffic from the rocprofv3 PMC passes of scripts/pmc_fine_spmv.py.
+
+  python scripts/pmc_summary.py FETCH.csv WRITE.csv OUT.json
+
+FETCH_SIZE / WRITE_SIZE are in KiB per dispatch.  The first ITERS SELL
+dispatches are the calibration (diagonal matrix, n = 256^3: exactly
+20 n + 4 ceil(n/64) + 4 bytes read, 8 n written); the last ITERS are the 7-point
+operator.  Read bytes = FETCH_SIZE * 1024 * (known calibration bytes /
+calibration FETCH_SIZE bytes) -- on gfx950 that factor is ~2 for streaming
+loads (MI355X_MICROARCH.md, HBM section).
+"""
+import csv
+import json
+import statistics
+import sys
+
+ITERS = 10
+N = 256 ** 3
+
+
+def sell_values(path, counter):
+    rows = [r for r in csv.DictReader(open(path))
+            if "spmv_sell_kernel" in r["Kernel_Name"] and r["Counter_Name"] == counter]
+    rows.sort(key=lambda r: int(r["Dispatch_Id"]))
+    vals = [float(r["Counter_Value"]) * 1024.0 for r in rows]
+    assert len(vals) == 2 * ITERS, (path, len(vals))
+    return vals[:ITERS], vals[ITERS:]
+
+
+def main(fetch_csv, write_csv, out_json):
+    cal_f, fine_f = sell_values(fetch_csv, "FETCH_SIZE")
+    cal_w, fine_w = sell_values(write_csv, "WRITE_SIZE")
+    cal_read_known = 20 * N + 4 * (-(-N // 64) + 1)
+    factor = cal_read_known / statistics.median(cal_f)
+    read = statistics.median(fine_f) * factor
+    write = statistics.median(fine_w)
+    out = {
+        "kernel": "spmv_sell_kernel<SET> on A_0 (7-pt 256^3)",
+        "fetch_correction_factor": round(factor, 4),
+        "calibration": {"known_read_bytes": cal_read_known,
+                        "fetch_size_bytes": statistics.median(cal_f),
+                        "write_size_bytes": statistics.median(cal_w), "known_write_bytes": 8 * N},
+        "read_bytes_per_launch": round(read),
+        "write_bytes_per_launch": round(write),
+        "hbm_bytes_per_launch": round(read + write),
+    }
+    json.dump(out, open(out_json, "w"), indent=1)
+    print(json.dumps(out, indent=1))
+
+
+if __name__ == "__main__":
+    main(*sys.argv[1:4])
