@@ -149,9 +149,16 @@ amg_status amg_ctx_join_stream(amg_ctx *ctx, void *other, int32_t ctx_waits) {
     });
 }
 
+amg_status amg_set_alloc_policy(int32_t policy) {
+    return guard([&] {
+        FAMG_REQUIRE(policy == 0 || policy == 1, AMG_ERR_INVALID, "policy must be 0 or 1");
+        g_alloc_policy = policy;
+    });
+}
+
 amg_status amg_set_spmv_format(int32_t policy) {
     return guard([&] {
-        FAMG_REQUIRE(policy >= 0 && policy <= 2, AMG_ERR_INVALID, "policy must be 0, 1 or 2");
+        FAMG_REQUIRE(policy >= 0 && policy <= 3, AMG_ERR_INVALID, "policy must be 0..3");
         g_spmv_format_policy = policy;
     });
 }
@@ -444,6 +451,19 @@ amg_status amg_multigrid_set_graph(amg_linop *mg, int32_t enable) {
         auto m = need_mg(mg);
         std::lock_guard<std::mutex> lk(m->mtx);
         m->use_graph = enable != 0;
+        m->invalidate_graphs();
+    });
+}
+
+amg_status amg_multigrid_set_option(amg_linop *mg, int32_t option, int64_t value) {
+    return guard([&] {
+        auto m = need_mg(mg);
+        std::lock_guard<std::mutex> lk(m->mtx);
+        switch (option) {
+        case 0: m->use_graph = value != 0; break;
+        case 1: m->sgs_residual_form = value != 0; break;
+        default: fail(AMG_ERR_INVALID, "unknown multigrid option");
+        }
         m->invalidate_graphs();
     });
 }

@@ -37,8 +37,15 @@ __global__ void k_narrow_rp(const int64_t *rp64, int32_t *rp32, int64_t n1) {
     if (i < n1) rp32[i] = static_cast<int32_t>(rp64[i]);
 }
 
-void csr_finalize(GpuCsr &m) {
+void csr_finalize(GpuCsr &m, const std::vector<int64_t> *segments) {
     Ctx &ctx = *m.ctx;
+    if (segments) {
+        FAMG_REQUIRE(segments->size() >= 2 && segments->front() == 0 && segments->back() == m.nrows,
+                     AMG_ERR_INVALID, "row segments must start at 0 and end at nrows");
+        m.seg_rows = *segments;
+    } else {
+        m.seg_rows = {0, m.nrows};
+    }
     if (m.nnz >= (int64_t(1) << 31)) {  // setup-only matrix: no SpMV view
         m.rp32.release();
         m.sched.release();
@@ -54,14 +61,14 @@ void csr_finalize(GpuCsr &m) {
                                   hipMemcpyDeviceToHost, ctx.stream));
     FAMG_CHECK_HIP(hipStreamSynchronize(ctx.stream));
     std::vector<int32_t> sched;
-    std::vector<int64_t> segb;
-    build_schedule(rp, {0, m.nrows}, sched, segb);
+    build_schedule(rp, m.seg_rows, sched, m.seg_blk);
     m.nblocks = static_cast<int64_t>(sched.size()) - 1;
     m.sched.resize(sched.size());
     FAMG_CHECK_HIP(hipMemcpyAsync(m.sched.get(), sched.data(), sched.size() * sizeof(int32_t),
                                   hipMemcpyHostToDevice, ctx.stream));
     FAMG_CHECK_HIP(hipStreamSynchronize(ctx.stream));
     build_sell(m, rp);
+    choose_kernel(m);
 }
 
 void csr_from_host(GpuCsr &m, Ctx *ctx, int64_t nrows, int64_t ncols, const int64_t *rowptr,

@@ -35,13 +35,18 @@ struct GpuCsr {
     DevBuf<double> val;    // padded by 2 entries
     DevBuf<int32_t> sched; // stream-SpMV row blocks: nblocks+1 row starts
     int64_t nblocks = 0;
-    // SELL-64 copy for short, regular rows: slice s holds rows [64s, 64s+64),
-    // width w_s = max row length in the slice, entries column-major
-    // (entry k of lane l at sell_off[s] + 64 k + l); padding = 0.0 * x[c_last].
+    // Row segments (SGS colors, halo boundary/interior): [seg_rows[g], seg_rows[g+1]).
+    // Schedule blocks and SELL slices never straddle a segment.
+    std::vector<int64_t> seg_rows, seg_blk, seg_slc;
+    // SELL-64 copy: slice s holds rows [sell_row0[s], sell_row0[s+1]) (<= 64),
+    // width w_s = its longest row; entry step k of the slice is a 768-B record
+    // [64 fp64 values | 64 int32 columns] at byte 12*sell_off[s] + 768 k (lane l
+    // = row sell_row0[s] + l); padding = 0.0 * x[c_last].
     DevBuf<int32_t> sell_off;
-    DevBuf<int32_t> sell_col;
-    DevBuf<double> sell_val;
+    DevBuf<int32_t> sell_row0;
+    DevBuf<char> sell_data;
     int64_t nslices = 0, sell_padded = 0;
+    int kernel = 0;  // SpmvKernel chosen at finalize
     bool spmv_ready() const { return rp32.get() != nullptr && sched.get() != nullptr; }
     bool has_sell() const { return sell_off.get() != nullptr; }
     int64_t index_bytes() const { return 12 * nnz + 4 * (nrows + 1); }
@@ -49,12 +54,17 @@ struct GpuCsr {
 
 // Allocate a CSR with the given shape/nnz (arrays uninitialised).
 void csr_alloc(GpuCsr &m, Ctx *ctx, int64_t nrows, int64_t ncols, int64_t nnz);
-// Build rp32 (if nnz < 2^31), the stream schedule and, for short regular rows,
-// the SELL-64 copy.  Host pass over the row pointers (setup only).
-void csr_finalize(GpuCsr &m);
-// Format policy (tests/bench can force a path): 0 auto, 1 CSR-stream only, 2 SELL when valid
+// Build rp32 (if nnz < 2^31), the stream schedule, the SELL-64 copy for short
+// regular rows, and pick the SpMV kernel; `segments` (row bounds, first 0, last
+// nrows) keeps blocks/slices inside segments.  Host pass over the row pointers
+// (setup only).  Must be called again after values change in place.
+void csr_finalize(GpuCsr &m, const std::vector<int64_t> *segments = nullptr);
+// Format policy (process-wide, for matrices finalized afterwards):
+// 0 auto, 1 CSR-stream only, 2 SELL whenever rows <= 256, 3 vector (no SELL)
 extern int g_spmv_format_policy;
+enum SpmvKernel : int { SPMV_KERNEL_STREAM = 0, SPMV_KERNEL_SELL = 1, SPMV_KERNEL_VECTOR = 2 };
 void build_sell(GpuCsr &m, const std::vector<int64_t> &rp);
+void choose_kernel(GpuCsr &m);
 // Host upload from usize-compatible arrays.
 void csr_from_host(GpuCsr &m, Ctx *ctx, int64_t nrows, int64_t ncols, const int64_t *rowptr,
                    const int64_t *col, const double *val);
@@ -79,10 +89,10 @@ struct SpmvEpi {
     const int32_t *perm = nullptr;
 };
 
-// Stream (LDS-staged) CSR SpMV over blocks [blk_begin, blk_end) of m's schedule.
+// y = epilogue(A x) over all rows (seg < 0) or over row segment `seg`, with the
+// kernel chosen for m at finalize (SELL-64 / vector / CSR-stream).
 void spmv(const GpuCsr &m, const double *x, double *y, SpmvMode mode, const SpmvEpi &epi,
-          hipStream_t s, int64_t blk_begin = 0, int64_t blk_end = -1,
-          const int32_t *sched_override = nullptr);
+          hipStream_t s, int64_t seg = -1);
 
 // BLAS-1 (n-vectors, device pointers)
 void vec_fill(double *x, double v, int64_t n, hipStream_t s);
@@ -166,8 +176,7 @@ struct SgsOp : LinOp {
     GpuCsr Ap;             // rows grouped by color (columns in original numbering)
     DevBuf<int32_t> perm;  // permuted row p -> original row
     DevBuf<double> dinv;   // 1/a_ii at permuted rows
-    std::vector<int64_t> color_ptr;   // rows of color c: [color_ptr[c], color_ptr[c+1])
-    std::vector<int64_t> color_blk;   // schedule blocks of color c
+    std::vector<int64_t> color_ptr;   // rows of color c: [color_ptr[c], color_ptr[c+1]) = Ap segment c
     std::vector<int32_t> host_colors;
     int64_t ncolors = 0;
     DevBuf<double> e_;     // scratch correction
@@ -175,6 +184,8 @@ struct SgsOp : LinOp {
     bool is_precond() const override { return true; }
     // e = SGS(r) from e = 0 (device pointers, e != r)
     void sweep(double *e, const double *r);
+    // x <- x + SGS(b - A x), in place on x
+    void sweep_x(double *x, const double *b);
     void apply(double *out, const double *rhs) override;
     void apply_in_place(double *rhs) override;
 };
@@ -196,6 +207,7 @@ struct MultigridOp : LinOp {
     std::vector<MgLevel> levels;
     int64_t mu = 1, steps = 1;
     bool use_graph = true;
+    bool sgs_residual_form = false;  // true: literal smooth() order (residual SpMV + SGS(r))
     std::mutex mtx;
     Kind kind() const override { return Kind::Multigrid; }
     bool is_precond() const override { return true; }
@@ -221,11 +233,15 @@ struct MultigridOp : LinOp {
 
 // ---------------------------------------------------------------- factories
 
+// sa_build_box(smoother = SGS): levels whose greedy coloring needs more colors
+// than this get the L1 smoother instead
+constexpr int64_t SGS_MAX_COLORS = 32;
+
 CsrPtr make_csr(Ctx *ctx);
 std::shared_ptr<DiagOp> make_jacobi(CsrOp &A, double omega);
 std::shared_ptr<DiagOp> make_l1(CsrOp &A);
 std::shared_ptr<DiagOp> make_l2(CsrOp &A);
-std::shared_ptr<SgsOp> make_sgs(const CsrPtr &A, const int32_t *colors);
+std::shared_ptr<SgsOp> make_sgs(const CsrPtr &A, const int32_t *colors, bool validate = true);
 std::shared_ptr<CoarseCholOp> make_coarse_chol(CsrOp &A);
 
 // SA setup pieces

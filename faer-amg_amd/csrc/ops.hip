@@ -132,9 +132,12 @@ std::shared_ptr<DiagOp> make_l2(CsrOp &A) {
 // --------------------------------------------------------- multicolor SGS
 
 int64_t greedy_coloring(const GpuCsr &A, std::vector<int32_t> &color) {
-    std::vector<int64_t> rp(A.nrows + 1), col(A.nnz);
-    std::vector<double> val(A.nnz);
-    csr_to_host(A, rp.data(), col.data(), val.data());
+    std::vector<int64_t> rp(A.nrows + 1);
+    std::vector<int32_t> col(A.nnz);
+    hipStream_t s = A.ctx->stream;
+    FAMG_CHECK_HIP(hipMemcpyAsync(rp.data(), A.rp64.get(), (A.nrows + 1) * sizeof(int64_t), hipMemcpyDeviceToHost, s));
+    if (A.nnz) FAMG_CHECK_HIP(hipMemcpyAsync(col.data(), A.col.get(), A.nnz * sizeof(int32_t), hipMemcpyDeviceToHost, s));
+    FAMG_CHECK_HIP(hipStreamSynchronize(s));
     color.assign(A.nrows, 0);
     std::vector<int64_t> mark(64, -1);
     int64_t nc = 0;
@@ -183,7 +186,7 @@ __global__ void k_sgs_first(const int32_t *perm, const double *dinv, const doubl
     }
 }
 
-std::shared_ptr<SgsOp> make_sgs(const CsrPtr &A, const int32_t *colors) {
+std::shared_ptr<SgsOp> make_sgs(const CsrPtr &A, const int32_t *colors, bool validate) {
     FAMG_REQUIRE(A->nrows == A->ncols, AMG_ERR_DIM, "sgs: matrix must be square");
     Ctx *ctx = A->ctx;
     hipStream_t s = ctx->stream;
@@ -200,14 +203,15 @@ std::shared_ptr<SgsOp> make_sgs(const CsrPtr &A, const int32_t *colors) {
             FAMG_REQUIRE(color[i] >= 0, AMG_ERR_INVALID, "negative color");
             op->ncolors = std::max<int64_t>(op->ncolors, color[i] + 1);
         }
-        // validate: no two coupled rows share a color
-        std::vector<int64_t> rp(n + 1), col(A->m.nnz);
-        std::vector<double> val(A->m.nnz);
-        csr_to_host(A->m, rp.data(), col.data(), val.data());
-        for (int64_t i = 0; i < n; i++)
-            for (int64_t e = rp[i]; e < rp[i + 1]; e++)
-                FAMG_REQUIRE(col[e] == i || color[col[e]] != color[i], AMG_ERR_INVALID,
-                             "coloring couples two rows of the same color");
+        if (validate) {  // no two coupled rows may share a color
+            std::vector<int64_t> rp(n + 1), col(A->m.nnz);
+            std::vector<double> val(A->m.nnz);
+            csr_to_host(A->m, rp.data(), col.data(), val.data());
+            for (int64_t i = 0; i < n; i++)
+                for (int64_t e = rp[i]; e < rp[i + 1]; e++)
+                    FAMG_REQUIRE(col[e] == i || color[col[e]] != color[i], AMG_ERR_INVALID,
+                                 "coloring couples two rows of the same color");
+        }
     } else {
         op->ncolors = greedy_coloring(A->m, color);
     }
@@ -236,17 +240,8 @@ std::shared_ptr<SgsOp> make_sgs(const CsrPtr &A, const int32_t *colors) {
                            A->m.val.get(), op->perm.get(), n, op->Ap.rp64.get(), op->Ap.col.get(),
                            op->Ap.val.get(), A->diagonal(), op->dinv.get());
     FAMG_CHECK_HIP(hipGetLastError());
-    csr_finalize(op->Ap);  // rp32 (the generic schedule is replaced below)
+    csr_finalize(op->Ap, &op->color_ptr);  // one row segment per color
     FAMG_REQUIRE(op->Ap.spmv_ready(), AMG_ERR_UNSUPPORTED, "sgs: nnz must be < 2^31");
-    std::vector<int64_t> rp(n + 1);
-    FAMG_CHECK_HIP(hipMemcpyAsync(rp.data(), op->Ap.rp64.get(), (n + 1) * sizeof(int64_t), hipMemcpyDeviceToHost, s));
-    FAMG_CHECK_HIP(hipStreamSynchronize(s));
-    std::vector<int32_t> sched;
-    build_schedule(rp, op->color_ptr, sched, op->color_blk);
-    op->Ap.nblocks = (int64_t)sched.size() - 1;
-    op->Ap.sched.resize(sched.size());
-    FAMG_CHECK_HIP(hipMemcpyAsync(op->Ap.sched.get(), sched.data(), sched.size() * sizeof(int32_t), hipMemcpyHostToDevice, s));
-    FAMG_CHECK_HIP(hipStreamSynchronize(s));
     op->e_.resize(n);
     return op;
 }
@@ -265,8 +260,22 @@ void SgsOp::sweep(double *e, const double *r) {
     epi.b = r;
     epi.d = dinv.get();
     epi.perm = perm.get();
-    for (int64_t c = 1; c < ncolors; c++) spmv(Ap, e, e, SPMV_SGS, epi, s, color_blk[c], color_blk[c + 1]);
-    for (int64_t c = ncolors - 2; c >= 0; c--) spmv(Ap, e, e, SPMV_SGS, epi, s, color_blk[c], color_blk[c + 1]);
+    for (int64_t c = 1; c < ncolors; c++) spmv(Ap, e, e, SPMV_SGS, epi, s, c);
+    for (int64_t c = ncolors - 2; c >= 0; c--) spmv(Ap, e, e, SPMV_SGS, epi, s, c);
+}
+
+// One smoothing step x <- x + SGS(b - A x) done directly on x (no residual
+// vector): the same color sweeps with b in place of r.  Equal to the
+// residual form in exact arithmetic; saves one SpMV with A per step.
+void SgsOp::sweep_x(double *x, const double *b) {
+    hipStream_t s = ctx->stream;
+    if (!nrows) return;
+    SpmvEpi epi;
+    epi.b = b;
+    epi.d = dinv.get();
+    epi.perm = perm.get();
+    for (int64_t c = 0; c < ncolors; c++) spmv(Ap, x, x, SPMV_SGS, epi, s, c);
+    for (int64_t c = ncolors - 2; c >= 0; c--) spmv(Ap, x, x, SPMV_SGS, epi, s, c);
 }
 
 void SgsOp::apply(double *out, const double *rhs) {
@@ -408,12 +417,14 @@ void MultigridOp::smooth(int64_t l, double *&v, double *&t, const double *f, boo
         } else if (A && G) {
             if (zero) {
                 G->sweep(v, f);  // e = SGS(f - A 0); v = 0 + e
-            } else {
+            } else if (sgs_residual_form) {
                 SpmvEpi epi;
                 epi.b = f;
                 spmv(A->m, v, L.r.get(), SPMV_RESID, epi, s);
                 G->sweep(t, L.r.get());
                 vec_add_inplace(v, t, n, s);
+            } else {
+                G->sweep_x(v, f);  // fused: x <- x + SGS(f - A x)
             }
         } else {
             if (zero) {
@@ -640,7 +651,15 @@ std::shared_ptr<MultigridOp> sa_build_box(const CsrPtr &A, int64_t nx, int64_t n
         switch (smoother) {
         case 0: return make_jacobi(*M, omega);
         case 1: return make_l1(*M);
-        case 2: return make_sgs(M, nullptr);
+        case 2: {
+            // multicolor SGS where the greedy coloring exposes parallelism
+            // (<= SGS_MAX_COLORS colors); L1 on the dense Galerkin levels, whose
+            // colorings need hundreds of colors (one launch per color)
+            std::vector<int32_t> colors;
+            const int64_t nc = greedy_coloring(M->m, colors);
+            if (nc <= SGS_MAX_COLORS) return make_sgs(M, colors.data(), false);
+            return make_l1(*M);
+        }
         default: fail(AMG_ERR_INVALID, "unknown smoother kind");
         }
     };

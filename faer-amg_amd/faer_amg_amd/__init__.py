@@ -49,6 +49,7 @@ SIGNATURES = {
     "amg_ctx_synchronize": (i32, [vp]),
     "amg_ctx_stream": (i32, [vp, P(vp)]),
     "amg_set_spmv_format": (i32, [i32]),
+    "amg_set_alloc_policy": (i32, [i32]),
     "amg_ctx_join_stream": (i32, [vp, vp, i32]),
     "amg_csr_create": (i32, [vp, i64, i64, vp, vp, vp, P(vp)]),
     "amg_csr_create_device_i32": (i32, [vp, i64, i64, vp, vp, vp, P(vp)]),
@@ -75,6 +76,7 @@ SIGNATURES = {
     "amg_multigrid_set": (i32, [vp, i64, i64]),
     "amg_multigrid_levels": (i32, [vp, P(i64)]),
     "amg_multigrid_set_graph": (i32, [vp, i32]),
+    "amg_multigrid_set_option": (i32, [vp, i32, i64]),
     "amg_multigrid_apply": (i32, [vp, vp, i64, vp, i64, i64, C.c_int]),
     "amg_multigrid_get_level": (i32, [vp, i64, P(vp), P(vp), P(vp), P(vp)]),
     "amg_spgemm": (i32, [vp, vp, P(vp)]),
@@ -132,12 +134,17 @@ def version():
     return _lib.amg_version().decode()
 
 
-SPMV_FORMATS = {"auto": 0, "csr": 1, "sell": 2}
+SPMV_FORMATS = {"auto": 0, "csr": 1, "sell": 2, "vector": 3}
 
 
 def set_spmv_format(policy):
-    """SpMV storage for matrices built afterwards: 'auto', 'csr' or 'sell'."""
+    """SpMV storage for matrices built afterwards: 'auto', 'csr', 'sell' or 'vector'."""
     _ck(_lib.amg_set_spmv_format(SPMV_FORMATS[policy]))
+
+
+def set_alloc_policy(contiguous):
+    """Physically contiguous device allocations for large buffers (default True)."""
+    _ck(_lib.amg_set_alloc_policy(1 if contiguous else 0))
 
 
 def _dptr(x):
@@ -431,6 +438,10 @@ class Multigrid(LinOp):
 
     def set_graph(self, enable):
         _ck(_lib.amg_multigrid_set_graph(self.h, 1 if enable else 0))
+
+    def set_sgs_residual_form(self, enable):
+        """Literal smooth() order for SGS (residual SpMV + SGS(r)) instead of the fused sweep."""
+        _ck(_lib.amg_multigrid_set_option(self.h, 1, 1 if enable else 0))
 
     def levels(self):
         v = i64()

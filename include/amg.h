@@ -77,10 +77,15 @@ amg_status amg_ctx_stream(amg_ctx *ctx, void **hip_stream);
  * the context stream.  Event-based, no host synchronisation. */
 amg_status amg_ctx_join_stream(amg_ctx *ctx, void *other, int32_t ctx_waits);
 /* SpMV storage policy for matrices built after the call (process-wide):
- * 0 auto (SELL-64 for short regular rows, CSR-stream otherwise), 1 CSR-stream
- * only, 2 SELL-64 whenever rows are <= 256 long.  Results are identical up to
- * the summation order of rows longer than 128 entries. */
+ * 0 auto (SELL-64 for short regular rows, wave-per-row for rows averaging >= 48
+ * entries, CSR-stream otherwise), 1 CSR-stream only, 2 SELL-64 whenever rows are
+ * <= 256 long, 3 wave-per-row for every matrix.  Results agree to the summation
+ * order of the rows (bitwise for rows summed by one lane). */
 amg_status amg_set_spmv_format(int32_t policy);
+/* Device allocation policy for buffers allocated after the call: 1 (default)
+ * requests physically contiguous memory for buffers >= 16 MiB (falls back to
+ * hipMalloc), 0 always uses hipMalloc. */
+amg_status amg_set_alloc_policy(int32_t policy);
 
 /* ---- sparse matrices (replaces SparseMatOp::new core.rs:56-74, ParSpmmOp::new
  *      par_spmm.rs:31-96, and the SparseRowMat<usize,f64> LinOp used at
@@ -166,6 +171,10 @@ amg_status amg_multigrid_set(amg_linop *mg, int64_t mu, int64_t steps);
 amg_status amg_multigrid_levels(const amg_linop *mg, int64_t *levels);
 /* Enable/disable hipGraph capture of whole V-cycles (default on). */
 amg_status amg_multigrid_set_graph(amg_linop *mg, int32_t enable);
+/* Options: 0 = hipGraph capture (as above); 1 = SGS smoothing in the literal
+ * residual form of smooth() (multigrid.rs:418-423: r = f - A x; x += SGS(r))
+ * instead of the fused in-place sweep on x (default 0: fused, one SpMV fewer). */
+amg_status amg_multigrid_set_option(amg_linop *mg, int32_t option, int64_t value);
 /* Multigrid::apply == amg_linop_apply on a multigrid handle. */
 amg_status amg_multigrid_apply(amg_linop *mg, double *out, int64_t ld_out, const double *rhs,
                                int64_t ld_rhs, int64_t k, amg_mem mem);

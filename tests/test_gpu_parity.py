@@ -99,7 +99,7 @@ def test_spmv_irregular_golden(ctx):
     assert np.all(y[np.diff(g["rowptr"]) == 0] == 0)
 
 
-@pytest.mark.parametrize("fmt", ["csr", "sell"])
+@pytest.mark.parametrize("fmt", ["csr", "sell", "vector"])
 def test_spmv_formats(ctx, fmt):
     """Both storage paths (CSR-stream and SELL-64) on short, long, empty and
     rectangular rows.  SELL sums every row sequentially in one lane (bitwise
@@ -109,14 +109,18 @@ def test_spmv_formats(ctx, fmt):
     try:
         OA = O.laplace3d_7pt(33, 17, 9)
         x = np.random.default_rng(10).standard_normal(OA.ncols)
-        assert np.array_equal(apply_dev(ctx, gpu_csr(ctx, OA), x, OA.nrows), OA.spmv(x))
+        y = apply_dev(ctx, gpu_csr(ctx, OA), x, OA.nrows)
+        if fmt == "vector":
+            assert np.all(np.abs(y - OA.spmv(x)) <= spmv_bound(OA.to_scipy(), x))
+        else:
+            assert np.array_equal(y, OA.spmv(x))
         g = load("g3_sa7pt16.npz")
         for key in ("P0", "R0", "A1"):
             m, n = g[f"{key}_shape"]
             OM = O.Csr.from_arrays(m, n, g[f"{key}_rowptr"], g[f"{key}_col"], g[f"{key}_val"])
             xx = np.random.default_rng(11).standard_normal(n)
             y = apply_dev(ctx, gpu_csr(ctx, OM), xx, m)
-            if fmt == "sell" or key == "P0":
+            if fmt == "sell" or (key == "P0" and fmt == "csr"):
                 assert np.array_equal(y, OM.spmv(xx)), key
             else:
                 assert np.all(np.abs(y - OM.spmv(xx)) <= spmv_bound(OM.to_scipy(), xx)), key
@@ -298,13 +302,21 @@ def test_sa_hierarchy_matches_oracle(ctx):
 # --------------------------------------------------------------- V-cycle
 
 def oracle_levels_from_gpu(mg, smoother):
+    """The GPU hierarchy's arrays as oracle levels, with the smoother each level
+    actually got (sa_build_box(smoother='sgs') puts L1 on levels whose greedy
+    coloring needs more than 32 colors)."""
     levels = []
     nl = mg.levels()
     for l in range(nl):
         Al, Sl, Rl, Pl = mg.level(l)
         m, n = Al.dims()
-        d = {"A": O.Csr.from_arrays(m, n, *Al.arrays()),
-             "smoother": "chol" if l == nl - 1 else smoother}
+        if l == nl - 1:
+            sm = "chol"
+        elif smoother == "sgs":
+            sm = "sgs" if Sl.kind == "sgs" else "l1"
+        else:
+            sm = smoother
+        d = {"A": O.Csr.from_arrays(m, n, *Al.arrays()), "smoother": sm}
         if Rl is not None:
             d["R"] = O.Csr.from_arrays(*Rl.dims(), *Rl.arrays())
             d["P"] = O.Csr.from_arrays(*Pl.dims(), *Pl.arrays())
@@ -324,6 +336,8 @@ def test_vcycle_parity(ctx, gen, dims, smoother):
         A = fa().SparseMatOp.aniso27(ctx, *dims, 1.0, 1.0, 0.01)
     mg = fa().sa_build_box(A, dims, (2, 2, 2), coarsest_dim=200, smoother=smoother)
     levels = oracle_levels_from_gpu(mg, smoother)
+    if smoother == "sgs":
+        assert levels[0]["smoother"] == "sgs"  # 8-color fine level
     import sys
     sys.path.insert(0, GOLD)
     from make_golden import splitmix_uniform
@@ -333,10 +347,14 @@ def test_vcycle_parity(ctx, gen, dims, smoother):
         zref = O.Multigrid(levels, mu=mu, steps=steps).apply(b)
         for graph in (True, False):
             mg.set_graph(graph)
-            z = apply_dev(ctx, mg, b, A.nrows)
-            assert np.linalg.norm(z - zref) <= 1e-11 * np.linalg.norm(zref), (mu, steps, graph)
+            for resid_form in ((False, True) if smoother == "sgs" else (False,)):
+                mg.set_sgs_residual_form(resid_form)
+                z = apply_dev(ctx, mg, b, A.nrows)
+                assert np.linalg.norm(z - zref) <= 1e-11 * np.linalg.norm(zref), \
+                    (mu, steps, graph, resid_form)
     mg.with_cycle_type(1).with_smoothing_steps(1)
     mg.set_graph(True)
+    mg.set_sgs_residual_form(False)
 
 
 def test_vcycle_golden_fixtures(ctx):
