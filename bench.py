@@ -291,7 +291,7 @@ def run_dist(args, world, rank, local_rank):
     obj = [fa.unique_id() if rank == 0 else None]
     dist.broadcast_object_list(obj, src=0)
     comm = fa.Comm(ctx, nranks=world, rank=rank, uid=obj[0])
-    dm = fa.DistMultigrid(comm, mg, splits, agglomerate_rows=args.agglomerate)
+    dm = fa.DistMultigrid(comm, mg, splits, agglomerate_rows=args.agglomerate).set_overlap(not args.no_overlap)
     infos = [dm.level_info(l) for l in range(nl)]
     del mg, A  # global fine levels are no longer needed on this rank
     torch.cuda.synchronize()
@@ -359,6 +359,7 @@ def run_dist(args, world, rank, local_rank):
                    "fine_spmv_with_halo_ms": round(halo_ms, 4),
                    "rel_residual_after_1_cycle": float(hist[1]) if len(hist) > 1 else None,
                    "agglomerate_rows": args.agglomerate,
+                   "halo_overlap": not args.no_overlap,
                    "parallelism": f"row-block z-slabs x{world}, RCCL halo exchange"},
         "fine_spmv_gbs": round(float(ga[0]), 1),
         "roofline": {"bound": "hbm", "achieved": round(float(ga[0]), 1), "peak": HBM_PEAK_GBS,
@@ -385,6 +386,8 @@ def main():
     ap.add_argument("--cpu-threads", type=int, default=int(os.environ.get("OMP_NUM_THREADS", "16")))
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--no-overlap", action="store_true",
+                    help="distributed: exchange halos before the SpMV instead of under its interior rows")
     ap.add_argument("--ab", action="store_true", help="A/B the SpMV storage formats (stderr)")
     args = ap.parse_args()
 

@@ -46,14 +46,21 @@ struct AmgError : std::runtime_error {
 // SpMV ran 15-20 % slower from some fragmented plain allocations.  0 = hipMalloc.
 extern int g_alloc_policy;
 
+extern bool g_alloc_debug;  // FAMG_ALLOC_DEBUG=1: log large allocations to stderr
+
 inline void *dev_alloc(size_t bytes) {
     void *p = nullptr;
-    if (g_alloc_policy == 1 && bytes >= (size_t(16) << 20)) {
-        if (hipExtMallocWithFlags(&p, bytes, hipDeviceMallocContiguous) == hipSuccess && p) return p;
+    const bool large = bytes >= (size_t(16) << 20);
+    if (g_alloc_policy == 1 && large) {
+        if (hipExtMallocWithFlags(&p, bytes, hipDeviceMallocContiguous) == hipSuccess && p) {
+            if (g_alloc_debug) fprintf(stderr, "famg alloc contiguous %p %zu\n", p, bytes);
+            return p;
+        }
         (void)hipGetLastError();
         p = nullptr;
     }
     FAMG_CHECK_HIP(hipMalloc(&p, bytes));
+    if (g_alloc_debug && large) fprintf(stderr, "famg alloc plain %p %zu\n", p, bytes);
     return p;
 }
 

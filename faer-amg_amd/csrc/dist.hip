@@ -319,26 +319,71 @@ static void space_plan(Space &sp, Transport &tr, Ctx *ctx) {
     FAMG_CHECK_HIP(hipStreamSynchronize(s));
 }
 
+// flag[i] = 1 when row i references a ghost column (local column >= n_own)
+__global__ void k_row_ghost(const int64_t *rp, const int32_t *col, int64_t n, int64_t n_own, uint8_t *flag) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    uint8_t g = 0;
+    for (int64_t e = rp[i]; e < rp[i + 1]; e++)
+        if (col[e] >= n_own) { g = 1; break; }
+    flag[i] = g;
+}
+
+// Remap a local matrix to the [owned | ghost] numbering and cut its rows into
+// three segments [0, lo) [lo, hi) [hi, n): [lo, hi) is the longest run of rows
+// that read owned entries only (the interior of a slab), which can run while
+// the halo is in flight.
 static void space_remap(const Space &sp, GpuCsr &local, Ctx *ctx) {
+    hipStream_t s = ctx->stream;
     if (local.nnz)
-        hipLaunchKernelGGL(k_remap_cols, dim3(g1(local.nnz)), dim3(256), 0, ctx->stream, local.col.get(),
+        hipLaunchKernelGGL(k_remap_cols, dim3(g1(local.nnz)), dim3(256), 0, s, local.col.get(),
                            local.nnz, sp.r0, sp.r1, sp.n_own, sp.scan.get());
     FAMG_CHECK_HIP(hipGetLastError());
     local.ncols = sp.n_own + sp.n_ghost;
-    csr_finalize(local);
+    const int64_t n = local.nrows;
+    if (sp.n_ghost == 0 || n == 0) {
+        csr_finalize(local);
+        return;
+    }
+    DevBuf<uint8_t> dflag(n);
+    hipLaunchKernelGGL(k_row_ghost, dim3(g1(n)), dim3(256), 0, s, local.rp64.get(), local.col.get(), n,
+                       sp.n_own, dflag.get());
+    std::vector<uint8_t> flag(n);
+    FAMG_CHECK_HIP(hipMemcpyAsync(flag.data(), dflag.get(), n, hipMemcpyDeviceToHost, s));
+    FAMG_CHECK_HIP(hipStreamSynchronize(s));
+    int64_t lo = 0, hi = 0;
+    for (int64_t i = 0; i < n;) {
+        if (flag[i]) { i++; continue; }
+        int64_t j = i;
+        while (j < n && !flag[j]) j++;
+        if (j - i > hi - lo) { lo = i; hi = j; }
+        i = j;
+    }
+    if (hi == lo) lo = hi = n;
+    const std::vector<int64_t> segs{0, lo, hi, n};
+    csr_finalize(local, &segs);
 }
 
-// refresh the ghost region of x (x has n_own + n_ghost entries)
-static void halo(Space &sp, double *x, Transport &tr, hipStream_t s) {
-    if (sp.redundant || sp.nbr.empty()) return;
+static void halo_pack(Space &sp, const double *x, hipStream_t s) {
     if (sp.nsend)
         hipLaunchKernelGGL(k_gather_idx, dim3(g1(sp.nsend)), dim3(256), 0, s, x, sp.send_idx.get(), sp.nsend,
                            sp.sendbuf.get());
+    FAMG_CHECK_HIP(hipGetLastError());
+}
+
+static void halo_exchange(Space &sp, double *x, Transport &tr, hipStream_t s) {
     sp.peers.clear();
     for (size_t k = 0; k < sp.nbr.size(); k++)
         sp.peers.push_back({sp.nbr[k], sp.sendbuf.get() + sp.soff[k], sp.scnt[k] * 8,
                             x + sp.n_own + sp.roff[k], sp.rcnt[k] * 8});
     tr.exchange(sp.peers, s);
+}
+
+// refresh the ghost region of x (x has n_own + n_ghost entries)
+static void halo(Space &sp, double *x, Transport &tr, hipStream_t s) {
+    if (sp.redundant || sp.nbr.empty()) return;
+    halo_pack(sp, x, s);
+    halo_exchange(sp, x, tr, s);
 }
 
 // ---------------------------------------------------------- multigrid
@@ -361,8 +406,39 @@ struct DistMultigridOp : LinOp {
     int64_t tail_max = 0;
     DevBuf<double> fc_own, gather, fc_full, vc_full;
     std::mutex mtx;
+    // halo/interior overlap: the exchange runs on comm_stream while the
+    // interior rows run on the context stream
+    bool overlap = true;
+    hipStream_t comm_stream = nullptr;
+    hipEvent_t ev_pack = nullptr, ev_halo = nullptr;
     Kind kind() const override { return Kind::DistMultigrid; }
     bool is_precond() const override { return true; }
+    ~DistMultigridOp() override {
+        if (ev_pack) (void)hipEventDestroy(ev_pack);
+        if (ev_halo) (void)hipEventDestroy(ev_halo);
+        if (comm_stream) (void)hipStreamDestroy(comm_stream);
+    }
+
+    // y = m x (with epilogue) after refreshing x's ghosts.  For a matrix cut
+    // into [boundary | interior | boundary] the interior rows run while the
+    // exchange is in flight on comm_stream.
+    void halo_spmv(Space &sp, double *x, const GpuCsr &m, double *y, SpmvMode mode, const SpmvEpi &epi) {
+        hipStream_t s = ctx->stream;
+        if (!overlap || sp.redundant || sp.nbr.empty() || m.seg_rows.size() != 4) {
+            halo(sp, x, *tr, s);
+            spmv(m, x, y, mode, epi, s);
+            return;
+        }
+        halo_pack(sp, x, s);
+        FAMG_CHECK_HIP(hipEventRecord(ev_pack, s));
+        FAMG_CHECK_HIP(hipStreamWaitEvent(comm_stream, ev_pack, 0));
+        halo_exchange(sp, x, *tr, comm_stream);
+        FAMG_CHECK_HIP(hipEventRecord(ev_halo, comm_stream));
+        spmv(m, x, y, mode, epi, s, 1);
+        FAMG_CHECK_HIP(hipStreamWaitEvent(s, ev_halo, 0));
+        spmv(m, x, y, mode, epi, s, 0);
+        spmv(m, x, y, mode, epi, s, 2);
+    }
 
     void smooth(int64_t l, double *&v, double *&t, const double *f, bool zero) {
         DLevel &D = L[l];
@@ -371,11 +447,10 @@ struct DistMultigridOp : LinOp {
             if (zero && it == 0) {
                 vec_mul(t, D.S->d.get(), f, D.sp.n_own, s);
             } else {
-                halo(D.sp, v, *tr, s);
                 SpmvEpi epi;
                 epi.b = f;
                 epi.d = D.S->d.get();
-                spmv(D.A->m, v, t, SPMV_JACOBI, epi, s);
+                halo_spmv(D.sp, v, D.A->m, t, SPMV_JACOBI, epi);
             }
             std::swap(v, t);
         }
@@ -400,20 +475,18 @@ struct DistMultigridOp : LinOp {
         double *v0 = v;
         double *t = (v == D.t.get()) ? D.v.get() : D.t.get();
         smooth(l, v, t, f, zero);
-        halo(D.sp, v, *tr, s);
         SpmvEpi epi;
         epi.b = f;
-        spmv(D.A->m, v, D.r.get(), SPMV_RESID, epi, s);
-        halo(D.sp, D.r.get(), *tr, s);
+        halo_spmv(D.sp, v, D.A->m, D.r.get(), SPMV_RESID, epi);
         if (l + 1 < La) {
             DLevel &C = L[l + 1];
-            spmv(D.R->m, D.r.get(), C.f.get(), SPMV_SET, SpmvEpi{}, s);
+            halo_spmv(D.sp, D.r.get(), D.R->m, C.f.get(), SPMV_SET, SpmvEpi{});
             for (int64_t k = 0; k < mu; k++) cycle(l + 1, C.v.get(), C.f.get(), k == 0);
-            halo(C.sp, C.v.get(), *tr, s);
-            spmv(D.P->m, C.v.get(), v, SPMV_ADD, SpmvEpi{}, s);
+            halo_spmv(C.sp, C.v.get(), D.P->m, v, SPMV_ADD, SpmvEpi{});
         } else {
             const int64_t cnt = tail_splits[tr->rank + 1] - tail_splits[tr->rank];
-            if (cnt) spmv(D.R->m, D.r.get(), gather.get() + tr->rank * tail_max, SPMV_SET, SpmvEpi{}, s);
+            if (cnt) halo_spmv(D.sp, D.r.get(), D.R->m, gather.get() + tr->rank * tail_max, SPMV_SET, SpmvEpi{});
+            else halo(D.sp, D.r.get(), *tr, s);
             gather_tail(gather.get() + tr->rank * tail_max);
             for (int64_t k = 0; k < mu; k++) tail->cycle(0, vc_full.get(), fc_full.get(), k == 0, nullptr);
             spmv(D.P->m, vc_full.get(), v, SPMV_ADD, SpmvEpi{}, s);
@@ -432,8 +505,7 @@ struct DistMultigridOp : LinOp {
             DLevel &D = L[0];
             if (xg_.size() < (size_t)(D.sp.n_own + D.sp.n_ghost + 1)) xg_.resize(D.sp.n_own + D.sp.n_ghost + 1);
             vec_copy(xg_.get(), x, D.sp.n_own, s);
-            halo(D.sp, xg_.get(), *tr, s);
-            spmv(D.A->m, xg_.get(), r, SPMV_RESID, epi, s);
+            halo_spmv(D.sp, xg_.get(), D.A->m, r, SPMV_RESID, epi);
             return;
         }
         // everything replicated: gather x, global SpMV, keep the owned rows
@@ -472,8 +544,7 @@ struct DistLevelOp : LinOp {
         DLevel &D = mg->L[level];
         hipStream_t s = ctx->stream;
         vec_copy(x.get(), rhs, D.sp.n_own, s);
-        halo(D.sp, x.get(), *mg->tr, s);
-        spmv(D.A->m, x.get(), out, SPMV_SET, SpmvEpi{}, s);
+        mg->halo_spmv(D.sp, x.get(), D.A->m, out, SPMV_SET, SpmvEpi{});
     }
 };
 
@@ -485,6 +556,9 @@ static std::shared_ptr<DistMultigridOp> build_dist(amg_comm *comm, const Multigr
     auto d = std::make_shared<DistMultigridOp>();
     d->ctx = ctx;
     d->tr = comm->tr;
+    FAMG_CHECK_HIP(hipStreamCreateWithFlags(&d->comm_stream, hipStreamNonBlocking));
+    FAMG_CHECK_HIP(hipEventCreateWithFlags(&d->ev_pack, hipEventDisableTiming));
+    FAMG_CHECK_HIP(hipEventCreateWithFlags(&d->ev_halo, hipEventDisableTiming));
     d->mu = g.mu;
     d->steps = g.steps;
     d->nlevels = (int64_t)g.levels.size();
@@ -775,6 +849,17 @@ amg_status amg_dist_level_matrix(const amg_linop *dist, int64_t level, int32_t w
                      "level must be distributed, which in {0,1,2}");
         const DLevel &D = d->L[level];
         *out = new amg_linop{which == 0 ? D.A : which == 1 ? D.R : D.P};
+    });
+}
+
+amg_status amg_dist_set_option(amg_linop *dist, int32_t option, int64_t value) {
+    return dguard([&] {
+        auto d = need_dist(dist);
+        std::lock_guard<std::mutex> lk(d->mtx);
+        switch (option) {
+        case 0: d->overlap = value != 0; break;
+        default: fail(AMG_ERR_INVALID, "unknown distributed multigrid option");
+        }
     });
 }
 

@@ -11,8 +11,8 @@
 //    row pointers; all loads of an <=8-entry chunk are issued before the
 //    dependent x gathers.  Rows are summed sequentially (bit-identical to the
 //    oracle).
-//  * vector (long rows, >= 48 entries on average: Galerkin operators of the
-//    coarse levels): one wavefront per row, lanes stride the row four 64-entry
+//  * vector (very long rows, >= 256 entries on average: the densest Galerkin
+//    operators near the coarsest level): one wavefront per row, lanes stride the row four 64-entry
 //    steps at a time, shuffle-tree reduction.
 //  * CSR-stream (everything else): blocks of <= 256 rows / <= 2048 entries
 //    staged HBM -> LDS with 16-B non-temporal loads, L lanes per row.
@@ -22,6 +22,7 @@
 // A matrix may be cut into row segments (SGS colors, halo boundary/interior);
 // every kernel can run one segment.
 #include <algorithm>
+#include <cstdlib>
 
 #include "famg.hpp"
 
@@ -32,6 +33,10 @@ typedef int32_t i32x4_t __attribute__((ext_vector_type(4)));
 
 int g_spmv_format_policy = 0;
 int g_alloc_policy = 1;
+bool g_alloc_debug = [] {
+    const char *e = getenv("FAMG_ALLOC_DEBUG");
+    return e && e[0] == '1';
+}();
 
 constexpr int SPMV_BS = 256;
 constexpr int SPMV_CAP = 2048;
@@ -147,8 +152,7 @@ __global__ __launch_bounds__(SPMV_BS) void spmv_stream_kernel(StreamArgs a) {
 
 // Interleaved slice storage: entry step k of a slice is one 768-B record
 // [64 fp64 values | 64 int32 columns], so a wavefront streams a single
-// contiguous region (separate value/index arrays showed placement-dependent
-// HBM channel conflicts: the same matrix ran 255 or 303 us by address).
+// contiguous region and a matrix needs one allocation.
 constexpr int SELL_STEP_BYTES = SELL_C * 12;
 constexpr int SELL_V_STRIDE = SELL_STEP_BYTES / 8;   // doubles per step
 constexpr int SELL_C_STRIDE = SELL_STEP_BYTES / 4;   // int32 per step

@@ -104,6 +104,7 @@ SIGNATURES = {
     "amg_dist_level_info": (i32, [vp, i64, vp]),
     "amg_dist_level_operator": (i32, [vp, i64, P(vp)]),
     "amg_dist_level_matrix": (i32, [vp, i64, i32, P(vp)]),
+    "amg_dist_set_option": (i32, [vp, i32, i64]),
     "amg_dist_stationary_solve": (i32, [vp, vp, vp, i64, dbl, vp, P(i64)]),
 }
 
@@ -625,6 +626,11 @@ class DistMultigrid(LinOp):
         h = vp()
         _ck(_lib.amg_dist_level_matrix(self.h, l, {"A": 0, "R": 1, "P": 2}[which], C.byref(h)))
         return SparseMatOp(h, self.ctx, refs=(self,))
+
+    def set_overlap(self, on=True):
+        """Overlap halo exchanges with the interior rows of their SpMV (default on)."""
+        _ck(_lib.amg_dist_set_option(self.h, 0, 1 if on else 0))
+        return self
 
     def stationary_solve(self, b, x, max_iter=100, rel_tol=1e-8):
         hist = np.zeros(max_iter)

@@ -281,7 +281,10 @@ amg_status amg_dist_level_operator(const amg_linop *dist, int64_t level, amg_lin
  * owned rows, columns in the level's [owned | ghost] numbering. */
 amg_status amg_dist_level_matrix(const amg_linop *dist, int64_t level, int32_t which,
                                  amg_linop **out);
-/* Distributed stationary solve / PCG (dots all-reduced over ranks): local vectors. */
+/* Options of a distributed multigrid: 0 = overlap each halo exchange with the
+ * interior rows of the SpMV that consumes it (default 1; 0 exchanges first). */
+amg_status amg_dist_set_option(amg_linop *dist, int32_t option, int64_t value);
+/* Distributed stationary solve (dots all-reduced over ranks): local vectors. */
 amg_status amg_dist_stationary_solve(amg_linop *dist_mg, const double *b, double *x,
                                      int64_t max_iter, double rel_tol, double *hist,
                                      int64_t *iters);

@@ -22,7 +22,8 @@ for s in "$@"; do
         dist2) step dist2 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
                   --master-addr 127.0.0.1 --master-port 29511 bench.py --gpus 2 --edge 64 --steps 5 --warmup 1 ;;
         ablevels) step ablevels 400 python scripts/ab_levels.py ;;
-        placement) step placement 300 python scripts/placement.py ;;
+        pstream) step pstream 300 python scripts/placement_stream.py ;;
+        placement) FAMG_ALLOC_DEBUG=1 step placement 300 python scripts/placement.py ;;
         bench27) step bench27 600 python bench.py --problem 27pt --smoother sgs --steps 10 --warmup 2 --no-cpu-baseline ;;
         pmc) export TMPDIR=/tmp; R=$(pwd)
               step pmc_fetch 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d "$R/gpurun_out/pmc_fetch" -o run \
