@@ -65,8 +65,16 @@ def measured_traffic(edge, problem):
 
 
 def spmv_bytes(nrows, ncols, nnz):
-    """Algorithmic bytes of y = A x with 32-bit indices."""
+    """Algorithmic bytes of y = A x in CSR with 32-bit indices."""
     return 12 * nnz + 4 * (nrows + 1) + 8 * ncols + 8 * nrows
+
+
+def spmv_bytes_fmt(M):
+    """Algorithmic bytes of y = M x in the storage the library chose for M: the
+    matrix bytes that format streams (SELL-64 values + compressed column indices
+    + slice metadata, or CSR) + x read once + y written."""
+    m, n = M.dims()
+    return M.spmv_info()["stream_bytes"] + 8 * n + 8 * m
 
 
 def time_kernel(fn, iters, stream):
@@ -132,23 +140,26 @@ def build_problem(fa, ctx, args, dims):
     return A, mg
 
 
-def vcycle_bytes(mg):
+def vcycle_bytes(mg, csr=False):
     """Algorithmic bytes of one V-cycle (s = 1, mu = 1, zero initial guess) from the
-    per-kernel formulas of SURVEY.md 8(d)."""
+    per-kernel formulas of SURVEY.md 8(d); matrix bytes of the chosen storage
+    (csr=False) or of 32-bit CSR (csr=True)."""
+    def mat(M):
+        return 12 * M.nnz + 4 * (M.nrows + 1) if csr else M.spmv_info()["stream_bytes"]
     tot = 0
     nl = mg.levels()
     for l in range(nl):
         A, _, R, P = mg.level(l)
-        n, nnz = A.nrows, A.nnz
-        bA = 12 * nnz + 4 * (n + 1)
+        n = A.nrows
         if l == nl - 1:
             tot += 8 * n * n + 16 * n
             continue
+        bA = mat(A)
         nc = R.nrows
         tot += 24 * n                                  # first smoothing step from 0
         tot += bA + 24 * n                             # residual
-        tot += 12 * R.nnz + 4 * (nc + 1) + 8 * n + 8 * nc   # restrict
-        tot += 12 * P.nnz + 4 * (n + 1) + 8 * nc + 16 * n   # interpolate + add
+        tot += mat(R) + 8 * n + 8 * nc                 # restrict
+        tot += mat(P) + 8 * nc + 16 * n                # interpolate + add
         tot += bA + 32 * n                             # post-smoothing Jacobi
     return tot
 
@@ -197,7 +208,9 @@ def run_single(args):
         A.apply(y, x)
     spmv_ms = time_kernel(lambda: A.apply(y, x), 20, stream)
     nnz = A.nnz
-    bytes_spmv = spmv_bytes(n, n, nnz)
+    info = A.spmv_info()
+    bytes_spmv = spmv_bytes_fmt(A)
+    bytes_csr = spmv_bytes(n, n, nnz)
     achieved = bytes_spmv / (spmv_ms * 1e-3) / 1e9
 
     if args.ab:
@@ -213,7 +226,7 @@ def run_single(args):
                 res[fmt].append(time_kernel(lambda: op.apply(y, x), 20, stream))
         for fmt, v in res.items():
             log(f"A/B fine SpMV {fmt}: median {np.median(v)*1e3:.1f} us  min {min(v)*1e3:.1f} us  "
-                f"-> {bytes_spmv / (min(v) * 1e-3) / 1e9:.0f} GB/s")
+                f"-> {spmv_bytes_fmt(ops[fmt]) / (min(v) * 1e-3) / 1e9:.0f} GB/s")
         del ops
 
     r = torch.empty_like(b)
@@ -221,6 +234,7 @@ def run_single(args):
     torch.cuda.synchronize()
     rho1 = float(torch.linalg.norm(b - r) / torch.linalg.norm(b))
     vbytes = vcycle_bytes(mg)
+    vbytes_csr = vcycle_bytes(mg, csr=True)
 
     cpu = None
     if not args.no_cpu_baseline:
@@ -256,14 +270,18 @@ def run_single(args):
                    "wall_ms_per_step": round(1000 * t_wall / args.steps, 4),
                    "vcycle_algorithmic_GB": round(vbytes / 1e9, 3),
                    "vcycle_GBs": round(vbytes / (ms_per_cycle * 1e-3) / 1e9, 1),
+                   "vcycle_csr_equivalent_GB": round(vbytes_csr / 1e9, 3),
                    "rel_residual_after_1_cycle": rho1,
                    "parallelism": "single GPU"},
         "fine_spmv_gbs": round(achieved, 1),
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                      "traffic_source": traffic_src,
-                     "kernel": "spmv_sell_kernel<SET> on A_0 (SELL-64)",
-                     "bytes_per_launch": bytes_spmv, "ms_per_launch": round(spmv_ms, 5)},
+                     "kernel": f"spmv_{'sell' if info['kernel'] == 'sell' else info['kernel']}_kernel<SET> on A_0",
+                     "storage": info,
+                     "bytes_per_launch": bytes_spmv, "ms_per_launch": round(spmv_ms, 5),
+                     "csr_bytes_per_launch": bytes_csr,
+                     "csr_equivalent_GBs": round(bytes_csr / (spmv_ms * 1e-3) / 1e9, 1)},
         "cpu_baseline": cpu,
     }
 
@@ -323,7 +341,7 @@ def run_dist(args, world, rank, local_rank):
     for _ in range(3):
         Al.apply(yl, xl)
     spmv_ms = time_kernel(lambda: Al.apply(yl, xl), 20, stream)
-    bytes_spmv = spmv_bytes(nloc, nloc, Al.nnz)
+    bytes_spmv = Al.spmv_info()["stream_bytes"] + 8 * nloc + 8 * nloc
     achieved = bytes_spmv / (spmv_ms * 1e-3) / 1e9
     # distributed fine SpMV including the halo exchange
     Ad = dm.level_operator(0)

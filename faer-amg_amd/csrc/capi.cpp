@@ -213,6 +213,21 @@ amg_status amg_csr_nnz(const amg_linop *op, int64_t *nnz) {
     });
 }
 
+amg_status amg_csr_spmv_info(const amg_linop *op, int64_t *info8) {
+    return guard([&] {
+        FAMG_REQUIRE(info8, AMG_ERR_INVALID, "null argument");
+        const GpuCsr &m = need_csr(op)->m;
+        info8[0] = m.kernel;
+        info8[1] = m.stream_bytes();
+        info8[2] = m.index_bytes();
+        info8[3] = m.nslices;
+        info8[4] = m.sell_steps * 64;
+        info8[5] = m.sell_mode_slices[0];
+        info8[6] = m.sell_mode_slices[1];
+        info8[7] = m.sell_mode_slices[2];
+    });
+}
+
 amg_status amg_csr_download(const amg_linop *op, int64_t *rowptr, int64_t *colidx, double *vals) {
     return guard([&] {
         auto p = need_csr(op);

@@ -38,18 +38,25 @@ struct GpuCsr {
     // Row segments (SGS colors, halo boundary/interior): [seg_rows[g], seg_rows[g+1]).
     // Schedule blocks and SELL slices never straddle a segment.
     std::vector<int64_t> seg_rows, seg_blk, seg_slc;
-    // SELL-64 copy: slice s holds rows [sell_row0[s], sell_row0[s+1]) (<= 64),
-    // width w_s = its longest row; entry step k of the slice is a 768-B record
-    // [64 fp64 values | 64 int32 columns] at byte 12*sell_off[s] + 768 k (lane l
-    // = row sell_row0[s] + l); padding = 0.0 * x[c_last].
-    DevBuf<int32_t> sell_off;
+    // SELL-64 copy with compressed column indices (spmv.hip, "SELL storage"):
+    // slice s holds rows [sell_row0[s], sell_row0[s+1]) (<= 64), one lane per
+    // row, sell_soff[s+1]-sell_soff[s] entry steps; sell_desc[s] = byte offset/128
+    // of its block in sell_data | column mode << 30; sell_base = one int32 per step.
     DevBuf<int32_t> sell_row0;
+    DevBuf<int32_t> sell_soff;
+    DevBuf<uint32_t> sell_desc;
+    DevBuf<int32_t> sell_base;
     DevBuf<char> sell_data;
-    int64_t nslices = 0, sell_padded = 0;
+    int64_t nslices = 0, sell_steps = 0, sell_bytes = 0;
+    int64_t sell_mode_slices[3] = {0, 0, 0};  // slices per column mode (implicit, u16, i32)
     int kernel = 0;  // SpmvKernel chosen at finalize
     bool spmv_ready() const { return rp32.get() != nullptr && sched.get() != nullptr; }
-    bool has_sell() const { return sell_off.get() != nullptr; }
+    bool has_sell() const { return sell_desc.get() != nullptr; }
     int64_t index_bytes() const { return 12 * nnz + 4 * (nrows + 1); }
+    // matrix bytes one SpMV streams with the chosen kernel (data + metadata)
+    int64_t stream_bytes() const {
+        return kernel == 1 ? sell_bytes + 12 * (nslices + 1) + 4 * sell_steps : index_bytes();
+    }
 };
 
 // Allocate a CSR with the given shape/nnz (arrays uninitialised).

@@ -149,31 +149,45 @@ __global__ __launch_bounds__(SPMV_BS) void spmv_stream_kernel(StreamArgs a) {
 }
 
 // ------------------------------------------------------------------- SELL-64
-
-// Interleaved slice storage: entry step k of a slice is one 768-B record
-// [64 fp64 values | 64 int32 columns], so a wavefront streams a single
-// contiguous region and a matrix needs one allocation.
-constexpr int SELL_STEP_BYTES = SELL_C * 12;
-constexpr int SELL_V_STRIDE = SELL_STEP_BYTES / 8;   // doubles per step
-constexpr int SELL_C_STRIDE = SELL_STEP_BYTES / 4;   // int32 per step
+//
+// Slice s = up to 64 consecutive rows, one lane per row, w_s entry steps.  The
+// slice's block in sell_data is [w_s x 64 fp64 values | column block], the
+// column of lane l at step t given by the slice's column mode:
+//   0 implicit  col = base[t] + l                    (0 B/entry)
+//   1 u16       col = base[t] + d16[t][l]            (2 B/entry)
+//   2 i32       col = c32[t][l]                      (4 B/entry)
+// Steps are either the k-th stored entry of every row ("plain") or, when it is
+// cheaper, the sorted union of the slice's column offsets col - row
+// ("aligned"; a stencil row then reads x[row + offset] for offset t: mode 0
+// and coalesced x loads).  A row without an entry at a step holds 0.0 at an
+// in-range column, so every row is still summed in its stored (ascending
+// column) order with fma, interleaved with exact +0 terms: bit-identical to the
+// CSR kernels for finite x.
+constexpr int SELL_VAL_STEP = SELL_C * 8;  // bytes of values per step
 
 struct SellArgs {
-    const int32_t *off;   // entry offset of each slice (nslices+1)
-    const int32_t *row0;  // first row of each slice (nslices+1; slices tile the rows)
-    const char *data;     // interleaved records, slice s at byte 12 * off[s]
+    const int32_t *row0;   // nslices+1 (slices tile the rows)
+    const int32_t *soff;   // nslices+1 step offsets
+    const uint32_t *desc;  // block offset / 128 | mode << 30
+    const int32_t *base;   // one per step
+    const char *data;
     int32_t slice0, nslices;
     Epi e;
 };
 
-template <int U>
-__device__ __forceinline__ void sell_chunk(const double *__restrict__ v, const int32_t *__restrict__ c,
+template <int CM, int U>
+__device__ __forceinline__ void sell_chunk(const double *__restrict__ v, const void *__restrict__ ix,
+                                           const int32_t *__restrict__ bs, int lane,
                                            const double *__restrict__ x, double &acc) {
     double vv[U];
     int32_t cc[U];
 #pragma unroll
     for (int u = 0; u < U; u++) {
-        vv[u] = __builtin_nontemporal_load(v + u * SELL_V_STRIDE);
-        cc[u] = __builtin_nontemporal_load(c + u * SELL_C_STRIDE);
+        vv[u] = __builtin_nontemporal_load(v + u * SELL_C);
+        if constexpr (CM == 0) cc[u] = bs[u] + lane;
+        else if constexpr (CM == 1)
+            cc[u] = bs[u] + (int32_t)__builtin_nontemporal_load(static_cast<const uint16_t *>(ix) + u * SELL_C);
+        else cc[u] = __builtin_nontemporal_load(static_cast<const int32_t *>(ix) + u * SELL_C);
     }
     double xx[U];
 #pragma unroll
@@ -182,10 +196,34 @@ __device__ __forceinline__ void sell_chunk(const double *__restrict__ v, const i
     for (int u = 0; u < U; u++) acc = fma(vv[u], xx[u], acc);
 }
 
+template <int CM>
+__device__ __forceinline__ double sell_walk(const double *v, const char *ix, const int32_t *bs, int w, int lane,
+                                            const double *x) {
+    constexpr int IB = CM == 0 ? 0 : CM == 1 ? 2 : 4;  // index bytes per entry
+    double acc = 0.0;
+    int k = 0;
+    for (; k + 8 <= w; k += 8)
+        sell_chunk<CM, 8>(v + k * SELL_C, ix + (int64_t)k * SELL_C * IB, bs + k, lane, x, acc);
+    v += k * SELL_C;
+    ix += (int64_t)k * SELL_C * IB;
+    bs += k;
+    switch (w - k) {
+    case 1: sell_chunk<CM, 1>(v, ix, bs, lane, x, acc); break;
+    case 2: sell_chunk<CM, 2>(v, ix, bs, lane, x, acc); break;
+    case 3: sell_chunk<CM, 3>(v, ix, bs, lane, x, acc); break;
+    case 4: sell_chunk<CM, 4>(v, ix, bs, lane, x, acc); break;
+    case 5: sell_chunk<CM, 5>(v, ix, bs, lane, x, acc); break;
+    case 6: sell_chunk<CM, 6>(v, ix, bs, lane, x, acc); break;
+    case 7: sell_chunk<CM, 7>(v, ix, bs, lane, x, acc); break;
+    default: break;
+    }
+    return acc;
+}
+
 template <int MODE>
 __global__ __launch_bounds__(256) void spmv_sell_kernel(SellArgs a) {
     const int blk = xcd_remap(blockIdx.x, gridDim.x);
-    const int sl = blk * 4 + (threadIdx.x >> 6);
+    const int sl = __builtin_amdgcn_readfirstlane(blk * 4 + (int)(threadIdx.x >> 6));
     if (sl >= a.nslices) return;
     const int slice = a.slice0 + sl;
     const int lane = threadIdx.x & 63;
@@ -193,26 +231,18 @@ __global__ __launch_bounds__(256) void spmv_sell_kernel(SellArgs a) {
     const bool live = row < a.row0[slice + 1];
     EpiOps<MODE> ep;
     if (live) ep.load(a.e, row);
-    const int o0 = a.off[slice];
-    const int w = (a.off[slice + 1] - o0) >> 6;
-    const char *base = a.data + (int64_t)o0 * 12;
-    const double *v = reinterpret_cast<const double *>(base) + lane;
-    const int32_t *c = reinterpret_cast<const int32_t *>(base + SELL_C * 8) + lane;
-    const double *x = a.e.x;
-    double acc = 0.0;
-    int k = 0;
-    for (; k + 8 <= w; k += 8) sell_chunk<8>(v + k * SELL_V_STRIDE, c + k * SELL_C_STRIDE, x, acc);
-    v += k * SELL_V_STRIDE;
-    c += k * SELL_C_STRIDE;
-    switch (w - k) {
-    case 1: sell_chunk<1>(v, c, x, acc); break;
-    case 2: sell_chunk<2>(v, c, x, acc); break;
-    case 3: sell_chunk<3>(v, c, x, acc); break;
-    case 4: sell_chunk<4>(v, c, x, acc); break;
-    case 5: sell_chunk<5>(v, c, x, acc); break;
-    case 6: sell_chunk<6>(v, c, x, acc); break;
-    case 7: sell_chunk<7>(v, c, x, acc); break;
-    default: break;
+    const int t0 = a.soff[slice];
+    const int w = a.soff[slice + 1] - t0;
+    const uint32_t d = a.desc[slice];
+    const char *blkp = a.data + (int64_t)(d & 0x3fffffffu) * 128;
+    const double *v = reinterpret_cast<const double *>(blkp) + lane;
+    const char *ix = blkp + (int64_t)w * SELL_VAL_STEP;
+    const int32_t *bs = a.base + t0;
+    double acc;
+    switch (d >> 30) {
+    case 0: acc = sell_walk<0>(v, nullptr, bs, w, lane, a.e.x); break;
+    case 1: acc = sell_walk<1>(v, ix + lane * 2, bs, w, lane, a.e.x); break;
+    default: acc = sell_walk<2>(v, ix + lane * 4, bs, w, lane, a.e.x); break;
     }
     if (live) ep.store(a.e, acc);
 }
@@ -289,72 +319,181 @@ void build_schedule(const std::vector<int64_t> &rp, const std::vector<int64_t> &
     }
 }
 
-__global__ void k_sell_fill(const int64_t *rp, const int32_t *col, const double *val,
-                            const int32_t *off, const int32_t *row0, int64_t nslices, char *data) {
-    const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    if (t >= nslices * SELL_C) return;
-    const int64_t s = t / SELL_C, lane = t % SELL_C;
-    const int64_t r = row0[s] + lane;
-    const bool live = r < row0[s + 1];
-    const int64_t len = live ? rp[r + 1] - rp[r] : 0;
-    const int64_t base = live ? rp[r] : 0;
-    const int w = (off[s + 1] - off[s]) / SELL_C;
-    const int32_t cpad = len > 0 ? col[base + len - 1] : 0;
-    char *slice = data + (int64_t)off[s] * 12;
-    for (int k = 0; k < w; k++) {
-        double *sv = reinterpret_cast<double *>(slice + (int64_t)k * SELL_STEP_BYTES) + lane;
-        int32_t *sc = reinterpret_cast<int32_t *>(slice + (int64_t)k * SELL_STEP_BYTES + SELL_C * 8) + lane;
-        if (k < len) { *sc = col[base + k]; *sv = val[base + k]; }
-        else { *sc = cpad; *sv = 0.0; }
+// ---- SELL build: one wavefront per slice walks its rows in step order.
+
+__device__ __forceinline__ int64_t wave_min64(int64_t v) {
+    for (int o = 32; o > 0; o >>= 1) v = min(v, (int64_t)__shfl_xor((long long)v, o));
+    return v;
+}
+__device__ __forceinline__ int64_t wave_max64(int64_t v) {
+    for (int o = 32; o > 0; o >>= 1) v = max(v, (int64_t)__shfl_xor((long long)v, o));
+    return v;
+}
+
+constexpr int64_t SELL_NONE = INT64_MAX;
+
+// Walk the steps of one slice (all 64 lanes of the wave, uniform control flow).
+// f(t, col, val, step_mode, step_base) per step; returns the step count, or -1
+// if it would exceed max_steps.
+template <bool ALIGNED, class F>
+__device__ int sell_walk_build(const int64_t *rp, const int32_t *col, const double *val, int64_t row, bool live,
+                               int64_t ncols, int max_steps, F &&f) {
+    const int lane = threadIdx.x & 63;
+    int64_t p = live ? rp[row] : 0;
+    const int64_t e = live ? rp[row + 1] : 0;
+    for (int t = 0;; t++) {
+        bool real;
+        if constexpr (ALIGNED) {
+            const int64_t my = p < e ? (int64_t)col[p] - row : SELL_NONE;
+            const int64_t m = wave_min64(my);
+            if (m == SELL_NONE) return t;
+            real = my == m;
+        } else {
+            real = p < e;
+            if (!__any(real)) return t;
+        }
+        if (t >= max_steps) return -1;
+        int64_t c = 0;
+        double v = 0.0;
+        if (real) { c = col[p]; v = val[p]; p++; }
+        const int64_t b = wave_min64(real ? c - lane : SELL_NONE);
+        if (!real) c = std::min<int64_t>(std::max<int64_t>(b + lane, 0), ncols - 1);
+        const bool impl = __all(c == b + lane);
+        const int64_t mn = wave_min64(c), mx = wave_max64(c);
+        const int mode = impl ? 0 : (mx - mn < 65536 ? 1 : 2);
+        f(t, c, v, mode, mode == 0 ? b : mn);
     }
 }
 
+__host__ __device__ inline int64_t sell_slice_bytes(int64_t w, int mode) {
+    return w * (SELL_VAL_STEP + (mode == 0 ? 0 : mode == 1 ? 2 * SELL_C : 4 * SELL_C));
+}
+
+// plan[4 s ..] = {w_aligned (-1 = too wide), mode_aligned, w_plain, mode_plain}
+__global__ __launch_bounds__(256) void k_sell_plan(const int64_t *rp, const int32_t *col, const double *val,
+                                                   const int32_t *row0, int64_t nslices, int64_t ncols,
+                                                   int max_steps, int32_t *plan) {
+    const int64_t sl = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (sl >= nslices) return;
+    const int64_t row = row0[sl] + (threadIdx.x & 63);
+    const bool live = row < row0[sl + 1];
+    int ma = 0, mp = 0;
+    const int wa = sell_walk_build<true>(rp, col, val, row, live, ncols, max_steps,
+                                         [&](int, int64_t, double, int m, int64_t) { ma = max(ma, m); });
+    const int wp = sell_walk_build<false>(rp, col, val, row, live, ncols, max_steps,
+                                          [&](int, int64_t, double, int m, int64_t) { mp = max(mp, m); });
+    if ((threadIdx.x & 63) == 0) {
+        plan[4 * sl + 0] = wa;
+        plan[4 * sl + 1] = ma;
+        plan[4 * sl + 2] = wp;
+        plan[4 * sl + 3] = mp;
+    }
+}
+
+// aligned[s] chooses the layout; desc/soff as uploaded
+__global__ __launch_bounds__(256) void k_sell_fill(const int64_t *rp, const int32_t *col, const double *val,
+                                                   const int32_t *row0, const int32_t *soff, const uint32_t *desc,
+                                                   const uint8_t *aligned, int64_t nslices, int64_t ncols,
+                                                   int32_t *base, char *data) {
+    const int64_t sl = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (sl >= nslices) return;
+    const int lane = threadIdx.x & 63;
+    const int64_t row = row0[sl] + lane;
+    const bool live = row < row0[sl + 1];
+    const int w = soff[sl + 1] - soff[sl];
+    const uint32_t d = desc[sl];
+    const int smode = (int)(d >> 30);
+    char *blkp = data + (int64_t)(d & 0x3fffffffu) * 128;
+    double *vals = reinterpret_cast<double *>(blkp);
+    int32_t *bs = base + soff[sl];
+    auto put = [&](int t, int64_t c, double v, int, int64_t b) {
+        // the slice mode can exceed the step's: u16 steps use base = min column
+        const int64_t sb = smode == 1 ? wave_min64(c) : b;
+        vals[t * SELL_C + lane] = v;
+        if (lane == 0) bs[t] = smode == 2 ? 0 : (int32_t)sb;
+        if (smode == 1)
+            reinterpret_cast<uint16_t *>(blkp + (int64_t)w * SELL_VAL_STEP)[t * SELL_C + lane] = (uint16_t)(c - sb);
+        else if (smode == 2)
+            reinterpret_cast<int32_t *>(blkp + (int64_t)w * SELL_VAL_STEP)[t * SELL_C + lane] = (int32_t)c;
+    };
+    if (aligned[sl]) sell_walk_build<true>(rp, col, val, row, live, ncols, w, put);
+    else sell_walk_build<false>(rp, col, val, row, live, ncols, w, put);
+}
+
 void build_sell(GpuCsr &m, const std::vector<int64_t> &rp) {
-    m.sell_off.release();
     m.sell_row0.release();
+    m.sell_soff.release();
+    m.sell_desc.release();
+    m.sell_base.release();
     m.sell_data.release();
-    m.nslices = m.sell_padded = 0;
+    m.nslices = m.sell_steps = m.sell_bytes = 0;
+    m.sell_mode_slices[0] = m.sell_mode_slices[1] = m.sell_mode_slices[2] = 0;
     m.seg_slc.clear();
     const int pol = g_spmv_format_policy;
     if (pol == 1 || pol == 3 || m.nrows == 0 || m.nnz == 0) return;
-    std::vector<int32_t> off{0}, row0;
+    // slices never straddle a segment
+    std::vector<int32_t> row0;
     std::vector<int64_t> seg_slc{0};
-    int64_t padded = 0, maxw = 0;
+    int64_t maxlen = 0;
     for (size_t g = 0; g + 1 < m.seg_rows.size(); g++) {
-        for (int64_t r0 = m.seg_rows[g]; r0 < m.seg_rows[g + 1]; r0 += SELL_C) {
-            const int64_t r1 = std::min<int64_t>(m.seg_rows[g + 1], r0 + SELL_C);
-            int64_t w = 0;
-            for (int64_t r = r0; r < r1; r++) w = std::max<int64_t>(w, rp[r + 1] - rp[r]);
-            maxw = std::max(maxw, w);
-            padded += w * SELL_C;
-            if (padded >= (int64_t(1) << 31)) return;
-            off.push_back(static_cast<int32_t>(padded));
-            row0.push_back(static_cast<int32_t>(r0));
-        }
-        seg_slc.push_back(static_cast<int64_t>(row0.size()));
+        for (int64_t r0 = m.seg_rows[g]; r0 < m.seg_rows[g + 1]; r0 += SELL_C) row0.push_back((int32_t)r0);
+        seg_slc.push_back((int64_t)row0.size());
     }
-    row0.push_back(static_cast<int32_t>(m.nrows));
-    // auto: SELL pays when there are enough slices to fill the chip (>= 1024
-    // slices = 64K rows) and padding is modest; measured on the 256^3 hierarchy
-    // (scripts/ab_levels.py) it beats CSR-stream up to ~170-entry rows.
-    const bool ok = pol == 2 ? maxw <= 256
-                             : (maxw <= SELL_MAX_W && padded * 100 <= m.nnz * 125 &&
-                                (m.nrows >= SELL_MIN_ROWS || maxw <= 16));
-    if (!ok) return;
-    const int64_t ns = static_cast<int64_t>(off.size()) - 1;
+    for (int64_t r = 0; r < m.nrows; r++) maxlen = std::max<int64_t>(maxlen, rp[r + 1] - rp[r]);
+    const int max_w = pol == 2 ? 256 : SELL_MAX_W;
+    if (maxlen > max_w) return;
+    row0.push_back((int32_t)m.nrows);
+    const int64_t ns = (int64_t)row0.size() - 1;
     hipStream_t s = m.ctx->stream;
-    m.sell_off.resize(ns + 1);
-    m.sell_row0.resize(ns + 1);
-    m.sell_data.resize(padded * 12);
-    FAMG_CHECK_HIP(hipMemcpyAsync(m.sell_off.get(), off.data(), (ns + 1) * sizeof(int32_t), hipMemcpyHostToDevice, s));
-    FAMG_CHECK_HIP(hipMemcpyAsync(m.sell_row0.get(), row0.data(), (ns + 1) * sizeof(int32_t), hipMemcpyHostToDevice, s));
-    hipLaunchKernelGGL(k_sell_fill, dim3((unsigned)ceil_div(ns * SELL_C, 256)), dim3(256), 0, s,
-                       m.rp64.get(), m.col.get(), m.val.get(), m.sell_off.get(), m.sell_row0.get(), ns,
-                       m.sell_data.get());
+    DevBuf<int32_t> drow0(ns + 1), dplan(4 * ns);
+    FAMG_CHECK_HIP(hipMemcpyAsync(drow0.get(), row0.data(), (ns + 1) * sizeof(int32_t), hipMemcpyHostToDevice, s));
+    const dim3 grid((unsigned)ceil_div(ns, 4));
+    hipLaunchKernelGGL(k_sell_plan, grid, dim3(256), 0, s, m.rp64.get(), m.col.get(), m.val.get(), drow0.get(), ns,
+                       m.ncols, max_w, dplan.get());
+    FAMG_CHECK_HIP(hipGetLastError());
+    std::vector<int32_t> plan(4 * ns);
+    FAMG_CHECK_HIP(hipMemcpyAsync(plan.data(), dplan.get(), plan.size() * sizeof(int32_t), hipMemcpyDeviceToHost, s));
+    FAMG_CHECK_HIP(hipStreamSynchronize(s));
+    // per slice: the cheaper layout; then offsets
+    std::vector<int32_t> soff(ns + 1, 0);
+    std::vector<uint32_t> desc(ns);
+    std::vector<uint8_t> aligned(ns);
+    int64_t bytes = 0, steps = 0, cnt[3] = {0, 0, 0};
+    for (int64_t k = 0; k < ns; k++) {
+        const int wa = plan[4 * k], ma = plan[4 * k + 1], wp = plan[4 * k + 2], mp = plan[4 * k + 3];
+        const bool al = wa >= 0 && sell_slice_bytes(wa, ma) <= sell_slice_bytes(wp, mp);
+        const int w = al ? wa : wp, md = al ? ma : mp;
+        aligned[k] = al;
+        if (bytes / 128 >= (int64_t(1) << 30) || steps + w >= (int64_t(1) << 31)) return;
+        desc[k] = (uint32_t)(bytes / 128) | ((uint32_t)md << 30);
+        bytes += sell_slice_bytes(w, md);
+        steps += w;
+        soff[k + 1] = (int32_t)steps;
+        cnt[md]++;
+    }
+    // auto: SELL pays when there are enough slices to fill the chip (>= 1024
+    // slices = 64K rows) and it streams no more than 1.25x the CSR bytes;
+    // measured on the 256^3 hierarchy (scripts/ab_levels.py).
+    const bool ok = pol == 2 || (bytes * 100 <= 12 * m.nnz * 125 && (m.nrows >= SELL_MIN_ROWS || maxlen <= 16));
+    if (!ok) return;
+    m.sell_row0 = std::move(drow0);
+    m.sell_soff.resize(ns + 1);
+    m.sell_desc.resize(ns);
+    m.sell_base.resize(std::max<int64_t>(1, steps));
+    m.sell_data.resize(std::max<int64_t>(128, bytes));
+    DevBuf<uint8_t> dal(ns);
+    FAMG_CHECK_HIP(hipMemcpyAsync(m.sell_soff.get(), soff.data(), (ns + 1) * sizeof(int32_t), hipMemcpyHostToDevice, s));
+    FAMG_CHECK_HIP(hipMemcpyAsync(m.sell_desc.get(), desc.data(), ns * sizeof(uint32_t), hipMemcpyHostToDevice, s));
+    FAMG_CHECK_HIP(hipMemcpyAsync(dal.get(), aligned.data(), ns, hipMemcpyHostToDevice, s));
+    hipLaunchKernelGGL(k_sell_fill, grid, dim3(256), 0, s, m.rp64.get(), m.col.get(), m.val.get(),
+                       m.sell_row0.get(), m.sell_soff.get(), m.sell_desc.get(), dal.get(), ns, m.ncols,
+                       m.sell_base.get(), m.sell_data.get());
     FAMG_CHECK_HIP(hipGetLastError());
     FAMG_CHECK_HIP(hipStreamSynchronize(s));
     m.nslices = ns;
-    m.sell_padded = padded;
+    m.sell_steps = steps;
+    m.sell_bytes = bytes;
+    for (int k = 0; k < 3; k++) m.sell_mode_slices[k] = cnt[k];
     m.seg_slc = seg_slc;
 }
 
@@ -388,8 +527,8 @@ void spmv(const GpuCsr &m, const double *x, double *y, SpmvMode mode, const Spmv
         const int64_t s0 = seg < 0 ? 0 : m.seg_slc[seg];
         const int64_t s1 = seg < 0 ? m.nslices : m.seg_slc[seg + 1];
         if (s1 <= s0) return;
-        SellArgs a{m.sell_off.get(), m.sell_row0.get(), m.sell_data.get(), (int32_t)s0,
-                   (int32_t)(s1 - s0), e};
+        SellArgs a{m.sell_row0.get(), m.sell_soff.get(), m.sell_desc.get(), m.sell_base.get(),
+                   m.sell_data.get(), (int32_t)s0, (int32_t)(s1 - s0), e};
         const dim3 grid((unsigned)ceil_div(s1 - s0, 4));
         FAMG_LAUNCH_MODES(spmv_sell_kernel, grid, block, s, a)
     } else if (m.kernel == SPMV_KERNEL_VECTOR) {

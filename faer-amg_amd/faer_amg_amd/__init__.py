@@ -54,6 +54,7 @@ SIGNATURES = {
     "amg_csr_create": (i32, [vp, i64, i64, vp, vp, vp, P(vp)]),
     "amg_csr_create_device_i32": (i32, [vp, i64, i64, vp, vp, vp, P(vp)]),
     "amg_csr_nnz": (i32, [vp, P(i64)]),
+    "amg_csr_spmv_info": (i32, [vp, vp]),
     "amg_csr_download": (i32, [vp, vp, vp, vp]),
     "amg_gen_laplace3d_7pt": (i32, [vp, i64, i64, i64, P(vp)]),
     "amg_gen_aniso27": (i32, [vp, i64, i64, i64, dbl, dbl, dbl, P(vp)]),
@@ -336,6 +337,16 @@ class SparseMatOp(LinOp):
         v = i64()
         _ck(_lib.amg_csr_nnz(self.h, C.byref(v)))
         return v.value
+
+    def spmv_info(self):
+        """SpMV storage chosen for this matrix (kernel, bytes streamed per SpMV, SELL stats)."""
+        info = np.zeros(8, np.int64)
+        _ck(_lib.amg_csr_spmv_info(self.h, info.ctypes.data_as(vp)))
+        keys = ("kernel", "stream_bytes", "csr_bytes", "slices", "stored_entries",
+                "slices_implicit", "slices_u16", "slices_i32")
+        d = dict(zip(keys, (int(v) for v in info)))
+        d["kernel"] = ("csr-stream", "sell", "vector")[d["kernel"]]
+        return d
 
     def arrays(self):
         m, n = self.dims()

@@ -103,6 +103,11 @@ amg_status amg_csr_create_device_i32(amg_ctx *ctx, int64_t nrows, int64_t ncols,
                                      const double *vals, amg_linop **out);
 /* Number of stored entries of a CSR operator. */
 amg_status amg_csr_nnz(const amg_linop *op, int64_t *nnz);
+/* SpMV storage chosen for a CSR operator: info8 = {kernel (0 CSR-stream,
+ * 1 SELL-64, 2 vector), matrix bytes one SpMV streams, CSR bytes (12 nnz +
+ * 4 (n+1)), SELL slices, SELL stored entries incl. padding, SELL slices with
+ * implicit / 16-bit delta / 32-bit column indices}. */
+amg_status amg_csr_spmv_info(const amg_linop *op, int64_t *info8);
 /* Copy a CSR operator back to host arrays (rowptr: nrows+1, colidx/vals: nnz). */
 amg_status amg_csr_download(const amg_linop *op, int64_t *rowptr, int64_t *colidx, double *vals);
 /* Device-side generators for the benchmark operators:

@@ -2,15 +2,16 @@
 
 Runs, on one GPU:
   * CAL: y = D x with D a diagonal 16.7M x 16.7M matrix through the same SELL-64
-    kernel (w = 1): exactly known traffic per launch (reads 8n val + 4n col +
-    8n x + 4 n/64 offsets, writes 8n y) -- calibrates FETCH_SIZE/WRITE_SIZE for
-    this kernel's access widths (the guide: only 16-B/lane streams are
-    calibrated, FETCH_SIZE = half the bytes).
+    kernel (one implicit-column step per slice): exactly known traffic per
+    launch (the matrix bytes the format streams + 8n x read, 8n y written) --
+    calibrates FETCH_SIZE/WRITE_SIZE for this kernel's access widths (the
+    guide: only 16-B/lane streams are calibrated, FETCH_SIZE = half the bytes).
   * FINE: y = A_0 x, the 256^3 7-point operator (SELL-64).
 The two are told apart in the trace by grid size (CAL 65536 blocks of 256
 threads for 262144 slices; FINE the same slice count -- so CAL runs first,
 ITERS launches, then FINE, ITERS launches; the summariser splits by order).
 """
+import json
 import os
 import sys
 
@@ -39,4 +40,7 @@ assert torch.equal(y, 2.0 * x)
 for _ in range(ITERS):
     A.apply(y, x)
 ctx.synchronize()
-print(f"done: n={n} nnz(A)={A.nnz}")
+info = {"cal": D.spmv_info(), "fine": A.spmv_info(), "n": n}
+os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
+json.dump(info, open(os.path.join(ROOT, "gpurun_out", "pmc_known.json"), "w"), indent=1)
+print(f"done: n={n} nnz(A)={A.nnz} storage={info}")

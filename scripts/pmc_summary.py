@@ -1,11 +1,11 @@
 """Fine-SpMV HBM traffic from the rocprofv3 PMC passes of scripts/pmc_fine_spmv.py.
 
-  python scripts/pmc_summary.py FETCH.csv WRITE.csv OUT.json
+  python scripts/pmc_summary.py FETCH.csv WRITE.csv KNOWN.json OUT.json
 
 FETCH_SIZE / WRITE_SIZE are in KiB per dispatch.  The first ITERS SELL
-dispatches are the calibration (diagonal matrix, n = 256^3: exactly
-20 n + 4 ceil(n/64) + 4 bytes read, 8 n written); the last ITERS are the 7-point
-operator.  Read bytes = FETCH_SIZE * 1024 * (known calibration bytes /
+dispatches are the calibration (diagonal matrix, n = 256^3: exactly the matrix
+stream bytes recorded in KNOWN.json + 8 n read, 8 n written); the last ITERS
+are the 7-point operator.  Read bytes = FETCH_SIZE * 1024 * (known calibration bytes /
 calibration FETCH_SIZE bytes) -- on gfx950 that factor is ~2 for streaming
 loads (MI355X_MICROARCH.md, HBM section).
 """
@@ -27,15 +27,18 @@ def sell_values(path, counter):
     return vals[:ITERS], vals[ITERS:]
 
 
-def main(fetch_csv, write_csv, out_json):
+def main(fetch_csv, write_csv, known_json, out_json):
+    known = json.load(open(known_json))
     cal_f, fine_f = sell_values(fetch_csv, "FETCH_SIZE")
     cal_w, fine_w = sell_values(write_csv, "WRITE_SIZE")
-    cal_read_known = 20 * N + 4 * (-(-N // 64) + 1)
+    cal_read_known = known["cal"]["stream_bytes"] + 8 * N
     factor = cal_read_known / statistics.median(cal_f)
     read = statistics.median(fine_f) * factor
     write = statistics.median(fine_w)
     out = {
         "kernel": "spmv_sell_kernel<SET> on A_0 (7-pt 256^3)",
+        "storage": known["fine"],
+        "algorithmic_bytes_per_launch": known["fine"]["stream_bytes"] + 16 * N,
         "fetch_correction_factor": round(factor, 4),
         "calibration": {"known_read_bytes": cal_read_known,
                         "fetch_size_bytes": statistics.median(cal_f),
@@ -49,4 +52,4 @@ def main(fetch_csv, write_csv, out_json):
 
 
 if __name__ == "__main__":
-    main(*sys.argv[1:4])
+    main(*sys.argv[1:5])

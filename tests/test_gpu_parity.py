@@ -134,6 +134,51 @@ def test_spmv_formats(ctx, fmt):
         fa().set_spmv_format("auto")
 
 
+def _random_rows(rng, m, n, per_row, spread):
+    """CSR with per_row random sorted columns per row within +-spread of the
+    diagonal position (clipped), plus some empty rows."""
+    rp, ci = [0], []
+    for i in range(m):
+        k = 0 if i % 17 == 5 else int(rng.integers(1, per_row + 1))
+        c0 = i * n // m
+        lo, hi = max(0, c0 - spread), min(n, c0 + spread + 1)
+        cols = np.sort(rng.choice(np.arange(lo, hi), size=min(k, hi - lo), replace=False))
+        ci.extend(cols.tolist())
+        rp.append(len(ci))
+    rp = np.asarray(rp, np.int64)
+    ci = np.asarray(ci, np.int64)
+    return O.Csr.from_arrays(m, n, rp, ci, rng.standard_normal(len(ci)))
+
+
+def test_sell_column_modes(ctx):
+    """SELL-64 stores a slice's columns implicitly (stencil offsets, aligned
+    steps), as 16-bit deltas or as int32; every mode sums each row in stored
+    order in one lane, so results are bitwise equal to the oracle."""
+    rng = np.random.default_rng(21)
+    fa().set_spmv_format("sell")
+    try:
+        cases = {
+            "7pt": (O.laplace3d_7pt(64, 12, 6), "slices_implicit"),
+            "27pt": (O.aniso27(64, 9, 5), "slices_implicit"),
+            "band": (_random_rows(rng, 3001, 3001, 12, 2000), "slices_u16"),
+            "wide": (_random_rows(rng, 1000, 400000, 9, 200000), "slices_i32"),
+        }
+        for name, (OM, dominant) in cases.items():
+            M = gpu_csr(ctx, OM)
+            info = M.spmv_info()
+            assert info["kernel"] == "sell", name
+            assert info[dominant] * 2 > info["slices"], (name, info)
+            x = rng.standard_normal(OM.ncols)
+            assert np.array_equal(apply_dev(ctx, M, x, OM.nrows), OM.spmv(x)), name
+            if name == "7pt":
+                # aligned steps: boundary rows padded, but < 20 % extra entries,
+                # and 8 B/entry + metadata instead of 12
+                assert info["stored_entries"] < 1.2 * OM.dims()[2]
+                assert info["stream_bytes"] < 0.8 * info["csr_bytes"]
+    finally:
+        fa().set_spmv_format("auto")
+
+
 def test_vcycle_forced_sell(ctx):
     fa().set_spmv_format("sell")
     try:
