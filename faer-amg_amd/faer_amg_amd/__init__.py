@@ -106,6 +106,19 @@ SIGNATURES = {
     "amg_dist_level_operator": (i32, [vp, i64, P(vp)]),
     "amg_dist_level_matrix": (i32, [vp, i64, i32, P(vp)]),
     "amg_dist_set_option": (i32, [vp, i32, i64]),
+    "amg_mtx_read": (i32, [C.c_char_p, P(vp)]),
+    "amg_host_csr_dims": (i32, [vp, P(i64), P(i64), P(i64)]),
+    "amg_host_csr_arrays": (i32, [vp, vp, vp, vp]),
+    "amg_host_csr_upload": (i32, [vp, vp, P(vp)]),
+    "amg_host_csr_destroy": (i32, [vp]),
+    "amg_mfem_load": (i32, [C.c_char_p, C.c_char_p, i32, P(vp)]),
+    "amg_mfem_info": (i32, [vp, vp]),
+    "amg_mfem_matrix": (i32, [vp, P(vp)]),
+    "amg_mfem_rhs": (i32, [vp, vp, i64]),
+    "amg_mfem_coords": (i32, [vp, vp, i64]),
+    "amg_mfem_boundary": (i32, [vp, vp]),
+    "amg_mfem_index_maps": (i32, [vp, vp, vp]),
+    "amg_mfem_destroy": (i32, [vp]),
     "amg_dist_stationary_solve": (i32, [vp, vp, vp, i64, dbl, vp, P(i64)]),
 }
 
@@ -668,3 +681,81 @@ def box_level_dims(dims, box, nlevels):
     for _ in range(nlevels - 1):
         d.append(tuple(-(-a // b) for a, b in zip(d[-1], box)))
     return d
+
+
+# ------------------------------------------------------------------ loaders
+
+class HostCsr:
+    """Host CSR from a loader (int64 row pointers / columns, f64 values)."""
+
+    def __init__(self, h, owner=None):
+        self.h = h
+        self._owner = owner  # borrowed from an MfemSystem when set
+
+    def __del__(self, _destroy=_lib.amg_host_csr_destroy):
+        if getattr(self, "h", None) and self._owner is None:
+            _destroy(self.h)
+            self.h = None
+
+    def dims(self):
+        m, n, z = i64(), i64(), i64()
+        _ck(_lib.amg_host_csr_dims(self.h, C.byref(m), C.byref(n), C.byref(z)))
+        return m.value, n.value, z.value
+
+    def arrays(self):
+        m, _, z = self.dims()
+        rp = np.zeros(m + 1, np.int64)
+        ci = np.zeros(z, np.int64)
+        va = np.zeros(z, np.float64)
+        _ck(_lib.amg_host_csr_arrays(self.h, rp.ctypes.data_as(vp), ci.ctypes.data_as(vp),
+                                     va.ctypes.data_as(vp)))
+        return rp, ci, va
+
+    def to_scipy(self):
+        import scipy.sparse as sps
+        m, n, _ = self.dims()
+        rp, ci, va = self.arrays()
+        return sps.csr_matrix((va, ci, rp), shape=(m, n))
+
+    def upload(self, ctx):
+        h = vp()
+        _ck(_lib.amg_host_csr_upload(ctx.h, self.h, C.byref(h)))
+        return SparseMatOp(h, ctx)
+
+
+def read_mtx(path):
+    """Matrix Market coordinate file -> HostCsr (utils.rs:508-534 semantics)."""
+    h = vp()
+    _ck(_lib.amg_mtx_read(os.fsencode(path), C.byref(h)))
+    return HostCsr(h)
+
+
+class MfemSystem:
+    """dir/name.{mtx,bdy,coords,rhs} (load_mfem_linear_system, utils.rs:269-350)."""
+
+    def __init__(self, directory, name, delete_boundary=True):
+        h = vp()
+        _ck(_lib.amg_mfem_load(os.fsencode(directory), os.fsencode(name),
+                               1 if delete_boundary else 0, C.byref(h)))
+        self.h = h
+        info = np.zeros(5, np.int64)
+        _ck(_lib.amg_mfem_info(self.h, info.ctypes.data_as(vp)))
+        self.n, self.rhs_cols, self.coord_dim, self.original_dim, nb = (int(v) for v in info)
+        mh = vp()
+        _ck(_lib.amg_mfem_matrix(self.h, C.byref(mh)))
+        self.matrix = HostCsr(mh, owner=self)
+        self.rhs = np.zeros((self.n, self.rhs_cols), order="F")
+        self.coords = np.zeros((self.n, self.coord_dim), order="F")
+        self.boundary = np.zeros(nb, np.int64)
+        self.solution_to_mesh = np.zeros(self.n, np.int64)
+        self.mesh_to_solution = np.zeros(self.original_dim, np.int64)
+        _ck(_lib.amg_mfem_rhs(self.h, self.rhs.ctypes.data_as(vp), max(1, self.n)))
+        _ck(_lib.amg_mfem_coords(self.h, self.coords.ctypes.data_as(vp), max(1, self.n)))
+        _ck(_lib.amg_mfem_boundary(self.h, self.boundary.ctypes.data_as(vp)))
+        _ck(_lib.amg_mfem_index_maps(self.h, self.solution_to_mesh.ctypes.data_as(vp),
+                                     self.mesh_to_solution.ctypes.data_as(vp)))
+
+    def __del__(self, _destroy=_lib.amg_mfem_destroy):
+        if getattr(self, "h", None):
+            _destroy(self.h)
+            self.h = None

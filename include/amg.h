@@ -294,6 +294,41 @@ amg_status amg_dist_stationary_solve(amg_linop *dist_mg, const double *b, double
                                      int64_t max_iter, double rel_tol, double *hist,
                                      int64_t *iters);
 
+/* ---- Dataset loaders (utils.rs:269-534) -------------------
+ * Host-side; no device needed.  Matrix Market: sparse coordinate files
+ * (real/integer/pattern, general/symmetric), 1-based indices, explicit 0.0
+ * entries dropped, symmetric entries mirrored, duplicates summed, columns
+ * sorted (load_matrix_triplets, utils.rs:508-534, + faer try_new_from_triplets). */
+typedef struct amg_host_csr amg_host_csr;
+amg_status amg_mtx_read(const char *path, amg_host_csr **out);
+amg_status amg_host_csr_dims(const amg_host_csr *h, int64_t *nrows, int64_t *ncols, int64_t *nnz);
+amg_status amg_host_csr_arrays(const amg_host_csr *h, int64_t *rowptr, int64_t *colidx, double *vals);
+/* Upload to the device (amg_csr_create). */
+amg_status amg_host_csr_upload(amg_ctx *ctx, const amg_host_csr *h, amg_linop **out);
+amg_status amg_host_csr_destroy(amg_host_csr *h);
+
+/* MFEM linear system dir/name.{mtx,bdy,coords,rhs} (load_mfem_linear_system,
+ * utils.rs:269-350); delete_boundary removes the .bdy rows/columns and
+ * renumbers the rest in order (utils.rs:446-480).  The VTK mesh geometry the
+ * reference also attaches (visualisation only) is not loaded. */
+typedef struct amg_mfem_system amg_mfem_system;
+amg_status amg_mfem_load(const char *dir, const char *name, int32_t delete_boundary,
+                         amg_mfem_system **out);
+/* info5 = {n (after deletion), rhs columns, coordinate dimension, original n,
+ * boundary indices (sorted, unique)} */
+amg_status amg_mfem_info(const amg_mfem_system *sys, int64_t *info5);
+/* The system matrix (borrowed; valid while sys lives). */
+amg_status amg_mfem_matrix(const amg_mfem_system *sys, const amg_host_csr **out);
+/* rhs (n x k) and coords (n x d), column-major with leading dimension ld. */
+amg_status amg_mfem_rhs(const amg_mfem_system *sys, double *out, int64_t ld);
+amg_status amg_mfem_coords(const amg_mfem_system *sys, double *out, int64_t ld);
+amg_status amg_mfem_boundary(const amg_mfem_system *sys, int64_t *out);
+/* solution_to_mesh (n entries), mesh_to_solution (original n entries, -1 =
+ * deleted); either may be NULL. */
+amg_status amg_mfem_index_maps(const amg_mfem_system *sys, int64_t *solution_to_mesh,
+                               int64_t *mesh_to_solution);
+amg_status amg_mfem_destroy(amg_mfem_system *sys);
+
 #ifdef __cplusplus
 }
 #endif

@@ -272,3 +272,94 @@ def sa_hierarchy_box(A, dims, box=(2, 2, 2), coarsest_dim=1000, omega=0.66):
         coarse_dim = Ac.shape[0]
     levels.append({"A": cur, "dims": cur_dims})
     return levels
+
+
+# ------------------------------------------------------------- dataset loaders
+
+def load_mtx(path):
+    """Matrix Market coordinate file -> scipy CSR, restating the reference's
+    load_matrix_triplets (utils.rs:508-534: 0.0 entries dropped, symmetric
+    entries mirrored) on top of the matrix-market-rs 0.1.3 parser (1-based
+    indices, real/integer/pattern fields) and faer's try_new_from_triplets
+    (duplicates summed in file order, sorted columns).  Pure-Python parsing,
+    independent of the library's mmap/strtod parser."""
+    with open(path) as f:
+        lines = f.read().split("\n")
+    head = lines[0].lower().split()
+    assert head[0] == "%%matrixmarket" and head[2] == "coordinate"
+    field, sym = head[3], head[4]
+    k = 1
+    while lines[k].strip() == "" or lines[k].lstrip().startswith("%"):
+        k += 1
+    m, n, nnz = (int(t) for t in lines[k].split())
+    trip = []
+    count = 0
+    for line in lines[k + 1:]:
+        s = line.strip()
+        if not s or s.startswith("%"):
+            continue
+        t = s.split()
+        count += 1
+        i, j = int(t[0]) - 1, int(t[1]) - 1
+        v = 1.0 if field == "pattern" else float(t[2])
+        if v == 0.0:
+            continue
+        trip.append((i, j, v))
+        if sym == "symmetric" and i != j:
+            trip.append((j, i, v))
+    assert count == nnz
+    return triplets_to_csr(m, n, trip)
+
+
+def triplets_to_csr(m, n, trip):
+    rows = [dict() for _ in range(m)]
+    for i, j, v in trip:  # file order: duplicates summed left to right
+        rows[i][j] = rows[i][j] + v if j in rows[i] else v
+    rp, ci, va = [0], [], []
+    for r in rows:
+        for j in sorted(r):
+            ci.append(j)
+            va.append(r[j])
+        rp.append(len(ci))
+    return sp.csr_matrix((np.asarray(va, float), np.asarray(ci, np.int64), np.asarray(rp, np.int64)),
+                         shape=(m, n))
+
+
+def load_mfem(directory, name, delete_boundary=True):
+    """load_mfem_linear_system (utils.rs:269-350) without the VTK mesh:
+    returns (A, rhs (n x k), coords (n x d), boundary (sorted unique),
+    solution_to_mesh, mesh_to_solution (-1 = deleted))."""
+    import os
+    base = os.path.join(directory, name)
+    with open(base + ".bdy") as f:
+        bl = f.read().split("\n")
+    expect = int(bl[0].strip())
+    bidx = [int(s) for s in (x.strip() for x in bl[1:]) if s]   # utils.rs:364-395
+    assert len(bidx) == expect
+    boundary = sorted(set(bidx))
+    A = load_mtx(base + ".mtx")
+    n = A.shape[0]
+    assert A.shape[0] == A.shape[1]
+    with open(base + ".coords") as f:                            # utils.rs:397-415
+        coords = [[float(t) for t in line.split()] for line in f if line.split()]
+    assert len(coords) == n
+    with open(base + ".rhs") as f:                               # utils.rs:417-430
+        flat = [float(t) for t in f.read().split()]
+    assert len(flat) % n == 0
+    k = len(flat) // n
+    rhs_full = np.asarray(flat).reshape(k, n).T                 # column-major (utils.rs:308-315)
+    if delete_boundary:                                         # utils.rs:446-480
+        isb = np.zeros(n, bool)
+        isb[boundary] = True
+        sel = np.flatnonzero(~isb)
+    else:
+        sel = np.arange(n)
+    m2s = -np.ones(n, np.int64)
+    m2s[sel] = np.arange(len(sel))
+    if delete_boundary:
+        # filter the (already summed) matrix: same as filtering the triplets,
+        # since rows/columns are removed whole
+        A = A[sel][:, sel].tocsr()
+        A.sort_indices()
+    C = np.asarray([coords[i] for i in sel]) if len(sel) else np.zeros((0, 0))
+    return A, rhs_full[sel], C, np.asarray(boundary, np.int64), sel.astype(np.int64), m2s
