@@ -576,85 +576,4 @@ amg_status amg_sa_build_box(amg_linop *A, int64_t nx, int64_t ny, int64_t nz, in
 
 // ------------------------------------------------------------ solve drivers
 
-amg_status amg_stationary_solve(amg_linop *A, amg_linop *M, const double *b, double *x, int64_t max_iter,
-                                double rel_tol, double *hist, int64_t *iters) {
-    return guard([&] {
-        LinOp &a = need(A);
-        LinOp &m = need(M);
-        FAMG_REQUIRE(b && x && iters && max_iter > 0, AMG_ERR_INVALID, "bad argument");
-        FAMG_REQUIRE(a.nrows == a.ncols && m.nrows == a.nrows, AMG_ERR_DIM, "solver dims");
-        Ctx &ctx = *a.ctx;
-        ctx.set_device();
-        hipStream_t s = ctx.stream;
-        const int64_t n = a.nrows;
-        DevBuf<double> r(n), z(n);
-        const double bn = std::sqrt(vec_dot(b, b, n, ctx));
-        auto *ac = dynamic_cast<CsrOp *>(&a);
-        int64_t it = 0;
-        for (;;) {
-            if (ac) {
-                SpmvEpi epi;
-                epi.b = b;
-                spmv(ac->m, x, r.get(), SPMV_RESID, epi, s);
-            } else {
-                a.apply(r.get(), x);
-                vec_sub(r.get(), b, r.get(), n, s);
-            }
-            const double rel = std::sqrt(vec_dot(r.get(), r.get(), n, ctx)) / bn;
-            it++;
-            if (hist) hist[it - 1] = rel;
-            if (rel < rel_tol || it >= max_iter) break;
-            m.apply(z.get(), r.get());
-            vec_add_inplace(x, z.get(), n, s);
-        }
-        FAMG_CHECK_HIP(hipStreamSynchronize(s));
-        *iters = it;
-    });
-}
-
-amg_status amg_pcg_solve(amg_linop *A, amg_linop *M, const double *b, double *x, int64_t max_iter,
-                         double rel_tol, double abs_tol, double *hist, int64_t *iters) {
-    return guard([&] {
-        LinOp &a = need(A);
-        FAMG_REQUIRE(b && x && iters && max_iter >= 0, AMG_ERR_INVALID, "bad argument");
-        LinOp *m = M ? &need(M) : nullptr;
-        FAMG_REQUIRE(a.nrows == a.ncols && (!m || m->nrows == a.nrows), AMG_ERR_DIM, "solver dims");
-        Ctx &ctx = *a.ctx;
-        ctx.set_device();
-        hipStream_t s = ctx.stream;
-        const int64_t n = a.nrows;
-        DevBuf<double> r(n), z(n), p(n), Ap(n);
-        a.apply(Ap.get(), x);
-        vec_sub(r.get(), b, Ap.get(), n, s);
-        const double bn = std::sqrt(vec_dot(b, b, n, ctx));
-        const double tol = std::max(rel_tol * bn, abs_tol);
-        int64_t it = 0;
-        if (std::sqrt(vec_dot(r.get(), r.get(), n, ctx)) > tol) {
-            auto pc = [&](double *dst, const double *src) {
-                if (m) m->apply(dst, src);
-                else vec_copy(dst, src, n, s);
-            };
-            pc(z.get(), r.get());
-            vec_copy(p.get(), z.get(), n, s);
-            double rz = vec_dot(r.get(), z.get(), n, ctx);
-            for (it = 1; it <= max_iter; it++) {
-                a.apply(Ap.get(), p.get());
-                const double alpha = rz / vec_dot(p.get(), Ap.get(), n, ctx);
-                vec_axpy(x, alpha, p.get(), n, s);
-                vec_axpy(r.get(), -alpha, Ap.get(), n, s);
-                const double rn = std::sqrt(vec_dot(r.get(), r.get(), n, ctx));
-                if (hist) hist[it - 1] = rn / bn;
-                if (rn <= tol) break;
-                pc(z.get(), r.get());
-                const double rzn = vec_dot(r.get(), z.get(), n, ctx);
-                const double beta = rzn / rz;
-                rz = rzn;
-                vec_xpay(p.get(), beta, z.get(), n, s);
-            }
-        }
-        FAMG_CHECK_HIP(hipStreamSynchronize(s));
-        *iters = it;
-    });
-}
-
 }  // extern "C"

@@ -27,6 +27,7 @@
 #include <mutex>
 
 #include "handles.hpp"
+#include "solve.hpp"
 
 using namespace famg;
 
@@ -518,6 +519,17 @@ struct DistMultigridOp : LinOp {
         if (cnt) vec_sub(r, b, rfull_.get() + r0, cnt, s);
     }
 
+    // out_own = (A_0 x)_own, distributed or not
+    DevBuf<double> zero_;
+    void apply0(double *out, const double *x) {
+        if (zero_.size() < (size_t)std::max<int64_t>(1, nrows)) {
+            zero_.resize(std::max<int64_t>(1, nrows));
+            vec_fill(zero_.get(), 0.0, nrows, ctx->stream);
+        }
+        residual0(zero_.get(), x, out);           // 0 - A x
+        vec_scale(out, -1.0, nrows, ctx->stream);  // exact
+    }
+
     void apply(double *out, const double *rhs) override {
         std::lock_guard<std::mutex> lk(mtx);
         hipStream_t s = ctx->stream;
@@ -863,40 +875,51 @@ amg_status amg_dist_set_option(amg_linop *dist, int32_t option, int64_t value) {
     });
 }
 
+static SolveOps dist_ops(const std::shared_ptr<DistMultigridOp> &d, bool precondition) {
+    SolveOps o;
+    o.ctx = d->ctx;
+    o.n = d->nrows;
+    DistMultigridOp *dm = d.get();
+    o.A = [dm](double *out, const double *x) {
+        std::lock_guard<std::mutex> lk(dm->mtx);
+        dm->apply0(out, x);
+    };
+    o.resid = [dm](double *r, const double *b, const double *x) {
+        std::lock_guard<std::mutex> lk(dm->mtx);
+        dm->residual0(b, x, r);
+    };
+    if (precondition) o.M = [dm](double *out, const double *r) { dm->apply(out, r); };
+    auto red = std::make_shared<DevBuf<double>>(1);
+    o.dot = [dm, red](const double *u, const double *w) {
+        Ctx &ctx = *dm->ctx;
+        hipStream_t s = ctx.stream;
+        vec_dot_dev(u, w, dm->nrows, red->get(), ctx);
+        dm->tr->allreduce(red->get(), 1, false, s);
+        double h = 0;
+        FAMG_CHECK_HIP(hipMemcpyAsync(&h, red->get(), 8, hipMemcpyDeviceToHost, s));
+        FAMG_CHECK_HIP(hipStreamSynchronize(s));
+        return h;
+    };
+    return o;
+}
+
 amg_status amg_dist_stationary_solve(amg_linop *dist_mg, const double *b, double *x, int64_t max_iter,
                                      double rel_tol, double *hist, int64_t *iters) {
     return dguard([&] {
         auto d = need_dist(dist_mg);
         FAMG_REQUIRE(b && x && iters && max_iter > 0, AMG_ERR_INVALID, "bad argument");
-        Ctx &ctx = *d->ctx;
-        ctx.set_device();
-        hipStream_t s = ctx.stream;
-        const int64_t n = d->nrows;
-        DevBuf<double> r(std::max<int64_t>(1, n)), z(std::max<int64_t>(1, n)), red(1);
-        auto gdot = [&](const double *u, const double *w) {
-            vec_dot_dev(u, w, n, red.get(), ctx);
-            d->tr->allreduce(red.get(), 1, false, s);
-            double h = 0;
-            FAMG_CHECK_HIP(hipMemcpyAsync(&h, red.get(), 8, hipMemcpyDeviceToHost, s));
-            FAMG_CHECK_HIP(hipStreamSynchronize(s));
-            return h;
-        };
-        const double bn = std::sqrt(gdot(b, b));
-        int64_t it = 0;
-        for (;;) {
-            {
-                std::lock_guard<std::mutex> lk(d->mtx);
-                d->residual0(b, x, r.get());
-            }
-            const double rel = std::sqrt(gdot(r.get(), r.get())) / bn;
-            it++;
-            if (hist) hist[it - 1] = rel;
-            if (rel < rel_tol || it >= max_iter) break;
-            d->apply(z.get(), r.get());
-            vec_add_inplace(x, z.get(), n, s);
-        }
-        FAMG_CHECK_HIP(hipStreamSynchronize(s));
-        *iters = it;
+        d->ctx->set_device();
+        *iters = stationary_impl(dist_ops(d, true), b, x, max_iter, rel_tol, hist);
+    });
+}
+
+amg_status amg_dist_pcg_solve(amg_linop *dist_mg, int32_t precondition, const double *b, double *x,
+                              int64_t max_iter, double rel_tol, double abs_tol, double *hist, int64_t *iters) {
+    return dguard([&] {
+        auto d = need_dist(dist_mg);
+        FAMG_REQUIRE(b && x && iters && max_iter >= 0, AMG_ERR_INVALID, "bad argument");
+        d->ctx->set_device();
+        *iters = pcg_impl(dist_ops(d, precondition != 0), b, x, max_iter, rel_tol, abs_tol, hist);
     });
 }
 

@@ -138,7 +138,8 @@ enum class Kind : int {
     Coarse = AMG_KIND_COARSE,
     Multigrid = AMG_KIND_MULTIGRID,
     DistCsr = AMG_KIND_DIST_CSR,
-    DistMultigrid = AMG_KIND_DIST_MULTIGRID
+    DistMultigrid = AMG_KIND_DIST_MULTIGRID,
+    Composite = AMG_KIND_COMPOSITE
 };
 
 struct LinOp : std::enable_shared_from_this<LinOp> {

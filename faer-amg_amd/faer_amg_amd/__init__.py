@@ -89,6 +89,9 @@ SIGNATURES = {
     "amg_sa_build_box": (i32, [vp, i64, i64, i64, i64, i64, i64, i64, i64, dbl, i32, P(vp)]),
     "amg_stationary_solve": (i32, [vp, vp, vp, vp, i64, dbl, vp, P(i64)]),
     "amg_pcg_solve": (i32, [vp, vp, vp, vp, i64, dbl, dbl, vp, P(i64)]),
+    "amg_composite_create": (i32, [vp, vp, i64, P(vp)]),
+    "amg_composite_push": (i32, [vp, vp]),
+    "amg_composite_ncomponents": (i32, [vp, P(i64)]),
     "amg_comm_unique_id_size": (i32, []),
     "amg_comm_get_unique_id": (i32, [vp]),
     "amg_comm_create": (i32, [vp, i32, i32, vp, P(vp)]),
@@ -120,6 +123,7 @@ SIGNATURES = {
     "amg_mfem_index_maps": (i32, [vp, vp, vp]),
     "amg_mfem_destroy": (i32, [vp]),
     "amg_dist_stationary_solve": (i32, [vp, vp, vp, i64, dbl, vp, P(i64)]),
+    "amg_dist_pcg_solve": (i32, [vp, i32, vp, vp, i64, dbl, dbl, vp, P(i64)]),
 }
 
 for _name, (_res, _args) in SIGNATURES.items():
@@ -554,6 +558,28 @@ def pcg_solve(A, M, b, x, max_iter=1000, rel_tol=1e-8, abs_tol=0.0):
     return it.value, hist[:min(it.value, max_iter)]
 
 
+class Composite(LinOp):
+    """Composite (preconditioners/composite.rs): components c_0..c_{m-1} applied
+    c_{m-1}..c_1, c_0, c_1..c_{m-1}, each step out += c(r); r = rhs - A out."""
+
+    def __init__(self, A, components):
+        comps = list(components)
+        arr = (vp * len(comps))(*[c.h for c in comps])
+        h = vp()
+        _ck(_lib.amg_composite_create(A.h, arr, len(comps), C.byref(h)))
+        super().__init__(h, A.ctx, refs=(A, *comps))
+
+    def push(self, component):
+        _ck(_lib.amg_composite_push(self.h, component.h))
+        self._refs = tuple(self._refs) + (component,)
+        return self
+
+    def ncomponents(self):
+        v = i64()
+        _ck(_lib.amg_composite_ncomponents(self.h, C.byref(v)))
+        return v.value
+
+
 # ------------------------------------------------------------------ multi-GPU
 
 def unique_id():
@@ -655,6 +681,16 @@ class DistMultigrid(LinOp):
         """Overlap halo exchanges with the interior rows of their SpMV (default on)."""
         _ck(_lib.amg_dist_set_option(self.h, 0, 1 if on else 0))
         return self
+
+    def pcg_solve(self, b, x, max_iter=1000, rel_tol=1e-8, abs_tol=0.0, precondition=True):
+        """Distributed PCG (dots all-reduced), one distributed V-cycle per iteration."""
+        hist = np.zeros(max(max_iter, 1))
+        it = i64()
+        with _ordered(self.ctx, AMG_MEM_DEVICE):
+            _ck(_lib.amg_dist_pcg_solve(self.h, 1 if precondition else 0, vp(b.data_ptr()),
+                                        vp(x.data_ptr()), max_iter, rel_tol, abs_tol,
+                                        hist.ctypes.data_as(vp), C.byref(it)))
+        return it.value, hist[:min(it.value, max_iter)]
 
     def stationary_solve(self, b, x, max_iter=100, rel_tol=1e-8):
         hist = np.zeros(max_iter)

@@ -51,7 +51,8 @@ typedef enum amg_linop_kind {
     AMG_KIND_COARSE = 3,    /* coarse Cholesky solve */
     AMG_KIND_MULTIGRID = 4, /* Multigrid */
     AMG_KIND_DIST_CSR = 5,  /* row-block distributed sparse matrix */
-    AMG_KIND_DIST_MULTIGRID = 6
+    AMG_KIND_DIST_MULTIGRID = 6,
+    AMG_KIND_COMPOSITE = 7  /* Composite (preconditioners/composite.rs) */
 } amg_linop_kind;
 
 typedef struct amg_ctx amg_ctx;
@@ -221,6 +222,15 @@ amg_status amg_multigrid_get_level(const amg_linop *mg, int64_t level, amg_linop
 
 /* ---- solve drivers (the callers of the hot path) ------- */
 
+/* Composite (preconditioners/composite.rs:11-83) as a LinOp/Precond on A:
+ * components c_0..c_{m-1} are applied c_{m-1},...,c_1,c_0,c_1,...,c_{m-1}
+ * (2m-1 steps), each step out += c(r); r = rhs - A out, from out = 0 and
+ * r = rhs.  Components are any preconditioning handles (apply_in_place). */
+amg_status amg_composite_create(const amg_linop *A, amg_linop *const *components,
+                                int64_t ncomponents, amg_linop **out);
+/* Composite::push */
+amg_status amg_composite_push(amg_linop *composite, const amg_linop *component);
+amg_status amg_composite_ncomponents(const amg_linop *composite, int64_t *n);
 /* Stationary solver of examples/simple_geometric.rs:117-158 on device vectors:
  * loop { r = b - A x; rho = ||r||/||b||; hist[it] = rho; stop if rho < rel_tol or
  * it+1 >= max_iter; x += M r }.  b, x device pointers (n); hist host (max_iter).
@@ -293,6 +303,13 @@ amg_status amg_dist_set_option(amg_linop *dist, int32_t option, int64_t value);
 amg_status amg_dist_stationary_solve(amg_linop *dist_mg, const double *b, double *x,
                                      int64_t max_iter, double rel_tol, double *hist,
                                      int64_t *iters);
+/* Distributed PCG on the finest distributed operator, preconditioned by one
+ * distributed V-cycle per iteration (precondition = 0: plain CG): the same loop
+ * as amg_pcg_solve with every dot all-reduced over the ranks;
+ * b, x local (owned rows). */
+amg_status amg_dist_pcg_solve(amg_linop *dist_mg, int32_t precondition, const double *b, double *x,
+                              int64_t max_iter, double rel_tol, double abs_tol, double *hist,
+                              int64_t *iters);
 
 /* ---- Dataset loaders (utils.rs:269-534) -------------------
  * Host-side; no device needed.  Matrix Market: sparse coordinate files

@@ -321,6 +321,21 @@ def pcg_solve(A, b, mg=None, diag=None, x0=None, max_iter=1000, rel_tol=1e-8, ab
     return x, int(it), hist[:min(it, max_iter)]
 
 
+def composite_apply(A, components, rhs):
+    """Composite::implementation (preconditioners/composite.rs:66-83): out = 0,
+    ws = rhs; for c in c_{m-1}..c_0 then c_1..c_{m-1}: ws = c(ws) (apply_in_place),
+    out += ws, ws = rhs - A out.  components: callables r -> c(r)."""
+    rhs = np.ascontiguousarray(rhs, np.float64)
+    out = np.zeros_like(rhs)
+    ws = rhs.copy()
+    m = len(components)
+    for k in list(range(m - 1, -1, -1)) + list(range(1, m)):
+        ws = components[k](ws)
+        out = out + ws
+        ws = rhs - A.spmv(out)
+    return out
+
+
 def sa_hierarchy_box(A, dims, box=(2, 2, 2), coarsest_dim=1000, max_levels=None,
                      omega=0.66, nn_iters=3, nn=None):
     """Hierarchy::coarsen restated (hierarchy.rs:190-248) for structured grids.

@@ -170,3 +170,48 @@ def test_dist_overlap_is_bitwise_neutral(split_kind):
     assert np.array_equal(z_on, z_off)
     for a, c in zip(res_on, res_off):
         assert np.array_equal(a[4], c[4])
+
+
+@pytest.mark.parametrize("nranks,agglo", [(2, 100), (3, 1 << 30)])
+def test_dist_pcg_matches_single_gpu(nranks, agglo):
+    """Distributed PCG (dots all-reduced, one distributed V-cycle per iteration)
+    against the single-GPU PCG on the same hierarchy: iteration counts equal or
+    +-1 (dot rounding differs), residual histories to 1e-8, and the assembled
+    solution solves the global system."""
+    import torch
+    dims = (16, 12, 20)
+    n = int(np.prod(dims))
+    b = np.random.default_rng(17).uniform(-1, 1, n)
+    ctx = fa().Context(0)
+    A = fa().SparseMatOp.laplace3d_7pt(ctx, *dims)
+    mg = fa().sa_build_box(A, dims, (2, 2, 2), coarsest_dim=60)
+    bd = torch.as_tensor(b, device="cuda:0")
+    x = torch.zeros_like(bd)
+    it1, h1 = fa().pcg_solve(A, mg, bd, x, max_iter=100, rel_tol=1e-10)
+    ctx.synchronize()
+    hub = fa().LoopbackHub(nranks)
+
+    def rank_fn(r):
+        c = fa().Context(0)
+        Ar = fa().SparseMatOp.laplace3d_7pt(c, *dims)
+        mr = fa().sa_build_box(Ar, dims, (2, 2, 2), coarsest_dim=60)
+        splits = fa().slab_splits(fa().box_level_dims(dims, (2, 2, 2), mr.levels()), nranks)
+        dm = fa().DistMultigrid(fa().Comm(c, hub=hub, rank=r), mr, splits, agglomerate_rows=agglo)
+        r0, r1 = dm.local_rows()
+        bl = torch.as_tensor(np.ascontiguousarray(b[r0:r1]), device="cuda:0")
+        xl = torch.zeros_like(bl)
+        it, hist = dm.pcg_solve(bl, xl, max_iter=100, rel_tol=1e-10)
+        itc, _ = dm.pcg_solve(bl, torch.zeros_like(bl), max_iter=2000, rel_tol=1e-6, precondition=False)
+        c.synchronize()
+        return r0, r1, xl.cpu().numpy(), it, hist, itc
+
+    res = run_ranks(nranks, rank_fn)
+    xs = np.zeros(n)
+    for r0, r1, xl, it, hist, itc in res:
+        xs[r0:r1] = xl
+        assert abs(it - it1) <= 1, (it, it1)
+        m = min(len(hist), len(h1))
+        assert np.allclose(hist[:m], h1[:m], rtol=1e-8, atol=1e-14)
+        assert itc > it  # plain CG needs far more iterations
+    OA = O.laplace3d_7pt(*dims)
+    assert np.linalg.norm(b - OA.spmv(xs)) <= 1e-9 * np.linalg.norm(b)

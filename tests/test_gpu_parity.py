@@ -12,6 +12,7 @@ import numpy as np
 import pytest
 import scipy.sparse as sp
 
+import np_oracle as N
 import oracle as O
 
 pytestmark = pytest.mark.gpu
@@ -468,3 +469,52 @@ def test_c1_gmg2d_stationary_and_pcg(ctx):
     x.zero_()
     it, _ = fa().pcg_solve(ops["A0"], mg, b, x, max_iter=6000, rel_tol=1e-8)
     assert abs(it - int(g["pcg_iters"][0])) <= 1
+
+
+# ------------------------------------------------------------------ Composite
+
+def test_composite_diag_components_bitwise(ctx):
+    """Composite(A, [Jacobi, L1]) = L1, Jacobi, L1 steps of out += c(r);
+    r = rhs - A out: every piece is bitwise (one-lane SpMV rows, diag scaling,
+    elementwise add), so the whole apply is bitwise equal to the restatement."""
+    OA = O.laplace3d_7pt(18, 14, 10)
+    A = gpu_csr(ctx, OA)
+    J, L = fa().new_jacobi(A, 0.66), fa().new_l1(A)
+    Cp = fa().Composite(A, [J, L])
+    assert Cp.ncomponents() == 2
+    dj, dl = O.jacobi_diag(OA, 0.66), O.l1_diag(OA)
+    b = np.random.default_rng(31).uniform(-1, 1, OA.nrows)
+    z = apply_dev(ctx, Cp, b, OA.nrows)
+    zref = O.composite_apply(OA, [lambda r: dj * r, lambda r: dl * r], b)
+    assert np.array_equal(z, zref)
+    Cp.push(J)  # Composite::push -> J, L, J, L, J
+    z3 = apply_dev(ctx, Cp, b, OA.nrows)
+    zref3 = O.composite_apply(OA, [lambda r: dj * r, lambda r: dl * r, lambda r: dj * r], b)
+    assert np.array_equal(z3, zref3)
+
+
+def test_composite_multigrid_and_pcg(ctx):
+    """Composite(A, [V-cycle, Jacobi]) against the restatement (1e-11, the
+    V-cycle tolerance), then as the PCG preconditioner: iteration count equal
+    or +-1 to the restatement's PCG with the same preconditioner."""
+    import torch
+    dims = (16, 14, 12)
+    A = fa().SparseMatOp.laplace3d_7pt(ctx, *dims)
+    mg = fa().sa_build_box(A, dims, (2, 2, 2), coarsest_dim=100)
+    J = fa().new_jacobi(A, 0.66)
+    Cp = fa().Composite(A, [mg, J])
+    OA = O.Csr.from_arrays(*A.dims(), *A.arrays())
+    omg = O.Multigrid(oracle_levels_from_gpu(mg, "jacobi"))
+    dj = O.jacobi_diag(OA, 0.66)
+    comps = [omg.apply, lambda r: dj * r]
+    b = np.random.default_rng(32).uniform(-1, 1, OA.nrows)
+    z = apply_dev(ctx, Cp, b, OA.nrows)
+    zref = O.composite_apply(OA, comps, b)
+    assert np.linalg.norm(z - zref) <= 1e-11 * np.linalg.norm(zref)
+    bd = T(b)
+    x = torch.zeros_like(bd)
+    it, hist = fa().pcg_solve(A, Cp, bd, x, max_iter=200, rel_tol=1e-10)
+    _, it_ref = N.pcg(OA.to_scipy(), b, lambda r: O.composite_apply(OA, comps, r), 200, 1e-10)
+    assert abs(it - it_ref) <= 1, (it, it_ref)
+    xr = H(x)
+    assert np.linalg.norm(b - OA.spmv(xr)) <= 1e-9 * np.linalg.norm(b)
