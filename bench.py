@@ -102,7 +102,7 @@ def weak_dims(n, N):
     return tuple(d)
 
 
-def cpu_baseline(mg, b, threads, budget_s=12.0, max_cycles=40):
+def cpu_baseline(mg, b, threads, smoother="jacobi", budget_s=12.0, max_cycles=40):
     """The reference's rayon path restated (oracle: ParSpmmOp 8192x8192 CSC tiles,
     usize indices, per-call temporaries) on the same hierarchy."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
@@ -111,9 +111,17 @@ def cpu_baseline(mg, b, threads, budget_s=12.0, max_cycles=40):
     levels = []
     nl = mg.levels()
     for l in range(nl):
-        Al, _, Rl, Pl = mg.level(l)
-        d = {"A": O.Csr.from_arrays(*Al.dims(), *Al.arrays()),
-             "smoother": "chol" if l == nl - 1 else "jacobi"}
+        Al, Sl, Rl, Pl = mg.level(l)
+        kind = Sl.kind
+        if l == nl - 1:
+            sm = "chol"
+        elif kind == "sgs":
+            sm = "sgs"
+        elif kind == "diag":
+            sm = "jacobi" if smoother == "jacobi" else "l1"
+        else:
+            raise NotImplementedError(f"no CPU restatement of the {kind} smoother in the C oracle")
+        d = {"A": O.Csr.from_arrays(*Al.dims(), *Al.arrays()), "smoother": sm}
         if Rl is not None:
             d["R"] = O.Csr.from_arrays(*Rl.dims(), *Rl.arrays())
             d["P"] = O.Csr.from_arrays(*Pl.dims(), *Pl.arrays())
@@ -239,7 +247,7 @@ def run_single(args):
     cpu = None
     if not args.no_cpu_baseline:
         try:
-            v, cyc, dt = cpu_baseline(mg, b_host, args.cpu_threads)
+            v, cyc, dt = cpu_baseline(mg, b_host, args.cpu_threads, args.smoother)
             cpu = {"value": round(v, 4), "unit": "V-cycles/s", "cores": args.cpu_threads,
                    "kind": "port",
                    "sample": f"{cyc} V-cycles of the same {args.edge}^3 hierarchy in {dt:.1f}s "
@@ -397,7 +405,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--edge", type=int, default=256, help="grid edge per GPU")
     ap.add_argument("--box", type=int, default=2)
-    ap.add_argument("--smoother", default="jacobi", choices=["jacobi", "l1", "sgs"])
+    ap.add_argument("--smoother", default="jacobi", choices=["jacobi", "l1", "sgs", "block"])
     ap.add_argument("--problem", default="7pt", choices=["7pt", "27pt"])
     ap.add_argument("--agglomerate", type=int, default=8192,
                     help="levels with fewer global rows run redundantly on every rank")

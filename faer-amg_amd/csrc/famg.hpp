@@ -139,7 +139,8 @@ enum class Kind : int {
     Multigrid = AMG_KIND_MULTIGRID,
     DistCsr = AMG_KIND_DIST_CSR,
     DistMultigrid = AMG_KIND_DIST_MULTIGRID,
-    Composite = AMG_KIND_COMPOSITE
+    Composite = AMG_KIND_COMPOSITE,
+    Block = AMG_KIND_BLOCK
 };
 
 struct LinOp : std::enable_shared_from_this<LinOp> {
@@ -261,6 +262,26 @@ CsrPtr transpose_op(const CsrOp &P);
 CsrPtr spgemm_op(const CsrOp &A, const CsrOp &B);
 void nn_stationary_l1(CsrOp &A, int64_t iters, double *x_host);
 int64_t greedy_coloring(const GpuCsr &A, std::vector<int32_t> &color);
+// BlockSmoother apply data: blocks in block-major row order, explicit inverses
+// (column-major), chunks of <= 256 rows of whole blocks (block.hip).
+struct BlockSmootherOp : LinOp {
+    int64_t nblocks = 0, vdim = 1, max_block = 0, nchunks = 0;
+    std::vector<int64_t> h_bptr;   // host copies (to_csr)
+    std::vector<int32_t> h_rows;
+    DevBuf<int32_t> rows;          // block-major original row ids (n)
+    DevBuf<int32_t> blk_of;        // block of each block-major position (n)
+    DevBuf<int64_t> bptr;          // nblocks+1
+    DevBuf<int64_t> ioff;          // nblocks+1 offsets of the inverses
+    DevBuf<int32_t> chunk;         // nchunks+1 position bounds (block aligned)
+    DevBuf<double> inv;
+    Kind kind() const override { return Kind::Block; }
+    bool is_precond() const override { return true; }
+    void apply(double *out, const double *rhs) override;
+    void apply_in_place(double *rhs) override { apply(rhs, rhs); }
+};
+// BlockSmoother (block_smoothers.rs:80-291) over a node partition (ids 0..nagg-1,
+// n/vdim nodes); blocks diagonally compensated and inverted exactly (block.hip).
+std::shared_ptr<BlockSmootherOp> make_block_smoother(CsrOp &A, const int64_t *part, int64_t nagg, int64_t vdim);
 std::shared_ptr<MultigridOp> sa_build_box(const CsrPtr &A, int64_t nx, int64_t ny, int64_t nz,
                                           int64_t bx, int64_t by, int64_t bz,
                                           int64_t coarsest_dim, int64_t max_levels,

@@ -623,6 +623,8 @@ std::shared_ptr<MultigridOp> sa_build_box(const CsrPtr &A, int64_t nx, int64_t n
     std::vector<double> nn(A->nrows, 1.0);
     int64_t cx = nx, cy = ny, cz = nz;
     int64_t level = 1, coarse_dim = -1;
+    std::vector<std::vector<int64_t>> aggs;  // per coarsened level (block smoother partition)
+    std::vector<int64_t> naggs;
     while ((coarse_dim < 0 || coarse_dim > coarsest_dim) && level < max_levels) {
         CsrPtr cur = As.back();
         const int64_t n = cur->nrows;
@@ -639,6 +641,10 @@ std::shared_ptr<MultigridOp> sa_build_box(const CsrPtr &A, int64_t nx, int64_t n
         CsrPtr R = transpose_op(*P);
         CsrPtr Ac = galerkin_rap(*R, *cur, *P);
         nn_stationary_l1(*Ac, 3, cnn.data());
+        if (smoother == 3) {
+            aggs.push_back(agg);
+            naggs.push_back(na);
+        }
         Rs.push_back(R);
         Ps.push_back(P);
         As.push_back(Ac);
@@ -647,7 +653,7 @@ std::shared_ptr<MultigridOp> sa_build_box(const CsrPtr &A, int64_t nx, int64_t n
         coarse_dim = Ac->nrows;
         level++;
     }
-    auto make_smoother = [&](const CsrPtr &M) -> LinOpPtr {
+    auto make_smoother = [&](const CsrPtr &M, size_t l) -> LinOpPtr {
         switch (smoother) {
         case 0: return make_jacobi(*M, omega);
         case 1: return make_l1(*M);
@@ -660,6 +666,8 @@ std::shared_ptr<MultigridOp> sa_build_box(const CsrPtr &A, int64_t nx, int64_t n
             if (nc <= SGS_MAX_COLORS) return make_sgs(M, colors.data(), false);
             return make_l1(*M);
         }
+        case 3:  // BlockSmoother over the level's box aggregates (block_smoothers.rs)
+            return make_block_smoother(*M, aggs[l].data(), naggs[l], 1);
         default: fail(AMG_ERR_INVALID, "unknown smoother kind");
         }
     };
@@ -668,10 +676,10 @@ std::shared_ptr<MultigridOp> sa_build_box(const CsrPtr &A, int64_t nx, int64_t n
     mg->nrows = mg->ncols = A->nrows;
     MgLevel L0;
     L0.A = A;
-    L0.S = As.size() == 1 ? LinOpPtr(make_coarse_chol(*A)) : make_smoother(A);
+    L0.S = As.size() == 1 ? LinOpPtr(make_coarse_chol(*A)) : make_smoother(A, 0);
     mg->levels.push_back(std::move(L0));
     for (size_t l = 1; l < As.size(); l++) {
-        LinOpPtr S = (l + 1 == As.size()) ? LinOpPtr(make_coarse_chol(*As[l])) : make_smoother(As[l]);
+        LinOpPtr S = (l + 1 == As.size()) ? LinOpPtr(make_coarse_chol(*As[l])) : make_smoother(As[l], l);
         mg->add_level(As[l], S, Rs[l - 1], Ps[l - 1]);
     }
     return mg;

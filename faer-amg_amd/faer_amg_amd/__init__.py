@@ -38,7 +38,7 @@ P = C.POINTER
 
 AMG_MEM_HOST, AMG_MEM_DEVICE = 0, 1
 KINDS = {0: "csr", 1: "diag", 2: "sgs", 3: "coarse", 4: "multigrid", 5: "dist_csr",
-         6: "dist_multigrid"}
+         6: "dist_multigrid", 7: "composite", 8: "block"}
 
 # name -> (restype, argtypes); every exported symbol of include/amg.h
 SIGNATURES = {
@@ -90,6 +90,8 @@ SIGNATURES = {
     "amg_stationary_solve": (i32, [vp, vp, vp, vp, i64, dbl, vp, P(i64)]),
     "amg_pcg_solve": (i32, [vp, vp, vp, vp, i64, dbl, dbl, vp, P(i64)]),
     "amg_composite_create": (i32, [vp, vp, i64, P(vp)]),
+    "amg_block_smoother_create": (i32, [vp, vp, i64, i64, P(vp)]),
+    "amg_block_smoother_to_csr": (i32, [vp, P(vp)]),
     "amg_composite_push": (i32, [vp, vp]),
     "amg_composite_ncomponents": (i32, [vp, P(i64)]),
     "amg_comm_unique_id_size": (i32, []),
@@ -526,7 +528,7 @@ def nn_stationary_l1(A, x, iters=3):
     return x
 
 
-SMOOTHERS = {"jacobi": 0, "l1": 1, "sgs": 2}
+SMOOTHERS = {"jacobi": 0, "l1": 1, "sgs": 2, "block": 3}
 
 
 def sa_build_box(A, dims, box=(2, 2, 2), coarsest_dim=1000, max_levels=0, omega=0.66,
@@ -556,6 +558,25 @@ def pcg_solve(A, M, b, x, max_iter=1000, rel_tol=1e-8, abs_tol=0.0):
                                vp(x.data_ptr()), max_iter, rel_tol, abs_tol,
                                hist.ctypes.data_as(vp), C.byref(it)))
     return it.value, hist[:min(it.value, max_iter)]
+
+
+class BlockSmoother(LinOp):
+    """BlockSmoother (block_smoothers.rs:80-291): block Jacobi over a node
+    partition, diagonally compensated blocks solved exactly."""
+
+    def __init__(self, A, node_partition, naggregates=None, block_size=1):
+        part = np.ascontiguousarray(node_partition, np.int64)
+        nagg = int(part.max()) + 1 if naggregates is None else int(naggregates)
+        h = vp()
+        _ck(_lib.amg_block_smoother_create(A.h, part.ctypes.data_as(vp), nagg, int(block_size),
+                                           C.byref(h)))
+        super().__init__(h, A.ctx, refs=(A,))
+
+    def to_sparse(self):
+        """BlockSmoother::into_sparse_mat: the block-diagonal inverse as a SparseMatOp."""
+        h = vp()
+        _ck(_lib.amg_block_smoother_to_csr(self.h, C.byref(h)))
+        return SparseMatOp(h, self.ctx)
 
 
 class Composite(LinOp):

@@ -52,7 +52,8 @@ typedef enum amg_linop_kind {
     AMG_KIND_MULTIGRID = 4, /* Multigrid */
     AMG_KIND_DIST_CSR = 5,  /* row-block distributed sparse matrix */
     AMG_KIND_DIST_MULTIGRID = 6,
-    AMG_KIND_COMPOSITE = 7  /* Composite (preconditioners/composite.rs) */
+    AMG_KIND_COMPOSITE = 7, /* Composite (preconditioners/composite.rs) */
+    AMG_KIND_BLOCK = 8      /* BlockSmoother (preconditioners/block_smoothers.rs) */
 } amg_linop_kind;
 
 typedef struct amg_ctx amg_ctx;
@@ -210,8 +211,9 @@ amg_status amg_nn_stationary_l1(const amg_linop *A, int64_t iters, double *x);
  * aggregates and one constant candidate (Hierarchy::coarsen, hierarchy.rs:190-248,
  * box aggregates standing in for the modularity partitioner -- DESIGN.md).
  * Coarsens until the coarse size <= coarsest_dim or max_levels (0 = unlimited).
- * smoother: 0 Jacobi(omega), 1 L1, 2 SGS (greedy coloring) on every level but
- * the coarsest, which gets the Cholesky coarse solve.  Returns the multigrid. */
+ * smoother: 0 Jacobi(omega), 1 L1, 2 SGS (greedy coloring; L1 on levels needing
+ * > 32 colors), 3 BlockSmoother over the level's box aggregates, on every level
+ * but the coarsest, which gets the Cholesky coarse solve.  Returns the multigrid. */
 amg_status amg_sa_build_box(amg_linop *A, int64_t nx, int64_t ny, int64_t nz, int64_t bx,
                             int64_t by, int64_t bz, int64_t coarsest_dim, int64_t max_levels,
                             double omega, int32_t smoother, amg_linop **mg_out);
@@ -222,6 +224,17 @@ amg_status amg_multigrid_get_level(const amg_linop *mg, int64_t level, amg_linop
 
 /* ---- solve drivers (the callers of the hot path) ------- */
 
+/* BlockSmoother (block_smoothers.rs:80-291), BlockSolver(Cholesky) kind:
+ * block Jacobi over a partition of the n/block_size nodes (node_partition[i] in
+ * 0..naggregates-1); each block is the aggregate's submatrix with the
+ * couplings leaving it folded into its diagonal (diagonally_compensate
+ * :293-324; block_size > 1: diagonally_compensate_vector :326-400) and is
+ * solved exactly (dense LL^T inverse per block, <= 8192 rows per block).
+ * AMG_ERR_NOT_SPD if a compensated block is not SPD. */
+amg_status amg_block_smoother_create(const amg_linop *A, const int64_t *node_partition,
+                                     int64_t naggregates, int64_t block_size, amg_linop **out);
+/* BlockSmoother::into_sparse_mat (:122-146): the block-diagonal inverse as CSR. */
+amg_status amg_block_smoother_to_csr(const amg_linop *bs, amg_linop **out);
 /* Composite (preconditioners/composite.rs:11-83) as a LinOp/Precond on A:
  * components c_0..c_{m-1} are applied c_{m-1},...,c_1,c_0,c_1,...,c_{m-1}
  * (2m-1 steps), each step out += c(r); r = rhs - A out, from out = 0 and

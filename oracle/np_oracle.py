@@ -120,7 +120,9 @@ class Multigrid:
             A = lev["A"].tocsr()
             kind = lev.get("smoother", "jacobi")
             d = A.diagonal()
-            if kind == "jacobi":
+            if callable(kind):                      # any Precond r -> M r
+                self.sm.append(("fn", kind))
+            elif kind == "jacobi":
                 self.sm.append(("diag", omega / d))
             elif kind == "l1":
                 self.sm.append(("diag", 1.0 / np.asarray(abs(A).sum(axis=1)).ravel()))
@@ -134,6 +136,8 @@ class Multigrid:
 
     def _pc(self, l, r):
         kind, data = self.sm[l]
+        if kind == "fn":
+            return data(r)
         if kind == "diag":
             return data * r
         if kind == "chol":
@@ -363,3 +367,53 @@ def load_mfem(directory, name, delete_boundary=True):
         A.sort_indices()
     C = np.asarray([coords[i] for i in sel]) if len(sel) else np.zeros((0, 0))
     return A, rhs_full[sel], C, np.asarray(boundary, np.int64), sel.astype(np.int64), m2s
+
+
+# ------------------------------------------------------------ block smoother
+
+def block_smoother(A, node_partition, block_size=1):
+    """BlockSmoother with BlockSolver(Cholesky) blocks (block_smoothers.rs:80-291):
+    returns r -> M r.  Blocks: aggregates' nodes ascending (BTreeSet order),
+    diagonally compensated (diagonally_compensate :293-324 for block_size 1:
+    a_ii += 0.5 sqrt(a_ii/a_jj) |a_ij| per coupling leaving the aggregate;
+    diagonally_compensate_vector :326-400: node diagonal blocks += 0.5 U S U^T
+    of the SVD of -A_IJ per coupled outside node J), each solved with a dense
+    Cholesky (scipy cho_solve)."""
+    A = A.tocsr()
+    v = int(block_size)
+    part = np.asarray(node_partition, np.int64)
+    nagg = int(part.max()) + 1 if len(part) else 0
+    d = A.diagonal()
+    blocks = []
+    for a in range(nagg):
+        nodes = np.flatnonzero(part == a)
+        if len(nodes) == 0:
+            continue
+        idx = (nodes[:, None] * v + np.arange(v)[None, :]).ravel()
+        pos = {int(g): k for k, g in enumerate(nodes)}
+        B = np.zeros((len(idx), len(idx)))
+        for k, I in enumerate(nodes):
+            outside = set()
+            for oi in range(v):
+                i = I * v + oi
+                for e in range(A.indptr[i], A.indptr[i + 1]):
+                    j = int(A.indices[e])
+                    J, oj = j // v, j % v
+                    if J in pos:
+                        B[k * v + oi, pos[J] * v + oj] += A.data[e]
+                    elif v == 1:
+                        B[k, k] += 0.5 * np.sqrt(d[i] / d[j]) * abs(A.data[e])
+                    else:
+                        outside.add(J)
+            for J in sorted(outside):
+                M = -A[I * v:(I + 1) * v, J * v:(J + 1) * v].toarray()
+                U, S, _ = np.linalg.svd(M)
+                B[k * v:(k + 1) * v, k * v:(k + 1) * v] += 0.5 * (U * S) @ U.T
+        blocks.append((idx, sla.cho_factor(B, lower=True)))
+
+    def apply(r):
+        out = np.zeros(len(r))
+        for idx, f in blocks:
+            out[idx] = sla.cho_solve(f, r[idx])
+        return out
+    return apply
