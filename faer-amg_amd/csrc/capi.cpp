@@ -293,10 +293,39 @@ amg_status amg_linop_dims(const amg_linop *op, int64_t *nrows, int64_t *ncols) {
     });
 }
 
+// k > 1 columns of a CSR operator: one SpMM (the matrix streamed once per 8
+// columns) instead of k SpMVs; host blocks are staged whole.
+static bool csr_multi_apply(LinOp &o, double *out, int64_t ld_out, const double *rhs, int64_t ld_rhs, int64_t k,
+                            amg_mem mem) {
+    auto *c = dynamic_cast<CsrOp *>(&o);
+    if (!c || k <= 1) return false;
+    FAMG_REQUIRE(out && rhs, AMG_ERR_INVALID, "null vector");
+    FAMG_REQUIRE(ld_out >= o.nrows && ld_rhs >= o.ncols, AMG_ERR_INVALID, "leading dimension too small");
+    Ctx &ctx = *o.ctx;
+    ctx.set_device();
+    if (mem == AMG_MEM_DEVICE) {
+        spmm(c->m, rhs, ld_rhs, out, ld_out, k, ctx.stream);
+        return true;
+    }
+    FAMG_REQUIRE(mem == AMG_MEM_HOST, AMG_ERR_INVALID, "bad amg_mem");
+    amg_ctx *ac = ctx_of(o);
+    const int64_t m = std::max<int64_t>(1, o.nrows), n = std::max<int64_t>(1, o.ncols);
+    if (ac->stage_in.size() < (size_t)(n * k)) ac->stage_in.resize(n * k);
+    if (ac->stage_out.size() < (size_t)(m * k)) ac->stage_out.resize(m * k);
+    FAMG_CHECK_HIP(hipMemcpy2DAsync(ac->stage_in.get(), n * sizeof(double), rhs, ld_rhs * sizeof(double),
+                                    o.ncols * sizeof(double), k, hipMemcpyHostToDevice, ctx.stream));
+    spmm(c->m, ac->stage_in.get(), n, ac->stage_out.get(), m, k, ctx.stream);
+    FAMG_CHECK_HIP(hipMemcpy2DAsync(out, ld_out * sizeof(double), ac->stage_out.get(), m * sizeof(double),
+                                    o.nrows * sizeof(double), k, hipMemcpyDeviceToHost, ctx.stream));
+    FAMG_CHECK_HIP(hipStreamSynchronize(ctx.stream));
+    return true;
+}
+
 amg_status amg_linop_apply(amg_linop *op, double *out, int64_t ld_out, const double *rhs,
                            int64_t ld_rhs, int64_t k, amg_mem mem) {
     return guard([&] {
         LinOp &o = need(op);
+        if (csr_multi_apply(o, out, ld_out, rhs, ld_rhs, k, mem)) return;
         for_columns(o, out, ld_out, rhs, ld_rhs, k, mem, o.nrows, o.ncols,
                     [&](double *y, const double *x) { o.apply(y, x); });
     });

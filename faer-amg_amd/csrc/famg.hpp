@@ -98,6 +98,9 @@ struct SpmvEpi {
 
 // y = epilogue(A x) over all rows (seg < 0) or over row segment `seg`, with the
 // kernel chosen for m at finalize (SELL-64 / vector / CSR-stream).
+// Y = A X for k columns (column-major, leading dimensions ldx/ldy): SELL
+// matrices stream once per 8 columns; bitwise equal to k SpMVs.
+void spmm(const GpuCsr &m, const double *x, int64_t ldx, double *y, int64_t ldy, int64_t k, hipStream_t s);
 void spmv(const GpuCsr &m, const double *x, double *y, SpmvMode mode, const SpmvEpi &epi,
           hipStream_t s, int64_t seg = -1);
 

@@ -247,6 +247,75 @@ __global__ __launch_bounds__(256) void spmv_sell_kernel(SellArgs a) {
     if (live) ep.store(a.e, acc);
 }
 
+// SpMM: Y = A X for up to SPMM_KB columns per launch (column-major X, Y with
+// leading dimensions).  The slice is streamed once per column group; each
+// (row, column) sum keeps the SpMV's order (ascending steps, fma), so every
+// column is bitwise equal to a single-column SpMV.
+constexpr int SPMM_KB = 8;
+
+template <int CM, int KB>
+__device__ __forceinline__ void spmm_step4(const double *__restrict__ v, const char *__restrict__ ix,
+                                           const int32_t *__restrict__ bs, int lane, int nu,
+                                           const double *__restrict__ x, int64_t ldx, double (&acc)[KB]) {
+    double vv[4];
+    int32_t cc[4];
+#pragma unroll
+    for (int u = 0; u < 4; u++) {
+        if (u < nu) {
+            vv[u] = __builtin_nontemporal_load(v + u * SELL_C);
+            if constexpr (CM == 0) cc[u] = bs[u] + lane;
+            else if constexpr (CM == 1)
+                cc[u] = bs[u] + (int32_t)__builtin_nontemporal_load(reinterpret_cast<const uint16_t *>(ix) + u * SELL_C);
+            else cc[u] = __builtin_nontemporal_load(reinterpret_cast<const int32_t *>(ix) + u * SELL_C);
+        }
+    }
+#pragma unroll
+    for (int u = 0; u < 4; u++) {
+        if (u < nu) {
+#pragma unroll
+            for (int c = 0; c < KB; c++) acc[c] = fma(vv[u], x[cc[u] + c * ldx], acc[c]);
+        }
+    }
+}
+
+template <int CM, int KB>
+__device__ __forceinline__ void spmm_walk(const double *v, const char *ix, const int32_t *bs, int w, int lane,
+                                          const double *x, int64_t ldx, double (&acc)[KB]) {
+    constexpr int IB = CM == 0 ? 0 : CM == 1 ? 2 : 4;
+    for (int k = 0; k < w; k += 4)
+        spmm_step4<CM, KB>(v + k * SELL_C, ix + (int64_t)k * SELL_C * IB, bs + k, lane, min(4, w - k), x, ldx, acc);
+}
+
+template <int KB>
+__global__ __launch_bounds__(256) void spmm_sell_kernel(SellArgs a, int64_t ldx, double *y, int64_t ldy) {
+    const int blk = xcd_remap(blockIdx.x, gridDim.x);
+    const int sl = __builtin_amdgcn_readfirstlane(blk * 4 + (int)(threadIdx.x >> 6));
+    if (sl >= a.nslices) return;
+    const int slice = a.slice0 + sl;
+    const int lane = threadIdx.x & 63;
+    const int row = a.row0[slice] + lane;
+    const bool live = row < a.row0[slice + 1];
+    const int t0 = a.soff[slice];
+    const int w = a.soff[slice + 1] - t0;
+    const uint32_t d = a.desc[slice];
+    const char *blkp = a.data + (int64_t)(d & 0x3fffffffu) * 128;
+    const double *v = reinterpret_cast<const double *>(blkp) + lane;
+    const char *ix = blkp + (int64_t)w * SELL_VAL_STEP;
+    const int32_t *bs = a.base + t0;
+    double acc[KB];
+#pragma unroll
+    for (int c = 0; c < KB; c++) acc[c] = 0.0;
+    switch (d >> 30) {
+    case 0: spmm_walk<0, KB>(v, nullptr, bs, w, lane, a.e.x, ldx, acc); break;
+    case 1: spmm_walk<1, KB>(v, ix + lane * 2, bs, w, lane, a.e.x, ldx, acc); break;
+    default: spmm_walk<2, KB>(v, ix + lane * 4, bs, w, lane, a.e.x, ldx, acc); break;
+    }
+    if (live) {
+#pragma unroll
+        for (int c = 0; c < KB; c++) y[row + c * ldy] = acc[c];
+    }
+}
+
 // --------------------------------------------------------------------- vector
 
 struct VecArgs {
@@ -515,6 +584,33 @@ void choose_kernel(GpuCsr &m) {
     case SPMV_JACOBI: hipLaunchKernelGGL(KERNEL<SPMV_JACOBI>, grid, block, 0, s, args); break; \
     case SPMV_SGS: hipLaunchKernelGGL(KERNEL<SPMV_SGS>, grid, block, 0, s, args); break;      \
     }
+
+void spmm(const GpuCsr &m, const double *x, int64_t ldx, double *y, int64_t ldy, int64_t k, hipStream_t s) {
+    if (m.kernel != SPMV_KERNEL_SELL) {  // other storages: one SpMV per column
+        for (int64_t c = 0; c < k; c++) spmv(m, x + c * ldx, y + c * ldy, SPMV_SET, SpmvEpi{}, s);
+        return;
+    }
+    if (m.nslices == 0) return;
+    const dim3 grid((unsigned)ceil_div(m.nslices, 4)), block(256);
+    for (int64_t c0 = 0; c0 < k; c0 += SPMM_KB) {
+        const int kb = (int)std::min<int64_t>(SPMM_KB, k - c0);
+        Epi e{x + c0 * ldx, nullptr, nullptr, nullptr, nullptr};
+        SellArgs a{m.sell_row0.get(), m.sell_soff.get(), m.sell_desc.get(), m.sell_base.get(),
+                   m.sell_data.get(), 0, (int32_t)m.nslices, e};
+        double *yc = y + c0 * ldy;
+        switch (kb) {
+        case 1: hipLaunchKernelGGL(spmm_sell_kernel<1>, grid, block, 0, s, a, ldx, yc, ldy); break;
+        case 2: hipLaunchKernelGGL(spmm_sell_kernel<2>, grid, block, 0, s, a, ldx, yc, ldy); break;
+        case 3: hipLaunchKernelGGL(spmm_sell_kernel<3>, grid, block, 0, s, a, ldx, yc, ldy); break;
+        case 4: hipLaunchKernelGGL(spmm_sell_kernel<4>, grid, block, 0, s, a, ldx, yc, ldy); break;
+        case 5: hipLaunchKernelGGL(spmm_sell_kernel<5>, grid, block, 0, s, a, ldx, yc, ldy); break;
+        case 6: hipLaunchKernelGGL(spmm_sell_kernel<6>, grid, block, 0, s, a, ldx, yc, ldy); break;
+        case 7: hipLaunchKernelGGL(spmm_sell_kernel<7>, grid, block, 0, s, a, ldx, yc, ldy); break;
+        default: hipLaunchKernelGGL(spmm_sell_kernel<8>, grid, block, 0, s, a, ldx, yc, ldy); break;
+        }
+        FAMG_CHECK_HIP(hipGetLastError());
+    }
+}
 
 void spmv(const GpuCsr &m, const double *x, double *y, SpmvMode mode, const SpmvEpi &epi,
           hipStream_t s, int64_t seg) {

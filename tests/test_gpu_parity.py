@@ -622,3 +622,40 @@ def test_vcycle_block_smoother(ctx):
     z = apply_dev(ctx, mg, b, A.nrows)
     zref = N.Multigrid(levels).apply(b)
     assert np.linalg.norm(z - zref) <= 1e-11 * np.linalg.norm(zref)
+
+
+# ------------------------------------------------------------ multi-RHS SpMM
+
+def _colmajor(rng, n, k, pad):
+    """(n x k) column-major device matrix with leading dimension n + pad."""
+    import torch
+    base = torch.as_tensor(rng.standard_normal((k, n + pad)), device="cuda:0")
+    return base.T[:n]
+
+
+@pytest.mark.parametrize("fmt", ["auto", "sell"])
+def test_spmm_multi_rhs(ctx, fmt):
+    """k-column apply of a CSR operator (the SpMV generalised to k
+    columns, matrix streamed once per 8 columns): every column bitwise equal
+    to the single-column oracle SpMV for one-lane rows, within the SpMV bound
+    otherwise; leading dimensions > n; k = 1, 3, 8, 13 (column groups 8 + 5)."""
+    rng = np.random.default_rng(51)
+    fa().set_spmv_format(fmt)
+    try:
+        for OA in (O.laplace3d_7pt(40, 20, 10), O.aniso27(16, 14, 9)):
+            A = gpu_csr(ctx, OA)
+            one_lane = A.spmv_info()["kernel"] == "sell"
+            m, n, _ = OA.dims()
+            for k in (1, 3, 8, 13):
+                X = _colmajor(rng, n, k, 5)
+                Y = _colmajor(rng, m, k, 3)
+                A.apply(Y, X)
+                Xh, Yh = H(X), H(Y)
+                for c in range(k):
+                    ref = OA.spmv(np.ascontiguousarray(Xh[:, c]))
+                    if one_lane:
+                        assert np.array_equal(Yh[:, c], ref), (k, c)
+                    else:
+                        assert np.all(np.abs(Yh[:, c] - ref) <= spmv_bound(OA.to_scipy(), Xh[:, c]))
+    finally:
+        fa().set_spmv_format("auto")
