@@ -506,6 +506,7 @@ amg_status amg_multigrid_set_option(amg_linop *mg, int32_t option, int64_t value
         switch (option) {
         case 0: m->use_graph = value != 0; break;
         case 1: m->sgs_residual_form = value != 0; break;
+        case 2: m->fold_zero_guess = value != 0; break;
         default: fail(AMG_ERR_INVALID, "unknown multigrid option");
         }
         m->invalidate_graphs();

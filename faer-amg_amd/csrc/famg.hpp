@@ -49,6 +49,7 @@ struct GpuCsr {
     DevBuf<char> sell_data;
     int64_t nslices = 0, sell_steps = 0, sell_bytes = 0;
     int64_t sell_mode_slices[3] = {0, 0, 0};  // slices per column mode (implicit, u16, i32)
+    bool sell_paired = true;  // step-pair layout (16-B value loads); false: one step per 512-B row
     int kernel = 0;  // SpmvKernel chosen at finalize
     bool spmv_ready() const { return rp32.get() != nullptr && sched.get() != nullptr; }
     bool has_sell() const { return sell_desc.get() != nullptr; }
@@ -87,7 +88,10 @@ enum SpmvMode : int {
     SPMV_ADD = 1,    // y = y + A x
     SPMV_RESID = 2,  // y = b - A x
     SPMV_JACOBI = 3, // y = x + d (b - A x)   (x != y)
-    SPMV_SGS = 4     // e[perm p] = e[perm p] + d_p (b[perm p] - (A e)_p)
+    SPMV_SGS = 4,    // e[perm p] = e[perm p] + d_p (b[perm p] - (A e)_p)
+    // the zero-guess Jacobi step v = d*b folded into its consumers (never stored):
+    SPMV_RESID0 = 5, // y = b - A (d*b)   (x == b; d gathered with x)
+    SPMV_ADD0 = 6    // y = d*b + A x
 };
 
 struct SpmvEpi {
@@ -220,6 +224,9 @@ struct MultigridOp : LinOp {
     int64_t mu = 1, steps = 1;
     bool use_graph = true;
     bool sgs_residual_form = false;  // true: literal smooth() order (residual SpMV + SGS(r))
+    // s = 1 Jacobi levels: fold the first smoothing step from v = 0 (v = d*f)
+    // into the residual (RESID0) and the correction (ADD0) instead of storing it
+    bool fold_zero_guess = true;
     std::mutex mtx;
     Kind kind() const override { return Kind::Multigrid; }
     bool is_precond() const override { return true; }

@@ -451,21 +451,40 @@ void MultigridOp::cycle(int64_t l, double *v, const double *f, bool v_zero, doub
     }
     double *v0 = v;
     double *t = (v == L.t.get()) ? L.v.get() : L.t.get();
-    smooth(l, v, t, f, v_zero);
     auto *A = dynamic_cast<CsrOp *>(L.A.get());
-    if (A) {
+    auto *D = dynamic_cast<DiagOp *>(L.S.get());
+    auto *P = dynamic_cast<CsrOp *>(L.P.get());
+    // One Jacobi step from v = 0 gives v = d*f; with s = 1 nothing else reads
+    // v before the correction, so the residual gathers d*f on the fly and the
+    // correction writes d*f + P v_c: the same rounded values, 16n bytes and one
+    // launch fewer per level.
+    const bool fold = fold_zero_guess && v_zero && steps == 1 && A && D && P;
+    if (fold) {
         SpmvEpi epi;
         epi.b = f;
-        spmv(A->m, v, L.r.get(), SPMV_RESID, epi, s);  // work = f - A v (:341-342)
+        epi.d = D->d.get();
+        spmv(A->m, f, L.r.get(), SPMV_RESID0, epi, s);  // work = f - A (d f)
     } else {
-        L.A->apply(L.r.get(), v);
-        vec_sub(L.r.get(), f, L.r.get(), n, s);
+        smooth(l, v, t, f, v_zero);
+        if (A) {
+            SpmvEpi epi;
+            epi.b = f;
+            spmv(A->m, v, L.r.get(), SPMV_RESID, epi, s);  // work = f - A v (:341-342)
+        } else {
+            L.A->apply(L.r.get(), v);
+            vec_sub(L.r.get(), f, L.r.get(), n, s);
+        }
     }
     MgLevel &C = levels[l + 1];
     L.R->apply(C.f.get(), L.r.get());  // f_c = R work (:343)
     for (int64_t k = 0; k < mu; k++) cycle(l + 1, C.v.get(), C.f.get(), k == 0, nullptr);
-    auto *P = dynamic_cast<CsrOp *>(L.P.get());
-    if (P) {
+    if (fold) {
+        SpmvEpi epi;
+        epi.b = f;
+        epi.d = D->d.get();
+        spmv(P->m, C.v.get(), t, SPMV_ADD0, epi, s);  // v = d f + P v_c
+        std::swap(v, t);                               // (where smooth() would have left v)
+    } else if (P) {
         spmv(P->m, C.v.get(), v, SPMV_ADD, SpmvEpi{}, s);  // v += P v_c (:349-350)
     } else {
         L.P->apply(L.r.get(), C.v.get());

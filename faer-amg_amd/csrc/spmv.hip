@@ -68,16 +68,24 @@ template <int MODE> struct EpiOps {
         i = row;
         if constexpr (MODE == SPMV_SGS) i = a.perm[row];
         if constexpr (MODE == SPMV_JACOBI || MODE == SPMV_SGS) { xr = a.x[i]; br = a.b[i]; dr = a.d[row]; }
-        if constexpr (MODE == SPMV_RESID) br = a.b[row];
+        if constexpr (MODE == SPMV_RESID || MODE == SPMV_RESID0) br = a.b[row];
         if constexpr (MODE == SPMV_ADD) yr = a.y[row];
+        if constexpr (MODE == SPMV_ADD0) yr = a.d[row] * a.b[row];
     }
     __device__ __forceinline__ void store(const Epi &a, double acc) const {
         if constexpr (MODE == SPMV_SET) a.y[i] = acc;
-        else if constexpr (MODE == SPMV_ADD) a.y[i] = yr + acc;
-        else if constexpr (MODE == SPMV_RESID) a.y[i] = br - acc;
+        else if constexpr (MODE == SPMV_ADD || MODE == SPMV_ADD0) a.y[i] = yr + acc;
+        else if constexpr (MODE == SPMV_RESID || MODE == SPMV_RESID0) a.y[i] = br - acc;
         else a.y[i] = xr + dr * (br - acc);  // JACOBI, SGS
     }
 };
+
+// The x operand of a row sum: x[c], or for RESID0 the zero-guess Jacobi
+// iterate d[c]*x[c] -- the same rounded product vec_mul would have stored.
+template <int MODE> __device__ __forceinline__ double gx(const Epi &e, int c) {
+    if constexpr (MODE == SPMV_RESID0) return e.d[c] * e.x[c];
+    else return e.x[c];
+}
 
 // ---------------------------------------------------------------- CSR-stream
 
@@ -104,7 +112,7 @@ __global__ __launch_bounds__(SPMV_BS) void spmv_stream_kernel(StreamArgs a) {
 
     if (nnz > SPMV_CAP) {  // one long row (r1 == r0 + 1): the whole workgroup reduces it
         double acc = 0.0;
-        for (int k = e0 + tid; k < e1; k += SPMV_BS) acc = fma(a.val[k], a.e.x[a.col[k]], acc);
+        for (int k = e0 + tid; k < e1; k += SPMV_BS) acc = fma(a.val[k], gx<MODE>(a.e, a.col[k]), acc);
         for (int off = 32; off > 0; off >>= 1) acc += __shfl_xor(acc, off);
         if ((tid & 63) == 0) sred[tid >> 6] = acc;
         __syncthreads();
@@ -142,7 +150,7 @@ __global__ __launch_bounds__(SPMV_BS) void spmv_stream_kernel(StreamArgs a) {
     if (rl < nrows) {
         const int rs = a.rowptr[r0 + rl] - e0;
         const int re = a.rowptr[r0 + rl + 1] - e0;
-        for (int k = rs + sub; k < re; k += L) acc = fma(sval[vo + k], a.e.x[scol[co + k]], acc);
+        for (int k = rs + sub; k < re; k += L) acc = fma(sval[vo + k], gx<MODE>(a.e, scol[co + k]), acc);
     }
     for (int off = L >> 1; off > 0; off >>= 1) acc += __shfl_xor(acc, off);
     if (rl < nrows && sub == 0) ep.store(a.e, acc);
@@ -154,8 +162,8 @@ __global__ __launch_bounds__(SPMV_BS) void spmv_stream_kernel(StreamArgs a) {
 // slice's block in sell_data is [w_s x 64 fp64 values | column block], the
 // column of lane l at step t given by the slice's column mode:
 //   0 implicit  col = base[t] + l                    (0 B/entry)
-//   1 u16       col = base[t] + d16[t][l]            (2 B/entry)
-//   2 i32       col = c32[t][l]                      (4 B/entry)
+//   1 u16       col = base[t] + d16(t, l)            (2 B/entry)
+//   2 i32       col = c32(t, l)                      (4 B/entry)
 // Steps are either the k-th stored entry of every row ("plain") or, when it is
 // cheaper, the sorted union of the slice's column offsets col - row
 // ("aligned"; a stencil row then reads x[row + offset] for offset t: mode 0
@@ -163,7 +171,23 @@ __global__ __launch_bounds__(SPMV_BS) void spmv_stream_kernel(StreamArgs a) {
 // in-range column, so every row is still summed in its stored (ascending
 // column) order with fma, interleaved with exact +0 terms: bit-identical to the
 // CSR kernels for finite x.
+//
+// Element order inside a block (values, and the u16/i32 column block alike):
+// steps are stored in PAIRS -- step t < 2*floor(w/2) of lane l at element
+// (t & ~1)*64 + 2l + (t & 1) -- so one 16-B load per lane brings the values of
+// two steps (4 B / 8 B for two compressed columns); an odd last step is stored
+// plainly at t*64 + l.  Streamed with 8-B non-temporal loads the values ran at
+// roughly 0.54-0.70x the 16-B rate (MI355X_MICROARCH.md, L2-served loads).
+// `sell_paired = false` keeps one 512-B row per step (A/B switch,
+// FAMG_SELL_LAYOUT=step at build time).
 constexpr int SELL_VAL_STEP = SELL_C * 8;  // bytes of values per step
+
+typedef int32_t i32x2_t __attribute__((ext_vector_type(2)));
+
+__host__ __device__ __forceinline__ int64_t sell_elem(int t, int w, int lane, bool paired) {
+    if (paired && (t | 1) < w) return (int64_t)(t & ~1) * SELL_C + 2 * lane + (t & 1);
+    return (int64_t)t * SELL_C + lane;
+}
 
 struct SellArgs {
     const int32_t *row0;   // nslices+1 (slices tile the rows)
@@ -175,10 +199,11 @@ struct SellArgs {
     Epi e;
 };
 
-template <int CM, int U>
+// ---- one step per 512-B row (sell_paired = false)
+
+template <int MODE, int CM, int U>
 __device__ __forceinline__ void sell_chunk(const double *__restrict__ v, const void *__restrict__ ix,
-                                           const int32_t *__restrict__ bs, int lane,
-                                           const double *__restrict__ x, double &acc) {
+                                           const int32_t *__restrict__ bs, int lane, const Epi &e, double &acc) {
     double vv[U];
     int32_t cc[U];
 #pragma unroll
@@ -191,36 +216,106 @@ __device__ __forceinline__ void sell_chunk(const double *__restrict__ v, const v
     }
     double xx[U];
 #pragma unroll
-    for (int u = 0; u < U; u++) xx[u] = x[cc[u]];
+    for (int u = 0; u < U; u++) xx[u] = gx<MODE>(e, cc[u]);
 #pragma unroll
     for (int u = 0; u < U; u++) acc = fma(vv[u], xx[u], acc);
 }
 
-template <int CM>
-__device__ __forceinline__ double sell_walk(const double *v, const char *ix, const int32_t *bs, int w, int lane,
-                                            const double *x) {
+template <int MODE, int CM>
+__device__ __forceinline__ double sell_walk_steps(const char *blkp, const int32_t *bs, int w, int lane,
+                                                  const Epi &e) {
     constexpr int IB = CM == 0 ? 0 : CM == 1 ? 2 : 4;  // index bytes per entry
+    const double *v = reinterpret_cast<const double *>(blkp) + lane;
+    const char *ix = blkp + (int64_t)w * SELL_VAL_STEP + lane * IB;
     double acc = 0.0;
     int k = 0;
     for (; k + 8 <= w; k += 8)
-        sell_chunk<CM, 8>(v + k * SELL_C, ix + (int64_t)k * SELL_C * IB, bs + k, lane, x, acc);
+        sell_chunk<MODE, CM, 8>(v + k * SELL_C, ix + (int64_t)k * SELL_C * IB, bs + k, lane, e, acc);
     v += k * SELL_C;
     ix += (int64_t)k * SELL_C * IB;
     bs += k;
     switch (w - k) {
-    case 1: sell_chunk<CM, 1>(v, ix, bs, lane, x, acc); break;
-    case 2: sell_chunk<CM, 2>(v, ix, bs, lane, x, acc); break;
-    case 3: sell_chunk<CM, 3>(v, ix, bs, lane, x, acc); break;
-    case 4: sell_chunk<CM, 4>(v, ix, bs, lane, x, acc); break;
-    case 5: sell_chunk<CM, 5>(v, ix, bs, lane, x, acc); break;
-    case 6: sell_chunk<CM, 6>(v, ix, bs, lane, x, acc); break;
-    case 7: sell_chunk<CM, 7>(v, ix, bs, lane, x, acc); break;
+    case 1: sell_chunk<MODE, CM, 1>(v, ix, bs, lane, e, acc); break;
+    case 2: sell_chunk<MODE, CM, 2>(v, ix, bs, lane, e, acc); break;
+    case 3: sell_chunk<MODE, CM, 3>(v, ix, bs, lane, e, acc); break;
+    case 4: sell_chunk<MODE, CM, 4>(v, ix, bs, lane, e, acc); break;
+    case 5: sell_chunk<MODE, CM, 5>(v, ix, bs, lane, e, acc); break;
+    case 6: sell_chunk<MODE, CM, 6>(v, ix, bs, lane, e, acc); break;
+    case 7: sell_chunk<MODE, CM, 7>(v, ix, bs, lane, e, acc); break;
     default: break;
     }
     return acc;
 }
 
-template <int MODE>
+// ---- step pairs (sell_paired = true)
+
+// UP step pairs starting at pair p0, plus the odd last step when TAIL; every
+// load of the group is issued before the dependent x gathers, and the row sum
+// still runs over t ascending.
+template <int MODE, int CM, int UP, bool TAIL>
+__device__ __forceinline__ void sell_pairs(const char *__restrict__ blkp, int w, int p0,
+                                           const int32_t *__restrict__ bs, int lane, const Epi &e, double &acc) {
+    constexpr int NS = 2 * UP + (TAIL ? 1 : 0);
+    double vv[NS];
+    int32_t cc[NS];
+    const char *ixb = blkp + (int64_t)w * SELL_VAL_STEP;
+#pragma unroll
+    for (int u = 0; u < UP; u++) {
+        const int64_t q = (int64_t)(p0 + u) * SELL_C + lane;  // 2-element unit of this lane
+        const dbl2_t v = __builtin_nontemporal_load(reinterpret_cast<const dbl2_t *>(blkp) + q);
+        vv[2 * u] = v.x;
+        vv[2 * u + 1] = v.y;
+        const int t = 2 * (p0 + u);
+        if constexpr (CM == 0) {
+            cc[2 * u] = bs[t] + lane;
+            cc[2 * u + 1] = bs[t + 1] + lane;
+        } else if constexpr (CM == 1) {
+            const uint32_t d = __builtin_nontemporal_load(reinterpret_cast<const uint32_t *>(ixb) + q);
+            cc[2 * u] = bs[t] + (int32_t)(d & 0xffffu);
+            cc[2 * u + 1] = bs[t + 1] + (int32_t)(d >> 16);
+        } else {
+            const i32x2_t d = __builtin_nontemporal_load(reinterpret_cast<const i32x2_t *>(ixb) + q);
+            cc[2 * u] = d.x;
+            cc[2 * u + 1] = d.y;
+        }
+    }
+    if constexpr (TAIL) {
+        const int t = w - 1;
+        const int64_t el = (int64_t)t * SELL_C + lane;
+        vv[NS - 1] = __builtin_nontemporal_load(reinterpret_cast<const double *>(blkp) + el);
+        if constexpr (CM == 0) cc[NS - 1] = bs[t] + lane;
+        else if constexpr (CM == 1)
+            cc[NS - 1] = bs[t] + (int32_t)__builtin_nontemporal_load(reinterpret_cast<const uint16_t *>(ixb) + el);
+        else cc[NS - 1] = __builtin_nontemporal_load(reinterpret_cast<const int32_t *>(ixb) + el);
+    }
+    double xx[NS];
+#pragma unroll
+    for (int u = 0; u < NS; u++) xx[u] = gx<MODE>(e, cc[u]);
+#pragma unroll
+    for (int u = 0; u < NS; u++) acc = fma(vv[u], xx[u], acc);
+}
+
+template <int MODE, int CM>
+__device__ __forceinline__ double sell_walk_pairs(const char *blkp, const int32_t *bs, int w, int lane,
+                                                  const Epi &e) {
+    double acc = 0.0;
+    const int np = w >> 1;
+    int p = 0;
+    for (; p + 4 <= np; p += 4) sell_pairs<MODE, CM, 4, false>(blkp, w, p, bs, lane, e, acc);
+    switch (2 * (np - p) + (w & 1)) {
+    case 1: sell_pairs<MODE, CM, 0, true>(blkp, w, p, bs, lane, e, acc); break;
+    case 2: sell_pairs<MODE, CM, 1, false>(blkp, w, p, bs, lane, e, acc); break;
+    case 3: sell_pairs<MODE, CM, 1, true>(blkp, w, p, bs, lane, e, acc); break;
+    case 4: sell_pairs<MODE, CM, 2, false>(blkp, w, p, bs, lane, e, acc); break;
+    case 5: sell_pairs<MODE, CM, 2, true>(blkp, w, p, bs, lane, e, acc); break;
+    case 6: sell_pairs<MODE, CM, 3, false>(blkp, w, p, bs, lane, e, acc); break;
+    case 7: sell_pairs<MODE, CM, 3, true>(blkp, w, p, bs, lane, e, acc); break;
+    default: break;
+    }
+    return acc;
+}
+
+template <int MODE, bool PAIRED>
 __global__ __launch_bounds__(256) void spmv_sell_kernel(SellArgs a) {
     const int blk = xcd_remap(blockIdx.x, gridDim.x);
     const int sl = __builtin_amdgcn_readfirstlane(blk * 4 + (int)(threadIdx.x >> 6));
@@ -235,14 +330,20 @@ __global__ __launch_bounds__(256) void spmv_sell_kernel(SellArgs a) {
     const int w = a.soff[slice + 1] - t0;
     const uint32_t d = a.desc[slice];
     const char *blkp = a.data + (int64_t)(d & 0x3fffffffu) * 128;
-    const double *v = reinterpret_cast<const double *>(blkp) + lane;
-    const char *ix = blkp + (int64_t)w * SELL_VAL_STEP;
     const int32_t *bs = a.base + t0;
     double acc;
-    switch (d >> 30) {
-    case 0: acc = sell_walk<0>(v, nullptr, bs, w, lane, a.e.x); break;
-    case 1: acc = sell_walk<1>(v, ix + lane * 2, bs, w, lane, a.e.x); break;
-    default: acc = sell_walk<2>(v, ix + lane * 4, bs, w, lane, a.e.x); break;
+    if constexpr (PAIRED) {
+        switch (d >> 30) {
+        case 0: acc = sell_walk_pairs<MODE, 0>(blkp, bs, w, lane, a.e); break;
+        case 1: acc = sell_walk_pairs<MODE, 1>(blkp, bs, w, lane, a.e); break;
+        default: acc = sell_walk_pairs<MODE, 2>(blkp, bs, w, lane, a.e); break;
+        }
+    } else {
+        switch (d >> 30) {
+        case 0: acc = sell_walk_steps<MODE, 0>(blkp, bs, w, lane, a.e); break;
+        case 1: acc = sell_walk_steps<MODE, 1>(blkp, bs, w, lane, a.e); break;
+        default: acc = sell_walk_steps<MODE, 2>(blkp, bs, w, lane, a.e); break;
+        }
     }
     if (live) ep.store(a.e, acc);
 }
@@ -254,19 +355,22 @@ __global__ __launch_bounds__(256) void spmv_sell_kernel(SellArgs a) {
 constexpr int SPMM_KB = 8;
 
 template <int CM, int KB>
-__device__ __forceinline__ void spmm_step4(const double *__restrict__ v, const char *__restrict__ ix,
+__device__ __forceinline__ void spmm_step4(const char *__restrict__ blkp, int w, int k, bool paired,
                                            const int32_t *__restrict__ bs, int lane, int nu,
                                            const double *__restrict__ x, int64_t ldx, double (&acc)[KB]) {
+    const char *ixb = blkp + (int64_t)w * SELL_VAL_STEP;
     double vv[4];
     int32_t cc[4];
 #pragma unroll
     for (int u = 0; u < 4; u++) {
         if (u < nu) {
-            vv[u] = __builtin_nontemporal_load(v + u * SELL_C);
-            if constexpr (CM == 0) cc[u] = bs[u] + lane;
+            const int t = k + u;
+            const int64_t el = sell_elem(t, w, lane, paired);
+            vv[u] = __builtin_nontemporal_load(reinterpret_cast<const double *>(blkp) + el);
+            if constexpr (CM == 0) cc[u] = bs[t] + lane;
             else if constexpr (CM == 1)
-                cc[u] = bs[u] + (int32_t)__builtin_nontemporal_load(reinterpret_cast<const uint16_t *>(ix) + u * SELL_C);
-            else cc[u] = __builtin_nontemporal_load(reinterpret_cast<const int32_t *>(ix) + u * SELL_C);
+                cc[u] = bs[t] + (int32_t)__builtin_nontemporal_load(reinterpret_cast<const uint16_t *>(ixb) + el);
+            else cc[u] = __builtin_nontemporal_load(reinterpret_cast<const int32_t *>(ixb) + el);
         }
     }
 #pragma unroll
@@ -279,15 +383,14 @@ __device__ __forceinline__ void spmm_step4(const double *__restrict__ v, const c
 }
 
 template <int CM, int KB>
-__device__ __forceinline__ void spmm_walk(const double *v, const char *ix, const int32_t *bs, int w, int lane,
+__device__ __forceinline__ void spmm_walk(const char *blkp, bool paired, const int32_t *bs, int w, int lane,
                                           const double *x, int64_t ldx, double (&acc)[KB]) {
-    constexpr int IB = CM == 0 ? 0 : CM == 1 ? 2 : 4;
-    for (int k = 0; k < w; k += 4)
-        spmm_step4<CM, KB>(v + k * SELL_C, ix + (int64_t)k * SELL_C * IB, bs + k, lane, min(4, w - k), x, ldx, acc);
+    for (int k = 0; k < w; k += 4) spmm_step4<CM, KB>(blkp, w, k, paired, bs, lane, min(4, w - k), x, ldx, acc);
 }
 
 template <int KB>
-__global__ __launch_bounds__(256) void spmm_sell_kernel(SellArgs a, int64_t ldx, double *y, int64_t ldy) {
+__global__ __launch_bounds__(256) void spmm_sell_kernel(SellArgs a, bool paired, int64_t ldx, double *y,
+                                                        int64_t ldy) {
     const int blk = xcd_remap(blockIdx.x, gridDim.x);
     const int sl = __builtin_amdgcn_readfirstlane(blk * 4 + (int)(threadIdx.x >> 6));
     if (sl >= a.nslices) return;
@@ -299,16 +402,14 @@ __global__ __launch_bounds__(256) void spmm_sell_kernel(SellArgs a, int64_t ldx,
     const int w = a.soff[slice + 1] - t0;
     const uint32_t d = a.desc[slice];
     const char *blkp = a.data + (int64_t)(d & 0x3fffffffu) * 128;
-    const double *v = reinterpret_cast<const double *>(blkp) + lane;
-    const char *ix = blkp + (int64_t)w * SELL_VAL_STEP;
     const int32_t *bs = a.base + t0;
     double acc[KB];
 #pragma unroll
     for (int c = 0; c < KB; c++) acc[c] = 0.0;
     switch (d >> 30) {
-    case 0: spmm_walk<0, KB>(v, nullptr, bs, w, lane, a.e.x, ldx, acc); break;
-    case 1: spmm_walk<1, KB>(v, ix + lane * 2, bs, w, lane, a.e.x, ldx, acc); break;
-    default: spmm_walk<2, KB>(v, ix + lane * 4, bs, w, lane, a.e.x, ldx, acc); break;
+    case 0: spmm_walk<0, KB>(blkp, paired, bs, w, lane, a.e.x, ldx, acc); break;
+    case 1: spmm_walk<1, KB>(blkp, paired, bs, w, lane, a.e.x, ldx, acc); break;
+    default: spmm_walk<2, KB>(blkp, paired, bs, w, lane, a.e.x, ldx, acc); break;
     }
     if (live) {
 #pragma unroll
@@ -338,7 +439,6 @@ __global__ __launch_bounds__(256) void spmv_vector_kernel(VecArgs a) {
     const int e0 = a.rowptr[row], e1 = a.rowptr[row + 1];
     const double *__restrict__ val = a.val;
     const int32_t *__restrict__ col = a.col;
-    const double *__restrict__ x = a.e.x;
     double acc = 0.0;
     int k = e0 + lane;
     for (; k + 3 * 64 < e1; k += 4 * 64) {
@@ -351,11 +451,12 @@ __global__ __launch_bounds__(256) void spmv_vector_kernel(VecArgs a) {
         }
         double xx[4];
 #pragma unroll
-        for (int u = 0; u < 4; u++) xx[u] = x[cc[u]];
+        for (int u = 0; u < 4; u++) xx[u] = gx<MODE>(a.e, cc[u]);
 #pragma unroll
         for (int u = 0; u < 4; u++) acc = fma(vv[u], xx[u], acc);
     }
-    for (; k < e1; k += 64) acc = fma(__builtin_nontemporal_load(val + k), x[__builtin_nontemporal_load(col + k)], acc);
+    for (; k < e1; k += 64)
+        acc = fma(__builtin_nontemporal_load(val + k), gx<MODE>(a.e, __builtin_nontemporal_load(col + k)), acc);
     for (int off = 32; off > 0; off >>= 1) acc += __shfl_xor(acc, off);
     if (lane == 0) ep.store(a.e, acc);
 }
@@ -463,7 +564,7 @@ __global__ __launch_bounds__(256) void k_sell_plan(const int64_t *rp, const int3
 __global__ __launch_bounds__(256) void k_sell_fill(const int64_t *rp, const int32_t *col, const double *val,
                                                    const int32_t *row0, const int32_t *soff, const uint32_t *desc,
                                                    const uint8_t *aligned, int64_t nslices, int64_t ncols,
-                                                   int32_t *base, char *data) {
+                                                   bool paired, int32_t *base, char *data) {
     const int64_t sl = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
     if (sl >= nslices) return;
     const int lane = threadIdx.x & 63;
@@ -478,12 +579,13 @@ __global__ __launch_bounds__(256) void k_sell_fill(const int64_t *rp, const int3
     auto put = [&](int t, int64_t c, double v, int, int64_t b) {
         // the slice mode can exceed the step's: u16 steps use base = min column
         const int64_t sb = smode == 1 ? wave_min64(c) : b;
-        vals[t * SELL_C + lane] = v;
+        const int64_t el = sell_elem(t, w, lane, paired);
+        vals[el] = v;
         if (lane == 0) bs[t] = smode == 2 ? 0 : (int32_t)sb;
         if (smode == 1)
-            reinterpret_cast<uint16_t *>(blkp + (int64_t)w * SELL_VAL_STEP)[t * SELL_C + lane] = (uint16_t)(c - sb);
+            reinterpret_cast<uint16_t *>(blkp + (int64_t)w * SELL_VAL_STEP)[el] = (uint16_t)(c - sb);
         else if (smode == 2)
-            reinterpret_cast<int32_t *>(blkp + (int64_t)w * SELL_VAL_STEP)[t * SELL_C + lane] = (int32_t)c;
+            reinterpret_cast<int32_t *>(blkp + (int64_t)w * SELL_VAL_STEP)[el] = (int32_t)c;
     };
     if (aligned[sl]) sell_walk_build<true>(rp, col, val, row, live, ncols, w, put);
     else sell_walk_build<false>(rp, col, val, row, live, ncols, w, put);
@@ -551,12 +653,14 @@ void build_sell(GpuCsr &m, const std::vector<int64_t> &rp) {
     m.sell_base.resize(std::max<int64_t>(1, steps));
     m.sell_data.resize(std::max<int64_t>(128, bytes));
     DevBuf<uint8_t> dal(ns);
+    const char *lay = getenv("FAMG_SELL_LAYOUT");
+    m.sell_paired = !(lay && std::string(lay) == "step");
     FAMG_CHECK_HIP(hipMemcpyAsync(m.sell_soff.get(), soff.data(), (ns + 1) * sizeof(int32_t), hipMemcpyHostToDevice, s));
     FAMG_CHECK_HIP(hipMemcpyAsync(m.sell_desc.get(), desc.data(), ns * sizeof(uint32_t), hipMemcpyHostToDevice, s));
     FAMG_CHECK_HIP(hipMemcpyAsync(dal.get(), aligned.data(), ns, hipMemcpyHostToDevice, s));
     hipLaunchKernelGGL(k_sell_fill, grid, dim3(256), 0, s, m.rp64.get(), m.col.get(), m.val.get(),
                        m.sell_row0.get(), m.sell_soff.get(), m.sell_desc.get(), dal.get(), ns, m.ncols,
-                       m.sell_base.get(), m.sell_data.get());
+                       m.sell_paired, m.sell_base.get(), m.sell_data.get());
     FAMG_CHECK_HIP(hipGetLastError());
     FAMG_CHECK_HIP(hipStreamSynchronize(s));
     m.nslices = ns;
@@ -576,14 +680,20 @@ void choose_kernel(GpuCsr &m) {
 
 // ------------------------------------------------------------------ dispatch
 
-#define FAMG_LAUNCH_MODES(KERNEL, grid, block, s, args)                                       \
-    switch (mode) {                                                                           \
-    case SPMV_SET: hipLaunchKernelGGL(KERNEL<SPMV_SET>, grid, block, 0, s, args); break;      \
-    case SPMV_ADD: hipLaunchKernelGGL(KERNEL<SPMV_ADD>, grid, block, 0, s, args); break;      \
-    case SPMV_RESID: hipLaunchKernelGGL(KERNEL<SPMV_RESID>, grid, block, 0, s, args); break;  \
-    case SPMV_JACOBI: hipLaunchKernelGGL(KERNEL<SPMV_JACOBI>, grid, block, 0, s, args); break; \
-    case SPMV_SGS: hipLaunchKernelGGL(KERNEL<SPMV_SGS>, grid, block, 0, s, args); break;      \
+// KERNEL<MODE [, extra template args]> on (grid, block, stream s); the optional
+// trailing argument is pasted after MODE (e.g. FAMG_PAIRED_T).
+#define FAMG_LAUNCH_MODES(KERNEL, grid, block, s, args, ...)                             \
+    switch (mode) {                                                                     \
+    case SPMV_SET: KERNEL<SPMV_SET __VA_ARGS__><<<grid, block, 0, s>>>(args); break;       \
+    case SPMV_ADD: KERNEL<SPMV_ADD __VA_ARGS__><<<grid, block, 0, s>>>(args); break;       \
+    case SPMV_RESID: KERNEL<SPMV_RESID __VA_ARGS__><<<grid, block, 0, s>>>(args); break;   \
+    case SPMV_JACOBI: KERNEL<SPMV_JACOBI __VA_ARGS__><<<grid, block, 0, s>>>(args); break; \
+    case SPMV_SGS: KERNEL<SPMV_SGS __VA_ARGS__><<<grid, block, 0, s>>>(args); break;       \
+    case SPMV_RESID0: KERNEL<SPMV_RESID0 __VA_ARGS__><<<grid, block, 0, s>>>(args); break; \
+    case SPMV_ADD0: KERNEL<SPMV_ADD0 __VA_ARGS__><<<grid, block, 0, s>>>(args); break;     \
     }
+#define FAMG_PAIRED_T , true
+#define FAMG_STEPS_T , false
 
 void spmm(const GpuCsr &m, const double *x, int64_t ldx, double *y, int64_t ldy, int64_t k, hipStream_t s) {
     if (m.kernel != SPMV_KERNEL_SELL) {  // other storages: one SpMV per column
@@ -599,14 +709,14 @@ void spmm(const GpuCsr &m, const double *x, int64_t ldx, double *y, int64_t ldy,
                    m.sell_data.get(), 0, (int32_t)m.nslices, e};
         double *yc = y + c0 * ldy;
         switch (kb) {
-        case 1: hipLaunchKernelGGL(spmm_sell_kernel<1>, grid, block, 0, s, a, ldx, yc, ldy); break;
-        case 2: hipLaunchKernelGGL(spmm_sell_kernel<2>, grid, block, 0, s, a, ldx, yc, ldy); break;
-        case 3: hipLaunchKernelGGL(spmm_sell_kernel<3>, grid, block, 0, s, a, ldx, yc, ldy); break;
-        case 4: hipLaunchKernelGGL(spmm_sell_kernel<4>, grid, block, 0, s, a, ldx, yc, ldy); break;
-        case 5: hipLaunchKernelGGL(spmm_sell_kernel<5>, grid, block, 0, s, a, ldx, yc, ldy); break;
-        case 6: hipLaunchKernelGGL(spmm_sell_kernel<6>, grid, block, 0, s, a, ldx, yc, ldy); break;
-        case 7: hipLaunchKernelGGL(spmm_sell_kernel<7>, grid, block, 0, s, a, ldx, yc, ldy); break;
-        default: hipLaunchKernelGGL(spmm_sell_kernel<8>, grid, block, 0, s, a, ldx, yc, ldy); break;
+        case 1: hipLaunchKernelGGL(spmm_sell_kernel<1>, grid, block, 0, s, a, m.sell_paired, ldx, yc, ldy); break;
+        case 2: hipLaunchKernelGGL(spmm_sell_kernel<2>, grid, block, 0, s, a, m.sell_paired, ldx, yc, ldy); break;
+        case 3: hipLaunchKernelGGL(spmm_sell_kernel<3>, grid, block, 0, s, a, m.sell_paired, ldx, yc, ldy); break;
+        case 4: hipLaunchKernelGGL(spmm_sell_kernel<4>, grid, block, 0, s, a, m.sell_paired, ldx, yc, ldy); break;
+        case 5: hipLaunchKernelGGL(spmm_sell_kernel<5>, grid, block, 0, s, a, m.sell_paired, ldx, yc, ldy); break;
+        case 6: hipLaunchKernelGGL(spmm_sell_kernel<6>, grid, block, 0, s, a, m.sell_paired, ldx, yc, ldy); break;
+        case 7: hipLaunchKernelGGL(spmm_sell_kernel<7>, grid, block, 0, s, a, m.sell_paired, ldx, yc, ldy); break;
+        default: hipLaunchKernelGGL(spmm_sell_kernel<8>, grid, block, 0, s, a, m.sell_paired, ldx, yc, ldy); break;
         }
         FAMG_CHECK_HIP(hipGetLastError());
     }
@@ -626,7 +736,11 @@ void spmv(const GpuCsr &m, const double *x, double *y, SpmvMode mode, const Spmv
         SellArgs a{m.sell_row0.get(), m.sell_soff.get(), m.sell_desc.get(), m.sell_base.get(),
                    m.sell_data.get(), (int32_t)s0, (int32_t)(s1 - s0), e};
         const dim3 grid((unsigned)ceil_div(s1 - s0, 4));
-        FAMG_LAUNCH_MODES(spmv_sell_kernel, grid, block, s, a)
+        if (m.sell_paired) {
+            FAMG_LAUNCH_MODES(spmv_sell_kernel, grid, block, s, a, FAMG_PAIRED_T)
+        } else {
+            FAMG_LAUNCH_MODES(spmv_sell_kernel, grid, block, s, a, FAMG_STEPS_T)
+        }
     } else if (m.kernel == SPMV_KERNEL_VECTOR) {
         const int64_t r0 = seg < 0 ? 0 : m.seg_rows[seg];
         const int64_t r1 = seg < 0 ? m.nrows : m.seg_rows[seg + 1];

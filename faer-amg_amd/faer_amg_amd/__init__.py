@@ -474,6 +474,10 @@ class Multigrid(LinOp):
         """Literal smooth() order for SGS (residual SpMV + SGS(r)) instead of the fused sweep."""
         _ck(_lib.amg_multigrid_set_option(self.h, 1, 1 if enable else 0))
 
+    def set_fold_zero_guess(self, enable):
+        """Fold the zero-guess Jacobi step into the residual/correction SpMVs (default on)."""
+        _ck(_lib.amg_multigrid_set_option(self.h, 2, 1 if enable else 0))
+
     def levels(self):
         v = i64()
         _ck(_lib.amg_multigrid_levels(self.h, C.byref(v)))

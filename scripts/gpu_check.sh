@@ -15,7 +15,7 @@ step() {  # step NAME SECONDS CMD...
 }
 for s in "$@"; do
     case $s in
-        tests) step pytest_gpu 900 python -m pytest tests -m gpu -q ;;
+        tests) step pytest_gpu 900 python -u -m pytest tests -m gpu -v --timeout 120 --timeout-method thread ;;
         smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
         bench) step bench 600 python bench.py --steps 20 --warmup 3 ;;
         benchq) step bench 400 python bench.py --steps 20 --warmup 3 --no-cpu-baseline --ab ;;
