@@ -148,10 +148,12 @@ def build_problem(fa, ctx, args, dims):
     return A, mg
 
 
-def vcycle_bytes(mg, csr=False):
+def vcycle_bytes(mg, csr=False, fold=True):
     """Algorithmic bytes of one V-cycle (s = 1, mu = 1, zero initial guess) from the
     per-kernel formulas of SURVEY.md 8(d); matrix bytes of the chosen storage
-    (csr=False) or of 32-bit CSR (csr=True)."""
+    (csr=False) or of 32-bit CSR (csr=True).  fold: diagonal smoothers fold the
+    first smoothing step v = d f into the residual (reads f, d; writes r) and the
+    correction (reads d, f, P, v_c; writes v) -- no separate 24n pass."""
     def mat(M):
         return 12 * M.nnz + 4 * (M.nrows + 1) if csr else M.spmv_info()["stream_bytes"]
     tot = 0
@@ -164,10 +166,10 @@ def vcycle_bytes(mg, csr=False):
             continue
         bA = mat(A)
         nc = R.nrows
-        tot += 24 * n                                  # first smoothing step from 0
+        tot += 0 if fold else 24 * n                   # first smoothing step from 0
         tot += bA + 24 * n                             # residual
         tot += mat(R) + 8 * n + 8 * nc                 # restrict
-        tot += mat(P) + 8 * nc + 16 * n                # interpolate + add
+        tot += mat(P) + 8 * nc + (24 if fold else 16) * n  # interpolate + add
         tot += bA + 32 * n                             # post-smoothing Jacobi
     return tot
 
@@ -221,6 +223,23 @@ def run_single(args):
     bytes_csr = spmv_bytes(n, n, nnz)
     achieved = bytes_spmv / (spmv_ms * 1e-3) / 1e9
 
+    # the same operator with fp64 values (value codes off): the uncompressed
+    # SELL kernel, reported beside the one the V-cycle uses
+    fa.set_value_codes(False)
+    A64 = (fa.SparseMatOp.laplace3d_7pt(ctx, *dims) if args.problem == "7pt"
+           else fa.SparseMatOp.aniso27(ctx, *dims, 1.0, 1.0, 0.01))
+    fa.set_value_codes(True)
+    for _ in range(3):
+        A64.apply(y, x)
+    spmv64_ms = time_kernel(lambda: A64.apply(y, x), 20, stream)
+    bytes64 = spmv_bytes_fmt(A64)
+    fp64_values = {"kernel": "spmv_sell_kernel<SET> on A_0, fp64 values", "ms_per_launch": round(spmv64_ms, 5),
+                   "bytes_per_launch": bytes64,
+                   "achieved": round(bytes64 / (spmv64_ms * 1e-3) / 1e9, 1),
+                   "frac": round(bytes64 / (spmv64_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                   "storage": A64.spmv_info()}
+    del A64
+
     if args.ab:
         ops = {}
         for fmt in ("csr", "sell"):
@@ -241,8 +260,9 @@ def run_single(args):
     A.apply(r, z)
     torch.cuda.synchronize()
     rho1 = float(torch.linalg.norm(b - r) / torch.linalg.norm(b))
-    vbytes = vcycle_bytes(mg)
-    vbytes_csr = vcycle_bytes(mg, csr=True)
+    fold = args.smoother in ("jacobi", "l1")
+    vbytes = vcycle_bytes(mg, fold=fold)
+    vbytes_csr = vcycle_bytes(mg, csr=True, fold=fold)
 
     cpu = None
     if not args.no_cpu_baseline:
@@ -289,7 +309,8 @@ def run_single(args):
                      "storage": info,
                      "bytes_per_launch": bytes_spmv, "ms_per_launch": round(spmv_ms, 5),
                      "csr_bytes_per_launch": bytes_csr,
-                     "csr_equivalent_GBs": round(bytes_csr / (spmv_ms * 1e-3) / 1e9, 1)},
+                     "csr_equivalent_GBs": round(bytes_csr / (spmv_ms * 1e-3) / 1e9, 1),
+                     "fp64_values": fp64_values},
         "cpu_baseline": cpu,
     }
 

@@ -156,6 +156,13 @@ amg_status amg_set_alloc_policy(int32_t policy) {
     });
 }
 
+amg_status amg_set_value_codes(int32_t enable) {
+    return guard([&] {
+        FAMG_REQUIRE(enable == 0 || enable == 1, AMG_ERR_INVALID, "enable must be 0 or 1");
+        g_value_codes = enable;
+    });
+}
+
 amg_status amg_set_spmv_format(int32_t policy) {
     return guard([&] {
         FAMG_REQUIRE(policy >= 0 && policy <= 3, AMG_ERR_INVALID, "policy must be 0..3");
@@ -225,6 +232,16 @@ amg_status amg_csr_spmv_info(const amg_linop *op, int64_t *info8) {
         info8[5] = m.sell_mode_slices[0];
         info8[6] = m.sell_mode_slices[1];
         info8[7] = m.sell_mode_slices[2];
+    });
+}
+
+amg_status amg_csr_value_codes(const amg_linop *op, int64_t *info2) {
+    return guard([&] {
+        FAMG_REQUIRE(info2, AMG_ERR_INVALID, "null argument");
+        const GpuCsr &m = need_csr(op)->m;
+        const bool sell = m.kernel == SPMV_KERNEL_SELL;
+        info2[0] = sell ? m.sell_vbits : 0;
+        info2[1] = sell ? m.sell_ntab : 0;
     });
 }
 

@@ -50,13 +50,18 @@ struct GpuCsr {
     int64_t nslices = 0, sell_steps = 0, sell_bytes = 0;
     int64_t sell_mode_slices[3] = {0, 0, 0};  // slices per column mode (implicit, u16, i32)
     bool sell_paired = true;  // step-pair layout (16-B value loads); false: one step per 512-B row
+    // value codes (spmv.hip "value codes"): 0 = fp64 values, else 4/8/16-bit codes
+    // into sell_vtab (sell_ntab distinct bit patterns, ascending)
+    int sell_vbits = 0;
+    int64_t sell_ntab = 0;
+    DevBuf<double> sell_vtab;
     int kernel = 0;  // SpmvKernel chosen at finalize
     bool spmv_ready() const { return rp32.get() != nullptr && sched.get() != nullptr; }
     bool has_sell() const { return sell_desc.get() != nullptr; }
     int64_t index_bytes() const { return 12 * nnz + 4 * (nrows + 1); }
     // matrix bytes one SpMV streams with the chosen kernel (data + metadata)
     int64_t stream_bytes() const {
-        return kernel == 1 ? sell_bytes + 12 * (nslices + 1) + 4 * sell_steps : index_bytes();
+        return kernel == 1 ? sell_bytes + 12 * (nslices + 1) + 4 * sell_steps + 8 * sell_ntab : index_bytes();
     }
 };
 
@@ -70,6 +75,9 @@ void csr_finalize(GpuCsr &m, const std::vector<int64_t> *segments = nullptr);
 // Format policy (process-wide, for matrices finalized afterwards):
 // 0 auto, 1 CSR-stream only, 2 SELL whenever rows <= 256, 3 vector (no SELL)
 extern int g_spmv_format_policy;
+// Value codes for SELL matrices finalized afterwards (1 = when <= 65536
+// distinct values, 0 = always fp64 values)
+extern int g_value_codes;
 enum SpmvKernel : int { SPMV_KERNEL_STREAM = 0, SPMV_KERNEL_SELL = 1, SPMV_KERNEL_VECTOR = 2 };
 void build_sell(GpuCsr &m, const std::vector<int64_t> &rp);
 void choose_kernel(GpuCsr &m);

@@ -32,6 +32,7 @@ typedef double dbl2_t __attribute__((ext_vector_type(2)));
 typedef int32_t i32x4_t __attribute__((ext_vector_type(4)));
 
 int g_spmv_format_policy = 0;
+int g_value_codes = 1;
 int g_alloc_policy = 1;
 bool g_alloc_debug = [] {
     const char *e = getenv("FAMG_ALLOC_DEBUG");
@@ -197,6 +198,8 @@ struct SellArgs {
     const char *data;
     int32_t slice0, nslices;
     Epi e;
+    const double *vtab;  // value table (code widths 4 / 8 / 16)
+    int32_t ntab;
 };
 
 // ---- one step per 512-B row (sell_paired = false)
@@ -315,8 +318,133 @@ __device__ __forceinline__ double sell_walk_pairs(const char *blkp, const int32_
     return acc;
 }
 
-template <int MODE, bool PAIRED>
+// ---- value codes (sell_vbits = 4, 8 or 16)
+//
+// A matrix whose stored values take at most 16 / 256 / 65536 distinct fp64 bit
+// patterns (the padding's +0.0 included) stores a 4 / 8 / 16-bit code per
+// entry into a per-matrix table sorted by bit pattern instead of the value
+// (index/value compression in the manner of CSR-VI).  The 8 codes of steps
+// 8g..8g+7 of one lane form one 4 / 8 / 16-B unit at g*64 + lane.  Column
+// blocks (u16 / i32) use the same grouping: step t of lane l at element
+// 8g*64 + r_g*l + (t - 8g), r_g = min(8, w - 8g), so a full group is one (u16)
+// or two (i32) 16-B loads per lane.  Tables of <= 256 entries are staged in
+// LDS per workgroup, 16-bit tables are read through the caches.  A decoded
+// value is the stored value bit for bit, so every row sum is unchanged.
+__host__ __device__ __forceinline__ int sell_code_bytes(int vb) { return vb == 4 ? 4 : vb == 8 ? 8 : 16; }
+
+__host__ __device__ __forceinline__ int64_t sell_value_bytes(int64_t w, int vb) {
+    return vb ? ((w + 7) >> 3) * SELL_C * sell_code_bytes(vb) : w * SELL_VAL_STEP;
+}
+
+__host__ __device__ __forceinline__ int64_t sell_group_elem(int t, int w, int lane) {
+    const int g0 = t & ~7;
+    const int r = w - g0 < 8 ? w - g0 : 8;
+    return (int64_t)g0 * SELL_C + r * lane + (t & 7);
+}
+
+template <int VB>
+__device__ __forceinline__ void sell_load_codes(const char *__restrict__ blkp, int g, int lane, uint32_t (&q)[4]) {
+    const int64_t unit = (int64_t)g * SELL_C + lane;
+    if constexpr (VB == 4) {
+        q[0] = __builtin_nontemporal_load(reinterpret_cast<const uint32_t *>(blkp) + unit);
+    } else if constexpr (VB == 8) {
+        const i32x2_t v = __builtin_nontemporal_load(reinterpret_cast<const i32x2_t *>(blkp) + unit);
+        q[0] = (uint32_t)v.x;
+        q[1] = (uint32_t)v.y;
+    } else {
+        const i32x4_t v = __builtin_nontemporal_load(reinterpret_cast<const i32x4_t *>(blkp) + unit);
+        q[0] = (uint32_t)v.x;
+        q[1] = (uint32_t)v.y;
+        q[2] = (uint32_t)v.z;
+        q[3] = (uint32_t)v.w;
+    }
+}
+
+template <int VB> __device__ __forceinline__ int sell_code(const uint32_t (&q)[4], int u) {
+    if constexpr (VB == 4) return (int)((q[0] >> (4 * u)) & 15u);
+    else if constexpr (VB == 8) return (int)((q[u >> 2] >> (8 * (u & 3))) & 255u);
+    else return (int)((q[u >> 1] >> (16 * (u & 1))) & 0xffffu);
+}
+
+// R (<= 8) steps of group g: every load of the group is issued before the
+// dependent x gathers; the row sum runs over t ascending.
+template <int MODE, int CM, int VB, int R>
+__device__ __forceinline__ void sellc_group(const char *__restrict__ blkp, const char *__restrict__ ixb, int g,
+                                            const int32_t *__restrict__ bs, int lane, const double *tab,
+                                            const Epi &e, double &acc) {
+    uint32_t q[4];
+    sell_load_codes<VB>(blkp, g, lane, q);
+    const int t0 = 8 * g;
+    int32_t cc[R];
+    if constexpr (CM == 0) {
+#pragma unroll
+        for (int u = 0; u < R; u++) cc[u] = bs[t0 + u] + lane;
+    } else if constexpr (R == 8) {
+        const int64_t el = (int64_t)t0 * SELL_C + 8 * lane;
+        if constexpr (CM == 1) {
+            const i32x4_t d = __builtin_nontemporal_load(reinterpret_cast<const i32x4_t *>(ixb + 2 * el));
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                cc[2 * u] = bs[t0 + 2 * u] + (int32_t)((uint32_t)d[u] & 0xffffu);
+                cc[2 * u + 1] = bs[t0 + 2 * u + 1] + (int32_t)((uint32_t)d[u] >> 16);
+            }
+        } else {
+            const i32x4_t *p = reinterpret_cast<const i32x4_t *>(ixb + 4 * el);
+            const i32x4_t d0 = __builtin_nontemporal_load(p);
+            const i32x4_t d1 = __builtin_nontemporal_load(p + 1);
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                cc[u] = d0[u];
+                cc[4 + u] = d1[u];
+            }
+        }
+    } else {
+        const int64_t el = (int64_t)t0 * SELL_C + R * lane;
+#pragma unroll
+        for (int u = 0; u < R; u++) {
+            if constexpr (CM == 1)
+                cc[u] = bs[t0 + u] +
+                        (int32_t)__builtin_nontemporal_load(reinterpret_cast<const uint16_t *>(ixb) + el + u);
+            else cc[u] = __builtin_nontemporal_load(reinterpret_cast<const int32_t *>(ixb) + el + u);
+        }
+    }
+    double xx[R];
+#pragma unroll
+    for (int u = 0; u < R; u++) xx[u] = gx<MODE>(e, cc[u]);
+#pragma unroll
+    for (int u = 0; u < R; u++) acc = fma(tab[sell_code<VB>(q, u)], xx[u], acc);
+}
+
+template <int MODE, int CM, int VB>
+__device__ __forceinline__ double sellc_walk(const char *blkp, const int32_t *bs, int w, int lane, const double *tab,
+                                             const Epi &e) {
+    const int ng = (w + 7) >> 3;
+    const char *ixb = blkp + (int64_t)ng * SELL_C * sell_code_bytes(VB);
+    double acc = 0.0;
+    const int full = w >> 3;
+    for (int g = 0; g < full; g++) sellc_group<MODE, CM, VB, 8>(blkp, ixb, g, bs, lane, tab, e, acc);
+    switch (w & 7) {
+    case 1: sellc_group<MODE, CM, VB, 1>(blkp, ixb, full, bs, lane, tab, e, acc); break;
+    case 2: sellc_group<MODE, CM, VB, 2>(blkp, ixb, full, bs, lane, tab, e, acc); break;
+    case 3: sellc_group<MODE, CM, VB, 3>(blkp, ixb, full, bs, lane, tab, e, acc); break;
+    case 4: sellc_group<MODE, CM, VB, 4>(blkp, ixb, full, bs, lane, tab, e, acc); break;
+    case 5: sellc_group<MODE, CM, VB, 5>(blkp, ixb, full, bs, lane, tab, e, acc); break;
+    case 6: sellc_group<MODE, CM, VB, 6>(blkp, ixb, full, bs, lane, tab, e, acc); break;
+    case 7: sellc_group<MODE, CM, VB, 7>(blkp, ixb, full, bs, lane, tab, e, acc); break;
+    default: break;
+    }
+    return acc;
+}
+
+// LAY: 0 one step per 512-B row, 1 step pairs (fp64 values); 4 / 8 / 16 value codes
+template <int MODE, int LAY>
 __global__ __launch_bounds__(256) void spmv_sell_kernel(SellArgs a) {
+    constexpr int TABN = LAY == 4 ? 16 : LAY == 8 ? 256 : 1;
+    __shared__ double stab[TABN];
+    if constexpr (LAY == 4 || LAY == 8) {
+        for (int i = threadIdx.x; i < a.ntab; i += 256) stab[i] = a.vtab[i];
+        __syncthreads();
+    }
     const int blk = xcd_remap(blockIdx.x, gridDim.x);
     const int sl = __builtin_amdgcn_readfirstlane(blk * 4 + (int)(threadIdx.x >> 6));
     if (sl >= a.nslices) return;
@@ -332,7 +460,19 @@ __global__ __launch_bounds__(256) void spmv_sell_kernel(SellArgs a) {
     const char *blkp = a.data + (int64_t)(d & 0x3fffffffu) * 128;
     const int32_t *bs = a.base + t0;
     double acc;
-    if constexpr (PAIRED) {
+    if constexpr (LAY == 16) {
+        switch (d >> 30) {
+        case 0: acc = sellc_walk<MODE, 0, 16>(blkp, bs, w, lane, a.vtab, a.e); break;
+        case 1: acc = sellc_walk<MODE, 1, 16>(blkp, bs, w, lane, a.vtab, a.e); break;
+        default: acc = sellc_walk<MODE, 2, 16>(blkp, bs, w, lane, a.vtab, a.e); break;
+        }
+    } else if constexpr (LAY == 4 || LAY == 8) {
+        switch (d >> 30) {
+        case 0: acc = sellc_walk<MODE, 0, LAY>(blkp, bs, w, lane, stab, a.e); break;
+        case 1: acc = sellc_walk<MODE, 1, LAY>(blkp, bs, w, lane, stab, a.e); break;
+        default: acc = sellc_walk<MODE, 2, LAY>(blkp, bs, w, lane, stab, a.e); break;
+        }
+    } else if constexpr (LAY == 1) {
         switch (d >> 30) {
         case 0: acc = sell_walk_pairs<MODE, 0>(blkp, bs, w, lane, a.e); break;
         case 1: acc = sell_walk_pairs<MODE, 1>(blkp, bs, w, lane, a.e); break;
@@ -535,8 +675,71 @@ __device__ int sell_walk_build(const int64_t *rp, const int32_t *col, const doub
     }
 }
 
-__host__ __device__ inline int64_t sell_slice_bytes(int64_t w, int mode) {
-    return w * (SELL_VAL_STEP + (mode == 0 ? 0 : mode == 1 ? 2 * SELL_C : 4 * SELL_C));
+__host__ __device__ inline int64_t sell_slice_bytes(int64_t w, int mode, int vb) {
+    return sell_value_bytes(w, vb) + w * (mode == 0 ? 0 : mode == 1 ? 2 * SELL_C : 4 * SELL_C);
+}
+
+// ---- value table: the distinct fp64 bit patterns of a matrix (open
+// addressing; stops counting past VT_MAX)
+constexpr int VT_MAX = 65536;
+constexpr int VT_SLOTS = 2 * VT_MAX;
+constexpr unsigned long long VT_EMPTY = ~0ull;  // a NaN payload: a matrix holding it keeps fp64 values
+
+__global__ __launch_bounds__(256) void k_value_set(const double *val, int64_t nnz, unsigned long long *slots,
+                                                   unsigned int *cnt) {
+    const int64_t stride = (int64_t)gridDim.x * 256;
+    for (int64_t k = (int64_t)blockIdx.x * 256 + threadIdx.x; k < nnz; k += stride) {
+        const unsigned long long b = (unsigned long long)__double_as_longlong(val[k]);
+        if (b == VT_EMPTY) {
+            atomicAdd(cnt, (unsigned)VT_SLOTS);
+            return;
+        }
+        unsigned h = (unsigned)((b * 0x9E3779B97F4A7C15ull) >> 47) & (VT_SLOTS - 1);
+        for (int p = 0; p < VT_SLOTS; p++, h = (h + 1) & (VT_SLOTS - 1)) {
+            unsigned long long cur = slots[h];
+            if (cur == b) break;
+            if ((cur == VT_EMPTY || p >= 16) && *(volatile unsigned *)cnt > (unsigned)VT_MAX) return;
+            if (cur == VT_EMPTY) {
+                cur = atomicCAS(&slots[h], VT_EMPTY, b);
+                if (cur == VT_EMPTY) {
+                    atomicAdd(cnt, 1u);
+                    break;
+                }
+                if (cur == b) break;
+            }
+        }
+    }
+}
+
+// Code width for m's values (0 = keep fp64, 4, 8 or 16) and the table: the
+// distinct bit patterns, +0.0 (padding) included, ascending as unsigned.
+static int value_table(const GpuCsr &m, std::vector<unsigned long long> &tab) {
+    tab.clear();
+    if (!g_value_codes || m.nnz == 0) return 0;
+    hipStream_t s = m.ctx->stream;
+    DevBuf<unsigned long long> slots(VT_SLOTS);
+    DevBuf<unsigned int> cnt(1);
+    FAMG_CHECK_HIP(hipMemsetAsync(slots.get(), 0xff, VT_SLOTS * sizeof(unsigned long long), s));
+    FAMG_CHECK_HIP(hipMemsetAsync(cnt.get(), 0, sizeof(unsigned int), s));
+    const unsigned grid = (unsigned)std::min<int64_t>(4096, ceil_div(m.nnz, 256));
+    hipLaunchKernelGGL(k_value_set, dim3(grid), dim3(256), 0, s, m.val.get(), m.nnz, slots.get(), cnt.get());
+    FAMG_CHECK_HIP(hipGetLastError());
+    std::vector<unsigned long long> h(VT_SLOTS);
+    unsigned int c = 0;
+    FAMG_CHECK_HIP(hipMemcpyAsync(h.data(), slots.get(), VT_SLOTS * sizeof(unsigned long long),
+                                  hipMemcpyDeviceToHost, s));
+    FAMG_CHECK_HIP(hipMemcpyAsync(&c, cnt.get(), sizeof(c), hipMemcpyDeviceToHost, s));
+    FAMG_CHECK_HIP(hipStreamSynchronize(s));
+    if (c > (unsigned)VT_MAX) return 0;
+    for (unsigned long long b : h)
+        if (b != VT_EMPTY) tab.push_back(b);
+    if (std::find(tab.begin(), tab.end(), 0ull) == tab.end()) tab.push_back(0ull);
+    std::sort(tab.begin(), tab.end());
+    if ((int64_t)tab.size() > VT_MAX) {
+        tab.clear();
+        return 0;
+    }
+    return tab.size() <= 16 ? 4 : tab.size() <= 256 ? 8 : 16;
 }
 
 // plan[4 s ..] = {w_aligned (-1 = too wide), mode_aligned, w_plain, mode_plain}
@@ -560,11 +763,13 @@ __global__ __launch_bounds__(256) void k_sell_plan(const int64_t *rp, const int3
     }
 }
 
-// aligned[s] chooses the layout; desc/soff as uploaded
+// aligned[s] chooses the layout; desc/soff as uploaded; vb != 0: values as
+// vb-bit codes into tab (ntab entries, ascending bit patterns)
 __global__ __launch_bounds__(256) void k_sell_fill(const int64_t *rp, const int32_t *col, const double *val,
                                                    const int32_t *row0, const int32_t *soff, const uint32_t *desc,
                                                    const uint8_t *aligned, int64_t nslices, int64_t ncols,
-                                                   bool paired, int32_t *base, char *data) {
+                                                   bool paired, int vb, const unsigned long long *tab, int ntab,
+                                                   int32_t *base, char *data) {
     const int64_t sl = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
     if (sl >= nslices) return;
     const int lane = threadIdx.x & 63;
@@ -574,18 +779,39 @@ __global__ __launch_bounds__(256) void k_sell_fill(const int64_t *rp, const int3
     const uint32_t d = desc[sl];
     const int smode = (int)(d >> 30);
     char *blkp = data + (int64_t)(d & 0x3fffffffu) * 128;
+    char *ixb = blkp + sell_value_bytes(w, vb);
     double *vals = reinterpret_cast<double *>(blkp);
     int32_t *bs = base + soff[sl];
+    unsigned long long cacc = 0;
     auto put = [&](int t, int64_t c, double v, int, int64_t b) {
         // the slice mode can exceed the step's: u16 steps use base = min column
         const int64_t sb = smode == 1 ? wave_min64(c) : b;
-        const int64_t el = sell_elem(t, w, lane, paired);
-        vals[el] = v;
+        const int64_t el = vb ? sell_group_elem(t, w, lane) : sell_elem(t, w, lane, paired);
+        if (vb == 0) {
+            vals[el] = v;
+        } else {
+            const unsigned long long bits = (unsigned long long)__double_as_longlong(v);
+            int lo = 0, hi = ntab - 1;
+            while (lo < hi) {
+                const int mid = (lo + hi) >> 1;
+                if (tab[mid] < bits) lo = mid + 1;
+                else hi = mid;
+            }
+            const int64_t unit = (int64_t)(t >> 3) * SELL_C + lane;
+            if (vb == 16) {
+                reinterpret_cast<uint16_t *>(blkp)[unit * 8 + (t & 7)] = (uint16_t)lo;
+            } else {
+                cacc |= (unsigned long long)lo << (vb * (t & 7));
+                if ((t & 7) == 7 || t == w - 1) {
+                    if (vb == 4) reinterpret_cast<uint32_t *>(blkp)[unit] = (uint32_t)cacc;
+                    else reinterpret_cast<unsigned long long *>(blkp)[unit] = cacc;
+                    cacc = 0;
+                }
+            }
+        }
         if (lane == 0) bs[t] = smode == 2 ? 0 : (int32_t)sb;
-        if (smode == 1)
-            reinterpret_cast<uint16_t *>(blkp + (int64_t)w * SELL_VAL_STEP)[el] = (uint16_t)(c - sb);
-        else if (smode == 2)
-            reinterpret_cast<int32_t *>(blkp + (int64_t)w * SELL_VAL_STEP)[el] = (int32_t)c;
+        if (smode == 1) reinterpret_cast<uint16_t *>(ixb)[el] = (uint16_t)(c - sb);
+        else if (smode == 2) reinterpret_cast<int32_t *>(ixb)[el] = (int32_t)c;
     };
     if (aligned[sl]) sell_walk_build<true>(rp, col, val, row, live, ncols, w, put);
     else sell_walk_build<false>(rp, col, val, row, live, ncols, w, put);
@@ -597,7 +823,9 @@ void build_sell(GpuCsr &m, const std::vector<int64_t> &rp) {
     m.sell_desc.release();
     m.sell_base.release();
     m.sell_data.release();
-    m.nslices = m.sell_steps = m.sell_bytes = 0;
+    m.sell_vtab.release();
+    m.nslices = m.sell_steps = m.sell_bytes = m.sell_ntab = 0;
+    m.sell_vbits = 0;
     m.sell_mode_slices[0] = m.sell_mode_slices[1] = m.sell_mode_slices[2] = 0;
     m.seg_slc.clear();
     const int pol = g_spmv_format_policy;
@@ -615,6 +843,8 @@ void build_sell(GpuCsr &m, const std::vector<int64_t> &rp) {
     if (maxlen > max_w) return;
     row0.push_back((int32_t)m.nrows);
     const int64_t ns = (int64_t)row0.size() - 1;
+    std::vector<unsigned long long> tab;
+    const int vb = value_table(m, tab);
     hipStream_t s = m.ctx->stream;
     DevBuf<int32_t> drow0(ns + 1), dplan(4 * ns);
     FAMG_CHECK_HIP(hipMemcpyAsync(drow0.get(), row0.data(), (ns + 1) * sizeof(int32_t), hipMemcpyHostToDevice, s));
@@ -632,12 +862,12 @@ void build_sell(GpuCsr &m, const std::vector<int64_t> &rp) {
     int64_t bytes = 0, steps = 0, cnt[3] = {0, 0, 0};
     for (int64_t k = 0; k < ns; k++) {
         const int wa = plan[4 * k], ma = plan[4 * k + 1], wp = plan[4 * k + 2], mp = plan[4 * k + 3];
-        const bool al = wa >= 0 && sell_slice_bytes(wa, ma) <= sell_slice_bytes(wp, mp);
+        const bool al = wa >= 0 && sell_slice_bytes(wa, ma, vb) <= sell_slice_bytes(wp, mp, vb);
         const int w = al ? wa : wp, md = al ? ma : mp;
         aligned[k] = al;
         if (bytes / 128 >= (int64_t(1) << 30) || steps + w >= (int64_t(1) << 31)) return;
         desc[k] = (uint32_t)(bytes / 128) | ((uint32_t)md << 30);
-        bytes += sell_slice_bytes(w, md);
+        bytes += sell_slice_bytes(w, md, vb);
         steps += w;
         soff[k + 1] = (int32_t)steps;
         cnt[md]++;
@@ -658,14 +888,22 @@ void build_sell(GpuCsr &m, const std::vector<int64_t> &rp) {
     FAMG_CHECK_HIP(hipMemcpyAsync(m.sell_soff.get(), soff.data(), (ns + 1) * sizeof(int32_t), hipMemcpyHostToDevice, s));
     FAMG_CHECK_HIP(hipMemcpyAsync(m.sell_desc.get(), desc.data(), ns * sizeof(uint32_t), hipMemcpyHostToDevice, s));
     FAMG_CHECK_HIP(hipMemcpyAsync(dal.get(), aligned.data(), ns, hipMemcpyHostToDevice, s));
+    if (vb) {
+        m.sell_vtab.resize(tab.size());
+        FAMG_CHECK_HIP(hipMemcpyAsync(m.sell_vtab.get(), tab.data(), tab.size() * sizeof(double),
+                                      hipMemcpyHostToDevice, s));
+    }
     hipLaunchKernelGGL(k_sell_fill, grid, dim3(256), 0, s, m.rp64.get(), m.col.get(), m.val.get(),
                        m.sell_row0.get(), m.sell_soff.get(), m.sell_desc.get(), dal.get(), ns, m.ncols,
-                       m.sell_paired, m.sell_base.get(), m.sell_data.get());
+                       m.sell_paired, vb, reinterpret_cast<const unsigned long long *>(m.sell_vtab.get()),
+                       (int)tab.size(), m.sell_base.get(), m.sell_data.get());
     FAMG_CHECK_HIP(hipGetLastError());
     FAMG_CHECK_HIP(hipStreamSynchronize(s));
     m.nslices = ns;
     m.sell_steps = steps;
     m.sell_bytes = bytes;
+    m.sell_vbits = vb;
+    m.sell_ntab = vb ? (int64_t)tab.size() : 0;
     for (int k = 0; k < 3; k++) m.sell_mode_slices[k] = cnt[k];
     m.seg_slc = seg_slc;
 }
@@ -681,7 +919,7 @@ void choose_kernel(GpuCsr &m) {
 // ------------------------------------------------------------------ dispatch
 
 // KERNEL<MODE [, extra template args]> on (grid, block, stream s); the optional
-// trailing argument is pasted after MODE (e.g. FAMG_PAIRED_T).
+// trailing argument is pasted after MODE (e.g. FAMG_LAY1).
 #define FAMG_LAUNCH_MODES(KERNEL, grid, block, s, args, ...)                             \
     switch (mode) {                                                                     \
     case SPMV_SET: KERNEL<SPMV_SET __VA_ARGS__><<<grid, block, 0, s>>>(args); break;       \
@@ -692,11 +930,14 @@ void choose_kernel(GpuCsr &m) {
     case SPMV_RESID0: KERNEL<SPMV_RESID0 __VA_ARGS__><<<grid, block, 0, s>>>(args); break; \
     case SPMV_ADD0: KERNEL<SPMV_ADD0 __VA_ARGS__><<<grid, block, 0, s>>>(args); break;     \
     }
-#define FAMG_PAIRED_T , true
-#define FAMG_STEPS_T , false
+#define FAMG_LAY0 , 0
+#define FAMG_LAY1 , 1
+#define FAMG_LAY4 , 4
+#define FAMG_LAY8 , 8
+#define FAMG_LAY16 , 16
 
 void spmm(const GpuCsr &m, const double *x, int64_t ldx, double *y, int64_t ldy, int64_t k, hipStream_t s) {
-    if (m.kernel != SPMV_KERNEL_SELL) {  // other storages: one SpMV per column
+    if (m.kernel != SPMV_KERNEL_SELL || m.sell_vbits) {  // other storages: one SpMV per column
         for (int64_t c = 0; c < k; c++) spmv(m, x + c * ldx, y + c * ldy, SPMV_SET, SpmvEpi{}, s);
         return;
     }
@@ -706,7 +947,7 @@ void spmm(const GpuCsr &m, const double *x, int64_t ldx, double *y, int64_t ldy,
         const int kb = (int)std::min<int64_t>(SPMM_KB, k - c0);
         Epi e{x + c0 * ldx, nullptr, nullptr, nullptr, nullptr};
         SellArgs a{m.sell_row0.get(), m.sell_soff.get(), m.sell_desc.get(), m.sell_base.get(),
-                   m.sell_data.get(), 0, (int32_t)m.nslices, e};
+                   m.sell_data.get(), 0, (int32_t)m.nslices, e, nullptr, 0};
         double *yc = y + c0 * ldy;
         switch (kb) {
         case 1: hipLaunchKernelGGL(spmm_sell_kernel<1>, grid, block, 0, s, a, m.sell_paired, ldx, yc, ldy); break;
@@ -734,12 +975,19 @@ void spmv(const GpuCsr &m, const double *x, double *y, SpmvMode mode, const Spmv
         const int64_t s1 = seg < 0 ? m.nslices : m.seg_slc[seg + 1];
         if (s1 <= s0) return;
         SellArgs a{m.sell_row0.get(), m.sell_soff.get(), m.sell_desc.get(), m.sell_base.get(),
-                   m.sell_data.get(), (int32_t)s0, (int32_t)(s1 - s0), e};
+                   m.sell_data.get(), (int32_t)s0, (int32_t)(s1 - s0), e, m.sell_vtab.get(),
+                   (int32_t)m.sell_ntab};
         const dim3 grid((unsigned)ceil_div(s1 - s0, 4));
-        if (m.sell_paired) {
-            FAMG_LAUNCH_MODES(spmv_sell_kernel, grid, block, s, a, FAMG_PAIRED_T)
+        if (m.sell_vbits == 4) {
+            FAMG_LAUNCH_MODES(spmv_sell_kernel, grid, block, s, a, FAMG_LAY4)
+        } else if (m.sell_vbits == 8) {
+            FAMG_LAUNCH_MODES(spmv_sell_kernel, grid, block, s, a, FAMG_LAY8)
+        } else if (m.sell_vbits == 16) {
+            FAMG_LAUNCH_MODES(spmv_sell_kernel, grid, block, s, a, FAMG_LAY16)
+        } else if (m.sell_paired) {
+            FAMG_LAUNCH_MODES(spmv_sell_kernel, grid, block, s, a, FAMG_LAY1)
         } else {
-            FAMG_LAUNCH_MODES(spmv_sell_kernel, grid, block, s, a, FAMG_STEPS_T)
+            FAMG_LAUNCH_MODES(spmv_sell_kernel, grid, block, s, a, FAMG_LAY0)
         }
     } else if (m.kernel == SPMV_KERNEL_VECTOR) {
         const int64_t r0 = seg < 0 ? 0 : m.seg_rows[seg];

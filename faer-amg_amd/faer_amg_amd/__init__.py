@@ -49,12 +49,14 @@ SIGNATURES = {
     "amg_ctx_synchronize": (i32, [vp]),
     "amg_ctx_stream": (i32, [vp, P(vp)]),
     "amg_set_spmv_format": (i32, [i32]),
+    "amg_set_value_codes": (i32, [i32]),
     "amg_set_alloc_policy": (i32, [i32]),
     "amg_ctx_join_stream": (i32, [vp, vp, i32]),
     "amg_csr_create": (i32, [vp, i64, i64, vp, vp, vp, P(vp)]),
     "amg_csr_create_device_i32": (i32, [vp, i64, i64, vp, vp, vp, P(vp)]),
     "amg_csr_nnz": (i32, [vp, P(i64)]),
     "amg_csr_spmv_info": (i32, [vp, vp]),
+    "amg_csr_value_codes": (i32, [vp, vp]),
     "amg_csr_download": (i32, [vp, vp, vp, vp]),
     "amg_gen_laplace3d_7pt": (i32, [vp, i64, i64, i64, P(vp)]),
     "amg_gen_aniso27": (i32, [vp, i64, i64, i64, dbl, dbl, dbl, P(vp)]),
@@ -161,6 +163,12 @@ SPMV_FORMATS = {"auto": 0, "csr": 1, "sell": 2, "vector": 3}
 def set_spmv_format(policy):
     """SpMV storage for matrices built afterwards: 'auto', 'csr', 'sell' or 'vector'."""
     _ck(_lib.amg_set_spmv_format(SPMV_FORMATS[policy]))
+
+
+def set_value_codes(enable):
+    """SELL matrices built afterwards store 4/8/16-bit codes into a per-matrix
+    table of distinct values when they have <= 65536 of them (default True)."""
+    _ck(_lib.amg_set_value_codes(1 if enable else 0))
 
 
 def set_alloc_policy(contiguous):
@@ -365,6 +373,9 @@ class SparseMatOp(LinOp):
                 "slices_implicit", "slices_u16", "slices_i32")
         d = dict(zip(keys, (int(v) for v in info)))
         d["kernel"] = ("csr-stream", "sell", "vector")[d["kernel"]]
+        vc = np.zeros(2, np.int64)
+        _ck(_lib.amg_csr_value_codes(self.h, vc.ctypes.data_as(vp)))
+        d["value_bits"], d["value_table"] = int(vc[0]), int(vc[1])
         return d
 
     def arrays(self):

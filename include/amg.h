@@ -84,6 +84,12 @@ amg_status amg_ctx_join_stream(amg_ctx *ctx, void *other, int32_t ctx_waits);
  * <= 256 long, 3 wave-per-row for every matrix.  Results agree to the summation
  * order of the rows (bitwise for rows summed by one lane). */
 amg_status amg_set_spmv_format(int32_t policy);
+/* Value storage of SELL-64 matrices built after the call (process-wide):
+ * 1 (default) stores a 4 / 8 / 16-bit code per entry into a per-matrix table of
+ * the distinct fp64 bit patterns when the matrix has at most 16 / 256 / 65536 of
+ * them (the padding's 0.0 included); 0 always stores fp64 values.  A decoded
+ * value is the stored value bit for bit, so results do not change. */
+amg_status amg_set_value_codes(int32_t enable);
 /* Device allocation policy for buffers allocated after the call: 1 (default)
  * requests physically contiguous memory for buffers >= 16 MiB (falls back to
  * hipMalloc), 0 always uses hipMalloc. */
@@ -110,6 +116,9 @@ amg_status amg_csr_nnz(const amg_linop *op, int64_t *nnz);
  * 4 (n+1)), SELL slices, SELL stored entries incl. padding, SELL slices with
  * implicit / 16-bit delta / 32-bit column indices}. */
 amg_status amg_csr_spmv_info(const amg_linop *op, int64_t *info8);
+/* Value codes of a CSR operator's SpMV storage: info2 = {code bits (0 = fp64
+ * values, 4, 8, 16), table entries}. */
+amg_status amg_csr_value_codes(const amg_linop *op, int64_t *info2);
 /* Copy a CSR operator back to host arrays (rowptr: nrows+1, colidx/vals: nnz). */
 amg_status amg_csr_download(const amg_linop *op, int64_t *rowptr, int64_t *colidx, double *vals);
 /* Device-side generators for the benchmark operators:

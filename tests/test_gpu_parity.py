@@ -695,3 +695,72 @@ def test_spmm_multi_rhs(ctx, fmt):
                         assert np.all(np.abs(Yh[:, c] - ref) <= spmv_bound(OA.to_scipy(), Xh[:, c]))
     finally:
         fa().set_spmv_format("auto")
+
+
+# ------------------------------------------------------------- value codes
+
+def _with_values(rng, OM, pool):
+    rp, ci, va = OM.arrays()
+    m, n, _ = OM.dims()
+    return O.Csr.from_arrays(m, n, rp, ci, rng.choice(np.asarray(pool, np.float64), size=len(va)))
+
+
+def test_sell_value_codes(ctx):
+    """SELL matrices with <= 16 / 256 / 65536 distinct values store 4 / 8 /
+    16-bit codes into a per-matrix table: the decoded value is the stored
+    value bit for bit, so y = A x is bitwise equal with codes on and off and to
+    the oracle, for implicit, u16 and i32 column blocks; -0.0 and 0.0 keep
+    separate codes; more than 65536 distinct values keep fp64."""
+    rng = np.random.default_rng(61)
+    fa().set_spmv_format("sell")
+    try:
+        cases = [
+            ("7pt", O.laplace3d_7pt(64, 12, 6), (4,)),
+            ("27pt", O.aniso27(64, 9, 5), (4, 8)),
+            ("band-u16", _with_values(rng, _random_rows(rng, 3001, 3001, 12, 2000), rng.standard_normal(200)), (8,)),
+            ("wide-i32", _random_rows(rng, 1000, 400000, 9, 200000), (16,)),
+            ("signed-zeros", _with_values(rng, O.laplace3d_7pt(40, 9, 3), [0.0, -0.0, 1.5, -2.25]), (4,)),
+            ("tail-groups", _with_values(rng, _random_rows(rng, 777, 900, 21, 300), rng.standard_normal(3000)),
+             (16,)),
+            ("fp64", _random_rows(rng, 14000, 14000, 15, 300), (0,)),  # > 65536 distinct values
+        ]
+        for name, OM, bits in cases:
+            fa().set_value_codes(True)
+            M = gpu_csr(ctx, OM)
+            info = M.spmv_info()
+            assert info["kernel"] == "sell" and info["value_bits"] in bits, (name, info)
+            fa().set_value_codes(False)
+            M0 = gpu_csr(ctx, OM)
+            info0 = M0.spmv_info()
+            assert info0["value_bits"] == 0
+            if info["value_bits"]:
+                assert info["stream_bytes"] < info0["stream_bytes"], name
+            x = rng.standard_normal(OM.ncols)
+            y = apply_dev(ctx, M, x, OM.nrows)
+            y0 = apply_dev(ctx, M0, x, OM.nrows)
+            assert np.array_equal(y.view(np.int64), y0.view(np.int64)), name
+            assert np.array_equal(y, OM.spmv(x)), name
+    finally:
+        fa().set_value_codes(True)
+        fa().set_spmv_format("auto")
+
+
+@pytest.mark.parametrize("gen,smoother", [("7pt", "jacobi"), ("27pt", "sgs")])
+def test_vcycle_value_codes_bitwise(ctx, gen, smoother):
+    """The whole V-cycle (every SELL operator of the hierarchy, SGS color
+    sweeps included) is bitwise identical with value codes on and off."""
+    dims = (40, 24, 18) if gen == "7pt" else (20, 16, 14)
+    b = np.random.default_rng(62).uniform(-1, 1, int(np.prod(dims)))
+    outs, bits = [], []
+    try:
+        for codes in (True, False):
+            fa().set_value_codes(codes)
+            A = (fa().SparseMatOp.laplace3d_7pt(ctx, *dims) if gen == "7pt"
+                 else fa().SparseMatOp.aniso27(ctx, *dims, 1.0, 1.0, 0.01))
+            mg = fa().sa_build_box(A, dims, (2, 2, 2), coarsest_dim=200, smoother=smoother)
+            bits.append([mg.level(l)[0].spmv_info()["value_bits"] for l in range(mg.levels())])
+            outs.append(apply_dev(ctx, mg, b, A.nrows))
+    finally:
+        fa().set_value_codes(True)
+    assert any(bits[0]) and not any(bits[1]), bits
+    assert np.array_equal(outs[0].view(np.int64), outs[1].view(np.int64))
