@@ -752,6 +752,7 @@ def test_vcycle_value_codes_bitwise(ctx, gen, smoother):
     dims = (40, 24, 18) if gen == "7pt" else (20, 16, 14)
     b = np.random.default_rng(62).uniform(-1, 1, int(np.prod(dims)))
     outs, bits = [], []
+    fa().set_spmv_format("sell")  # every level in SELL storage (the small 27-pt levels too)
     try:
         for codes in (True, False):
             fa().set_value_codes(codes)
@@ -762,5 +763,6 @@ def test_vcycle_value_codes_bitwise(ctx, gen, smoother):
             outs.append(apply_dev(ctx, mg, b, A.nrows))
     finally:
         fa().set_value_codes(True)
+        fa().set_spmv_format("auto")
     assert any(bits[0]) and not any(bits[1]), bits
     assert np.array_equal(outs[0].view(np.int64), outs[1].view(np.int64))
