@@ -366,16 +366,10 @@ template <int VB> __device__ __forceinline__ int sell_code(const uint32_t (&q)[4
     else return (int)((q[u >> 1] >> (16 * (u & 1))) & 0xffffu);
 }
 
-// R (<= 8) steps of group g: every load of the group is issued before the
-// dependent x gathers; the row sum runs over t ascending.
-template <int MODE, int CM, int VB, int R>
-__device__ __forceinline__ void sellc_group(const char *__restrict__ blkp, const char *__restrict__ ixb, int g,
-                                            const int32_t *__restrict__ bs, int lane, const double *tab,
-                                            const Epi &e, double &acc) {
-    uint32_t q[4];
-    sell_load_codes<VB>(blkp, g, lane, q);
-    const int t0 = 8 * g;
-    int32_t cc[R];
+// Columns of the R (<= 8) steps of group g (first step t0 = 8g).
+template <int CM, int R>
+__device__ __forceinline__ void sell_group_cols(const char *__restrict__ ixb, const int32_t *__restrict__ bs, int t0,
+                                                int lane, int32_t (&cc)[R]) {
     if constexpr (CM == 0) {
 #pragma unroll
         for (int u = 0; u < R; u++) cc[u] = bs[t0 + u] + lane;
@@ -408,11 +402,73 @@ __device__ __forceinline__ void sellc_group(const char *__restrict__ blkp, const
             else cc[u] = __builtin_nontemporal_load(reinterpret_cast<const int32_t *>(ixb) + el + u);
         }
     }
+}
+
+// R (<= 8) steps of group g: every load of the group is issued before the
+// dependent x gathers; the row sum runs over t ascending.
+template <int MODE, int CM, int VB, int R>
+__device__ __forceinline__ void sellc_group(const char *__restrict__ blkp, const char *__restrict__ ixb, int g,
+                                            const int32_t *__restrict__ bs, int lane, const double *tab,
+                                            const Epi &e, double &acc) {
+    uint32_t q[4];
+    sell_load_codes<VB>(blkp, g, lane, q);
+    int32_t cc[R];
+    sell_group_cols<CM, R>(ixb, bs, 8 * g, lane, cc);
     double xx[R];
 #pragma unroll
     for (int u = 0; u < R; u++) xx[u] = gx<MODE>(e, cc[u]);
 #pragma unroll
     for (int u = 0; u < R; u++) acc = fma(tab[sell_code<VB>(q, u)], xx[u], acc);
+}
+
+// The same for two slices of equal width and column mode in lockstep: the
+// loads of both slices are in flight together (a codes slice streams few
+// bytes, so one slice per wave leaves the memory system latency-bound).
+template <int MODE, int CM, int VB, int R>
+__device__ __forceinline__ void sellc_group2(const char *__restrict__ ba, const char *__restrict__ bb,
+                                             const char *__restrict__ ia, const char *__restrict__ ib, int g,
+                                             const int32_t *__restrict__ sa, const int32_t *__restrict__ sb,
+                                             int lane, const double *tab, const Epi &e, double &acca,
+                                             double &accb) {
+    uint32_t qa[4], qb[4];
+    sell_load_codes<VB>(ba, g, lane, qa);
+    sell_load_codes<VB>(bb, g, lane, qb);
+    int32_t ca[R], cb[R];
+    sell_group_cols<CM, R>(ia, sa, 8 * g, lane, ca);
+    sell_group_cols<CM, R>(ib, sb, 8 * g, lane, cb);
+    double xa[R], xb[R];
+#pragma unroll
+    for (int u = 0; u < R; u++) {
+        xa[u] = gx<MODE>(e, ca[u]);
+        xb[u] = gx<MODE>(e, cb[u]);
+    }
+#pragma unroll
+    for (int u = 0; u < R; u++) acca = fma(tab[sell_code<VB>(qa, u)], xa[u], acca);
+#pragma unroll
+    for (int u = 0; u < R; u++) accb = fma(tab[sell_code<VB>(qb, u)], xb[u], accb);
+}
+
+template <int MODE, int CM, int VB>
+__device__ __forceinline__ void sellc_walk2(const char *ba, const char *bb, const int32_t *sa, const int32_t *sb,
+                                            int w, int lane, const double *tab, const Epi &e, double &acca,
+                                            double &accb) {
+    const int ng = (w + 7) >> 3;
+    const char *ia = ba + (int64_t)ng * SELL_C * sell_code_bytes(VB);
+    const char *ib = bb + (int64_t)ng * SELL_C * sell_code_bytes(VB);
+    acca = 0.0;
+    accb = 0.0;
+    const int full = w >> 3;
+    for (int g = 0; g < full; g++) sellc_group2<MODE, CM, VB, 8>(ba, bb, ia, ib, g, sa, sb, lane, tab, e, acca, accb);
+    switch (w & 7) {
+    case 1: sellc_group2<MODE, CM, VB, 1>(ba, bb, ia, ib, full, sa, sb, lane, tab, e, acca, accb); break;
+    case 2: sellc_group2<MODE, CM, VB, 2>(ba, bb, ia, ib, full, sa, sb, lane, tab, e, acca, accb); break;
+    case 3: sellc_group2<MODE, CM, VB, 3>(ba, bb, ia, ib, full, sa, sb, lane, tab, e, acca, accb); break;
+    case 4: sellc_group2<MODE, CM, VB, 4>(ba, bb, ia, ib, full, sa, sb, lane, tab, e, acca, accb); break;
+    case 5: sellc_group2<MODE, CM, VB, 5>(ba, bb, ia, ib, full, sa, sb, lane, tab, e, acca, accb); break;
+    case 6: sellc_group2<MODE, CM, VB, 6>(ba, bb, ia, ib, full, sa, sb, lane, tab, e, acca, accb); break;
+    case 7: sellc_group2<MODE, CM, VB, 7>(ba, bb, ia, ib, full, sa, sb, lane, tab, e, acca, accb); break;
+    default: break;
+    }
 }
 
 template <int MODE, int CM, int VB>
@@ -422,6 +478,9 @@ __device__ __forceinline__ double sellc_walk(const char *blkp, const int32_t *bs
     const char *ixb = blkp + (int64_t)ng * SELL_C * sell_code_bytes(VB);
     double acc = 0.0;
     const int full = w >> 3;
+    // two groups' loads in one block, except RESID0 (two gathers per entry
+    // already; the doubled footprint cost occupancy)
+#pragma unroll(MODE == SPMV_RESID0 ? 1 : 2)
     for (int g = 0; g < full; g++) sellc_group<MODE, CM, VB, 8>(blkp, ixb, g, bs, lane, tab, e, acc);
     switch (w & 7) {
     case 1: sellc_group<MODE, CM, VB, 1>(blkp, ixb, full, bs, lane, tab, e, acc); break;
@@ -436,6 +495,20 @@ __device__ __forceinline__ double sellc_walk(const char *blkp, const int32_t *bs
     return acc;
 }
 
+template <int MODE, int CM, int LAY>
+__device__ __forceinline__ double sellc_walk_any(const char *blkp, const int32_t *bs, int w, int lane,
+                                                 const double *stab, const SellArgs &a) {
+    if constexpr (LAY == 16) return sellc_walk<MODE, CM, 16>(blkp, bs, w, lane, a.vtab, a.e);
+    else return sellc_walk<MODE, CM, LAY>(blkp, bs, w, lane, stab, a.e);
+}
+
+// Slices per wave: one for fp64 values, two (in lockstep when their width and
+// column mode agree) for value codes -- except RESID0, whose rows gather two
+// vectors (d and x) and which ran slower with the doubled register footprint.
+__host__ __device__ constexpr int sell_slices_per_wave(int lay, int mode) {
+    return lay >= 4 && mode != SPMV_RESID0 ? 2 : 1;
+}
+
 // LAY: 0 one step per 512-B row, 1 step pairs (fp64 values); 4 / 8 / 16 value codes
 template <int MODE, int LAY>
 __global__ __launch_bounds__(256) void spmv_sell_kernel(SellArgs a) {
@@ -445,8 +518,9 @@ __global__ __launch_bounds__(256) void spmv_sell_kernel(SellArgs a) {
         for (int i = threadIdx.x; i < a.ntab; i += 256) stab[i] = a.vtab[i];
         __syncthreads();
     }
+    constexpr int SPW = sell_slices_per_wave(LAY, MODE);
     const int blk = xcd_remap(blockIdx.x, gridDim.x);
-    const int sl = __builtin_amdgcn_readfirstlane(blk * 4 + (int)(threadIdx.x >> 6));
+    const int sl = __builtin_amdgcn_readfirstlane((blk * 4 + (int)(threadIdx.x >> 6)) * SPW);
     if (sl >= a.nslices) return;
     const int slice = a.slice0 + sl;
     const int lane = threadIdx.x & 63;
@@ -460,18 +534,52 @@ __global__ __launch_bounds__(256) void spmv_sell_kernel(SellArgs a) {
     const char *blkp = a.data + (int64_t)(d & 0x3fffffffu) * 128;
     const int32_t *bs = a.base + t0;
     double acc;
-    if constexpr (LAY == 16) {
+    if constexpr (LAY >= 4 && SPW == 1) {
         switch (d >> 30) {
-        case 0: acc = sellc_walk<MODE, 0, 16>(blkp, bs, w, lane, a.vtab, a.e); break;
-        case 1: acc = sellc_walk<MODE, 1, 16>(blkp, bs, w, lane, a.vtab, a.e); break;
-        default: acc = sellc_walk<MODE, 2, 16>(blkp, bs, w, lane, a.vtab, a.e); break;
+        case 0: acc = sellc_walk_any<MODE, 0, LAY>(blkp, bs, w, lane, stab, a); break;
+        case 1: acc = sellc_walk_any<MODE, 1, LAY>(blkp, bs, w, lane, stab, a); break;
+        default: acc = sellc_walk_any<MODE, 2, LAY>(blkp, bs, w, lane, stab, a); break;
         }
-    } else if constexpr (LAY == 4 || LAY == 8) {
-        switch (d >> 30) {
-        case 0: acc = sellc_walk<MODE, 0, LAY>(blkp, bs, w, lane, stab, a.e); break;
-        case 1: acc = sellc_walk<MODE, 1, LAY>(blkp, bs, w, lane, stab, a.e); break;
-        default: acc = sellc_walk<MODE, 2, LAY>(blkp, bs, w, lane, stab, a.e); break;
+    } else if constexpr (LAY >= 4) {
+        // second slice of the wave
+        const bool two = sl + 1 < a.nslices;
+        int rowb = 0, wb = 0;
+        bool liveb = false;
+        uint32_t db = 0;
+        EpiOps<MODE> epb;
+        if (two) {
+            rowb = a.row0[slice + 1] + lane;
+            liveb = rowb < a.row0[slice + 2];
+            if (liveb) epb.load(a.e, rowb);
+            wb = a.soff[slice + 2] - a.soff[slice + 1];
+            db = a.desc[slice + 1];
         }
+        const char *blkb = a.data + (int64_t)(db & 0x3fffffffu) * 128;
+        const int32_t *bsb = a.base + t0 + w;
+        double accb = 0.0;
+        if (two && wb == w && (db >> 30) == (d >> 30)) {
+            switch (d >> 30) {
+            case 0: sellc_walk2<MODE, 0, LAY>(blkp, blkb, bs, bsb, w, lane, LAY == 16 ? a.vtab : stab, a.e, acc, accb); break;
+            case 1: sellc_walk2<MODE, 1, LAY>(blkp, blkb, bs, bsb, w, lane, LAY == 16 ? a.vtab : stab, a.e, acc, accb); break;
+            default: sellc_walk2<MODE, 2, LAY>(blkp, blkb, bs, bsb, w, lane, LAY == 16 ? a.vtab : stab, a.e, acc, accb); break;
+            }
+        } else {
+            switch (d >> 30) {
+            case 0: acc = sellc_walk_any<MODE, 0, LAY>(blkp, bs, w, lane, stab, a); break;
+            case 1: acc = sellc_walk_any<MODE, 1, LAY>(blkp, bs, w, lane, stab, a); break;
+            default: acc = sellc_walk_any<MODE, 2, LAY>(blkp, bs, w, lane, stab, a); break;
+            }
+            if (two) {
+                switch (db >> 30) {
+                case 0: accb = sellc_walk_any<MODE, 0, LAY>(blkb, bsb, wb, lane, stab, a); break;
+                case 1: accb = sellc_walk_any<MODE, 1, LAY>(blkb, bsb, wb, lane, stab, a); break;
+                default: accb = sellc_walk_any<MODE, 2, LAY>(blkb, bsb, wb, lane, stab, a); break;
+                }
+            }
+        }
+        if (live) ep.store(a.e, acc);
+        if (liveb) epb.store(a.e, accb);
+        return;
     } else if constexpr (LAY == 1) {
         switch (d >> 30) {
         case 0: acc = sell_walk_pairs<MODE, 0>(blkp, bs, w, lane, a.e); break;
@@ -977,7 +1085,7 @@ void spmv(const GpuCsr &m, const double *x, double *y, SpmvMode mode, const Spmv
         SellArgs a{m.sell_row0.get(), m.sell_soff.get(), m.sell_desc.get(), m.sell_base.get(),
                    m.sell_data.get(), (int32_t)s0, (int32_t)(s1 - s0), e, m.sell_vtab.get(),
                    (int32_t)m.sell_ntab};
-        const dim3 grid((unsigned)ceil_div(s1 - s0, 4));
+        const dim3 grid((unsigned)ceil_div(s1 - s0, 4 * sell_slices_per_wave(m.sell_vbits ? 4 : 0, mode)));
         if (m.sell_vbits == 4) {
             FAMG_LAUNCH_MODES(spmv_sell_kernel, grid, block, s, a, FAMG_LAY4)
         } else if (m.sell_vbits == 8) {

@@ -414,6 +414,7 @@ def test_vcycle_fold_and_sell_layout_bitwise(ctx, layout):
     old = os.environ.get("FAMG_SELL_LAYOUT")
     os.environ["FAMG_SELL_LAYOUT"] = layout
     fa().set_spmv_format("sell")
+    fa().set_value_codes(False)  # the fold applies to fp64-valued storage
     try:
         dims = (70, 20, 12)  # > 1 slice per x-line, tail slices
         A = fa().SparseMatOp.laplace3d_7pt(ctx, *dims)
@@ -433,6 +434,7 @@ def test_vcycle_fold_and_sell_layout_bitwise(ctx, layout):
         assert np.array_equal(apply_dev(ctx, A, x, A.nrows), OA.spmv(x))
     finally:
         fa().set_spmv_format("auto")
+        fa().set_value_codes(True)
         if old is None:
             os.environ.pop("FAMG_SELL_LAYOUT", None)
         else:
