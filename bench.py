@@ -167,8 +167,9 @@ def vcycle_bytes(mg, csr=False, fold=True):
             continue
         bA = mat(A)
         nc = R.nrows
-        # the library folds only diagonal smoothers on fp64-valued storage
-        fold = fold_all and S.kind == "diag" and A.spmv_info()["value_bits"] == 0
+        # the library folds only diagonal smoothers on fp64-valued SELL storage
+        info = A.spmv_info()
+        fold = fold_all and S.kind == "diag" and info["kernel"] == "sell" and info["value_bits"] == 0
         tot += 0 if fold else 24 * n                   # first smoothing step from 0
         tot += bA + 24 * n                             # residual
         tot += mat(R) + 8 * n + 8 * nc                 # restrict

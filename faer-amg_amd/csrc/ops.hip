@@ -457,11 +457,12 @@ void MultigridOp::cycle(int64_t l, double *v, const double *f, bool v_zero, doub
     // One Jacobi step from v = 0 gives v = d*f; with s = 1 nothing else reads
     // v before the correction, so the residual gathers d*f on the fly and the
     // correction writes d*f + P v_c: the same rounded values, 16n bytes and one
-    // launch fewer per level.  Only for fp64-valued storage: with value codes
-    // the residual is latency-bound and gathering d beside x cost more than the
-    // separate streaming pass (measured on the 256^3 hierarchy).
+    // launch fewer per level.  Only for bandwidth-bound storage (SELL with fp64
+    // values): value-code SELL and the wave-per-row kernel are latency-bound,
+    // and gathering d beside x cost more there than the separate streaming
+    // pass (measured on the 256^3 hierarchy).
     const bool fold = fold_zero_guess && v_zero && steps == 1 && A && D && P &&
-                      !(A->m.kernel == SPMV_KERNEL_SELL && A->m.sell_vbits);
+                      A->m.kernel == SPMV_KERNEL_SELL && A->m.sell_vbits == 0;
     if (fold) {
         SpmvEpi epi;
         epi.b = f;

@@ -191,7 +191,8 @@ amg_status amg_multigrid_set_graph(amg_linop *mg, int32_t enable);
  * residual form of smooth() (multigrid.rs:418-423: r = f - A x; x += SGS(r))
  * instead of the fused in-place sweep on x (default 0: fused, one SpMV fewer);
  * 2 = fold the first Jacobi step from v = 0 (v = d f, s = 1) into the residual
- * and correction SpMVs instead of storing it (default 1; bitwise identical). */
+ * and correction SpMVs instead of storing it, on levels whose operator is SELL
+ * storage with fp64 values (default 1; bitwise identical). */
 amg_status amg_multigrid_set_option(amg_linop *mg, int32_t option, int64_t value);
 /* Multigrid::apply == amg_linop_apply on a multigrid handle. */
 amg_status amg_multigrid_apply(amg_linop *mg, double *out, int64_t ld_out, const double *rhs,
