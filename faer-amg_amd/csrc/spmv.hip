@@ -495,6 +495,175 @@ __device__ __forceinline__ double sellc_walk(const char *blkp, const int32_t *bs
     return acc;
 }
 
+// ---- lockstep pair, two adjacent rows per lane
+//
+// Lanes 0-31 take rows 2h, 2h+1 (h = lane & 31) of slice A, lanes 32-63 the
+// same rows of slice B.  A value-code slice streams few matrix bytes, so its
+// time goes to the vector accesses; with two rows per lane the codes, the
+// column blocks, x (implicit columns), b, d and y all move in 16-B accesses
+// (8-B-per-lane accesses run at ~0.5-0.7x the 16-B rate on MI355X).  Each row
+// is still summed by one lane in ascending steps: bitwise unchanged.
+typedef double dbl2u_t __attribute__((ext_vector_type(2), aligned(8)));
+
+template <int MODE, int CM, int VB, int R>
+__device__ __forceinline__ void sellc_group_rp(const char *__restrict__ blk, const char *__restrict__ ixb, int g,
+                                               const int32_t *__restrict__ sa, const int32_t *__restrict__ sb,
+                                               bool hb, int r0, const double *tab, const Epi &e, double &acc0,
+                                               double &acc1) {
+    const int t0 = 8 * g;
+    uint32_t q0[4], q1[4];
+    if constexpr (VB == 4) {
+        const i32x2_t v = __builtin_nontemporal_load(reinterpret_cast<const i32x2_t *>(blk) + ((int64_t)g * SELL_C + r0) / 2);
+        q0[0] = (uint32_t)v.x;
+        q1[0] = (uint32_t)v.y;
+    } else if constexpr (VB == 8) {
+        const i32x4_t v = __builtin_nontemporal_load(reinterpret_cast<const i32x4_t *>(blk) + ((int64_t)g * SELL_C + r0) / 2);
+        q0[0] = (uint32_t)v.x;
+        q0[1] = (uint32_t)v.y;
+        q1[0] = (uint32_t)v.z;
+        q1[1] = (uint32_t)v.w;
+    } else {
+        const i32x4_t *p = reinterpret_cast<const i32x4_t *>(blk) + (int64_t)g * SELL_C + r0;
+        const i32x4_t v0 = __builtin_nontemporal_load(p);
+        const i32x4_t v1 = __builtin_nontemporal_load(p + 1);
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            q0[k] = (uint32_t)v0[k];
+            q1[k] = (uint32_t)v1[k];
+        }
+    }
+    int32_t bse[R];
+#pragma unroll
+    for (int u = 0; u < R; u++) bse[u] = hb ? sb[t0 + u] : sa[t0 + u];
+    int32_t c0[R], c1[R];
+    if constexpr (CM == 0) {
+#pragma unroll
+        for (int u = 0; u < R; u++) {
+            c0[u] = bse[u] + r0;
+            c1[u] = c0[u] + 1;
+        }
+    } else if constexpr (R == 8) {
+        const int64_t el = (int64_t)t0 * SELL_C + 8 * r0;  // row r0: 8 elements, then row r0 + 1
+        if constexpr (CM == 1) {
+            const i32x4_t *p = reinterpret_cast<const i32x4_t *>(ixb + 2 * el);
+            const i32x4_t d0 = __builtin_nontemporal_load(p);
+            const i32x4_t d1 = __builtin_nontemporal_load(p + 1);
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                c0[2 * u] = bse[2 * u] + (int32_t)((uint32_t)d0[u] & 0xffffu);
+                c0[2 * u + 1] = bse[2 * u + 1] + (int32_t)((uint32_t)d0[u] >> 16);
+                c1[2 * u] = bse[2 * u] + (int32_t)((uint32_t)d1[u] & 0xffffu);
+                c1[2 * u + 1] = bse[2 * u + 1] + (int32_t)((uint32_t)d1[u] >> 16);
+            }
+        } else {
+            const i32x4_t *p = reinterpret_cast<const i32x4_t *>(ixb + 4 * el);
+            const i32x4_t d0 = __builtin_nontemporal_load(p), d1 = __builtin_nontemporal_load(p + 1);
+            const i32x4_t d2 = __builtin_nontemporal_load(p + 2), d3 = __builtin_nontemporal_load(p + 3);
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                c0[u] = d0[u];
+                c0[4 + u] = d1[u];
+                c1[u] = d2[u];
+                c1[4 + u] = d3[u];
+            }
+        }
+    } else {
+        const int64_t el = (int64_t)t0 * SELL_C + R * r0;  // row r0: R elements, then row r0 + 1
+#pragma unroll
+        for (int u = 0; u < R; u++) {
+            if constexpr (CM == 1) {
+                const uint16_t *p = reinterpret_cast<const uint16_t *>(ixb) + el;
+                c0[u] = bse[u] + (int32_t)__builtin_nontemporal_load(p + u);
+                c1[u] = bse[u] + (int32_t)__builtin_nontemporal_load(p + R + u);
+            } else {
+                const int32_t *p = reinterpret_cast<const int32_t *>(ixb) + el;
+                c0[u] = __builtin_nontemporal_load(p + u);
+                c1[u] = __builtin_nontemporal_load(p + R + u);
+            }
+        }
+    }
+    double x0[R], x1[R];
+#pragma unroll
+    for (int u = 0; u < R; u++) {
+        if constexpr (CM == 0) {
+            const dbl2_t v = *reinterpret_cast<const dbl2u_t *>(e.x + c0[u]);
+            x0[u] = v.x;
+            x1[u] = v.y;
+        } else {
+            x0[u] = e.x[c0[u]];
+            x1[u] = e.x[c1[u]];
+        }
+    }
+#pragma unroll
+    for (int u = 0; u < R; u++) acc0 = fma(tab[sell_code<VB>(q0, u)], x0[u], acc0);
+#pragma unroll
+    for (int u = 0; u < R; u++) acc1 = fma(tab[sell_code<VB>(q1, u)], x1[u], acc1);
+}
+
+template <int MODE, int CM, int VB>
+__device__ __forceinline__ void sellc_walk_rp(const char *ba, const char *bb, const int32_t *sa, const int32_t *sb,
+                                              int w, int lane, const double *tab, const Epi &e, double &acc0,
+                                              double &acc1) {
+    const bool hb = lane >= 32;
+    const int r0 = 2 * (lane & 31);
+    const char *blk = hb ? bb : ba;
+    const int ng = (w + 7) >> 3;
+    const char *ixb = blk + (int64_t)ng * SELL_C * sell_code_bytes(VB);
+    acc0 = 0.0;
+    acc1 = 0.0;
+    const int full = w >> 3;
+    for (int g = 0; g < full; g++) sellc_group_rp<MODE, CM, VB, 8>(blk, ixb, g, sa, sb, hb, r0, tab, e, acc0, acc1);
+    switch (w & 7) {
+    case 1: sellc_group_rp<MODE, CM, VB, 1>(blk, ixb, full, sa, sb, hb, r0, tab, e, acc0, acc1); break;
+    case 2: sellc_group_rp<MODE, CM, VB, 2>(blk, ixb, full, sa, sb, hb, r0, tab, e, acc0, acc1); break;
+    case 3: sellc_group_rp<MODE, CM, VB, 3>(blk, ixb, full, sa, sb, hb, r0, tab, e, acc0, acc1); break;
+    case 4: sellc_group_rp<MODE, CM, VB, 4>(blk, ixb, full, sa, sb, hb, r0, tab, e, acc0, acc1); break;
+    case 5: sellc_group_rp<MODE, CM, VB, 5>(blk, ixb, full, sa, sb, hb, r0, tab, e, acc0, acc1); break;
+    case 6: sellc_group_rp<MODE, CM, VB, 6>(blk, ixb, full, sa, sb, hb, r0, tab, e, acc0, acc1); break;
+    case 7: sellc_group_rp<MODE, CM, VB, 7>(blk, ixb, full, sa, sb, hb, r0, tab, e, acc0, acc1); break;
+    default: break;
+    }
+}
+
+// Epilogue of two adjacent rows (row, row + 1) with 16-B accesses when both live.
+template <int MODE> struct EpiOps2 {
+    dbl2_t xr = {0.0, 0.0}, br = {0.0, 0.0}, dr = {0.0, 0.0}, yr = {0.0, 0.0};
+    int i = 0;
+    bool l0 = false, l1 = false;
+    __device__ __forceinline__ dbl2_t ld(const double *p) const {
+        if (l1) return *reinterpret_cast<const dbl2u_t *>(p + i);
+        dbl2_t v = {p[i], 0.0};
+        return v;
+    }
+    __device__ __forceinline__ void load(const Epi &a, int row, bool live0, bool live1) {
+        i = row;
+        l0 = live0;
+        l1 = live1;
+        if (!l0) return;
+        if constexpr (MODE == SPMV_JACOBI) { xr = ld(a.x); br = ld(a.b); dr = ld(a.d); }
+        if constexpr (MODE == SPMV_RESID) br = ld(a.b);
+        if constexpr (MODE == SPMV_ADD) yr = ld(a.y);
+        if constexpr (MODE == SPMV_ADD0) yr = ld(a.d) * ld(a.b);
+    }
+    __device__ __forceinline__ void store(const Epi &a, double acc0, double acc1) const {
+        if (!l0) return;
+        const dbl2_t acc = {acc0, acc1};
+        dbl2_t out;
+        if constexpr (MODE == SPMV_SET) out = acc;
+        else if constexpr (MODE == SPMV_ADD || MODE == SPMV_ADD0) out = yr + acc;
+        else if constexpr (MODE == SPMV_RESID) out = br - acc;
+        else out = xr + dr * (br - acc);  // JACOBI
+        if (l1) *reinterpret_cast<dbl2u_t *>(a.y + i) = out;
+        else a.y[i] = out.x;
+    }
+};
+
+template <int MODE>
+__host__ __device__ constexpr bool sell_row_pairs(int lay) {
+    return lay >= 4 && (MODE == SPMV_SET || MODE == SPMV_ADD || MODE == SPMV_RESID || MODE == SPMV_JACOBI ||
+                        MODE == SPMV_ADD0);
+}
+
 template <int MODE, int CM, int LAY>
 __device__ __forceinline__ double sellc_walk_any(const char *blkp, const int32_t *bs, int w, int lane,
                                                  const double *stab, const SellArgs &a) {
@@ -511,19 +680,36 @@ __host__ __device__ constexpr int sell_slices_per_wave(int lay, int mode) {
 
 // LAY: 0 one step per 512-B row, 1 step pairs (fp64 values); 4 / 8 / 16 value codes
 template <int MODE, int LAY>
-__global__ __launch_bounds__(256) void spmv_sell_kernel(SellArgs a) {
-    constexpr int TABN = LAY == 4 ? 16 : LAY == 8 ? 256 : 1;
-    __shared__ double stab[TABN];
-    if constexpr (LAY == 4 || LAY == 8) {
-        for (int i = threadIdx.x; i < a.ntab; i += 256) stab[i] = a.vtab[i];
-        __syncthreads();
-    }
-    constexpr int SPW = sell_slices_per_wave(LAY, MODE);
-    const int blk = xcd_remap(blockIdx.x, gridDim.x);
-    const int sl = __builtin_amdgcn_readfirstlane((blk * 4 + (int)(threadIdx.x >> 6)) * SPW);
-    if (sl >= a.nslices) return;
+__device__ __forceinline__ void sell_wave(const SellArgs &a, const double *stab, int sl) {
     const int slice = a.slice0 + sl;
     const int lane = threadIdx.x & 63;
+    if constexpr (sell_row_pairs<MODE>(LAY) && sell_slices_per_wave(LAY, MODE) == 2) {
+        // two slices of equal width and column mode: two adjacent rows per lane
+        if (sl + 1 < a.nslices) {
+            const int ta = a.soff[slice], tb = a.soff[slice + 1], te = a.soff[slice + 2];
+            const uint32_t da = a.desc[slice], db = a.desc[slice + 1];
+            if (tb - ta == te - tb && (da >> 30) == (db >> 30)) {
+                const bool hb = lane >= 32;
+                const int rs = hb ? a.row0[slice + 1] : a.row0[slice];
+                const int re = hb ? a.row0[slice + 2] : a.row0[slice + 1];
+                const int row = rs + 2 * (lane & 31);
+                EpiOps2<MODE> ep2;
+                ep2.load(a.e, row, row < re, row + 1 < re);
+                const char *ba = a.data + (int64_t)(da & 0x3fffffffu) * 128;
+                const char *bb = a.data + (int64_t)(db & 0x3fffffffu) * 128;
+                const int32_t *sa = a.base + ta, *sbp = a.base + tb;
+                const double *tab = LAY == 16 ? a.vtab : stab;
+                double acc0, acc1;
+                switch (da >> 30) {
+                case 0: sellc_walk_rp<MODE, 0, LAY>(ba, bb, sa, sbp, tb - ta, lane, tab, a.e, acc0, acc1); break;
+                case 1: sellc_walk_rp<MODE, 1, LAY>(ba, bb, sa, sbp, tb - ta, lane, tab, a.e, acc0, acc1); break;
+                default: sellc_walk_rp<MODE, 2, LAY>(ba, bb, sa, sbp, tb - ta, lane, tab, a.e, acc0, acc1); break;
+                }
+                ep2.store(a.e, acc0, acc1);
+                return;
+            }
+        }
+    }
     const int row = a.row0[slice] + lane;
     const bool live = row < a.row0[slice + 1];
     EpiOps<MODE> ep;
@@ -534,7 +720,7 @@ __global__ __launch_bounds__(256) void spmv_sell_kernel(SellArgs a) {
     const char *blkp = a.data + (int64_t)(d & 0x3fffffffu) * 128;
     const int32_t *bs = a.base + t0;
     double acc;
-    if constexpr (LAY >= 4 && SPW == 1) {
+    if constexpr (LAY >= 4 && sell_slices_per_wave(LAY, MODE) == 1) {
         switch (d >> 30) {
         case 0: acc = sellc_walk_any<MODE, 0, LAY>(blkp, bs, w, lane, stab, a); break;
         case 1: acc = sellc_walk_any<MODE, 1, LAY>(blkp, bs, w, lane, stab, a); break;
@@ -594,6 +780,30 @@ __global__ __launch_bounds__(256) void spmv_sell_kernel(SellArgs a) {
         }
     }
     if (live) ep.store(a.e, acc);
+}
+
+
+// Consecutive slice groups per wave (1: four per wave made the small coarse
+// levels launch too few waves and did not speed up the fine level).
+__host__ __device__ constexpr int sell_groups_per_wave(int) { return 1; }
+
+template <int MODE, int LAY>
+__global__ __launch_bounds__(256) void spmv_sell_kernel(SellArgs a) {
+    constexpr int TABN = LAY == 4 ? 16 : LAY == 8 ? 256 : 1;
+    __shared__ double stab[TABN];
+    if constexpr (LAY == 4 || LAY == 8) {
+        for (int i = threadIdx.x; i < a.ntab; i += 256) stab[i] = a.vtab[i];
+        __syncthreads();
+    }
+    constexpr int SPW = sell_slices_per_wave(LAY, MODE);
+    constexpr int NSEQ = sell_groups_per_wave(LAY);
+    const int blk = xcd_remap(blockIdx.x, gridDim.x);
+    const int wv = __builtin_amdgcn_readfirstlane(blk * 4 + (int)(threadIdx.x >> 6));
+    for (int k = 0; k < NSEQ; k++) {
+        const int sl = (wv * NSEQ + k) * SPW;
+        if (sl >= a.nslices) return;
+        sell_wave<MODE, LAY>(a, stab, sl);
+    }
 }
 
 // SpMM: Y = A X for up to SPMM_KB columns per launch (column-major X, Y with
@@ -1085,7 +1295,8 @@ void spmv(const GpuCsr &m, const double *x, double *y, SpmvMode mode, const Spmv
         SellArgs a{m.sell_row0.get(), m.sell_soff.get(), m.sell_desc.get(), m.sell_base.get(),
                    m.sell_data.get(), (int32_t)s0, (int32_t)(s1 - s0), e, m.sell_vtab.get(),
                    (int32_t)m.sell_ntab};
-        const dim3 grid((unsigned)ceil_div(s1 - s0, 4 * sell_slices_per_wave(m.sell_vbits ? 4 : 0, mode)));
+        const int lay = m.sell_vbits ? 4 : 0;
+        const dim3 grid((unsigned)ceil_div(s1 - s0, 4 * sell_slices_per_wave(lay, mode) * sell_groups_per_wave(lay)));
         if (m.sell_vbits == 4) {
             FAMG_LAUNCH_MODES(spmv_sell_kernel, grid, block, s, a, FAMG_LAY4)
         } else if (m.sell_vbits == 8) {
