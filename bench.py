@@ -309,7 +309,7 @@ def run_single(args):
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                      "traffic_source": traffic_src,
-                     "kernel": f"spmv_{'sell' if info['kernel'] == 'sell' else info['kernel']}_kernel<SET> on A_0",
+                     "kernel": f"spmv_{info['kernel'].replace('-', '_')}_kernel<SET> on A_0",
                      "storage": info,
                      "bytes_per_launch": bytes_spmv, "ms_per_launch": round(spmv_ms, 5),
                      "csr_bytes_per_launch": bytes_csr,

@@ -239,7 +239,7 @@ amg_status amg_csr_value_codes(const amg_linop *op, int64_t *info2) {
     return guard([&] {
         FAMG_REQUIRE(info2, AMG_ERR_INVALID, "null argument");
         const GpuCsr &m = need_csr(op)->m;
-        const bool sell = m.kernel == SPMV_KERNEL_SELL;
+        const bool sell = m.kernel == SPMV_KERNEL_SELL || m.kernel == SPMV_KERNEL_DIA;
         info2[0] = sell ? m.sell_vbits : 0;
         info2[1] = sell ? m.sell_ntab : 0;
     });

@@ -55,12 +55,19 @@ struct GpuCsr {
     int sell_vbits = 0;
     int64_t sell_ntab = 0;
     DevBuf<double> sell_vtab;
+    // DIA codes (spmv.hip "DIA codes"): dia_cw words of codes per row for the
+    // dia_k diagonals dia_off (ascending); value table = sell_vtab
+    DevBuf<uint32_t> dia_codes;
+    int dia_k = 0, dia_cw = 0;
+    std::vector<int> dia_off;
     int kernel = 0;  // SpmvKernel chosen at finalize
     bool spmv_ready() const { return rp32.get() != nullptr && sched.get() != nullptr; }
     bool has_sell() const { return sell_desc.get() != nullptr; }
+    bool has_dia() const { return dia_codes.get() != nullptr; }
     int64_t index_bytes() const { return 12 * nnz + 4 * (nrows + 1); }
     // matrix bytes one SpMV streams with the chosen kernel (data + metadata)
     int64_t stream_bytes() const {
+        if (kernel == 3) return 4 * dia_cw * nrows + 8 * sell_ntab;
         return kernel == 1 ? sell_bytes + 12 * (nslices + 1) + 4 * sell_steps + 8 * sell_ntab : index_bytes();
     }
 };
@@ -78,7 +85,7 @@ extern int g_spmv_format_policy;
 // Value codes for SELL matrices finalized afterwards (1 = when <= 65536
 // distinct values, 0 = always fp64 values)
 extern int g_value_codes;
-enum SpmvKernel : int { SPMV_KERNEL_STREAM = 0, SPMV_KERNEL_SELL = 1, SPMV_KERNEL_VECTOR = 2 };
+enum SpmvKernel : int { SPMV_KERNEL_STREAM = 0, SPMV_KERNEL_SELL = 1, SPMV_KERNEL_VECTOR = 2, SPMV_KERNEL_DIA = 3 };
 void build_sell(GpuCsr &m, const std::vector<int64_t> &rp);
 void choose_kernel(GpuCsr &m);
 // Host upload from usize-compatible arrays.

@@ -480,7 +480,8 @@ __device__ __forceinline__ double sellc_walk(const char *blkp, const int32_t *bs
     const int full = w >> 3;
     // two groups' loads in one block, except RESID0 (two gathers per entry
     // already; the doubled footprint cost occupancy)
-#pragma unroll(MODE == SPMV_RESID0 ? 1 : 2)
+    constexpr int UNR = MODE == SPMV_RESID0 ? 1 : 2;
+#pragma unroll UNR
     for (int g = 0; g < full; g++) sellc_group<MODE, CM, VB, 8>(blkp, ixb, g, bs, lane, tab, e, acc);
     switch (w & 7) {
     case 1: sellc_group<MODE, CM, VB, 1>(blkp, ixb, full, bs, lane, tab, e, acc); break;
@@ -641,7 +642,7 @@ template <int MODE> struct EpiOps2 {
         l1 = live1;
         if (!l0) return;
         if constexpr (MODE == SPMV_JACOBI) { xr = ld(a.x); br = ld(a.b); dr = ld(a.d); }
-        if constexpr (MODE == SPMV_RESID) br = ld(a.b);
+        if constexpr (MODE == SPMV_RESID || MODE == SPMV_RESID0) br = ld(a.b);
         if constexpr (MODE == SPMV_ADD) yr = ld(a.y);
         if constexpr (MODE == SPMV_ADD0) yr = ld(a.d) * ld(a.b);
     }
@@ -651,7 +652,7 @@ template <int MODE> struct EpiOps2 {
         dbl2_t out;
         if constexpr (MODE == SPMV_SET) out = acc;
         else if constexpr (MODE == SPMV_ADD || MODE == SPMV_ADD0) out = yr + acc;
-        else if constexpr (MODE == SPMV_RESID) out = br - acc;
+        else if constexpr (MODE == SPMV_RESID || MODE == SPMV_RESID0) out = br - acc;
         else out = xr + dr * (br - acc);  // JACOBI
         if (l1) *reinterpret_cast<dbl2u_t *>(a.y + i) = out;
         else a.y[i] = out.x;
@@ -804,6 +805,99 @@ __global__ __launch_bounds__(256) void spmv_sell_kernel(SellArgs a) {
         if (sl >= a.nslices) return;
         sell_wave<MODE, LAY>(a, stab, sl);
     }
+}
+
+// ---------------------------------------------------------------- DIA codes
+//
+// A square matrix whose entries lie on at most DIA_MAX diagonals (the union of
+// col - row offsets; a constant stencil: 7 for the 7-pt Laplacian, 27 for the
+// 27-pt operator), that fills them to >= 80 % and whose values have a 4/8-bit
+// value table is stored as one code word group per row: the codes of its K
+// diagonals, ascending offset (= ascending column, the stored order), with
+// the +0.0 code where a row has no entry.  No per-slice metadata exists, so a
+// row's only dependent chain is code + x loads -> fma -> store; each lane takes
+// two adjacent rows (16-B accesses throughout).  x indices outside [0, ncols)
+// belong to padding entries (value 0.0) and are clamped.
+constexpr int DIA_MAX = 32;
+
+struct DiaArgs {
+    const uint32_t *codes;  // cw words per row (rows padded by 2)
+    const double *vtab;
+    int32_t ntab, k, row_begin, row_end, ncols;
+    int32_t off[DIA_MAX];
+    Epi e;
+};
+
+typedef int32_t i32x2u_t __attribute__((ext_vector_type(2), aligned(4)));
+typedef int32_t i32x4u_t __attribute__((ext_vector_type(4), aligned(4)));
+
+template <int MODE> __device__ __forceinline__ void dia_gx2(const Epi &e, int c, int ncols, double &x0, double &x1) {
+    if (c >= 0 && c + 1 < ncols) {
+        const dbl2_t v = *reinterpret_cast<const dbl2u_t *>(e.x + c);
+        if constexpr (MODE == SPMV_RESID0) {
+            const dbl2_t d = *reinterpret_cast<const dbl2u_t *>(e.d + c);
+            x0 = d.x * v.x;
+            x1 = d.y * v.y;
+        } else {
+            x0 = v.x;
+            x1 = v.y;
+        }
+    } else {
+        const int c0 = min(max(c, 0), ncols - 1), c1 = min(max(c + 1, 0), ncols - 1);
+        x0 = gx<MODE>(e, c0);
+        x1 = gx<MODE>(e, c1);
+    }
+}
+
+template <int MODE, int VB, int CW>
+__global__ __launch_bounds__(256) void spmv_dia_kernel(DiaArgs a) {
+    __shared__ double stab[VB == 4 ? 16 : 256];
+    for (int i = threadIdx.x; i < a.ntab; i += 256) stab[i] = a.vtab[i];
+    __syncthreads();
+    const int blk = xcd_remap(blockIdx.x, gridDim.x);
+    const int row = a.row_begin + 2 * (blk * 256 + (int)threadIdx.x);
+    if (row >= a.row_end) return;
+    EpiOps2<MODE> ep;
+    ep.load(a.e, row, true, row + 1 < a.row_end);
+    uint32_t w0[CW], w1[CW];
+    const uint32_t *cp = a.codes + (int64_t)row * CW;
+    if constexpr (CW == 1) {
+        const i32x2u_t v = __builtin_nontemporal_load(reinterpret_cast<const i32x2u_t *>(cp));
+        w0[0] = (uint32_t)v.x;
+        w1[0] = (uint32_t)v.y;
+    } else if constexpr (CW == 2) {
+        const i32x4u_t v = __builtin_nontemporal_load(reinterpret_cast<const i32x4u_t *>(cp));
+        w0[0] = (uint32_t)v.x;
+        w0[1] = (uint32_t)v.y;
+        w1[0] = (uint32_t)v.z;
+        w1[1] = (uint32_t)v.w;
+    } else {
+#pragma unroll
+        for (int q = 0; q < CW / 4; q++) {
+            const i32x4u_t v0 = __builtin_nontemporal_load(reinterpret_cast<const i32x4u_t *>(cp) + q);
+            const i32x4u_t v1 = __builtin_nontemporal_load(reinterpret_cast<const i32x4u_t *>(cp + CW) + q);
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                w0[4 * q + j] = (uint32_t)v0[j];
+                w1[4 * q + j] = (uint32_t)v1[j];
+            }
+        }
+    }
+    constexpr int KMAX = CW * 32 / VB < DIA_MAX ? CW * 32 / VB : DIA_MAX;
+    constexpr uint32_t MASK = (1u << VB) - 1;
+    double x0[KMAX], x1[KMAX];
+#pragma unroll
+    for (int k = 0; k < KMAX; k++)
+        if (k < a.k) dia_gx2<MODE>(a.e, row + a.off[k], a.ncols, x0[k], x1[k]);
+    double acc0 = 0.0, acc1 = 0.0;
+#pragma unroll
+    for (int k = 0; k < KMAX; k++) {
+        if (k < a.k) {
+            acc0 = fma(stab[(w0[(k * VB) >> 5] >> ((k * VB) & 31)) & MASK], x0[k], acc0);
+            acc1 = fma(stab[(w1[(k * VB) >> 5] >> ((k * VB) & 31)) & MASK], x1[k], acc1);
+        }
+    }
+    ep.store(a.e, acc0, acc1);
 }
 
 // SpMM: Y = A X for up to SPMM_KB columns per launch (column-major X, Y with
@@ -1135,6 +1229,121 @@ __global__ __launch_bounds__(256) void k_sell_fill(const int64_t *rp, const int3
     else sell_walk_build<false>(rp, col, val, row, live, ncols, w, put);
 }
 
+// ---- DIA build
+constexpr int DIA_SLOTS = 256;
+constexpr int DIA_EMPTY = INT32_MIN;
+
+__global__ __launch_bounds__(256) void k_dia_offsets(const int64_t *rp, const int32_t *col, int64_t n, int *slots,
+                                                     unsigned int *cnt) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    for (int64_t e = rp[i]; e < rp[i + 1]; e++) {
+        const int64_t o64 = (int64_t)col[e] - i;
+        if (o64 <= INT32_MIN / 2 || o64 >= INT32_MAX / 2) {
+            atomicAdd(cnt, (unsigned)DIA_SLOTS);
+            return;
+        }
+        const int o = (int)o64;
+        unsigned h = ((unsigned)o * 2654435761u) >> 24;
+        for (int p = 0; p < DIA_SLOTS; p++, h = (h + 1) & (DIA_SLOTS - 1)) {
+            int cur = slots[h];
+            if (cur == o) break;
+            if ((cur == DIA_EMPTY || p >= 8) && *(volatile unsigned *)cnt > (unsigned)DIA_MAX) return;
+            if (cur == DIA_EMPTY) {
+                cur = atomicCAS(&slots[h], DIA_EMPTY, o);
+                if (cur == DIA_EMPTY) {
+                    atomicAdd(cnt, 1u);
+                    break;
+                }
+                if (cur == o) break;
+            }
+        }
+    }
+}
+
+// codes of row i (rows >= n: padding, all +0.0)
+__global__ __launch_bounds__(256) void k_dia_fill(const int64_t *rp, const int32_t *col, const double *val,
+                                                  int64_t n, int64_t nrows_alloc, DiaArgs off, int vb, int cw,
+                                                  const unsigned long long *tab, int ntab, int zero_code,
+                                                  uint32_t *codes) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= nrows_alloc) return;
+    int c[DIA_MAX];
+    for (int k = 0; k < off.k; k++) c[k] = zero_code;
+    if (i < n) {
+        for (int64_t e = rp[i]; e < rp[i + 1]; e++) {
+            const int o = (int)((int64_t)col[e] - i);
+            int k = 0;
+            while (off.off[k] != o) k++;
+            const unsigned long long bits = (unsigned long long)__double_as_longlong(val[e]);
+            int lo = 0, hi = ntab - 1;
+            while (lo < hi) {
+                const int mid = (lo + hi) >> 1;
+                if (tab[mid] < bits) lo = mid + 1;
+                else hi = mid;
+            }
+            c[k] = lo;
+        }
+    }
+    for (int q = 0; q < cw; q++) {
+        uint32_t wd = 0;
+        for (int k = 0; k < off.k; k++)
+            if ((k * vb) >> 5 == q) wd |= (uint32_t)c[k] << ((k * vb) & 31);
+        codes[i * cw + q] = wd;
+    }
+}
+
+// DIA codes storage for m (auto policy, square, >= SELL_MIN_ROWS rows, 4/8-bit
+// value table, <= DIA_MAX diagonals filled to >= 80 %).  Returns true if built.
+static bool build_dia(GpuCsr &m, int vb, const std::vector<unsigned long long> &tab) {
+    if (g_spmv_format_policy != 0 || (vb != 4 && vb != 8) || m.nrows != m.ncols || m.nrows < SELL_MIN_ROWS ||
+        m.nrows >= (int64_t(1) << 30))
+        return false;
+    hipStream_t s = m.ctx->stream;
+    DevBuf<int> slots(DIA_SLOTS);
+    DevBuf<unsigned int> cnt(1);
+    std::vector<int> hs(DIA_SLOTS, DIA_EMPTY);
+    FAMG_CHECK_HIP(hipMemcpyAsync(slots.get(), hs.data(), DIA_SLOTS * sizeof(int), hipMemcpyHostToDevice, s));
+    FAMG_CHECK_HIP(hipMemsetAsync(cnt.get(), 0, sizeof(unsigned int), s));
+    hipLaunchKernelGGL(k_dia_offsets, dim3((unsigned)ceil_div(m.nrows, 256)), dim3(256), 0, s, m.rp64.get(),
+                       m.col.get(), m.nrows, slots.get(), cnt.get());
+    FAMG_CHECK_HIP(hipGetLastError());
+    unsigned int c = 0;
+    FAMG_CHECK_HIP(hipMemcpyAsync(hs.data(), slots.get(), DIA_SLOTS * sizeof(int), hipMemcpyDeviceToHost, s));
+    FAMG_CHECK_HIP(hipMemcpyAsync(&c, cnt.get(), sizeof(c), hipMemcpyDeviceToHost, s));
+    FAMG_CHECK_HIP(hipStreamSynchronize(s));
+    if (c > (unsigned)DIA_MAX) return false;
+    std::vector<int> offs;
+    for (int o : hs)
+        if (o != DIA_EMPTY) offs.push_back(o);
+    std::sort(offs.begin(), offs.end());
+    const int K = (int)offs.size();
+    if (K == 0 || (int64_t)K * m.nrows * 4 > m.nnz * 5) return false;  // >= 80 % filled
+    const int bits = K * vb;
+    int cw = 1;
+    while (cw * 32 < bits) cw *= 2;
+    DiaArgs oa{};
+    oa.k = K;
+    for (int k = 0; k < K; k++) oa.off[k] = offs[k];
+    const int zero_code = (int)(std::lower_bound(tab.begin(), tab.end(), 0ull) - tab.begin());
+    const int64_t nalloc = m.nrows + 2;
+    m.dia_codes.resize(nalloc * cw);
+    m.sell_vtab.resize(tab.size());
+    FAMG_CHECK_HIP(hipMemcpyAsync(m.sell_vtab.get(), tab.data(), tab.size() * sizeof(double), hipMemcpyHostToDevice, s));
+    hipLaunchKernelGGL(k_dia_fill, dim3((unsigned)ceil_div(nalloc, 256)), dim3(256), 0, s, m.rp64.get(), m.col.get(),
+                       m.val.get(), m.nrows, nalloc, oa, vb, cw,
+                       reinterpret_cast<const unsigned long long *>(m.sell_vtab.get()), (int)tab.size(), zero_code,
+                       m.dia_codes.get());
+    FAMG_CHECK_HIP(hipGetLastError());
+    FAMG_CHECK_HIP(hipStreamSynchronize(s));
+    m.dia_k = K;
+    m.dia_cw = cw;
+    m.dia_off = offs;
+    m.sell_vbits = vb;
+    m.sell_ntab = (int64_t)tab.size();
+    return true;
+}
+
 void build_sell(GpuCsr &m, const std::vector<int64_t> &rp) {
     m.sell_row0.release();
     m.sell_soff.release();
@@ -1142,6 +1351,9 @@ void build_sell(GpuCsr &m, const std::vector<int64_t> &rp) {
     m.sell_base.release();
     m.sell_data.release();
     m.sell_vtab.release();
+    m.dia_codes.release();
+    m.dia_k = m.dia_cw = 0;
+    m.dia_off.clear();
     m.nslices = m.sell_steps = m.sell_bytes = m.sell_ntab = 0;
     m.sell_vbits = 0;
     m.sell_mode_slices[0] = m.sell_mode_slices[1] = m.sell_mode_slices[2] = 0;
@@ -1163,6 +1375,7 @@ void build_sell(GpuCsr &m, const std::vector<int64_t> &rp) {
     const int64_t ns = (int64_t)row0.size() - 1;
     std::vector<unsigned long long> tab;
     const int vb = value_table(m, tab);
+    if (build_dia(m, vb, tab)) return;
     hipStream_t s = m.ctx->stream;
     DevBuf<int32_t> drow0(ns + 1), dplan(4 * ns);
     FAMG_CHECK_HIP(hipMemcpyAsync(drow0.get(), row0.data(), (ns + 1) * sizeof(int32_t), hipMemcpyHostToDevice, s));
@@ -1227,7 +1440,8 @@ void build_sell(GpuCsr &m, const std::vector<int64_t> &rp) {
 }
 
 void choose_kernel(GpuCsr &m) {
-    if (m.has_sell()) m.kernel = SPMV_KERNEL_SELL;
+    if (m.has_dia()) m.kernel = SPMV_KERNEL_DIA;
+    else if (m.has_sell()) m.kernel = SPMV_KERNEL_SELL;
     else if (g_spmv_format_policy == 3 ||
              (g_spmv_format_policy == 0 && m.nrows > 0 && m.nnz >= VECTOR_MIN_AVG * m.nrows))
         m.kernel = SPMV_KERNEL_VECTOR;
@@ -1308,6 +1522,44 @@ void spmv(const GpuCsr &m, const double *x, double *y, SpmvMode mode, const Spmv
         } else {
             FAMG_LAUNCH_MODES(spmv_sell_kernel, grid, block, s, a, FAMG_LAY0)
         }
+    } else if (m.kernel == SPMV_KERNEL_DIA) {
+        FAMG_REQUIRE(mode != SPMV_SGS, AMG_ERR_UNSUPPORTED, "DIA storage has no SGS sweep");
+        const int64_t r0 = seg < 0 ? 0 : m.seg_rows[seg];
+        const int64_t r1 = seg < 0 ? m.nrows : m.seg_rows[seg + 1];
+        if (r1 <= r0) return;
+        DiaArgs a{};
+        a.codes = m.dia_codes.get();
+        a.vtab = m.sell_vtab.get();
+        a.ntab = (int32_t)m.sell_ntab;
+        a.k = m.dia_k;
+        a.row_begin = (int32_t)r0;
+        a.row_end = (int32_t)r1;
+        a.ncols = (int32_t)m.ncols;
+        for (int k = 0; k < m.dia_k; k++) a.off[k] = m.dia_off[k];
+        a.e = e;
+        const dim3 grid((unsigned)ceil_div(r1 - r0, 512));
+        const int key = m.sell_vbits * 16 + m.dia_cw;
+#define FAMG_DIA(VB, CW)                                                                          \
+    switch (mode) {                                                                               \
+    case SPMV_SET: spmv_dia_kernel<SPMV_SET, VB, CW><<<grid, block, 0, s>>>(a); break;          \
+    case SPMV_ADD: spmv_dia_kernel<SPMV_ADD, VB, CW><<<grid, block, 0, s>>>(a); break;          \
+    case SPMV_RESID: spmv_dia_kernel<SPMV_RESID, VB, CW><<<grid, block, 0, s>>>(a); break;      \
+    case SPMV_JACOBI: spmv_dia_kernel<SPMV_JACOBI, VB, CW><<<grid, block, 0, s>>>(a); break;    \
+    case SPMV_RESID0: spmv_dia_kernel<SPMV_RESID0, VB, CW><<<grid, block, 0, s>>>(a); break;    \
+    case SPMV_ADD0: spmv_dia_kernel<SPMV_ADD0, VB, CW><<<grid, block, 0, s>>>(a); break;        \
+    default: break;                                                                               \
+    }
+        switch (key) {
+        case 4 * 16 + 1: FAMG_DIA(4, 1) break;
+        case 4 * 16 + 2: FAMG_DIA(4, 2) break;
+        case 4 * 16 + 4: FAMG_DIA(4, 4) break;
+        case 8 * 16 + 1: FAMG_DIA(8, 1) break;
+        case 8 * 16 + 2: FAMG_DIA(8, 2) break;
+        case 8 * 16 + 4: FAMG_DIA(8, 4) break;
+        case 8 * 16 + 8: FAMG_DIA(8, 8) break;
+        default: fail(AMG_ERR_INVALID, "DIA: unsupported code layout");
+        }
+#undef FAMG_DIA
     } else if (m.kernel == SPMV_KERNEL_VECTOR) {
         const int64_t r0 = seg < 0 ? 0 : m.seg_rows[seg];
         const int64_t r1 = seg < 0 ? m.nrows : m.seg_rows[seg + 1];

@@ -18,9 +18,9 @@ ITERS = 10
 N = 256 ** 3
 
 
-def sell_values(path, counter):
+def sell_values(path, counter, kernel="spmv_sell_kernel"):
     rows = [r for r in csv.DictReader(open(path))
-            if "spmv_sell_kernel" in r["Kernel_Name"] and r["Counter_Name"] == counter]
+            if kernel in r["Kernel_Name"] and r["Counter_Name"] == counter]
     rows.sort(key=lambda r: int(r["Dispatch_Id"]))
     vals = [float(r["Counter_Value"]) * 1024.0 for r in rows]
     assert len(vals) == 2 * ITERS, (path, len(vals))
@@ -29,14 +29,16 @@ def sell_values(path, counter):
 
 def main(fetch_csv, write_csv, known_json, out_json):
     known = json.load(open(known_json))
-    cal_f, fine_f = sell_values(fetch_csv, "FETCH_SIZE")
-    cal_w, fine_w = sell_values(write_csv, "WRITE_SIZE")
+    kern = "spmv_%s_kernel" % known["fine"]["kernel"]
+    assert known["cal"]["kernel"] == known["fine"]["kernel"], known
+    cal_f, fine_f = sell_values(fetch_csv, "FETCH_SIZE", kern)
+    cal_w, fine_w = sell_values(write_csv, "WRITE_SIZE", kern)
     cal_read_known = known["cal"]["stream_bytes"] + 8 * N
     factor = cal_read_known / statistics.median(cal_f)
     read = statistics.median(fine_f) * factor
     write = statistics.median(fine_w)
     out = {
-        "kernel": "spmv_sell_kernel<SET> on A_0 (7-pt 256^3)",
+        "kernel": kern + "<SET> on A_0 (7-pt 256^3)",
         "storage": known["fine"],
         "algorithmic_bytes_per_launch": known["fine"]["stream_bytes"] + 16 * N,
         "fetch_correction_factor": round(factor, 4),
