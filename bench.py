@@ -236,7 +236,7 @@ def run_single(args):
     fa.set_value_codes(True)
     for _ in range(3):
         A64.apply(y, x)
-    spmv64_ms = time_kernel(lambda: A64.apply(y, x), 20, stream)
+    spmv64_ms = time_kernel(lambda: A64.apply(y, x), 25, stream)  # 28 launches: apart from the cycle's in a trace
     bytes64 = spmv_bytes_fmt(A64)
     fp64_values = {"kernel": "spmv_sell_kernel<SET> on A_0, fp64 values", "ms_per_launch": round(spmv64_ms, 5),
                    "bytes_per_launch": bytes64,

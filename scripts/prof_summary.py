@@ -21,15 +21,15 @@ def short(name):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("trace")
-    ap.add_argument("--kernel-prefix", default="spmv_stream_kernel")
+    ap.add_argument("--cycles", type=int, default=23, help="V-cycles in the trace (warm-up + timed)")
     args = ap.parse_args()
     rows = list(csv.DictReader(open(args.trace)))
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
-    # cycle kernels: everything after the last setup kernel (spgemm/sort/...)
-    setup = ("spgemm", "row_sort", "k_t_", "sten", "k_diag", "scan", "narrow", "perm", "abs_row",
-             "smooth_fix", "k_recip", "k_jacobi", "k_l2", "k_divs", "nn_step", "k_dot")
-    last_setup = max(i for i, r in enumerate(rows) if any(s in r["Kernel_Name"] for s in setup))
-    cyc = rows[last_setup + 1:]
+    # cycle kernels: the (kernel, grid) pairs dispatched once per V-cycle, i.e.
+    # at least --cycles times (warm-up + timed cycles of bench.py)
+    count = collections.Counter((r["Kernel_Name"], r["Grid_Size_X"]) for r in rows)
+    cyc = [r for r in rows if args.cycles <= count[(r["Kernel_Name"], r["Grid_Size_X"])] <= args.cycles + 2
+           and not r["Kernel_Name"].startswith("__amd")]
     groups = collections.OrderedDict()
     for r in cyc:
         key = (short(r["Kernel_Name"]), int(r["Grid_Size_X"]) // int(r["Workgroup_Size_X"]))
@@ -40,6 +40,8 @@ def main():
     for (k, g), v in sorted(groups.items(), key=lambda kv: -sum(kv[1])):
         print(f"{k:34s} {g:9d} {len(v):6d} {sum(v)/len(v):9.2f} {min(v):9.2f} {100*sum(v)/total:5.1f}%")
     # gaps between consecutive dispatches inside the cycle region
+    per_cycle = total / args.cycles
+    print(f"per V-cycle: {per_cycle / 1e3:.3f} ms of kernel time (sum of the kernels above / {args.cycles})")
     gaps = [(int(b["Start_Timestamp"]) - int(a["End_Timestamp"])) / 1e3 for a, b in zip(cyc, cyc[1:])]
     gaps = [g for g in gaps if g < 50]
     if gaps:
