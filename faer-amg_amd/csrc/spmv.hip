@@ -45,6 +45,7 @@ constexpr int SELL_C = 64;
 constexpr int SELL_MAX_W = 512;
 constexpr int64_t SELL_MIN_ROWS = 65536;
 constexpr int VECTOR_MIN_AVG = 256;
+constexpr int64_t SELL_PAIR_MIN_SLICES = 1;  // pairing paid on every level measured (A_2: 55 vs 60 us)
 
 __device__ __forceinline__ int xcd_remap(int b, int nb) {
     const int q = nb >> 3, r = nb & 7;
@@ -200,6 +201,7 @@ struct SellArgs {
     Epi e;
     const double *vtab;  // value table (code widths 4 / 8 / 16)
     int32_t ntab;
+    int32_t spw;  // slices per wave (value codes: 2 on large matrices, else 1)
 };
 
 // ---- one step per 512-B row (sell_paired = false)
@@ -686,7 +688,7 @@ __device__ __forceinline__ void sell_wave(const SellArgs &a, const double *stab,
     const int lane = threadIdx.x & 63;
     if constexpr (sell_row_pairs<MODE>(LAY) && sell_slices_per_wave(LAY, MODE) == 2) {
         // two slices of equal width and column mode: two adjacent rows per lane
-        if (sl + 1 < a.nslices) {
+        if (a.spw == 2 && sl + 1 < a.nslices) {
             const int ta = a.soff[slice], tb = a.soff[slice + 1], te = a.soff[slice + 2];
             const uint32_t da = a.desc[slice], db = a.desc[slice + 1];
             if (tb - ta == te - tb && (da >> 30) == (db >> 30)) {
@@ -721,7 +723,7 @@ __device__ __forceinline__ void sell_wave(const SellArgs &a, const double *stab,
     const char *blkp = a.data + (int64_t)(d & 0x3fffffffu) * 128;
     const int32_t *bs = a.base + t0;
     double acc;
-    if constexpr (LAY >= 4 && sell_slices_per_wave(LAY, MODE) == 1) {
+    if (LAY >= 4 && (sell_slices_per_wave(LAY, MODE) == 1 || a.spw == 1)) {
         switch (d >> 30) {
         case 0: acc = sellc_walk_any<MODE, 0, LAY>(blkp, bs, w, lane, stab, a); break;
         case 1: acc = sellc_walk_any<MODE, 1, LAY>(blkp, bs, w, lane, stab, a); break;
@@ -801,7 +803,7 @@ __global__ __launch_bounds__(256) void spmv_sell_kernel(SellArgs a) {
     const int blk = xcd_remap(blockIdx.x, gridDim.x);
     const int wv = __builtin_amdgcn_readfirstlane(blk * 4 + (int)(threadIdx.x >> 6));
     for (int k = 0; k < NSEQ; k++) {
-        const int sl = (wv * NSEQ + k) * SPW;
+        const int sl = (wv * NSEQ + k) * (SPW == 2 ? a.spw : 1);
         if (sl >= a.nslices) return;
         sell_wave<MODE, LAY>(a, stab, sl);
     }
@@ -1479,7 +1481,7 @@ void spmm(const GpuCsr &m, const double *x, int64_t ldx, double *y, int64_t ldy,
         const int kb = (int)std::min<int64_t>(SPMM_KB, k - c0);
         Epi e{x + c0 * ldx, nullptr, nullptr, nullptr, nullptr};
         SellArgs a{m.sell_row0.get(), m.sell_soff.get(), m.sell_desc.get(), m.sell_base.get(),
-                   m.sell_data.get(), 0, (int32_t)m.nslices, e, nullptr, 0};
+                   m.sell_data.get(), 0, (int32_t)m.nslices, e, nullptr, 0, 1};
         double *yc = y + c0 * ldy;
         switch (kb) {
         case 1: hipLaunchKernelGGL(spmm_sell_kernel<1>, grid, block, 0, s, a, m.sell_paired, ldx, yc, ldy); break;
@@ -1508,9 +1510,11 @@ void spmv(const GpuCsr &m, const double *x, double *y, SpmvMode mode, const Spmv
         if (s1 <= s0) return;
         SellArgs a{m.sell_row0.get(), m.sell_soff.get(), m.sell_desc.get(), m.sell_base.get(),
                    m.sell_data.get(), (int32_t)s0, (int32_t)(s1 - s0), e, m.sell_vtab.get(),
-                   (int32_t)m.sell_ntab};
+                   (int32_t)m.sell_ntab, 1};
+        // value codes: two slices per wave when there are enough waves to fill the chip twice over
         const int lay = m.sell_vbits ? 4 : 0;
-        const dim3 grid((unsigned)ceil_div(s1 - s0, 4 * sell_slices_per_wave(lay, mode) * sell_groups_per_wave(lay)));
+        if (sell_slices_per_wave(lay, mode) == 2 && s1 - s0 >= SELL_PAIR_MIN_SLICES) a.spw = 2;
+        const dim3 grid((unsigned)ceil_div(s1 - s0, 4 * a.spw * sell_groups_per_wave(lay)));
         if (m.sell_vbits == 4) {
             FAMG_LAUNCH_MODES(spmv_sell_kernel, grid, block, s, a, FAMG_LAY4)
         } else if (m.sell_vbits == 8) {
