@@ -60,6 +60,12 @@ struct GpuCsr {
     DevBuf<uint32_t> dia_codes;
     int dia_k = 0, dia_cw = 0;
     std::vector<int> dia_off;
+    // wave-per-row storage compression: 8/16-bit value codes (vec_codes, table
+    // sell_vtab) and 16-bit column offsets from the row (vec_off)
+    DevBuf<uint8_t> vec_codes;
+    DevBuf<int16_t> vec_off;
+    int vec_vbits = 0;
+    bool vec_o16 = false;
     int kernel = 0;  // SpmvKernel chosen at finalize
     bool spmv_ready() const { return rp32.get() != nullptr && sched.get() != nullptr; }
     bool has_sell() const { return sell_desc.get() != nullptr; }
@@ -68,6 +74,8 @@ struct GpuCsr {
     // matrix bytes one SpMV streams with the chosen kernel (data + metadata)
     int64_t stream_bytes() const {
         if (kernel == 3) return 4 * dia_cw * nrows + 8 * sell_ntab;
+        if (kernel == 2)
+            return nnz * ((vec_vbits ? vec_vbits / 8 : 8) + (vec_o16 ? 2 : 4)) + 4 * (nrows + 1) + 8 * sell_ntab;
         return kernel == 1 ? sell_bytes + 12 * (nslices + 1) + 4 * sell_steps + 8 * sell_ntab : index_bytes();
     }
 };

@@ -975,13 +975,27 @@ __global__ __launch_bounds__(256) void spmm_sell_kernel(SellArgs a, bool paired,
 
 struct VecArgs {
     const int32_t *rowptr;
-    const int32_t *col;
-    const double *val;
+    const int32_t *col;     // int32 columns (O16 == false)
+    const int16_t *off;     // col = row + off (O16)
+    const double *val;      // fp64 values (VB == 0)
+    const void *codes;      // 8 / 16-bit value codes (VB == 8 / 16) into vtab
+    const double *vtab;
     int32_t row_begin, nrows;
     Epi e;
 };
 
-template <int MODE>
+// Value and column of entry k (CSR order) for the wave-per-row kernel: fp64 or
+// a code into the value table; int32 or a 16-bit offset from the row.
+template <int VB, bool O16>
+__device__ __forceinline__ void vec_entry(const VecArgs &a, int row, int k, double &v, int32_t &c) {
+    if constexpr (VB == 0) v = __builtin_nontemporal_load(a.val + k);
+    else if constexpr (VB == 8) v = a.vtab[__builtin_nontemporal_load(static_cast<const uint8_t *>(a.codes) + k)];
+    else v = a.vtab[__builtin_nontemporal_load(static_cast<const uint16_t *>(a.codes) + k)];
+    if constexpr (O16) c = row + (int32_t)__builtin_nontemporal_load(a.off + k);
+    else c = __builtin_nontemporal_load(a.col + k);
+}
+
+template <int MODE, int VB, bool O16>
 __global__ __launch_bounds__(256) void spmv_vector_kernel(VecArgs a) {
     const int blk = xcd_remap(blockIdx.x, gridDim.x);
     const int w = blk * 4 + (threadIdx.x >> 6);
@@ -991,26 +1005,25 @@ __global__ __launch_bounds__(256) void spmv_vector_kernel(VecArgs a) {
     EpiOps<MODE> ep;
     if (lane == 0) ep.load(a.e, row);
     const int e0 = a.rowptr[row], e1 = a.rowptr[row + 1];
-    const double *__restrict__ val = a.val;
-    const int32_t *__restrict__ col = a.col;
     double acc = 0.0;
     int k = e0 + lane;
     for (; k + 3 * 64 < e1; k += 4 * 64) {
         double vv[4];
         int32_t cc[4];
 #pragma unroll
-        for (int u = 0; u < 4; u++) {
-            vv[u] = __builtin_nontemporal_load(val + k + 64 * u);
-            cc[u] = __builtin_nontemporal_load(col + k + 64 * u);
-        }
+        for (int u = 0; u < 4; u++) vec_entry<VB, O16>(a, row, k + 64 * u, vv[u], cc[u]);
         double xx[4];
 #pragma unroll
         for (int u = 0; u < 4; u++) xx[u] = gx<MODE>(a.e, cc[u]);
 #pragma unroll
         for (int u = 0; u < 4; u++) acc = fma(vv[u], xx[u], acc);
     }
-    for (; k < e1; k += 64)
-        acc = fma(__builtin_nontemporal_load(val + k), gx<MODE>(a.e, __builtin_nontemporal_load(col + k)), acc);
+    for (; k < e1; k += 64) {
+        double v;
+        int32_t c;
+        vec_entry<VB, O16>(a, row, k, v, c);
+        acc = fma(v, gx<MODE>(a.e, c), acc);
+    }
     for (int off = 32; off > 0; off >>= 1) acc += __shfl_xor(acc, off);
     if (lane == 0) ep.store(a.e, acc);
 }
@@ -1441,12 +1454,85 @@ void build_sell(GpuCsr &m, const std::vector<int64_t> &rp) {
     m.seg_slc = seg_slc;
 }
 
+// ---- wave-per-row storage: value codes (8/16-bit) and 16-bit row offsets
+__global__ __launch_bounds__(256) void k_vec_maxoff(const int64_t *rp, const int32_t *col, int64_t n,
+                                                    unsigned long long *mx) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    unsigned long long m = 0;
+    for (int64_t e = rp[i]; e < rp[i + 1]; e++) {
+        const int64_t o = (int64_t)col[e] - i;
+        const unsigned long long a = (unsigned long long)(o < 0 ? -o : o);
+        m = a > m ? a : m;
+    }
+    atomicMax(mx, m);
+}
+
+__global__ __launch_bounds__(256) void k_vec_fill(const int64_t *rp, const int32_t *col, const double *val, int64_t n,
+                                                  int vb, const unsigned long long *tab, int ntab, bool o16,
+                                                  void *codes, int16_t *off) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    for (int64_t e = rp[i]; e < rp[i + 1]; e++) {
+        if (o16) off[e] = (int16_t)((int64_t)col[e] - i);
+        if (vb) {
+            const unsigned long long bits = (unsigned long long)__double_as_longlong(val[e]);
+            int lo = 0, hi = ntab - 1;
+            while (lo < hi) {
+                const int mid = (lo + hi) >> 1;
+                if (tab[mid] < bits) lo = mid + 1;
+                else hi = mid;
+            }
+            if (vb == 8) static_cast<uint8_t *>(codes)[e] = (uint8_t)lo;
+            else static_cast<uint16_t *>(codes)[e] = (uint16_t)lo;
+        }
+    }
+}
+
+static void build_vec_codes(GpuCsr &m) {
+    m.vec_codes.release();
+    m.vec_off.release();
+    m.vec_vbits = 0;
+    m.vec_o16 = false;
+    if (m.nnz == 0) return;
+    hipStream_t s = m.ctx->stream;
+    std::vector<unsigned long long> tab;
+    int vb = value_table(m, tab);
+    if (vb == 4) vb = 8;
+    DevBuf<unsigned long long> mx(1);
+    FAMG_CHECK_HIP(hipMemsetAsync(mx.get(), 0, sizeof(unsigned long long), s));
+    hipLaunchKernelGGL(k_vec_maxoff, dim3((unsigned)ceil_div(m.nrows, 256)), dim3(256), 0, s, m.rp64.get(),
+                       m.col.get(), m.nrows, mx.get());
+    unsigned long long hmx = 0;
+    FAMG_CHECK_HIP(hipMemcpyAsync(&hmx, mx.get(), sizeof(hmx), hipMemcpyDeviceToHost, s));
+    FAMG_CHECK_HIP(hipStreamSynchronize(s));
+    const bool o16 = g_value_codes && hmx <= 32767;
+    if (!vb && !o16) return;
+    if (vb) {
+        m.sell_vtab.resize(tab.size());
+        FAMG_CHECK_HIP(hipMemcpyAsync(m.sell_vtab.get(), tab.data(), tab.size() * sizeof(double),
+                                      hipMemcpyHostToDevice, s));
+        m.vec_codes.resize(m.nnz * (vb / 8));
+    }
+    if (o16) m.vec_off.resize(m.nnz);
+    hipLaunchKernelGGL(k_vec_fill, dim3((unsigned)ceil_div(m.nrows, 256)), dim3(256), 0, s, m.rp64.get(), m.col.get(),
+                       m.val.get(), m.nrows, vb, reinterpret_cast<const unsigned long long *>(m.sell_vtab.get()),
+                       (int)tab.size(), o16, (void *)m.vec_codes.get(), m.vec_off.get());
+    FAMG_CHECK_HIP(hipGetLastError());
+    FAMG_CHECK_HIP(hipStreamSynchronize(s));
+    m.vec_vbits = vb;
+    m.vec_o16 = o16;
+    m.sell_ntab = vb ? (int64_t)tab.size() : 0;
+}
+
 void choose_kernel(GpuCsr &m) {
     if (m.has_dia()) m.kernel = SPMV_KERNEL_DIA;
     else if (m.has_sell()) m.kernel = SPMV_KERNEL_SELL;
     else if (g_spmv_format_policy == 3 ||
-             (g_spmv_format_policy == 0 && m.nrows > 0 && m.nnz >= VECTOR_MIN_AVG * m.nrows))
+             (g_spmv_format_policy == 0 && m.nrows > 0 && m.nnz >= VECTOR_MIN_AVG * m.nrows)) {
         m.kernel = SPMV_KERNEL_VECTOR;
+        build_vec_codes(m);
+    }
     else m.kernel = SPMV_KERNEL_STREAM;
 }
 
@@ -1464,6 +1550,7 @@ void choose_kernel(GpuCsr &m) {
     case SPMV_RESID0: KERNEL<SPMV_RESID0 __VA_ARGS__><<<grid, block, 0, s>>>(args); break; \
     case SPMV_ADD0: KERNEL<SPMV_ADD0 __VA_ARGS__><<<grid, block, 0, s>>>(args); break;     \
     }
+#define FAMG_VEC(VB, O16) , VB, O16
 #define FAMG_LAY0 , 0
 #define FAMG_LAY1 , 1
 #define FAMG_LAY4 , 4
@@ -1568,9 +1655,18 @@ void spmv(const GpuCsr &m, const double *x, double *y, SpmvMode mode, const Spmv
         const int64_t r0 = seg < 0 ? 0 : m.seg_rows[seg];
         const int64_t r1 = seg < 0 ? m.nrows : m.seg_rows[seg + 1];
         if (r1 <= r0) return;
-        VecArgs a{m.rp32.get(), m.col.get(), m.val.get(), (int32_t)r0, (int32_t)(r1 - r0), e};
+        VecArgs a{m.rp32.get(), m.col.get(), m.vec_off.get(), m.val.get(), m.vec_codes.get(), m.sell_vtab.get(),
+                  (int32_t)r0, (int32_t)(r1 - r0), e};
         const dim3 grid((unsigned)ceil_div(r1 - r0, 4));
-        FAMG_LAUNCH_MODES(spmv_vector_kernel, grid, block, s, a)
+        const int key = m.vec_vbits * 2 + (m.vec_o16 ? 1 : 0);
+        switch (key) {
+        case 0: FAMG_LAUNCH_MODES(spmv_vector_kernel, grid, block, s, a, FAMG_VEC(0, false)) break;
+        case 1: FAMG_LAUNCH_MODES(spmv_vector_kernel, grid, block, s, a, FAMG_VEC(0, true)) break;
+        case 16: FAMG_LAUNCH_MODES(spmv_vector_kernel, grid, block, s, a, FAMG_VEC(8, false)) break;
+        case 17: FAMG_LAUNCH_MODES(spmv_vector_kernel, grid, block, s, a, FAMG_VEC(8, true)) break;
+        case 32: FAMG_LAUNCH_MODES(spmv_vector_kernel, grid, block, s, a, FAMG_VEC(16, false)) break;
+        default: FAMG_LAUNCH_MODES(spmv_vector_kernel, grid, block, s, a, FAMG_VEC(16, true)) break;
+        }
     } else {
         const int64_t b0 = seg < 0 ? 0 : m.seg_blk[seg];
         const int64_t b1 = seg < 0 ? m.nblocks : m.seg_blk[seg + 1];
