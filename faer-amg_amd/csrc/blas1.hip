@@ -45,6 +45,31 @@ __global__ __launch_bounds__(EW_BS) void k_mul2(dbl2 *o, const dbl2 *d, const db
     for (int64_t i = (int64_t)blockIdx.x * EW_BS + threadIdx.x; i < n2; i += stride) o[i] = d[i] * a[i];
 }
 
+// out = dt[dc] * a, two elements per lane (16-B accesses of out and a)
+__global__ __launch_bounds__(EW_BS) void k_mul2_coded(dbl2 *o, const uint8_t *dc, const double *dt, const dbl2 *a,
+                                                      int64_t n2) {
+    const int64_t stride = (int64_t)gridDim.x * EW_BS;
+    for (int64_t i = (int64_t)blockIdx.x * EW_BS + threadIdx.x; i < n2; i += stride) {
+        const dbl2 d = {dt[dc[2 * i]], dt[dc[2 * i + 1]]};
+        o[i] = d * a[i];
+    }
+}
+FAMG_EW_KERNEL(k_mul_coded, (double *o, const uint8_t *dc, const double *dt, const double *a, int64_t n),
+               o[i] = dt[dc[i]] * a[i])
+
+void vec_mul_coded(double *o, const uint8_t *dc, const double *dt, const double *a, int64_t n, hipStream_t s) {
+    if (n <= 0) return;
+    const bool aligned = ((reinterpret_cast<uintptr_t>(o) | reinterpret_cast<uintptr_t>(a)) & 15) == 0;
+    if (aligned && n >= 2) {
+        const int64_t n2 = n / 2;
+        hipLaunchKernelGGL(k_mul2_coded, dim3(ew_grid(n2)), dim3(EW_BS), 0, s, (dbl2 *)o, dc, dt, (const dbl2 *)a, n2);
+        if (n & 1)
+            hipLaunchKernelGGL(k_mul_coded, dim3(1), dim3(EW_BS), 0, s, o + n - 1, dc + n - 1, dt, a + n - 1, (int64_t)1);
+    } else {
+        hipLaunchKernelGGL(k_mul_coded, dim3(ew_grid(n)), dim3(EW_BS), 0, s, o, dc, dt, a, n);
+    }
+}
+
 void vec_fill(double *x, double v, int64_t n, hipStream_t s) {
     if (n > 0) hipLaunchKernelGGL(k_fill, dim3(ew_grid(n)), dim3(EW_BS), 0, s, x, v, n);
 }

@@ -121,6 +121,8 @@ struct SpmvEpi {
     const double *b = nullptr;
     const double *d = nullptr;
     const int32_t *perm = nullptr;
+    const uint8_t *dc = nullptr;  // JACOBI only: 8-bit codes of d into dt
+    const double *dt = nullptr;
 };
 
 // y = epilogue(A x) over all rows (seg < 0) or over row segment `seg`, with the
@@ -137,6 +139,10 @@ void vec_copy(double *dst, const double *src, int64_t n, hipStream_t s);
 void vec_sub(double *out, const double *a, const double *b, int64_t n, hipStream_t s);  // a-b
 void vec_add_inplace(double *x, const double *y, int64_t n, hipStream_t s);           // x+=y
 void vec_mul(double *out, const double *d, const double *a, int64_t n, hipStream_t s); // d*a
+// out = dt[dc] * a (8-bit codes of the diagonal)
+void vec_mul_coded(double *out, const uint8_t *dc, const double *dt, const double *a, int64_t n, hipStream_t s);
+// 8-bit codes of v (<= 256 distinct values): returns the table size, 0 if none built
+int64_t array_codes_u8(const double *v, int64_t n, Ctx &ctx, DevBuf<uint8_t> &code, DevBuf<double> &table);
 void vec_axpy(double *y, double alpha, const double *x, int64_t n, hipStream_t s);      // y+=a x
 void vec_xpay(double *y, double beta, const double *x, int64_t n, hipStream_t s);       // y=x+b y
 void vec_scale(double *x, double alpha, int64_t n, hipStream_t s);                      // x*=a
@@ -204,6 +210,11 @@ using CsrPtr = std::shared_ptr<CsrOp>;
 
 struct DiagOp : LinOp {
     DevBuf<double> d;
+    // 8-bit codes of d (built by the multigrid when d has <= 256 distinct
+    // values; the V-cycle's Jacobi steps then read 1 B per row instead of 8)
+    DevBuf<uint8_t> dcode;
+    DevBuf<double> dtab;
+    bool codes_tried = false;
     Kind kind() const override { return Kind::Diag; }
     bool is_precond() const override { return true; }
     void apply(double *out, const double *rhs) override;

@@ -385,9 +385,13 @@ void MultigridOp::ensure_workspace() {
         L.t.resize(n);
         L.r.resize(n);
     }
-    // make sure smoothers' own scratch exists before any graph capture
+    // 8-bit codes of the Jacobi diagonals (bitwise the same d), before any graph capture
     for (auto &L : levels) {
-        if (auto *sg = dynamic_cast<SgsOp *>(L.S.get())) (void)sg;
+        auto *D = dynamic_cast<DiagOp *>(L.S.get());
+        if (D && !D->codes_tried) {
+            array_codes_u8(D->d.get(), D->nrows, *ctx, D->dcode, D->dtab);
+            D->codes_tried = true;
+        }
     }
     workspace_ready_ = true;
 }
@@ -406,11 +410,14 @@ void MultigridOp::smooth(int64_t l, double *&v, double *&t, const double *f, boo
         const bool zero = v_zero && it == 0;
         if (A && D) {
             if (zero) {
-                vec_mul(t, D->d.get(), f, n, s);  // 0 + d (f - A 0)
+                if (D->dcode.get()) vec_mul_coded(t, D->dcode.get(), D->dtab.get(), f, n, s);
+                else vec_mul(t, D->d.get(), f, n, s);  // 0 + d (f - A 0)
             } else {
                 SpmvEpi epi;
                 epi.b = f;
                 epi.d = D->d.get();
+                epi.dc = D->dcode.get();
+                epi.dt = D->dtab.get();
                 spmv(A->m, v, t, SPMV_JACOBI, epi, s);
             }
             std::swap(v, t);

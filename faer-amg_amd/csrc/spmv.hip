@@ -59,6 +59,8 @@ struct Epi {
     const double *b;
     const double *d;
     const int32_t *perm;
+    const uint8_t *dc;  // JACOBI: d[i] = dt[dc[i]] when set (8-bit codes of the diagonal)
+    const double *dt;
 };
 
 // Operands of the epilogue that do not depend on the row sum are fetched
@@ -69,7 +71,11 @@ template <int MODE> struct EpiOps {
     __device__ __forceinline__ void load(const Epi &a, int row) {
         i = row;
         if constexpr (MODE == SPMV_SGS) i = a.perm[row];
-        if constexpr (MODE == SPMV_JACOBI || MODE == SPMV_SGS) { xr = a.x[i]; br = a.b[i]; dr = a.d[row]; }
+        if constexpr (MODE == SPMV_JACOBI || MODE == SPMV_SGS) {
+            xr = a.x[i];
+            br = a.b[i];
+            dr = (MODE == SPMV_JACOBI && a.dc) ? a.dt[a.dc[row]] : a.d[row];
+        }
         if constexpr (MODE == SPMV_RESID || MODE == SPMV_RESID0) br = a.b[row];
         if constexpr (MODE == SPMV_ADD) yr = a.y[row];
         if constexpr (MODE == SPMV_ADD0) yr = a.d[row] * a.b[row];
@@ -643,7 +649,16 @@ template <int MODE> struct EpiOps2 {
         l0 = live0;
         l1 = live1;
         if (!l0) return;
-        if constexpr (MODE == SPMV_JACOBI) { xr = ld(a.x); br = ld(a.b); dr = ld(a.d); }
+        if constexpr (MODE == SPMV_JACOBI) {
+            xr = ld(a.x);
+            br = ld(a.b);
+            if (a.dc) {
+                dr.x = a.dt[a.dc[i]];
+                dr.y = l1 ? a.dt[a.dc[i + 1]] : 0.0;
+            } else {
+                dr = ld(a.d);
+            }
+        }
         if constexpr (MODE == SPMV_RESID || MODE == SPMV_RESID0) br = ld(a.b);
         if constexpr (MODE == SPMV_ADD) yr = ld(a.y);
         if constexpr (MODE == SPMV_ADD0) yr = ld(a.d) * ld(a.b);
@@ -1140,16 +1155,22 @@ __global__ __launch_bounds__(256) void k_value_set(const double *val, int64_t nn
 
 // Code width for m's values (0 = keep fp64, 4, 8 or 16) and the table: the
 // distinct bit patterns, +0.0 (padding) included, ascending as unsigned.
+static int value_table_of(const double *val, int64_t nnz, hipStream_t s, std::vector<unsigned long long> &tab);
+
 static int value_table(const GpuCsr &m, std::vector<unsigned long long> &tab) {
     tab.clear();
     if (!g_value_codes || m.nnz == 0) return 0;
-    hipStream_t s = m.ctx->stream;
+    return value_table_of(m.val.get(), m.nnz, m.ctx->stream, tab);
+}
+
+static int value_table_of(const double *val, int64_t nnz, hipStream_t s, std::vector<unsigned long long> &tab) {
+    tab.clear();
     DevBuf<unsigned long long> slots(VT_SLOTS);
     DevBuf<unsigned int> cnt(1);
     FAMG_CHECK_HIP(hipMemsetAsync(slots.get(), 0xff, VT_SLOTS * sizeof(unsigned long long), s));
     FAMG_CHECK_HIP(hipMemsetAsync(cnt.get(), 0, sizeof(unsigned int), s));
-    const unsigned grid = (unsigned)std::min<int64_t>(4096, ceil_div(m.nnz, 256));
-    hipLaunchKernelGGL(k_value_set, dim3(grid), dim3(256), 0, s, m.val.get(), m.nnz, slots.get(), cnt.get());
+    const unsigned grid = (unsigned)std::min<int64_t>(4096, ceil_div(nnz, 256));
+    hipLaunchKernelGGL(k_value_set, dim3(grid), dim3(256), 0, s, val, nnz, slots.get(), cnt.get());
     FAMG_CHECK_HIP(hipGetLastError());
     std::vector<unsigned long long> h(VT_SLOTS);
     unsigned int c = 0;
@@ -1242,6 +1263,40 @@ __global__ __launch_bounds__(256) void k_sell_fill(const int64_t *rp, const int3
     };
     if (aligned[sl]) sell_walk_build<true>(rp, col, val, row, live, ncols, w, put);
     else sell_walk_build<false>(rp, col, val, row, live, ncols, w, put);
+}
+
+// ---- 8-bit codes of a vector (the Jacobi diagonal): table + codes, or 0
+__global__ __launch_bounds__(256) void k_array_codes(const double *v, int64_t n, const unsigned long long *tab,
+                                                     int ntab, uint8_t *code) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    const unsigned long long bits = (unsigned long long)__double_as_longlong(v[i]);
+    int lo = 0, hi = ntab - 1;
+    while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (tab[mid] < bits) lo = mid + 1;
+        else hi = mid;
+    }
+    code[i] = (uint8_t)lo;
+}
+
+int64_t array_codes_u8(const double *v, int64_t n, Ctx &ctx, DevBuf<uint8_t> &code, DevBuf<double> &table) {
+    code.release();
+    table.release();
+    if (!g_value_codes || n == 0) return 0;
+    std::vector<unsigned long long> tab;
+    const int vb = value_table_of(v, n, ctx.stream, tab);
+    if (vb != 4 && vb != 8) return 0;
+    table.resize(tab.size());
+    code.resize(n + 2);
+    FAMG_CHECK_HIP(hipMemcpyAsync(table.get(), tab.data(), tab.size() * sizeof(double), hipMemcpyHostToDevice,
+                                  ctx.stream));
+    FAMG_CHECK_HIP(hipMemsetAsync(code.get(), 0, n + 2, ctx.stream));
+    hipLaunchKernelGGL(k_array_codes, dim3((unsigned)ceil_div(n, 256)), dim3(256), 0, ctx.stream, v, n,
+                       reinterpret_cast<const unsigned long long *>(table.get()), (int)tab.size(), code.get());
+    FAMG_CHECK_HIP(hipGetLastError());
+    FAMG_CHECK_HIP(hipStreamSynchronize(ctx.stream));
+    return (int64_t)tab.size();
 }
 
 // ---- DIA build
@@ -1566,7 +1621,7 @@ void spmm(const GpuCsr &m, const double *x, int64_t ldx, double *y, int64_t ldy,
     const dim3 grid((unsigned)ceil_div(m.nslices, 4)), block(256);
     for (int64_t c0 = 0; c0 < k; c0 += SPMM_KB) {
         const int kb = (int)std::min<int64_t>(SPMM_KB, k - c0);
-        Epi e{x + c0 * ldx, nullptr, nullptr, nullptr, nullptr};
+        Epi e{x + c0 * ldx, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
         SellArgs a{m.sell_row0.get(), m.sell_soff.get(), m.sell_desc.get(), m.sell_base.get(),
                    m.sell_data.get(), 0, (int32_t)m.nslices, e, nullptr, 0, 1};
         double *yc = y + c0 * ldy;
@@ -1589,7 +1644,7 @@ void spmv(const GpuCsr &m, const double *x, double *y, SpmvMode mode, const Spmv
     FAMG_REQUIRE(m.spmv_ready(), AMG_ERR_UNSUPPORTED, "SpMV needs nnz < 2^31 (32-bit row pointers)");
     FAMG_REQUIRE(seg < (int64_t)m.seg_rows.size() - 1, AMG_ERR_INVALID, "SpMV segment out of range");
     FAMG_REQUIRE(mode != SPMV_SGS || epi.perm, AMG_ERR_INVALID, "SGS mode needs a permutation");
-    Epi e{x, y, epi.b, epi.d, epi.perm};
+    Epi e{x, y, epi.b, epi.d, epi.perm, epi.dc, epi.dt};
     const dim3 block(256);
     if (m.kernel == SPMV_KERNEL_SELL) {
         const int64_t s0 = seg < 0 ? 0 : m.seg_slc[seg];
