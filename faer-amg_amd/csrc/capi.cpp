@@ -239,9 +239,14 @@ amg_status amg_csr_value_codes(const amg_linop *op, int64_t *info2) {
     return guard([&] {
         FAMG_REQUIRE(info2, AMG_ERR_INVALID, "null argument");
         const GpuCsr &m = need_csr(op)->m;
-        const bool sell = m.kernel == SPMV_KERNEL_SELL || m.kernel == SPMV_KERNEL_DIA;
-        info2[0] = sell ? m.sell_vbits : 0;
-        info2[1] = sell ? m.sell_ntab : 0;
+        if (m.kernel == SPMV_KERNEL_DIA) {
+            info2[0] = m.dia_vbits;
+            info2[1] = m.dia_ntab;
+        } else {
+            const bool coded = m.kernel == SPMV_KERNEL_SELL || m.kernel == SPMV_KERNEL_VECTOR;
+            info2[0] = !coded ? 0 : m.kernel == SPMV_KERNEL_SELL ? m.sell_vbits : m.vec_vbits;
+            info2[1] = coded && info2[0] ? m.sell_ntab : 0;
+        }
     });
 }
 

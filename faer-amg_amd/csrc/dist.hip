@@ -446,11 +446,14 @@ struct DistMultigridOp : LinOp {
         hipStream_t s = ctx->stream;
         for (int64_t it = 0; it < steps; it++) {
             if (zero && it == 0) {
-                vec_mul(t, D.S->d.get(), f, D.sp.n_own, s);
+                if (D.S->dcode.get()) vec_mul_coded(t, D.S->dcode.get(), D.S->dtab.get(), f, D.sp.n_own, s);
+                else vec_mul(t, D.S->d.get(), f, D.sp.n_own, s);
             } else {
                 SpmvEpi epi;
                 epi.b = f;
                 epi.d = D.S->d.get();
+                epi.dc = D.S->dcode.get();
+                epi.dt = D.S->dtab.get();
                 halo_spmv(D.sp, v, D.A->m, t, SPMV_JACOBI, epi);
             }
             std::swap(v, t);
@@ -625,6 +628,8 @@ static std::shared_ptr<DistMultigridOp> build_dist(amg_comm *comm, const Multigr
         D.S->nrows = D.S->ncols = D.sp.n_own;
         D.S->d.resize(D.sp.n_own);
         if (D.sp.n_own) vec_copy(D.S->d.get(), S->d.get() + D.sp.r0, D.sp.n_own, ctx->stream);
+        array_codes_u8(D.S->d.get(), D.sp.n_own, *ctx, D.S->dcode, D.S->dtab);  // 1 B per row when few values
+        D.S->codes_tried = true;
     }
     // ghost sets: space l collects A_l, R_l (fine columns) and P_{l-1} (coarse columns)
     for (int64_t l = 0; l < d->La; l++) {

@@ -58,8 +58,13 @@ struct GpuCsr {
     // DIA codes (spmv.hip "DIA codes"): dia_cw words of codes per row for the
     // dia_k diagonals dia_off (ascending); value table = sell_vtab
     DevBuf<uint32_t> dia_codes;
-    int dia_k = 0, dia_cw = 0;
+    DevBuf<double> dia_vtab;
+    int64_t dia_ntab = 0;
+    int dia_k = 0, dia_cw = 0, dia_vbits = 0;
     std::vector<int> dia_off;
+    // DIA row range: the whole matrix (kernel == DIA) or one row segment
+    // (dia_seg, e.g. the halo interior of a distributed level) beside SELL
+    int64_t dia_r0 = 0, dia_r1 = 0, dia_seg = 0;
     // wave-per-row storage compression: 8/16-bit value codes (vec_codes, table
     // sell_vtab) and 16-bit column offsets from the row (vec_off)
     DevBuf<uint8_t> vec_codes;
@@ -73,7 +78,7 @@ struct GpuCsr {
     int64_t index_bytes() const { return 12 * nnz + 4 * (nrows + 1); }
     // matrix bytes one SpMV streams with the chosen kernel (data + metadata)
     int64_t stream_bytes() const {
-        if (kernel == 3) return 4 * dia_cw * nrows + 8 * sell_ntab;
+        if (kernel == 3) return 4 * dia_cw * nrows + 8 * dia_ntab;
         if (kernel == 2)
             return nnz * ((vec_vbits ? vec_vbits / 8 : 8) + (vec_o16 ? 2 : 4)) + 4 * (nrows + 1) + 8 * sell_ntab;
         return kernel == 1 ? sell_bytes + 12 * (nslices + 1) + 4 * sell_steps + 8 * sell_ntab : index_bytes();

@@ -841,6 +841,7 @@ struct DiaArgs {
     const uint32_t *codes;  // cw words per row (rows padded by 2)
     const double *vtab;
     int32_t ntab, k, row_begin, row_end, ncols;
+    int32_t code_row0;  // first row with codes (the DIA row range may be one segment)
     int32_t off[DIA_MAX];
     Epi e;
 };
@@ -877,7 +878,7 @@ __global__ __launch_bounds__(256) void spmv_dia_kernel(DiaArgs a) {
     EpiOps2<MODE> ep;
     ep.load(a.e, row, true, row + 1 < a.row_end);
     uint32_t w0[CW], w1[CW];
-    const uint32_t *cp = a.codes + (int64_t)row * CW;
+    const uint32_t *cp = a.codes + (int64_t)(row - a.code_row0) * CW;
     if constexpr (CW == 1) {
         const i32x2u_t v = __builtin_nontemporal_load(reinterpret_cast<const i32x2u_t *>(cp));
         w0[0] = (uint32_t)v.x;
@@ -1303,10 +1304,10 @@ int64_t array_codes_u8(const double *v, int64_t n, Ctx &ctx, DevBuf<uint8_t> &co
 constexpr int DIA_SLOTS = 256;
 constexpr int DIA_EMPTY = INT32_MIN;
 
-__global__ __launch_bounds__(256) void k_dia_offsets(const int64_t *rp, const int32_t *col, int64_t n, int *slots,
-                                                     unsigned int *cnt) {
-    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    if (i >= n) return;
+__global__ __launch_bounds__(256) void k_dia_offsets(const int64_t *rp, const int32_t *col, int64_t r0, int64_t r1,
+                                                     int *slots, unsigned int *cnt) {
+    const int64_t i = r0 + (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= r1) return;
     for (int64_t e = rp[i]; e < rp[i + 1]; e++) {
         const int64_t o64 = (int64_t)col[e] - i;
         if (o64 <= INT32_MIN / 2 || o64 >= INT32_MAX / 2) {
@@ -1333,14 +1334,15 @@ __global__ __launch_bounds__(256) void k_dia_offsets(const int64_t *rp, const in
 
 // codes of row i (rows >= n: padding, all +0.0)
 __global__ __launch_bounds__(256) void k_dia_fill(const int64_t *rp, const int32_t *col, const double *val,
-                                                  int64_t n, int64_t nrows_alloc, DiaArgs off, int vb, int cw,
-                                                  const unsigned long long *tab, int ntab, int zero_code,
+                                                  int64_t r0, int64_t r1, int64_t nrows_alloc, DiaArgs off, int vb,
+                                                  int cw, const unsigned long long *tab, int ntab, int zero_code,
                                                   uint32_t *codes) {
-    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    if (i >= nrows_alloc) return;
+    const int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (j >= nrows_alloc) return;
+    const int64_t i = r0 + j;
     int c[DIA_MAX];
     for (int k = 0; k < off.k; k++) c[k] = zero_code;
-    if (i < n) {
+    if (i < r1) {
         for (int64_t e = rp[i]; e < rp[i + 1]; e++) {
             const int o = (int)((int64_t)col[e] - i);
             int k = 0;
@@ -1359,14 +1361,17 @@ __global__ __launch_bounds__(256) void k_dia_fill(const int64_t *rp, const int32
         uint32_t wd = 0;
         for (int k = 0; k < off.k; k++)
             if ((k * vb) >> 5 == q) wd |= (uint32_t)c[k] << ((k * vb) & 31);
-        codes[i * cw + q] = wd;
+        codes[j * cw + q] = wd;
     }
 }
 
-// DIA codes storage for m (auto policy, square, >= SELL_MIN_ROWS rows, 4/8-bit
-// value table, <= DIA_MAX diagonals filled to >= 80 %).  Returns true if built.
-static bool build_dia(GpuCsr &m, int vb, const std::vector<unsigned long long> &tab) {
-    if (g_spmv_format_policy != 0 || (vb != 4 && vb != 8) || m.nrows != m.ncols || m.nrows < SELL_MIN_ROWS ||
+// DIA codes storage for rows [r0, r1) of m (auto policy, square, >= SELL_MIN_ROWS
+// rows, 4/8-bit value table, <= DIA_MAX diagonals filled to >= 80 %).  Returns
+// true if built.
+static bool build_dia(GpuCsr &m, int vb, const std::vector<unsigned long long> &tab,
+                      const std::vector<int64_t> &rp, int64_t r0, int64_t r1) {
+    const int64_t nr = r1 - r0;
+    if (g_spmv_format_policy != 0 || (vb != 4 && vb != 8) || m.nrows != m.ncols || nr < SELL_MIN_ROWS ||
         m.nrows >= (int64_t(1) << 30))
         return false;
     hipStream_t s = m.ctx->stream;
@@ -1375,8 +1380,8 @@ static bool build_dia(GpuCsr &m, int vb, const std::vector<unsigned long long> &
     std::vector<int> hs(DIA_SLOTS, DIA_EMPTY);
     FAMG_CHECK_HIP(hipMemcpyAsync(slots.get(), hs.data(), DIA_SLOTS * sizeof(int), hipMemcpyHostToDevice, s));
     FAMG_CHECK_HIP(hipMemsetAsync(cnt.get(), 0, sizeof(unsigned int), s));
-    hipLaunchKernelGGL(k_dia_offsets, dim3((unsigned)ceil_div(m.nrows, 256)), dim3(256), 0, s, m.rp64.get(),
-                       m.col.get(), m.nrows, slots.get(), cnt.get());
+    hipLaunchKernelGGL(k_dia_offsets, dim3((unsigned)ceil_div(nr, 256)), dim3(256), 0, s, m.rp64.get(),
+                       m.col.get(), r0, r1, slots.get(), cnt.get());
     FAMG_CHECK_HIP(hipGetLastError());
     unsigned int c = 0;
     FAMG_CHECK_HIP(hipMemcpyAsync(hs.data(), slots.get(), DIA_SLOTS * sizeof(int), hipMemcpyDeviceToHost, s));
@@ -1388,7 +1393,7 @@ static bool build_dia(GpuCsr &m, int vb, const std::vector<unsigned long long> &
         if (o != DIA_EMPTY) offs.push_back(o);
     std::sort(offs.begin(), offs.end());
     const int K = (int)offs.size();
-    if (K == 0 || (int64_t)K * m.nrows * 4 > m.nnz * 5) return false;  // >= 80 % filled
+    if (K == 0 || (int64_t)K * nr * 4 > (rp[r1] - rp[r0]) * 5) return false;  // >= 80 % filled
     const int bits = K * vb;
     int cw = 1;
     while (cw * 32 < bits) cw *= 2;
@@ -1396,21 +1401,23 @@ static bool build_dia(GpuCsr &m, int vb, const std::vector<unsigned long long> &
     oa.k = K;
     for (int k = 0; k < K; k++) oa.off[k] = offs[k];
     const int zero_code = (int)(std::lower_bound(tab.begin(), tab.end(), 0ull) - tab.begin());
-    const int64_t nalloc = m.nrows + 2;
+    const int64_t nalloc = nr + 2;
     m.dia_codes.resize(nalloc * cw);
-    m.sell_vtab.resize(tab.size());
-    FAMG_CHECK_HIP(hipMemcpyAsync(m.sell_vtab.get(), tab.data(), tab.size() * sizeof(double), hipMemcpyHostToDevice, s));
+    m.dia_vtab.resize(tab.size());
+    FAMG_CHECK_HIP(hipMemcpyAsync(m.dia_vtab.get(), tab.data(), tab.size() * sizeof(double), hipMemcpyHostToDevice, s));
     hipLaunchKernelGGL(k_dia_fill, dim3((unsigned)ceil_div(nalloc, 256)), dim3(256), 0, s, m.rp64.get(), m.col.get(),
-                       m.val.get(), m.nrows, nalloc, oa, vb, cw,
-                       reinterpret_cast<const unsigned long long *>(m.sell_vtab.get()), (int)tab.size(), zero_code,
+                       m.val.get(), r0, r1, nalloc, oa, vb, cw,
+                       reinterpret_cast<const unsigned long long *>(m.dia_vtab.get()), (int)tab.size(), zero_code,
                        m.dia_codes.get());
     FAMG_CHECK_HIP(hipGetLastError());
     FAMG_CHECK_HIP(hipStreamSynchronize(s));
     m.dia_k = K;
     m.dia_cw = cw;
     m.dia_off = offs;
-    m.sell_vbits = vb;
-    m.sell_ntab = (int64_t)tab.size();
+    m.dia_r0 = r0;
+    m.dia_r1 = r1;
+    m.dia_vbits = vb;
+    m.dia_ntab = (int64_t)tab.size();
     return true;
 }
 
@@ -1422,7 +1429,10 @@ void build_sell(GpuCsr &m, const std::vector<int64_t> &rp) {
     m.sell_data.release();
     m.sell_vtab.release();
     m.dia_codes.release();
-    m.dia_k = m.dia_cw = 0;
+    m.dia_vtab.release();
+    m.dia_ntab = 0;
+    m.dia_k = m.dia_cw = m.dia_vbits = 0;
+    m.dia_r0 = m.dia_r1 = m.dia_seg = 0;
     m.dia_off.clear();
     m.nslices = m.sell_steps = m.sell_bytes = m.sell_ntab = 0;
     m.sell_vbits = 0;
@@ -1445,7 +1455,15 @@ void build_sell(GpuCsr &m, const std::vector<int64_t> &rp) {
     const int64_t ns = (int64_t)row0.size() - 1;
     std::vector<unsigned long long> tab;
     const int vb = value_table(m, tab);
-    if (build_dia(m, vb, tab)) return;
+    // DIA codes on the whole matrix, or (several row segments: the halo
+    // interior of a distributed level) on its longest segment beside SELL
+    int64_t dseg = 0;
+    for (size_t g = 1; g + 1 < m.seg_rows.size(); g++)
+        if (m.seg_rows[g + 1] - m.seg_rows[g] > m.seg_rows[dseg + 1] - m.seg_rows[dseg]) dseg = (int64_t)g;
+    if (build_dia(m, vb, tab, rp, m.seg_rows[dseg], m.seg_rows[dseg + 1])) {
+        m.dia_seg = dseg;
+        if (m.dia_r0 == 0 && m.dia_r1 == m.nrows) return;
+    }
     hipStream_t s = m.ctx->stream;
     DevBuf<int32_t> drow0(ns + 1), dplan(4 * ns);
     FAMG_CHECK_HIP(hipMemcpyAsync(drow0.get(), row0.data(), (ns + 1) * sizeof(int32_t), hipMemcpyHostToDevice, s));
@@ -1581,7 +1599,7 @@ static void build_vec_codes(GpuCsr &m) {
 }
 
 void choose_kernel(GpuCsr &m) {
-    if (m.has_dia()) m.kernel = SPMV_KERNEL_DIA;
+    if (m.has_dia() && m.dia_r0 == 0 && m.dia_r1 == m.nrows) m.kernel = SPMV_KERNEL_DIA;
     else if (m.has_sell()) m.kernel = SPMV_KERNEL_SELL;
     else if (g_spmv_format_policy == 3 ||
              (g_spmv_format_policy == 0 && m.nrows > 0 && m.nnz >= VECTOR_MIN_AVG * m.nrows)) {
@@ -1668,23 +1686,25 @@ void spmv(const GpuCsr &m, const double *x, double *y, SpmvMode mode, const Spmv
         } else {
             FAMG_LAUNCH_MODES(spmv_sell_kernel, grid, block, s, a, FAMG_LAY0)
         }
-    } else if (m.kernel == SPMV_KERNEL_DIA) {
+    } else if (m.kernel == SPMV_KERNEL_DIA ||
+               (m.has_dia() && seg >= 0 && seg == m.dia_seg && mode != SPMV_SGS)) {
         FAMG_REQUIRE(mode != SPMV_SGS, AMG_ERR_UNSUPPORTED, "DIA storage has no SGS sweep");
         const int64_t r0 = seg < 0 ? 0 : m.seg_rows[seg];
         const int64_t r1 = seg < 0 ? m.nrows : m.seg_rows[seg + 1];
         if (r1 <= r0) return;
         DiaArgs a{};
         a.codes = m.dia_codes.get();
-        a.vtab = m.sell_vtab.get();
-        a.ntab = (int32_t)m.sell_ntab;
+        a.ntab = (int32_t)m.dia_ntab;
         a.k = m.dia_k;
         a.row_begin = (int32_t)r0;
         a.row_end = (int32_t)r1;
         a.ncols = (int32_t)m.ncols;
+        a.code_row0 = (int32_t)m.dia_r0;
+        a.vtab = m.dia_vtab.get();
         for (int k = 0; k < m.dia_k; k++) a.off[k] = m.dia_off[k];
         a.e = e;
         const dim3 grid((unsigned)ceil_div(r1 - r0, 512));
-        const int key = m.sell_vbits * 16 + m.dia_cw;
+        const int key = m.dia_vbits * 16 + m.dia_cw;
 #define FAMG_DIA(VB, CW)                                                                          \
     switch (mode) {                                                                               \
     case SPMV_SET: spmv_dia_kernel<SPMV_SET, VB, CW><<<grid, block, 0, s>>>(a); break;          \
