@@ -38,6 +38,15 @@ bool g_alloc_debug = [] {
     const char *e = getenv("FAMG_ALLOC_DEBUG");
     return e && e[0] == '1';
 }();
+// DIA storage: FAMG_DIA_NT=1 streams the epilogue operands (b, d, y) with
+// non-temporal accesses (A/B switch; results are bitwise equal).
+static bool dia_nt() {
+    static const bool on = [] {
+        const char *e = getenv("FAMG_DIA_NT");
+        return e && e[0] == '1';
+    }();
+    return on;
+}
 
 constexpr int SPMV_BS = 256;
 constexpr int SPMV_CAP = 2048;
@@ -635,7 +644,8 @@ __device__ __forceinline__ void sellc_walk_rp(const char *ba, const char *bb, co
 }
 
 // Epilogue of two adjacent rows (row, row + 1) with 16-B accesses when both live.
-template <int MODE> struct EpiOps2 {
+// NT: b, d and y (streamed once, never gathered) bypass the caches.
+template <int MODE, bool NT = false> struct EpiOps2 {
     dbl2_t xr = {0.0, 0.0}, br = {0.0, 0.0}, dr = {0.0, 0.0}, yr = {0.0, 0.0};
     int i = 0;
     bool l0 = false, l1 = false;
@@ -644,6 +654,15 @@ template <int MODE> struct EpiOps2 {
         dbl2_t v = {p[i], 0.0};
         return v;
     }
+    __device__ __forceinline__ dbl2_t lds(const double *p) const {  // streamed operand
+        if constexpr (NT) {
+            if (l1) return __builtin_nontemporal_load(reinterpret_cast<const dbl2u_t *>(p + i));
+            dbl2_t v = {__builtin_nontemporal_load(p + i), 0.0};
+            return v;
+        } else {
+            return ld(p);
+        }
+    }
     __device__ __forceinline__ void load(const Epi &a, int row, bool live0, bool live1) {
         i = row;
         l0 = live0;
@@ -651,17 +670,17 @@ template <int MODE> struct EpiOps2 {
         if (!l0) return;
         if constexpr (MODE == SPMV_JACOBI) {
             xr = ld(a.x);
-            br = ld(a.b);
+            br = lds(a.b);
             if (a.dc) {
                 dr.x = a.dt[a.dc[i]];
                 dr.y = l1 ? a.dt[a.dc[i + 1]] : 0.0;
             } else {
-                dr = ld(a.d);
+                dr = lds(a.d);
             }
         }
-        if constexpr (MODE == SPMV_RESID || MODE == SPMV_RESID0) br = ld(a.b);
-        if constexpr (MODE == SPMV_ADD) yr = ld(a.y);
-        if constexpr (MODE == SPMV_ADD0) yr = ld(a.d) * ld(a.b);
+        if constexpr (MODE == SPMV_RESID || MODE == SPMV_RESID0) br = lds(a.b);
+        if constexpr (MODE == SPMV_ADD) yr = lds(a.y);
+        if constexpr (MODE == SPMV_ADD0) yr = lds(a.d) * lds(a.b);
     }
     __device__ __forceinline__ void store(const Epi &a, double acc0, double acc1) const {
         if (!l0) return;
@@ -671,8 +690,13 @@ template <int MODE> struct EpiOps2 {
         else if constexpr (MODE == SPMV_ADD || MODE == SPMV_ADD0) out = yr + acc;
         else if constexpr (MODE == SPMV_RESID || MODE == SPMV_RESID0) out = br - acc;
         else out = xr + dr * (br - acc);  // JACOBI
-        if (l1) *reinterpret_cast<dbl2u_t *>(a.y + i) = out;
-        else a.y[i] = out.x;
+        if constexpr (NT) {
+            if (l1) __builtin_nontemporal_store(out, reinterpret_cast<dbl2u_t *>(a.y + i));
+            else __builtin_nontemporal_store(out.x, a.y + i);
+        } else {
+            if (l1) *reinterpret_cast<dbl2u_t *>(a.y + i) = out;
+            else a.y[i] = out.x;
+        }
     }
 };
 
@@ -849,36 +873,20 @@ struct DiaArgs {
 typedef int32_t i32x2u_t __attribute__((ext_vector_type(2), aligned(4)));
 typedef int32_t i32x4u_t __attribute__((ext_vector_type(4), aligned(4)));
 
+// x operands of rows (r, r+1) at column c = r + off: x[clamp(c)], x[clamp(c+1)]
+// from one 16-B load at clamp(c, 0, ncols-2) and selects -- branch-free, so
+// the loads of all diagonals stay in flight together (a divergent edge path
+// made the compiler wait for each load at its join).  Needs ncols >= 2.
 template <int MODE> __device__ __forceinline__ void dia_gx2(const Epi &e, int c, int ncols, double &x0, double &x1) {
-    if (c >= 0 && c + 1 < ncols) {
-        const dbl2_t v = *reinterpret_cast<const dbl2u_t *>(e.x + c);
-        if constexpr (MODE == SPMV_RESID0) {
-            const dbl2_t d = *reinterpret_cast<const dbl2u_t *>(e.d + c);
-            x0 = d.x * v.x;
-            x1 = d.y * v.y;
-        } else {
-            x0 = v.x;
-            x1 = v.y;
-        }
-    } else {
-        const int c0 = min(max(c, 0), ncols - 1), c1 = min(max(c + 1, 0), ncols - 1);
-        x0 = gx<MODE>(e, c0);
-        x1 = gx<MODE>(e, c1);
-    }
+    const int cc = min(max(c, 0), ncols - 2);
+    dbl2_t v = *reinterpret_cast<const dbl2u_t *>(e.x + cc);
+    if constexpr (MODE == SPMV_RESID0) v = *reinterpret_cast<const dbl2u_t *>(e.d + cc) * v;
+    x0 = c > ncols - 2 ? v.y : v.x;
+    x1 = c < 0 ? v.x : v.y;
 }
 
-template <int MODE, int VB, int CW>
-__global__ __launch_bounds__(256) void spmv_dia_kernel(DiaArgs a) {
-    __shared__ double stab[VB == 4 ? 16 : 256];
-    for (int i = threadIdx.x; i < a.ntab; i += 256) stab[i] = a.vtab[i];
-    __syncthreads();
-    const int blk = xcd_remap(blockIdx.x, gridDim.x);
-    const int row = a.row_begin + 2 * (blk * 256 + (int)threadIdx.x);
-    if (row >= a.row_end) return;
-    EpiOps2<MODE> ep;
-    ep.load(a.e, row, true, row + 1 < a.row_end);
-    uint32_t w0[CW], w1[CW];
-    const uint32_t *cp = a.codes + (int64_t)(row - a.code_row0) * CW;
+template <int CW>
+__device__ __forceinline__ void dia_codes2(const uint32_t *cp, uint32_t (&w0)[CW], uint32_t (&w1)[CW]) {
     if constexpr (CW == 1) {
         const i32x2u_t v = __builtin_nontemporal_load(reinterpret_cast<const i32x2u_t *>(cp));
         w0[0] = (uint32_t)v.x;
@@ -901,21 +909,111 @@ __global__ __launch_bounds__(256) void spmv_dia_kernel(DiaArgs a) {
             }
         }
     }
+}
+
+// The weighted-Jacobi epilogue with the 8-bit coded diagonal (d = dt[dc[i]],
+// dt padded to 256 entries and staged in LDS with the value table).
+constexpr int DIA_JACOBI_DC = 16;
+
+// Epilogue operands of a DIA row pair, loaded without divergence: one 16-B
+// load at i2 = min(row, row_end - 2) per vector; a tail row (row_end - 1)
+// takes the upper half.  Lanes past row_end load in-range data and store
+// nothing.
+template <int MODE, bool NT> struct DiaEpi {
+    dbl2_t xr = {0.0, 0.0}, br = {0.0, 0.0}, dr = {0.0, 0.0}, yr = {0.0, 0.0};
+    int row = 0, i2 = 0;
+    uint32_t dc0 = 0, dc1 = 0;
+    bool l0 = false, l1 = false;
+    __device__ __forceinline__ dbl2_t ldv(const double *p) const {
+        const dbl2u_t *q = reinterpret_cast<const dbl2u_t *>(p + i2);
+        dbl2_t v = NT ? __builtin_nontemporal_load(q) : *q;
+        if (row != i2) v.x = v.y;
+        return v;
+    }
+    // the diagonal codes are loaded first: waiting for them later waits for nothing else
+    __device__ __forceinline__ void load_codes(const Epi &a, int r, int row_end) {
+        if constexpr (MODE == DIA_JACOBI_DC) {
+            dc0 = a.dc[min(r, row_end - 1)];
+            dc1 = a.dc[min(r + 1, row_end - 1)];
+        }
+    }
+    __device__ __forceinline__ void load(const Epi &a, int r, int row_end) {
+        row = r;
+        i2 = min(r, row_end - 2);
+        l0 = r < row_end;
+        l1 = r + 1 < row_end;
+        if constexpr (MODE == SPMV_JACOBI || MODE == DIA_JACOBI_DC) {
+            const dbl2u_t *q = reinterpret_cast<const dbl2u_t *>(a.x + i2);  // x is gathered: cached
+            xr = *q;
+            if (row != i2) xr.x = xr.y;
+            br = ldv(a.b);
+        }
+        if constexpr (MODE == SPMV_JACOBI) dr = ldv(a.d);
+        if constexpr (MODE == SPMV_RESID || MODE == SPMV_RESID0) br = ldv(a.b);
+        if constexpr (MODE == SPMV_ADD) yr = ldv(a.y);
+        if constexpr (MODE == SPMV_ADD0) yr = ldv(a.d) * ldv(a.b);
+    }
+    __device__ __forceinline__ void store(const Epi &a, const double *sdt, double acc0, double acc1) {
+        const dbl2_t acc = {acc0, acc1};
+        dbl2_t out;
+        if constexpr (MODE == DIA_JACOBI_DC) dr = dbl2_t{sdt[dc0], sdt[dc1]};
+        if constexpr (MODE == SPMV_SET) out = acc;
+        else if constexpr (MODE == SPMV_ADD || MODE == SPMV_ADD0) out = yr + acc;
+        else if constexpr (MODE == SPMV_RESID || MODE == SPMV_RESID0) out = br - acc;
+        else out = xr + dr * (br - acc);  // JACOBI
+        if (l1) {
+            if constexpr (NT) __builtin_nontemporal_store(out, reinterpret_cast<dbl2u_t *>(a.y + row));
+            else *reinterpret_cast<dbl2u_t *>(a.y + row) = out;
+        } else if (l0) {
+            if constexpr (NT) __builtin_nontemporal_store(out.x, a.y + row);
+            else a.y[row] = out.x;
+        }
+    }
+};
+
+// Two adjacent rows per lane, 512 rows per workgroup.  Every load is issued
+// unconditionally (clamped indices; all KMAX diagonals, off[k] = 0 past K,
+// whose terms are not added), so no load waits on another -- a divergent edge
+// path or a per-diagonal guard made the compiler wait for each load at the
+// join.  The value table (and the coded diagonal's table) is fetched first and
+// published to LDS behind an LDS-only barrier after the row loads are issued,
+// so they stay in flight across it.
+template <int MODE, int VB, int CW, bool NT>
+__global__ __launch_bounds__(256) void spmv_dia_kernel(DiaArgs a) {
+    constexpr bool DC = MODE == DIA_JACOBI_DC;
+    constexpr int GM = DC ? SPMV_JACOBI : MODE;  // x operand of the row sums
+    __shared__ double stab[VB == 4 ? 16 : 256];
+    __shared__ double sdt[DC ? 256 : 1];
+    const double tv = (int)threadIdx.x < a.ntab ? a.vtab[threadIdx.x] : 0.0;
+    double dv = 0.0;
+    if constexpr (DC) dv = a.e.dt[threadIdx.x];
+    const int blk = xcd_remap(blockIdx.x, gridDim.x);
+    const int row = a.row_begin + 512 * blk + 2 * (int)threadIdx.x;
     constexpr int KMAX = CW * 32 / VB < DIA_MAX ? CW * 32 / VB : DIA_MAX;
     constexpr uint32_t MASK = (1u << VB) - 1;
+    DiaEpi<MODE, NT> ep;
+    uint32_t w0[CW], w1[CW];
     double x0[KMAX], x1[KMAX];
+    ep.load_codes(a.e, row, a.row_end);
+    ep.load(a.e, row, a.row_end);
+    dia_codes2<CW>(a.codes + (int64_t)(min(row, a.row_end - 1) - a.code_row0) * CW, w0, w1);
 #pragma unroll
-    for (int k = 0; k < KMAX; k++)
-        if (k < a.k) dia_gx2<MODE>(a.e, row + a.off[k], a.ncols, x0[k], x1[k]);
+    for (int k = 0; k < KMAX; k++) dia_gx2<GM>(a.e, row + a.off[k], a.ncols, x0[k], x1[k]);
+    if ((int)threadIdx.x < a.ntab) stab[threadIdx.x] = tv;
+    if constexpr (DC) sdt[threadIdx.x] = dv;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+    if (row >= a.row_end) return;
     double acc0 = 0.0, acc1 = 0.0;
 #pragma unroll
     for (int k = 0; k < KMAX; k++) {
-        if (k < a.k) {
-            acc0 = fma(stab[(w0[(k * VB) >> 5] >> ((k * VB) & 31)) & MASK], x0[k], acc0);
-            acc1 = fma(stab[(w1[(k * VB) >> 5] >> ((k * VB) & 31)) & MASK], x1[k], acc1);
-        }
+        const double f0 = fma(stab[(w0[(k * VB) >> 5] >> ((k * VB) & 31)) & MASK], x0[k], acc0);
+        const double f1 = fma(stab[(w1[(k * VB) >> 5] >> ((k * VB) & 31)) & MASK], x1[k], acc1);
+        acc0 = k < a.k ? f0 : acc0;
+        acc1 = k < a.k ? f1 : acc1;
     }
-    ep.store(a.e, acc0, acc1);
+    ep.store(a.e, sdt, acc0, acc1);
 }
 
 // SpMM: Y = A X for up to SPMM_KB columns per launch (column-major X, Y with
@@ -1288,7 +1386,8 @@ int64_t array_codes_u8(const double *v, int64_t n, Ctx &ctx, DevBuf<uint8_t> &co
     std::vector<unsigned long long> tab;
     const int vb = value_table_of(v, n, ctx.stream, tab);
     if (vb != 4 && vb != 8) return 0;
-    table.resize(tab.size());
+    table.resize(256);  // padded: kernels stage all 256 entries without a bound
+    FAMG_CHECK_HIP(hipMemsetAsync(table.get(), 0, 256 * sizeof(double), ctx.stream));
     code.resize(n + 2);
     FAMG_CHECK_HIP(hipMemcpyAsync(table.get(), tab.data(), tab.size() * sizeof(double), hipMemcpyHostToDevice,
                                   ctx.stream));
@@ -1705,14 +1804,24 @@ void spmv(const GpuCsr &m, const double *x, double *y, SpmvMode mode, const Spmv
         a.e = e;
         const dim3 grid((unsigned)ceil_div(r1 - r0, 512));
         const int key = m.dia_vbits * 16 + m.dia_cw;
+        const bool nt = dia_nt();
+#define FAMG_DIA2(M, VB, CW)                                                                      \
+    if (nt) spmv_dia_kernel<M, VB, CW, true><<<grid, block, 0, s>>>(a);                          \
+    else spmv_dia_kernel<M, VB, CW, false><<<grid, block, 0, s>>>(a);
 #define FAMG_DIA(VB, CW)                                                                          \
     switch (mode) {                                                                               \
-    case SPMV_SET: spmv_dia_kernel<SPMV_SET, VB, CW><<<grid, block, 0, s>>>(a); break;          \
-    case SPMV_ADD: spmv_dia_kernel<SPMV_ADD, VB, CW><<<grid, block, 0, s>>>(a); break;          \
-    case SPMV_RESID: spmv_dia_kernel<SPMV_RESID, VB, CW><<<grid, block, 0, s>>>(a); break;      \
-    case SPMV_JACOBI: spmv_dia_kernel<SPMV_JACOBI, VB, CW><<<grid, block, 0, s>>>(a); break;    \
-    case SPMV_RESID0: spmv_dia_kernel<SPMV_RESID0, VB, CW><<<grid, block, 0, s>>>(a); break;    \
-    case SPMV_ADD0: spmv_dia_kernel<SPMV_ADD0, VB, CW><<<grid, block, 0, s>>>(a); break;        \
+    case SPMV_SET: FAMG_DIA2(SPMV_SET, VB, CW) break;                                             \
+    case SPMV_ADD: FAMG_DIA2(SPMV_ADD, VB, CW) break;                                             \
+    case SPMV_RESID: FAMG_DIA2(SPMV_RESID, VB, CW) break;                                         \
+    case SPMV_JACOBI:                                                                             \
+        if (e.dc) {                                                                               \
+            FAMG_DIA2(DIA_JACOBI_DC, VB, CW)                                                      \
+        } else {                                                                                  \
+            FAMG_DIA2(SPMV_JACOBI, VB, CW)                                                        \
+        }                                                                                         \
+        break;                                                                                    \
+    case SPMV_RESID0: FAMG_DIA2(SPMV_RESID0, VB, CW) break;                                       \
+    case SPMV_ADD0: FAMG_DIA2(SPMV_ADD0, VB, CW) break;                                           \
     default: break;                                                                               \
     }
         switch (key) {
@@ -1726,6 +1835,7 @@ void spmv(const GpuCsr &m, const double *x, double *y, SpmvMode mode, const Spmv
         default: fail(AMG_ERR_INVALID, "DIA: unsupported code layout");
         }
 #undef FAMG_DIA
+#undef FAMG_DIA2
     } else if (m.kernel == SPMV_KERNEL_VECTOR) {
         const int64_t r0 = seg < 0 ? 0 : m.seg_rows[seg];
         const int64_t r1 = seg < 0 ? m.nrows : m.seg_rows[seg + 1];
