@@ -54,6 +54,16 @@ constexpr int SELL_C = 64;
 constexpr int SELL_MAX_W = 512;
 constexpr int64_t SELL_MIN_ROWS = 65536;
 constexpr int VECTOR_MIN_AVG = 256;
+// rows at least this long on average take the wave-per-row kernel; A/B switch
+// FAMG_VECTOR_MIN_AVG (lower values replace SELL on A_2: measured 2.7x slower)
+static int64_t vec_min_avg() {
+    static const int64_t v = [] {
+        const char *e = getenv("FAMG_VECTOR_MIN_AVG");
+        const int64_t x = e ? atoll(e) : 0;
+        return x > 0 ? x : (int64_t)VECTOR_MIN_AVG;
+    }();
+    return v;
+}
 constexpr int64_t SELL_PAIR_MIN_SLICES = 1;  // pairing paid on every level measured (A_2: 55 vs 60 us)
 
 __device__ __forceinline__ int xcd_remap(int b, int nb) {
@@ -1593,7 +1603,8 @@ void build_sell(GpuCsr &m, const std::vector<int64_t> &rp) {
     // auto: SELL pays when there are enough slices to fill the chip (>= 1024
     // slices = 64K rows) and it streams no more than 1.25x the CSR bytes;
     // measured on the 256^3 hierarchy (scripts/ab_levels.py).
-    const bool ok = pol == 2 || (bytes * 100 <= 12 * m.nnz * 125 && (m.nrows >= SELL_MIN_ROWS || maxlen <= 16));
+    const bool ok = pol == 2 || (bytes * 100 <= 12 * m.nnz * 125 && (m.nrows >= SELL_MIN_ROWS || maxlen <= 16) &&
+                                 (vec_min_avg() >= VECTOR_MIN_AVG || m.nnz < vec_min_avg() * m.nrows));
     if (!ok) return;
     m.sell_row0 = std::move(drow0);
     m.sell_soff.resize(ns + 1);
@@ -1701,7 +1712,7 @@ void choose_kernel(GpuCsr &m) {
     if (m.has_dia() && m.dia_r0 == 0 && m.dia_r1 == m.nrows) m.kernel = SPMV_KERNEL_DIA;
     else if (m.has_sell()) m.kernel = SPMV_KERNEL_SELL;
     else if (g_spmv_format_policy == 3 ||
-             (g_spmv_format_policy == 0 && m.nrows > 0 && m.nnz >= VECTOR_MIN_AVG * m.nrows)) {
+             (g_spmv_format_policy == 0 && m.nrows > 0 && m.nnz >= vec_min_avg() * m.nrows)) {
         m.kernel = SPMV_KERNEL_VECTOR;
         build_vec_codes(m);
     }

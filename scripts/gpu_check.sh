@@ -22,6 +22,7 @@ for s in "$@"; do
         dist2) step dist2 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
                   --master-addr 127.0.0.1 --master-port 29511 bench.py --gpus 2 --edge 64 --steps 5 --warmup 1 ;;
         benchnolds) FAMG_DIA_LDS=0 step bench_nolds 400 python bench.py --steps 20 --warmup 3 --no-cpu-baseline ;;
+        levelinfo) step levelinfo 300 python scripts/level_info.py ;;
         ablevels) step ablevels 400 python scripts/ab_levels.py ;;
         pstream) step pstream 300 python scripts/placement_stream.py ;;
         placement) FAMG_ALLOC_DEBUG=1 step placement 300 python scripts/placement.py ;;
