@@ -399,6 +399,15 @@ void MultigridOp::ensure_workspace() {
 // smooth (multigrid.rs:407-424), `steps` times: x <- x + S (b - A x).
 // Fused forms per smoother; the first step from x = 0 needs no SpMV.
 // v/t are the two buffers of the level; Jacobi ping-pongs between them.
+// FAMG_FOLD_DIA=1: fold the zero-guess step on DIA levels too (A/B switch)
+static bool fold_dia_enabled() {
+    static const bool on = [] {
+        const char *e = getenv("FAMG_FOLD_DIA");
+        return e && e[0] == '1';
+    }();
+    return on;
+}
+
 void MultigridOp::smooth(int64_t l, double *&v, double *&t, const double *f, bool v_zero) {
     MgLevel &L = levels[l];
     const int64_t n = L.A->nrows;
@@ -468,8 +477,12 @@ void MultigridOp::cycle(int64_t l, double *v, const double *f, bool v_zero, doub
     // values): value-code SELL and the wave-per-row kernel are latency-bound,
     // and gathering d beside x cost more there than the separate streaming
     // pass (measured on the 256^3 hierarchy).
+    // DIA storage folds only on request (FAMG_FOLD_DIA=1): the residual then
+    // gathers d beside x (139 us vs 105 + 49 for RESID + the d*f pass) but the
+    // correction's d*f epilogue on P_0 cost as much (153 vs 122 us).
     const bool fold = fold_zero_guess && v_zero && steps == 1 && A && D && P &&
-                      A->m.kernel == SPMV_KERNEL_SELL && A->m.sell_vbits == 0;
+                      ((A->m.kernel == SPMV_KERNEL_SELL && A->m.sell_vbits == 0) ||
+                       (A->m.kernel == SPMV_KERNEL_DIA && fold_dia_enabled()));
     if (fold) {
         SpmvEpi epi;
         epi.b = f;
@@ -493,6 +506,8 @@ void MultigridOp::cycle(int64_t l, double *v, const double *f, bool v_zero, doub
         SpmvEpi epi;
         epi.b = f;
         epi.d = D->d.get();
+        epi.dc = D->dcode.get();
+        epi.dt = D->dtab.get();
         spmv(P->m, C.v.get(), t, SPMV_ADD0, epi, s);  // v = d f + P v_c
         std::swap(v, t);                               // (where smooth() would have left v)
     } else if (P) {

@@ -97,7 +97,7 @@ template <int MODE> struct EpiOps {
         }
         if constexpr (MODE == SPMV_RESID || MODE == SPMV_RESID0) br = a.b[row];
         if constexpr (MODE == SPMV_ADD) yr = a.y[row];
-        if constexpr (MODE == SPMV_ADD0) yr = a.d[row] * a.b[row];
+        if constexpr (MODE == SPMV_ADD0) yr = (a.dc ? a.dt[a.dc[row]] : a.d[row]) * a.b[row];
     }
     __device__ __forceinline__ void store(const Epi &a, double acc) const {
         if constexpr (MODE == SPMV_SET) a.y[i] = acc;
@@ -690,7 +690,15 @@ template <int MODE, bool NT = false> struct EpiOps2 {
         }
         if constexpr (MODE == SPMV_RESID || MODE == SPMV_RESID0) br = lds(a.b);
         if constexpr (MODE == SPMV_ADD) yr = lds(a.y);
-        if constexpr (MODE == SPMV_ADD0) yr = lds(a.d) * lds(a.b);
+        if constexpr (MODE == SPMV_ADD0) {
+            if (a.dc) {  // coded diagonal: 1 B per row instead of 8
+                dr.x = a.dt[a.dc[i]];
+                dr.y = l1 ? a.dt[a.dc[i + 1]] : 0.0;
+                yr = dr * lds(a.b);
+            } else {
+                yr = lds(a.d) * lds(a.b);
+            }
+        }
     }
     __device__ __forceinline__ void store(const Epi &a, double acc0, double acc1) const {
         if (!l0) return;
