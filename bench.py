@@ -415,7 +415,7 @@ def run_dist(args, world, rank, local_rank):
         "fine_spmv_gbs": round(float(ga[0]), 1),
         "roofline": {"bound": "hbm", "achieved": round(float(ga[0]), 1), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(float(ga[0]) / HBM_PEAK_GBS, 4), "traffic": None,
-                     "kernel": "spmv_sell_kernel<SET> on the rank-local A_0 (min over ranks)",
+                     "kernel": f"{Al.spmv_info()['kernel']} SpMV (SET) on the rank-local A_0 (min over ranks)",
                      "bytes_per_launch": bytes_spmv, "ms_per_launch": round(spmv_ms, 5)},
         "cpu_baseline": None,
     }
@@ -442,12 +442,14 @@ def main():
     ap.add_argument("--ab", action="store_true", help="A/B the SpMV storage formats (stderr)")
     ap.add_argument("--no-fold", action="store_true",
                     help="store the zero-guess smoothing step instead of folding it into the residual")
+    ap.add_argument("--dist", action="store_true",
+                    help="distributed path even at world size 1 (1-rank RCCL; a check of run_dist)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
+    if world > 1 or args.dist:
         out = run_dist(args, world, rank, local_rank)
     else:
         out = run_single(args)

@@ -23,6 +23,8 @@ for s in "$@"; do
                   --master-addr 127.0.0.1 --master-port 29511 bench.py --gpus 2 --edge 64 --steps 5 --warmup 1 ;;
         benchnolds) FAMG_DIA_LDS=0 step bench_nolds 400 python bench.py --steps 20 --warmup 3 --no-cpu-baseline ;;
         levelinfo) step levelinfo 300 python scripts/level_info.py ;;
+        dist1) step dist1 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 \
+                  --master-addr 127.0.0.1 --master-port 29513 bench.py --dist --edge 256 --steps 10 --warmup 2 ;;
         ablevels) step ablevels 400 python scripts/ab_levels.py ;;
         pstream) step pstream 300 python scripts/placement_stream.py ;;
         placement) FAMG_ALLOC_DEBUG=1 step placement 300 python scripts/placement.py ;;
