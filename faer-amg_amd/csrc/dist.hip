@@ -441,10 +441,12 @@ struct DistMultigridOp : LinOp {
         spmv(m, x, y, mode, epi, s, 2);
     }
 
-    void smooth(int64_t l, double *&v, double *&t, const double *f, bool zero) {
+    // last_out: the final step writes there (owned rows only) instead of t
+    void smooth(int64_t l, double *&v, double *&t, const double *f, bool zero, double *last_out = nullptr) {
         DLevel &D = L[l];
         hipStream_t s = ctx->stream;
         for (int64_t it = 0; it < steps; it++) {
+            if (last_out && it + 1 == steps) t = last_out;
             if (zero && it == 0) {
                 if (D.S->dcode.get()) vec_mul_coded(t, D.S->dcode.get(), D.S->dtab.get(), f, D.sp.n_own, s);
                 else vec_mul(t, D.S->d.get(), f, D.sp.n_own, s);
@@ -473,7 +475,9 @@ struct DistMultigridOp : LinOp {
         }
     }
 
-    void cycle(int64_t l, double *v, const double *f, bool zero) {
+    // out (level 0 only, may be null): the post-smoothing's last Jacobi step
+    // writes the owned rows there directly, saving the final n_own copy
+    void cycle(int64_t l, double *v, const double *f, bool zero, double *out = nullptr) {
         DLevel &D = L[l];
         hipStream_t s = ctx->stream;
         double *v0 = v;
@@ -495,7 +499,9 @@ struct DistMultigridOp : LinOp {
             for (int64_t k = 0; k < mu; k++) tail->cycle(0, vc_full.get(), fc_full.get(), k == 0, nullptr);
             spmv(D.P->m, vc_full.get(), v, SPMV_ADD, SpmvEpi{}, s);
         }
-        smooth(l, v, t, f, false);
+        const bool direct = out && steps >= 1 && D.S;
+        smooth(l, v, t, f, false, direct ? out : nullptr);
+        if (direct) return;
         if (v != v0) vec_copy(v0, v, D.sp.n_own, s);
     }
 
@@ -544,8 +550,12 @@ struct DistMultigridOp : LinOp {
             if (cnt) vec_copy(out, vc_full.get() + r0, cnt, s);
             return;
         }
-        cycle(0, L[0].v.get(), rhs, true);
-        vec_copy(out, L[0].v.get(), L[0].sp.n_own, s);
+        if (out != rhs) {
+            cycle(0, L[0].v.get(), rhs, true, out);
+        } else {  // in place: rhs is read by the last step's epilogue
+            cycle(0, L[0].v.get(), rhs, true);
+            vec_copy(out, L[0].v.get(), L[0].sp.n_own, s);
+        }
     }
 };
 
@@ -678,6 +688,14 @@ static std::shared_ptr<DistMultigridOp> build_dist(amg_comm *comm, const Multigr
     d->tail->steps = g.steps;
     for (int64_t l = d->La; l < d->nlevels; l++) d->tail->levels.push_back(MgLevel{g.levels[l].A, g.levels[l].S, g.levels[l].R, g.levels[l].P});
     d->tail->nrows = d->tail->ncols = g.levels[d->La].A->nrows;
+    // the tail is cycled redundantly on every rank: under the auto policy,
+    // CSR-stream matrices (e.g. from a global setup copy built CSR-only) get
+    // the storage the policy picks now (SELL / wave-per-row)
+    if (g_spmv_format_policy == 0)
+        for (auto &lv : d->tail->levels)
+            for (const LinOpPtr &op : {lv.A, lv.R, lv.P})
+                if (auto *c = dynamic_cast<CsrOp *>(op.get()))
+                    if (c->m.kernel == SPMV_KERNEL_STREAM) csr_finalize(c->m, nullptr);
     d->tail_splits = sp_of(d->La);
     for (int q = 0; q < P; q++) d->tail_max = std::max(d->tail_max, d->tail_splits[q + 1] - d->tail_splits[q]);
     const int64_t nt = g.levels[d->La].A->nrows;
