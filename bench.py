@@ -102,41 +102,128 @@ def weak_dims(n, N):
     return tuple(d)
 
 
-def cpu_baseline(mg, b, threads, smoother="jacobi", budget_s=12.0, max_cycles=40):
-    """The reference's rayon path restated (oracle: ParSpmmOp 8192x8192 CSC tiles,
-    usize indices, per-call temporaries) on the same hierarchy."""
+def oracle_levels(mg, smoother):
+    """The GPU hierarchy's arrays (A_l, R_l, P_l exactly as the V-cycle uses them)
+    as oracle levels, with the smoother each level actually got."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
-    import numpy as np
     import oracle as O
     levels = []
     nl = mg.levels()
     for l in range(nl):
         Al, Sl, Rl, Pl = mg.level(l)
         kind = Sl.kind
+        d = {"A": O.Csr.from_arrays(*Al.dims(), *Al.arrays())}
         if l == nl - 1:
-            sm = "chol"
+            d["smoother"] = "chol"
         elif kind == "sgs":
-            sm = "sgs"
+            d["smoother"] = "sgs"
         elif kind == "diag":
-            sm = "jacobi" if smoother == "jacobi" else "l1"
+            d["smoother"] = "jacobi" if smoother == "jacobi" else "l1"
+        elif kind == "block":
+            # BlockSmoother::into_sparse_mat (block_smoothers.rs:122-146)
+            M = fa_block_to_csr(Sl)
+            d["smoother"] = ("csr", O.Csr.from_arrays(*M.dims(), *M.arrays()))
         else:
-            raise NotImplementedError(f"no CPU restatement of the {kind} smoother in the C oracle")
-        d = {"A": O.Csr.from_arrays(*Al.dims(), *Al.arrays()), "smoother": sm}
+            raise ValueError(f"no CPU restatement of the {kind} smoother")
         if Rl is not None:
             d["R"] = O.Csr.from_arrays(*Rl.dims(), *Rl.arrays())
             d["P"] = O.Csr.from_arrays(*Pl.dims(), *Pl.arrays())
         levels.append(d)
-    omg = O.Multigrid(levels)
-    omg.set_parallel(threads)
+    return levels
+
+
+def fa_block_to_csr(S):
+    import faer_amg_amd as fa
+    h = fa.vp()
+    fa._ck(fa.lib().amg_block_smoother_to_csr(S.h, fa.C.byref(h)))
+    return fa.SparseMatOp(h, S.ctx)
+
+
+def _time_cycles(omg, b, budget_s, max_cycles=60, min_cycles=3):
+    """Per-V-cycle wall times of the oracle (after one warm-up cycle)."""
+    import numpy as np
+    import oracle as O
     out = np.empty_like(b)
-    O.lib().orc_mg_apply(omg.h, b, out)  # warm-up (page faults)
-    t0 = time.perf_counter()
-    cycles = 0
-    while cycles < max_cycles and (time.perf_counter() - t0) < budget_s:
+    O.lib().orc_mg_apply(omg.h, b, out)  # warm-up (page faults, ParSpmm tiles)
+    ts = []
+    t_end = time.perf_counter() + budget_s
+    while len(ts) < max_cycles and (len(ts) < min_cycles or time.perf_counter() < t_end):
+        t0 = time.perf_counter()
         O.lib().orc_mg_apply(omg.h, b, out)
-        cycles += 1
-    dt = time.perf_counter() - t0
-    return cycles / dt, cycles, dt
+        ts.append(time.perf_counter() - t0)
+    return ts, out
+
+
+def cpu_side(mg, A, b_host, z_gpu, args):
+    """Everything the CPU restatement contributes to the bench line, on the SAME
+    hierarchy (the GPU's A_l, R_l, P_l arrays):
+      parity      -- ||z_gpu - z_oracle|| / ||z_oracle|| for one V-cycle (<= 1e-11,
+                     SURVEY.md 8(c)) and rho_k of 10 stationary cycles GPU vs oracle
+      cpu_baseline -- the reference's rayon path restated (ParSpmmOp 8192x8192 CSC
+                     tiles with usize indices, per-call temporaries; par_spmm.rs,
+                     multigrid.rs:251-424): median V-cycle time at 16 threads
+                     (Par::Rayon(16), examples/amg/main.rs:227) and at all host cores,
+                     plus the fine-level ParSpmm SpMV in GB/s."""
+    import numpy as np
+    import torch
+    import faer_amg_amd as fa
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as O
+
+    t_imp = time.perf_counter()
+    levels = oracle_levels(mg, args.smoother)
+    omg = O.Multigrid(levels)
+    OA = levels[0]["A"]
+    log(f"oracle hierarchy import {time.perf_counter() - t_imp:.1f}s")
+    nproc = os.cpu_count() or 1
+    all_threads = min(nproc, 64)
+    t16 = args.cpu_threads
+
+    # parity of one V-cycle (the bench's own z from the timed loop)
+    omg.set_parallel(t16)
+    ts16, zref = _time_cycles(omg, b_host, args.cpu_budget)
+    rel_err = float(np.linalg.norm(z_gpu - zref) / np.linalg.norm(zref))
+    # residual history of 10 stationary cycles (simple_geometric.rs:117-158)
+    K = 10
+    bd = torch.as_tensor(b_host, device="cuda:0")
+    xd = torch.zeros_like(bd)
+    _, hist_gpu = fa.stationary_solve(A, mg, bd, xd, max_iter=K + 1, rel_tol=1e-300)
+    _, _, hist_cpu = O.stationary_solve(OA, omg, b_host, max_iter=K + 1, rel_tol=1e-300)
+    torch.cuda.synchronize()
+    rho_rel = float(np.max(np.abs(hist_gpu - hist_cpu) / hist_cpu))
+
+    # fine-level SpMV of the restated rayon path (ParSpmmOp), 16 threads
+    par = O.ParSpmm(OA)
+    x = np.ones(OA.ncols)
+    par.apply(x)
+    tsp = []
+    for _ in range(5):
+        t0 = time.perf_counter()
+        par.apply(x)
+        tsp.append(time.perf_counter() - t0)
+    m, n, nnz = OA.dims()
+    spmv_t = float(np.median(tsp))
+    del par
+
+    res = {"value": round(1.0 / float(np.median(ts16)), 4), "unit": "V-cycles/s", "cores": t16,
+           "kind": "port",
+           "sample": f"median of {len(ts16)} V-cycles of the same {args.edge}^3 hierarchy "
+                     f"(oracle restatement of the rayon path: ParSpmmOp 8192x8192 CSC tiles, "
+                     f"usize indices, per-call temporaries; OpenMP {t16} threads = Par::Rayon(16))",
+           "fine_spmv_ms": round(spmv_t * 1e3, 3),
+           "fine_spmv_GBs_32bit_formula": round(spmv_bytes(m, n, nnz) / spmv_t / 1e9, 2),
+           "fine_spmv_GBs_usize_layout": round((16 * nnz + 8 * (m + 1) + 8 * n + 8 * m) / spmv_t / 1e9, 2)}
+    if all_threads != t16:
+        omg.set_parallel(all_threads)
+        tsa, _ = _time_cycles(omg, b_host, args.cpu_budget / 2)
+        res["all_cores"] = {"value": round(1.0 / float(np.median(tsa)), 4), "cores": all_threads,
+                            "nproc": nproc, "sample": f"median of {len(tsa)} V-cycles"}
+    parity = {"vcycle_rel_err": rel_err, "tol": 1e-11, "ok": rel_err <= 1e-11,
+              "rho_k_gpu": [float(v) for v in hist_gpu], "rho_k_cpu": [float(v) for v in hist_cpu],
+              "rho_k_max_rel_diff": rho_rel,
+              "what": "one V-cycle z = M b and 10 stationary cycles (rho_k = ||b - A x_k||/||b||), "
+                      "GPU vs the oracle restatement on the same hierarchy"}
+    return res, parity
 
 
 def build_problem(fa, ctx, args, dims):
@@ -268,17 +355,14 @@ def run_single(args):
     vbytes = vcycle_bytes(mg, fold=not args.no_fold)
     vbytes_csr = vcycle_bytes(mg, csr=True, fold=not args.no_fold)
 
-    cpu = None
+    cpu, parity = None, None
     if not args.no_cpu_baseline:
         try:
-            v, cyc, dt = cpu_baseline(mg, b_host, args.cpu_threads, args.smoother)
-            cpu = {"value": round(v, 4), "unit": "V-cycles/s", "cores": args.cpu_threads,
-                   "kind": "port",
-                   "sample": f"{cyc} V-cycles of the same {args.edge}^3 hierarchy in {dt:.1f}s "
-                             f"(oracle restatement of the rayon path: ParSpmmOp 8192x8192 CSC "
-                             f"tiles, usize indices; OpenMP {args.cpu_threads} threads)"}
+            cpu, parity = cpu_side(mg, A, b_host, z.cpu().numpy(), args)
+            log(f"parity: V-cycle rel err {parity['vcycle_rel_err']:.3e}, "
+                f"rho_k max rel diff {parity['rho_k_max_rel_diff']:.3e}")
         except Exception as e:  # the baseline must not kill the GPU measurement
-            log(f"cpu baseline failed: {e!r}")
+            log(f"cpu baseline / parity failed: {e!r}")
 
     cycles_per_s = 1000.0 / ms_per_cycle
     traffic, traffic_src = measured_traffic(args.edge, args.problem)
@@ -316,6 +400,7 @@ def run_single(args):
                      "csr_equivalent_GBs": round(bytes_csr / (spmv_ms * 1e-3) / 1e9, 1),
                      "fp64_values": fp64_values},
         "cpu_baseline": cpu,
+        "parity": parity,
     }
 
 
@@ -436,6 +521,8 @@ def main():
                     help="levels with fewer global rows run redundantly on every rank")
     ap.add_argument("--cpu-threads", type=int, default=int(os.environ.get("OMP_NUM_THREADS", "16")))
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-budget", type=float, default=20.0,
+                    help="seconds of CPU V-cycles at --cpu-threads (half that at all cores)")
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--no-overlap", action="store_true",
                     help="distributed: exchange halos before the SpMV instead of under its interior rows")

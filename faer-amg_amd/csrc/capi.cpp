@@ -250,6 +250,18 @@ amg_status amg_csr_value_codes(const amg_linop *op, int64_t *info2) {
     });
 }
 
+amg_status amg_csr_dia_range(const amg_linop *op, int64_t *info4) {
+    return guard([&] {
+        FAMG_REQUIRE(info4, AMG_ERR_INVALID, "null argument");
+        const GpuCsr &m = need_csr(op)->m;
+        const bool on = m.has_dia();
+        info4[0] = on ? m.dia_r0 : 0;
+        info4[1] = on ? m.dia_r1 : 0;
+        info4[2] = on ? m.dia_k : 0;
+        info4[3] = on ? m.dia_vbits : 0;
+    });
+}
+
 amg_status amg_csr_download(const amg_linop *op, int64_t *rowptr, int64_t *colidx, double *vals) {
     return guard([&] {
         auto p = need_csr(op);

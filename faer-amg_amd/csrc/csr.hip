@@ -32,6 +32,18 @@ void csr_alloc(GpuCsr &m, Ctx *ctx, int64_t nrows, int64_t ncols, int64_t nnz) {
     m.nblocks = 0;
 }
 
+void csr_clone(const GpuCsr &src, GpuCsr &dst) {
+    csr_alloc(dst, src.ctx, src.nrows, src.ncols, src.nnz);
+    hipStream_t s = src.ctx->stream;
+    FAMG_CHECK_HIP(hipMemcpyAsync(dst.rp64.get(), src.rp64.get(), (src.nrows + 1) * sizeof(int64_t),
+                                  hipMemcpyDeviceToDevice, s));
+    if (src.nnz) {
+        FAMG_CHECK_HIP(hipMemcpyAsync(dst.col.get(), src.col.get(), src.nnz * sizeof(int32_t), hipMemcpyDeviceToDevice, s));
+        FAMG_CHECK_HIP(hipMemcpyAsync(dst.val.get(), src.val.get(), src.nnz * sizeof(double), hipMemcpyDeviceToDevice, s));
+    }
+    FAMG_CHECK_HIP(hipStreamSynchronize(s));
+}
+
 __global__ void k_narrow_rp(const int64_t *rp64, int32_t *rp32, int64_t n1) {
     const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
     if (i < n1) rp32[i] = static_cast<int32_t>(rp64[i]);

@@ -505,17 +505,19 @@ struct DistMultigridOp : LinOp {
         if (v != v0) vec_copy(v0, v, D.sp.n_own, s);
     }
 
-    // r_own = b_own - (A_0 x)_own for the finest level, distributed or not
-    DevBuf<double> xg_, rfull_;
-    void residual0(const double *b, const double *x, double *r) {
+    // Allocation length of a level-0 vector that A_0 reads in place: the owned
+    // rows, then room for the halo entries (the solve loops keep x and p so)
+    int64_t n_alloc0() const { return La > 0 ? L[0].sp.n_own + L[0].sp.n_ghost : nrows; }
+
+    // r_own = b_own - (A_0 x)_own for the finest level, distributed or not; x
+    // has n_alloc0() entries and its halo region is overwritten (no copy)
+    DevBuf<double> rfull_;
+    void residual0(const double *b, double *x, double *r) {
         hipStream_t s = ctx->stream;
         SpmvEpi epi;
         epi.b = b;
         if (La > 0) {
-            DLevel &D = L[0];
-            if (xg_.size() < (size_t)(D.sp.n_own + D.sp.n_ghost + 1)) xg_.resize(D.sp.n_own + D.sp.n_ghost + 1);
-            vec_copy(xg_.get(), x, D.sp.n_own, s);
-            halo_spmv(D.sp, xg_.get(), D.A->m, r, SPMV_RESID, epi);
+            halo_spmv(L[0].sp, x, L[0].A->m, r, SPMV_RESID, epi);
             return;
         }
         // everything replicated: gather x, global SpMV, keep the owned rows
@@ -528,15 +530,20 @@ struct DistMultigridOp : LinOp {
         if (cnt) vec_sub(r, b, rfull_.get() + r0, cnt, s);
     }
 
-    // out_own = (A_0 x)_own, distributed or not
-    DevBuf<double> zero_;
-    void apply0(double *out, const double *x) {
-        if (zero_.size() < (size_t)std::max<int64_t>(1, nrows)) {
-            zero_.resize(std::max<int64_t>(1, nrows));
-            vec_fill(zero_.get(), 0.0, nrows, ctx->stream);
+    // out_own = (A_0 x)_own, distributed or not (x as in residual0)
+    void apply0(double *out, double *x) {
+        hipStream_t s = ctx->stream;
+        if (La > 0) {
+            halo_spmv(L[0].sp, x, L[0].A->m, out, SPMV_SET, SpmvEpi{});
+            return;
         }
-        residual0(zero_.get(), x, out);           // 0 - A x
-        vec_scale(out, -1.0, nrows, ctx->stream);  // exact
+        auto *A = dynamic_cast<CsrOp *>(tail->levels[0].A.get());
+        FAMG_REQUIRE(A, AMG_ERR_UNSUPPORTED, "finest operator is not CSR");
+        const int64_t r0 = tail_splits[tr->rank], cnt = tail_splits[tr->rank + 1] - r0;
+        if (rfull_.size() < (size_t)A->nrows) rfull_.resize(A->nrows);
+        gather_tail(x);
+        spmv(A->m, fc_full.get(), rfull_.get(), SPMV_SET, SpmvEpi{}, s);
+        if (cnt) vec_copy(out, rfull_.get() + r0, cnt, s);
     }
 
     void apply(double *out, const double *rhs) override {
@@ -565,7 +572,12 @@ struct DistLevelOp : LinOp {
     int64_t level = 0;
     DevBuf<double> x;
     Kind kind() const override { return Kind::DistCsr; }
+    // The caller's rhs holds the owned rows only (LinOp::apply hands over an
+    // n_own vector), so it is staged into a buffer with room for the halo; the
+    // V-cycle and the solve loops read their own padded vectors in place.
     void apply(double *out, const double *rhs) override {
+        std::lock_guard<std::mutex> lk(mg->mtx);  // halo buffers/events are shared with the V-cycle
+        ctx->set_device();
         DLevel &D = mg->L[level];
         hipStream_t s = ctx->stream;
         vec_copy(x.get(), rhs, D.sp.n_own, s);
@@ -686,16 +698,27 @@ static std::shared_ptr<DistMultigridOp> build_dist(amg_comm *comm, const Multigr
     d->tail->ctx = ctx;
     d->tail->mu = g.mu;
     d->tail->steps = g.steps;
+    d->tail->fold_zero_guess = g.fold_zero_guess;
+    d->tail->sgs_residual_form = g.sgs_residual_form;
     for (int64_t l = d->La; l < d->nlevels; l++) d->tail->levels.push_back(MgLevel{g.levels[l].A, g.levels[l].S, g.levels[l].R, g.levels[l].P});
     d->tail->nrows = d->tail->ncols = g.levels[d->La].A->nrows;
     // the tail is cycled redundantly on every rank: under the auto policy,
     // CSR-stream matrices (e.g. from a global setup copy built CSR-only) get
-    // the storage the policy picks now (SELL / wave-per-row)
+    // the storage the policy picks now (SELL / wave-per-row).  That happens on
+    // private copies: g's operators (and any hipGraph g captured over their
+    // buffers) stay untouched.
     if (g_spmv_format_policy == 0)
         for (auto &lv : d->tail->levels)
-            for (const LinOpPtr &op : {lv.A, lv.R, lv.P})
-                if (auto *c = dynamic_cast<CsrOp *>(op.get()))
-                    if (c->m.kernel == SPMV_KERNEL_STREAM) csr_finalize(c->m, nullptr);
+            for (LinOpPtr *op : {&lv.A, &lv.R, &lv.P})
+                if (auto *c = dynamic_cast<CsrOp *>(op->get()))
+                    if (c->m.kernel == SPMV_KERNEL_STREAM) {
+                        CsrPtr cp = make_csr(ctx);
+                        csr_clone(c->m, cp->m);
+                        csr_finalize(cp->m, nullptr);
+                        cp->nrows = c->nrows;
+                        cp->ncols = c->ncols;
+                        if (cp->m.kernel != SPMV_KERNEL_STREAM) *op = cp;
+                    }
     d->tail_splits = sp_of(d->La);
     for (int q = 0; q < P; q++) d->tail_max = std::max(d->tail_max, d->tail_splits[q + 1] - d->tail_splits[q]);
     const int64_t nt = g.levels[d->La].A->nrows;
@@ -902,12 +925,14 @@ static SolveOps dist_ops(const std::shared_ptr<DistMultigridOp> &d, bool precond
     SolveOps o;
     o.ctx = d->ctx;
     o.n = d->nrows;
+    o.n_alloc = d->n_alloc0();
     DistMultigridOp *dm = d.get();
-    o.A = [dm](double *out, const double *x) {
+    o.A = [dm](double *out, double *x) {
         std::lock_guard<std::mutex> lk(dm->mtx);
+        dm->ctx->set_device();
         dm->apply0(out, x);
     };
-    o.resid = [dm](double *r, const double *b, const double *x) {
+    o.resid = [dm](double *r, const double *b, double *x) {
         std::lock_guard<std::mutex> lk(dm->mtx);
         dm->residual0(b, x, r);
     };

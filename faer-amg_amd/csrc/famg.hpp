@@ -87,6 +87,9 @@ struct GpuCsr {
 
 // Allocate a CSR with the given shape/nnz (arrays uninitialised).
 void csr_alloc(GpuCsr &m, Ctx *ctx, int64_t nrows, int64_t ncols, int64_t nnz);
+// Device copy of the CSR arrays (rp64/col/val) of src into dst; dst is not
+// finalized (call csr_finalize for its SpMV storage).
+void csr_clone(const GpuCsr &src, GpuCsr &dst);
 // Build rp32 (if nnz < 2^31), the stream schedule, the SELL-64 copy for short
 // regular rows, and pick the SpMV kernel; `segments` (row bounds, first 0, last
 // nrows) keeps blocks/slices inside segments.  Host pass over the row pointers

@@ -21,11 +21,20 @@ void residual(LinOp &A, double *r, const double *b, const double *x) {
     vec_sub(r, b, r, A.nrows, s);
 }
 
-int64_t stationary_impl(const SolveOps &o, const double *b, double *x, int64_t max_iter, double rel_tol,
+// x in a buffer of the operator's allocation length (the caller's when that is n)
+static double *padded_x(const SolveOps &o, double *x, DevBuf<double> &xp) {
+    if (o.n_alloc <= o.n) return x;
+    xp.resize(o.n_alloc);
+    vec_copy(xp.get(), x, o.n, o.ctx->stream);
+    return xp.get();
+}
+
+int64_t stationary_impl(const SolveOps &o, const double *b, double *x_user, int64_t max_iter, double rel_tol,
                         double *hist) {
     hipStream_t s = o.ctx->stream;
     const int64_t n = o.n;
-    DevBuf<double> r(std::max<int64_t>(1, n)), z(std::max<int64_t>(1, n));
+    DevBuf<double> r(std::max<int64_t>(1, n)), z(std::max<int64_t>(1, n)), xp;
+    double *x = padded_x(o, x_user, xp);
     const double bn = std::sqrt(o.dot(b, b));
     int64_t it = 0;
     for (;;) {
@@ -37,6 +46,7 @@ int64_t stationary_impl(const SolveOps &o, const double *b, double *x, int64_t m
         o.M(z.get(), r.get());
         vec_add_inplace(x, z.get(), n, s);
     }
+    if (x != x_user) vec_copy(x_user, x, n, s);
     FAMG_CHECK_HIP(hipStreamSynchronize(s));
     return it;
 }
@@ -46,8 +56,8 @@ int64_t pcg_impl(const SolveOps &o, const double *b, double *x, int64_t max_iter
     hipStream_t s = o.ctx->stream;
     const int64_t n = o.n;
     const int64_t nb = std::max<int64_t>(1, n);
-    DevBuf<double> r(nb), z(nb), p(nb), Ap(nb);
-    o.resid(r.get(), b, x);
+    DevBuf<double> r(nb), z(nb), p(std::max(nb, o.n_alloc)), Ap(nb), xp;
+    o.resid(r.get(), b, padded_x(o, x, xp));  // x itself only moves by axpys below
     const double bn = std::sqrt(o.dot(b, b));
     const double tol = std::max(rel_tol * bn, abs_tol);
     int64_t it = 0;
@@ -107,8 +117,9 @@ SolveOps single_gpu_ops(LinOp &a, LinOp *m) {
     SolveOps o;
     o.ctx = a.ctx;
     o.n = a.nrows;
-    o.A = [&a](double *out, const double *x) { a.apply(out, x); };
-    o.resid = [&a](double *r, const double *b, const double *x) { residual(a, r, b, x); };
+    o.n_alloc = a.nrows;
+    o.A = [&a](double *out, double *x) { a.apply(out, x); };
+    o.resid = [&a](double *r, const double *b, double *x) { residual(a, r, b, x); };
     if (m) o.M = [m](double *out, const double *r) { m->apply(out, r); };
     Ctx *ctx = a.ctx;
     const int64_t n = a.nrows;

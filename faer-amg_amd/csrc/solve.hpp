@@ -16,8 +16,12 @@ namespace famg {
 struct SolveOps {
     Ctx *ctx = nullptr;
     int64_t n = 0;                                                          // local rows
-    std::function<void(double *out, const double *x)> A;                    // out = A x
-    std::function<void(double *r, const double *b, const double *x)> resid;  // r = b - A x
+    // allocation length of the vectors A and resid read (>= n): a distributed
+    // operator keeps its halo entries behind the owned rows, so the loops keep
+    // x and p in buffers of this length and A reads them in place
+    int64_t n_alloc = 0;
+    std::function<void(double *out, double *x)> A;                          // out = A x (x: n_alloc, halo written)
+    std::function<void(double *r, const double *b, double *x)> resid;        // r = b - A x (x: n_alloc)
     std::function<void(double *out, const double *r)> M;                    // out = M r (empty: identity)
     std::function<double(const double *, const double *)> dot;              // global dot
 };

@@ -1488,8 +1488,12 @@ __global__ __launch_bounds__(256) void k_dia_fill(const int64_t *rp, const int32
 static bool build_dia(GpuCsr &m, int vb, const std::vector<unsigned long long> &tab,
                       const std::vector<int64_t> &rp, int64_t r0, int64_t r1) {
     const int64_t nr = r1 - r0;
-    if (g_spmv_format_policy != 0 || (vb != 4 && vb != 8) || m.nrows != m.ncols || nr < SELL_MIN_ROWS ||
-        m.nrows >= (int64_t(1) << 30))
+    // a rectangular matrix qualifies only through a row segment (the halo
+    // interior of a distributed level: [owned | ghost] columns); every stored
+    // entry's column is row + off, so only padding entries are clamped
+    const bool square_or_segment = m.nrows == m.ncols || (m.seg_rows.size() > 2 && m.ncols >= m.nrows);
+    if (g_spmv_format_policy != 0 || (vb != 4 && vb != 8) || !square_or_segment || nr < SELL_MIN_ROWS ||
+        m.ncols >= (int64_t(1) << 30))
         return false;
     hipStream_t s = m.ctx->stream;
     DevBuf<int> slots(DIA_SLOTS);
@@ -1782,30 +1786,10 @@ void spmv(const GpuCsr &m, const double *x, double *y, SpmvMode mode, const Spmv
     FAMG_REQUIRE(mode != SPMV_SGS || epi.perm, AMG_ERR_INVALID, "SGS mode needs a permutation");
     Epi e{x, y, epi.b, epi.d, epi.perm, epi.dc, epi.dt};
     const dim3 block(256);
-    if (m.kernel == SPMV_KERNEL_SELL) {
-        const int64_t s0 = seg < 0 ? 0 : m.seg_slc[seg];
-        const int64_t s1 = seg < 0 ? m.nslices : m.seg_slc[seg + 1];
-        if (s1 <= s0) return;
-        SellArgs a{m.sell_row0.get(), m.sell_soff.get(), m.sell_desc.get(), m.sell_base.get(),
-                   m.sell_data.get(), (int32_t)s0, (int32_t)(s1 - s0), e, m.sell_vtab.get(),
-                   (int32_t)m.sell_ntab, 1};
-        // value codes: two slices per wave when there are enough waves to fill the chip twice over
-        const int lay = m.sell_vbits ? 4 : 0;
-        if (sell_slices_per_wave(lay, mode) == 2 && s1 - s0 >= SELL_PAIR_MIN_SLICES) a.spw = 2;
-        const dim3 grid((unsigned)ceil_div(s1 - s0, 4 * a.spw * sell_groups_per_wave(lay)));
-        if (m.sell_vbits == 4) {
-            FAMG_LAUNCH_MODES(spmv_sell_kernel, grid, block, s, a, FAMG_LAY4)
-        } else if (m.sell_vbits == 8) {
-            FAMG_LAUNCH_MODES(spmv_sell_kernel, grid, block, s, a, FAMG_LAY8)
-        } else if (m.sell_vbits == 16) {
-            FAMG_LAUNCH_MODES(spmv_sell_kernel, grid, block, s, a, FAMG_LAY16)
-        } else if (m.sell_paired) {
-            FAMG_LAUNCH_MODES(spmv_sell_kernel, grid, block, s, a, FAMG_LAY1)
-        } else {
-            FAMG_LAUNCH_MODES(spmv_sell_kernel, grid, block, s, a, FAMG_LAY0)
-        }
-    } else if (m.kernel == SPMV_KERNEL_DIA ||
-               (m.has_dia() && seg >= 0 && seg == m.dia_seg && mode != SPMV_SGS)) {
+    // a DIA row segment (the halo interior of a distributed level) runs DIA
+    // even when the rest of the matrix is SELL storage
+    if (m.kernel == SPMV_KERNEL_DIA ||
+        (m.has_dia() && seg >= 0 && seg == m.dia_seg && mode != SPMV_SGS)) {
         FAMG_REQUIRE(mode != SPMV_SGS, AMG_ERR_UNSUPPORTED, "DIA storage has no SGS sweep");
         const int64_t r0 = seg < 0 ? 0 : m.seg_rows[seg];
         const int64_t r1 = seg < 0 ? m.nrows : m.seg_rows[seg + 1];
@@ -1855,6 +1839,28 @@ void spmv(const GpuCsr &m, const double *x, double *y, SpmvMode mode, const Spmv
         }
 #undef FAMG_DIA
 #undef FAMG_DIA2
+    } else if (m.kernel == SPMV_KERNEL_SELL) {
+        const int64_t s0 = seg < 0 ? 0 : m.seg_slc[seg];
+        const int64_t s1 = seg < 0 ? m.nslices : m.seg_slc[seg + 1];
+        if (s1 <= s0) return;
+        SellArgs a{m.sell_row0.get(), m.sell_soff.get(), m.sell_desc.get(), m.sell_base.get(),
+                   m.sell_data.get(), (int32_t)s0, (int32_t)(s1 - s0), e, m.sell_vtab.get(),
+                   (int32_t)m.sell_ntab, 1};
+        // value codes: two slices per wave when there are enough waves to fill the chip twice over
+        const int lay = m.sell_vbits ? 4 : 0;
+        if (sell_slices_per_wave(lay, mode) == 2 && s1 - s0 >= SELL_PAIR_MIN_SLICES) a.spw = 2;
+        const dim3 grid((unsigned)ceil_div(s1 - s0, 4 * a.spw * sell_groups_per_wave(lay)));
+        if (m.sell_vbits == 4) {
+            FAMG_LAUNCH_MODES(spmv_sell_kernel, grid, block, s, a, FAMG_LAY4)
+        } else if (m.sell_vbits == 8) {
+            FAMG_LAUNCH_MODES(spmv_sell_kernel, grid, block, s, a, FAMG_LAY8)
+        } else if (m.sell_vbits == 16) {
+            FAMG_LAUNCH_MODES(spmv_sell_kernel, grid, block, s, a, FAMG_LAY16)
+        } else if (m.sell_paired) {
+            FAMG_LAUNCH_MODES(spmv_sell_kernel, grid, block, s, a, FAMG_LAY1)
+        } else {
+            FAMG_LAUNCH_MODES(spmv_sell_kernel, grid, block, s, a, FAMG_LAY0)
+        }
     } else if (m.kernel == SPMV_KERNEL_VECTOR) {
         const int64_t r0 = seg < 0 ? 0 : m.seg_rows[seg];
         const int64_t r1 = seg < 0 ? m.nrows : m.seg_rows[seg + 1];

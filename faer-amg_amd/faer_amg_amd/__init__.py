@@ -58,6 +58,7 @@ SIGNATURES = {
     "amg_csr_spmv_info": (i32, [vp, vp]),
     "amg_csr_value_codes": (i32, [vp, vp]),
     "amg_csr_download": (i32, [vp, vp, vp, vp]),
+    "amg_csr_dia_range": (i32, [vp, vp]),
     "amg_gen_laplace3d_7pt": (i32, [vp, i64, i64, i64, P(vp)]),
     "amg_gen_aniso27": (i32, [vp, i64, i64, i64, dbl, dbl, dbl, P(vp)]),
     "amg_linop_kind_of": (i32, [vp, P(i32)]),
@@ -376,6 +377,10 @@ class SparseMatOp(LinOp):
         vc = np.zeros(2, np.int64)
         _ck(_lib.amg_csr_value_codes(self.h, vc.ctypes.data_as(vp)))
         d["value_bits"], d["value_table"] = int(vc[0]), int(vc[1])
+        dr = np.zeros(4, np.int64)
+        _ck(_lib.amg_csr_dia_range(self.h, dr.ctypes.data_as(vp)))
+        d["dia_rows"] = (int(dr[0]), int(dr[1]))
+        d["dia_diagonals"], d["dia_bits"] = int(dr[2]), int(dr[3])
         return d
 
     def arrays(self):

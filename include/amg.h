@@ -119,6 +119,11 @@ amg_status amg_csr_spmv_info(const amg_linop *op, int64_t *info8);
 /* Value codes of a CSR operator's SpMV storage: info2 = {code bits (0 = fp64
  * values, 4, 8, 16), table entries}. */
 amg_status amg_csr_value_codes(const amg_linop *op, int64_t *info2);
+/* DIA-code rows of a CSR operator's SpMV storage: info4 = {first row, end row,
+ * diagonals, code bits}; all 0 without DIA storage.  The range is the whole
+ * matrix (kernel 3 in amg_csr_spmv_info) or one row segment beside SELL / CSR
+ * storage (the halo interior of a distributed level). */
+amg_status amg_csr_dia_range(const amg_linop *op, int64_t *info4);
 /* Copy a CSR operator back to host arrays (rowptr: nrows+1, colidx/vals: nnz). */
 amg_status amg_csr_download(const amg_linop *op, int64_t *rowptr, int64_t *colidx, double *vals);
 /* Device-side generators for the benchmark operators:

@@ -693,6 +693,7 @@ typedef struct {
     int64_t *color;    /* sgs */
     int64_t ncolors;
     double *L;         /* dense Cholesky factor */
+    const orc_csr *M;  /* explicit smoother matrix (borrowed) */
 } orc_smoother;
 
 struct orc_mg {
@@ -779,6 +780,13 @@ int orc_mg_set_chol(orc_mg *mg, int64_t level) {
     return rc;
 }
 
+void orc_mg_set_csr_smoother(orc_mg *mg, int64_t level, const orc_csr *M) {
+    orc_smoother *s = &mg->S[level];
+    free_smoother(s);
+    s->kind = ORC_SM_CSR;
+    s->M = M;
+}
+
 void orc_mg_set_cycle(orc_mg *mg, int64_t mu, int64_t steps) {
     mg->mu = mu;
     mg->steps = steps;
@@ -824,6 +832,14 @@ static void smoother_in_place(const orc_mg *mg, int64_t level, double *r) {
     case ORC_SM_CHOL:
         orc_chol_solve(n, s->L, r);
         break;
+    case ORC_SM_CSR: {
+        double *t = (double *)xmalloc((size_t)n * sizeof(double));
+        if (mg->parallel) orc_spmv_omp(s->M, r, t);
+        else orc_spmv(s->M, r, t);
+        memcpy(r, t, (size_t)n * sizeof(double));
+        free(t);
+        break;
+    }
     default:
         ORC_DIE("bad smoother kind");
     }
@@ -909,7 +925,9 @@ int64_t orc_stationary_solve(const orc_csr *A, orc_mg *mg, const double *b, doub
     double *z = (double *)xmalloc((size_t)n * sizeof(double));
     double b_norm = norm2(n, b);
     for (;;) {
-        orc_spmv(A, x, work);
+        /* the residual SpMV in the cycle's parallel mode (same per-row order) */
+        if (mg->parallel) orc_spmv_omp(A, x, work);
+        else orc_spmv(A, x, work);
         for (int64_t i = 0; i < n; i++) r[i] = b[i] - work[i];
         double rel = norm2(n, r) / b_norm;
         iter += 1;

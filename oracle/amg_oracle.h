@@ -72,7 +72,7 @@ int64_t orc_box_aggregates(int64_t nx, int64_t ny, int64_t nz, int64_t bx, int64
 
 /* ---- multigrid ---- */
 typedef struct orc_mg orc_mg;
-enum { ORC_SM_DIAG = 0, ORC_SM_SGS = 1, ORC_SM_CHOL = 2 };
+enum { ORC_SM_DIAG = 0, ORC_SM_SGS = 1, ORC_SM_CHOL = 2, ORC_SM_CSR = 3 };
 orc_mg *orc_mg_new(int64_t nlevels);
 void orc_mg_free(orc_mg *mg);
 void orc_mg_set_op(orc_mg *mg, int64_t level, const orc_csr *A);
@@ -80,6 +80,9 @@ void orc_mg_set_transfer(orc_mg *mg, int64_t level, const orc_csr *R, const orc_
 void orc_mg_set_diag(orc_mg *mg, int64_t level, const double *d);
 void orc_mg_set_sgs(orc_mg *mg, int64_t level, const int64_t *color, int64_t ncolors);
 int orc_mg_set_chol(orc_mg *mg, int64_t level);
+/* Smoother given as an explicit sparse matrix M (apply_in_place: r <- M r), e.g.
+ * BlockSmoother::into_sparse_mat (block_smoothers.rs:122-146).  M is borrowed. */
+void orc_mg_set_csr_smoother(orc_mg *mg, int64_t level, const orc_csr *M);
 void orc_mg_set_cycle(orc_mg *mg, int64_t mu, int64_t steps);
 void orc_mg_set_parallel(orc_mg *mg, int64_t enable, int64_t nthreads);
 void orc_mg_apply(orc_mg *mg, const double *rhs, double *out);

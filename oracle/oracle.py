@@ -75,6 +75,7 @@ def lib():
             "orc_mg_set_diag": (None, [vp, i64, P_DBL]),
             "orc_mg_set_sgs": (None, [vp, i64, P_I64, i64]),
             "orc_mg_set_chol": (C.c_int, [vp, i64]),
+            "orc_mg_set_csr_smoother": (None, [vp, i64, vp]),
             "orc_mg_set_cycle": (None, [vp, i64, i64]),
             "orc_mg_set_parallel": (None, [vp, i64, i64]),
             "orc_mg_apply": (None, [vp, P_DBL, P_DBL]),
@@ -259,7 +260,8 @@ class Multigrid:
     """Restatement of reference Multigrid (src/preconditioners/multigrid.rs:171-424).
 
     levels: list of dicts with keys A (Csr), smoother ('jacobi', 'l1', 'sgs',
-    'chol', or ('diag', array)), omega, and for every non-coarsest level R, P.
+    'chol', ('diag', array) or ('csr', Csr) -- an explicit smoother matrix such as
+    BlockSmoother::into_sparse_mat), omega, and for every non-coarsest level R, P.
     """
 
     def __init__(self, levels, mu=1, steps=1, omega=0.66):
@@ -283,6 +285,8 @@ class Multigrid:
             elif sm == "sgs":
                 color, nc = lev.get("coloring") or greedy_coloring(A)
                 L.orc_mg_set_sgs(self.h, l, np.ascontiguousarray(color, np.int64), nc)
+            elif isinstance(sm, tuple) and sm[0] == "csr":
+                L.orc_mg_set_csr_smoother(self.h, l, sm[1].h)  # sm[1]: Csr kept alive by self.levels
             elif sm == "chol":
                 if L.orc_mg_set_chol(self.h, l) != 0:
                     raise ValueError("coarse matrix is not SPD")

@@ -814,3 +814,47 @@ def test_dia_codes(ctx, gen):
     it, hist = fa().stationary_solve(A, fa().new_jacobi(A, 0.66), bd, torch.zeros_like(bd), max_iter=3,
                                      rel_tol=1e-300)
     assert it == 3 and hist[2] < hist[0]
+
+
+@pytest.mark.timeout(400)
+def test_vcycle_256_storage_mix(ctx):
+    """The benchmark configuration itself (C2: 7-pt 256^3, SA 2^3 boxes, Jacobi,
+    6 levels) against the oracle on the same hierarchy, so the exact storage mix
+    the bench times is what is checked: DIA codes on A_0, 4-bit value-code SELL
+    with u16 column deltas on P_0/R_0, 8-bit codes on A_1, 16-bit codes on
+    A_2/R_1/P_1, the wave-per-row kernel on the dense coarse levels.  One
+    V-cycle to 1e-11 and 10 stationary cycles (rho_k) to 1e-8 (+ noise floor).
+    The oracle runs its ParSpmmOp restatement on 16 threads (same per-row order
+    as the sequential CSR)."""
+    import torch
+    dims = (256, 256, 256)
+    A = fa().SparseMatOp.laplace3d_7pt(ctx, *dims)
+    mg = fa().sa_build_box(A, dims, (2, 2, 2), coarsest_dim=1000)
+    assert mg.levels() == 6
+    info = [(mg.level(l)[0].spmv_info(), mg.level(l)[2].spmv_info() if l < 5 else None,
+             mg.level(l)[3].spmv_info() if l < 5 else None) for l in range(6)]
+    a0, r0, p0 = info[0]
+    assert a0["kernel"] == "dia" and a0["value_bits"] == 4
+    for m in (r0, p0):
+        assert m["kernel"] == "sell" and m["value_bits"] == 4 and m["slices_u16"] > 0
+    assert info[1][0]["kernel"] == "sell" and info[1][0]["value_bits"] == 8
+    assert info[2][0]["kernel"] == "sell" and info[2][0]["value_bits"] == 16
+    assert info[1][1]["value_bits"] == 16 and info[1][2]["value_bits"] == 16
+    assert info[3][0]["kernel"] == "vector" and info[4][0]["kernel"] == "vector"
+    levels = oracle_levels_from_gpu(mg, "jacobi")
+    import sys
+    sys.path.insert(0, GOLD)
+    from make_golden import splitmix_uniform
+    b = splitmix_uniform(A.nrows, 42)
+    omg = O.Multigrid(levels)
+    omg.set_parallel(16)
+    zref = omg.apply(b)
+    z = apply_dev(ctx, mg, b, A.nrows)
+    assert np.linalg.norm(z - zref) <= 1e-11 * np.linalg.norm(zref)
+    x = torch.zeros(A.nrows, dtype=torch.float64, device="cuda:0")
+    it, hist = fa().stationary_solve(A, mg, T(b), x, max_iter=11, rel_tol=1e-300)
+    OA = levels[0]["A"]
+    _, it_o, hist_o = O.stationary_solve(OA, omg, b, max_iter=11, rel_tol=1e-300)
+    assert it == it_o == 11
+    floor = EPS * 12.0 * np.max(np.abs(H(x))) / np.max(np.abs(b))  # ||A||_inf = 12
+    assert np.all(np.abs(hist - hist_o) <= 1e-8 * hist_o + floor), (hist, hist_o)
