@@ -276,7 +276,9 @@ def test_dist_build_leaves_global_operators_untouched():
     z3 = torch.empty_like(bd)
     dm.apply(z3, bd)
     ctx.synchronize()
-    assert torch.allclose(z3, z1, rtol=1e-13, atol=0)
+    # the distributed levels use SELL/DIA storage, the CSR-only global copy the
+    # CSR-stream kernel (long rows split over lanes): rounding-level differences
+    assert float(torch.linalg.norm(z3 - z1)) <= 1e-13 * float(torch.linalg.norm(z1))
 
 
 def test_dist_eight_ranks_c4_shaped():
