@@ -207,7 +207,7 @@ def cpu_side(mg, A, b_host, z_gpu, args):
 
     res = {"value": round(1.0 / float(np.median(ts16)), 4), "unit": "V-cycles/s", "cores": t16,
            "kind": "port",
-           "sample": f"median of {len(ts16)} V-cycles of the same {args.edge}^3 hierarchy "
+           "sample": f"median of {len(ts16)} V-cycles of the same hierarchy as the GPU run "
                      f"(oracle restatement of the rayon path: ParSpmmOp 8192x8192 CSC tiles, "
                      f"usize indices, per-call temporaries; OpenMP {t16} threads = Par::Rayon(16))",
            "fine_spmv_ms": round(spmv_t * 1e3, 3),
@@ -226,13 +226,40 @@ def cpu_side(mg, A, b_host, z_gpu, args):
     return res, parity
 
 
-def build_problem(fa, ctx, args, dims):
+def make_operator(fa, ctx, args, dims):
+    """The fine operator of the workload (device-resident)."""
     if args.problem == "7pt":
-        A = fa.SparseMatOp.laplace3d_7pt(ctx, *dims)
-    else:
-        A = fa.SparseMatOp.aniso27(ctx, *dims, 1.0, 1.0, 0.01)
-    mg = fa.sa_build_box(A, dims, (args.box,) * 3, coarsest_dim=1000, smoother=args.smoother)
+        return fa.SparseMatOp.laplace3d_7pt(ctx, *dims)
+    if args.problem == "27pt":
+        return fa.SparseMatOp.aniso27(ctx, *dims, 1.0, 1.0, 0.01)
+    if args.problem == "elast":  # in-tree C5 stand-in (Flan_1565 cannot be fetched)
+        e = args.elements
+        return fa.elasticity_q1((e, e, e), contrast=1.0, nu=0.3, seed=42, permute=True).upload(ctx)
+    if args.problem == "mtx":  # a Matrix Market file placed on the box (e.g. Flan_1565.mtx)
+        return fa.read_mtx(args.mtx).upload(ctx)
+    raise ValueError(args.problem)
+
+
+def build_problem(fa, ctx, args, dims):
+    A = make_operator(fa, ctx, args, dims)
+    if args.problem in ("7pt", "27pt"):
+        mg = fa.sa_build_box(A, dims, (args.box,) * 3, coarsest_dim=1000, smoother=args.smoother)
+    else:  # general SA: block size b, b constant-per-component candidates (C5)
+        bs = args.block_size
+        nn = fa.constant_candidates(A.nrows, bs)
+        mg = fa.smoothed_aggregation(A, nn, block_size=bs, candidate_dimension=bs, coarsest_dim=1000,
+                                     smoother=args.smoother)
     return A, mg
+
+
+def workload_name(args, dims):
+    if args.problem in ("7pt", "27pt"):
+        return (f"SA V-cycle, 3D {args.problem} {dims[0]}x{dims[1]}x{dims[2]}, box {args.box}^3, "
+                f"{args.smoother} s=1 mu=1, Cholesky coarsest")
+    src = (f"Q1 elasticity {args.elements}^3 elements (C5 stand-in: permuted nodes, random E)"
+           if args.problem == "elast" else f"Matrix Market {os.path.basename(args.mtx)}")
+    return (f"SA V-cycle, {src}, block size {args.block_size}, {args.block_size} constant candidates, "
+            f"MIS aggregates, block-Jacobi P smoothing, {args.smoother} s=1 mu=1, Cholesky coarsest")
 
 
 def vcycle_bytes(mg, csr=False, fold=True):
@@ -318,8 +345,7 @@ def run_single(args):
     # the same operator with fp64 values (value codes off): the uncompressed
     # SELL kernel, reported beside the one the V-cycle uses
     fa.set_value_codes(False)
-    A64 = (fa.SparseMatOp.laplace3d_7pt(ctx, *dims) if args.problem == "7pt"
-           else fa.SparseMatOp.aniso27(ctx, *dims, 1.0, 1.0, 0.01))
+    A64 = make_operator(fa, ctx, args, dims)
     fa.set_value_codes(True)
     for _ in range(3):
         A64.apply(y, x)
@@ -336,8 +362,7 @@ def run_single(args):
         ops = {}
         for fmt in ("csr", "sell"):
             fa.set_spmv_format(fmt)
-            ops[fmt] = (fa.SparseMatOp.laplace3d_7pt(ctx, *dims) if args.problem == "7pt"
-                        else fa.SparseMatOp.aniso27(ctx, *dims, 1.0, 1.0, 0.01))
+            ops[fmt] = make_operator(fa, ctx, args, dims)
         fa.set_spmv_format("auto")
         res = {k: [] for k in ops}
         for _ in range(5):
@@ -379,8 +404,7 @@ def run_single(args):
         "vs_baseline": None,
         "dtype": "f64",
         "data": "synthetic (device-generated operator, splitmix64 rhs seed 42)",
-        "config": {"workload": f"SA V-cycle, 3D {args.problem} {args.edge}^3, box {args.box}^3, "
-                               f"{args.smoother} s=1 mu=1, Cholesky coarsest",
+        "config": {"workload": workload_name(args, dims),
                    "levels": len(levels), "fine_rows": n, "fine_nnz": nnz,
                    "hierarchy": levels, "setup_s": round(setup_s, 2),
                    "wall_ms_per_step": round(1000 * t_wall / args.steps, 4),
@@ -515,8 +539,13 @@ def main():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--edge", type=int, default=256, help="grid edge per GPU")
     ap.add_argument("--box", type=int, default=2)
-    ap.add_argument("--smoother", default="jacobi", choices=["jacobi", "l1", "sgs", "block"])
-    ap.add_argument("--problem", default="7pt", choices=["7pt", "27pt"])
+    ap.add_argument("--smoother", default=None, choices=["jacobi", "l1", "sgs", "block"],
+                    help="default: jacobi (7pt), sgs (27pt), l1 (elast/mtx)")
+    ap.add_argument("--problem", default="7pt", choices=["7pt", "27pt", "elast", "mtx"],
+                    help="7pt (C2), 27pt (C3), elast (C5 stand-in), mtx (C5 with --mtx Flan_1565.mtx)")
+    ap.add_argument("--elements", type=int, default=80, help="elast: elements per edge (80: 1.57M rows)")
+    ap.add_argument("--mtx", default=None, help="mtx: path of a Matrix Market file")
+    ap.add_argument("--block-size", type=int, default=3, help="elast/mtx: dofs per node")
     ap.add_argument("--agglomerate", type=int, default=8192,
                     help="levels with fewer global rows run redundantly on every rank")
     ap.add_argument("--cpu-threads", type=int, default=int(os.environ.get("OMP_NUM_THREADS", "16")))
@@ -532,6 +561,10 @@ def main():
     ap.add_argument("--dist", action="store_true",
                     help="distributed path even at world size 1 (1-rank RCCL; a check of run_dist)")
     args = ap.parse_args()
+    if args.smoother is None:
+        args.smoother = {"7pt": "jacobi", "27pt": "sgs"}.get(args.problem, "l1")
+    if args.problem == "mtx" and not args.mtx:
+        ap.error("--problem mtx needs --mtx PATH")
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))

@@ -167,7 +167,10 @@ void dense_gemv(const double *M, const double *x, double *out, int64_t n, hipStr
 int64_t scan_counts(const int64_t *counts, int64_t *out, int64_t n, Ctx &ctx);
 
 // sparse products / setup
-void spgemm(const GpuCsr &A, const GpuCsr &B, GpuCsr &C);
+// C = A B; finalize = false leaves C without SpMV storage (setup intermediates)
+void spgemm(const GpuCsr &A, const GpuCsr &B, GpuCsr &C, bool finalize = true);
+// S += P where P's pattern lies within S's (values only; S is not re-finalized)
+void csr_add_into(GpuCsr &S, const GpuCsr &P);
 void transpose(const GpuCsr &A, GpuCsr &T);
 void smooth_interp_fixup(GpuCsr &S, const GpuCsr &P, const double *diag, double omega);
 void gen_stencil(GpuCsr &m, Ctx *ctx, int64_t nx, int64_t ny, int64_t nz, const int *offs,
@@ -338,5 +341,38 @@ std::shared_ptr<MultigridOp> sa_build_box(const CsrPtr &A, int64_t nx, int64_t n
                                           int64_t bx, int64_t by, int64_t bz,
                                           int64_t coarsest_dim, int64_t max_levels,
                                           double omega, int smoother);
+
+// ------------------------------------------------ general SA setup (sa.hip)
+
+// Node-level strength graph (partitioners/mod.rs:337-393, block-reduced
+// :294-301): CSR with strengths in (0, 1].
+struct StrengthGraph {
+    int64_t n = 0;
+    std::vector<int64_t> rp;
+    std::vector<int32_t> col;
+    std::vector<double> w;
+};
+StrengthGraph strength_graph(const CsrOp &A, const double *nn, int64_t ld, int64_t k, const double *w,
+                             int64_t depth, int64_t bs);
+// MIS-seeded aggregates of a strength graph; returns the aggregate count
+int64_t aggregate_mis(const StrengthGraph &G, std::vector<int64_t> &agg_of);
+// tentative P for k candidates on nodes of bs dofs (interpolation/mod.rs:754-805)
+CsrPtr sa_tentative_block(Ctx *ctx, int64_t nnodes, int64_t bs, const int64_t *agg_of, int64_t naggs,
+                          const double *nn, int64_t ld, int64_t k, int64_t cd, double *coarse_nn);
+// block_jacobi P smoothing (interpolation/mod.rs:963-1028)
+CsrPtr block_jacobi_smooth(CsrOp &A, const CsrOp &P, int64_t bs, double omega);
+// coarse near-null post-processing for k columns (hierarchy.rs:219-228)
+void nn_postprocess(CsrOp &A, int64_t iters, double *x, int64_t ld, int64_t k);
+struct SaConfig {
+    int64_t block_size = 1, candidate_dimension = 1, strength_depth = 1, smoothing_steps = 1;
+    int64_t coarsest_dim = 1000, max_levels = 0;
+    double omega = 0.66;
+    int smoother = 1;
+};
+struct SaLevelInfo {
+    int64_t n, block_size, nodes, aggregates, strength_edges;
+};
+std::shared_ptr<MultigridOp> sa_build(const CsrPtr &A, const double *nn, int64_t ld, int64_t k,
+                                      const double *weights, const SaConfig &cfg, std::vector<SaLevelInfo> *info);
 
 }  // namespace famg

@@ -17,6 +17,13 @@ struct amg_linop {
     famg::LinOpPtr op;
 };
 
+// host CSR (loaders, generators, strength graphs): int64 indices, fp64 values
+struct amg_host_csr {
+    int64_t nrows = 0, ncols = 0;
+    std::vector<int64_t> rp, ci;
+    std::vector<double> va;
+};
+
 namespace famg {
 // record the thread-local message returned by amg_last_error(); returns s
 amg_status set_last_error(amg_status s, const char *msg);

@@ -32,12 +32,6 @@
 
 using namespace famg;
 
-struct amg_host_csr {
-    int64_t nrows = 0, ncols = 0;
-    std::vector<int64_t> rp, ci;
-    std::vector<double> va;
-};
-
 struct amg_mfem_system {
     amg_host_csr A;
     int64_t rhs_cols = 0, coord_dim = 0, original_dim = 0;
@@ -285,6 +279,27 @@ amg_status amg_mtx_read(const char *path, amg_host_csr **out) {
         std::vector<Triplet> t;
         read_mtx_triplets(path, m, n, t);
         to_csr(m, n, t, *h);
+        *out = h.release();
+    });
+}
+
+amg_status amg_host_csr_create(int64_t nrows, int64_t ncols, const int64_t *rowptr, const int64_t *colidx,
+                               const double *vals, amg_host_csr **out) {
+    return guard([&] {
+        FAMG_REQUIRE(out && rowptr && nrows >= 0 && ncols >= 0 && rowptr[0] == 0, AMG_ERR_INVALID, "bad argument");
+        const int64_t nnz = rowptr[nrows];
+        FAMG_REQUIRE(nnz == 0 || (colidx && vals), AMG_ERR_INVALID, "null column/value array");
+        auto h = std::make_unique<amg_host_csr>();
+        h->nrows = nrows;
+        h->ncols = ncols;
+        h->rp.assign(rowptr, rowptr + nrows + 1);
+        h->ci.assign(colidx, colidx + nnz);
+        h->va.assign(vals, vals + nnz);
+        for (int64_t i = 0; i < nrows; i++) {
+            FAMG_REQUIRE(h->rp[i + 1] >= h->rp[i], AMG_ERR_INVALID, "rowptr not monotone");
+            for (int64_t e = h->rp[i]; e < h->rp[i + 1]; e++)
+                FAMG_REQUIRE(h->ci[e] >= 0 && h->ci[e] < ncols, AMG_ERR_INVALID, "column index out of range");
+        }
         *out = h.release();
     });
 }

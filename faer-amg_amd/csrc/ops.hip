@@ -615,7 +615,7 @@ CsrPtr transpose_op(const CsrOp &P) {
 CsrPtr smooth_interpolation(CsrOp &A, const CsrOp &P, double omega) {
     FAMG_REQUIRE(A.nrows == A.ncols && A.ncols == P.nrows, AMG_ERR_DIM, "smooth_interpolation dims");
     GpuCsr S;
-    spgemm(A.m, P.m, S);
+    spgemm(A.m, P.m, S, false);  // finalized by the fixup
     smooth_interp_fixup(S, P.m, A.diagonal(), omega);
     return wrap(A.ctx, std::move(S));
 }
@@ -625,7 +625,7 @@ CsrPtr galerkin_rap(const CsrOp &R, const CsrOp &A, const CsrOp &P) {
     FAMG_REQUIRE(R.ncols == A.nrows && A.ncols == P.nrows && R.nrows == P.ncols, AMG_ERR_DIM,
                  "galerkin_rap dims");
     GpuCsr AP, C;
-    spgemm(A.m, P.m, AP);
+    spgemm(A.m, P.m, AP, false);
     spgemm(R.m, AP, C);
     return wrap(A.ctx, std::move(C));
 }

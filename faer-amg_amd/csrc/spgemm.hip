@@ -176,7 +176,7 @@ static void spgemm_numeric(const GpuCsr &A, const GpuCsr &B, GpuCsr &C, Ctx &ctx
     FAMG_CHECK_HIP(hipGetLastError());
 }
 
-void spgemm(const GpuCsr &A, const GpuCsr &B, GpuCsr &C) {
+void spgemm(const GpuCsr &A, const GpuCsr &B, GpuCsr &C, bool finalize) {
     FAMG_REQUIRE(A.ncols == B.nrows, AMG_ERR_DIM, "spgemm: A.ncols != B.nrows");
     Ctx &ctx = *A.ctx;
     hipStream_t s = ctx.stream;
@@ -209,7 +209,7 @@ void spgemm(const GpuCsr &A, const GpuCsr &B, GpuCsr &C) {
     else if (maxc <= 512) spgemm_numeric<1024>(A, B, C, ctx);
     else if (maxc <= 2048) spgemm_numeric<4096>(A, B, C, ctx);
     else spgemm_numeric<8192>(A, B, C, ctx);
-    csr_finalize(C);
+    if (finalize) csr_finalize(C);
 }
 
 // ------------------------------------------------------------- transpose

@@ -116,6 +116,7 @@ SIGNATURES = {
     "amg_dist_set_option": (i32, [vp, i32, i64]),
     "amg_mtx_read": (i32, [C.c_char_p, P(vp)]),
     "amg_host_csr_dims": (i32, [vp, P(i64), P(i64), P(i64)]),
+    "amg_host_csr_create": (i32, [i64, i64, vp, vp, vp, P(vp)]),
     "amg_host_csr_arrays": (i32, [vp, vp, vp, vp]),
     "amg_host_csr_upload": (i32, [vp, vp, P(vp)]),
     "amg_host_csr_destroy": (i32, [vp]),
@@ -128,6 +129,14 @@ SIGNATURES = {
     "amg_mfem_index_maps": (i32, [vp, vp, vp]),
     "amg_mfem_destroy": (i32, [vp]),
     "amg_dist_stationary_solve": (i32, [vp, vp, vp, i64, dbl, vp, P(i64)]),
+    "amg_sa_config_default": (i32, [vp]),
+    "amg_sa_build": (i32, [vp, vp, i64, i64, vp, vp, P(vp)]),
+    "amg_strength_graph": (i32, [vp, vp, i64, i64, vp, i64, i64, P(vp)]),
+    "amg_aggregate_mis": (i32, [vp, vp, P(i64)]),
+    "amg_sa_tentative_block": (i32, [vp, i64, i64, vp, i64, vp, i64, i64, i64, P(vp), vp]),
+    "amg_block_jacobi_smooth": (i32, [vp, vp, i64, dbl, P(vp)]),
+    "amg_nn_postprocess": (i32, [vp, i64, vp, i64, i64]),
+    "amg_gen_elasticity_q1": (i32, [i64, i64, i64, dbl, dbl, C.c_uint64, i32, P(vp)]),
     "amg_dist_pcg_solve": (i32, [vp, i32, vp, vp, i64, dbl, dbl, vp, P(i64)]),
 }
 
@@ -558,6 +567,124 @@ def sa_build_box(A, dims, box=(2, 2, 2), coarsest_dim=1000, max_levels=0, omega=
     _ck(_lib.amg_sa_build_box(A.h, dims[0], dims[1], dims[2], box[0], box[1], box[2],
                               coarsest_dim, max_levels, omega, SMOOTHERS[smoother], C.byref(h)))
     return Multigrid._from_handle(h, A.ctx)
+
+
+class SaConfig(C.Structure):
+    """amg_sa_config: AggregationConfig + HierarchyConfig + the smoother choice
+    (interpolation/mod.rs:62-79, hierarchy.rs:21-36)."""
+    _fields_ = [("block_size", i64), ("candidate_dimension", i64), ("strength_depth", i64),
+                ("smoothing_steps", i64), ("coarsest_dim", i64), ("max_levels", i64),
+                ("omega", dbl), ("smoother", i32), ("reserved", i32)]
+
+    def __init__(self, **kw):
+        super().__init__()
+        _ck(_lib.amg_sa_config_default(C.byref(self)))
+        for k, v in kw.items():
+            if k == "smoother" and isinstance(v, str):
+                v = SMOOTHERS[v]
+            setattr(self, k, v)
+
+
+def _colmajor_host(x, nrows):
+    x = np.asarray(x, np.float64)
+    if x.ndim == 1:
+        x = x[:, None]
+    x = np.asfortranarray(x)
+    if x.shape[0] != nrows:
+        raise ValueError("near-null space must have one row per matrix row")
+    return x
+
+
+def smoothed_aggregation(A, near_null, weights=None, **config):
+    """SA hierarchy + multigrid for a general SPD matrix (Hierarchy::coarsen with
+    AggregationConfig, hierarchy.rs:190-248; interpolation/mod.rs:730-836).
+    near_null: n x k candidates; weights: k strength weights (None: 1/v^T A v);
+    config: SaConfig fields (block_size, candidate_dimension, strength_depth,
+    smoothing_steps, coarsest_dim, max_levels, omega, smoother)."""
+    cfg = SaConfig(**config)
+    nn = _colmajor_host(near_null, A.nrows)
+    w = None if weights is None else np.ascontiguousarray(weights, np.float64)
+    h = vp()
+    _ck(_lib.amg_sa_build(A.h, nn.ctypes.data_as(vp), nn.shape[0], nn.shape[1],
+                          None if w is None else w.ctypes.data_as(vp), C.byref(cfg), C.byref(h)))
+    return Multigrid._from_handle(h, A.ctx)
+
+
+def strength_graph(A, near_null, weights, depth=1, block_size=1):
+    """Node-level strength graph (partitioners/mod.rs:337-393) as scipy CSR."""
+    nn = _colmajor_host(near_null, A.nrows)
+    w = np.ascontiguousarray(weights, np.float64)
+    h = vp()
+    _ck(_lib.amg_strength_graph(A.h, nn.ctypes.data_as(vp), nn.shape[0], nn.shape[1],
+                                w.ctypes.data_as(vp), depth, block_size, C.byref(h)))
+    return HostCsr(h).to_scipy()
+
+
+def aggregate_mis(G):
+    """MIS-seeded aggregates of a strength graph (scipy CSR): (agg_of, naggs)."""
+    G = G.tocsr()
+    n = G.shape[0]
+    tmp = HostCsr(_host_csr_from_scipy(G))
+    agg = np.zeros(n, np.int64)
+    na = i64()
+    _ck(_lib.amg_aggregate_mis(tmp.h, agg.ctypes.data_as(vp), C.byref(na)))
+    return agg, na.value
+
+
+def _host_csr_from_scipy(G):
+    G = G.tocsr()
+    rp = np.ascontiguousarray(G.indptr, np.int64)
+    ci = np.ascontiguousarray(G.indices, np.int64)
+    va = np.ascontiguousarray(G.data, np.float64)
+    h = vp()
+    _ck(_lib.amg_host_csr_create(G.shape[0], G.shape[1], rp.ctypes.data_as(vp), ci.ctypes.data_as(vp),
+                                 va.ctypes.data_as(vp), C.byref(h)))
+    return h
+
+
+def sa_tentative_block(ctx, agg_of, naggs, near_null, block_size=1, candidate_dimension=None):
+    """Tentative SA interpolation for k candidates (interpolation/mod.rs:754-805):
+    returns (P, coarse near-null (naggs*cd) x k)."""
+    agg = np.ascontiguousarray(agg_of, np.int64)
+    nn = _colmajor_host(near_null, len(agg) * block_size)
+    k = nn.shape[1]
+    cd = k if candidate_dimension is None else candidate_dimension
+    cnn = np.zeros((naggs * cd, k), order="F")
+    h = vp()
+    _ck(_lib.amg_sa_tentative_block(ctx.h, len(agg), block_size, agg.ctypes.data_as(vp), naggs,
+                                    nn.ctypes.data_as(vp), nn.shape[0], k, cd, C.byref(h),
+                                    cnn.ctypes.data_as(vp)))
+    return SparseMatOp(h, ctx), cnn
+
+
+def block_jacobi(A, P_, block_size, omega=0.66):
+    """block_jacobi P smoothing (interpolation/mod.rs:963-1028)."""
+    h = vp()
+    _ck(_lib.amg_block_jacobi_smooth(A.h, P_.h, block_size, omega, C.byref(h)))
+    return SparseMatOp(h, A.ctx)
+
+
+def nn_postprocess(A, x, iters=3):
+    """Coarse near-null post-processing for k columns (hierarchy.rs:219-228)."""
+    x = np.array(_colmajor_host(x, A.nrows), copy=True, order="F")
+    _ck(_lib.amg_nn_postprocess(A.h, iters, x.ctypes.data_as(vp), x.shape[0], x.shape[1]))
+    return x
+
+
+def elasticity_q1(elements, contrast=1.0, nu=0.3, seed=42, permute=True):
+    """Host CSR of the C5 stand-in: Q1 hex elasticity, block size 3 (gen.cpp)."""
+    ex, ey, ez = elements
+    h = vp()
+    _ck(_lib.amg_gen_elasticity_q1(ex, ey, ez, contrast, nu, seed, 1 if permute else 0, C.byref(h)))
+    return HostCsr(h)
+
+
+def constant_candidates(n, block_size):
+    """block_size constant-per-component near-null vectors, orthonormal (n x bs)."""
+    nn = np.zeros((n, block_size), order="F")
+    for c in range(block_size):
+        nn[c::block_size, c] = 1.0
+    return nn / np.sqrt(n // block_size)
 
 
 def stationary_solve(A, M, b, x, max_iter=100, rel_tol=1e-8):

@@ -58,6 +58,7 @@ typedef enum amg_linop_kind {
 
 typedef struct amg_ctx amg_ctx;
 typedef struct amg_linop amg_linop;
+typedef struct amg_host_csr amg_host_csr; /* host CSR (loaders, generators, strength graphs) */
 
 /* ---- errors, context ------------------------------------------------------ */
 
@@ -133,6 +134,15 @@ amg_status amg_gen_laplace3d_7pt(amg_ctx *ctx, int64_t nx, int64_t ny, int64_t n
                                  amg_linop **out);
 amg_status amg_gen_aniso27(amg_ctx *ctx, int64_t nx, int64_t ny, int64_t nz, double ex,
                            double ey, double ez, amg_linop **out);
+
+/* In-tree stand-in for config C5 (Flan_1565, which cannot be fetched): Q1
+ * hexahedral linear elasticity on an ex x ey x ez element box, per-element
+ * Young's modulus 10^(contrast (2u - 1)) (u ~ U[0,1) from splitmix64(seed)),
+ * Poisson ratio nu, the x = 0 face clamped, free nodes renumbered by a seeded
+ * random permutation when permute != 0; 3 dofs per node interleaved
+ * (block_size 3).  Host CSR (upload with amg_host_csr_upload). */
+amg_status amg_gen_elasticity_q1(int64_t ex, int64_t ey, int64_t ez, double contrast, double nu,
+                                 uint64_t seed, int32_t permute, amg_host_csr **out);
 
 /* ---- generic LinOp / Precond / BiPrecond (faer matrix_free traits) -------- */
 
@@ -234,6 +244,48 @@ amg_status amg_nn_stationary_l1(const amg_linop *A, int64_t iters, double *x);
 amg_status amg_sa_build_box(amg_linop *A, int64_t nx, int64_t ny, int64_t nz, int64_t bx,
                             int64_t by, int64_t bz, int64_t coarsest_dim, int64_t max_levels,
                             double omega, int32_t smoother, amg_linop **mg_out);
+/* ---- smoothed aggregation on general (unstructured, block) matrices -----------
+ * Hierarchy::coarsen (hierarchy.rs:190-248) with AggregationConfig /
+ * smoothed_aggregation (interpolation/mod.rs:62-156, 730-836): strength graph
+ * (partitioners/mod.rs:337-393, block-reduced :294-301), aggregates seeded by
+ * maximal_independent_set (:395-423; stands in for the modularity partitioner,
+ * DESIGN.md), tentative P from a per-aggregate thin SVD of the near-null block,
+ * P smoothing by Jacobi (block size 1) or block_jacobi (:963-1028), R = P^T,
+ * A_c = R A P, coarse near-null by 3 L1 stationary steps + thin QR; the coarse
+ * block size is candidate_dimension. */
+typedef struct amg_sa_config {
+    int64_t block_size;          /* dofs per node of A (SparseMatOp block_size, core.rs:56) */
+    int64_t candidate_dimension; /* candidates kept per aggregate (<= near-null columns) */
+    int64_t strength_depth;      /* BFS depth of the strength graph (reference: 3) */
+    int64_t smoothing_steps;     /* P smoothing steps (AggregationConfig default 1) */
+    int64_t coarsest_dim;        /* stop when the coarse size <= this (default 1000) */
+    int64_t max_levels;          /* 0 = unlimited */
+    double omega;                /* Jacobi smoother weight (smoother 0) */
+    int32_t smoother;            /* 0 Jacobi, 1 L1 (default), 2 SGS, 3 BlockSmoother(aggregates) */
+    int32_t reserved;
+} amg_sa_config;
+amg_status amg_sa_config_default(amg_sa_config *cfg);
+/* near_null: n x k column-major (leading dimension ld), host; weights: k host
+ * values of the strength inner product or NULL for create_weights
+ * (examples/amg/main.rs:571-580: 1 / v^T A v).  Returns the multigrid (smoother
+ * per cfg on every level but the coarsest, which gets the Cholesky solve). */
+amg_status amg_sa_build(amg_linop *A, const double *near_null, int64_t ld, int64_t k, const double *weights,
+                        const amg_sa_config *cfg, amg_linop **mg_out);
+/* The pieces (for tests and custom hierarchies): node-level strength graph as a
+ * host CSR (values = strengths); MIS-seeded aggregates of such a graph;
+ * tentative P for k candidates on nnodes nodes of block_size dofs (coarse_nn:
+ * (naggs*cd) x k column-major, leading dimension naggs*cd); block_jacobi P
+ * smoothing; coarse near-null post-processing of x (n x k, ld) in place. */
+amg_status amg_strength_graph(const amg_linop *A, const double *near_null, int64_t ld, int64_t k,
+                              const double *weights, int64_t depth, int64_t block_size, amg_host_csr **out);
+amg_status amg_aggregate_mis(const amg_host_csr *graph, int64_t *agg_of, int64_t *naggs);
+amg_status amg_sa_tentative_block(amg_ctx *ctx, int64_t nnodes, int64_t block_size, const int64_t *agg_of,
+                                  int64_t naggs, const double *near_null, int64_t ld, int64_t k, int64_t cd,
+                                  amg_linop **P, double *coarse_nn);
+amg_status amg_block_jacobi_smooth(const amg_linop *A, const amg_linop *P, int64_t block_size, double omega,
+                                   amg_linop **out);
+amg_status amg_nn_postprocess(const amg_linop *A, int64_t iters, double *x, int64_t ld, int64_t k);
+
 /* Level accessors of a multigrid: A_l, R_l, P_l (l < levels-1), smoother S_l.
  * Returned handles are new references. */
 amg_status amg_multigrid_get_level(const amg_linop *mg, int64_t level, amg_linop **A,
@@ -346,8 +398,10 @@ amg_status amg_dist_pcg_solve(amg_linop *dist_mg, int32_t precondition, const do
  * (real/integer/pattern, general/symmetric), 1-based indices, explicit 0.0
  * entries dropped, symmetric entries mirrored, duplicates summed, columns
  * sorted (load_matrix_triplets, utils.rs:508-534, + faer try_new_from_triplets). */
-typedef struct amg_host_csr amg_host_csr;
 amg_status amg_mtx_read(const char *path, amg_host_csr **out);
+/* Host CSR from arrays (copied; values kept as given, zeros included). */
+amg_status amg_host_csr_create(int64_t nrows, int64_t ncols, const int64_t *rowptr, const int64_t *colidx,
+                               const double *vals, amg_host_csr **out);
 amg_status amg_host_csr_dims(const amg_host_csr *h, int64_t *nrows, int64_t *ncols, int64_t *nnz);
 amg_status amg_host_csr_arrays(const amg_host_csr *h, int64_t *rowptr, int64_t *colidx, double *vals);
 /* Upload to the device (amg_csr_create). */

@@ -16,6 +16,9 @@ step() {  # step NAME SECONDS CMD...
 for s in "$@"; do
     case $s in
         tests) step pytest_gpu 900 python -u -m pytest tests -m gpu -v --timeout 120 --timeout-method thread ;;
+        satests) step pytest_sa 600 python -u -m pytest tests/test_gpu_sa.py tests/test_gpu_dist.py -m gpu -v --timeout 120 --timeout-method thread ;;
+        elast30) step bench_elast30 400 python bench.py --problem elast --elements 30 --steps 20 --warmup 3 ;;
+        elast) step bench_elast 900 python bench.py --problem elast --steps 20 --warmup 3 ;;
         smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
         bench) step bench 600 python bench.py --steps 20 --warmup 3 ;;
         benchq) step bench 400 python bench.py --steps 20 --warmup 3 --no-cpu-baseline --ab ;;

@@ -1,0 +1,205 @@
+"""General smoothed aggregation (config C5 path: unstructured SPD, block size 3,
+three candidates) on the GPU against the restatements: oracle/sa_oracle.py for
+the setup pieces, oracle/amg_oracle.c for the V-cycle on the same hierarchy.
+
+Tolerances: strength graph and aggregates bitwise (same operation order);
+tentative P through basis-independent checks (per-aggregate projector equal to
+LAPACK's to 1e-12, orthonormal columns, P * coarse_nn = near-null) because the
+SVD of a degenerate block has no unique basis; block_jacobi / RAP to 1e-12 of
+the row scale; V-cycle 1e-11; rho_k 1e-8 (+ noise floor).
+"""
+import numpy as np
+import pytest
+import scipy.sparse as sp
+
+import oracle as O
+import sa_oracle as SO
+
+pytestmark = pytest.mark.gpu
+EPS = np.finfo(float).eps
+
+
+def fa():
+    import faer_amg_amd
+    return faer_amg_amd
+
+
+def elasticity(ctx, elements, seed=11):
+    H = fa().elasticity_q1(elements, seed=seed)
+    return H.upload(ctx), H.to_scipy()
+
+
+def weights(S, nn):
+    return [1.0 / float(nn[:, c] @ (S @ nn[:, c])) for c in range(nn.shape[1])]
+
+
+def csr_close(G, R, rtol):
+    """Same matrix up to rtol of the largest entry (pattern may carry explicit zeros)."""
+    D = (G - R).tocsr()
+    return abs(D).max() <= rtol * abs(R).max() if D.nnz else True
+
+
+def test_strength_graph_bitwise(ctx):
+    A, S = elasticity(ctx, (4, 3, 3))
+    nn = fa().constant_candidates(S.shape[0], 3)
+    w = weights(S, nn)
+    G = fa().strength_graph(A, nn, w, depth=1, block_size=3)
+    R = SO.strength_graph(S, nn, w, depth=1, block_size=3)
+    assert np.array_equal(G.indptr, R.indptr) and np.array_equal(G.indices, R.indices)
+    assert np.array_equal(G.data, R.data)
+    # depth 2 on a scalar problem with two random candidates (extract_local_subgraph BFS)
+    L = fa().SparseMatOp.laplace3d_7pt(ctx, 5, 4, 3)
+    LS = L.to_scipy()
+    rnn = np.random.default_rng(3).standard_normal((LS.shape[0], 2))
+    G2 = fa().strength_graph(L, rnn, [1.0, 0.5], depth=2, block_size=1)
+    R2 = SO.strength_graph(LS, rnn, [1.0, 0.5], depth=2, block_size=1)
+    assert np.array_equal(G2.indptr, R2.indptr) and np.array_equal(G2.indices, R2.indices)
+    assert np.array_equal(G2.data, R2.data)
+
+
+@pytest.mark.parametrize("kind", ["constant", "random"])
+def test_tentative_block(ctx, kind):
+    A, S = elasticity(ctx, (4, 4, 3))
+    n = S.shape[0]
+    if kind == "constant":
+        nn, cd = fa().constant_candidates(n, 3), 3
+    else:
+        nn, cd = np.asfortranarray(np.random.default_rng(4).standard_normal((n, 4))), 2
+    G = SO.strength_graph(S, fa().constant_candidates(n, 3), [1.0] * 3, 1, 3)
+    agg, na = fa().aggregate_mis(G)
+    P, cnn = fa().sa_tentative_block(ctx, agg, na, nn, block_size=3, candidate_dimension=cd)
+    Ph = P.to_scipy()
+    assert Ph.shape == (n, na * cd) and np.all(np.diff(Ph.indptr) == cd)
+    node_agg = np.repeat(agg, 3)
+    for a, (rows, proj, s) in enumerate(SO.tentative_projectors(agg, na, nn, 3, cd)):
+        Pa = Ph[rows][:, a * cd:(a + 1) * cd].toarray()
+        assert np.allclose(Pa.T @ Pa, np.eye(cd), atol=1e-13)          # orthonormal columns
+        assert np.max(np.abs(Pa @ Pa.T - proj)) <= 1e-12               # same subspace as LAPACK
+        assert np.all(node_agg[rows] == a)
+        # coarse near-null = S V^T: its first cd rows carry the singular values
+        assert np.allclose(np.sort(np.linalg.svd(cnn[a * cd:(a + 1) * cd], compute_uv=False))[::-1],
+                           s[:cd], rtol=1e-12)
+    if cd == nn.shape[1]:
+        assert np.max(np.abs(Ph @ cnn - nn)) <= 1e-13 * np.max(np.abs(nn))  # exact reconstruction
+    if kind == "constant":  # orthogonal candidates: U = local / sqrt(|agg|), no rotation
+        sizes = np.bincount(agg)
+        for i in range(0, n, 37):
+            row = Ph[i].toarray().ravel()
+            a = agg[i // 3]
+            expect = np.zeros(na * 3)
+            expect[a * 3 + i % 3] = 1.0 / np.sqrt(sizes[a])
+            assert np.allclose(row, expect, rtol=1e-14, atol=0)
+
+
+def test_block_jacobi_and_rap(ctx):
+    A, S = elasticity(ctx, (4, 4, 3))
+    n = S.shape[0]
+    nn = fa().constant_candidates(n, 3)
+    G = SO.strength_graph(S, nn, weights(S, nn), 1, 3)
+    agg, na = fa().aggregate_mis(G)
+    P, cnn = fa().sa_tentative_block(ctx, agg, na, nn, block_size=3)
+    Ps = fa().block_jacobi(A, P, 3)
+    ref = SO.block_jacobi(S, P.to_scipy(), 3)
+    assert csr_close(Ps.to_scipy(), ref, 1e-12)
+    R = fa().transpose(Ps)
+    Ac = fa().galerkin_rap(R, A, Ps)
+    Psh = Ps.to_scipy()
+    assert csr_close(Ac.to_scipy(), (Psh.T @ S @ Psh).tocsr(), 1e-12)
+    # block size 1: the scalar Jacobi smoothing (smooth_interpolation)
+    P1 = fa().smooth_interpolation(A, P)
+    assert csr_close(P1.to_scipy(), SO.smooth_interpolation(S, P.to_scipy()), 1e-12)
+    # coarse near-null post-processing (3 L1 steps + thin QR) for 3 columns
+    x = fa().nn_postprocess(Ac, cnn, 3)
+    xr = SO.nn_postprocess(Ac.to_scipy(), cnn, 3)
+    assert np.max(np.abs(x - xr)) <= 1e-10
+    assert np.allclose(x.T @ x, np.eye(3), atol=1e-12)
+
+
+def _build(ctx, elements, smoother="l1", coarsest=150, seed=11):
+    A, S = elasticity(ctx, elements, seed)
+    nn = fa().constant_candidates(S.shape[0], 3)
+    mg = fa().smoothed_aggregation(A, nn, weights=weights(S, nn), block_size=3, candidate_dimension=3,
+                                   coarsest_dim=coarsest, smoother=smoother)
+    return A, S, nn, mg
+
+
+def test_sa_build_equals_composition(ctx):
+    """amg_sa_build's first level is the pieces composed as Hierarchy::coarsen
+    does (strength -> MIS -> tentative -> block_jacobi -> R, RAP): bitwise."""
+    A, S, nn, mg = _build(ctx, (5, 4, 4))
+    assert mg.levels() >= 3
+    G = fa().strength_graph(A, nn, weights(S, nn), depth=1, block_size=3)
+    agg, na = fa().aggregate_mis(G)
+    P, cnn = fa().sa_tentative_block(ctx, agg, na, nn, block_size=3)
+    Ps = fa().block_jacobi(A, P, 3)
+    Ac = fa().galerkin_rap(fa().transpose(Ps), A, Ps)
+    A1, _, _, _ = mg.level(1)
+    _, _, R0, P0 = mg.level(0)
+    for X, Y in ((P0, Ps), (A1, Ac)):
+        a, b = X.arrays(), Y.arrays()
+        assert all(np.array_equal(u, v) for u, v in zip(a, b))
+    assert R0.dims() == (na * 3, S.shape[0])
+
+
+def oracle_levels(mg, smoother):
+    levels = []
+    nl = mg.levels()
+    for l in range(nl):
+        Al, Sl, Rl, Pl = mg.level(l)
+        d = {"A": O.Csr.from_arrays(*Al.dims(), *Al.arrays()), "smoother": "chol" if l == nl - 1 else smoother}
+        if Rl is not None:
+            d["R"] = O.Csr.from_arrays(*Rl.dims(), *Rl.arrays())
+            d["P"] = O.Csr.from_arrays(*Pl.dims(), *Pl.arrays())
+        levels.append(d)
+    return levels
+
+
+@pytest.mark.parametrize("smoother", ["l1", "jacobi"])
+def test_sa_elasticity_vcycle_parity(ctx, smoother):
+    """C5's path end to end on the stand-in: one V-cycle to 1e-11 of the oracle
+    on the same hierarchy, 10 stationary cycles (rho_k) to 1e-8, PCG converges."""
+    import torch
+    A, S, nn, mg = _build(ctx, (8, 6, 6), smoother=smoother)
+    n = S.shape[0]
+    levels = oracle_levels(mg, smoother)
+    b = np.random.default_rng(12).uniform(-1, 1, n)
+    zref = O.Multigrid(levels).apply(b)
+    bd = torch.as_tensor(b, device="cuda:0")
+    z = torch.empty_like(bd)
+    mg.apply(z, bd)
+    ctx.synchronize()
+    assert np.linalg.norm(z.cpu().numpy() - zref) <= 1e-11 * np.linalg.norm(zref)
+    x = torch.zeros_like(bd)
+    it, hist = fa().stationary_solve(A, mg, bd, x, max_iter=11, rel_tol=1e-300)
+    _, it_o, hist_o = O.stationary_solve(levels[0]["A"], O.Multigrid(levels), b, max_iter=11, rel_tol=1e-300)
+    floor = EPS * abs(S).sum(axis=1).max() * float(torch.max(torch.abs(x))) / np.max(np.abs(b))
+    assert it == it_o == 11
+    assert np.all(np.abs(hist - hist_o) <= 1e-8 * hist_o + floor)
+    assert hist[-1] < hist[0]
+    x = torch.zeros_like(bd)
+    itp, _ = fa().pcg_solve(A, mg, bd, x, max_iter=200, rel_tol=1e-8)
+    itc, _ = fa().pcg_solve(A, None, bd, torch.zeros_like(bd), max_iter=2000, rel_tol=1e-8)
+    assert itp < 60 and itp < itc
+    assert np.linalg.norm(b - S @ x.cpu().numpy()) <= 1e-7 * np.linalg.norm(b)
+
+
+def test_sa_scalar_random_candidates(ctx):
+    """Block size 1, two random candidates, one kept (cd < k), depth 2 strength:
+    the scalar smooth_interpolation path and the k > 1 QR post-processing."""
+    import torch
+    dims = (12, 10, 9)
+    A = fa().SparseMatOp.laplace3d_7pt(ctx, *dims)
+    n = A.nrows
+    rng = np.random.default_rng(6)
+    nn = np.asfortranarray(np.column_stack([np.ones(n), rng.uniform(0.5, 1.5, n)]))
+    mg = fa().smoothed_aggregation(A, nn, block_size=1, candidate_dimension=1, strength_depth=2,
+                                   coarsest_dim=60, smoother="jacobi")
+    assert mg.levels() >= 2
+    levels = oracle_levels(mg, "jacobi")
+    b = rng.uniform(-1, 1, n)
+    zref = O.Multigrid(levels).apply(b)
+    bd = torch.as_tensor(b, device="cuda:0")
+    z = torch.empty_like(bd)
+    mg.apply(z, bd)
+    ctx.synchronize()
+    assert np.linalg.norm(z.cpu().numpy() - zref) <= 1e-11 * np.linalg.norm(zref)
