@@ -441,23 +441,33 @@ def run_dist(args, world, rank, local_rank):
     stream = torch.cuda.Stream()
     torch.cuda.set_stream(stream)
     ctx = fa.Context(local_rank, stream=stream.cuda_stream)
-    dims = weak_dims(args.edge, world)
+    strong = args.workload == "c4"
+    dims = (512, 512, 512) if strong else weak_dims(args.edge, world)
     t0 = time.perf_counter()
     fa.set_spmv_format("csr")  # global (setup) copy: no SELL needed
     A, mg = build_problem(fa, ctx, args, dims)
     fa.set_spmv_format("auto")
     nl = mg.levels()
-    splits = fa.slab_splits(fa.box_level_dims(dims, (args.box,) * 3, nl), world)
+    if args.problem in ("7pt", "27pt"):
+        splits = fa.slab_splits(fa.box_level_dims(dims, (args.box,) * 3, nl), world)
+    else:  # equal row splits aligned to the level's block size
+        splits = []
+        for l in range(nl):
+            n_l = mg.level(l)[0].nrows
+            bs = args.block_size
+            nb = n_l // bs
+            splits.append([((p * nb) // world) * bs for p in range(world)] + [n_l])
     obj = [fa.unique_id() if rank == 0 else None]
     dist.broadcast_object_list(obj, src=0)
     comm = fa.Comm(ctx, nranks=world, rank=rank, uid=obj[0])
     dm = fa.DistMultigrid(comm, mg, splits, agglomerate_rows=args.agglomerate).set_overlap(not args.no_overlap)
     infos = [dm.level_info(l) for l in range(nl)]
+    n_glob = A.nrows
     del mg, A  # global fine levels are no longer needed on this rank
     torch.cuda.synchronize()
     setup_s = time.perf_counter() - t0
+    log(f"rank {rank}: setup {setup_s:.1f}s, RCCL {fa.rccl_library()}")
     r0, r1 = dm.local_rows()
-    n_glob = int(np.prod(dims))
     b = torch.as_tensor(splitmix_uniform(n_glob, 42)[r0:r1].copy(), device=f"cuda:{local_rank}")
     z = torch.empty_like(b)
     for _ in range(args.warmup):
@@ -483,7 +493,8 @@ def run_dist(args, world, rank, local_rank):
     for _ in range(3):
         Al.apply(yl, xl)
     spmv_ms = time_kernel(lambda: Al.apply(yl, xl), 20, stream)
-    bytes_spmv = Al.spmv_info()["stream_bytes"] + 8 * nloc + 8 * nloc
+    al_info = Al.spmv_info()
+    bytes_spmv = al_info["stream_bytes"] + 8 * nloc + 8 * nloc
     achieved = bytes_spmv / (spmv_ms * 1e-3) / 1e9
     # distributed fine SpMV including the halo exchange
     Ad = dm.level_operator(0)
@@ -498,38 +509,75 @@ def run_dist(args, world, rank, local_rank):
     ga = torch.tensor([achieved], dtype=torch.float64)
     dist.all_reduce(ga, op=dist.ReduceOp.MIN)
     cycles_per_s = 1000.0 / ms_per_cycle
+    c4 = None
+    if dims == (512, 512, 512) and args.problem == "7pt" and not args.no_c4_base:
+        # C4 strong-scaling ratio: the same 512^3 problem on one
+        # GPU, timed in this job by rank 0 while the other ranks wait
+        base = None
+        if rank == 0:
+            del dm, Ad, Al
+            torch.cuda.synchronize()
+            base = c4_single_gpu_rate(fa, ctx, args, stream)
+        tb = torch.tensor([base or 0.0], dtype=torch.float64)
+        dist.broadcast(tb, src=0)
+        base = float(tb[0])
+        c4 = {"global_vcycles_per_s": round(cycles_per_s, 3), "one_gpu_512_vcycles_per_s": round(base, 3),
+              "ratio_vs_1gpu": round(cycles_per_s / base, 3) if base > 0 else None, "gpus": world,
+              "what": "512^3 7-pt (C4): V-cycles/s of this row-split run / V-cycles/s of the same "
+                      "hierarchy on one GPU (single-GPU path, measured in this job by rank 0)"}
     out = {
         "metric": METRIC,
-        "value": round(cycles_per_s * world, 3),
+        "value": round(cycles_per_s if strong else cycles_per_s * world, 3),
         "unit": "V-cycles/s",
         "n_gpus": world,
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": round(ms_per_cycle, 4),
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong" if strong else "weak",
         "vs_baseline": None,
         "dtype": "f64",
         "data": "synthetic (device-generated operator, splitmix64 rhs seed 42)",
-        "config": {"workload": f"SA V-cycle, 3D {args.problem} {dims[0]}x{dims[1]}x{dims[2]} "
-                               f"({world} x {args.edge}^3 rows), box {args.box}^3, {args.smoother} "
-                               f"s=1 mu=1, Cholesky coarsest; value = global V-cycles/s x {world}",
+        "config": {"workload": workload_name(args, dims) + (
+                       f"; C4 strong scaling: fixed 512^3 over {world} GPUs, value = global V-cycles/s"
+                       if strong else f"; weak scaling: {world} x {args.edge}^3 rows, "
+                                      f"value = global V-cycles/s x {world}"),
+                   "c4_strong": c4,
                    "global_vcycles_per_s": round(cycles_per_s, 3),
                    "levels": nl, "level_plan_rank0": infos, "setup_s": round(setup_s, 2),
                    "fine_spmv_with_halo_ms": round(halo_ms, 4),
                    "rel_residual_after_1_cycle": float(hist[1]) if len(hist) > 1 else None,
                    "agglomerate_rows": args.agglomerate,
                    "halo_overlap": not args.no_overlap,
-                   "parallelism": f"row-block z-slabs x{world}, RCCL halo exchange"},
+                   "rccl": fa.rccl_library(),
+                   "parallelism": f"row-block {'z-slabs' if args.problem in ('7pt', '27pt') else 'row ranges'} "
+                                  f"x{world}, RCCL halo exchange"},
         "fine_spmv_gbs": round(float(ga[0]), 1),
         "roofline": {"bound": "hbm", "achieved": round(float(ga[0]), 1), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(float(ga[0]) / HBM_PEAK_GBS, 4), "traffic": None,
-                     "kernel": f"{Al.spmv_info()['kernel']} SpMV (SET) on the rank-local A_0 (min over ranks)",
+                     "kernel": f"{al_info['kernel']} SpMV (SET) on the rank-local A_0 (min over ranks)",
                      "bytes_per_launch": bytes_spmv, "ms_per_launch": round(spmv_ms, 5)},
         "cpu_baseline": None,
     }
     dist.destroy_process_group()
     return out if rank == 0 else None
+
+
+def c4_single_gpu_rate(fa, ctx, args, stream, cycles=10):
+    """V-cycles/s of the 512^3 hierarchy on this one GPU (the C4 base rate)."""
+    import torch
+    dims = (512, 512, 512)
+    A, mg = build_problem(fa, ctx, args, dims)
+    n = A.nrows
+    b = torch.as_tensor(splitmix_uniform(n, 42), device=torch.cuda.current_device())
+    z = torch.empty_like(b)
+    for _ in range(2):
+        mg.apply(z, b)
+    ms = time_kernel(lambda: mg.apply(z, b), cycles, stream)
+    del mg, A
+    torch.cuda.synchronize()
+    log(f"C4 base: 512^3 on one GPU {1000.0 / ms:.2f} V-cycles/s")
+    return 1000.0 / ms
 
 
 def main():
@@ -558,6 +606,11 @@ def main():
     ap.add_argument("--ab", action="store_true", help="A/B the SpMV storage formats (stderr)")
     ap.add_argument("--no-fold", action="store_true",
                     help="store the zero-guess smoothing step instead of folding it into the residual")
+    ap.add_argument("--workload", default="weak", choices=["weak", "c4"],
+                    help="N > 1: weak (N x edge^3 rows; at N = 8 the grid is 512^3 = C4 and the line "
+                         "carries the C4 strong-scaling ratio) or c4 (512^3 fixed at every N, strong)")
+    ap.add_argument("--no-c4-base", action="store_true",
+                    help="skip the one-GPU 512^3 measurement behind the C4 ratio")
     ap.add_argument("--dist", action="store_true",
                     help="distributed path even at world size 1 (1-rank RCCL; a check of run_dist)")
     args = ap.parse_args()
@@ -569,6 +622,8 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.workload == "c4" and world == 1 and not args.dist:
+        args.edge = 512  # C4 on one GPU: the base of the strong-scaling curve
     if world > 1 or args.dist:
         out = run_dist(args, world, rank, local_rank)
     else:

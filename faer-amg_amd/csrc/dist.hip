@@ -19,12 +19,16 @@
 // context stream, over xGMI) and a loopback hub (virtual ranks as host threads
 // of one process sharing one GPU) that validates the whole algorithm on a
 // single device.
+#include <dlfcn.h>
+#include <link.h>
 #include <rccl/rccl.h>
 
 #include <algorithm>
 #include <condition_variable>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
+#include <string>
 
 #include "handles.hpp"
 #include "solve.hpp"
@@ -32,6 +36,81 @@
 using namespace famg;
 
 namespace famg {
+
+// ------------------------------------------------------------- RCCL binding
+//
+// One RCCL per process: the library is not linked against librccl; the entry
+// points are resolved at first use from the librccl the process has already
+// mapped (torch's bundled one when torch is imported), else from
+// $FAMG_RCCL_PATH, librccl.so.1 on the loader path, /opt/rocm/lib/librccl.so.1.
+// Two RCCL builds in one process (the linked one and torch's) would share
+// symbol names and interpose on each other.
+struct RcclApi {
+    void *h = nullptr;
+    std::string path, error;
+    decltype(&ncclGetErrorString) GetErrorString = nullptr;
+    decltype(&ncclGetUniqueId) GetUniqueId = nullptr;
+    decltype(&ncclCommInitRank) CommInitRank = nullptr;
+    decltype(&ncclCommDestroy) CommDestroy = nullptr;
+    decltype(&ncclGroupStart) GroupStart = nullptr;
+    decltype(&ncclGroupEnd) GroupEnd = nullptr;
+    decltype(&ncclSend) Send = nullptr;
+    decltype(&ncclRecv) Recv = nullptr;
+    decltype(&ncclAllGather) AllGather = nullptr;
+    decltype(&ncclAllReduce) AllReduce = nullptr;
+};
+
+static int find_mapped_rccl(struct dl_phdr_info *info, size_t, void *data) {
+    if (info->dlpi_name && std::strstr(info->dlpi_name, "librccl")) {
+        *static_cast<std::string *>(data) = info->dlpi_name;
+        return 1;
+    }
+    return 0;
+}
+
+static RcclApi load_rccl() {
+    RcclApi a;
+    std::string mapped;
+    dl_iterate_phdr(find_mapped_rccl, &mapped);
+    std::vector<std::pair<std::string, int>> cands;
+    if (!mapped.empty()) cands.push_back({mapped, RTLD_NOW | RTLD_NOLOAD});
+    if (const char *e = getenv("FAMG_RCCL_PATH")) cands.push_back({e, RTLD_NOW});
+    cands.push_back({"librccl.so.1", RTLD_NOW});
+    cands.push_back({"/opt/rocm/lib/librccl.so.1", RTLD_NOW});
+    for (auto &c : cands) {
+        a.h = dlopen(c.first.c_str(), c.second);
+        if (a.h) {
+            a.path = c.first;
+            break;
+        }
+    }
+    if (!a.h) {
+        a.error = "cannot load librccl (tried the mapped one, $FAMG_RCCL_PATH, librccl.so.1, /opt/rocm/lib)";
+        return a;
+    }
+    auto sym = [&](const char *name) {
+        void *f = dlsym(a.h, name);
+        if (!f && a.error.empty()) a.error = std::string("librccl lacks ") + name;
+        return f;
+    };
+    a.GetErrorString = reinterpret_cast<decltype(a.GetErrorString)>(sym("ncclGetErrorString"));
+    a.GetUniqueId = reinterpret_cast<decltype(a.GetUniqueId)>(sym("ncclGetUniqueId"));
+    a.CommInitRank = reinterpret_cast<decltype(a.CommInitRank)>(sym("ncclCommInitRank"));
+    a.CommDestroy = reinterpret_cast<decltype(a.CommDestroy)>(sym("ncclCommDestroy"));
+    a.GroupStart = reinterpret_cast<decltype(a.GroupStart)>(sym("ncclGroupStart"));
+    a.GroupEnd = reinterpret_cast<decltype(a.GroupEnd)>(sym("ncclGroupEnd"));
+    a.Send = reinterpret_cast<decltype(a.Send)>(sym("ncclSend"));
+    a.Recv = reinterpret_cast<decltype(a.Recv)>(sym("ncclRecv"));
+    a.AllGather = reinterpret_cast<decltype(a.AllGather)>(sym("ncclAllGather"));
+    a.AllReduce = reinterpret_cast<decltype(a.AllReduce)>(sym("ncclAllReduce"));
+    return a;
+}
+
+static const RcclApi &rccl() {
+    static const RcclApi api = load_rccl();
+    FAMG_REQUIRE(api.error.empty(), AMG_ERR_RCCL, api.error);
+    return api;
+}
 
 // ------------------------------------------------------------- transports
 
@@ -56,33 +135,33 @@ struct Transport {
     do {                                                                                   \
         ncclResult_t r_ = (expr);                                                          \
         if (r_ != ncclSuccess)                                                             \
-            ::famg::fail(AMG_ERR_RCCL, std::string(#expr) + ": " + ncclGetErrorString(r_)); \
+            ::famg::fail(AMG_ERR_RCCL, std::string(#expr) + ": " + rccl().GetErrorString(r_)); \
     } while (0)
 
 struct RcclTransport : Transport {
     ncclComm_t comm = nullptr;
     DevBuf<double> one;
     ~RcclTransport() override {
-        if (comm) ncclCommDestroy(comm);
+        if (comm) rccl().CommDestroy(comm);
     }
     void exchange(const std::vector<Peer> &peers, hipStream_t s) override {
         if (peers.empty()) return;
-        FAMG_CHECK_NCCL(ncclGroupStart());
+        FAMG_CHECK_NCCL(rccl().GroupStart());
         for (const Peer &p : peers) {
-            if (p.sbytes) FAMG_CHECK_NCCL(ncclSend(p.sbuf, p.sbytes, ncclUint8, p.rank, comm, s));
-            if (p.rbytes) FAMG_CHECK_NCCL(ncclRecv(p.rbuf, p.rbytes, ncclUint8, p.rank, comm, s));
+            if (p.sbytes) FAMG_CHECK_NCCL(rccl().Send(p.sbuf, p.sbytes, ncclUint8, p.rank, comm, s));
+            if (p.rbytes) FAMG_CHECK_NCCL(rccl().Recv(p.rbuf, p.rbytes, ncclUint8, p.rank, comm, s));
         }
-        FAMG_CHECK_NCCL(ncclGroupEnd());
+        FAMG_CHECK_NCCL(rccl().GroupEnd());
     }
     void allgather(const void *sbuf, void *rbuf, int64_t bytes, hipStream_t s) override {
-        FAMG_CHECK_NCCL(ncclAllGather(sbuf, rbuf, bytes, ncclUint8, comm, s));
+        FAMG_CHECK_NCCL(rccl().AllGather(sbuf, rbuf, bytes, ncclUint8, comm, s));
     }
     void allreduce(double *buf, int64_t count, bool is_max, hipStream_t s) override {
-        FAMG_CHECK_NCCL(ncclAllReduce(buf, buf, count, ncclDouble, is_max ? ncclMax : ncclSum, comm, s));
+        FAMG_CHECK_NCCL(rccl().AllReduce(buf, buf, count, ncclDouble, is_max ? ncclMax : ncclSum, comm, s));
     }
     void barrier(hipStream_t s) override {
         if (one.size() < 1) one.resize(1);
-        FAMG_CHECK_NCCL(ncclAllReduce(one.get(), one.get(), 1, ncclDouble, ncclSum, comm, s));
+        FAMG_CHECK_NCCL(rccl().AllReduce(one.get(), one.get(), 1, ncclDouble, ncclSum, comm, s));
         FAMG_CHECK_HIP(hipStreamSynchronize(s));
     }
 };
@@ -750,11 +829,21 @@ extern "C" {
 
 int32_t amg_comm_unique_id_size(void) { return (int32_t)sizeof(ncclUniqueId); }
 
+const char *amg_rccl_library(void) {
+    static std::string p;
+    try {
+        p = rccl().path;
+    } catch (...) {
+        p.clear();
+    }
+    return p.c_str();
+}
+
 amg_status amg_comm_get_unique_id(void *id) {
     return dguard([&] {
         FAMG_REQUIRE(id, AMG_ERR_INVALID, "null id buffer");
         ncclUniqueId u;
-        FAMG_CHECK_NCCL(ncclGetUniqueId(&u));
+        FAMG_CHECK_NCCL(rccl().GetUniqueId(&u));
         std::memcpy(id, &u, sizeof(u));
     });
 }
@@ -769,7 +858,7 @@ amg_status amg_comm_create(amg_ctx *ctx, int32_t nranks, int32_t rank, const voi
         t->rank = rank;
         ncclUniqueId u;
         std::memcpy(&u, id, sizeof(u));
-        FAMG_CHECK_NCCL(ncclCommInitRank(&t->comm, nranks, u, rank));
+        FAMG_CHECK_NCCL(rccl().CommInitRank(&t->comm, nranks, u, rank));
         *out = new amg_comm{c, t};
     });
 }

@@ -654,8 +654,70 @@ void nn_stationary_l1(CsrOp &A, int64_t iters, double *x_host) {
     FAMG_CHECK_HIP(hipStreamSynchronize(s));
 }
 
+// ---- box-aggregate setup kernels (device-resident: no host pass over the
+// fine rows; the 512^3 global setup copy of the distributed bench has 134M)
+
+// agg[i] = box index of row i (x fastest)
+__global__ void k_box_agg(int64_t cx, int64_t cy, int64_t cz, int64_t bx, int64_t by, int64_t bz, int64_t ncx,
+                          int64_t ncy, int32_t *agg) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= cx * cy * cz) return;
+    const int64_t x = i % cx, y = (i / cx) % cy, z = i / (cx * cy);
+    agg[i] = (int32_t)(x / bx + ncx * (y / by + ncy * (z / bz)));
+}
+
+// coarse candidate of box J: sqrt(sum nn_i^2) over its nodes in ascending index
+// order (the host loop of sa_tentative, bit for bit); *bad = 1 on a zero candidate
+__global__ void k_box_norm(const double *nn, int64_t cx, int64_t cy, int64_t cz, int64_t bx, int64_t by, int64_t bz,
+                           int64_t ncx, int64_t ncy, int64_t na, double *cnn, int *bad) {
+    const int64_t J = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (J >= na) return;
+    const int64_t ax = J % ncx, ay = (J / ncx) % ncy, az = J / (ncx * ncy);
+    double ss = 0.0;
+    for (int64_t z = az * bz; z < min(cz, (az + 1) * bz); z++)
+        for (int64_t y = ay * by; y < min(cy, (ay + 1) * by); y++)
+            for (int64_t x = ax * bx; x < min(cx, (ax + 1) * bx); x++) {
+                const double v = nn[x + cx * (y + cy * z)];
+                ss = ss + v * v;
+            }
+    cnn[J] = sqrt(ss);
+    if (!(cnn[J] > 0.0)) *bad = 1;
+}
+
+// tentative P for one candidate: row i has one entry nn_i / cnn[agg_i] at agg_i
+__global__ void k_tent_fill(const int32_t *agg, const double *nn, const double *cnn, int64_t n, int64_t *rp,
+                            int32_t *col, double *val) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i > n) return;
+    rp[i] = i;
+    if (i < n) {
+        col[i] = agg[i];
+        val[i] = nn[i] / cnn[agg[i]];
+    }
+}
+
+// hierarchy.rs:219-228 on a device vector (nn_stationary_l1 without the host copies)
+static void nn_stationary_l1_dev(CsrOp &A, int64_t iters, double *x) {
+    Ctx &ctx = *A.ctx;
+    hipStream_t s = ctx.stream;
+    const int64_t n = A.nrows;
+    auto d = make_l1(A);
+    DevBuf<double> xin(n), r(n);
+    vec_copy(xin.get(), x, n, s);
+    vec_mul(x, d->d.get(), xin.get(), n, s);
+    for (int64_t it = 1; it < iters; it++) {
+        spmv(A.m, x, r.get(), SPMV_SET, SpmvEpi{}, s);
+        vec_nn_step(x, d->d.get(), r.get(), n, s);
+    }
+    const double nrm = std::sqrt(vec_dot(x, x, n, ctx));
+    if (n) hipLaunchKernelGGL(k_divs, dim3((unsigned)ceil_div(n, 256)), dim3(256), 0, s, x, nrm, n);
+    FAMG_CHECK_HIP(hipGetLastError());
+}
+
 // Hierarchy::coarsen (hierarchy.rs:190-248) with box aggregates, then a
 // Multigrid assembled as Multigrid::new / add_level (multigrid.rs:190-239).
+// Every per-row pass runs on the device; the results are those of the host
+// sa_tentative / nn_stationary_l1 (same operation order).
 std::shared_ptr<MultigridOp> sa_build_box(const CsrPtr &A, int64_t nx, int64_t ny, int64_t nz,
                                           int64_t bx, int64_t by, int64_t bz,
                                           int64_t coarsest_dim, int64_t max_levels,
@@ -663,37 +725,57 @@ std::shared_ptr<MultigridOp> sa_build_box(const CsrPtr &A, int64_t nx, int64_t n
     FAMG_REQUIRE(nx * ny * nz == A->nrows, AMG_ERR_DIM, "grid dims do not match the matrix");
     FAMG_REQUIRE(bx > 0 && by > 0 && bz > 0, AMG_ERR_INVALID, "box sizes must be positive");
     Ctx *ctx = A->ctx;
+    hipStream_t s = ctx->stream;
     if (max_levels <= 0) max_levels = INT64_MAX;
     std::vector<CsrPtr> As{A}, Rs, Ps;
-    std::vector<double> nn(A->nrows, 1.0);
+    DevBuf<double> nn(std::max<int64_t>(1, A->nrows));
+    vec_fill(nn.get(), 1.0, A->nrows, s);
     int64_t cx = nx, cy = ny, cz = nz;
     int64_t level = 1, coarse_dim = -1;
     std::vector<std::vector<int64_t>> aggs;  // per coarsened level (block smoother partition)
     std::vector<int64_t> naggs;
+    DevBuf<int> bad(1);
     while ((coarse_dim < 0 || coarse_dim > coarsest_dim) && level < max_levels) {
         CsrPtr cur = As.back();
         const int64_t n = cur->nrows;
         const int64_t ncx = ceil_div(cx, bx), ncy = ceil_div(cy, by), ncz = ceil_div(cz, bz);
-        std::vector<int64_t> agg(n);
-        for (int64_t z = 0; z < cz; z++)
-            for (int64_t y = 0; y < cy; y++)
-                for (int64_t x = 0; x < cx; x++)
-                    agg[x + cx * (y + cy * z)] = x / bx + ncx * (y / by + ncy * (z / bz));
         const int64_t na = ncx * ncy * ncz;
-        std::vector<double> cnn(na);
-        CsrPtr Pt = sa_tentative(ctx, n, agg.data(), na, nn.data(), cnn.data());
+        DevBuf<int32_t> agg(std::max<int64_t>(1, n));
+        DevBuf<double> cnn(std::max<int64_t>(1, na));
+        FAMG_CHECK_HIP(hipMemsetAsync(bad.get(), 0, sizeof(int), s));
+        hipLaunchKernelGGL(k_box_agg, dim3((unsigned)ceil_div(n, 256)), dim3(256), 0, s, cx, cy, cz, bx, by, bz,
+                           ncx, ncy, agg.get());
+        hipLaunchKernelGGL(k_box_norm, dim3((unsigned)ceil_div(na, 256)), dim3(256), 0, s, nn.get(), cx, cy, cz, bx,
+                           by, bz, ncx, ncy, na, cnn.get(), bad.get());
+        int h = 0;
+        FAMG_CHECK_HIP(hipMemcpyAsync(&h, bad.get(), sizeof(int), hipMemcpyDeviceToHost, s));
+        FAMG_CHECK_HIP(hipStreamSynchronize(s));
+        FAMG_REQUIRE(h == 0, AMG_ERR_INVALID, "aggregate with a zero candidate");
+        // tentative P (interpolation/mod.rs:754-805), one candidate: only the
+        // SpGEMM reads it, so it gets no SpMV storage
+        auto Pt = make_csr(ctx);
+        csr_alloc(Pt->m, ctx, n, na, n);
+        hipLaunchKernelGGL(k_tent_fill, dim3((unsigned)ceil_div(n + 1, 256)), dim3(256), 0, s, agg.get(), nn.get(),
+                           cnn.get(), n, Pt->m.rp64.get(), Pt->m.col.get(), Pt->m.val.get());
+        FAMG_CHECK_HIP(hipGetLastError());
+        Pt->nrows = n;
+        Pt->ncols = na;
         CsrPtr P = smooth_interpolation(*cur, *Pt, omega);
+        Pt.reset();
         CsrPtr R = transpose_op(*P);
         CsrPtr Ac = galerkin_rap(*R, *cur, *P);
-        nn_stationary_l1(*Ac, 3, cnn.data());
+        nn_stationary_l1_dev(*Ac, 3, cnn.get());
         if (smoother == 3) {
-            aggs.push_back(agg);
+            std::vector<int32_t> a32(n);
+            FAMG_CHECK_HIP(hipMemcpyAsync(a32.data(), agg.get(), n * sizeof(int32_t), hipMemcpyDeviceToHost, s));
+            FAMG_CHECK_HIP(hipStreamSynchronize(s));
+            aggs.emplace_back(a32.begin(), a32.end());
             naggs.push_back(na);
         }
         Rs.push_back(R);
         Ps.push_back(P);
         As.push_back(Ac);
-        nn.swap(cnn);
+        nn = std::move(cnn);
         cx = ncx; cy = ncy; cz = ncz;
         coarse_dim = Ac->nrows;
         level++;

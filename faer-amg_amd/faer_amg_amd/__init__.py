@@ -98,6 +98,7 @@ SIGNATURES = {
     "amg_composite_push": (i32, [vp, vp]),
     "amg_composite_ncomponents": (i32, [vp, P(i64)]),
     "amg_comm_unique_id_size": (i32, []),
+    "amg_rccl_library": (C.c_char_p, []),
     "amg_comm_get_unique_id": (i32, [vp]),
     "amg_comm_create": (i32, [vp, i32, i32, vp, P(vp)]),
     "amg_loopback_hub_create": (i32, [i32, P(vp)]),
@@ -749,6 +750,11 @@ class Composite(LinOp):
 
 
 # ------------------------------------------------------------------ multi-GPU
+
+def rccl_library():
+    """Path of the librccl the library bound to ('' if none could be loaded)."""
+    return _lib.amg_rccl_library().decode()
+
 
 def unique_id():
     """ncclUniqueId bytes (create on rank 0, broadcast out of band)."""

@@ -337,6 +337,9 @@ amg_status amg_pcg_solve(amg_linop *A, amg_linop *M, const double *b, double *x,
  * redundantly on every rank. */
 typedef struct amg_comm amg_comm;
 typedef struct amg_loopback_hub amg_loopback_hub;
+/* Path of the librccl the library bound to (the one already mapped in the
+ * process, e.g. torch's, else $FAMG_RCCL_PATH / librccl.so.1); "" if none loads. */
+const char *amg_rccl_library(void);
 /* ncclUniqueId size in bytes (128). */
 int32_t amg_comm_unique_id_size(void);
 /* Fill `id` (amg_comm_unique_id_size() bytes) on rank 0; broadcast it out of band. */

@@ -19,6 +19,9 @@ for s in "$@"; do
         satests) step pytest_sa 600 python -u -m pytest tests/test_gpu_sa.py tests/test_gpu_dist.py -m gpu -v --timeout 120 --timeout-method thread ;;
         elast30) step bench_elast30 400 python bench.py --problem elast --elements 30 --steps 20 --warmup 3 ;;
         elast) step bench_elast 900 python bench.py --problem elast --steps 20 --warmup 3 ;;
+        c4one) step bench_c4one 600 python bench.py --workload c4 --steps 10 --warmup 2 --no-cpu-baseline ;;
+        dist1c4) step dist1c4 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 \
+                  --master-addr 127.0.0.1 --master-port 29515 bench.py --dist --workload c4 --steps 5 --warmup 1 ;;
         smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
         bench) step bench 600 python bench.py --steps 20 --warmup 3 ;;
         benchq) step bench 400 python bench.py --steps 20 --warmup 3 --no-cpu-baseline --ab ;;
