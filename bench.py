@@ -358,6 +358,11 @@ def run_single(args):
                    "storage": A64.spmv_info()}
     del A64
 
+    general = None
+    if args.problem == "7pt" and not args.no_general:
+        general = general_roofline(fa, ctx, dims, stream, x, y)
+        log("roofline.general: " + json.dumps(general))
+
     if args.ab:
         ops = {}
         for fmt in ("csr", "sell"):
@@ -422,7 +427,8 @@ def run_single(args):
                      "bytes_per_launch": bytes_spmv, "ms_per_launch": round(spmv_ms, 5),
                      "csr_bytes_per_launch": bytes_csr,
                      "csr_equivalent_GBs": round(bytes_csr / (spmv_ms * 1e-3) / 1e9, 1),
-                     "fp64_values": fp64_values},
+                     "fp64_values": fp64_values,
+                     "general": general},
         "cpu_baseline": cpu,
         "parity": parity,
     }
@@ -563,6 +569,41 @@ def run_dist(args, world, rank, local_rank):
     return out if rank == 0 else None
 
 
+def general_roofline(fa, ctx, dims, stream, x, y):
+    """roofline.general: the fine SpMV on a matrix without stencil structure --
+    the 7-pt graph with random edge weights (> 65536 distinct values: fp64
+    values) and a symmetric row permutation (columns i32 / u16) -- in the SELL
+    storage the auto policy picks and in CSR-stream, priced on SURVEY.md 8(d)'s
+    CSR bytes (12 nnz + 4 (n+1) + 8 n + 8 n).  Two permutations: within windows
+    of 4096 rows (the locality of a mesh numbering) and over all rows (every x
+    gather random)."""
+    out = {}
+    for name, window in (("window4096", 4096), ("random", 0)):
+        res = {}
+        for fmt in ("auto", "csr"):
+            fa.set_spmv_format(fmt)
+            try:
+                M = fa.SparseMatOp.random7(ctx, *dims, seed=42, window=window)
+            finally:
+                fa.set_spmv_format("auto")
+            for _ in range(3):
+                M.apply(y, x)
+            ms = time_kernel(lambda: M.apply(y, x), 20, stream)
+            info = M.spmv_info()
+            n, nnz = M.nrows, M.nnz
+            csr_b = spmv_bytes(n, n, nnz)
+            res[info["kernel"]] = {"ms_per_launch": round(ms, 5),
+                                   "csr_bytes_per_launch": csr_b,
+                                   "achieved_csr_GBs": round(csr_b / (ms * 1e-3) / 1e9, 1),
+                                   "frac_csr": round(csr_b / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                                   "format_bytes_per_launch": info["stream_bytes"] + 16 * n,
+                                   "storage": {k: info[k] for k in ("stream_bytes", "slices_u16", "slices_i32",
+                                                                    "slices_implicit", "value_bits")}}
+            del M
+        out[name] = res
+    return out
+
+
 def c4_single_gpu_rate(fa, ctx, args, stream, cycles=10):
     """V-cycles/s of the 512^3 hierarchy on this one GPU (the C4 base rate)."""
     import torch
@@ -604,6 +645,7 @@ def main():
     ap.add_argument("--no-overlap", action="store_true",
                     help="distributed: exchange halos before the SpMV instead of under its interior rows")
     ap.add_argument("--ab", action="store_true", help="A/B the SpMV storage formats (stderr)")
+    ap.add_argument("--no-general", action="store_true", help="skip roofline.general (random 7-pt)")
     ap.add_argument("--no-fold", action="store_true",
                     help="store the zero-guess smoothing step instead of folding it into the residual")
     ap.add_argument("--workload", default="weak", choices=["weak", "c4"],

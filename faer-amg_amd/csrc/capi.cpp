@@ -284,6 +284,18 @@ amg_status amg_gen_laplace3d_7pt(amg_ctx *ctx, int64_t nx, int64_t ny, int64_t n
     });
 }
 
+amg_status amg_gen_random_7pt(amg_ctx *ctx, int64_t nx, int64_t ny, int64_t nz, uint64_t seed, int64_t window,
+                              amg_linop **out) {
+    return guard([&] {
+        FAMG_REQUIRE(ctx && out, AMG_ERR_INVALID, "null argument");
+        ctx->ctx.set_device();
+        auto p = make_csr(&ctx->ctx);
+        gen_random_7pt(p->m, &ctx->ctx, nx, ny, nz, seed, window);
+        p->nrows = p->ncols = p->m.nrows;
+        *out = box(p);
+    });
+}
+
 amg_status amg_gen_aniso27(amg_ctx *ctx, int64_t nx, int64_t ny, int64_t nz, double ex, double ey,
                            double ez, amg_linop **out) {
     return guard([&] {

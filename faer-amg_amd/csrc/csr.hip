@@ -207,6 +207,122 @@ __global__ void k_sten_fill(Stencil st, int64_t nx, int64_t ny, int64_t nz, cons
     }
 }
 
+// ---- random-coefficient 7-pt operator, symmetrically permuted (the general
+// matrix of roofline.general: > 65536 distinct values, no stencil structure)
+
+__device__ __host__ __forceinline__ uint64_t g_splitmix(uint64_t z) {
+    z += 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+
+// edge weight of the unordered pair (a, b): 0.5 + U[0,1)
+__device__ __forceinline__ double edge_w(uint64_t seed, int64_t a, int64_t b) {
+    const uint64_t lo = (uint64_t)min(a, b), hi = (uint64_t)max(a, b);
+    const uint64_t h = g_splitmix(seed ^ g_splitmix(lo * 0x9E3779B97F4A7C15ull + hi));
+    return 0.5 + (double)(h >> 11) * 0x1.0p-53;
+}
+
+// Feistel bijection on [0, 2^(2h)) keyed by (seed, key), 4 rounds; inverse = rounds reversed
+__device__ __forceinline__ uint64_t feistel(uint64_t v, int h, uint64_t seed, uint64_t key, bool inv) {
+    const uint64_t mask = (uint64_t(1) << h) - 1;
+    uint64_t L = v >> h, R = v & mask;
+    for (int k = 0; k < 4; k++) {
+        const int rk = inv ? 3 - k : k;
+        const uint64_t f = g_splitmix(seed ^ (key * 0xD1B54A32D192ED03ull) ^ ((uint64_t)rk << 56) ^ (inv ? L : R)) & mask;
+        if (!inv) { const uint64_t t = L ^ f; L = R; R = t; }
+        else { const uint64_t t = R ^ f; R = L; L = t; }
+    }
+    return (L << h) | R;
+}
+
+// permutation of [0, m) (m <= 2^(2h)) by cycle walking
+__device__ __forceinline__ int64_t perm_walk(int64_t v, int64_t m, int h, uint64_t seed, uint64_t key, bool inv) {
+    uint64_t u = (uint64_t)v;
+    do { u = feistel(u, h, seed, key, inv); } while (u >= (uint64_t)m);
+    return (int64_t)u;
+}
+
+struct RandPerm {
+    int64_t n, window;  // window < 0: identity; 0: one window of n rows
+    int h;              // Feistel half-width for a full window
+    uint64_t seed;
+    __device__ int64_t apply(int64_t i, bool inv) const {
+        if (window < 0) return i;
+        const int64_t W = window == 0 ? n : window;
+        const int64_t w = i / W, base = w * W, m = min(W, n - base);
+        int hh = h;
+        while ((int64_t(1) << (2 * hh)) >= 4 * m && hh > 1) hh--;  // a partial last window walks less
+        return base + perm_walk(i - base, m, hh, seed, (uint64_t)w, inv);
+    }
+};
+
+__global__ void k_rand7_count(RandPerm pm, int64_t nx, int64_t ny, int64_t nz, int64_t *cnt) {
+    const int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    const int64_t n = nx * ny * nz;
+    if (r >= n) return;
+    const int64_t i = pm.apply(r, true);
+    const int64_t x = i % nx, y = (i / nx) % ny, z = i / (nx * ny);
+    cnt[r] = 1 + (x > 0) + (x + 1 < nx) + (y > 0) + (y + 1 < ny) + (z > 0) + (z + 1 < nz);
+}
+
+__global__ void k_rand7_fill(RandPerm pm, int64_t nx, int64_t ny, int64_t nz, uint64_t seed, const int64_t *rp,
+                             int32_t *col, double *val) {
+    const int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    const int64_t n = nx * ny * nz;
+    if (r >= n) return;
+    const int64_t i = pm.apply(r, true);
+    const int64_t x = i % nx, y = (i / nx) % ny, z = i / (nx * ny);
+    const int64_t nb[6] = {x > 0 ? i - 1 : -1, x + 1 < nx ? i + 1 : -1, y > 0 ? i - nx : -1,
+                           y + 1 < ny ? i + nx : -1, z > 0 ? i - nx * ny : -1, z + 1 < nz ? i + nx * ny : -1};
+    int32_t c[7];
+    double v[7];
+    int k = 0;
+    double diag = 0.0;
+    for (int d = 0; d < 6; d++) {
+        if (nb[d] < 0) { diag = diag + 1.0; continue; }  // Dirichlet neighbour
+        const double w = edge_w(seed, i, nb[d]);
+        diag = diag + w;
+        c[k] = (int32_t)pm.apply(nb[d], false);
+        v[k] = -w;
+        k++;
+    }
+    c[k] = (int32_t)r;
+    v[k] = diag;
+    k++;
+    for (int a = 1; a < k; a++)  // ascending columns
+        for (int b = a; b > 0 && c[b - 1] > c[b]; b--) {
+            const int32_t tc = c[b]; c[b] = c[b - 1]; c[b - 1] = tc;
+            const double tv = v[b]; v[b] = v[b - 1]; v[b - 1] = tv;
+        }
+    for (int a = 0; a < k; a++) {
+        col[rp[r] + a] = c[a];
+        val[rp[r] + a] = v[a];
+    }
+}
+
+void gen_random_7pt(GpuCsr &m, Ctx *ctx, int64_t nx, int64_t ny, int64_t nz, uint64_t seed, int64_t window) {
+    FAMG_REQUIRE(nx > 0 && ny > 0 && nz > 0, AMG_ERR_INVALID, "grid dims must be positive");
+    const int64_t n = nx * ny * nz;
+    RandPerm pm{n, window, 1, seed};
+    const int64_t W = window == 0 ? n : window;
+    while ((int64_t(1) << (2 * pm.h)) < W) pm.h++;
+    FAMG_REQUIRE(pm.h <= 31, AMG_ERR_UNSUPPORTED, "permutation window too large");
+    DevBuf<int64_t> cnt(n);
+    hipStream_t s = ctx->stream;
+    const unsigned g = (unsigned)ceil_div(n, 256);
+    hipLaunchKernelGGL(k_rand7_count, dim3(g), dim3(256), 0, s, pm, nx, ny, nz, cnt.get());
+    DevBuf<int64_t> rp(n + 1);
+    const int64_t nnz = scan_counts(cnt.get(), rp.get(), n, *ctx);
+    csr_alloc(m, ctx, n, n, nnz);
+    m.rp64 = std::move(rp);
+    hipLaunchKernelGGL(k_rand7_fill, dim3(g), dim3(256), 0, s, pm, nx, ny, nz, seed, m.rp64.get(), m.col.get(),
+                       m.val.get());
+    FAMG_CHECK_HIP(hipGetLastError());
+    csr_finalize(m);
+}
+
 // offs: nsten triples (dx,dy,dz) in ascending linear-offset order (dz, dy, dx).
 void gen_stencil(GpuCsr &m, Ctx *ctx, int64_t nx, int64_t ny, int64_t nz, const int *offs,
                  const double *coef, int nsten) {

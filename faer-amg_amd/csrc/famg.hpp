@@ -175,6 +175,10 @@ void transpose(const GpuCsr &A, GpuCsr &T);
 void smooth_interp_fixup(GpuCsr &S, const GpuCsr &P, const double *diag, double omega);
 void gen_stencil(GpuCsr &m, Ctx *ctx, int64_t nx, int64_t ny, int64_t nz, const int *offs,
                  const double *coef, int nsten);
+// random-coefficient 7-pt operator (edge weights 0.5 + U[0,1), Dirichlet
+// diagonal), rows/columns permuted symmetrically (window < 0 none, 0 all rows,
+// > 0 within consecutive windows of that many rows)
+void gen_random_7pt(GpuCsr &m, Ctx *ctx, int64_t nx, int64_t ny, int64_t nz, uint64_t seed, int64_t window);
 
 // ------------------------------------------------------------------ operators
 

@@ -61,6 +61,7 @@ SIGNATURES = {
     "amg_csr_dia_range": (i32, [vp, vp]),
     "amg_gen_laplace3d_7pt": (i32, [vp, i64, i64, i64, P(vp)]),
     "amg_gen_aniso27": (i32, [vp, i64, i64, i64, dbl, dbl, dbl, P(vp)]),
+    "amg_gen_random_7pt": (i32, [vp, i64, i64, i64, C.c_uint64, i64, P(vp)]),
     "amg_linop_kind_of": (i32, [vp, P(i32)]),
     "amg_linop_dims": (i32, [vp, P(i64), P(i64)]),
     "amg_linop_apply": (i32, [vp, vp, i64, vp, i64, i64, C.c_int]),
@@ -368,6 +369,14 @@ class SparseMatOp(LinOp):
     def aniso27(cls, ctx, nx, ny, nz, ex=1.0, ey=1.0, ez=0.01):
         h = vp()
         _ck(_lib.amg_gen_aniso27(ctx.h, nx, ny, nz, ex, ey, ez, C.byref(h)))
+        return cls(h, ctx)
+
+    @classmethod
+    def random7(cls, ctx, nx, ny, nz, seed=42, window=4096):
+        """Random-coefficient 7-pt SPD operator, symmetrically permuted
+        (window < 0 none, 0 all rows, > 0 within windows of that many rows)."""
+        h = vp()
+        _ck(_lib.amg_gen_random_7pt(ctx.h, nx, ny, nz, seed, window, C.byref(h)))
         return cls(h, ctx)
 
     @property

@@ -134,6 +134,14 @@ amg_status amg_gen_laplace3d_7pt(amg_ctx *ctx, int64_t nx, int64_t ny, int64_t n
                                  amg_linop **out);
 amg_status amg_gen_aniso27(amg_ctx *ctx, int64_t nx, int64_t ny, int64_t nz, double ex,
                            double ey, double ez, amg_linop **out);
+/* General (non-stencil) SPD operator of the same size: the 7-point graph with
+ * edge weights 0.5 + U[0,1) (splitmix64 of the edge and seed), a_ij = -w_ij,
+ * a_ii = sum of the six incident weights (1.0 for a missing, Dirichlet
+ * neighbour), rows and columns permuted symmetrically by a seeded bijection:
+ * window < 0 none, 0 over all rows, > 0 within consecutive windows of that many
+ * rows (locality of a mesh numbering without stencil structure). */
+amg_status amg_gen_random_7pt(amg_ctx *ctx, int64_t nx, int64_t ny, int64_t nz, uint64_t seed, int64_t window,
+                              amg_linop **out);
 
 /* In-tree stand-in for config C5 (Flan_1565, which cannot be fetched): Q1
  * hexahedral linear elasticity on an ex x ey x ez element box, per-element

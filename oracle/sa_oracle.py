@@ -305,3 +305,78 @@ def nn_postprocess(A, x, iters=3):
         x[:, c] = v
     Q, R = np.linalg.qr(x)
     return Q * np.sign(np.diag(R))
+
+
+# ------------------------------------------------------- general 7-pt operator
+
+_M64 = (1 << 64) - 1
+
+
+def _edge_w(seed, a, b):
+    lo, hi = min(a, b), max(a, b)
+    h = _splitmix64((seed ^ _splitmix64((lo * 0x9E3779B97F4A7C15 + hi) & _M64)) & _M64)
+    return 0.5 + float(h >> 11) * 2.0 ** -53
+
+
+def _feistel(v, h, seed, key, inv):
+    mask = (1 << h) - 1
+    L, R = v >> h, v & mask
+    for k in range(4):
+        rk = 3 - k if inv else k
+        x = seed ^ ((key * 0xD1B54A32D192ED03) & _M64) ^ (rk << 56) ^ (L if inv else R)
+        f = _splitmix64(x & _M64) & mask
+        if not inv:
+            L, R = R, L ^ f
+        else:
+            L, R = R ^ f, L
+    return (L << h) | R
+
+
+def _perm(i, n, window, h, seed, inv):
+    if window < 0:
+        return i
+    W = n if window == 0 else window
+    w = i // W
+    base = w * W
+    m = min(W, n - base)
+    hh = h
+    while (1 << (2 * hh)) >= 4 * m and hh > 1:
+        hh -= 1
+    u = i - base
+    while True:
+        u = _feistel(u, hh, seed, w, inv)
+        if u < m:
+            return base + u
+
+
+def random_7pt(nx, ny, nz, seed=42, window=4096):
+    """Restatement of amg_gen_random_7pt (csr.hip): edge weights 0.5 + U[0,1),
+    Dirichlet diagonal, symmetric permutation by 4-round Feistel bijections
+    with cycle walking.  Returns scipy CSR (columns ascending)."""
+    n = nx * ny * nz
+    W = n if window == 0 else window
+    h = 1
+    while (1 << (2 * h)) < W:
+        h += 1
+    rows, cols, vals = [], [], []
+    for r in range(n):
+        i = _perm(r, n, window, h, seed, True)
+        x, y, z = i % nx, (i // nx) % ny, i // (nx * ny)
+        nb = [i - 1 if x > 0 else -1, i + 1 if x + 1 < nx else -1, i - nx if y > 0 else -1,
+              i + nx if y + 1 < ny else -1, i - nx * ny if z > 0 else -1, i + nx * ny if z + 1 < nz else -1]
+        diag = 0.0
+        for j in nb:
+            if j < 0:
+                diag = diag + 1.0
+                continue
+            w = _edge_w(seed, i, j)
+            diag = diag + w
+            rows.append(r)
+            cols.append(_perm(j, n, window, h, seed, False))
+            vals.append(-w)
+        rows.append(r)
+        cols.append(r)
+        vals.append(diag)
+    A = sp.csr_matrix((vals, (rows, cols)), shape=(n, n))
+    A.sort_indices()
+    return A

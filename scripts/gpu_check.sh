@@ -22,6 +22,7 @@ for s in "$@"; do
         c4one) step bench_c4one 600 python bench.py --workload c4 --steps 10 --warmup 2 --no-cpu-baseline ;;
         dist1c4) step dist1c4 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 \
                   --master-addr 127.0.0.1 --master-port 29515 bench.py --dist --workload c4 --steps 5 --warmup 1 ;;
+        benchg) step bench_g 500 python bench.py --steps 20 --warmup 3 --no-cpu-baseline ;;
         smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
         bench) step bench 600 python bench.py --steps 20 --warmup 3 ;;
         benchq) step bench 400 python bench.py --steps 20 --warmup 3 --no-cpu-baseline --ab ;;

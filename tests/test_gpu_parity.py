@@ -858,3 +858,28 @@ def test_vcycle_256_storage_mix(ctx):
     assert it == it_o == 11
     floor = EPS * 12.0 * np.max(np.abs(H(x))) / np.max(np.abs(b))  # ||A||_inf = 12
     assert np.all(np.abs(hist - hist_o) <= 1e-8 * hist_o + floor), (hist, hist_o)
+
+
+@pytest.mark.parametrize("window", [-1, 0, 64])
+def test_random_7pt_generator_and_spmv(ctx, window):
+    """The general operator of roofline.general (random coefficients, symmetric
+    permutation) against its restatement, and its SpMV bitwise in both the
+    SELL (i32 / u16 columns, fp64 values) and the CSR-stream storage."""
+    import sa_oracle as SO
+    dims = (11, 9, 7)
+    A = fa().SparseMatOp.random7(ctx, *dims, seed=5, window=window)
+    R = SO.random_7pt(*dims, seed=5, window=window)
+    rp, ci, va = A.arrays()
+    assert np.array_equal(rp, R.indptr) and np.array_equal(ci, R.indices) and np.array_equal(va, R.data)
+    assert abs(R - R.T).max() == 0
+    if window != -1:
+        assert len(np.unique(R.tocoo().col - R.tocoo().row)) > 50  # no stencil structure
+    x = np.random.default_rng(3).standard_normal(R.shape[0])
+    OA = O.Csr.from_scipy(R)
+    for fmt in ("sell", "csr"):
+        fa().set_spmv_format(fmt)
+        try:
+            M = fa().SparseMatOp.random7(ctx, *dims, seed=5, window=window)
+        finally:
+            fa().set_spmv_format("auto")
+        assert np.array_equal(apply_dev(ctx, M, x, R.shape[0]), OA.spmv(x)), fmt
