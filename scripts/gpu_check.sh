@@ -23,6 +23,12 @@ for s in "$@"; do
         dist1c4) step dist1c4 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 \
                   --master-addr 127.0.0.1 --master-port 29515 bench.py --dist --workload c4 --steps 5 --warmup 1 ;;
         benchg) step bench_g 500 python bench.py --steps 20 --warmup 3 --no-cpu-baseline ;;
+        prof27) export TMPDIR=/tmp; R=$(pwd)
+              step prof27 600 rocprofv3 --kernel-trace --stats -d "$R/gpurun_out/prof27" -o run \
+                  --output-format csv -- python3 "$R/bench.py" --problem 27pt --smoother sgs --steps 10 --warmup 2 --no-cpu-baseline ;;
+        profelast) export TMPDIR=/tmp; R=$(pwd)
+              step profelast 600 rocprofv3 --kernel-trace --stats -d "$R/gpurun_out/profelast" -o run \
+                  --output-format csv -- python3 "$R/bench.py" --problem elast --steps 20 --warmup 3 --no-cpu-baseline ;;
         smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
         bench) step bench 600 python bench.py --steps 20 --warmup 3 ;;
         benchq) step bench 400 python bench.py --steps 20 --warmup 3 --no-cpu-baseline --ab ;;
