@@ -479,6 +479,19 @@ amg_status amg_sgs_ncolors(const amg_linop *op, int64_t *ncolors) {
     });
 }
 
+amg_status amg_sgs_info(const amg_linop *op, int64_t *info4) {
+    return guard([&] {
+        FAMG_REQUIRE(info4, AMG_ERR_INVALID, "null output");
+        auto p = std::dynamic_pointer_cast<SgsOp>(need(op).shared_from_this());
+        FAMG_REQUIRE(p, AMG_ERR_INVALID, "operator is not an SGS smoother");
+        const bool dia = p->Ap.has_dia() && p->Ap.dia_rowid;
+        info4[0] = p->ncolors;
+        info4[1] = dia ? SPMV_KERNEL_DIA : p->Ap.kernel;
+        info4[2] = dia ? p->Ap.dia_k : 0;
+        info4[3] = dia ? p->Ap.dia_vbits : 0;
+    });
+}
+
 amg_status amg_coarse_chol_create(const amg_linop *A, amg_linop **out) {
     return guard([&] {
         FAMG_REQUIRE(out, AMG_ERR_INVALID, "null output");

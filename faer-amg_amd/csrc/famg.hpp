@@ -65,6 +65,9 @@ struct GpuCsr {
     // DIA row range: the whole matrix (kernel == DIA) or one row segment
     // (dia_seg, e.g. the halo interior of a distributed level) beside SELL
     int64_t dia_r0 = 0, dia_r1 = 0, dia_seg = 0;
+    // set when the DIA codes describe a color-permuted SGS copy: stored row p
+    // is original row dia_rowid[p] (device array owned by the SgsOp)
+    const int32_t *dia_rowid = nullptr;
     // wave-per-row storage compression: 8/16-bit value codes (vec_codes, table
     // sell_vtab) and 16-bit column offsets from the row (vec_off)
     DevBuf<uint8_t> vec_codes;
@@ -103,6 +106,8 @@ extern int g_spmv_format_policy;
 extern int g_value_codes;
 enum SpmvKernel : int { SPMV_KERNEL_STREAM = 0, SPMV_KERNEL_SELL = 1, SPMV_KERNEL_VECTOR = 2, SPMV_KERNEL_DIA = 3 };
 void build_sell(GpuCsr &m, const std::vector<int64_t> &rp);
+// DIA codes of a color-permuted SGS copy (diagonals col - rowid[p]); true if built
+bool build_dia_sgs(GpuCsr &m, const int32_t *rowid);
 void choose_kernel(GpuCsr &m);
 // Host upload from usize-compatible arrays.
 void csr_from_host(GpuCsr &m, Ctx *ctx, int64_t nrows, int64_t ncols, const int64_t *rowptr,
@@ -302,8 +307,10 @@ struct MultigridOp : LinOp {
 // ---------------------------------------------------------------- factories
 
 // sa_build_box(smoother = SGS): levels whose greedy coloring needs more colors
-// than this get the L1 smoother instead
-constexpr int64_t SGS_MAX_COLORS = 32;
+// than this get the L1 smoother instead (each color is one launch over 1/C of
+// the rows: a dense Galerkin level with 20+ colors spent 1.6 ms of the 27-pt
+// 256^3 V-cycle in latency-bound color launches, profiles/r02)
+constexpr int64_t SGS_MAX_COLORS = 8;
 
 CsrPtr make_csr(Ctx *ctx);
 std::shared_ptr<DiagOp> make_jacobi(CsrOp &A, double omega);

@@ -242,6 +242,7 @@ std::shared_ptr<SgsOp> make_sgs(const CsrPtr &A, const int32_t *colors, bool val
     FAMG_CHECK_HIP(hipGetLastError());
     csr_finalize(op->Ap, &op->color_ptr);  // one row segment per color
     FAMG_REQUIRE(op->Ap.spmv_ready(), AMG_ERR_UNSUPPORTED, "sgs: nnz must be < 2^31");
+    build_dia_sgs(op->Ap, op->perm.get());  // constant-stencil operators: DIA codes for the sweeps
     op->e_.resize(n);
     return op;
 }

@@ -1034,6 +1034,55 @@ __global__ __launch_bounds__(256) void spmv_dia_kernel(DiaArgs a) {
     ep.store(a.e, sdt, acc0, acc1);
 }
 
+// One SGS color update with DIA codes of the color-permuted copy: stored row p
+// (one per lane, rows of one color contiguous) is original row i = rowid[p];
+// x[i] <- x[i] + d[p] (b[i] - sum_k a_k x[i + off_k]) in place (rows of one
+// color never couple).  Loads branch-free as in spmv_dia_kernel; padding
+// entries (code of +0.0) read a clamped in-range x and add exact zeros.
+template <int VB, int CW>
+__global__ __launch_bounds__(256) void spmv_dia_sgs_kernel(DiaArgs a, const int32_t *rowid) {
+    __shared__ double stab[VB == 4 ? 16 : 256];
+    const double tv = (int)threadIdx.x < a.ntab ? a.vtab[threadIdx.x] : 0.0;
+    const int blk = xcd_remap(blockIdx.x, gridDim.x);
+    const int p = a.row_begin + 256 * blk + (int)threadIdx.x;
+    const int pc = min(p, a.row_end - 1);
+    constexpr int KMAX = CW * 32 / VB < DIA_MAX ? CW * 32 / VB : DIA_MAX;
+    constexpr uint32_t MASK = (1u << VB) - 1;
+    uint32_t w[CW];
+    const uint32_t *cp = a.codes + (int64_t)(pc - a.code_row0) * CW;
+    if constexpr (CW == 1) {
+        w[0] = __builtin_nontemporal_load(cp);
+    } else if constexpr (CW == 2) {
+        const i32x2_t v = __builtin_nontemporal_load(reinterpret_cast<const i32x2_t *>(cp));
+        w[0] = (uint32_t)v.x;
+        w[1] = (uint32_t)v.y;
+    } else {
+#pragma unroll
+        for (int q = 0; q < CW / 4; q++) {
+            const i32x4_t v = __builtin_nontemporal_load(reinterpret_cast<const i32x4_t *>(cp) + q);
+#pragma unroll
+            for (int j = 0; j < 4; j++) w[4 * q + j] = (uint32_t)v[j];
+        }
+    }
+    const int i = rowid[pc];
+    const double xr = a.e.x[i], br = a.e.b[i], dr = a.e.d[pc];
+    double xv[KMAX];
+#pragma unroll
+    for (int k = 0; k < KMAX; k++) xv[k] = a.e.x[min(max(i + a.off[k], 0), a.ncols - 1)];
+    if ((int)threadIdx.x < a.ntab) stab[threadIdx.x] = tv;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+    if (p >= a.row_end) return;
+    double acc = 0.0;
+#pragma unroll
+    for (int k = 0; k < KMAX; k++) {
+        const double f = fma(stab[(w[(k * VB) >> 5] >> ((k * VB) & 31)) & MASK], xv[k], acc);
+        acc = k < a.k ? f : acc;
+    }
+    a.e.y[i] = xr + dr * (br - acc);
+}
+
 // SpMM: Y = A X for up to SPMM_KB columns per launch (column-major X, Y with
 // leading dimensions).  The slice is streamed once per column group; each
 // (row, column) sum keeps the SpMV's order (ascending steps, fma), so every
@@ -1421,12 +1470,15 @@ int64_t array_codes_u8(const double *v, int64_t n, Ctx &ctx, DevBuf<uint8_t> &co
 constexpr int DIA_SLOTS = 256;
 constexpr int DIA_EMPTY = INT32_MIN;
 
+// rowid (optional): stored row p is the original row rowid[p] (a color-permuted
+// SGS copy); offsets are taken against the original row
 __global__ __launch_bounds__(256) void k_dia_offsets(const int64_t *rp, const int32_t *col, int64_t r0, int64_t r1,
-                                                     int *slots, unsigned int *cnt) {
+                                                     const int32_t *rowid, int *slots, unsigned int *cnt) {
     const int64_t i = r0 + (int64_t)blockIdx.x * 256 + threadIdx.x;
     if (i >= r1) return;
+    const int64_t ri = rowid ? rowid[i] : i;
     for (int64_t e = rp[i]; e < rp[i + 1]; e++) {
-        const int64_t o64 = (int64_t)col[e] - i;
+        const int64_t o64 = (int64_t)col[e] - ri;
         if (o64 <= INT32_MIN / 2 || o64 >= INT32_MAX / 2) {
             atomicAdd(cnt, (unsigned)DIA_SLOTS);
             return;
@@ -1451,17 +1503,18 @@ __global__ __launch_bounds__(256) void k_dia_offsets(const int64_t *rp, const in
 
 // codes of row i (rows >= n: padding, all +0.0)
 __global__ __launch_bounds__(256) void k_dia_fill(const int64_t *rp, const int32_t *col, const double *val,
-                                                  int64_t r0, int64_t r1, int64_t nrows_alloc, DiaArgs off, int vb,
-                                                  int cw, const unsigned long long *tab, int ntab, int zero_code,
-                                                  uint32_t *codes) {
+                                                  int64_t r0, int64_t r1, int64_t nrows_alloc, const int32_t *rowid,
+                                                  DiaArgs off, int vb, int cw, const unsigned long long *tab, int ntab,
+                                                  int zero_code, uint32_t *codes) {
     const int64_t j = (int64_t)blockIdx.x * 256 + threadIdx.x;
     if (j >= nrows_alloc) return;
     const int64_t i = r0 + j;
     int c[DIA_MAX];
     for (int k = 0; k < off.k; k++) c[k] = zero_code;
     if (i < r1) {
+        const int64_t ri = rowid ? rowid[i] : i;
         for (int64_t e = rp[i]; e < rp[i + 1]; e++) {
-            const int o = (int)((int64_t)col[e] - i);
+            const int o = (int)((int64_t)col[e] - ri);
             int k = 0;
             while (off.off[k] != o) k++;
             const unsigned long long bits = (unsigned long long)__double_as_longlong(val[e]);
@@ -1486,7 +1539,7 @@ __global__ __launch_bounds__(256) void k_dia_fill(const int64_t *rp, const int32
 // rows, 4/8-bit value table, <= DIA_MAX diagonals filled to >= 80 %).  Returns
 // true if built.
 static bool build_dia(GpuCsr &m, int vb, const std::vector<unsigned long long> &tab,
-                      const std::vector<int64_t> &rp, int64_t r0, int64_t r1) {
+                      const std::vector<int64_t> &rp, int64_t r0, int64_t r1, const int32_t *rowid = nullptr) {
     const int64_t nr = r1 - r0;
     // a rectangular matrix qualifies only through a row segment (the halo
     // interior of a distributed level: [owned | ghost] columns); every stored
@@ -1502,7 +1555,7 @@ static bool build_dia(GpuCsr &m, int vb, const std::vector<unsigned long long> &
     FAMG_CHECK_HIP(hipMemcpyAsync(slots.get(), hs.data(), DIA_SLOTS * sizeof(int), hipMemcpyHostToDevice, s));
     FAMG_CHECK_HIP(hipMemsetAsync(cnt.get(), 0, sizeof(unsigned int), s));
     hipLaunchKernelGGL(k_dia_offsets, dim3((unsigned)ceil_div(nr, 256)), dim3(256), 0, s, m.rp64.get(),
-                       m.col.get(), r0, r1, slots.get(), cnt.get());
+                       m.col.get(), r0, r1, rowid, slots.get(), cnt.get());
     FAMG_CHECK_HIP(hipGetLastError());
     unsigned int c = 0;
     FAMG_CHECK_HIP(hipMemcpyAsync(hs.data(), slots.get(), DIA_SLOTS * sizeof(int), hipMemcpyDeviceToHost, s));
@@ -1527,7 +1580,7 @@ static bool build_dia(GpuCsr &m, int vb, const std::vector<unsigned long long> &
     m.dia_vtab.resize(tab.size());
     FAMG_CHECK_HIP(hipMemcpyAsync(m.dia_vtab.get(), tab.data(), tab.size() * sizeof(double), hipMemcpyHostToDevice, s));
     hipLaunchKernelGGL(k_dia_fill, dim3((unsigned)ceil_div(nalloc, 256)), dim3(256), 0, s, m.rp64.get(), m.col.get(),
-                       m.val.get(), r0, r1, nalloc, oa, vb, cw,
+                       m.val.get(), r0, r1, nalloc, rowid, oa, vb, cw,
                        reinterpret_cast<const unsigned long long *>(m.dia_vtab.get()), (int)tab.size(), zero_code,
                        m.dia_codes.get());
     FAMG_CHECK_HIP(hipGetLastError());
@@ -1539,6 +1592,30 @@ static bool build_dia(GpuCsr &m, int vb, const std::vector<unsigned long long> &
     m.dia_r1 = r1;
     m.dia_vbits = vb;
     m.dia_ntab = (int64_t)tab.size();
+    m.dia_rowid = rowid;
+    return true;
+}
+
+// DIA codes of a color-permuted SGS copy (rows grouped by color, columns in the
+// original numbering): diagonals are col - rowid[p].  Used only by the SGS
+// sweep; the copy's other storage stays as chosen.
+bool build_dia_sgs(GpuCsr &m, const int32_t *rowid) {
+    if (g_spmv_format_policy != 0 || !g_value_codes || m.nrows == 0 || m.nrows != m.ncols) return false;
+    std::vector<int64_t> rp(m.nrows + 1);
+    FAMG_CHECK_HIP(hipMemcpyAsync(rp.data(), m.rp64.get(), (m.nrows + 1) * sizeof(int64_t), hipMemcpyDeviceToHost,
+                                  m.ctx->stream));
+    FAMG_CHECK_HIP(hipStreamSynchronize(m.ctx->stream));
+    std::vector<unsigned long long> tab;
+    const int vb = value_table(m, tab);
+    DevBuf<uint32_t> keep_codes = std::move(m.dia_codes);  // a segment DIA the finalize may have built
+    DevBuf<double> keep_tab = std::move(m.dia_vtab);
+    if (!build_dia(m, vb, tab, rp, 0, m.nrows, rowid)) {
+        m.dia_codes = std::move(keep_codes);
+        m.dia_vtab = std::move(keep_tab);
+        m.dia_rowid = nullptr;
+        return false;
+    }
+    m.dia_seg = -2;  // not a row segment of the plain SpMV
     return true;
 }
 
@@ -1554,6 +1631,7 @@ void build_sell(GpuCsr &m, const std::vector<int64_t> &rp) {
     m.dia_ntab = 0;
     m.dia_k = m.dia_cw = m.dia_vbits = 0;
     m.dia_r0 = m.dia_r1 = m.dia_seg = 0;
+    m.dia_rowid = nullptr;
     m.dia_off.clear();
     m.nslices = m.sell_steps = m.sell_bytes = m.sell_ntab = 0;
     m.sell_vbits = 0;
@@ -1721,7 +1799,7 @@ static void build_vec_codes(GpuCsr &m) {
 }
 
 void choose_kernel(GpuCsr &m) {
-    if (m.has_dia() && m.dia_r0 == 0 && m.dia_r1 == m.nrows) m.kernel = SPMV_KERNEL_DIA;
+    if (m.has_dia() && !m.dia_rowid && m.dia_r0 == 0 && m.dia_r1 == m.nrows) m.kernel = SPMV_KERNEL_DIA;
     else if (m.has_sell()) m.kernel = SPMV_KERNEL_SELL;
     else if (g_spmv_format_policy == 3 ||
              (g_spmv_format_policy == 0 && m.nrows > 0 && m.nnz >= vec_min_avg() * m.nrows)) {
@@ -1786,10 +1864,40 @@ void spmv(const GpuCsr &m, const double *x, double *y, SpmvMode mode, const Spmv
     FAMG_REQUIRE(mode != SPMV_SGS || epi.perm, AMG_ERR_INVALID, "SGS mode needs a permutation");
     Epi e{x, y, epi.b, epi.d, epi.perm, epi.dc, epi.dt};
     const dim3 block(256);
+    if (mode == SPMV_SGS && m.has_dia() && m.dia_rowid) {  // color sweep of a color-permuted copy
+        FAMG_REQUIRE(epi.perm == m.dia_rowid, AMG_ERR_INVALID, "SGS DIA: permutation mismatch");
+        const int64_t r0 = seg < 0 ? 0 : m.seg_rows[seg];
+        const int64_t r1 = seg < 0 ? m.nrows : m.seg_rows[seg + 1];
+        if (r1 <= r0) return;
+        DiaArgs a{};
+        a.codes = m.dia_codes.get();
+        a.ntab = (int32_t)m.dia_ntab;
+        a.k = m.dia_k;
+        a.row_begin = (int32_t)r0;
+        a.row_end = (int32_t)r1;
+        a.ncols = (int32_t)m.ncols;
+        a.code_row0 = (int32_t)m.dia_r0;
+        a.vtab = m.dia_vtab.get();
+        for (int k = 0; k < m.dia_k; k++) a.off[k] = m.dia_off[k];
+        a.e = e;
+        const dim3 grid((unsigned)ceil_div(r1 - r0, 256));
+        switch (m.dia_vbits * 16 + m.dia_cw) {
+        case 4 * 16 + 1: spmv_dia_sgs_kernel<4, 1><<<grid, block, 0, s>>>(a, m.dia_rowid); break;
+        case 4 * 16 + 2: spmv_dia_sgs_kernel<4, 2><<<grid, block, 0, s>>>(a, m.dia_rowid); break;
+        case 4 * 16 + 4: spmv_dia_sgs_kernel<4, 4><<<grid, block, 0, s>>>(a, m.dia_rowid); break;
+        case 8 * 16 + 1: spmv_dia_sgs_kernel<8, 1><<<grid, block, 0, s>>>(a, m.dia_rowid); break;
+        case 8 * 16 + 2: spmv_dia_sgs_kernel<8, 2><<<grid, block, 0, s>>>(a, m.dia_rowid); break;
+        case 8 * 16 + 4: spmv_dia_sgs_kernel<8, 4><<<grid, block, 0, s>>>(a, m.dia_rowid); break;
+        case 8 * 16 + 8: spmv_dia_sgs_kernel<8, 8><<<grid, block, 0, s>>>(a, m.dia_rowid); break;
+        default: fail(AMG_ERR_INVALID, "SGS DIA: unsupported code layout");
+        }
+        FAMG_CHECK_HIP(hipGetLastError());
+        return;
+    }
     // a DIA row segment (the halo interior of a distributed level) runs DIA
     // even when the rest of the matrix is SELL storage
     if (m.kernel == SPMV_KERNEL_DIA ||
-        (m.has_dia() && seg >= 0 && seg == m.dia_seg && mode != SPMV_SGS)) {
+        (m.has_dia() && !m.dia_rowid && seg >= 0 && seg == m.dia_seg && mode != SPMV_SGS)) {
         FAMG_REQUIRE(mode != SPMV_SGS, AMG_ERR_UNSUPPORTED, "DIA storage has no SGS sweep");
         const int64_t r0 = seg < 0 ? 0 : m.seg_rows[seg];
         const int64_t r1 = seg < 0 ? m.nrows : m.seg_rows[seg + 1];

@@ -75,6 +75,7 @@ SIGNATURES = {
     "amg_diag_create": (i32, [vp, i64, vp, P(vp)]),
     "amg_sgs_create": (i32, [vp, vp, P(vp)]),
     "amg_sgs_ncolors": (i32, [vp, P(i64)]),
+    "amg_sgs_info": (i32, [vp, vp]),
     "amg_coarse_chol_create": (i32, [vp, P(vp)]),
     "amg_multigrid_create": (i32, [vp, vp, P(vp)]),
     "amg_multigrid_add_level": (i32, [vp, vp, vp, vp, vp]),
@@ -462,6 +463,17 @@ class SymGaussSeidel(LinOp):
         v = i64()
         _ck(_lib.amg_sgs_ncolors(self.h, C.byref(v)))
         return v.value
+
+    def sweep_storage(self):
+        """{'colors', 'kernel' ('sell', 'dia', ...), 'diagonals', 'bits'} of the color sweeps."""
+        return sgs_info(self)
+
+
+def sgs_info(S):
+    info = np.zeros(4, np.int64)
+    _ck(_lib.amg_sgs_info(S.h, info.ctypes.data_as(vp)))
+    return {"colors": int(info[0]), "kernel": ("csr-stream", "sell", "vector", "dia")[int(info[1])],
+            "diagonals": int(info[2]), "bits": int(info[3])}
 
 
 def CoarseCholesky(A):

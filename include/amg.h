@@ -191,6 +191,9 @@ amg_status amg_diag_create(amg_ctx *ctx, int64_t n, const double *d, amg_linop *
 amg_status amg_sgs_create(const amg_linop *A, const int32_t *colors, amg_linop **out);
 /* Number of colors of an SGS smoother. */
 amg_status amg_sgs_ncolors(const amg_linop *op, int64_t *ncolors);
+/* Storage of the color sweeps: info4 = {colors, kernel (as amg_csr_spmv_info:
+ * 1 SELL, 3 DIA codes of the color-permuted copy, ...), diagonals, code bits}. */
+amg_status amg_sgs_info(const amg_linop *op, int64_t *info4);
 /* CoarseSolverKind::Cholesky (coarse_solvers.rs:21-33, SparseCholeskySolve
  * :172-181): exact coarse solve.  Returns AMG_ERR_NOT_SPD if A is not SPD and
  * AMG_ERR_UNSUPPORTED above 16384 rows (dense factor). */
