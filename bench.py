@@ -262,12 +262,33 @@ def workload_name(args, dims):
             f"MIS aggregates, block-Jacobi P smoothing, {args.smoother} s=1 mu=1, Cholesky coarsest")
 
 
+def sgs_sweep_bytes(S, A, n, launches):
+    """Algorithmic bytes of `launches` color updates of a multicolor SGS sweep
+    (DESIGN.md 5): per launch over the n_c = n / C rows of one color, that
+    color's share of the sweep storage (DIA codes of the color-permuted copy,
+    or its SELL bytes), perm + d + b (20 B), x read and written (16 B) per row,
+    and the other colors' x entries the rows gather (8 (n - n_c))."""
+    import faer_amg_amd as fa
+    st = fa.sgs_info(S)
+    C = st["colors"]
+    if st["kernel"] == "dia":
+        cw = 1
+        while 32 * cw < st["diagonals"] * st["bits"]:
+            cw *= 2
+        sweep = 4 * cw * n
+    else:
+        sweep = A.spmv_info()["stream_bytes"]
+    nc = n / C
+    return launches * (sweep / C + 36 * nc + 8 * (n - nc)), C
+
+
 def vcycle_bytes(mg, csr=False, fold=True):
     """Algorithmic bytes of one V-cycle (s = 1, mu = 1, zero initial guess) from the
     per-kernel formulas of SURVEY.md 8(d); matrix bytes of the chosen storage
     (csr=False) or of 32-bit CSR (csr=True).  fold: diagonal smoothers fold the
     first smoothing step v = d f into the residual (reads f, d; writes r) and the
-    correction (reads d, f, P, v_c; writes v) -- no separate 24n pass."""
+    correction (reads d, f, P, v_c; writes v) -- no separate 24n pass.  SGS
+    levels count their 2C - 1 color launches per smoothing step (sgs_sweep_bytes)."""
     def mat(M):
         return 12 * M.nnz + 4 * (M.nrows + 1) if csr else M.spmv_info()["stream_bytes"]
     tot = 0
@@ -281,12 +302,20 @@ def vcycle_bytes(mg, csr=False, fold=True):
             continue
         bA = mat(A)
         nc = R.nrows
-        # the library folds only diagonal smoothers on fp64-valued SELL storage
         info = A.spmv_info()
-        fold = fold_all and S.kind == "diag" and info["kernel"] == "sell" and info["value_bits"] == 0
-        tot += 0 if fold else 24 * n                   # first smoothing step from 0
         tot += bA + 24 * n                             # residual
         tot += mat(R) + 8 * n + 8 * nc                 # restrict
+        if S.kind == "sgs":
+            pre, C = sgs_sweep_bytes(S, A, n, 1)
+            post, _ = sgs_sweep_bytes(S, A, n, 2 * C - 1)
+            tot += 8 * n + (2 * C - 2) * pre + 28 * n / C  # e = 0, first color e = d r, 2C - 2 launches
+            tot += mat(P) + 8 * nc + 16 * n           # interpolate + add
+            tot += post                                # post-smoothing sweep on x
+            continue
+        # the library folds only diagonal smoothers on fp64-valued SELL storage
+        fold = (fold_all and S.kind == "diag" and info["kernel"] == "sell" and info["value_bits"] == 0
+                and 2 * info["slices_i32"] < info["slices"])
+        tot += 0 if fold else 24 * n                   # first smoothing step from 0
         tot += mat(P) + 8 * nc + (24 if fold else 16) * n  # interpolate + add
         tot += bA + 32 * n                             # post-smoothing Jacobi
     return tot

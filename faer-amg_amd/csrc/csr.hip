@@ -80,6 +80,16 @@ void csr_finalize(GpuCsr &m, const std::vector<int64_t> *segments) {
                                   hipMemcpyHostToDevice, ctx.stream));
     FAMG_CHECK_HIP(hipStreamSynchronize(ctx.stream));
     build_sell(m, rp);
+    const bool dia_all = m.has_dia() && m.dia_r0 == 0 && m.dia_r1 == m.nrows;
+    const int64_t sell_b = m.sell_bytes + 12 * (m.nslices + 1) + 4 * m.sell_steps + 8 * m.sell_ntab;
+    if (!dia_all && build_bsr(m, rp, m.has_sell() ? sell_b : m.index_bytes())) {
+        // the block storage replaces the SELL copy (release its HBM)
+        m.sell_row0.release(); m.sell_soff.release(); m.sell_desc.release(); m.sell_base.release();
+        m.sell_data.release(); m.sell_vtab.release();
+        m.nslices = m.sell_steps = m.sell_bytes = m.sell_ntab = 0;
+        m.sell_vbits = 0;
+        m.sell_mode_slices[0] = m.sell_mode_slices[1] = m.sell_mode_slices[2] = 0;
+    }
     choose_kernel(m);
 }
 

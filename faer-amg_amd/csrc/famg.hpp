@@ -20,6 +20,15 @@
 
 namespace famg {
 
+// Workgroup b of nb -> the b-th of a contiguous range per XCD (consecutive
+// workgroups round-robin over the 8 XCDs, each with its own L2): each XCD then
+// walks a contiguous slab of rows and keeps its x window in its L2.
+__device__ __forceinline__ int xcd_remap(int b, int nb) {
+    const int q = nb >> 3, r = nb & 7;
+    const int x = b & 7, idx = b >> 3;
+    return x * q + min(x, r) + idx;
+}
+
 // ------------------------------------------------------------------ CSR data
 
 // A CSR matrix resident on the device.  rp64 (int64 row pointers) always
@@ -74,14 +83,22 @@ struct GpuCsr {
     DevBuf<int16_t> vec_off;
     int vec_vbits = 0;
     bool vec_o16 = false;
+    // 3x3 block storage (bsr.hip): node-row slices, one 4864-B unit per block step
+    DevBuf<char> bsr_data;
+    DevBuf<int32_t> bsr_row0, bsr_soff;
+    int64_t bsr_slices = 0, bsr_steps = 0;
+    std::vector<int64_t> bsr_seg_slc;
+    bool no_bsr = false;  // e.g. a color-permuted SGS copy
     int kernel = 0;  // SpmvKernel chosen at finalize
     bool spmv_ready() const { return rp32.get() != nullptr && sched.get() != nullptr; }
     bool has_sell() const { return sell_desc.get() != nullptr; }
     bool has_dia() const { return dia_codes.get() != nullptr; }
+    bool has_bsr() const { return bsr_data.get() != nullptr; }
     int64_t index_bytes() const { return 12 * nnz + 4 * (nrows + 1); }
     // matrix bytes one SpMV streams with the chosen kernel (data + metadata)
     int64_t stream_bytes() const {
         if (kernel == 3) return 4 * dia_cw * nrows + 8 * dia_ntab;
+        if (kernel == 4) return bsr_steps * (64 * 76) + 8 * (bsr_slices + 1);
         if (kernel == 2)
             return nnz * ((vec_vbits ? vec_vbits / 8 : 8) + (vec_o16 ? 2 : 4)) + 4 * (nrows + 1) + 8 * sell_ntab;
         return kernel == 1 ? sell_bytes + 12 * (nslices + 1) + 4 * sell_steps + 8 * sell_ntab : index_bytes();
@@ -104,7 +121,12 @@ extern int g_spmv_format_policy;
 // Value codes for SELL matrices finalized afterwards (1 = when <= 65536
 // distinct values, 0 = always fp64 values)
 extern int g_value_codes;
-enum SpmvKernel : int { SPMV_KERNEL_STREAM = 0, SPMV_KERNEL_SELL = 1, SPMV_KERNEL_VECTOR = 2, SPMV_KERNEL_DIA = 3 };
+enum SpmvKernel : int {
+    SPMV_KERNEL_STREAM = 0, SPMV_KERNEL_SELL = 1, SPMV_KERNEL_VECTOR = 2, SPMV_KERNEL_DIA = 3, SPMV_KERNEL_BSR = 4
+};
+// 3x3 block storage when the matrix is blocked and it streams fewer bytes than
+// other_bytes; true if built (bsr.hip)
+bool build_bsr(GpuCsr &m, const std::vector<int64_t> &rp, int64_t other_bytes);
 void build_sell(GpuCsr &m, const std::vector<int64_t> &rp);
 // DIA codes of a color-permuted SGS copy (diagonals col - rowid[p]); true if built
 bool build_dia_sgs(GpuCsr &m, const int32_t *rowid);
@@ -145,6 +167,8 @@ struct SpmvEpi {
 void spmm(const GpuCsr &m, const double *x, int64_t ldx, double *y, int64_t ldy, int64_t k, hipStream_t s);
 void spmv(const GpuCsr &m, const double *x, double *y, SpmvMode mode, const SpmvEpi &epi,
           hipStream_t s, int64_t seg = -1);
+void spmv_bsr(const GpuCsr &m, const double *x, double *y, SpmvMode mode, const SpmvEpi &epi, hipStream_t s,
+              int64_t seg);
 
 // BLAS-1 (n-vectors, device pointers)
 void vec_fill(double *x, double v, int64_t n, hipStream_t s);

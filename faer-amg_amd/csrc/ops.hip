@@ -234,6 +234,7 @@ std::shared_ptr<SgsOp> make_sgs(const CsrPtr &A, const int32_t *colors, bool val
     const int64_t nnz = scan_counts(cnt.get(), prp.get(), n, *ctx);
     csr_alloc(op->Ap, ctx, n, n, nnz);
     op->Ap.rp64 = std::move(prp);
+    op->Ap.no_bsr = true;  // swept in SGS mode only
     op->dinv.resize(n);
     if (n)
         hipLaunchKernelGGL(k_perm_rows, dim3(g), dim3(256), 0, s, A->m.rp64.get(), A->m.col.get(),
@@ -481,8 +482,12 @@ void MultigridOp::cycle(int64_t l, double *v, const double *f, bool v_zero, doub
     // DIA storage folds only on request (FAMG_FOLD_DIA=1): the residual then
     // gathers d beside x (139 us vs 105 + 49 for RESID + the d*f pass) but the
     // correction's d*f epilogue on P_0 cost as much (153 vs 122 us).
+    // Not where most slices carry 32-bit columns (unstructured operators): the
+    // residual then gathers d as randomly as x, and that doubled gather cost more
+    // than the pass it saves (Q1 elasticity 1.57M rows: 640 vs 388 + 15 us).
+    const bool gather_cheap = A && 2 * A->m.sell_mode_slices[2] < A->m.nslices;
     const bool fold = fold_zero_guess && v_zero && steps == 1 && A && D && P &&
-                      ((A->m.kernel == SPMV_KERNEL_SELL && A->m.sell_vbits == 0) ||
+                      ((A->m.kernel == SPMV_KERNEL_SELL && A->m.sell_vbits == 0 && gather_cheap) ||
                        (A->m.kernel == SPMV_KERNEL_DIA && fold_dia_enabled()));
     if (fold) {
         SpmvEpi epi;

@@ -66,11 +66,6 @@ static int64_t vec_min_avg() {
 }
 constexpr int64_t SELL_PAIR_MIN_SLICES = 1;  // pairing paid on every level measured (A_2: 55 vs 60 us)
 
-__device__ __forceinline__ int xcd_remap(int b, int nb) {
-    const int q = nb >> 3, r = nb & 7;
-    const int x = b & 7, idx = b >> 3;
-    return x * q + min(x, r) + idx;
-}
 
 struct Epi {
     const double *x;
@@ -1800,6 +1795,7 @@ static void build_vec_codes(GpuCsr &m) {
 
 void choose_kernel(GpuCsr &m) {
     if (m.has_dia() && !m.dia_rowid && m.dia_r0 == 0 && m.dia_r1 == m.nrows) m.kernel = SPMV_KERNEL_DIA;
+    else if (m.has_bsr()) m.kernel = SPMV_KERNEL_BSR;
     else if (m.has_sell()) m.kernel = SPMV_KERNEL_SELL;
     else if (g_spmv_format_policy == 3 ||
              (g_spmv_format_policy == 0 && m.nrows > 0 && m.nnz >= vec_min_avg() * m.nrows)) {
@@ -1864,6 +1860,11 @@ void spmv(const GpuCsr &m, const double *x, double *y, SpmvMode mode, const Spmv
     FAMG_REQUIRE(mode != SPMV_SGS || epi.perm, AMG_ERR_INVALID, "SGS mode needs a permutation");
     Epi e{x, y, epi.b, epi.d, epi.perm, epi.dc, epi.dt};
     const dim3 block(256);
+    if (m.kernel == SPMV_KERNEL_BSR) {
+        FAMG_REQUIRE(mode != SPMV_SGS, AMG_ERR_UNSUPPORTED, "block storage has no SGS sweep");
+        spmv_bsr(m, x, y, mode, epi, s, seg);
+        return;
+    }
     if (mode == SPMV_SGS && m.has_dia() && m.dia_rowid) {  // color sweep of a color-permuted copy
         FAMG_REQUIRE(epi.perm == m.dia_rowid, AMG_ERR_INVALID, "SGS DIA: permutation mismatch");
         const int64_t r0 = seg < 0 ? 0 : m.seg_rows[seg];

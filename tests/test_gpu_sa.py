@@ -205,3 +205,55 @@ def test_sa_scalar_random_candidates(ctx):
     mg.apply(z, bd)
     ctx.synchronize()
     assert np.linalg.norm(z.cpu().numpy() - zref) <= 1e-11 * np.linalg.norm(zref)
+
+
+@pytest.mark.parametrize("gap", [False, True])
+def test_bsr_storage_bitwise(ctx, gap):
+    """3x3 block storage: picked for the elasticity operator and its SA levels,
+    SpMV bitwise equal to the oracle's CSR row sums (blocks summed in ascending
+    column order), V-cycle bitwise equal to the same hierarchy with the block
+    storage disabled (FAMG_NO_BSR is read at first use: compared through a
+    CSR-only copy instead).  gap: explicit entries removed from blocks (partly
+    filled blocks carry zeros)."""
+    import torch
+    H = fa().elasticity_q1((9, 8, 8), seed=5)
+    S = H.to_scipy().tocsr()
+    if gap:  # drop ~10% of the off-diagonal entries (keeps symmetry, blocks partly filled)
+        C = S.tocoo()
+        keep = (C.row == C.col) | (((C.row // 3 * 7 + C.col // 3 * 7) % 10) != 0)
+        S = sp.csr_matrix((C.data[keep], (C.row[keep], C.col[keep])), shape=S.shape)
+        S.sort_indices()
+    A = fa().SparseMatOp.from_scipy(ctx, S)
+    info = A.spmv_info()
+    assert info["kernel"] == "bsr", info
+    assert info["stream_bytes"] < 12 * S.nnz
+    OA = O.Csr.from_scipy(S)
+    x = np.random.default_rng(2).standard_normal(S.shape[0])
+    xd = torch.as_tensor(x, device="cuda:0")
+    yd = torch.empty_like(xd)
+    A.apply(yd, xd)
+    ctx.synchronize()
+    assert np.array_equal(yd.cpu().numpy(), OA.spmv(x))
+    nn = fa().constant_candidates(S.shape[0], 3)
+    w = weights(S, nn)
+    mg = fa().smoothed_aggregation(A, nn, weights=w, block_size=3, candidate_dimension=3, coarsest_dim=150,
+                                   smoother="l1")
+    kinds = [mg.level(l)[0].spmv_info()["kernel"] for l in range(mg.levels() - 1)]
+    assert kinds[0] == "bsr"
+    fa().set_spmv_format("csr")
+    try:
+        Ac = fa().SparseMatOp.from_scipy(ctx, S)
+        mgc = fa().smoothed_aggregation(Ac, nn, weights=w, block_size=3, candidate_dimension=3, coarsest_dim=150,
+                                        smoother="l1")
+    finally:
+        fa().set_spmv_format("auto")
+    b = torch.as_tensor(np.random.default_rng(3).uniform(-1, 1, S.shape[0]), device="cuda:0")
+    z1, z2 = torch.empty_like(b), torch.empty_like(b)
+    mg.apply(z1, b)
+    mgc.apply(z2, b)
+    ctx.synchronize()
+    # CSR-stream splits long rows over lanes: equal to rounding, not bitwise
+    assert float(torch.linalg.norm(z1 - z2)) <= 1e-13 * float(torch.linalg.norm(z2))
+    levels = oracle_levels(mg, "l1")
+    zref = O.Multigrid(levels).apply(b.cpu().numpy())
+    assert np.linalg.norm(z1.cpu().numpy() - zref) <= 1e-11 * np.linalg.norm(zref)
