@@ -40,6 +40,14 @@ bool g_alloc_debug = [] {
 }();
 // DIA storage: FAMG_DIA_NT=1 streams the epilogue operands (b, d, y) with
 // non-temporal accesses (A/B switch; results are bitwise equal).
+// FAMG_DIA_BANDS=0 turns the 2.5-D (plane-band per XCD) block order off
+static bool dia_bands() {
+    static const bool on = [] {
+        const char *e = getenv("FAMG_DIA_BANDS");
+        return !(e && e[0] == '0');
+    }();
+    return on;
+}
 static bool dia_nt() {
     static const bool on = [] {
         const char *e = getenv("FAMG_DIA_NT");
@@ -879,6 +887,7 @@ struct DiaArgs {
     const double *vtab;
     int32_t ntab, k, row_begin, row_end, ncols;
     int32_t code_row0;  // first row with codes (the DIA row range may be one segment)
+    int32_t band_bp;    // > 0: 512-row blocks per plane; XCD x walks band x of every plane
     int32_t off[DIA_MAX];
     Epi e;
 };
@@ -1000,7 +1009,16 @@ __global__ __launch_bounds__(256) void spmv_dia_kernel(DiaArgs a) {
     const double tv = (int)threadIdx.x < a.ntab ? a.vtab[threadIdx.x] : 0.0;
     double dv = 0.0;
     if constexpr (DC) dv = a.e.dt[threadIdx.x];
-    const int blk = xcd_remap(blockIdx.x, gridDim.x);
+    int blk;
+    if (a.band_bp > 0) {
+        // 2.5-D order: XCD x takes band x (1/8 of the rows) of every plane in
+        // turn, so its x window is three plane bands (768 KB at 512^2 planes),
+        // not three whole planes (6 MB > its 4 MB L2)
+        const int bb = a.band_bp >> 3, x = blockIdx.x & 7, i = blockIdx.x >> 3;
+        blk = (i / bb) * a.band_bp + x * bb + (i % bb);
+    } else {
+        blk = xcd_remap(blockIdx.x, gridDim.x);
+    }
     const int row = a.row_begin + 512 * blk + 2 * (int)threadIdx.x;
     constexpr int KMAX = CW * 32 / VB < DIA_MAX ? CW * 32 / VB : DIA_MAX;
     constexpr uint32_t MASK = (1u << VB) - 1;
@@ -1914,6 +1932,12 @@ void spmv(const GpuCsr &m, const double *x, double *y, SpmvMode mode, const Spmv
         a.vtab = m.dia_vtab.get();
         for (int k = 0; k < m.dia_k; k++) a.off[k] = m.dia_off[k];
         a.e = e;
+        a.band_bp = 0;
+        {  // plane = the largest diagonal offset (a 3-D stencil's z neighbour)
+            const int64_t plane = std::max<int64_t>(std::abs((int64_t)m.dia_off.front()), std::abs((int64_t)m.dia_off.back()));
+            if (dia_bands() && plane % 4096 == 0 && plane >= 8 * 4096 && (r1 - r0) % plane == 0)
+                a.band_bp = (int32_t)(plane / 512);
+        }
         const dim3 grid((unsigned)ceil_div(r1 - r0, 512));
         const int key = m.dia_vbits * 16 + m.dia_cw;
         const bool nt = dia_nt();
