@@ -664,8 +664,11 @@ def main():
     ap.add_argument("--elements", type=int, default=80, help="elast: elements per edge (80: 1.57M rows)")
     ap.add_argument("--mtx", default=None, help="mtx: path of a Matrix Market file")
     ap.add_argument("--block-size", type=int, default=3, help="elast/mtx: dofs per node")
-    ap.add_argument("--agglomerate", type=int, default=8192,
-                    help="levels with fewer global rows run redundantly on every rank")
+    ap.add_argument("--agglomerate", type=int, default=None,
+                    help="levels with fewer global rows run redundantly on every rank "
+                         "(default 16384 x world: a level is distributed while every rank owns "
+                         ">= 16K of its rows; below that its halo exchanges cost more than the "
+                         "redundant cycle)")
     ap.add_argument("--cpu-threads", type=int, default=int(os.environ.get("OMP_NUM_THREADS", "16")))
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=20.0,
@@ -685,6 +688,8 @@ def main():
     ap.add_argument("--dist", action="store_true",
                     help="distributed path even at world size 1 (1-rank RCCL; a check of run_dist)")
     args = ap.parse_args()
+    if args.agglomerate is None:
+        args.agglomerate = 16384 * max(1, int(os.environ.get("WORLD_SIZE", "1")))
     if args.smoother is None:
         args.smoother = {"7pt": "jacobi", "27pt": "sgs"}.get(args.problem, "l1")
     if args.problem == "mtx" and not args.mtx:

@@ -42,6 +42,7 @@ for s in "$@"; do
         pstream) step pstream 300 python scripts/placement_stream.py ;;
         placement) FAMG_ALLOC_DEBUG=1 step placement 300 python scripts/placement.py ;;
         bench27) step bench27 600 python bench.py --problem 27pt --smoother sgs --steps 10 --warmup 2 --no-cpu-baseline ;;
+        bench27p) step bench27p 900 python bench.py --problem 27pt --smoother sgs --steps 10 --warmup 2 --cpu-budget 4 --no-general ;;
         bench512) step bench512 600 python bench.py --edge 512 --steps 5 --warmup 1 --no-cpu-baseline ;;
         benchblock) step benchblock 600 python bench.py --smoother block --steps 10 --warmup 2 --no-cpu-baseline ;;
         pmc) export TMPDIR=/tmp; R=$(pwd)
