@@ -7,7 +7,9 @@
 // (u_e from splitmix64(seed, e), so the operator has as many distinct values as
 // elements), Poisson ratio nu, the nodes of the x = 0 face clamped (their rows
 // and columns removed), and the free nodes optionally renumbered by a seeded
-// random permutation so the sparsity pattern has no stencil structure.  Dofs
+// random permutation (permute = 1: over all nodes; permute = W >= 2: within
+// consecutive windows of W nodes, the locality of a mesh numbering) so the
+// sparsity pattern has no stencil structure.  Dofs
 // are interleaved per node (3p + c), the reference's block_size = 3 layout.
 // Element matrices: 2x2x2 Gauss quadrature of B^T D B on the unit cube;
 // assembly sums element contributions in ascending element order.
@@ -91,13 +93,18 @@ extern "C" amg_status amg_gen_elasticity_q1(int64_t ex, int64_t ey, int64_t ez, 
             for (int64_t z = 0; z < nz; z++)
                 for (int64_t y = 0; y < ny; y++)
                     for (int64_t x = 1; x < nx; x++) id[x + nx * (y + ny * z)] = k++;
-            if (permute) {  // Fisher-Yates on the ids, splitmix64 stream
+            if (permute) {  // Fisher-Yates on the ids (within windows), splitmix64 stream
+                const int64_t W = permute == 1 ? nfree : permute;
                 std::vector<int64_t> perm(nfree);
                 for (int64_t i = 0; i < nfree; i++) perm[i] = i;
-                for (int64_t i = nfree - 1; i > 0; i--) {
-                    const uint64_t r = splitmix64(seed ^ 0xA5A5A5A5ull) ^ splitmix64(seed + 7 * (uint64_t)i);
-                    const int64_t j = (int64_t)(r % (uint64_t)(i + 1));
-                    std::swap(perm[i], perm[j]);
+                for (int64_t w0 = 0; w0 < nfree; w0 += W) {
+                    const int64_t m = std::min<int64_t>(W, nfree - w0);
+                    for (int64_t i = m - 1; i > 0; i--) {
+                        const uint64_t r =
+                            splitmix64(seed ^ 0xA5A5A5A5ull) ^ splitmix64(seed + 7 * (uint64_t)(w0 + i));
+                        const int64_t j = (int64_t)(r % (uint64_t)(i + 1));
+                        std::swap(perm[w0 + i], perm[w0 + j]);
+                    }
                 }
                 for (auto &v : id)
                     if (v >= 0) v = perm[v];

@@ -694,10 +694,12 @@ def nn_postprocess(A, x, iters=3):
 
 
 def elasticity_q1(elements, contrast=1.0, nu=0.3, seed=42, permute=True):
-    """Host CSR of the C5 stand-in: Q1 hex elasticity, block size 3 (gen.cpp)."""
+    """Host CSR of the C5 stand-in: Q1 hex elasticity, block size 3 (gen.cpp).
+    permute: False none, True over all nodes, an int W >= 2 within windows of W nodes."""
     ex, ey, ez = elements
+    mode = 0 if permute is False else 1 if permute is True else int(permute)
     h = vp()
-    _ck(_lib.amg_gen_elasticity_q1(ex, ey, ez, contrast, nu, seed, 1 if permute else 0, C.byref(h)))
+    _ck(_lib.amg_gen_elasticity_q1(ex, ey, ez, contrast, nu, seed, mode, C.byref(h)))
     return HostCsr(h)
 
 

@@ -147,7 +147,8 @@ amg_status amg_gen_random_7pt(amg_ctx *ctx, int64_t nx, int64_t ny, int64_t nz, 
  * hexahedral linear elasticity on an ex x ey x ez element box, per-element
  * Young's modulus 10^(contrast (2u - 1)) (u ~ U[0,1) from splitmix64(seed)),
  * Poisson ratio nu, the x = 0 face clamped, free nodes renumbered by a seeded
- * random permutation when permute != 0; 3 dofs per node interleaved
+ * random permutation (permute 0: none, 1: over all nodes, W >= 2: within
+ * consecutive windows of W nodes); 3 dofs per node interleaved
  * (block_size 3).  Host CSR (upload with amg_host_csr_upload). */
 amg_status amg_gen_elasticity_q1(int64_t ex, int64_t ey, int64_t ez, double contrast, double nu,
                                  uint64_t seed, int32_t permute, amg_host_csr **out);

@@ -76,13 +76,16 @@ def elasticity_q1(ex, ey, ez, contrast=1.0, nu=0.3, seed=42, permute=True):
                 ids[x + nx * (y + ny * z)] = k
                 k += 1
     if permute:
+        W = nfree if permute is True or permute == 1 else int(permute)
         perm = list(range(nfree))
         M = (1 << 64) - 1
         a = _splitmix64(seed ^ 0xA5A5A5A5)
-        for i in range(nfree - 1, 0, -1):
-            r = a ^ _splitmix64((seed + 7 * i) & M)
-            j = r % (i + 1)
-            perm[i], perm[j] = perm[j], perm[i]
+        for w0 in range(0, nfree, W):
+            m = min(W, nfree - w0)
+            for i in range(m - 1, 0, -1):
+                r = a ^ _splitmix64((seed + 7 * (w0 + i)) & M)
+                j = r % (i + 1)
+                perm[w0 + i], perm[w0 + j] = perm[w0 + j], perm[w0 + i]
         perm = np.array(perm)
         ids = np.where(ids >= 0, perm[np.maximum(ids, 0)], -1)
     K = q1_reference_stiffness(nu)

@@ -20,7 +20,7 @@ def fa():
     return faer_amg_amd
 
 
-@pytest.mark.parametrize("elements,permute", [((3, 2, 4), False), ((4, 3, 3), True)])
+@pytest.mark.parametrize("elements,permute", [((3, 2, 4), False), ((4, 3, 3), True), ((5, 3, 3), 13)])
 def test_elasticity_generator(elements, permute):
     H = fa().elasticity_q1(elements, contrast=1.0, nu=0.3, seed=7, permute=permute)
     G = H.to_scipy()
