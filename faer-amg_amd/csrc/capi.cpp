@@ -243,6 +243,11 @@ amg_status amg_csr_value_codes(const amg_linop *op, int64_t *info2) {
             info2[0] = m.dia_vbits;
             info2[1] = m.dia_ntab;
         } else {
+            if (m.kernel == SPMV_KERNEL_SELLP) {
+                info2[0] = m.sellp_vbits;
+                info2[1] = m.sellp_ntab;
+                return;
+            }
             const bool coded = m.kernel == SPMV_KERNEL_SELL || m.kernel == SPMV_KERNEL_VECTOR;
             info2[0] = !coded ? 0 : m.kernel == SPMV_KERNEL_SELL ? m.sell_vbits : m.vec_vbits;
             info2[1] = coded && info2[0] ? m.sell_ntab : 0;

@@ -89,16 +89,27 @@ struct GpuCsr {
     int64_t bsr_slices = 0, bsr_steps = 0;
     std::vector<int64_t> bsr_seg_slc;
     bool no_bsr = false;  // e.g. a color-permuted SGS copy
+    // pattern SELL with L lanes per row (sellp.hip): values / codes only, columns
+    // from per-slice offset patterns
+    DevBuf<char> sellp_vals;
+    DevBuf<int64_t> sellp_eoff;
+    DevBuf<int32_t> sellp_row0, sellp_pid, sellp_poff, sellp_offs;
+    DevBuf<double> sellp_vtab;
+    int64_t sellp_slices = 0, sellp_elems = 0, sellp_ntab = 0, sellp_meta_bytes = 0;
+    int sellp_L = 0, sellp_vbits = 0;
+    std::vector<int64_t> sellp_seg_slc;
     int kernel = 0;  // SpmvKernel chosen at finalize
     bool spmv_ready() const { return rp32.get() != nullptr && sched.get() != nullptr; }
     bool has_sell() const { return sell_desc.get() != nullptr; }
     bool has_dia() const { return dia_codes.get() != nullptr; }
     bool has_bsr() const { return bsr_data.get() != nullptr; }
+    bool has_sellp() const { return sellp_vals.get() != nullptr; }
     int64_t index_bytes() const { return 12 * nnz + 4 * (nrows + 1); }
     // matrix bytes one SpMV streams with the chosen kernel (data + metadata)
     int64_t stream_bytes() const {
         if (kernel == 3) return 4 * dia_cw * nrows + 8 * dia_ntab;
         if (kernel == 4) return bsr_steps * (64 * 76) + 8 * (bsr_slices + 1);
+        if (kernel == 5) return sellp_elems * (sellp_vbits ? sellp_vbits / 8 : 8) + sellp_meta_bytes + 8 * sellp_ntab;
         if (kernel == 2)
             return nnz * ((vec_vbits ? vec_vbits / 8 : 8) + (vec_o16 ? 2 : 4)) + 4 * (nrows + 1) + 8 * sell_ntab;
         return kernel == 1 ? sell_bytes + 12 * (nslices + 1) + 4 * sell_steps + 8 * sell_ntab : index_bytes();
@@ -122,8 +133,12 @@ extern int g_spmv_format_policy;
 // distinct values, 0 = always fp64 values)
 extern int g_value_codes;
 enum SpmvKernel : int {
-    SPMV_KERNEL_STREAM = 0, SPMV_KERNEL_SELL = 1, SPMV_KERNEL_VECTOR = 2, SPMV_KERNEL_DIA = 3, SPMV_KERNEL_BSR = 4
+    SPMV_KERNEL_STREAM = 0, SPMV_KERNEL_SELL = 1, SPMV_KERNEL_VECTOR = 2, SPMV_KERNEL_DIA = 3, SPMV_KERNEL_BSR = 4,
+    SPMV_KERNEL_SELLP = 5
 };
+// pattern SELL with L lanes per row for dense structured operators; true if built (sellp.hip)
+bool build_sellp(GpuCsr &m, const std::vector<int64_t> &rp);
+int csr_value_table(const GpuCsr &m, std::vector<unsigned long long> &tab);
 // 3x3 block storage when the matrix is blocked and it streams fewer bytes than
 // other_bytes; true if built (bsr.hip)
 bool build_bsr(GpuCsr &m, const std::vector<int64_t> &rp, int64_t other_bytes);
@@ -169,6 +184,8 @@ void spmv(const GpuCsr &m, const double *x, double *y, SpmvMode mode, const Spmv
           hipStream_t s, int64_t seg = -1);
 void spmv_bsr(const GpuCsr &m, const double *x, double *y, SpmvMode mode, const SpmvEpi &epi, hipStream_t s,
               int64_t seg);
+void spmv_sellp(const GpuCsr &m, const double *x, double *y, SpmvMode mode, const SpmvEpi &epi, hipStream_t s,
+                int64_t seg);
 
 // BLAS-1 (n-vectors, device pointers)
 void vec_fill(double *x, double v, int64_t n, hipStream_t s);

@@ -1336,7 +1336,9 @@ __global__ __launch_bounds__(256) void k_value_set(const double *val, int64_t nn
 // distinct bit patterns, +0.0 (padding) included, ascending as unsigned.
 static int value_table_of(const double *val, int64_t nnz, hipStream_t s, std::vector<unsigned long long> &tab);
 
-static int value_table(const GpuCsr &m, std::vector<unsigned long long> &tab) {
+int csr_value_table(const GpuCsr &m, std::vector<unsigned long long> &tab);
+static int value_table(const GpuCsr &m, std::vector<unsigned long long> &tab) { return csr_value_table(m, tab); }
+int csr_value_table(const GpuCsr &m, std::vector<unsigned long long> &tab) {
     tab.clear();
     if (!g_value_codes || m.nnz == 0) return 0;
     return value_table_of(m.val.get(), m.nnz, m.ctx->stream, tab);
@@ -1814,6 +1816,7 @@ static void build_vec_codes(GpuCsr &m) {
 void choose_kernel(GpuCsr &m) {
     if (m.has_dia() && !m.dia_rowid && m.dia_r0 == 0 && m.dia_r1 == m.nrows) m.kernel = SPMV_KERNEL_DIA;
     else if (m.has_bsr()) m.kernel = SPMV_KERNEL_BSR;
+    else if (m.has_sellp()) m.kernel = SPMV_KERNEL_SELLP;
     else if (m.has_sell()) m.kernel = SPMV_KERNEL_SELL;
     else if (g_spmv_format_policy == 3 ||
              (g_spmv_format_policy == 0 && m.nrows > 0 && m.nnz >= vec_min_avg() * m.nrows)) {
@@ -1881,6 +1884,11 @@ void spmv(const GpuCsr &m, const double *x, double *y, SpmvMode mode, const Spmv
     if (m.kernel == SPMV_KERNEL_BSR) {
         FAMG_REQUIRE(mode != SPMV_SGS, AMG_ERR_UNSUPPORTED, "block storage has no SGS sweep");
         spmv_bsr(m, x, y, mode, epi, s, seg);
+        return;
+    }
+    if (m.kernel == SPMV_KERNEL_SELLP) {
+        FAMG_REQUIRE(mode != SPMV_SGS, AMG_ERR_UNSUPPORTED, "pattern SELL has no SGS sweep");
+        spmv_sellp(m, x, y, mode, epi, s, seg);
         return;
     }
     if (mode == SPMV_SGS && m.has_dia() && m.dia_rowid) {  // color sweep of a color-permuted copy

@@ -393,7 +393,7 @@ class SparseMatOp(LinOp):
         keys = ("kernel", "stream_bytes", "csr_bytes", "slices", "stored_entries",
                 "slices_implicit", "slices_u16", "slices_i32")
         d = dict(zip(keys, (int(v) for v in info)))
-        d["kernel"] = ("csr-stream", "sell", "vector", "dia", "bsr")[d["kernel"]]
+        d["kernel"] = ("csr-stream", "sell", "vector", "dia", "bsr", "sellp")[d["kernel"]]
         vc = np.zeros(2, np.int64)
         _ck(_lib.amg_csr_value_codes(self.h, vc.ctypes.data_as(vp)))
         d["value_bits"], d["value_table"] = int(vc[0]), int(vc[1])
@@ -472,7 +472,7 @@ class SymGaussSeidel(LinOp):
 def sgs_info(S):
     info = np.zeros(4, np.int64)
     _ck(_lib.amg_sgs_info(S.h, info.ctypes.data_as(vp)))
-    return {"colors": int(info[0]), "kernel": ("csr-stream", "sell", "vector", "dia", "bsr")[int(info[1])],
+    return {"colors": int(info[0]), "kernel": ("csr-stream", "sell", "vector", "dia", "bsr", "sellp")[int(info[1])],
             "diagonals": int(info[2]), "bits": int(info[3])}
 
 
