@@ -194,6 +194,10 @@ bool build_sellp(GpuCsr &m, const std::vector<int64_t> &rp) {
     std::vector<unsigned long long> tab;
     int vb = csr_value_table(m, tab);
     if (vb == 4) vb = 8;
+    // operators with a value table keep the value-code SELL: its 16-B code units
+    // with two rows per lane beat L lanes per row there (A_2 of the 256^3 cycle:
+    // 56 vs 91 us), the dependent table gather is the chain either way
+    if (vb) return false;
     std::vector<double> ev(elems, 0.0);
 #pragma omp parallel for schedule(dynamic, 64)
     for (int64_t k = 0; k < ns; k++) {
