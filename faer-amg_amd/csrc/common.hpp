@@ -41,9 +41,12 @@ struct AmgError : std::runtime_error {
         if (!(cond)) ::famg::fail(status, msg);                                            \
     } while (0)
 
-// Allocation policy: 1 (default) = buffers of >= 16 MiB are requested physically
-// contiguous (hipDeviceMallocContiguous, falling back to hipMalloc): the same
-// SpMV ran 15-20 % slower from some fragmented plain allocations.  0 = hipMalloc.
+// Allocation policy: 0 (default) = hipMalloc.  1 = buffers of >= 16 MiB
+// requested physically contiguous (hipDeviceMallocContiguous): measured
+// UNSAFE on gfx950 -- with it, kernels on one stream read stale values written
+// by the previous kernel (a SELL copy built from a half-updated smoothed P,
+// 12 of 12 hierarchy builds, 0 of 12 with hipMalloc; scripts/dbg_p1d.py), so
+// amg_set_alloc_policy(1) is refused.
 extern int g_alloc_policy;
 
 extern bool g_alloc_debug;  // FAMG_ALLOC_DEBUG=1: log large allocations to stderr

@@ -49,6 +49,46 @@ __global__ void k_narrow_rp(const int64_t *rp64, int32_t *rp32, int64_t n1) {
     if (i < n1) rp32[i] = static_cast<int32_t>(rp64[i]);
 }
 
+// FAMG_CHECK_STORAGE=1 (debugging aid): after every finalize, the chosen
+// storage's SpMV against the CSR-stream kernel on a fixed vector; mismatching
+// rows are reported on stderr.
+static bool storage_check_enabled() {
+    static const bool on = [] {
+        const char *e = getenv("FAMG_CHECK_STORAGE");
+        return e && e[0] == '1';
+    }();
+    return on;
+}
+
+__global__ void k_check_x(double *x, int64_t n) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i < n) x[i] = 1.0 + (double)((i * 2654435761LL) % 1000) * 1e-3;
+}
+
+static void storage_check(GpuCsr &m) {
+    if (m.kernel == SPMV_KERNEL_STREAM || m.nrows == 0 || m.ncols == 0) return;
+    hipStream_t s = m.ctx->stream;
+    DevBuf<double> x, y0(m.nrows), y1(m.nrows);
+    x.resize(m.ncols, 2);
+    hipLaunchKernelGGL(k_check_x, dim3((unsigned)ceil_div(m.ncols, 256)), dim3(256), 0, s, x.get(), m.ncols);
+    spmv(m, x.get(), y0.get(), SPMV_SET, SpmvEpi{}, s);
+    const int k = m.kernel;
+    m.kernel = SPMV_KERNEL_STREAM;
+    spmv(m, x.get(), y1.get(), SPMV_SET, SpmvEpi{}, s);
+    m.kernel = k;
+    std::vector<double> h0(m.nrows), h1(m.nrows);
+    FAMG_CHECK_HIP(hipMemcpyAsync(h0.data(), y0.get(), m.nrows * 8, hipMemcpyDeviceToHost, s));
+    FAMG_CHECK_HIP(hipMemcpyAsync(h1.data(), y1.get(), m.nrows * 8, hipMemcpyDeviceToHost, s));
+    FAMG_CHECK_HIP(hipStreamSynchronize(s));
+    int64_t bad = 0, first = -1;
+    double mx = 0;
+    for (int64_t i = 0; i < m.nrows; i++) mx = std::max(mx, std::abs(h1[i]));
+    for (int64_t i = 0; i < m.nrows; i++)
+        if (std::abs(h0[i] - h1[i]) > 1e-12 * mx) { bad++; if (first < 0) first = i; }
+    fprintf(stderr, "famg storage check %ldx%ld nnz %ld kernel %d: %ld bad rows (first %ld)\n", (long)m.nrows,
+            (long)m.ncols, (long)m.nnz, (int)k, (long)bad, (long)first);
+}
+
 void csr_finalize(GpuCsr &m, const std::vector<int64_t> *segments) {
     Ctx &ctx = *m.ctx;
     if (segments) {
@@ -99,6 +139,7 @@ void csr_finalize(GpuCsr &m, const std::vector<int64_t> *segments) {
         m.sell_mode_slices[0] = m.sell_mode_slices[1] = m.sell_mode_slices[2] = 0;
     }
     choose_kernel(m);
+    if (storage_check_enabled()) storage_check(m);
 }
 
 void csr_from_host(GpuCsr &m, Ctx *ctx, int64_t nrows, int64_t ncols, const int64_t *rowptr,

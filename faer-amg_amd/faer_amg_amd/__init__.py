@@ -185,7 +185,8 @@ def set_value_codes(enable):
 
 
 def set_alloc_policy(contiguous):
-    """Physically contiguous device allocations for large buffers (default True)."""
+    """Physically contiguous device allocations for large buffers: refused (True
+    raises) -- they read stale data across kernels on gfx950."""
     _ck(_lib.amg_set_alloc_policy(1 if contiguous else 0))
 
 

@@ -91,9 +91,10 @@ amg_status amg_set_spmv_format(int32_t policy);
  * them (the padding's 0.0 included); 0 always stores fp64 values.  A decoded
  * value is the stored value bit for bit, so results do not change. */
 amg_status amg_set_value_codes(int32_t enable);
-/* Device allocation policy for buffers allocated after the call: 1 (default)
- * requests physically contiguous memory for buffers >= 16 MiB (falls back to
- * hipMalloc), 0 always uses hipMalloc. */
+/* Device allocation policy for buffers allocated after the call: 0 (default)
+ * hipMalloc.  1 (physically contiguous buffers >= 16 MiB) is refused with
+ * AMG_ERR_UNSUPPORTED: on gfx950 it let kernels read stale data written by the
+ * previous kernel on the same stream. */
 amg_status amg_set_alloc_policy(int32_t policy);
 
 /* ---- sparse matrices (replaces SparseMatOp::new core.rs:56-74, ParSpmmOp::new

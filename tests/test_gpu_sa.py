@@ -224,6 +224,9 @@ def test_bsr_storage_bitwise(ctx, gap):
         hole = ((I + J) % 5 == 0) & (I != J) & (((C.row % 3 == 0) & (C.col % 3 == 1)) | ((C.row % 3 == 1) & (C.col % 3 == 0)))
         keep = ~hole
         S = sp.csr_matrix((C.data[keep], (C.row[keep], C.col[keep])), shape=S.shape)
+        # each removed symmetric pair a_ij is given back as |a_ij| on both
+        # diagonals (a PSD 2x2 update): the operator stays SPD
+        S = (S + sp.diags(np.bincount(C.row[hole], weights=np.abs(C.data[hole]), minlength=S.shape[0]))).tocsr()
         S.sort_indices()
     A = fa().SparseMatOp.from_scipy(ctx, S)
     info = A.spmv_info()
