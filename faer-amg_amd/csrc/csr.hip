@@ -130,8 +130,9 @@ void csr_finalize(GpuCsr &m, const std::vector<int64_t> *segments) {
         m.sell_vbits = 0;
         m.sell_mode_slices[0] = m.sell_mode_slices[1] = m.sell_mode_slices[2] = 0;
     }
-    // dense structured operators: the pattern SELL replaces SELL-64 / wave-per-row
-    if (!dia_all && !m.has_bsr() && build_sellp(m, rp)) {
+    // structured operators: the pattern SELL replaces SELL-64 / wave-per-row
+    const int64_t other_b = m.has_sell() ? sell_b : 10 * m.nnz + 4 * (m.nrows + 1);
+    if (!dia_all && !m.has_bsr() && build_sellp(m, rp, other_b)) {
         m.sell_row0.release(); m.sell_soff.release(); m.sell_desc.release(); m.sell_base.release();
         m.sell_data.release(); m.sell_vtab.release();
         m.nslices = m.sell_steps = m.sell_bytes = m.sell_ntab = 0;

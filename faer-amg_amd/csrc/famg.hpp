@@ -93,9 +93,11 @@ struct GpuCsr {
     // from per-slice offset patterns
     DevBuf<char> sellp_vals;
     DevBuf<int64_t> sellp_eoff;
-    DevBuf<int32_t> sellp_row0, sellp_pid, sellp_poff, sellp_offs;
+    DevBuf<int32_t> sellp_row0, sellp_pat, sellp_offs;  // pat: {offs start, width} per slice
+    DevBuf<int32_t> sellp_rbase;  // per-row column base (rectangular matrices)
     DevBuf<double> sellp_vtab;
-    int64_t sellp_slices = 0, sellp_elems = 0, sellp_ntab = 0, sellp_meta_bytes = 0;
+    int64_t sellp_slices = 0, sellp_elems = 0, sellp_ntab = 0, sellp_meta_bytes = 0, sellp_stream = 0;
+    bool no_sellp = false;  // e.g. a color-permuted SGS copy (swept in SGS mode)
     int sellp_L = 0, sellp_vbits = 0;
     std::vector<int64_t> sellp_seg_slc;
     int kernel = 0;  // SpmvKernel chosen at finalize
@@ -109,7 +111,7 @@ struct GpuCsr {
     int64_t stream_bytes() const {
         if (kernel == 3) return 4 * dia_cw * nrows + 8 * dia_ntab;
         if (kernel == 4) return bsr_steps * (64 * 76) + 8 * (bsr_slices + 1);
-        if (kernel == 5) return sellp_elems * (sellp_vbits ? sellp_vbits / 8 : 8) + sellp_meta_bytes + 8 * sellp_ntab;
+        if (kernel == 5) return sellp_stream;
         if (kernel == 2)
             return nnz * ((vec_vbits ? vec_vbits / 8 : 8) + (vec_o16 ? 2 : 4)) + 4 * (nrows + 1) + 8 * sell_ntab;
         return kernel == 1 ? sell_bytes + 12 * (nslices + 1) + 4 * sell_steps + 8 * sell_ntab : index_bytes();
@@ -136,8 +138,9 @@ enum SpmvKernel : int {
     SPMV_KERNEL_STREAM = 0, SPMV_KERNEL_SELL = 1, SPMV_KERNEL_VECTOR = 2, SPMV_KERNEL_DIA = 3, SPMV_KERNEL_BSR = 4,
     SPMV_KERNEL_SELLP = 5
 };
-// pattern SELL with L lanes per row for dense structured operators; true if built (sellp.hip)
-bool build_sellp(GpuCsr &m, const std::vector<int64_t> &rp);
+// pattern SELL (implicit columns from per-slice offset patterns) for structured
+// operators; true if built (sellp.hip)
+bool build_sellp(GpuCsr &m, const std::vector<int64_t> &rp, int64_t other_bytes);
 int csr_value_table(const GpuCsr &m, std::vector<unsigned long long> &tab);
 // 3x3 block storage when the matrix is blocked and it streams fewer bytes than
 // other_bytes; true if built (bsr.hip)

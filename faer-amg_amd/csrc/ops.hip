@@ -235,6 +235,7 @@ std::shared_ptr<SgsOp> make_sgs(const CsrPtr &A, const int32_t *colors, bool val
     csr_alloc(op->Ap, ctx, n, n, nnz);
     op->Ap.rp64 = std::move(prp);
     op->Ap.no_bsr = true;  // swept in SGS mode only
+    op->Ap.no_sellp = true;
     op->dinv.resize(n);
     if (n)
         hipLaunchKernelGGL(k_perm_rows, dim3(g), dim3(256), 0, s, A->m.rp64.get(), A->m.col.get(),

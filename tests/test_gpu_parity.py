@@ -823,9 +823,11 @@ def test_dia_codes(ctx, gen):
 def test_vcycle_256_storage_mix(ctx):
     """The benchmark configuration itself (C2: 7-pt 256^3, SA 2^3 boxes, Jacobi,
     6 levels) against the oracle on the same hierarchy, so the exact storage mix
-    the bench times is what is checked: DIA codes on A_0, 4-bit value-code SELL
-    with u16 column deltas on P_0/R_0, 8-bit codes on A_1, 16-bit codes on
-    A_2/R_1/P_1, the pattern SELL (lanes per row) on A_3, the wave-per-row kernel on A_4.  One
+    the bench times is what is checked: DIA codes on A_0, 4-bit-coded pattern
+    SELL on R_0 (row bases, implicit columns), 4-bit SELL with u16 column deltas
+    on P_0, 8-bit-code SELL on A_1,
+    16-bit codes on A_2/R_1/P_1, the fp64 pattern SELL (lanes per row) on A_3,
+    the wave-per-row kernel on A_4.  One
     V-cycle to 1e-11 and 10 stationary cycles (rho_k) to 1e-8 (+ noise floor).
     The oracle runs its ParSpmmOp restatement on 16 threads (same per-row order
     as the sequential CSR)."""
@@ -838,8 +840,8 @@ def test_vcycle_256_storage_mix(ctx):
              mg.level(l)[3].spmv_info() if l < 5 else None) for l in range(6)]
     a0, r0, p0 = info[0]
     assert a0["kernel"] == "dia" and a0["value_bits"] == 4
-    for m in (r0, p0):
-        assert m["kernel"] == "sell" and m["value_bits"] == 4 and m["slices_u16"] > 0
+    assert r0["kernel"] == "sellp" and r0["value_bits"] == 4
+    assert p0["kernel"] == "sell" and p0["value_bits"] == 4 and p0["slices_u16"] > 0
     assert info[1][0]["kernel"] == "sell" and info[1][0]["value_bits"] == 8
     assert info[2][0]["kernel"] == "sell" and info[2][0]["value_bits"] == 16
     assert info[1][1]["value_bits"] == 16 and info[1][2]["value_bits"] == 16
@@ -948,3 +950,56 @@ def test_sellp_dense_coarse_levels(ctx):
     levels = oracle_levels_from_gpu(mg, "jacobi")
     zref = O.Multigrid(levels).apply(b)
     assert np.linalg.norm(z - zref) <= 1e-11 * np.linalg.norm(zref)
+
+
+def test_sellp_coded_transfer_operators(ctx):
+    """Pattern SELL with 4-bit codes and per-row column bases (rectangular,
+    implicit columns) on a synthetic structured interpolation P (12 entries per
+    row around row // 16, four distinct values) and R = P^T: storage picked
+    automatically, P (one lane per row) bitwise equal to the oracle's row sums,
+    R within the summation-order bound, and a two-level V-cycle on a DIA fine
+    level within 1e-11 of the oracle with and without the zero-guess fold (P in
+    ADD0, else ADD; R in SET)."""
+    import scipy.sparse as sp
+    dims = (50, 49, 31)  # 75950 rows: DIA fine level, not a multiple of 3 (no 3x3 blocks)
+    A = fa().SparseMatOp.laplace3d_7pt(ctx, *dims)
+    nf = A.nrows
+    nc = (nf + 15) // 16
+    rows, cols, data = [], [], []
+    for k in range(12):  # 1.0 on the row's own coarse column, small couplings around it
+        i = np.arange(nf)
+        c = i // 16 + k - 5
+        ok = (c >= 0) & (c < nc)
+        rows.append(i[ok]); cols.append(c[ok])
+        data.append(np.full(ok.sum(), 1.0) if k == 5 else 0.125 * (1 + (i[ok] + k) % 3))
+    Ps = sp.csr_matrix((np.concatenate(data), (np.concatenate(rows), np.concatenate(cols))), shape=(nf, nc))
+    Ps.sort_indices()
+    Rs = Ps.T.tocsr()
+    Rs.sort_indices()
+    P = fa().SparseMatOp.from_scipy(ctx, Ps)
+    R = fa().SparseMatOp.from_scipy(ctx, Rs)
+    for M in (P, R):
+        info = M.spmv_info()
+        assert info["kernel"] == "sellp" and info["value_bits"] == 4, info
+    rng = np.random.default_rng(77)
+    OP, OR = O.Csr.from_scipy(Ps), O.Csr.from_scipy(Rs)
+    xc = rng.standard_normal(nc)
+    assert np.array_equal(apply_dev(ctx, P, xc, nf), OP.spmv(xc))
+    xf = rng.standard_normal(nf)
+    yr = apply_dev(ctx, R, xf, nc)
+    assert np.all(np.abs(yr - OR.spmv(xf)) <= spmv_bound(Rs, xf))
+    assert A.spmv_info()["kernel"] == "dia"
+    As = A.to_scipy()
+    Acs = (Rs @ As @ Ps).tocsr()
+    Acs.sort_indices()
+    Ac = fa().SparseMatOp.from_scipy(ctx, Acs)
+    mg = fa().Multigrid(A, fa().new_jacobi(A, 0.66))
+    mg.add_level(Ac, fa().CoarseCholesky(Ac), R, P)
+    levels = [{"A": O.Csr.from_scipy(As), "smoother": "jacobi", "R": OR, "P": OP},
+              {"A": O.Csr.from_scipy(Acs), "smoother": "chol"}]
+    b = rng.uniform(-1, 1, nf)
+    zref = O.Multigrid(levels).apply(b)
+    for fold in (True, False):
+        mg.set_fold_zero_guess(fold)
+        z = apply_dev(ctx, mg, b, nf)
+        assert np.linalg.norm(z - zref) <= 1e-11 * np.linalg.norm(zref), fold
