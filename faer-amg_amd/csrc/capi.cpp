@@ -257,6 +257,18 @@ amg_status amg_csr_value_codes(const amg_linop *op, int64_t *info2) {
     });
 }
 
+amg_status amg_csr_class_info(const amg_linop *op, int64_t *info4) {
+    return guard([&] {
+        FAMG_REQUIRE(info4, AMG_ERR_INVALID, "null argument");
+        const GpuCsr &m = need_csr(op)->m;
+        const bool on = m.has_scs();
+        info4[0] = on ? m.scs_nclass : 0;
+        info4[1] = on ? m.scs_k : 0;
+        info4[2] = on ? 8 * m.scs_ib : 0;
+        info4[3] = on ? 8 * m.scs_k * m.scs_nclass : 0;
+    });
+}
+
 amg_status amg_csr_dia_range(const amg_linop *op, int64_t *info4) {
     return guard([&] {
         FAMG_REQUIRE(info4, AMG_ERR_INVALID, "null argument");

@@ -119,6 +119,8 @@ void csr_finalize(GpuCsr &m, const std::vector<int64_t> *segments) {
     FAMG_CHECK_HIP(hipMemcpyAsync(m.sched.get(), sched.data(), sched.size() * sizeof(int32_t),
                                   hipMemcpyHostToDevice, ctx.stream));
     FAMG_CHECK_HIP(hipStreamSynchronize(ctx.stream));
+    scs_release(m);
+    sellp_release(m);
     build_sell(m, rp);
     const bool dia_all = m.has_dia() && m.dia_r0 == 0 && m.dia_r1 == m.nrows;
     const int64_t sell_b = m.sell_bytes + 12 * (m.nslices + 1) + 4 * m.sell_steps + 8 * m.sell_ntab;
@@ -130,9 +132,11 @@ void csr_finalize(GpuCsr &m, const std::vector<int64_t> *segments) {
         m.sell_vbits = 0;
         m.sell_mode_slices[0] = m.sell_mode_slices[1] = m.sell_mode_slices[2] = 0;
     }
-    // structured operators: the pattern SELL replaces SELL-64 / wave-per-row
+    // structured operators: stencil classes, else the pattern SELL, replace
+    // SELL-64 / wave-per-row
     const int64_t other_b = m.has_sell() ? sell_b : 10 * m.nnz + 4 * (m.nrows + 1);
-    if (!dia_all && !m.has_bsr() && build_sellp(m, rp, other_b)) {
+    const bool scs = !dia_all && !m.has_bsr() && build_scs(m, rp, other_b);
+    if (!dia_all && !m.has_bsr() && (scs || build_sellp(m, rp, other_b))) {
         m.sell_row0.release(); m.sell_soff.release(); m.sell_desc.release(); m.sell_base.release();
         m.sell_data.release(); m.sell_vtab.release();
         m.nslices = m.sell_steps = m.sell_bytes = m.sell_ntab = 0;

@@ -100,18 +100,27 @@ struct GpuCsr {
     bool no_sellp = false;  // e.g. a color-permuted SGS copy (swept in SGS mode)
     int sellp_L = 0, sellp_vbits = 0;
     std::vector<int64_t> sellp_seg_slc;
+    // stencil-class storage (scs.hip): one 8/16-bit class id per row, a
+    // dictionary of class stencils over the union of the rows' offsets
+    DevBuf<char> scs_cls;
+    DevBuf<double> scs_dict;
+    DevBuf<int32_t> scs_offs;
+    int64_t scs_k = 0, scs_nclass = 0;
+    int scs_ib = 0;
     int kernel = 0;  // SpmvKernel chosen at finalize
     bool spmv_ready() const { return rp32.get() != nullptr && sched.get() != nullptr; }
     bool has_sell() const { return sell_desc.get() != nullptr; }
     bool has_dia() const { return dia_codes.get() != nullptr; }
     bool has_bsr() const { return bsr_data.get() != nullptr; }
     bool has_sellp() const { return sellp_vals.get() != nullptr; }
+    bool has_scs() const { return scs_cls.get() != nullptr; }
     int64_t index_bytes() const { return 12 * nnz + 4 * (nrows + 1); }
     // matrix bytes one SpMV streams with the chosen kernel (data + metadata)
     int64_t stream_bytes() const {
         if (kernel == 3) return 4 * dia_cw * nrows + 8 * dia_ntab;
         if (kernel == 4) return bsr_steps * (64 * 76) + 8 * (bsr_slices + 1);
         if (kernel == 5) return sellp_stream;
+        if (kernel == 6) return scs_ib * nrows + 8 * scs_k * scs_nclass + 4 * scs_k;
         if (kernel == 2)
             return nnz * ((vec_vbits ? vec_vbits / 8 : 8) + (vec_o16 ? 2 : 4)) + 4 * (nrows + 1) + 8 * sell_ntab;
         return kernel == 1 ? sell_bytes + 12 * (nslices + 1) + 4 * sell_steps + 8 * sell_ntab : index_bytes();
@@ -136,8 +145,13 @@ extern int g_spmv_format_policy;
 extern int g_value_codes;
 enum SpmvKernel : int {
     SPMV_KERNEL_STREAM = 0, SPMV_KERNEL_SELL = 1, SPMV_KERNEL_VECTOR = 2, SPMV_KERNEL_DIA = 3, SPMV_KERNEL_BSR = 4,
-    SPMV_KERNEL_SELLP = 5
+    SPMV_KERNEL_SELLP = 5, SPMV_KERNEL_SCS = 6
 };
+// stencil-class storage for structured operators whose rows repeat up to a
+// shift; true if built (scs.hip)
+bool build_scs(GpuCsr &m, const std::vector<int64_t> &rp, int64_t other_bytes);
+void scs_release(GpuCsr &m);
+void sellp_release(GpuCsr &m);
 // pattern SELL (implicit columns from per-slice offset patterns) for structured
 // operators; true if built (sellp.hip)
 bool build_sellp(GpuCsr &m, const std::vector<int64_t> &rp, int64_t other_bytes);
@@ -186,6 +200,8 @@ void spmm(const GpuCsr &m, const double *x, int64_t ldx, double *y, int64_t ldy,
 void spmv(const GpuCsr &m, const double *x, double *y, SpmvMode mode, const SpmvEpi &epi,
           hipStream_t s, int64_t seg = -1);
 void spmv_bsr(const GpuCsr &m, const double *x, double *y, SpmvMode mode, const SpmvEpi &epi, hipStream_t s,
+              int64_t seg);
+void spmv_scs(const GpuCsr &m, const double *x, double *y, SpmvMode mode, const SpmvEpi &epi, hipStream_t s,
               int64_t seg);
 void spmv_sellp(const GpuCsr &m, const double *x, double *y, SpmvMode mode, const SpmvEpi &epi, hipStream_t s,
                 int64_t seg);

@@ -1,0 +1,268 @@
+// scs.hip -- stencil-class storage for structured Galerkin operators.
+//
+// The coarse operators of a box-aggregation hierarchy on a structured grid are
+// stencils whose rows repeat bit for bit away from the boundary: A_1 of the
+// 256^3 cycle (2M rows, 32 entries per row) has 125 distinct rows up to a shift
+// (5^3 boundary-distance classes), A_2 (262K rows, 168 entries) 2197 (13^3).  The
+// storage keeps
+//   offs[K]      the sorted union of all rows' column offsets (col - row), K
+//                padded to a multiple of 8 with offset 0,
+//   dict[C][K]   for every class c its value at every offset (+0.0 where the
+//                class has no entry), class-major: a wave meets a handful of
+//                classes (rows along a grid line differ only near its ends), so
+//                an XCD touches only the stencils of its rows' classes,
+//   cls[n]       one 8/16-bit class id per row,
+// i.e. 1-2 B per row instead of 1-8 B per entry.  Row i's sum walks the K
+// offsets in ascending order with fma -- the stored entries in ascending column
+// order with exact zero terms between them, which is the oracle's CSR order:
+// row sums bitwise equal (x finite).  Offsets leaving [0, n) carry +0.0 and are
+// clamped.  Built for square matrices with 64 <= K <= 1024, <= 65536 classes, a
+// dictionary of <= 16 MiB and at most half the bytes of the storage finalize
+// chose.
+#include <algorithm>
+#include <cstdlib>
+#include <cstring>
+#include <unordered_map>
+
+#include "famg.hpp"
+
+namespace famg {
+
+constexpr int SCS_KMAX = 1024;
+constexpr int SCS_KMIN = 64;
+constexpr int SCS_U = 8;  // offsets per load group (K is padded to a multiple)
+
+struct ScsArgs {
+    const void *cls;
+    const double *dict;
+    const int32_t *offs;
+    int32_t k, nclass, row_begin, row_end, ncols;
+    const double *x;
+    double *y;
+    const double *b;
+    const double *d;
+    const uint8_t *dc;
+    const double *dt;
+};
+
+typedef double scs_dbl2_t __attribute__((ext_vector_type(2), aligned(8)));
+
+// x operands of rows (r, r+1) at column c = r + off: one 16-B load at clamp(c, 0,
+// ncols - 2) and selects (a column outside [0, ncols) belongs to a +0.0 term, so
+// any finite value will do there)
+template <int MODE>
+__device__ __forceinline__ void scs_x2(const ScsArgs &a, int c, double &xa, double &xb) {
+    const int p = min(max(c, 0), a.ncols - 2);
+    scs_dbl2_t v = *reinterpret_cast<const scs_dbl2_t *>(a.x + p);
+    xa = c > p ? v.y : v.x;
+    xb = c < p ? v.x : v.y;
+}
+
+// Two adjacent rows per lane (16-B x loads); the dictionary is read through
+// the caches (staging A_1's 40 KB dictionary in LDS per workgroup measured the
+// same, 47 vs 48 us).
+template <int MODE, int IB>
+__global__ __launch_bounds__(256) void spmv_scs_kernel(ScsArgs a) {
+    const double *dict = a.dict;
+    const int blk = xcd_remap(blockIdx.x, gridDim.x);
+    const int row = a.row_begin + 2 * (blk * 256 + (int)threadIdx.x);
+    const bool l0 = row < a.row_end, l1 = row + 1 < a.row_end;
+    const int r0 = l0 ? row : a.row_begin;
+    auto cls_of = [&](int r) {
+        return IB == 1 ? (int)static_cast<const uint8_t *>(a.cls)[r] : (int)static_cast<const uint16_t *>(a.cls)[r];
+    };
+    const int c0 = cls_of(r0), c1 = l1 ? cls_of(row + 1) : c0;
+    double br[2] = {0.0, 0.0}, xr[2] = {0.0, 0.0}, dr[2] = {0.0, 0.0}, yr[2] = {0.0, 0.0};
+#pragma unroll
+    for (int j = 0; j < 2; j++) {  // epilogue operands first
+        if (!(j ? l1 : l0)) continue;
+        const int i = row + j;
+        if constexpr (MODE == SPMV_RESID) br[j] = a.b[i];
+        if constexpr (MODE == SPMV_ADD) yr[j] = a.y[i];
+        if constexpr (MODE == SPMV_JACOBI) {
+            xr[j] = a.x[i];
+            br[j] = a.b[i];
+            dr[j] = a.dc ? a.dt[a.dc[i]] : a.d[i];
+        }
+    }
+    const double *da = dict + (int64_t)c0 * a.k, *db = dict + (int64_t)c1 * a.k;
+    double acc0 = 0.0, acc1 = 0.0;
+    for (int k0 = 0; k0 < a.k; k0 += SCS_U) {
+        double va[SCS_U], vb[SCS_U], xa[SCS_U], xb[SCS_U];
+#pragma unroll
+        for (int u = 0; u < SCS_U; u++) {
+            scs_x2<MODE>(a, r0 + a.offs[k0 + u], xa[u], xb[u]);
+            va[u] = da[k0 + u];
+            vb[u] = db[k0 + u];
+        }
+#pragma unroll
+        for (int u = 0; u < SCS_U; u++) {
+            acc0 = fma(va[u], xa[u], acc0);
+            acc1 = fma(vb[u], xb[u], acc1);
+        }
+    }
+    const double acc[2] = {acc0, acc1};
+#pragma unroll
+    for (int j = 0; j < 2; j++) {
+        if (!(j ? l1 : l0)) continue;
+        const int i = row + j;
+        if constexpr (MODE == SPMV_SET) a.y[i] = acc[j];
+        else if constexpr (MODE == SPMV_ADD) a.y[i] = yr[j] + acc[j];
+        else if constexpr (MODE == SPMV_RESID) a.y[i] = br[j] - acc[j];
+        else a.y[i] = xr[j] + dr[j] * (br[j] - acc[j]);  // JACOBI
+    }
+}
+
+static bool scs_disabled() {
+    static const bool off = [] {
+        const char *e = getenv("FAMG_NO_SCS");
+        return e && e[0] == '1';
+    }();
+    return off;
+}
+
+void scs_release(GpuCsr &m) {
+    m.scs_cls.release();
+    m.scs_dict.release();
+    m.scs_offs.release();
+    m.scs_k = m.scs_nclass = m.scs_ib = 0;
+}
+
+bool build_scs(GpuCsr &m, const std::vector<int64_t> &rp, int64_t other_bytes) {
+    scs_release(m);
+    if (g_spmv_format_policy != 0 || scs_disabled() || m.no_sellp || m.nrows != m.ncols || m.nrows < 1024 ||
+        m.nnz == 0)
+        return false;
+    const int64_t n = m.nrows;
+    hipStream_t st = m.ctx->stream;
+    std::vector<int32_t> col(m.nnz);
+    FAMG_CHECK_HIP(hipMemcpyAsync(col.data(), m.col.get(), m.nnz * sizeof(int32_t), hipMemcpyDeviceToHost, st));
+    FAMG_CHECK_HIP(hipStreamSynchronize(st));
+    // union of the offsets: bounded first (K <= SCS_KMAX), then a bitmap over the span
+    int64_t omin = INT64_MAX, omax = INT64_MIN;
+#pragma omp parallel for reduction(min : omin) reduction(max : omax) schedule(static)
+    for (int64_t i = 0; i < n; i++)
+        for (int64_t e = rp[i]; e < rp[i + 1]; e++) {
+            const int64_t o = (int64_t)col[e] - i;
+            omin = std::min(omin, o);
+            omax = std::max(omax, o);
+        }
+    const int64_t span = omax - omin + 1;
+    if (span > (int64_t(1) << 26)) return false;
+    std::vector<uint8_t> seen(span, 0);
+#pragma omp parallel for schedule(static)
+    for (int64_t i = 0; i < n; i++)
+        for (int64_t e = rp[i]; e < rp[i + 1]; e++) seen[(int64_t)col[e] - i - omin] = 1;  // benign same-value race
+    std::vector<int32_t> offs;
+    for (int64_t o = 0; o < span; o++)
+        if (seen[o]) {
+            offs.push_back((int32_t)(o + omin));
+            if ((int64_t)offs.size() > SCS_KMAX) return false;
+        }
+    const int K = (int)offs.size();
+    if (K == 0 || (double)K * (double)n > 2.0 * (double)m.nnz) return false;  // mostly padding
+    // short stencils stay on SELL-64: A_1 of the 256^3 cycle (33 offsets, 8-bit
+    // codes) ran 47 vs 44 us here; A_2 (179 offsets, 16-bit codes) 31-46 vs 55 us
+    if (K < SCS_KMIN) return false;
+    std::vector<double> val(m.nnz);
+    FAMG_CHECK_HIP(hipMemcpyAsync(val.data(), m.val.get(), m.nnz * sizeof(double), hipMemcpyDeviceToHost, st));
+    FAMG_CHECK_HIP(hipStreamSynchronize(st));
+    // class of a row: its (offset, value bits) list; hashed in parallel, grouped serially
+    std::vector<uint64_t> h(n);
+#pragma omp parallel for schedule(static)
+    for (int64_t i = 0; i < n; i++) {
+        uint64_t x = 0x9E3779B97F4A7C15ull ^ (uint64_t)(rp[i + 1] - rp[i]);
+        for (int64_t e = rp[i]; e < rp[i + 1]; e++) {
+            uint64_t bits;
+            std::memcpy(&bits, &val[e], 8);
+            x = (x ^ (uint64_t)(uint32_t)((int64_t)col[e] - i)) * 0x100000001B3ull;
+            x = (x ^ bits) * 0xFF51AFD7ED558CCDull;
+            x ^= x >> 29;
+        }
+        h[i] = x;
+    }
+    auto same_row = [&](int64_t i, int64_t j) {
+        if (rp[i + 1] - rp[i] != rp[j + 1] - rp[j]) return false;
+        for (int64_t a = rp[i], b = rp[j]; a < rp[i + 1]; a++, b++) {
+            if ((int64_t)col[a] - i != (int64_t)col[b] - j) return false;
+            if (std::memcmp(&val[a], &val[b], 8) != 0) return false;
+        }
+        return true;
+    };
+    std::unordered_map<uint64_t, std::vector<int32_t>> by_hash;  // hash -> classes (collisions chained)
+    std::vector<int64_t> rep;                                     // a row of every class
+    std::vector<uint16_t> cls(n);
+    for (int64_t i = 0; i < n; i++) {
+        auto &cands = by_hash[h[i]];
+        int32_t c = -1;
+        for (int32_t q : cands)
+            if (same_row(rep[q], i)) { c = q; break; }
+        if (c < 0) {
+            c = (int32_t)rep.size();
+            if (c >= 65536) return false;
+            rep.push_back(i);
+            cands.push_back(c);
+        }
+        cls[i] = (uint16_t)c;
+    }
+    const int64_t C = (int64_t)rep.size();
+    const int Kp = (K + SCS_U - 1) / SCS_U * SCS_U;
+    const int ib = C <= 256 ? 1 : 2;
+    const int64_t dict_bytes = (int64_t)Kp * C * 8;
+    const int64_t stream = ib * n + dict_bytes + 4 * Kp;
+    if (dict_bytes > (int64_t(16) << 20) || (double)stream > 0.5 * (double)other_bytes) return false;
+    std::vector<double> dict((size_t)Kp * C, 0.0);
+    for (int64_t c = 0; c < C; c++) {
+        const int64_t i = rep[c];
+        for (int64_t e = rp[i]; e < rp[i + 1]; e++) {
+            const int32_t o = (int32_t)((int64_t)col[e] - i);
+            const int k = (int)(std::lower_bound(offs.begin(), offs.end(), o) - offs.begin());
+            dict[(size_t)c * Kp + k] = val[e];
+        }
+    }
+    offs.resize(Kp, 0);  // padding offsets: value +0.0 at the row itself
+    m.scs_offs.resize(Kp);
+    m.scs_dict.resize((size_t)Kp * C);
+    m.scs_cls.resize(n * ib);
+    FAMG_CHECK_HIP(hipMemcpyAsync(m.scs_offs.get(), offs.data(), Kp * 4, hipMemcpyHostToDevice, st));
+    FAMG_CHECK_HIP(hipMemcpyAsync(m.scs_dict.get(), dict.data(), dict.size() * 8, hipMemcpyHostToDevice, st));
+    if (ib == 1) {
+        std::vector<uint8_t> c8(n);
+        for (int64_t i = 0; i < n; i++) c8[i] = (uint8_t)cls[i];
+        FAMG_CHECK_HIP(hipMemcpyAsync(m.scs_cls.get(), c8.data(), n, hipMemcpyHostToDevice, st));
+        FAMG_CHECK_HIP(hipStreamSynchronize(st));
+    } else {
+        FAMG_CHECK_HIP(hipMemcpyAsync(m.scs_cls.get(), cls.data(), n * 2, hipMemcpyHostToDevice, st));
+        FAMG_CHECK_HIP(hipStreamSynchronize(st));
+    }
+    m.scs_k = Kp;
+    m.scs_nclass = C;
+    m.scs_ib = ib;
+    return true;
+}
+
+void spmv_scs(const GpuCsr &m, const double *x, double *y, SpmvMode mode, const SpmvEpi &epi, hipStream_t s,
+              int64_t seg) {
+    const int64_t r0 = seg < 0 ? 0 : m.seg_rows[seg];
+    const int64_t r1 = seg < 0 ? m.nrows : m.seg_rows[seg + 1];
+    if (r1 <= r0) return;
+    ScsArgs a{m.scs_cls.get(), m.scs_dict.get(), m.scs_offs.get(), (int32_t)m.scs_k, (int32_t)m.scs_nclass,
+              (int32_t)r0, (int32_t)r1, (int32_t)m.ncols, x, y, epi.b, epi.d, epi.dc, epi.dt};
+    const dim3 grid((unsigned)ceil_div(r1 - r0, 512)), block(256);
+#define FAMG_SCS2(M, IB) spmv_scs_kernel<M, IB><<<grid, block, 0, s>>>(a);
+#define FAMG_SCS(IB)                                                                               \
+    switch (mode) {                                                                                \
+    case SPMV_SET: FAMG_SCS2(SPMV_SET, IB) break;                                                  \
+    case SPMV_ADD: FAMG_SCS2(SPMV_ADD, IB) break;                                                  \
+    case SPMV_RESID: FAMG_SCS2(SPMV_RESID, IB) break;                                              \
+    case SPMV_JACOBI: FAMG_SCS2(SPMV_JACOBI, IB) break;                                            \
+    default: fail(AMG_ERR_UNSUPPORTED, "stencil-class storage: unsupported SpMV epilogue");        \
+    }
+    if (m.scs_ib == 1) { FAMG_SCS(1) }
+    else { FAMG_SCS(2) }
+#undef FAMG_SCS
+#undef FAMG_SCS2
+    FAMG_CHECK_HIP(hipGetLastError());
+}
+
+}  // namespace famg

@@ -49,10 +49,7 @@ struct SellpArgs {
     const double *dt;
 };
 
-template <int MODE> __device__ __forceinline__ double sellp_x(const SellpArgs &a, int c) {
-    if constexpr (MODE == SPMV_RESID0) return a.d[c] * a.x[c];  // the zero-guess Jacobi iterate
-    else return a.x[c];
-}
+template <int MODE> __device__ __forceinline__ double sellp_x(const SellpArgs &a, int c) { return a.x[c]; }
 
 // fp64 values: U lane-steps, every load issued before the fmas
 template <int MODE, int L, int U>
@@ -114,7 +111,7 @@ __global__ __launch_bounds__(256) void spmv_sellp_kernel(SellpArgs a) {
     const int base = a.rbase ? a.rbase[rowc] : rowc;
     double br = 0.0, xr = 0.0, dr = 0.0, yr = 0.0;
     if (live && q == 0) {  // epilogue operands first
-        if constexpr (MODE == SPMV_RESID || MODE == SPMV_RESID0) br = a.b[row];
+        if constexpr (MODE == SPMV_RESID) br = a.b[row];
         if constexpr (MODE == SPMV_ADD) yr = a.y[row];
         if constexpr (MODE == SPMV_ADD0) yr = (a.dc ? a.dt[a.dc[row]] : a.d[row]) * a.b[row];
         if constexpr (MODE == SPMV_JACOBI) {
@@ -151,7 +148,7 @@ __global__ __launch_bounds__(256) void spmv_sellp_kernel(SellpArgs a) {
     if (live && q == 0) {
         if constexpr (MODE == SPMV_SET) a.y[row] = acc;
         else if constexpr (MODE == SPMV_ADD || MODE == SPMV_ADD0) a.y[row] = yr + acc;
-        else if constexpr (MODE == SPMV_RESID || MODE == SPMV_RESID0) a.y[row] = br - acc;
+        else if constexpr (MODE == SPMV_RESID) a.y[row] = br - acc;
         else a.y[row] = xr + dr * (br - acc);  // JACOBI
     }
 }
@@ -164,7 +161,7 @@ static bool sellp_disabled() {
     return off;
 }
 
-static void sellp_release(GpuCsr &m) {
+void sellp_release(GpuCsr &m) {
     m.sellp_vals.release();
     m.sellp_eoff.release();
     m.sellp_row0.release();
@@ -359,7 +356,6 @@ void spmv_sellp(const GpuCsr &m, const double *x, double *y, SpmvMode mode, cons
     case SPMV_ADD: spmv_sellp_kernel<SPMV_ADD, L, VB><<<grid, block, 0, s>>>(a); break;            \
     case SPMV_RESID: spmv_sellp_kernel<SPMV_RESID, L, VB><<<grid, block, 0, s>>>(a); break;        \
     case SPMV_JACOBI: spmv_sellp_kernel<SPMV_JACOBI, L, VB><<<grid, block, 0, s>>>(a); break;      \
-    case SPMV_RESID0: spmv_sellp_kernel<SPMV_RESID0, L, VB><<<grid, block, 0, s>>>(a); break;      \
     case SPMV_ADD0: spmv_sellp_kernel<SPMV_ADD0, L, VB><<<grid, block, 0, s>>>(a); break;          \
     default: fail(AMG_ERR_UNSUPPORTED, "pattern SELL: unsupported SpMV epilogue");                 \
     }

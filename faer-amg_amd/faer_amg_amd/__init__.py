@@ -59,6 +59,7 @@ SIGNATURES = {
     "amg_csr_value_codes": (i32, [vp, vp]),
     "amg_csr_download": (i32, [vp, vp, vp, vp]),
     "amg_csr_dia_range": (i32, [vp, vp]),
+    "amg_csr_class_info": (i32, [vp, vp]),
     "amg_gen_laplace3d_7pt": (i32, [vp, i64, i64, i64, P(vp)]),
     "amg_gen_aniso27": (i32, [vp, i64, i64, i64, dbl, dbl, dbl, P(vp)]),
     "amg_gen_random_7pt": (i32, [vp, i64, i64, i64, C.c_uint64, i64, P(vp)]),
@@ -394,7 +395,7 @@ class SparseMatOp(LinOp):
         keys = ("kernel", "stream_bytes", "csr_bytes", "slices", "stored_entries",
                 "slices_implicit", "slices_u16", "slices_i32")
         d = dict(zip(keys, (int(v) for v in info)))
-        d["kernel"] = ("csr-stream", "sell", "vector", "dia", "bsr", "sellp")[d["kernel"]]
+        d["kernel"] = ("csr-stream", "sell", "vector", "dia", "bsr", "sellp", "classes")[d["kernel"]]
         vc = np.zeros(2, np.int64)
         _ck(_lib.amg_csr_value_codes(self.h, vc.ctypes.data_as(vp)))
         d["value_bits"], d["value_table"] = int(vc[0]), int(vc[1])
@@ -402,6 +403,9 @@ class SparseMatOp(LinOp):
         _ck(_lib.amg_csr_dia_range(self.h, dr.ctypes.data_as(vp)))
         d["dia_rows"] = (int(dr[0]), int(dr[1]))
         d["dia_diagonals"], d["dia_bits"] = int(dr[2]), int(dr[3])
+        ci = np.zeros(4, np.int64)
+        _ck(_lib.amg_csr_class_info(self.h, ci.ctypes.data_as(vp)))
+        d["classes"], d["class_offsets"], d["class_id_bits"] = int(ci[0]), int(ci[1]), int(ci[2])
         return d
 
     def arrays(self):

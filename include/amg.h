@@ -101,6 +101,13 @@ amg_status amg_set_alloc_policy(int32_t policy);
  *      par_spmm.rs:31-96, and the SparseRowMat<usize,f64> LinOp used at
  *      multigrid.rs:137-158) -------------------------------------------------- */
 
+/* Stencil-class storage of a CSR operator (structured Galerkin operators whose
+ * rows repeat up to a shift; replaces the value/column streams of
+ * interpolation/mod.rs:828's A_c in SpMV): info4 = {classes, offsets K (padded
+ * to 8), class-id bits, dictionary bytes}; zeros when the operator uses another
+ * storage. */
+amg_status amg_csr_class_info(const amg_linop *op, int64_t *info4);
+
 /* Copy a host CSR with usize-compatible (int64) row pointers and column indices
  * and fp64 values to the device.  Columns must be sorted ascending within each
  * row and in [0, ncols).  Stored internally with 32-bit indices: returns

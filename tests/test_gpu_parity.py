@@ -825,8 +825,8 @@ def test_vcycle_256_storage_mix(ctx):
     6 levels) against the oracle on the same hierarchy, so the exact storage mix
     the bench times is what is checked: DIA codes on A_0, 4-bit-coded pattern
     SELL on R_0 (row bases, implicit columns), 4-bit SELL with u16 column deltas
-    on P_0, 8-bit-code SELL on A_1,
-    16-bit codes on A_2/R_1/P_1, the fp64 pattern SELL (lanes per row) on A_3,
+    on P_0, 8-bit-code SELL on A_1, stencil classes on A_2 (2197 classes),
+    16-bit codes on R_1/P_1, the fp64 pattern SELL (lanes per row) on A_3,
     the wave-per-row kernel on A_4.  One
     V-cycle to 1e-11 and 10 stationary cycles (rho_k) to 1e-8 (+ noise floor).
     The oracle runs its ParSpmmOp restatement on 16 threads (same per-row order
@@ -843,7 +843,7 @@ def test_vcycle_256_storage_mix(ctx):
     assert r0["kernel"] == "sellp" and r0["value_bits"] == 4
     assert p0["kernel"] == "sell" and p0["value_bits"] == 4 and p0["slices_u16"] > 0
     assert info[1][0]["kernel"] == "sell" and info[1][0]["value_bits"] == 8
-    assert info[2][0]["kernel"] == "sell" and info[2][0]["value_bits"] == 16
+    assert info[2][0]["kernel"] == "classes" and info[2][0]["classes"] == 2197
     assert info[1][1]["value_bits"] == 16 and info[1][2]["value_bits"] == 16
     assert info[3][0]["kernel"] == "sellp" and info[4][0]["kernel"] == "vector"
     levels = oracle_levels_from_gpu(mg, "jacobi")
@@ -1003,3 +1003,26 @@ def test_sellp_coded_transfer_operators(ctx):
         mg.set_fold_zero_guess(fold)
         z = apply_dev(ctx, mg, b, nf)
         assert np.linalg.norm(z - zref) <= 1e-11 * np.linalg.norm(zref), fold
+
+
+def test_stencil_classes(ctx):
+    """Stencil-class storage (one class id per row, a dictionary of the distinct
+    rows up to a shift) on A_2 of a 128^3 SA hierarchy (32^3 rows, 13^3 boundary
+    classes): SpMV bitwise equal to the oracle's row sums (ascending offsets with
+    exact zero terms), every row's class reproduces its CSR row, and the V-cycle
+    through it (RESID / JACOBI epilogues) within 1e-11 of the oracle."""
+    dims = (128, 128, 128)
+    A = fa().SparseMatOp.laplace3d_7pt(ctx, *dims)
+    mg = fa().sa_build_box(A, dims, (2, 2, 2), coarsest_dim=100)
+    A2 = mg.level(2)[0]
+    info = A2.spmv_info()
+    assert info["kernel"] == "classes" and info["classes"] == 2197, info
+    assert info["class_offsets"] >= 179 and info["class_id_bits"] == 16
+    assert info["stream_bytes"] < 0.5 * 12 * A2.nnz
+    OA2 = O.Csr.from_arrays(*A2.dims(), *A2.arrays())
+    x = np.random.default_rng(41).standard_normal(A2.ncols)
+    assert np.array_equal(apply_dev(ctx, A2, x, A2.nrows), OA2.spmv(x))
+    b = np.random.default_rng(42).uniform(-1, 1, A.nrows)
+    zref = O.Multigrid(oracle_levels_from_gpu(mg, "jacobi")).apply(b)
+    z = apply_dev(ctx, mg, b, A.nrows)
+    assert np.linalg.norm(z - zref) <= 1e-11 * np.linalg.norm(zref)
