@@ -128,6 +128,54 @@ void scs_release(GpuCsr &m) {
     m.scs_k = m.scs_nclass = m.scs_ib = 0;
 }
 
+// Class of every row: rows with the same (col - base[i], value bits) list share
+// one; hashed in parallel, grouped serially with a full comparison.  Returns the
+// number of classes (ids in cls, one representative row per class in rep), or
+// -1 past 65536.
+static int64_t row_classes(const std::vector<int64_t> &rp, const std::vector<int32_t> &col,
+                           const std::vector<double> &val, const std::vector<int64_t> &base,
+                           std::vector<uint16_t> &cls, std::vector<int64_t> &rep) {
+    const int64_t n = (int64_t)rp.size() - 1;
+    std::vector<uint64_t> h(n);
+#pragma omp parallel for schedule(static)
+    for (int64_t i = 0; i < n; i++) {
+        uint64_t x = 0x9E3779B97F4A7C15ull ^ (uint64_t)(rp[i + 1] - rp[i]);
+        for (int64_t e = rp[i]; e < rp[i + 1]; e++) {
+            uint64_t bits;
+            std::memcpy(&bits, &val[e], 8);
+            x = (x ^ (uint64_t)(uint32_t)((int64_t)col[e] - base[i])) * 0x100000001B3ull;
+            x = (x ^ bits) * 0xFF51AFD7ED558CCDull;
+            x ^= x >> 29;
+        }
+        h[i] = x;
+    }
+    auto same_row = [&](int64_t i, int64_t j) {
+        if (rp[i + 1] - rp[i] != rp[j + 1] - rp[j]) return false;
+        for (int64_t a = rp[i], b = rp[j]; a < rp[i + 1]; a++, b++) {
+            if ((int64_t)col[a] - base[i] != (int64_t)col[b] - base[j]) return false;
+            if (std::memcmp(&val[a], &val[b], 8) != 0) return false;
+        }
+        return true;
+    };
+    std::unordered_map<uint64_t, std::vector<int32_t>> by_hash;  // hash -> classes (collisions chained)
+    rep.clear();
+    cls.assign(n, 0);
+    for (int64_t i = 0; i < n; i++) {
+        auto &cands = by_hash[h[i]];
+        int32_t c = -1;
+        for (int32_t q : cands)
+            if (same_row(rep[q], i)) { c = q; break; }
+        if (c < 0) {
+            c = (int32_t)rep.size();
+            if (c >= 65536) return -1;
+            rep.push_back(i);
+            cands.push_back(c);
+        }
+        cls[i] = (uint16_t)c;
+    }
+    return (int64_t)rep.size();
+}
+
 bool build_scs(GpuCsr &m, const std::vector<int64_t> &rp, int64_t other_bytes) {
     scs_release(m);
     if (g_spmv_format_policy != 0 || scs_disabled() || m.no_sellp || m.nrows != m.ncols || m.nrows < 1024 ||
@@ -167,44 +215,11 @@ bool build_scs(GpuCsr &m, const std::vector<int64_t> &rp, int64_t other_bytes) {
     std::vector<double> val(m.nnz);
     FAMG_CHECK_HIP(hipMemcpyAsync(val.data(), m.val.get(), m.nnz * sizeof(double), hipMemcpyDeviceToHost, st));
     FAMG_CHECK_HIP(hipStreamSynchronize(st));
-    // class of a row: its (offset, value bits) list; hashed in parallel, grouped serially
-    std::vector<uint64_t> h(n);
-#pragma omp parallel for schedule(static)
-    for (int64_t i = 0; i < n; i++) {
-        uint64_t x = 0x9E3779B97F4A7C15ull ^ (uint64_t)(rp[i + 1] - rp[i]);
-        for (int64_t e = rp[i]; e < rp[i + 1]; e++) {
-            uint64_t bits;
-            std::memcpy(&bits, &val[e], 8);
-            x = (x ^ (uint64_t)(uint32_t)((int64_t)col[e] - i)) * 0x100000001B3ull;
-            x = (x ^ bits) * 0xFF51AFD7ED558CCDull;
-            x ^= x >> 29;
-        }
-        h[i] = x;
-    }
-    auto same_row = [&](int64_t i, int64_t j) {
-        if (rp[i + 1] - rp[i] != rp[j + 1] - rp[j]) return false;
-        for (int64_t a = rp[i], b = rp[j]; a < rp[i + 1]; a++, b++) {
-            if ((int64_t)col[a] - i != (int64_t)col[b] - j) return false;
-            if (std::memcmp(&val[a], &val[b], 8) != 0) return false;
-        }
-        return true;
-    };
-    std::unordered_map<uint64_t, std::vector<int32_t>> by_hash;  // hash -> classes (collisions chained)
-    std::vector<int64_t> rep;                                     // a row of every class
-    std::vector<uint16_t> cls(n);
-    for (int64_t i = 0; i < n; i++) {
-        auto &cands = by_hash[h[i]];
-        int32_t c = -1;
-        for (int32_t q : cands)
-            if (same_row(rep[q], i)) { c = q; break; }
-        if (c < 0) {
-            c = (int32_t)rep.size();
-            if (c >= 65536) return false;
-            rep.push_back(i);
-            cands.push_back(c);
-        }
-        cls[i] = (uint16_t)c;
-    }
+    std::vector<int64_t> base(n);
+    for (int64_t i = 0; i < n; i++) base[i] = i;
+    std::vector<uint16_t> cls;
+    std::vector<int64_t> rep;
+    if (row_classes(rp, col, val, base, cls, rep) < 0) return false;
     const int64_t C = (int64_t)rep.size();
     const int Kp = (K + SCS_U - 1) / SCS_U * SCS_U;
     const int ib = C <= 256 ? 1 : 2;
@@ -264,5 +279,6 @@ void spmv_scs(const GpuCsr &m, const double *x, double *y, SpmvMode mode, const 
 #undef FAMG_SCS2
     FAMG_CHECK_HIP(hipGetLastError());
 }
+
 
 }  // namespace famg
