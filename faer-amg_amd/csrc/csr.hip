@@ -136,7 +136,8 @@ void csr_finalize(GpuCsr &m, const std::vector<int64_t> *segments) {
     // SELL-64 / wave-per-row
     const int64_t other_b = m.has_sell() ? sell_b : 10 * m.nnz + 4 * (m.nrows + 1);
     const bool scs = !dia_all && !m.has_bsr() && build_scs(m, rp, other_b);
-    if (!dia_all && !m.has_bsr() && (scs || build_sellp(m, rp, other_b))) {
+    const bool scs_all = scs && m.scs_seg < 0;  // else a row segment beside SELL-64
+    if (!dia_all && !m.has_bsr() && (scs_all || (!scs && build_sellp(m, rp, other_b)))) {
         m.sell_row0.release(); m.sell_soff.release(); m.sell_desc.release(); m.sell_base.release();
         m.sell_data.release(); m.sell_vtab.release();
         m.nslices = m.sell_steps = m.sell_bytes = m.sell_ntab = 0;

@@ -106,6 +106,7 @@ struct GpuCsr {
     DevBuf<double> scs_dict;
     DevBuf<int32_t> scs_offs;
     int64_t scs_k = 0, scs_nclass = 0;
+    int64_t scs_seg = -1;  // >= 0: only this row segment (a distributed level's halo interior) beside SELL
     int scs_ib = 0;
     int kernel = 0;  // SpmvKernel chosen at finalize
     bool spmv_ready() const { return rp32.get() != nullptr && sched.get() != nullptr; }

@@ -16,9 +16,10 @@
 // offsets in ascending order with fma -- the stored entries in ascending column
 // order with exact zero terms between them, which is the oracle's CSR order:
 // row sums bitwise equal (x finite).  Offsets leaving [0, n) carry +0.0 and are
-// clamped.  Built for square matrices with 64 <= K <= 1024, <= 65536 classes, a
-// dictionary of <= 16 MiB and at most half the bytes of the storage finalize
-// chose.
+// clamped.  Built with 64 <= K <= 1024, <= 65536 classes, a dictionary of <= 16
+// MiB and at most half the bytes of the storage finalize chose, for a square
+// matrix or for the halo-interior row segment of a distributed level (rows that
+// read owned columns only; the boundary segments keep SELL-64).
 #include <algorithm>
 #include <cstdlib>
 #include <cstring>
@@ -126,19 +127,20 @@ void scs_release(GpuCsr &m) {
     m.scs_dict.release();
     m.scs_offs.release();
     m.scs_k = m.scs_nclass = m.scs_ib = 0;
+    m.scs_seg = -1;
 }
 
-// Class of every row: rows with the same (col - base[i], value bits) list share
+// Class of every row of [r0, r1): rows with the same (col - base[i], value bits) list share
 // one; hashed in parallel, grouped serially with a full comparison.  Returns the
 // number of classes (ids in cls, one representative row per class in rep), or
 // -1 past 65536.
 static int64_t row_classes(const std::vector<int64_t> &rp, const std::vector<int32_t> &col,
-                           const std::vector<double> &val, const std::vector<int64_t> &base,
-                           std::vector<uint16_t> &cls, std::vector<int64_t> &rep) {
+                           const std::vector<double> &val, const std::vector<int64_t> &base, int64_t r0,
+                           int64_t r1, std::vector<uint16_t> &cls, std::vector<int64_t> &rep) {
     const int64_t n = (int64_t)rp.size() - 1;
     std::vector<uint64_t> h(n);
 #pragma omp parallel for schedule(static)
-    for (int64_t i = 0; i < n; i++) {
+    for (int64_t i = r0; i < r1; i++) {
         uint64_t x = 0x9E3779B97F4A7C15ull ^ (uint64_t)(rp[i + 1] - rp[i]);
         for (int64_t e = rp[i]; e < rp[i + 1]; e++) {
             uint64_t bits;
@@ -160,7 +162,7 @@ static int64_t row_classes(const std::vector<int64_t> &rp, const std::vector<int
     std::unordered_map<uint64_t, std::vector<int32_t>> by_hash;  // hash -> classes (collisions chained)
     rep.clear();
     cls.assign(n, 0);
-    for (int64_t i = 0; i < n; i++) {
+    for (int64_t i = r0; i < r1; i++) {
         auto &cands = by_hash[h[i]];
         int32_t c = -1;
         for (int32_t q : cands)
@@ -178,18 +180,34 @@ static int64_t row_classes(const std::vector<int64_t> &rp, const std::vector<int
 
 bool build_scs(GpuCsr &m, const std::vector<int64_t> &rp, int64_t other_bytes) {
     scs_release(m);
-    if (g_spmv_format_policy != 0 || scs_disabled() || m.no_sellp || m.nrows != m.ncols || m.nrows < 1024 ||
-        m.nnz == 0)
+    if (g_spmv_format_policy != 0 || scs_disabled() || m.no_sellp || m.nrows < 1024 || m.nnz == 0 ||
+        m.ncols < m.nrows)
         return false;
     const int64_t n = m.nrows;
+    // the whole matrix (square), or the longest row segment of a [owned | ghost]
+    // distributed level when its rows read owned columns only (the halo interior)
+    int64_t r0 = 0, r1 = n, seg = -1;
+    if (m.nrows != m.ncols) {
+        if (m.seg_rows.size() < 3) return false;
+        seg = 0;
+        for (size_t g = 1; g + 1 < m.seg_rows.size(); g++)
+            if (m.seg_rows[g + 1] - m.seg_rows[g] > m.seg_rows[seg + 1] - m.seg_rows[seg]) seg = (int64_t)g;
+        r0 = m.seg_rows[seg];
+        r1 = m.seg_rows[seg + 1];
+        if (r1 - r0 < 1024 || (m.has_dia() && m.dia_seg == seg)) return false;
+        other_bytes = (int64_t)((double)other_bytes * (double)(r1 - r0) / (double)n);
+    }
     hipStream_t st = m.ctx->stream;
     std::vector<int32_t> col(m.nnz);
     FAMG_CHECK_HIP(hipMemcpyAsync(col.data(), m.col.get(), m.nnz * sizeof(int32_t), hipMemcpyDeviceToHost, st));
     FAMG_CHECK_HIP(hipStreamSynchronize(st));
+    if (seg >= 0)
+        for (int64_t e = rp[r0]; e < rp[r1]; e++)
+            if (col[e] >= n) return false;  // a ghost column
     // union of the offsets: bounded first (K <= SCS_KMAX), then a bitmap over the span
     int64_t omin = INT64_MAX, omax = INT64_MIN;
 #pragma omp parallel for reduction(min : omin) reduction(max : omax) schedule(static)
-    for (int64_t i = 0; i < n; i++)
+    for (int64_t i = r0; i < r1; i++)
         for (int64_t e = rp[i]; e < rp[i + 1]; e++) {
             const int64_t o = (int64_t)col[e] - i;
             omin = std::min(omin, o);
@@ -199,7 +217,7 @@ bool build_scs(GpuCsr &m, const std::vector<int64_t> &rp, int64_t other_bytes) {
     if (span > (int64_t(1) << 26)) return false;
     std::vector<uint8_t> seen(span, 0);
 #pragma omp parallel for schedule(static)
-    for (int64_t i = 0; i < n; i++)
+    for (int64_t i = r0; i < r1; i++)
         for (int64_t e = rp[i]; e < rp[i + 1]; e++) seen[(int64_t)col[e] - i - omin] = 1;  // benign same-value race
     std::vector<int32_t> offs;
     for (int64_t o = 0; o < span; o++)
@@ -208,7 +226,7 @@ bool build_scs(GpuCsr &m, const std::vector<int64_t> &rp, int64_t other_bytes) {
             if ((int64_t)offs.size() > SCS_KMAX) return false;
         }
     const int K = (int)offs.size();
-    if (K == 0 || (double)K * (double)n > 2.0 * (double)m.nnz) return false;  // mostly padding
+    if (K == 0 || (double)K * (double)(r1 - r0) > 2.0 * (double)(rp[r1] - rp[r0])) return false;  // mostly padding
     // short stencils stay on SELL-64: A_1 of the 256^3 cycle (33 offsets, 8-bit
     // codes) ran 47 vs 44 us here; A_2 (179 offsets, 16-bit codes) 31-46 vs 55 us
     if (K < SCS_KMIN) return false;
@@ -219,12 +237,12 @@ bool build_scs(GpuCsr &m, const std::vector<int64_t> &rp, int64_t other_bytes) {
     for (int64_t i = 0; i < n; i++) base[i] = i;
     std::vector<uint16_t> cls;
     std::vector<int64_t> rep;
-    if (row_classes(rp, col, val, base, cls, rep) < 0) return false;
+    if (row_classes(rp, col, val, base, r0, r1, cls, rep) < 0) return false;
     const int64_t C = (int64_t)rep.size();
     const int Kp = (K + SCS_U - 1) / SCS_U * SCS_U;
     const int ib = C <= 256 ? 1 : 2;
     const int64_t dict_bytes = (int64_t)Kp * C * 8;
-    const int64_t stream = ib * n + dict_bytes + 4 * Kp;
+    const int64_t stream = ib * (r1 - r0) + dict_bytes + 4 * Kp;
     if (dict_bytes > (int64_t(16) << 20) || (double)stream > 0.5 * (double)other_bytes) return false;
     std::vector<double> dict((size_t)Kp * C, 0.0);
     for (int64_t c = 0; c < C; c++) {
@@ -253,6 +271,7 @@ bool build_scs(GpuCsr &m, const std::vector<int64_t> &rp, int64_t other_bytes) {
     m.scs_k = Kp;
     m.scs_nclass = C;
     m.scs_ib = ib;
+    m.scs_seg = seg;
     return true;
 }
 

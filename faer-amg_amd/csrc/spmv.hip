@@ -1816,7 +1816,7 @@ static void build_vec_codes(GpuCsr &m) {
 void choose_kernel(GpuCsr &m) {
     if (m.has_dia() && !m.dia_rowid && m.dia_r0 == 0 && m.dia_r1 == m.nrows) m.kernel = SPMV_KERNEL_DIA;
     else if (m.has_bsr()) m.kernel = SPMV_KERNEL_BSR;
-    else if (m.has_scs()) m.kernel = SPMV_KERNEL_SCS;
+    else if (m.has_scs() && m.scs_seg < 0) m.kernel = SPMV_KERNEL_SCS;
     else if (m.has_sellp()) m.kernel = SPMV_KERNEL_SELLP;
     else if (m.has_sell()) m.kernel = SPMV_KERNEL_SELL;
     else if (g_spmv_format_policy == 3 ||
@@ -1887,7 +1887,7 @@ void spmv(const GpuCsr &m, const double *x, double *y, SpmvMode mode, const Spmv
         spmv_bsr(m, x, y, mode, epi, s, seg);
         return;
     }
-    if (m.kernel == SPMV_KERNEL_SCS) {
+    if (m.kernel == SPMV_KERNEL_SCS || (m.has_scs() && seg >= 0 && seg == m.scs_seg && mode != SPMV_SGS)) {
         FAMG_REQUIRE(mode != SPMV_SGS, AMG_ERR_UNSUPPORTED, "stencil-class storage has no SGS sweep");
         spmv_scs(m, x, y, mode, epi, s, seg);
         return;

@@ -61,7 +61,7 @@ def global_reference(dims, coarsest, b, problem="7pt"):
     return z.cpu().numpy(), zref, mg.levels()
 
 
-def dist_apply(nranks, dims, coarsest, b, agglo, split_kind="slab", problem="7pt", overlap=True):
+def dist_apply(nranks, dims, coarsest, b, agglo, split_kind="slab", problem="7pt", overlap=True, storage_level=0):
     import torch
     hub = fa().LoopbackHub(nranks)
 
@@ -89,7 +89,8 @@ def dist_apply(nranks, dims, coarsest, b, agglo, split_kind="slab", problem="7pt
         # distributed stationary solve (3 cycles) as well
         x = torch.zeros_like(bl)
         it, hist = dm.stationary_solve(bl, x, max_iter=4, rel_tol=1e-300)
-        storage = dm.level_matrix(0, "A").spmv_info() if infos[0]["redundant"] == 0 else None
+        storage = (dm.level_matrix(storage_level, "A").spmv_info()
+                   if infos[storage_level]["redundant"] == 0 else None)
         return r0, r1, zl.cpu().numpy(), infos, hist, storage
 
     res = run_ranks(nranks, rank_fn)
@@ -300,3 +301,22 @@ def test_dist_eight_ranks_c4_shaped():
     h0 = res[0][4]
     for r in res[1:]:
         assert np.allclose(r[4], h0, rtol=1e-12, atol=0)
+
+
+@pytest.mark.parametrize("overlap", [True, False])
+def test_dist_stencil_classes_on_interior_segment(overlap):
+    """Two virtual ranks on 128^3: each rank's level-2 operator (16K rows of a
+    32^3 Galerkin stencil, [owned | ghost] columns) keeps its SELL-64 / CSR-stream
+    storage for the boundary planes and stencil classes for the halo-interior
+    segment (overlap path: that
+    segment alone while the halo is in flight).  V-cycle equal to the single-GPU
+    one to 1e-13 and to the oracle to 1e-11."""
+    dims = (128, 128, 128)
+    b = np.random.default_rng(17).uniform(-1, 1, int(np.prod(dims)))
+    zg, zref, nl = global_reference(dims, 100, b)
+    z, res = dist_apply(2, dims, 100, b, 1000, "slab", overlap=overlap, storage_level=2)
+    for r in res:
+        st = r[5]
+        assert st["kernel"] in ("sell", "csr-stream") and st["classes"] > 0, st
+    assert np.linalg.norm(z - zg) <= 1e-13 * np.linalg.norm(zg)
+    assert np.linalg.norm(z - zref) <= 1e-11 * np.linalg.norm(zref)
