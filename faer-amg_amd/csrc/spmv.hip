@@ -598,19 +598,27 @@ __device__ __forceinline__ void sellc_group_rp(const char *__restrict__ blk, con
                 c1[4 + u] = d3[u];
             }
         }
+    } else if constexpr (CM == 1) {
+        // the 2R u16 of rows r0, r0 + 1 as R dwords (4-B aligned: r0 is even)
+        // instead of 2R 2-B loads (P_0: 4-5 steps per row)
+        const int64_t el = (int64_t)t0 * SELL_C + R * r0;
+        const uint32_t *p = reinterpret_cast<const uint32_t *>(ixb + 2 * el);
+        uint32_t dw[R];
+#pragma unroll
+        for (int k = 0; k < R; k++) dw[k] = __builtin_nontemporal_load(p + k);
+#pragma unroll
+        for (int u = 0; u < R; u++) {
+            const int j0 = u, j1 = R + u;  // element indices of the two rows
+            c0[u] = bse[u] + (int32_t)((dw[j0 >> 1] >> (16 * (j0 & 1))) & 0xffffu);
+            c1[u] = bse[u] + (int32_t)((dw[j1 >> 1] >> (16 * (j1 & 1))) & 0xffffu);
+        }
     } else {
         const int64_t el = (int64_t)t0 * SELL_C + R * r0;  // row r0: R elements, then row r0 + 1
 #pragma unroll
         for (int u = 0; u < R; u++) {
-            if constexpr (CM == 1) {
-                const uint16_t *p = reinterpret_cast<const uint16_t *>(ixb) + el;
-                c0[u] = bse[u] + (int32_t)__builtin_nontemporal_load(p + u);
-                c1[u] = bse[u] + (int32_t)__builtin_nontemporal_load(p + R + u);
-            } else {
-                const int32_t *p = reinterpret_cast<const int32_t *>(ixb) + el;
-                c0[u] = __builtin_nontemporal_load(p + u);
-                c1[u] = __builtin_nontemporal_load(p + R + u);
-            }
+            const int32_t *p = reinterpret_cast<const int32_t *>(ixb) + el;
+            c0[u] = __builtin_nontemporal_load(p + u);
+            c1[u] = __builtin_nontemporal_load(p + R + u);
         }
     }
     double x0[R], x1[R];
