@@ -40,7 +40,7 @@ struct SellpArgs {
     const int32_t *offs;    // concatenated sorted offset patterns
     const int32_t *rbase;   // per row: column base (nullptr: the row itself)
     const double *vtab;
-    int32_t ntab, slice0, nslices, ncols, w2;
+    int32_t ntab, slice0, nslices, ncols, w2, spw;
     const double *x;
     double *y;
     const double *b;
@@ -93,15 +93,7 @@ __device__ __forceinline__ void sellp_words(const SellpArgs &a, const double *st
 }
 
 template <int MODE, int L, int VB>
-__global__ __launch_bounds__(256) void spmv_sellp_kernel(SellpArgs a) {
-    __shared__ double stab[VB ? 256 : 1];
-    if constexpr (VB != 0) {
-        for (int i = threadIdx.x; i < a.ntab; i += 256) stab[i] = a.vtab[i];
-        __syncthreads();
-    }
-    const int blk = xcd_remap(blockIdx.x, gridDim.x);
-    const int sl = __builtin_amdgcn_readfirstlane(blk * 4 + (int)(threadIdx.x >> 6));
-    if (sl >= a.nslices) return;
+__device__ __forceinline__ void sellp_slice(const SellpArgs &a, const double *stab, int sl) {
     const int s = a.slice0 + sl;
     const int lane = threadIdx.x & 63;
     const int r = lane / L, q = lane % L;
@@ -128,6 +120,8 @@ __global__ __launch_bounds__(256) void spmv_sellp_kernel(SellpArgs a) {
     double acc = 0.0;
     if constexpr (VB == 0) {
         int s0 = 0;
+        if (a.w2)  // A/B (FAMG_SELLP_W1=1: groups of 4): groups of 8 lane-steps
+            for (; s0 + 8 <= S; s0 += 8) sellp_f64<MODE, L, 8>(a, e0, off, w, s0, q, base, lane, acc);
         for (; s0 + 4 <= S; s0 += 4) sellp_f64<MODE, L, 4>(a, e0, off, w, s0, q, base, lane, acc);
         switch (S - s0) {
         case 1: sellp_f64<MODE, L, 1>(a, e0, off, w, s0, q, base, lane, acc); break;
@@ -151,6 +145,21 @@ __global__ __launch_bounds__(256) void spmv_sellp_kernel(SellpArgs a) {
         else if constexpr (MODE == SPMV_RESID) a.y[row] = br - acc;
         else a.y[row] = xr + dr * (br - acc);  // JACOBI
     }
+}
+
+// Each wave takes a.spw consecutive slices (contiguous per XCD through the
+// block remap).
+template <int MODE, int L, int VB>
+__global__ __launch_bounds__(256) void spmv_sellp_kernel(SellpArgs a) {
+    __shared__ double stab[VB ? 256 : 1];
+    if constexpr (VB != 0) {
+        for (int i = threadIdx.x; i < a.ntab; i += 256) stab[i] = a.vtab[i];
+        __syncthreads();
+    }
+    const int blk = xcd_remap(blockIdx.x, gridDim.x);
+    const int wv = __builtin_amdgcn_readfirstlane(blk * 4 + (int)(threadIdx.x >> 6));
+    const int s0 = wv * a.spw, s1 = min(s0 + a.spw, a.nslices);
+    for (int sl = s0; sl < s1; sl++) sellp_slice<MODE, L, VB>(a, stab, sl);
 }
 
 static bool sellp_disabled() {
@@ -341,6 +350,16 @@ static int sellp_w2_enabled() {
     return on;
 }
 
+// slices per wave (A/B switch FAMG_SELLP_SPW=n, default 1)
+static int sellp_spw() {
+    static const int v = [] {
+        const char *e = getenv("FAMG_SELLP_SPW");
+        const int k = e ? atoi(e) : 1;
+        return k > 0 ? k : 1;
+    }();
+    return v;
+}
+
 void spmv_sellp(const GpuCsr &m, const double *x, double *y, SpmvMode mode, const SpmvEpi &epi, hipStream_t s,
                 int64_t seg) {
     const int64_t s0 = seg < 0 ? 0 : m.sellp_seg_slc[seg];
@@ -348,8 +367,8 @@ void spmv_sellp(const GpuCsr &m, const double *x, double *y, SpmvMode mode, cons
     if (s1 <= s0) return;
     SellpArgs a{m.sellp_vals.get(), m.sellp_eoff.get(), m.sellp_row0.get(),
                 reinterpret_cast<const int2 *>(m.sellp_pat.get()), m.sellp_offs.get(), m.sellp_rbase.get(), m.sellp_vtab.get(), (int32_t)m.sellp_ntab,
-                (int32_t)s0, (int32_t)(s1 - s0), (int32_t)m.ncols, sellp_w2_enabled(), x, y, epi.b, epi.d, epi.dc, epi.dt};
-    const dim3 grid((unsigned)ceil_div(s1 - s0, 4)), block(256);
+                (int32_t)s0, (int32_t)(s1 - s0), (int32_t)m.ncols, sellp_w2_enabled(), sellp_spw(), x, y, epi.b, epi.d, epi.dc, epi.dt};
+    const dim3 grid((unsigned)ceil_div(s1 - s0, 4 * (int64_t)a.spw)), block(256);
 #define FAMG_SELLP(L, VB)                                                                          \
     switch (mode) {                                                                                \
     case SPMV_SET: spmv_sellp_kernel<SPMV_SET, L, VB><<<grid, block, 0, s>>>(a); break;            \
