@@ -24,7 +24,7 @@ import os
 import numpy as np
 
 _PKG_DIR = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(os.path.dirname(_PKG_DIR), "libfaer_amg_amd.so")
+LIB_PATH = os.environ.get("FAMG_LIB") or os.path.join(os.path.dirname(_PKG_DIR), "libfaer_amg_amd.so")
 
 if not os.path.exists(LIB_PATH):
     raise ImportError(
