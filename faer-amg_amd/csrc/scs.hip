@@ -230,6 +230,14 @@ bool build_scs(GpuCsr &m, const std::vector<int64_t> &rp, int64_t other_bytes) {
     // short stencils stay on SELL-64: A_1 of the 256^3 cycle (33 offsets, 8-bit
     // codes) ran 47 vs 44 us here; A_2 (179 offsets, 16-bit codes) 31-46 vs 55 us
     if (K < SCS_KMIN) return false;
+    // operators with a <= 256-entry value table keep SELL-64, whose codes decode
+    // from an LDS table: A_1 of the 27-pt cycle (125 offsets, 8-bit codes) ran
+    // 135 vs 121 us here (two dictionary loads per step per row pair)
+    {
+        std::vector<unsigned long long> tab;
+        const int vb = csr_value_table(m, tab);
+        if (vb == 4 || vb == 8) return false;
+    }
     std::vector<double> val(m.nnz);
     FAMG_CHECK_HIP(hipMemcpyAsync(val.data(), m.val.get(), m.nnz * sizeof(double), hipMemcpyDeviceToHost, st));
     FAMG_CHECK_HIP(hipStreamSynchronize(st));

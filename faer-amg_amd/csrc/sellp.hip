@@ -201,6 +201,11 @@ bool build_sellp(GpuCsr &m, const std::vector<int64_t> &rp, int64_t other_bytes)
     if (vb == 16) return false;  // SELL-64 16-bit codes (see the header)
     const double avg = (double)m.nnz / (double)n;
     if (vb == 0 && m.nnz < 48 * n) return false;
+    // coded rows need >= 16 entries: one lane per short row plus its column base
+    // cost more than the bytes save (P_0: 4-8 entries per row, 124 -> 131-155 us
+    // on the 7-pt and 153 -> 167 us on the 27-pt cycle; R_0, 32-64 entries:
+    // 83 -> 64 and 137 -> 91 us)
+    if (vb != 0 && m.nnz < 16 * n) return false;
     // lanes per row: enough waves to fill the chip (>= 32K), >= 8 steps per lane
     int L = 1;
     while (L < 64 && (n * L) / 64 < 32768 && avg / (2 * L) >= 8) L *= 2;

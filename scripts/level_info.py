@@ -1,7 +1,7 @@
 """Print the SpMV storage of every operator of the bench hierarchy (A_l, R_l, P_l):
 kernel, stream bytes, value-code bits and table size.  GPU box only.
 
-  python scripts/level_info.py [--edge 256]
+  python scripts/level_info.py [--edge 256] [--problem 7pt|27pt]
 """
 import argparse
 import json
@@ -15,11 +15,16 @@ import faer_amg_amd as fa  # noqa: E402
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--edge", type=int, default=256)
+    ap.add_argument("--problem", choices=("7pt", "27pt"), default="7pt")
     args = ap.parse_args()
     ctx = fa.Context()
     dims = (args.edge,) * 3
-    A = fa.SparseMatOp.laplace3d_7pt(ctx, *dims)
-    mg = fa.sa_build_box(A, dims, (2, 2, 2), coarsest_dim=1000, smoother="jacobi")
+    if args.problem == "7pt":
+        A = fa.SparseMatOp.laplace3d_7pt(ctx, *dims)
+        mg = fa.sa_build_box(A, dims, (2, 2, 2), coarsest_dim=1000, smoother="jacobi")
+    else:
+        A = fa.SparseMatOp.aniso27(ctx, *dims, 1.0, 1.0, 0.01)
+        mg = fa.sa_build_box(A, dims, (2, 2, 2), coarsest_dim=1000, smoother="sgs")
     for l in range(mg.levels()):
         a, _, r, p = mg.level(l)
         for name, M in (("A", a), ("R", r), ("P", p)):

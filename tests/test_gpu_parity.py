@@ -954,10 +954,10 @@ def test_sellp_dense_coarse_levels(ctx):
 
 def test_sellp_coded_transfer_operators(ctx):
     """Pattern SELL with 4-bit codes and per-row column bases (rectangular,
-    implicit columns) on a synthetic structured interpolation P (12 entries per
+    implicit columns) on a synthetic structured interpolation P (20 entries per
     row around row // 16, four distinct values) and R = P^T: storage picked
-    automatically, P (one lane per row) bitwise equal to the oracle's row sums,
-    R within the summation-order bound, and a two-level V-cycle on a DIA fine
+    automatically, P and R (two and more lanes per row) within the
+    summation-order bound of the oracle's row sums, and a two-level V-cycle on a DIA fine
     level within 1e-11 of the oracle with and without the zero-guess fold (P in
     ADD0, else ADD; R in SET)."""
     import scipy.sparse as sp
@@ -966,12 +966,12 @@ def test_sellp_coded_transfer_operators(ctx):
     nf = A.nrows
     nc = (nf + 15) // 16
     rows, cols, data = [], [], []
-    for k in range(12):  # 1.0 on the row's own coarse column, small couplings around it
+    for k in range(20):  # 1.0 on the row's own coarse column, small couplings around it
         i = np.arange(nf)
-        c = i // 16 + k - 5
+        c = i // 16 + k - 9
         ok = (c >= 0) & (c < nc)
         rows.append(i[ok]); cols.append(c[ok])
-        data.append(np.full(ok.sum(), 1.0) if k == 5 else 0.125 * (1 + (i[ok] + k) % 3))
+        data.append(np.full(ok.sum(), 1.0) if k == 9 else 0.125 * (1 + (i[ok] + k) % 3))
     Ps = sp.csr_matrix((np.concatenate(data), (np.concatenate(rows), np.concatenate(cols))), shape=(nf, nc))
     Ps.sort_indices()
     Rs = Ps.T.tocsr()
@@ -984,7 +984,8 @@ def test_sellp_coded_transfer_operators(ctx):
     rng = np.random.default_rng(77)
     OP, OR = O.Csr.from_scipy(Ps), O.Csr.from_scipy(Rs)
     xc = rng.standard_normal(nc)
-    assert np.array_equal(apply_dev(ctx, P, xc, nf), OP.spmv(xc))
+    yp = apply_dev(ctx, P, xc, nf)
+    assert np.all(np.abs(yp - OP.spmv(xc)) <= spmv_bound(Ps, xc))
     xf = rng.standard_normal(nf)
     yr = apply_dev(ctx, R, xf, nc)
     assert np.all(np.abs(yr - OR.spmv(xf)) <= spmv_bound(Rs, xf))
