@@ -1008,7 +1008,31 @@ template <int MODE, bool NT> struct DiaEpi {
 // join.  The value table (and the coded diagonal's table) is fetched first and
 // published to LDS behind an LDS-only barrier after the row loads are issued,
 // so they stay in flight across it.
-template <int MODE, int VB, int CW, bool NT>
+// x[c .. c+3] of rows (r, r+1) for a run of three diagonals (offsets o-1, o, o+1,
+// c = r + o - 1) from two 16-B loads at clamp(c) and clamp(c + 2); selects keep
+// every in-range position exact at the matrix edges (out-of-range positions
+// belong to +0.0 terms).
+template <int MODE>
+__device__ __forceinline__ void dia_gx4(const Epi &e, int c, int ncols, double (&v)[4]) {
+    const int p0 = min(max(c, 0), ncols - 2), p1 = min(max(c + 2, 0), ncols - 2);
+    dbl2_t q0 = *reinterpret_cast<const dbl2u_t *>(e.x + p0);
+    dbl2_t q1 = *reinterpret_cast<const dbl2u_t *>(e.x + p1);
+    if constexpr (MODE == SPMV_RESID0) {
+        q0 = *reinterpret_cast<const dbl2u_t *>(e.d + p0) * q0;
+        q1 = *reinterpret_cast<const dbl2u_t *>(e.d + p1) * q1;
+    }
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+        const int t = c + j;
+        v[j] = t == p0 ? q0.x : t == p0 + 1 ? q0.y : t == p1 ? q1.x : q1.y;
+    }
+}
+
+// NR > 0: the K = 3 NR diagonals come in runs of three consecutive offsets (a
+// 27-point stencil: NR = 9); a row pair's three x operands per run are four
+// consecutive values, two 16-B loads instead of three and 4 NR instead of 2 KMAX
+// registers.  The row sums run over the same diagonals in the same order.
+template <int MODE, int VB, int CW, bool NT, int NR = 0>
 __global__ __launch_bounds__(256) void spmv_dia_kernel(DiaArgs a) {
     constexpr bool DC = MODE == DIA_JACOBI_DC;
     constexpr int GM = DC ? SPMV_JACOBI : MODE;  // x operand of the row sums
@@ -1030,14 +1054,21 @@ __global__ __launch_bounds__(256) void spmv_dia_kernel(DiaArgs a) {
     const int row = a.row_begin + 512 * blk + 2 * (int)threadIdx.x;
     constexpr int KMAX = CW * 32 / VB < DIA_MAX ? CW * 32 / VB : DIA_MAX;
     constexpr uint32_t MASK = (1u << VB) - 1;
+    constexpr int KX = NR > 0 ? 1 : KMAX;  // per-diagonal operands (generic path)
+    constexpr int NRX = NR > 0 ? NR : 1;   // per-run operands (run path)
     DiaEpi<MODE, NT> ep;
     uint32_t w0[CW], w1[CW];
-    double x0[KMAX], x1[KMAX];
+    double x0[KX], x1[KX], xq[NRX][4];
     ep.load_codes(a.e, row, a.row_end);
     ep.load(a.e, row, a.row_end);
     dia_codes2<CW>(a.codes + (int64_t)(min(row, a.row_end - 1) - a.code_row0) * CW, w0, w1);
+    if constexpr (NR > 0) {
 #pragma unroll
-    for (int k = 0; k < KMAX; k++) dia_gx2<GM>(a.e, row + a.off[k], a.ncols, x0[k], x1[k]);
+        for (int j = 0; j < NR; j++) dia_gx4<GM>(a.e, row + a.off[3 * j], a.ncols, xq[j]);
+    } else {
+#pragma unroll
+        for (int k = 0; k < KMAX; k++) dia_gx2<GM>(a.e, row + a.off[k], a.ncols, x0[k], x1[k]);
+    }
     if ((int)threadIdx.x < a.ntab) stab[threadIdx.x] = tv;
     if constexpr (DC) sdt[threadIdx.x] = dv;
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
@@ -1045,12 +1076,20 @@ __global__ __launch_bounds__(256) void spmv_dia_kernel(DiaArgs a) {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
     if (row >= a.row_end) return;
     double acc0 = 0.0, acc1 = 0.0;
+    if constexpr (NR > 0) {
 #pragma unroll
-    for (int k = 0; k < KMAX; k++) {
-        const double f0 = fma(stab[(w0[(k * VB) >> 5] >> ((k * VB) & 31)) & MASK], x0[k], acc0);
-        const double f1 = fma(stab[(w1[(k * VB) >> 5] >> ((k * VB) & 31)) & MASK], x1[k], acc1);
-        acc0 = k < a.k ? f0 : acc0;
-        acc1 = k < a.k ? f1 : acc1;
+        for (int k = 0; k < 3 * NR; k++) {
+            acc0 = fma(stab[(w0[(k * VB) >> 5] >> ((k * VB) & 31)) & MASK], xq[k / 3][k % 3], acc0);
+            acc1 = fma(stab[(w1[(k * VB) >> 5] >> ((k * VB) & 31)) & MASK], xq[k / 3][k % 3 + 1], acc1);
+        }
+    } else {
+#pragma unroll
+        for (int k = 0; k < KMAX; k++) {
+            const double f0 = fma(stab[(w0[(k * VB) >> 5] >> ((k * VB) & 31)) & MASK], x0[k], acc0);
+            const double f1 = fma(stab[(w1[(k * VB) >> 5] >> ((k * VB) & 31)) & MASK], x1[k], acc1);
+            acc0 = k < a.k ? f0 : acc0;
+            acc1 = k < a.k ? f1 : acc1;
+        }
     }
     ep.store(a.e, sdt, acc0, acc1);
 }
@@ -1060,7 +1099,9 @@ __global__ __launch_bounds__(256) void spmv_dia_kernel(DiaArgs a) {
 // x[i] <- x[i] + d[p] (b[i] - sum_k a_k x[i + off_k]) in place (rows of one
 // color never couple).  Loads branch-free as in spmv_dia_kernel; padding
 // entries (code of +0.0) read a clamped in-range x and add exact zeros.
-template <int VB, int CW>
+// NR > 0: nine runs of three consecutive offsets (27-point stencil), each run's
+// x[c], x[c+1], x[c+2] from one 16-B and one 8-B load (18 loads instead of 32).
+template <int VB, int CW, int NR = 0>
 __global__ __launch_bounds__(256) void spmv_dia_sgs_kernel(DiaArgs a, const int32_t *rowid) {
     __shared__ double stab[VB == 4 ? 16 : 256];
     const double tv = (int)threadIdx.x < a.ntab ? a.vtab[threadIdx.x] : 0.0;
@@ -1087,9 +1128,25 @@ __global__ __launch_bounds__(256) void spmv_dia_sgs_kernel(DiaArgs a, const int3
     }
     const int i = rowid[pc];
     const double xr = a.e.x[i], br = a.e.b[i], dr = a.e.d[pc];
-    double xv[KMAX];
+    constexpr int KX = NR > 0 ? 3 * NR : KMAX;
+    double xv[KX];
+    if constexpr (NR > 0) {
 #pragma unroll
-    for (int k = 0; k < KMAX; k++) xv[k] = a.e.x[min(max(i + a.off[k], 0), a.ncols - 1)];
+        for (int j = 0; j < NR; j++) {
+            const int c = i + a.off[3 * j];
+            const int p0 = min(max(c, 0), a.ncols - 2);
+            const dbl2_t q = *reinterpret_cast<const dbl2u_t *>(a.e.x + p0);
+            const double s2 = a.e.x[min(max(c + 2, 0), a.ncols - 1)];
+#pragma unroll
+            for (int u = 0; u < 3; u++) {
+                const int t = c + u;
+                xv[3 * j + u] = t == p0 ? q.x : t == p0 + 1 ? q.y : s2;
+            }
+        }
+    } else {
+#pragma unroll
+        for (int k = 0; k < KMAX; k++) xv[k] = a.e.x[min(max(i + a.off[k], 0), a.ncols - 1)];
+    }
     if ((int)threadIdx.x < a.ntab) stab[threadIdx.x] = tv;
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
     __builtin_amdgcn_s_barrier();
@@ -1097,9 +1154,9 @@ __global__ __launch_bounds__(256) void spmv_dia_sgs_kernel(DiaArgs a, const int3
     if (p >= a.row_end) return;
     double acc = 0.0;
 #pragma unroll
-    for (int k = 0; k < KMAX; k++) {
+    for (int k = 0; k < KX; k++) {
         const double f = fma(stab[(w[(k * VB) >> 5] >> ((k * VB) & 31)) & MASK], xv[k], acc);
-        acc = k < a.k ? f : acc;
+        acc = (NR > 0 || k < a.k) ? f : acc;
     }
     a.e.y[i] = xr + dr * (br - acc);
 }
@@ -1883,6 +1940,27 @@ void spmm(const GpuCsr &m, const double *x, int64_t ldx, double *y, int64_t ldy,
     }
 }
 
+template <int M, int VB, int CW>
+static void launch_dia(bool runs9, bool nt, dim3 grid, dim3 block, hipStream_t s, const DiaArgs &a) {
+    if constexpr (CW * 32 / VB >= 27) {
+        if (runs9) {
+            spmv_dia_kernel<M, VB, CW, false, 9><<<grid, block, 0, s>>>(a);
+            return;
+        }
+    }
+    if (nt) spmv_dia_kernel<M, VB, CW, true><<<grid, block, 0, s>>>(a);
+    else spmv_dia_kernel<M, VB, CW, false><<<grid, block, 0, s>>>(a);
+}
+
+// A/B switch FAMG_DIA_RUNS=0: the 27-point DIA kernels load every diagonal's pair
+static bool dia_runs() {
+    static const bool on = [] {
+        const char *e = getenv("FAMG_DIA_RUNS");
+        return !(e && e[0] == '0');
+    }();
+    return on;
+}
+
 void spmv(const GpuCsr &m, const double *x, double *y, SpmvMode mode, const SpmvEpi &epi,
           hipStream_t s, int64_t seg) {
     FAMG_REQUIRE(m.spmv_ready(), AMG_ERR_UNSUPPORTED, "SpMV needs nnz < 2^31 (32-bit row pointers)");
@@ -1922,6 +2000,19 @@ void spmv(const GpuCsr &m, const double *x, double *y, SpmvMode mode, const Spmv
         for (int k = 0; k < m.dia_k; k++) a.off[k] = m.dia_off[k];
         a.e = e;
         const dim3 grid((unsigned)ceil_div(r1 - r0, 256));
+        bool runs9 = m.dia_k == 27 && dia_runs();
+        for (int j = 0; runs9 && j < 9; j++)
+            runs9 = m.dia_off[3 * j + 1] == m.dia_off[3 * j] + 1 && m.dia_off[3 * j + 2] == m.dia_off[3 * j] + 2;
+        if (runs9 && m.dia_vbits == 4 && m.dia_cw == 4) {
+            spmv_dia_sgs_kernel<4, 4, 9><<<grid, block, 0, s>>>(a, m.dia_rowid);
+            FAMG_CHECK_HIP(hipGetLastError());
+            return;
+        }
+        if (runs9 && m.dia_vbits == 8 && m.dia_cw == 8) {
+            spmv_dia_sgs_kernel<8, 8, 9><<<grid, block, 0, s>>>(a, m.dia_rowid);
+            FAMG_CHECK_HIP(hipGetLastError());
+            return;
+        }
         switch (m.dia_vbits * 16 + m.dia_cw) {
         case 4 * 16 + 1: spmv_dia_sgs_kernel<4, 1><<<grid, block, 0, s>>>(a, m.dia_rowid); break;
         case 4 * 16 + 2: spmv_dia_sgs_kernel<4, 2><<<grid, block, 0, s>>>(a, m.dia_rowid); break;
@@ -1963,9 +2054,11 @@ void spmv(const GpuCsr &m, const double *x, double *y, SpmvMode mode, const Spmv
         const dim3 grid((unsigned)ceil_div(r1 - r0, 512));
         const int key = m.dia_vbits * 16 + m.dia_cw;
         const bool nt = dia_nt();
-#define FAMG_DIA2(M, VB, CW)                                                                      \
-    if (nt) spmv_dia_kernel<M, VB, CW, true><<<grid, block, 0, s>>>(a);                          \
-    else spmv_dia_kernel<M, VB, CW, false><<<grid, block, 0, s>>>(a);
+        // 27 diagonals in nine runs of three consecutive offsets (27-point stencil)
+        bool runs9 = m.dia_k == 27 && dia_runs();
+        for (int j = 0; runs9 && j < 9; j++)
+            runs9 = m.dia_off[3 * j + 1] == m.dia_off[3 * j] + 1 && m.dia_off[3 * j + 2] == m.dia_off[3 * j] + 2;
+#define FAMG_DIA2(M, VB, CW) launch_dia<M, VB, CW>(runs9, nt, grid, block, s, a);
 #define FAMG_DIA(VB, CW)                                                                          \
     switch (mode) {                                                                               \
     case SPMV_SET: FAMG_DIA2(SPMV_SET, VB, CW) break;                                             \
