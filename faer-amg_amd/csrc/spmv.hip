@@ -1031,7 +1031,8 @@ __device__ __forceinline__ void dia_gx4(const Epi &e, int c, int ncols, double (
 // NR > 0: the K = 3 NR diagonals come in runs of three consecutive offsets (a
 // 27-point stencil: NR = 9); a row pair's three x operands per run are four
 // consecutive values, two 16-B loads instead of three and 4 NR instead of 2 KMAX
-// registers.  The row sums run over the same diagonals in the same order.
+// registers.  NR = -1: the 7-point pattern (single, single, run of three,
+// single, single).  The row sums run over the same diagonals in the same order.
 template <int MODE, int VB, int CW, bool NT, int NR = 0>
 __global__ __launch_bounds__(256) void spmv_dia_kernel(DiaArgs a) {
     constexpr bool DC = MODE == DIA_JACOBI_DC;
@@ -1054,17 +1055,24 @@ __global__ __launch_bounds__(256) void spmv_dia_kernel(DiaArgs a) {
     const int row = a.row_begin + 512 * blk + 2 * (int)threadIdx.x;
     constexpr int KMAX = CW * 32 / VB < DIA_MAX ? CW * 32 / VB : DIA_MAX;
     constexpr uint32_t MASK = (1u << VB) - 1;
-    constexpr int KX = NR > 0 ? 1 : KMAX;  // per-diagonal operands (generic path)
-    constexpr int NRX = NR > 0 ? NR : 1;   // per-run operands (run path)
+    constexpr int KX = NR != 0 ? 1 : KMAX;  // per-diagonal operands (generic path)
+    constexpr int NRX = NR > 0 ? NR : 1;    // per-run operands (run path)
     DiaEpi<MODE, NT> ep;
     uint32_t w0[CW], w1[CW];
     double x0[KX], x1[KX], xq[NRX][4];
     ep.load_codes(a.e, row, a.row_end);
     ep.load(a.e, row, a.row_end);
     dia_codes2<CW>(a.codes + (int64_t)(min(row, a.row_end - 1) - a.code_row0) * CW, w0, w1);
+    double xs7[4][2];  // NR == -1 (7-point): the four single diagonals
     if constexpr (NR > 0) {
 #pragma unroll
         for (int j = 0; j < NR; j++) dia_gx4<GM>(a.e, row + a.off[3 * j], a.ncols, xq[j]);
+    } else if constexpr (NR == -1) {
+        dia_gx2<GM>(a.e, row + a.off[0], a.ncols, xs7[0][0], xs7[0][1]);
+        dia_gx2<GM>(a.e, row + a.off[1], a.ncols, xs7[1][0], xs7[1][1]);
+        dia_gx4<GM>(a.e, row + a.off[2], a.ncols, xq[0]);
+        dia_gx2<GM>(a.e, row + a.off[5], a.ncols, xs7[2][0], xs7[2][1]);
+        dia_gx2<GM>(a.e, row + a.off[6], a.ncols, xs7[3][0], xs7[3][1]);
     } else {
 #pragma unroll
         for (int k = 0; k < KMAX; k++) dia_gx2<GM>(a.e, row + a.off[k], a.ncols, x0[k], x1[k]);
@@ -1076,7 +1084,15 @@ __global__ __launch_bounds__(256) void spmv_dia_kernel(DiaArgs a) {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
     if (row >= a.row_end) return;
     double acc0 = 0.0, acc1 = 0.0;
-    if constexpr (NR > 0) {
+    if constexpr (NR == -1) {
+#pragma unroll
+        for (int k = 0; k < 7; k++) {
+            const double y0 = k < 2 ? xs7[k][0] : k < 5 ? xq[0][k - 2] : xs7[k - 3][0];
+            const double y1 = k < 2 ? xs7[k][1] : k < 5 ? xq[0][k - 1] : xs7[k - 3][1];
+            acc0 = fma(stab[(w0[(k * VB) >> 5] >> ((k * VB) & 31)) & MASK], y0, acc0);
+            acc1 = fma(stab[(w1[(k * VB) >> 5] >> ((k * VB) & 31)) & MASK], y1, acc1);
+        }
+    } else if constexpr (NR > 0) {
 #pragma unroll
         for (int k = 0; k < 3 * NR; k++) {
             acc0 = fma(stab[(w0[(k * VB) >> 5] >> ((k * VB) & 31)) & MASK], xq[k / 3][k % 3], acc0);
@@ -1941,10 +1957,16 @@ void spmm(const GpuCsr &m, const double *x, int64_t ldx, double *y, int64_t ldy,
 }
 
 template <int M, int VB, int CW>
-static void launch_dia(bool runs9, bool nt, dim3 grid, dim3 block, hipStream_t s, const DiaArgs &a) {
+static void launch_dia(int runs, bool nt, dim3 grid, dim3 block, hipStream_t s, const DiaArgs &a) {
     if constexpr (CW * 32 / VB >= 27) {
-        if (runs9) {
+        if (runs == 9) {
             spmv_dia_kernel<M, VB, CW, false, 9><<<grid, block, 0, s>>>(a);
+            return;
+        }
+    }
+    if constexpr (CW * 32 / VB >= 7) {
+        if (runs == -1) {
+            spmv_dia_kernel<M, VB, CW, false, -1><<<grid, block, 0, s>>>(a);
             return;
         }
     }
@@ -1956,6 +1978,15 @@ static void launch_dia(bool runs9, bool nt, dim3 grid, dim3 block, hipStream_t s
 static bool dia_runs() {
     static const bool on = [] {
         const char *e = getenv("FAMG_DIA_RUNS");
+        return !(e && e[0] == '0');
+    }();
+    return on;
+}
+
+// A/B switch FAMG_DIA_RUNS7=0: the 7-point DIA kernels load every diagonal's pair
+static bool dia_runs7() {
+    static const bool on = [] {
+        const char *e = getenv("FAMG_DIA_RUNS7");
         return !(e && e[0] == '0');
     }();
     return on;
@@ -2054,11 +2085,15 @@ void spmv(const GpuCsr &m, const double *x, double *y, SpmvMode mode, const Spmv
         const dim3 grid((unsigned)ceil_div(r1 - r0, 512));
         const int key = m.dia_vbits * 16 + m.dia_cw;
         const bool nt = dia_nt();
-        // 27 diagonals in nine runs of three consecutive offsets (27-point stencil)
+        // 27 diagonals in nine runs of three consecutive offsets (27-point
+        // stencil), or the 7-point pattern with its x run in the middle
         bool runs9 = m.dia_k == 27 && dia_runs();
         for (int j = 0; runs9 && j < 9; j++)
             runs9 = m.dia_off[3 * j + 1] == m.dia_off[3 * j] + 1 && m.dia_off[3 * j + 2] == m.dia_off[3 * j] + 2;
-#define FAMG_DIA2(M, VB, CW) launch_dia<M, VB, CW>(runs9, nt, grid, block, s, a);
+        const bool run7 = m.dia_k == 7 && dia_runs7() && m.dia_off[3] == m.dia_off[2] + 1 &&
+                          m.dia_off[4] == m.dia_off[2] + 2;
+        const int runs9i = runs9 ? 9 : run7 ? -1 : 0;
+#define FAMG_DIA2(M, VB, CW) launch_dia<M, VB, CW>(runs9i, nt, grid, block, s, a);
 #define FAMG_DIA(VB, CW)                                                                          \
     switch (mode) {                                                                               \
     case SPMV_SET: FAMG_DIA2(SPMV_SET, VB, CW) break;                                             \
