@@ -59,6 +59,7 @@ struct GpuCsr {
     int64_t nslices = 0, sell_steps = 0, sell_bytes = 0;
     int64_t sell_mode_slices[3] = {0, 0, 0};  // slices per column mode (implicit, u16, i32)
     bool sell_paired = true;  // step-pair layout (16-B value loads); false: one step per 512-B row
+    bool sell_short = false;  // coded slices of <= 4 steps in equal pairs (spmv_sell_short_kernel)
     // value codes (spmv.hip "value codes"): 0 = fp64 values, else 4/8/16-bit codes
     // into sell_vtab (sell_ntab distinct bit patterns, ascending)
     int sell_vbits = 0;

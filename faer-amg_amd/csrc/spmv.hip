@@ -877,6 +877,53 @@ __global__ __launch_bounds__(256) void spmv_sell_kernel(SellArgs a) {
     }
 }
 
+// Value-code SELL whose slices are all at most 4 steps wide with implicit or
+// u16 columns and pair up (equal width and column mode): P_0 of a box
+// hierarchy (4 entries per row).  Only the lockstep row-pair path of
+// spmv_sell_kernel, with R = w known per case: a fraction of the generic
+// kernel's registers (which it sizes for 8-step groups of every layout), so
+// more waves keep their loads in flight.  Same row sums in the same order.
+template <int MODE, int LAY>
+__global__ __launch_bounds__(256) void spmv_sell_short_kernel(SellArgs a) {
+    constexpr int TABN = LAY == 4 ? 16 : LAY == 8 ? 256 : 1;
+    __shared__ double stab[TABN];
+    if constexpr (LAY == 4 || LAY == 8) {
+        for (int i = threadIdx.x; i < a.ntab; i += 256) stab[i] = a.vtab[i];
+        __syncthreads();
+    }
+    const double *tab = LAY == 16 ? a.vtab : stab;
+    const int blk = xcd_remap(blockIdx.x, gridDim.x);
+    const int sl = 2 * __builtin_amdgcn_readfirstlane(blk * 4 + (int)(threadIdx.x >> 6));
+    if (sl >= a.nslices) return;
+    const int slice = a.slice0 + sl;
+    const int lane = threadIdx.x & 63;
+    const int ta = a.soff[slice], tb = a.soff[slice + 1];
+    const uint32_t da = a.desc[slice], db = a.desc[slice + 1];
+    const bool hb = lane >= 32;
+    const int rs = hb ? a.row0[slice + 1] : a.row0[slice];
+    const int re = hb ? a.row0[slice + 2] : a.row0[slice + 1];
+    const int row = rs + 2 * (lane & 31);
+    EpiOps2<MODE> ep2;
+    ep2.load(a.e, row, row < re, row + 1 < re);
+    const char *blk2 = a.data + (int64_t)((hb ? db : da) & 0x3fffffffu) * 128;
+    const char *ixb = blk2 + (int64_t)SELL_C * sell_code_bytes(LAY);
+    const int32_t *sa = a.base + ta, *sbp = a.base + tb;
+    const int r0 = 2 * (lane & 31);
+    double acc0 = 0.0, acc1 = 0.0;
+    switch ((int)(da >> 30) * 8 + (tb - ta)) {
+    case 1: sellc_group_rp<MODE, 0, LAY, 1>(blk2, ixb, 0, sa, sbp, hb, r0, tab, a.e, acc0, acc1); break;
+    case 2: sellc_group_rp<MODE, 0, LAY, 2>(blk2, ixb, 0, sa, sbp, hb, r0, tab, a.e, acc0, acc1); break;
+    case 3: sellc_group_rp<MODE, 0, LAY, 3>(blk2, ixb, 0, sa, sbp, hb, r0, tab, a.e, acc0, acc1); break;
+    case 4: sellc_group_rp<MODE, 0, LAY, 4>(blk2, ixb, 0, sa, sbp, hb, r0, tab, a.e, acc0, acc1); break;
+    case 9: sellc_group_rp<MODE, 1, LAY, 1>(blk2, ixb, 0, sa, sbp, hb, r0, tab, a.e, acc0, acc1); break;
+    case 10: sellc_group_rp<MODE, 1, LAY, 2>(blk2, ixb, 0, sa, sbp, hb, r0, tab, a.e, acc0, acc1); break;
+    case 11: sellc_group_rp<MODE, 1, LAY, 3>(blk2, ixb, 0, sa, sbp, hb, r0, tab, a.e, acc0, acc1); break;
+    case 12: sellc_group_rp<MODE, 1, LAY, 4>(blk2, ixb, 0, sa, sbp, hb, r0, tab, a.e, acc0, acc1); break;
+    default: break;  // width 0
+    }
+    ep2.store(a.e, acc0, acc1);
+}
+
 // ---------------------------------------------------------------- DIA codes
 //
 // A square matrix whose entries lie on at most DIA_MAX diagonals (the union of
@@ -1732,6 +1779,7 @@ void build_sell(GpuCsr &m, const std::vector<int64_t> &rp) {
     m.nslices = m.sell_steps = m.sell_bytes = m.sell_ntab = 0;
     m.sell_vbits = 0;
     m.sell_mode_slices[0] = m.sell_mode_slices[1] = m.sell_mode_slices[2] = 0;
+    m.sell_short = false;
     m.seg_slc.clear();
     const int pol = g_spmv_format_policy;
     if (pol == 1 || pol == 3 || m.nrows == 0 || m.nnz == 0) return;
@@ -1821,6 +1869,14 @@ void build_sell(GpuCsr &m, const std::vector<int64_t> &rp) {
     m.sell_ntab = vb ? (int64_t)tab.size() : 0;
     for (int k = 0; k < 3; k++) m.sell_mode_slices[k] = cnt[k];
     m.seg_slc = seg_slc;
+    // short slices (coded, <= 4 steps, implicit / u16 columns, pairs of equal
+    // width and column mode, one row segment): spmv_sell_short_kernel
+    bool sh = vb != 0 && ns % 2 == 0 && cnt[2] == 0 && m.seg_rows.size() == 2;
+    for (int64_t k = 0; sh && k < ns; k += 2) {
+        const int32_t wa = soff[k + 1] - soff[k], wb = soff[k + 2] - soff[k + 1];
+        sh = wa <= 4 && wa == wb && (desc[k] >> 30) == (desc[k + 1] >> 30) && row0[k + 1] - row0[k] == 64;
+    }
+    m.sell_short = sh;
 }
 
 // ---- wave-per-row storage: value codes (8/16-bit) and 16-bit row offsets
@@ -1983,6 +2039,15 @@ static bool dia_runs() {
     return on;
 }
 
+// A/B switch FAMG_SELL_SHORT=0: short-slice operators take the generic SELL kernel
+static bool sell_short_enabled() {
+    static const bool on = [] {
+        const char *e = getenv("FAMG_SELL_SHORT");
+        return !(e && e[0] == '0');
+    }();
+    return on;
+}
+
 // A/B switch FAMG_DIA_RUNS7=0: the 7-point DIA kernels load every diagonal's pair
 static bool dia_runs7() {
     static const bool on = [] {
@@ -2133,7 +2198,16 @@ void spmv(const GpuCsr &m, const double *x, double *y, SpmvMode mode, const Spmv
         const int lay = m.sell_vbits ? 4 : 0;
         if (sell_slices_per_wave(lay, mode) == 2 && s1 - s0 >= SELL_PAIR_MIN_SLICES) a.spw = 2;
         const dim3 grid((unsigned)ceil_div(s1 - s0, 4 * a.spw * sell_groups_per_wave(lay)));
-        if (m.sell_vbits == 4) {
+        if (m.sell_short && seg < 0 && mode != SPMV_SGS && mode != SPMV_RESID0 && sell_short_enabled()) {
+            const dim3 g2((unsigned)ceil_div(s1 - s0, 8));
+            if (m.sell_vbits == 4) {
+                FAMG_LAUNCH_MODES(spmv_sell_short_kernel, g2, block, s, a, FAMG_LAY4)
+            } else if (m.sell_vbits == 8) {
+                FAMG_LAUNCH_MODES(spmv_sell_short_kernel, g2, block, s, a, FAMG_LAY8)
+            } else {
+                FAMG_LAUNCH_MODES(spmv_sell_short_kernel, g2, block, s, a, FAMG_LAY16)
+            }
+        } else if (m.sell_vbits == 4) {
             FAMG_LAUNCH_MODES(spmv_sell_kernel, grid, block, s, a, FAMG_LAY4)
         } else if (m.sell_vbits == 8) {
             FAMG_LAUNCH_MODES(spmv_sell_kernel, grid, block, s, a, FAMG_LAY8)
