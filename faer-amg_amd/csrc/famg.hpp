@@ -71,6 +71,7 @@ struct GpuCsr {
     DevBuf<double> dia_vtab;
     int64_t dia_ntab = 0;
     int dia_k = 0, dia_cw = 0, dia_vbits = 0;
+    int dia_pat = 0;  // > 32 diagonals: the run pattern (spmv_dia_pat_kernel)
     std::vector<int> dia_off;
     // DIA row range: the whole matrix (kernel == DIA) or one row segment
     // (dia_seg, e.g. the halo interior of a distributed level) beside SELL

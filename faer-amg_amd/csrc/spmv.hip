@@ -935,7 +935,7 @@ __global__ __launch_bounds__(256) void spmv_sell_short_kernel(SellArgs a) {
 // row's only dependent chain is code + x loads -> fma -> store; each lane takes
 // two adjacent rows (16-B accesses throughout).  x indices outside [0, ncols)
 // belong to padding entries (value 0.0) and are clamped.
-constexpr int DIA_MAX = 32;
+constexpr int DIA_MAX = 40;  // 32 for the generic kernels; longer stencils through a run pattern
 
 struct DiaArgs {
     const uint32_t *codes;  // cw words per row (rows padded by 2)
@@ -1155,6 +1155,158 @@ __global__ __launch_bounds__(256) void spmv_dia_kernel(DiaArgs a) {
         }
     }
     ep.store(a.e, sdt, acc0, acc1);
+}
+
+// Run patterns of longer stencils (more than 32 diagonals): the lengths of the
+// runs of consecutive offsets, ascending.  PAT 33: the Galerkin operator of
+// smoothed aggregation on 2^3 boxes of the 7-point operator (A_1 of the C2
+// cycle: the 27 neighbours in {-1,0,1}^3 plus +-2 along each axis) --
+// z-2 | three x runs in z-1 | y-2 | x run | x run of five | x run | y+2 |
+// three x runs in z+1 | z+2.
+// PAT 27: the 27-point stencil, nine x runs of three.
+__host__ __device__ constexpr int dia_pat_nrun(int pat) { return pat == 33 ? 13 : pat == 27 ? 9 : 0; }
+__host__ __device__ constexpr int dia_pat_len(int pat, int j) {
+    return pat == 33 ? (j == 0 || j == 4 || j == 8 || j == 12 ? 1 : j == 6 ? 5 : 3) : pat == 27 ? 3 : 0;
+}
+__host__ __device__ constexpr int dia_pat_k(int pat) {
+    int s = 0;
+    for (int j = 0; j < dia_pat_nrun(pat); j++) s += dia_pat_len(pat, j);
+    return s;
+}
+// x registers of run j for a row pair: L + 1 values from (L + 2) / 2 16-B loads
+__host__ __device__ constexpr int dia_pat_nq(int pat, int j) { return (dia_pat_len(pat, j) + 2) / 2; }
+__host__ __device__ constexpr int dia_pat_nv(int pat) {
+    int s = 0;
+    for (int j = 0; j < dia_pat_nrun(pat); j++) s += 2 * dia_pat_nq(pat, j);
+    return s;
+}
+
+// The DIA kernel for a run pattern: two rows per lane as spmv_dia_kernel; run
+// j (L diagonals, first offset o) reads x[c .. c+L] of the row pair (c = row +
+// o) with (L+2)/2 16-B loads at clamp(c + 2q); value c + i sits in load i/2
+// (low half iff it is the load's clamped position), exact for every in-range
+// column (out-of-range ones belong to +0.0 terms and read some finite x).
+// Codes: cw words per row (not a power of two), the row pair's 2 cw words
+// loaded as 16-B + 8-B + 4-B pieces.  Row sums over the K diagonals in
+// ascending order, as the other DIA kernels.
+template <int GM, int PAT, bool CLAMP>
+__device__ __forceinline__ void dia_pat_loads(const DiaArgs &a, int row, double (&xv)[dia_pat_nv(PAT)]) {
+    int kd = 0, vo = 0;
+#pragma unroll
+    for (int j = 0; j < dia_pat_nrun(PAT); j++) {
+        const int c = row + a.off[kd];
+#pragma unroll
+        for (int q = 0; q < dia_pat_nq(PAT, j); q++) {
+            const int p = CLAMP ? min(max(c + 2 * q, 0), a.ncols - 2) : c + 2 * q;
+            dbl2_t v = *reinterpret_cast<const dbl2u_t *>(a.e.x + p);
+            if constexpr (GM == SPMV_RESID0) v = *reinterpret_cast<const dbl2u_t *>(a.e.d + p) * v;
+            if constexpr (CLAMP) {
+                xv[vo + 2 * q] = c + 2 * q == p ? v.x : v.y;
+                xv[vo + 2 * q + 1] = c + 2 * q + 1 == p ? v.x : v.y;
+            } else {
+                xv[vo + 2 * q] = v.x;
+                xv[vo + 2 * q + 1] = v.y;
+            }
+        }
+        kd += dia_pat_len(PAT, j);
+        vo += 2 * dia_pat_nq(PAT, j);
+    }
+}
+
+template <int MODE, int VB, int CW, int PAT>
+__global__ __launch_bounds__(256) void spmv_dia_pat_kernel(DiaArgs a) {
+    constexpr bool DC = MODE == DIA_JACOBI_DC;
+    constexpr int GM = DC ? SPMV_JACOBI : MODE;
+    constexpr int NRUN = dia_pat_nrun(PAT), NV = dia_pat_nv(PAT);
+    constexpr uint32_t MASK = (1u << VB) - 1;
+    static_assert(dia_pat_k(PAT) * VB <= 32 * CW, "code words too short for the pattern");
+    __shared__ double stab[VB == 4 ? 16 : 256];
+    __shared__ double sdt[DC ? 256 : 1];
+    const double tv = (int)threadIdx.x < a.ntab ? a.vtab[threadIdx.x] : 0.0;
+    double dv = 0.0;
+    if constexpr (DC) dv = a.e.dt[threadIdx.x];
+    int blk;
+    if (a.band_bp > 0) {
+        const int bb = a.band_bp >> 3, x = blockIdx.x & 7, i = blockIdx.x >> 3;
+        blk = (i / bb) * a.band_bp + x * bb + (i % bb);
+    } else {
+        blk = xcd_remap(blockIdx.x, gridDim.x);
+    }
+    const int row = a.row_begin + 512 * blk + 2 * (int)threadIdx.x;
+    DiaEpi<MODE, false> ep;
+    ep.load_codes(a.e, row, a.row_end);
+    ep.load(a.e, row, a.row_end);
+    uint32_t u[2 * CW];
+    {
+        const uint32_t *cp = a.codes + (int64_t)(min(row, a.row_end - 1) - a.code_row0) * CW;
+#pragma unroll
+        for (int q = 0; q < (2 * CW) / 4; q++) {
+            const i32x4u_t v = __builtin_nontemporal_load(reinterpret_cast<const i32x4u_t *>(cp) + q);
+#pragma unroll
+            for (int j = 0; j < 4; j++) u[4 * q + j] = (uint32_t)v[j];
+        }
+        if constexpr ((2 * CW) % 4 >= 2) {
+            const i32x2u_t v = __builtin_nontemporal_load(reinterpret_cast<const i32x2u_t *>(cp + (2 * CW) / 4 * 4));
+            u[(2 * CW) / 4 * 4] = (uint32_t)v.x;
+            u[(2 * CW) / 4 * 4 + 1] = (uint32_t)v.y;
+        }
+        if constexpr ((2 * CW) % 2 == 1) u[2 * CW - 1] = __builtin_nontemporal_load(cp + 2 * CW - 1);
+    }
+    double xv[NV];
+    // a block whose x runs all lie inside [0, ncols) (all but the first and last
+    // plane or two of blocks) loads them unclamped: no selects, fewer registers
+    const int rb = a.row_begin + 512 * blk;
+    if (rb + a.off[0] >= 0 && rb + 511 + a.off[dia_pat_k(PAT) - 1] + 1 <= a.ncols - 1)
+        dia_pat_loads<GM, PAT, false>(a, row, xv);
+    else
+        dia_pat_loads<GM, PAT, true>(a, row, xv);
+    if ((int)threadIdx.x < a.ntab) stab[threadIdx.x] = tv;
+    if constexpr (DC) sdt[threadIdx.x] = dv;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+    if (row >= a.row_end) return;
+    double acc0 = 0.0, acc1 = 0.0;
+    {
+        int kd = 0, vo = 0;
+#pragma unroll
+        for (int j = 0; j < NRUN; j++) {
+#pragma unroll
+            for (int m = 0; m < dia_pat_len(PAT, j); m++) {
+                const int k = kd + m;
+                acc0 = fma(stab[(u[(k * VB) >> 5] >> ((k * VB) & 31)) & MASK], xv[vo + m], acc0);
+                acc1 = fma(stab[(u[CW + ((k * VB) >> 5)] >> ((k * VB) & 31)) & MASK], xv[vo + m + 1], acc1);
+            }
+            kd += dia_pat_len(PAT, j);
+            vo += 2 * dia_pat_nq(PAT, j);
+        }
+    }
+    ep.store(a.e, sdt, acc0, acc1);
+}
+
+// A/B switch FAMG_DIA_PAT=0: no DIA storage for more than 32 diagonals
+static bool dia_pat_enabled() {
+    static const bool on = [] {
+        const char *e = getenv("FAMG_DIA_PAT");
+        return !(e && e[0] == '0');
+    }();
+    return on;
+}
+
+// The run pattern of a sorted offset list (0: none of the patterns above)
+static int dia_pattern_of(const std::vector<int> &offs) {
+    std::vector<int> len;
+    for (size_t k = 0; k < offs.size(); k++) {
+        if (k > 0 && offs[k] == offs[k - 1] + 1) len.back()++;
+        else len.push_back(1);
+    }
+    for (int pat : {33, 27}) {
+        if ((int)len.size() != dia_pat_nrun(pat)) continue;
+        bool ok = true;
+        for (int j = 0; ok && j < dia_pat_nrun(pat); j++) ok = len[j] == dia_pat_len(pat, j);
+        if (ok) return pat;
+    }
+    return 0;
 }
 
 // One SGS color update with DIA codes of the color-permuted copy: stored row p
@@ -1711,9 +1863,14 @@ static bool build_dia(GpuCsr &m, int vb, const std::vector<unsigned long long> &
     std::sort(offs.begin(), offs.end());
     const int K = (int)offs.size();
     if (K == 0 || (int64_t)K * nr * 4 > (rp[r1] - rp[r0]) * 5) return false;  // >= 80 % filled
+    // more than 32 diagonals: only a run pattern's kernel (no SGS sweep)
+    const int pat = K > 32 && dia_pat_enabled() ? dia_pattern_of(offs) : 0;
+    if (K > 32 && (rowid || pat == 0)) return false;
     const int bits = K * vb;
     int cw = 1;
-    while (cw * 32 < bits) cw *= 2;
+    if (pat) cw = (bits + 31) / 32;
+    else
+        while (cw * 32 < bits) cw *= 2;
     DiaArgs oa{};
     oa.k = K;
     for (int k = 0; k < K; k++) oa.off[k] = offs[k];
@@ -1736,6 +1893,7 @@ static bool build_dia(GpuCsr &m, int vb, const std::vector<unsigned long long> &
     m.dia_vbits = vb;
     m.dia_ntab = (int64_t)tab.size();
     m.dia_rowid = rowid;
+    m.dia_pat = pat;
     return true;
 }
 
@@ -1772,7 +1930,7 @@ void build_sell(GpuCsr &m, const std::vector<int64_t> &rp) {
     m.dia_codes.release();
     m.dia_vtab.release();
     m.dia_ntab = 0;
-    m.dia_k = m.dia_cw = m.dia_vbits = 0;
+    m.dia_k = m.dia_cw = m.dia_vbits = m.dia_pat = 0;
     m.dia_r0 = m.dia_r1 = m.dia_seg = 0;
     m.dia_rowid = nullptr;
     m.dia_off.clear();
@@ -2048,6 +2206,15 @@ static bool sell_short_enabled() {
     return on;
 }
 
+// A/B switch FAMG_DIA_PAT27=0: the 27-point DIA SpMV takes spmv_dia_kernel<NR = 9>
+static bool dia_pat27() {
+    static const bool on = [] {
+        const char *e = getenv("FAMG_DIA_PAT27");
+        return !(e && e[0] == '0');
+    }();
+    return on;
+}
+
 // A/B switch FAMG_DIA_RUNS7=0: the 7-point DIA kernels load every diagonal's pair
 static bool dia_runs7() {
     static const bool on = [] {
@@ -2158,6 +2325,42 @@ void spmv(const GpuCsr &m, const double *x, double *y, SpmvMode mode, const Spmv
         const bool run7 = m.dia_k == 7 && dia_runs7() && m.dia_off[3] == m.dia_off[2] + 1 &&
                           m.dia_off[4] == m.dia_off[2] + 2;
         const int runs9i = runs9 ? 9 : run7 ? -1 : 0;
+        const int pat = m.dia_pat ? m.dia_pat : runs9 && dia_pat27() && (key == 4 * 16 + 4 || key == 8 * 16 + 8) ? 27 : 0;
+        if (pat) {
+#define FAMG_DIAP2(M, VB, CW, P) spmv_dia_pat_kernel<M, VB, CW, P><<<grid, block, 0, s>>>(a);
+#define FAMG_DIAP(VB, CW, P)                                                                        \
+    switch (mode) {                                                                               \
+    case SPMV_SET: FAMG_DIAP2(SPMV_SET, VB, CW, P) break;                                            \
+    case SPMV_ADD: FAMG_DIAP2(SPMV_ADD, VB, CW, P) break;                                            \
+    case SPMV_RESID: FAMG_DIAP2(SPMV_RESID, VB, CW, P) break;                                        \
+    case SPMV_JACOBI:                                                                             \
+        if (e.dc) {                                                                               \
+            FAMG_DIAP2(DIA_JACOBI_DC, VB, CW, P)                                                     \
+        } else {                                                                                  \
+            FAMG_DIAP2(SPMV_JACOBI, VB, CW, P)                                                       \
+        }                                                                                         \
+        break;                                                                                    \
+    case SPMV_RESID0: FAMG_DIAP2(SPMV_RESID0, VB, CW, P) break;                                      \
+    case SPMV_ADD0: FAMG_DIAP2(SPMV_ADD0, VB, CW, P) break;                                          \
+    default: break;                                                                               \
+    }
+            FAMG_REQUIRE(pat == 33 || pat == 27, AMG_ERR_INVALID, "DIA: unsupported run pattern");
+            if (pat == 33 && key == 8 * 16 + 9) {
+                FAMG_DIAP(8, 9, 33)
+            } else if (pat == 33 && key == 4 * 16 + 5) {
+                FAMG_DIAP(4, 5, 33)
+            } else if (pat == 27 && key == 8 * 16 + 8) {
+                FAMG_DIAP(8, 8, 27)
+            } else if (pat == 27 && key == 4 * 16 + 4) {
+                FAMG_DIAP(4, 4, 27)
+            } else {
+                fail(AMG_ERR_INVALID, "DIA: unsupported code layout");
+            }
+#undef FAMG_DIAP
+#undef FAMG_DIAP2
+            FAMG_CHECK_HIP(hipGetLastError());
+            return;
+        }
 #define FAMG_DIA2(M, VB, CW) launch_dia<M, VB, CW>(runs9i, nt, grid, block, s, a);
 #define FAMG_DIA(VB, CW)                                                                          \
     switch (mode) {                                                                               \

@@ -819,13 +819,39 @@ def test_dia_codes(ctx, gen):
     assert it == 3 and hist[2] < hist[0]
 
 
+def test_dia_pattern33(ctx):
+    """A_1 of smoothed aggregation on 2^3 boxes of the 7-pt operator has 33
+    diagonals in runs (z-2 | 3 x runs | y-2 | x run | x run of five | x run |
+    y+2 | 3 x runs | z+2) and takes DIA codes through the run-pattern kernel
+    (9 code words per row, not a power of two): SpMV bitwise equal to the
+    oracle (odd row count: a lane's second row dead; boundary rows: clamped x
+    runs), and the V-cycle whose level 1 smooths and forms residuals on it
+    within 1e-11 of the restatement, fold on and off."""
+    dims = (97, 85, 73)  # level 1: 49 x 43 x 37 = 77959 rows (odd, > 65536)
+    A = fa().SparseMatOp.laplace3d_7pt(ctx, *dims)
+    mg = fa().sa_build_box(A, dims, (2, 2, 2), coarsest_dim=1000)
+    A1 = mg.level(1)[0]
+    info = A1.spmv_info()
+    assert info["kernel"] == "dia" and info["dia_diagonals"] == 33 and info["value_bits"] in (4, 8), info
+    OA1 = O.Csr.from_arrays(*A1.dims(), *A1.arrays())
+    rng = np.random.default_rng(33)
+    x = rng.standard_normal(OA1.ncols)
+    assert np.array_equal(apply_dev(ctx, A1, x, OA1.nrows).view(np.int64), OA1.spmv(x).view(np.int64))
+    b = rng.uniform(-1, 1, A.nrows)
+    zref = O.Multigrid(oracle_levels_from_gpu(mg, "jacobi")).apply(b)
+    for fold in (True, False):
+        mg.set_fold_zero_guess(fold)
+        z = apply_dev(ctx, mg, b, A.nrows)
+        assert np.linalg.norm(z - zref) <= 1e-11 * np.linalg.norm(zref)
+
+
 @pytest.mark.timeout(400)
 def test_vcycle_256_storage_mix(ctx):
     """The benchmark configuration itself (C2: 7-pt 256^3, SA 2^3 boxes, Jacobi,
     6 levels) against the oracle on the same hierarchy, so the exact storage mix
     the bench times is what is checked: DIA codes on A_0, 4-bit-coded pattern
     SELL on R_0 (row bases, implicit columns), 4-bit SELL with u16 column deltas
-    on P_0, 8-bit-code SELL on A_1, stencil classes on A_2 (2197 classes),
+    on P_0, 8-bit DIA codes in the 33-diagonal run pattern on A_1, stencil classes on A_2 (2197 classes),
     16-bit codes on R_1/P_1, the fp64 pattern SELL (lanes per row) on A_3,
     the wave-per-row kernel on A_4.  One
     V-cycle to 1e-11 and 10 stationary cycles (rho_k) to 1e-8 (+ noise floor).
@@ -842,7 +868,7 @@ def test_vcycle_256_storage_mix(ctx):
     assert a0["kernel"] == "dia" and a0["value_bits"] == 4
     assert r0["kernel"] == "sellp" and r0["value_bits"] == 4
     assert p0["kernel"] == "sell" and p0["value_bits"] == 4 and p0["slices_u16"] > 0
-    assert info[1][0]["kernel"] == "sell" and info[1][0]["value_bits"] == 8
+    assert info[1][0]["kernel"] == "dia" and info[1][0]["value_bits"] == 8 and info[1][0]["dia_diagonals"] == 33
     assert info[2][0]["kernel"] == "classes" and info[2][0]["classes"] == 2197
     assert info[1][1]["value_bits"] == 16 and info[1][2]["value_bits"] == 16
     assert info[3][0]["kernel"] == "sellp" and info[4][0]["kernel"] == "vector"
