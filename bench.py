@@ -606,13 +606,15 @@ def general_roofline(fa, ctx, dims, stream, x, y):
     the 7-pt graph with random edge weights (> 65536 distinct values: fp64
     values) and a symmetric row permutation (columns i32 / u16) -- in the SELL
     storage the auto policy picks and in CSR-stream, priced on SURVEY.md 8(d)'s
-    CSR bytes (12 nnz + 4 (n+1) + 8 n + 8 n).  Two permutations: within windows
+    CSR bytes (12 nnz + 4 (n+1) + 8 n + 8 n); the auto policy picks the x-staged
+    SELL (xsell.hip) where each 4096-row group's x footprint fits LDS, SELL-64
+    with u16/i32 columns otherwise.  Two permutations: within windows
     of 4096 rows (the locality of a mesh numbering) and over all rows (every x
     gather random)."""
     out = {}
     for name, window in (("window4096", 4096), ("random", 0)):
         res = {}
-        for fmt in ("auto", "csr"):
+        for fmt in ("auto", "sell", "csr"):
             fa.set_spmv_format(fmt)
             try:
                 M = fa.SparseMatOp.random7(ctx, *dims, seed=42, window=window)

@@ -234,6 +234,13 @@ amg_status amg_csr_spmv_info(const amg_linop *op, int64_t *info8) {
         info8[5] = m.sell_mode_slices[0];
         info8[6] = m.sell_mode_slices[1];
         info8[7] = m.sell_mode_slices[2];
+        if (m.kernel == SPMV_KERNEL_XS) {  // slices with LDS indices as "u16", escape slices as "i32"
+            info8[3] = (int64_t)m.xs_desc.size();
+            info8[4] = m.xs_steps * 64;
+            info8[5] = 0;
+            info8[6] = info8[3] - m.xs_escape_slices;
+            info8[7] = m.xs_escape_slices;
+        }
     });
 }
 

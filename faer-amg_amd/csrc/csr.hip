@@ -144,6 +144,15 @@ void csr_finalize(GpuCsr &m, const std::vector<int64_t> *segments) {
         m.sell_vbits = 0;
         m.sell_mode_slices[0] = m.sell_mode_slices[1] = m.sell_mode_slices[2] = 0;
     }
+    // gather-heavy fp64 SELL: x staged in LDS per row group (replaces SELL-64)
+    xs_release(m);
+    if (!dia_all && !m.has_bsr() && !m.has_sellp() && !m.has_scs() && build_xs(m, rp)) {
+        m.sell_row0.release(); m.sell_soff.release(); m.sell_desc.release(); m.sell_base.release();
+        m.sell_data.release(); m.sell_vtab.release();
+        m.nslices = m.sell_steps = m.sell_bytes = m.sell_ntab = 0;
+        m.sell_vbits = 0;
+        m.sell_mode_slices[0] = m.sell_mode_slices[1] = m.sell_mode_slices[2] = 0;
+    }
     choose_kernel(m);
     if (storage_check_enabled()) storage_check(m);
 }

@@ -110,6 +110,12 @@ struct GpuCsr {
     int64_t scs_k = 0, scs_nclass = 0;
     int64_t scs_seg = -1;  // >= 0: only this row segment (a distributed level's halo interior) beside SELL
     int scs_ib = 0;
+    // x-staged SELL (xsell.hip): per group of 4096 rows the x chunks staged in LDS,
+    // per slice fp64 values + 16-bit LDS indices (or 32-bit columns: escape slices)
+    DevBuf<char> xs_data;
+    DevBuf<uint32_t> xs_desc;
+    DevBuf<int32_t> xs_soff, xs_coff, xs_chunks;
+    int64_t xs_groups = 0, xs_bytes = 0, xs_steps = 0, xs_chunk_total = 0, xs_escape_slices = 0;
     int kernel = 0;  // SpmvKernel chosen at finalize
     bool spmv_ready() const { return rp32.get() != nullptr && sched.get() != nullptr; }
     bool has_sell() const { return sell_desc.get() != nullptr; }
@@ -117,6 +123,7 @@ struct GpuCsr {
     bool has_bsr() const { return bsr_data.get() != nullptr; }
     bool has_sellp() const { return sellp_vals.get() != nullptr; }
     bool has_scs() const { return scs_cls.get() != nullptr; }
+    bool has_xs() const { return xs_data.get() != nullptr; }
     int64_t index_bytes() const { return 12 * nnz + 4 * (nrows + 1); }
     // matrix bytes one SpMV streams with the chosen kernel (data + metadata)
     int64_t stream_bytes() const {
@@ -124,6 +131,7 @@ struct GpuCsr {
         if (kernel == 4) return bsr_steps * (64 * 76) + 8 * (bsr_slices + 1);
         if (kernel == 5) return sellp_stream;
         if (kernel == 6) return scs_ib * nrows + 8 * scs_k * scs_nclass + 4 * scs_k;
+        if (kernel == 7) return xs_bytes + 8 * (int64_t)(xs_desc.size() + 1) + 4 * xs_chunk_total + 4 * (xs_groups + 1);
         if (kernel == 2)
             return nnz * ((vec_vbits ? vec_vbits / 8 : 8) + (vec_o16 ? 2 : 4)) + 4 * (nrows + 1) + 8 * sell_ntab;
         return kernel == 1 ? sell_bytes + 12 * (nslices + 1) + 4 * sell_steps + 8 * sell_ntab : index_bytes();
@@ -148,12 +156,15 @@ extern int g_spmv_format_policy;
 extern int g_value_codes;
 enum SpmvKernel : int {
     SPMV_KERNEL_STREAM = 0, SPMV_KERNEL_SELL = 1, SPMV_KERNEL_VECTOR = 2, SPMV_KERNEL_DIA = 3, SPMV_KERNEL_BSR = 4,
-    SPMV_KERNEL_SELLP = 5, SPMV_KERNEL_SCS = 6
+    SPMV_KERNEL_SELLP = 5, SPMV_KERNEL_SCS = 6, SPMV_KERNEL_XS = 7
 };
 // stencil-class storage for structured operators whose rows repeat up to a
 // shift; true if built (scs.hip)
 bool build_scs(GpuCsr &m, const std::vector<int64_t> &rp, int64_t other_bytes);
 void scs_release(GpuCsr &m);
+// x-staged SELL for gather-heavy fp64 SELL matrices; true if built (xsell.hip)
+bool build_xs(GpuCsr &m, const std::vector<int64_t> &rp);
+void xs_release(GpuCsr &m);
 void sellp_release(GpuCsr &m);
 // pattern SELL (implicit columns from per-slice offset patterns) for structured
 // operators; true if built (sellp.hip)
@@ -206,6 +217,8 @@ void spmv_bsr(const GpuCsr &m, const double *x, double *y, SpmvMode mode, const 
               int64_t seg);
 void spmv_scs(const GpuCsr &m, const double *x, double *y, SpmvMode mode, const SpmvEpi &epi, hipStream_t s,
               int64_t seg);
+bool xs_supports(SpmvMode mode);
+void spmv_xs(const GpuCsr &m, const double *x, double *y, SpmvMode mode, const SpmvEpi &epi, hipStream_t s);
 void spmv_sellp(const GpuCsr &m, const double *x, double *y, SpmvMode mode, const SpmvEpi &epi, hipStream_t s,
                 int64_t seg);
 

@@ -2113,6 +2113,7 @@ void choose_kernel(GpuCsr &m) {
     else if (m.has_bsr()) m.kernel = SPMV_KERNEL_BSR;
     else if (m.has_scs() && m.scs_seg < 0) m.kernel = SPMV_KERNEL_SCS;
     else if (m.has_sellp()) m.kernel = SPMV_KERNEL_SELLP;
+    else if (m.has_xs()) m.kernel = SPMV_KERNEL_XS;
     else if (m.has_sell()) m.kernel = SPMV_KERNEL_SELL;
     else if (g_spmv_format_policy == 3 ||
              (g_spmv_format_policy == 0 && m.nrows > 0 && m.nnz >= vec_min_avg() * m.nrows)) {
@@ -2239,6 +2240,10 @@ void spmv(const GpuCsr &m, const double *x, double *y, SpmvMode mode, const Spmv
     if (m.kernel == SPMV_KERNEL_SCS || (m.has_scs() && seg >= 0 && seg == m.scs_seg && mode != SPMV_SGS)) {
         FAMG_REQUIRE(mode != SPMV_SGS, AMG_ERR_UNSUPPORTED, "stencil-class storage has no SGS sweep");
         spmv_scs(m, x, y, mode, epi, s, seg);
+        return;
+    }
+    if (m.kernel == SPMV_KERNEL_XS && seg < 0 && xs_supports(mode)) {  // other modes: CSR-stream below
+        spmv_xs(m, x, y, mode, epi, s);
         return;
     }
     if (m.kernel == SPMV_KERNEL_SELLP) {

@@ -1,0 +1,304 @@
+// xsell.hip -- x-staged SELL for gather-heavy general operators.
+//
+// A general sparse matrix whose rows are not stored in a locality-preserving
+// order (the roofline.general operator: random coefficients, rows shuffled
+// within windows of 4096) gathers every x operand from a different cache line:
+// on gfx950 each 8-B gather pulls a 128-B line from L2 into L1, and with three
+// 32-KB x windows per row group against a 32-KB L1 those fills, not HBM, bound
+// the SpMV (SELL with u16/i32 columns: 0.47 ms for 1.25 GB of matrix stream).
+//
+// Here the x footprint of each group of 64 slices (4096 rows) is copied once
+// into LDS and the row sums read it there.  Group g stages up to XS_MAXCH
+// chunks of 64 consecutive x entries (512 B; 160 KB, the whole LDS of a CU):
+// the chunks its entries reference, the most referenced first.  A slice whose
+// entries all fall in staged chunks stores a 16-bit LDS index per entry
+// (slot * 64 + column % 64); a slice with any entry outside them keeps 32-bit
+// global columns (escape slices, gathered through the caches).  Values stay
+// fp64, one step per 512-B row per slice (step t of lane l at t * 64 + l), the
+// index block after the values.
+//
+// One 1024-thread workgroup per group: the 16 waves stage the chunks (16-B
+// loads), meet at one barrier, then each wave walks slices w, w + 16, w + 32,
+// w + 48 of the group, 8 steps at a time with all value/index loads of a step
+// group issued before the LDS (or global) gathers.  A row's sum runs over its
+// stored entries in order with fma -- the oracle's order, bitwise.  Padding
+// steps add fma(0.0, x, acc) with an in-range staged x.
+//
+// Modes SET / ADD / RESID / JACOBI; the others (the zero-guess folds, SGS)
+// run on the CSR-stream kernel of the same matrix.
+#include <algorithm>
+#include <cstdlib>
+#include <cstring>
+#include <numeric>
+
+#include "famg.hpp"
+
+namespace famg {
+
+typedef double xs_dbl2_t __attribute__((ext_vector_type(2)));
+
+constexpr int XS_SLICES = 64;                // slices per group (4096 rows)
+constexpr int XS_ROWS = XS_SLICES * 64;
+constexpr int XS_CH = 64;                    // x entries per chunk
+constexpr int XS_MAXCH = 320;                // chunks per group (160 KB: all of the LDS)
+constexpr int XS_BS = 1024;                  // threads per workgroup
+constexpr int XS_MAX_W = 64;                 // widest slice stored
+
+struct XsArgs {
+    const char *data;       // per slice: values (w x 64 fp64) then indices (w x 64 u16 / i32)
+    const uint32_t *desc;   // per slice: byte offset / 128 | mode << 30 (1: LDS u16, 2: global i32)
+    const int32_t *soff;    // per slice: first step (+1 sentinel); w = soff[s+1] - soff[s]
+    const int32_t *coff;    // per group: first chunk (+1 sentinel)
+    const int32_t *chunks;  // staged chunk ids, per group ascending
+    int32_t nrows, ncols, ngroups;
+    const double *x;
+    double *y;
+    const double *b;
+    const double *d;
+    const uint8_t *dc;
+    const double *dt;
+};
+
+// all loads of U steps issued before the gathers, then U fmas in step order
+template <int CM, int U>
+__device__ __forceinline__ void xs_steps(const char *__restrict__ blk, int w, int t0, int lane,
+                                         const double *__restrict__ sx, const double *__restrict__ x, double &acc) {
+    double v[U], xv[U];
+    int32_t ix[U];
+    const double *vp = reinterpret_cast<const double *>(blk) + (int64_t)t0 * 64 + lane;
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+        v[u] = __builtin_nontemporal_load(vp + u * 64);
+        if constexpr (CM == 1)
+            ix[u] = __builtin_nontemporal_load(reinterpret_cast<const uint16_t *>(blk + (int64_t)w * 512) +
+                                               (int64_t)(t0 + u) * 64 + lane);
+        else
+            ix[u] = __builtin_nontemporal_load(reinterpret_cast<const int32_t *>(blk + (int64_t)w * 512) +
+                                               (int64_t)(t0 + u) * 64 + lane);
+    }
+#pragma unroll
+    for (int u = 0; u < U; u++) xv[u] = CM == 1 ? sx[ix[u]] : x[ix[u]];
+#pragma unroll
+    for (int u = 0; u < U; u++) acc = fma(v[u], xv[u], acc);
+}
+
+template <int CM>
+__device__ __forceinline__ double xs_walk(const char *blk, int w, int lane, const double *sx, const double *x) {
+    double acc = 0.0;
+    int t = 0;
+    for (; t + 8 <= w; t += 8) xs_steps<CM, 8>(blk, w, t, lane, sx, x, acc);
+    switch (w - t) {
+    case 1: xs_steps<CM, 1>(blk, w, t, lane, sx, x, acc); break;
+    case 2: xs_steps<CM, 2>(blk, w, t, lane, sx, x, acc); break;
+    case 3: xs_steps<CM, 3>(blk, w, t, lane, sx, x, acc); break;
+    case 4: xs_steps<CM, 4>(blk, w, t, lane, sx, x, acc); break;
+    case 5: xs_steps<CM, 5>(blk, w, t, lane, sx, x, acc); break;
+    case 6: xs_steps<CM, 6>(blk, w, t, lane, sx, x, acc); break;
+    case 7: xs_steps<CM, 7>(blk, w, t, lane, sx, x, acc); break;
+    default: break;
+    }
+    return acc;
+}
+
+template <int MODE>
+__global__ __launch_bounds__(XS_BS) void spmv_xs_kernel(XsArgs a) {
+    __shared__ double sx[XS_MAXCH * XS_CH];
+    const int g = xcd_remap(blockIdx.x, gridDim.x);
+    const int c0 = a.coff[g], nch = a.coff[g + 1] - c0;
+    for (int i = threadIdx.x; i < nch * (XS_CH / 2); i += XS_BS) {
+        const int64_t e = (int64_t)a.chunks[c0 + i / (XS_CH / 2)] * XS_CH + 2 * (i % (XS_CH / 2));
+        xs_dbl2_t v = {0.0, 0.0};
+        if (e + 1 < a.ncols) v = *reinterpret_cast<const xs_dbl2_t *>(a.x + e);
+        else if (e < a.ncols) v.x = a.x[e];
+        *reinterpret_cast<xs_dbl2_t *>(sx + 2 * i) = v;
+    }
+    __syncthreads();
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int s_end = min((g + 1) * XS_SLICES, (a.nrows + 63) / 64);
+    for (int s = g * XS_SLICES + wave; s < s_end; s += XS_BS / 64) {
+        const int row = s * 64 + lane;
+        const bool live = row < a.nrows;
+        double xr = 0.0, br = 0.0, dr = 0.0, yr = 0.0;  // epilogue operands first
+        if (live) {
+            if constexpr (MODE == SPMV_JACOBI) {
+                xr = a.x[row];
+                dr = a.dc ? a.dt[a.dc[row]] : a.d[row];
+            }
+            if constexpr (MODE == SPMV_JACOBI || MODE == SPMV_RESID) br = a.b[row];
+            if constexpr (MODE == SPMV_ADD) yr = a.y[row];
+        }
+        const int w = a.soff[s + 1] - a.soff[s];
+        const uint32_t d = a.desc[s];
+        const char *blk = a.data + (int64_t)(d & 0x3fffffffu) * 128;
+        const double acc = (d >> 30) == 1 ? xs_walk<1>(blk, w, lane, sx, a.x) : xs_walk<2>(blk, w, lane, sx, a.x);
+        if (live) {
+            if constexpr (MODE == SPMV_SET) a.y[row] = acc;
+            else if constexpr (MODE == SPMV_ADD) a.y[row] = yr + acc;
+            else if constexpr (MODE == SPMV_RESID) a.y[row] = br - acc;
+            else a.y[row] = xr + dr * (br - acc);  // JACOBI
+        }
+    }
+}
+
+// one thread per row: values and indices of its lane in its slice
+__global__ __launch_bounds__(256) void k_xs_fill(const int64_t *rp, const int32_t *col, const double *val,
+                                                 int64_t n, int64_t ns, const uint32_t *desc, const int32_t *soff,
+                                                 const int32_t *coff, const int32_t *chunks, char *data) {
+    const int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (r >= ns * 64) return;  // lanes past n in the last slice: padding (value 0, index 0)
+    const int64_t s = r / 64, lane = r % 64, g = s / XS_SLICES;
+    const int w = soff[s + 1] - soff[s];
+    const uint32_t dsc = desc[s];
+    char *blk = data + (int64_t)(dsc & 0x3fffffffu) * 128;
+    double *vp = reinterpret_cast<double *>(blk);
+    const int c0 = coff[g], nch = coff[g + 1] - c0;
+    const int64_t e0 = r < n ? rp[r] : 0, len = r < n ? rp[r + 1] - e0 : 0;
+    for (int t = 0; t < w; t++) {
+        const bool in = t < len;
+        const int32_t c = in ? col[e0 + t] : (len > 0 ? col[e0] : 0);
+        vp[(int64_t)t * 64 + lane] = in ? val[e0 + t] : 0.0;
+        if ((dsc >> 30) == 1) {
+            const int32_t ch = c / XS_CH;
+            int lo = 0, hi = nch - 1;  // the chunk's slot (present for every entry of an LDS slice)
+            while (lo < hi) {
+                const int mid = (lo + hi) >> 1;
+                if (chunks[c0 + mid] < ch) lo = mid + 1;
+                else hi = mid;
+            }
+            // padding of an empty row: slot 0, any in-range LDS entry
+            const int32_t ix = (in || len > 0) ? lo * XS_CH + c % XS_CH : 0;
+            reinterpret_cast<uint16_t *>(blk + (int64_t)w * 512)[(int64_t)t * 64 + lane] = (uint16_t)ix;
+        } else {
+            reinterpret_cast<int32_t *>(blk + (int64_t)w * 512)[(int64_t)t * 64 + lane] = c;
+        }
+    }
+}
+
+static bool xs_disabled() {
+    static const bool off = [] {
+        const char *e = getenv("FAMG_XS");
+        return e && e[0] == '0';
+    }();
+    return off;
+}
+
+void xs_release(GpuCsr &m) {
+    m.xs_data.release();
+    m.xs_desc.release();
+    m.xs_soff.release();
+    m.xs_coff.release();
+    m.xs_chunks.release();
+    m.xs_groups = m.xs_bytes = m.xs_steps = m.xs_chunk_total = m.xs_escape_slices = 0;
+}
+
+// Built for a single-segment matrix of >= SELL rows whose SELL copy gathers
+// (fewer than half of its slices with implicit columns) with fp64 values, when
+// at most 1/16 of the slices escape.  True if built (the caller drops SELL).
+bool build_xs(GpuCsr &m, const std::vector<int64_t> &rp) {
+    xs_release(m);
+    if (xs_disabled() || g_spmv_format_policy != 0 || m.no_sellp || m.seg_rows.size() != 2 || !m.has_sell() ||
+        m.sell_vbits != 0 || m.nrows < 65536 || 2 * m.sell_mode_slices[0] >= m.nslices || m.ncols >= (1 << 30))
+        return false;
+    const int64_t n = m.nrows, ns = (n + 63) / 64, ng = (ns + XS_SLICES - 1) / XS_SLICES;
+    hipStream_t st = m.ctx->stream;
+    std::vector<int32_t> col(m.nnz);
+    FAMG_CHECK_HIP(hipMemcpyAsync(col.data(), m.col.get(), m.nnz * sizeof(int32_t), hipMemcpyDeviceToHost, st));
+    FAMG_CHECK_HIP(hipStreamSynchronize(st));
+    std::vector<int32_t> w(ns), mode(ns);
+    std::vector<std::vector<int32_t>> gch(ng);
+    bool too_wide = false;
+#pragma omp parallel for schedule(dynamic, 16) reduction(|| : too_wide)
+    for (int64_t g = 0; g < ng; g++) {
+        const int64_t r0 = g * XS_ROWS, r1 = std::min(n, r0 + XS_ROWS);
+        std::vector<int32_t> ch;
+        ch.reserve(rp[r1] - rp[r0]);
+        for (int64_t e = rp[r0]; e < rp[r1]; e++) ch.push_back(col[e] / XS_CH);
+        std::sort(ch.begin(), ch.end());
+        // distinct chunks with their reference counts; keep the XS_MAXCH most referenced
+        std::vector<std::pair<int32_t, int32_t>> cnt;  // (-count, chunk)
+        for (size_t i = 0; i < ch.size();) {
+            size_t j = i;
+            while (j < ch.size() && ch[j] == ch[i]) j++;
+            cnt.push_back({-(int32_t)(j - i), ch[i]});
+            i = j;
+        }
+        if ((int)cnt.size() > XS_MAXCH) {
+            std::nth_element(cnt.begin(), cnt.begin() + XS_MAXCH, cnt.end());
+            cnt.resize(XS_MAXCH);
+        }
+        std::vector<int32_t> keep;
+        for (auto &p : cnt) keep.push_back(p.second);
+        std::sort(keep.begin(), keep.end());
+        for (int64_t s = r0 / 64; s < (r1 + 63) / 64; s++) {
+            int32_t ws = 0;
+            bool esc = false;
+            for (int64_t r = s * 64; r < std::min(n, s * 64 + 64); r++) {
+                ws = std::max<int32_t>(ws, (int32_t)(rp[r + 1] - rp[r]));
+                for (int64_t e = rp[r]; e < rp[r + 1] && !esc; e++)
+                    esc = !std::binary_search(keep.begin(), keep.end(), col[e] / XS_CH);
+            }
+            if (ws > XS_MAX_W) too_wide = true;
+            w[s] = ws;
+            mode[s] = esc ? 2 : 1;
+        }
+        if (keep.empty()) keep.push_back(0);
+        gch[g] = std::move(keep);
+    }
+    if (too_wide) return false;
+    int64_t esc = 0;
+    for (int64_t s = 0; s < ns; s++) esc += mode[s] == 2;
+    if (esc * 16 > ns) return false;
+    std::vector<int32_t> soff(ns + 1, 0), coff(ng + 1, 0), chunks;
+    std::vector<uint32_t> desc(ns);
+    int64_t bytes = 0;
+    for (int64_t s = 0; s < ns; s++) {
+        if (bytes / 128 >= (int64_t(1) << 30)) return false;
+        desc[s] = (uint32_t)(bytes / 128) | ((uint32_t)mode[s] << 30);
+        bytes += ((int64_t)w[s] * 64 * (8 + (mode[s] == 1 ? 2 : 4)) + 127) / 128 * 128;
+        soff[s + 1] = soff[s] + w[s];
+    }
+    for (int64_t g = 0; g < ng; g++) {
+        chunks.insert(chunks.end(), gch[g].begin(), gch[g].end());
+        coff[g + 1] = (int32_t)chunks.size();
+    }
+    m.xs_data.resize(std::max<int64_t>(128, bytes));
+    m.xs_desc.resize(ns);
+    m.xs_soff.resize(ns + 1);
+    m.xs_coff.resize(ng + 1);
+    m.xs_chunks.resize(chunks.size());
+    FAMG_CHECK_HIP(hipMemcpyAsync(m.xs_desc.get(), desc.data(), ns * 4, hipMemcpyHostToDevice, st));
+    FAMG_CHECK_HIP(hipMemcpyAsync(m.xs_soff.get(), soff.data(), (ns + 1) * 4, hipMemcpyHostToDevice, st));
+    FAMG_CHECK_HIP(hipMemcpyAsync(m.xs_coff.get(), coff.data(), (ng + 1) * 4, hipMemcpyHostToDevice, st));
+    FAMG_CHECK_HIP(hipMemcpyAsync(m.xs_chunks.get(), chunks.data(), chunks.size() * 4, hipMemcpyHostToDevice, st));
+    hipLaunchKernelGGL(k_xs_fill, dim3((unsigned)ceil_div(ns * 64, 256)), dim3(256), 0, st, m.rp64.get(), m.col.get(),
+                       m.val.get(), n, ns, m.xs_desc.get(), m.xs_soff.get(), m.xs_coff.get(), m.xs_chunks.get(),
+                       m.xs_data.get());
+    FAMG_CHECK_HIP(hipGetLastError());
+    FAMG_CHECK_HIP(hipStreamSynchronize(st));
+    m.xs_groups = ng;
+    m.xs_bytes = bytes;
+    m.xs_steps = soff[ns];
+    m.xs_chunk_total = (int64_t)chunks.size();
+    m.xs_escape_slices = esc;
+    return true;
+}
+
+bool xs_supports(SpmvMode mode) {
+    return mode == SPMV_SET || mode == SPMV_ADD || mode == SPMV_RESID || mode == SPMV_JACOBI;
+}
+
+void spmv_xs(const GpuCsr &m, const double *x, double *y, SpmvMode mode, const SpmvEpi &epi, hipStream_t s) {
+    XsArgs a{m.xs_data.get(), m.xs_desc.get(), m.xs_soff.get(), m.xs_coff.get(), m.xs_chunks.get(),
+             (int32_t)m.nrows, (int32_t)m.ncols, (int32_t)m.xs_groups, x, y, epi.b, epi.d, epi.dc, epi.dt};
+    const dim3 grid((unsigned)m.xs_groups), block(XS_BS);
+    switch (mode) {
+    case SPMV_SET: spmv_xs_kernel<SPMV_SET><<<grid, block, 0, s>>>(a); break;
+    case SPMV_ADD: spmv_xs_kernel<SPMV_ADD><<<grid, block, 0, s>>>(a); break;
+    case SPMV_RESID: spmv_xs_kernel<SPMV_RESID><<<grid, block, 0, s>>>(a); break;
+    case SPMV_JACOBI: spmv_xs_kernel<SPMV_JACOBI><<<grid, block, 0, s>>>(a); break;
+    default: fail(AMG_ERR_UNSUPPORTED, "x-staged SELL: unsupported SpMV epilogue");
+    }
+    FAMG_CHECK_HIP(hipGetLastError());
+}
+
+}  // namespace famg

@@ -121,7 +121,9 @@ amg_status amg_csr_create_device_i32(amg_ctx *ctx, int64_t nrows, int64_t ncols,
 /* Number of stored entries of a CSR operator. */
 amg_status amg_csr_nnz(const amg_linop *op, int64_t *nnz);
 /* SpMV storage chosen for a CSR operator: info8 = {kernel (0 CSR-stream,
- * 1 SELL-64, 2 vector, 3 DIA codes, 4 3x3 blocks, 5 pattern SELL with lanes per row), matrix
+ * 1 SELL-64, 2 vector, 3 DIA codes, 4 3x3 blocks, 5 pattern SELL with lanes per row, 6 stencil
+ * classes, 7 x-staged SELL: slices counted as 16-bit when their x is staged in LDS, 32-bit
+ * when they escape to global columns), matrix
  * bytes one SpMV streams, CSR bytes (12 nnz +
  * 4 (n+1)), SELL slices, SELL stored entries incl. padding, SELL slices with
  * implicit / 16-bit delta / 32-bit column indices}. */

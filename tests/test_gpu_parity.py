@@ -916,6 +916,51 @@ def test_random_7pt_generator_and_spmv(ctx, window):
         assert np.array_equal(apply_dev(ctx, M, x, R.shape[0]), OA.spmv(x)), fmt
 
 
+def test_xsell_general_operator(ctx):
+    """x-staged SELL (xsell.hip): the random-coefficient 7-pt operator with rows
+    shuffled within windows of 4096 stages each 4096-row group's x chunks in LDS
+    (auto policy); SpMV bitwise equal to the oracle and to SELL-64 (ragged last
+    group: 163840 + 1000 rows are not a multiple of 4096), and a V-cycle on it
+    (residual and Jacobi epilogues on xsell, the folded zero-guess residual on
+    the CSR-stream fallback) within 1e-11 of the restatement.  The fully
+    shuffled operator escapes the LDS budget and keeps SELL-64."""
+    import sa_oracle as SO
+    dims = (64, 64, 40)
+    A = fa().SparseMatOp.random7(ctx, *dims, seed=9, window=4096)
+    info = A.spmv_info()
+    assert info["kernel"] == "xsell" and info["slices_u16"] > 0, info
+    R = SO.random_7pt(*dims, seed=9, window=4096)
+    OA = O.Csr.from_scipy(R)
+    x = np.random.default_rng(4).standard_normal(R.shape[0])
+    y = apply_dev(ctx, A, x, R.shape[0])
+    assert np.array_equal(y.view(np.int64), OA.spmv(x).view(np.int64))
+    fa().set_spmv_format("sell")
+    try:
+        S = fa().SparseMatOp.random7(ctx, *dims, seed=9, window=4096)
+    finally:
+        fa().set_spmv_format("auto")
+    assert S.spmv_info()["kernel"] == "sell"
+    assert np.array_equal(apply_dev(ctx, S, x, R.shape[0]).view(np.int64), y.view(np.int64))
+    # ragged: rows not a multiple of the group (and of the slice)
+    Rr = R[:R.shape[0] - 3096, :R.shape[0] - 3096].tocsr()
+    Ar = fa().SparseMatOp.from_scipy(ctx, Rr)
+    assert Ar.spmv_info()["kernel"] == "xsell"
+    xr = x[:Rr.shape[0]]
+    assert np.array_equal(apply_dev(ctx, Ar, xr, Rr.shape[0]).view(np.int64),
+                          O.Csr.from_scipy(Rr).spmv(xr).view(np.int64))
+    # V-cycle: box aggregates of the index grid (any SPD hierarchy will do)
+    mg = fa().sa_build_box(A, dims, (2, 2, 2), coarsest_dim=1000)
+    assert mg.level(0)[0].spmv_info()["kernel"] == "xsell"
+    b = np.random.default_rng(5).uniform(-1, 1, R.shape[0])
+    zref = O.Multigrid(oracle_levels_from_gpu(mg, "jacobi")).apply(b)
+    for fold in (True, False):
+        mg.set_fold_zero_guess(fold)
+        z = apply_dev(ctx, mg, b, R.shape[0])
+        assert np.linalg.norm(z - zref) <= 1e-11 * np.linalg.norm(zref)
+    Rw = fa().SparseMatOp.random7(ctx, *dims, seed=9, window=0)
+    assert Rw.spmv_info()["kernel"] == "sell"
+
+
 def test_sgs_dia_sweeps(ctx):
     """Color sweeps of a constant-stencil operator run on DIA codes of the
     color-permuted copy (diagonals taken against the original row): the same
