@@ -47,6 +47,7 @@ struct ScsArgs {
 };
 
 typedef double scs_dbl2_t __attribute__((ext_vector_type(2), aligned(8)));
+typedef double scs_dbl2a_t __attribute__((ext_vector_type(2)));
 
 // x operands of rows (r, r+1) at column c = r + off: one 16-B load at clamp(c, 0,
 // ncols - 2) and selects (a column outside [0, ncols) belongs to a +0.0 term, so
@@ -91,10 +92,16 @@ __global__ __launch_bounds__(256) void spmv_scs_kernel(ScsArgs a) {
     for (int k0 = 0; k0 < a.k; k0 += SCS_U) {
         double va[SCS_U], vb[SCS_U], xa[SCS_U], xb[SCS_U];
 #pragma unroll
-        for (int u = 0; u < SCS_U; u++) {
-            scs_x2<MODE>(a, r0 + a.offs[k0 + u], xa[u], xb[u]);
-            va[u] = da[k0 + u];
-            vb[u] = db[k0 + u];
+        for (int u = 0; u < SCS_U; u++) scs_x2<MODE>(a, r0 + a.offs[k0 + u], xa[u], xb[u]);
+        // dictionary values of offsets (k, k+1) as one 16-B load (rows of K = 8j doubles)
+#pragma unroll
+        for (int u = 0; u < SCS_U; u += 2) {
+            const scs_dbl2a_t pa = *reinterpret_cast<const scs_dbl2a_t *>(da + k0 + u);
+            const scs_dbl2a_t pb = *reinterpret_cast<const scs_dbl2a_t *>(db + k0 + u);
+            va[u] = pa.x;
+            va[u + 1] = pa.y;
+            vb[u] = pb.x;
+            vb[u + 1] = pb.y;
         }
 #pragma unroll
         for (int u = 0; u < SCS_U; u++) {

@@ -24,8 +24,9 @@
 // stored entries in order with fma -- the oracle's order, bitwise.  Padding
 // steps add fma(0.0, x, acc) with an in-range staged x.
 //
-// Modes SET / ADD / RESID / JACOBI; the others (the zero-guess folds, SGS)
-// run on the CSR-stream kernel of the same matrix.
+// Every mode but SGS (whose color-permuted copies never get this storage): the
+// folded zero-guess residual stages d*x (the product vec_mul would store), the
+// folded correction adds d*b in its epilogue.
 #include <algorithm>
 #include <cstdlib>
 #include <cstring>
@@ -60,9 +61,9 @@ struct XsArgs {
 };
 
 // all loads of U steps issued before the gathers, then U fmas in step order
-template <int CM, int U>
+template <int CM, int MODE, int U>
 __device__ __forceinline__ void xs_steps(const char *__restrict__ blk, int w, int t0, int lane,
-                                         const double *__restrict__ sx, const double *__restrict__ x, double &acc) {
+                                         const double *__restrict__ sx, const XsArgs &a, double &acc) {
     double v[U], xv[U];
     int32_t ix[U];
     const double *vp = reinterpret_cast<const double *>(blk) + (int64_t)t0 * 64 + lane;
@@ -77,24 +78,28 @@ __device__ __forceinline__ void xs_steps(const char *__restrict__ blk, int w, in
                                                (int64_t)(t0 + u) * 64 + lane);
     }
 #pragma unroll
-    for (int u = 0; u < U; u++) xv[u] = CM == 1 ? sx[ix[u]] : x[ix[u]];
+    for (int u = 0; u < U; u++) {
+        if constexpr (CM == 1) xv[u] = sx[ix[u]];
+        else if constexpr (MODE == SPMV_RESID0) xv[u] = a.d[ix[u]] * a.x[ix[u]];
+        else xv[u] = a.x[ix[u]];
+    }
 #pragma unroll
     for (int u = 0; u < U; u++) acc = fma(v[u], xv[u], acc);
 }
 
-template <int CM>
-__device__ __forceinline__ double xs_walk(const char *blk, int w, int lane, const double *sx, const double *x) {
+template <int CM, int MODE>
+__device__ __forceinline__ double xs_walk(const char *blk, int w, int lane, const double *sx, const XsArgs &a) {
     double acc = 0.0;
     int t = 0;
-    for (; t + 8 <= w; t += 8) xs_steps<CM, 8>(blk, w, t, lane, sx, x, acc);
+    for (; t + 8 <= w; t += 8) xs_steps<CM, MODE, 8>(blk, w, t, lane, sx, a, acc);
     switch (w - t) {
-    case 1: xs_steps<CM, 1>(blk, w, t, lane, sx, x, acc); break;
-    case 2: xs_steps<CM, 2>(blk, w, t, lane, sx, x, acc); break;
-    case 3: xs_steps<CM, 3>(blk, w, t, lane, sx, x, acc); break;
-    case 4: xs_steps<CM, 4>(blk, w, t, lane, sx, x, acc); break;
-    case 5: xs_steps<CM, 5>(blk, w, t, lane, sx, x, acc); break;
-    case 6: xs_steps<CM, 6>(blk, w, t, lane, sx, x, acc); break;
-    case 7: xs_steps<CM, 7>(blk, w, t, lane, sx, x, acc); break;
+    case 1: xs_steps<CM, MODE, 1>(blk, w, t, lane, sx, a, acc); break;
+    case 2: xs_steps<CM, MODE, 2>(blk, w, t, lane, sx, a, acc); break;
+    case 3: xs_steps<CM, MODE, 3>(blk, w, t, lane, sx, a, acc); break;
+    case 4: xs_steps<CM, MODE, 4>(blk, w, t, lane, sx, a, acc); break;
+    case 5: xs_steps<CM, MODE, 5>(blk, w, t, lane, sx, a, acc); break;
+    case 6: xs_steps<CM, MODE, 6>(blk, w, t, lane, sx, a, acc); break;
+    case 7: xs_steps<CM, MODE, 7>(blk, w, t, lane, sx, a, acc); break;
     default: break;
     }
     return acc;
@@ -110,6 +115,12 @@ __global__ __launch_bounds__(XS_BS) void spmv_xs_kernel(XsArgs a) {
         xs_dbl2_t v = {0.0, 0.0};
         if (e + 1 < a.ncols) v = *reinterpret_cast<const xs_dbl2_t *>(a.x + e);
         else if (e < a.ncols) v.x = a.x[e];
+        if constexpr (MODE == SPMV_RESID0) {  // the x operand is the zero-guess iterate d*x (vec_mul's product)
+            xs_dbl2_t dv = {0.0, 0.0};
+            if (e + 1 < a.ncols) dv = *reinterpret_cast<const xs_dbl2_t *>(a.d + e);
+            else if (e < a.ncols) dv.x = a.d[e];
+            v = dv * v;
+        }
         *reinterpret_cast<xs_dbl2_t *>(sx + 2 * i) = v;
     }
     __syncthreads();
@@ -124,17 +135,19 @@ __global__ __launch_bounds__(XS_BS) void spmv_xs_kernel(XsArgs a) {
                 xr = a.x[row];
                 dr = a.dc ? a.dt[a.dc[row]] : a.d[row];
             }
-            if constexpr (MODE == SPMV_JACOBI || MODE == SPMV_RESID) br = a.b[row];
+            if constexpr (MODE == SPMV_JACOBI || MODE == SPMV_RESID || MODE == SPMV_RESID0) br = a.b[row];
             if constexpr (MODE == SPMV_ADD) yr = a.y[row];
+            if constexpr (MODE == SPMV_ADD0) yr = (a.dc ? a.dt[a.dc[row]] : a.d[row]) * a.b[row];
         }
         const int w = a.soff[s + 1] - a.soff[s];
         const uint32_t d = a.desc[s];
         const char *blk = a.data + (int64_t)(d & 0x3fffffffu) * 128;
-        const double acc = (d >> 30) == 1 ? xs_walk<1>(blk, w, lane, sx, a.x) : xs_walk<2>(blk, w, lane, sx, a.x);
+        // escape slices gather x (RESID0: d*x) through the caches
+        const double acc = (d >> 30) == 1 ? xs_walk<1, MODE>(blk, w, lane, sx, a) : xs_walk<2, MODE>(blk, w, lane, sx, a);
         if (live) {
             if constexpr (MODE == SPMV_SET) a.y[row] = acc;
-            else if constexpr (MODE == SPMV_ADD) a.y[row] = yr + acc;
-            else if constexpr (MODE == SPMV_RESID) a.y[row] = br - acc;
+            else if constexpr (MODE == SPMV_ADD || MODE == SPMV_ADD0) a.y[row] = yr + acc;
+            else if constexpr (MODE == SPMV_RESID || MODE == SPMV_RESID0) a.y[row] = br - acc;
             else a.y[row] = xr + dr * (br - acc);  // JACOBI
         }
     }
@@ -283,9 +296,7 @@ bool build_xs(GpuCsr &m, const std::vector<int64_t> &rp) {
     return true;
 }
 
-bool xs_supports(SpmvMode mode) {
-    return mode == SPMV_SET || mode == SPMV_ADD || mode == SPMV_RESID || mode == SPMV_JACOBI;
-}
+bool xs_supports(SpmvMode mode) { return mode != SPMV_SGS; }
 
 void spmv_xs(const GpuCsr &m, const double *x, double *y, SpmvMode mode, const SpmvEpi &epi, hipStream_t s) {
     XsArgs a{m.xs_data.get(), m.xs_desc.get(), m.xs_soff.get(), m.xs_coff.get(), m.xs_chunks.get(),
@@ -296,6 +307,8 @@ void spmv_xs(const GpuCsr &m, const double *x, double *y, SpmvMode mode, const S
     case SPMV_ADD: spmv_xs_kernel<SPMV_ADD><<<grid, block, 0, s>>>(a); break;
     case SPMV_RESID: spmv_xs_kernel<SPMV_RESID><<<grid, block, 0, s>>>(a); break;
     case SPMV_JACOBI: spmv_xs_kernel<SPMV_JACOBI><<<grid, block, 0, s>>>(a); break;
+    case SPMV_RESID0: spmv_xs_kernel<SPMV_RESID0><<<grid, block, 0, s>>>(a); break;
+    case SPMV_ADD0: spmv_xs_kernel<SPMV_ADD0><<<grid, block, 0, s>>>(a); break;
     default: fail(AMG_ERR_UNSUPPORTED, "x-staged SELL: unsupported SpMV epilogue");
     }
     FAMG_CHECK_HIP(hipGetLastError());
