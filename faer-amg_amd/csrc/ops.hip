@@ -489,6 +489,7 @@ void MultigridOp::cycle(int64_t l, double *v, const double *f, bool v_zero, doub
     const bool gather_cheap = A && 2 * A->m.sell_mode_slices[2] < A->m.nslices;
     const bool fold = fold_zero_guess && v_zero && steps == 1 && A && D && P &&
                       ((A->m.kernel == SPMV_KERNEL_SELL && A->m.sell_vbits == 0 && gather_cheap) ||
+                       A->m.kernel == SPMV_KERNEL_XS ||  // x-staged: d*x staged with x, no extra gather
                        (A->m.kernel == SPMV_KERNEL_DIA && fold_dia_enabled()));
     if (fold) {
         SpmvEpi epi;

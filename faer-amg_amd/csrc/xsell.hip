@@ -204,13 +204,18 @@ void xs_release(GpuCsr &m) {
     m.xs_groups = m.xs_bytes = m.xs_steps = m.xs_chunk_total = m.xs_escape_slices = 0;
 }
 
-// Built for a single-segment matrix of >= SELL rows whose SELL copy gathers
-// (fewer than half of its slices with implicit columns) with fp64 values, when
-// at most 1/16 of the slices escape.  True if built (the caller drops SELL).
+// Built for a single-segment matrix of >= XS_MIN_GROUPS groups (one workgroup
+// per group: fewer leave CUs idle -- P_2 of the 256^3 cycle, 64 groups, ran 45 us
+// against 21 us on SELL-64) whose SELL copy gathers (fewer than half of its
+// slices with implicit columns) with fp64 values, when at most 1/16 of the
+// slices escape.  True if built (the caller drops SELL).
+constexpr int64_t XS_MIN_GROUPS = 512;
+
 bool build_xs(GpuCsr &m, const std::vector<int64_t> &rp) {
     xs_release(m);
     if (xs_disabled() || g_spmv_format_policy != 0 || m.no_sellp || m.seg_rows.size() != 2 || !m.has_sell() ||
-        m.sell_vbits != 0 || m.nrows < 65536 || 2 * m.sell_mode_slices[0] >= m.nslices || m.ncols >= (1 << 30))
+        m.sell_vbits != 0 || m.nrows < (XS_MIN_GROUPS - 1) * XS_ROWS + 1 || 2 * m.sell_mode_slices[0] >= m.nslices ||
+        m.ncols >= (1 << 30))
         return false;
     const int64_t n = m.nrows, ns = (n + 63) / 64, ng = (ns + XS_SLICES - 1) / XS_SLICES;
     hipStream_t st = m.ctx->stream;
