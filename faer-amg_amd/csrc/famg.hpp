@@ -110,6 +110,7 @@ struct GpuCsr {
     int64_t scs_k = 0, scs_nclass = 0;
     int64_t scs_seg = -1;  // >= 0: only this row segment (a distributed level's halo interior) beside SELL
     int scs_ib = 0;
+    bool scs_lanes = false;  // one row per wave (few long rows: spmv_scs_lanes_kernel)
     // x-staged SELL (xsell.hip): per group of 4096 rows the x chunks staged in LDS,
     // per slice fp64 values + 16-bit LDS indices (or 32-bit columns: escape slices)
     DevBuf<char> xs_data;

@@ -121,6 +121,77 @@ __global__ __launch_bounds__(256) void spmv_scs_kernel(ScsArgs a) {
     }
 }
 
+// Few long rows (A_3 of the 256^3 cycle: 32768 rows of 638 entries, 15625
+// classes): one row per wave, lane q takes offsets q, q + 64, ... (the class's
+// dictionary row and the x operands both coalesced), then a fixed butterfly --
+// the pattern SELL's lanes-per-row order (deterministic; rounding-level
+// differences from the oracle's sequential order, covered by the V-cycle
+// tolerance).  Interior rows share their class, so the dictionary streams about
+// half of the fp64 values the pattern SELL reads.
+template <int MODE, int IB>
+__global__ __launch_bounds__(256) void spmv_scs_lanes_kernel(ScsArgs a) {
+    const int blk = xcd_remap(blockIdx.x, gridDim.x);
+    const int row = a.row_begin + __builtin_amdgcn_readfirstlane(blk * 4 + (int)(threadIdx.x >> 6));
+    if (row >= a.row_end) return;
+    const int lane = threadIdx.x & 63;
+    const int c = IB == 1 ? (int)static_cast<const uint8_t *>(a.cls)[row] : (int)static_cast<const uint16_t *>(a.cls)[row];
+    double br = 0.0, xr = 0.0, dr = 0.0, yr = 0.0;
+    if (lane == 0) {  // epilogue operands first
+        if constexpr (MODE == SPMV_RESID) br = a.b[row];
+        if constexpr (MODE == SPMV_ADD) yr = a.y[row];
+        if constexpr (MODE == SPMV_JACOBI) {
+            xr = a.x[row];
+            br = a.b[row];
+            dr = a.dc ? a.dt[a.dc[row]] : a.d[row];
+        }
+    }
+    const double *dct = a.dict + (int64_t)c * a.k;
+    double acc = 0.0;
+    int k0 = 0;
+    for (; k0 + 8 * 64 <= a.k; k0 += 8 * 64) {
+        double v[8], xv[8];
+#pragma unroll
+        for (int u = 0; u < 8; u++) {
+            const int k = k0 + 64 * u + lane;
+            v[u] = dct[k];
+            xv[u] = a.x[min(max(row + a.offs[k], 0), a.ncols - 1)];
+        }
+#pragma unroll
+        for (int u = 0; u < 8; u++) acc = fma(v[u], xv[u], acc);
+    }
+    {  // the last < 512 offsets (K is a multiple of 8): clamped loads, +0.0 terms past K
+        double v[8], xv[8];
+#pragma unroll
+        for (int u = 0; u < 8; u++) {
+            const int k = k0 + 64 * u + lane;
+            const int kc = min(k, a.k - 1);
+            v[u] = k < a.k ? dct[kc] : 0.0;
+            xv[u] = a.x[min(max(row + a.offs[kc], 0), a.ncols - 1)];
+        }
+#pragma unroll
+        for (int u = 0; u < 8; u++) acc = fma(v[u], xv[u], acc);
+    }
+#pragma unroll
+    for (int m = 32; m > 0; m >>= 1) acc += __shfl_xor(acc, m);
+    if (lane == 0) {
+        if constexpr (MODE == SPMV_SET) a.y[row] = acc;
+        else if constexpr (MODE == SPMV_ADD) a.y[row] = yr + acc;
+        else if constexpr (MODE == SPMV_RESID) a.y[row] = br - acc;
+        else a.y[row] = xr + dr * (br - acc);  // JACOBI
+    }
+}
+
+// the lanes-per-row kernel for row ranges of < SCS_LANES_ROWS rows with >= 256
+// offsets (A/B switch FAMG_SCS_LANES=0: no stencil classes for them)
+constexpr int64_t SCS_LANES_ROWS = 131072;
+static bool scs_lanes_enabled() {
+    static const bool on = [] {
+        const char *e = getenv("FAMG_SCS_LANES");
+        return !(e && e[0] == '0');
+    }();
+    return on;
+}
+
 static bool scs_disabled() {
     static const bool off = [] {
         const char *e = getenv("FAMG_NO_SCS");
@@ -135,6 +206,7 @@ void scs_release(GpuCsr &m) {
     m.scs_offs.release();
     m.scs_k = m.scs_nclass = m.scs_ib = 0;
     m.scs_seg = -1;
+    m.scs_lanes = false;
 }
 
 // Class of every row of [r0, r1): rows with the same (col - base[i], value bits) list share
@@ -258,7 +330,10 @@ bool build_scs(GpuCsr &m, const std::vector<int64_t> &rp, int64_t other_bytes) {
     const int ib = C <= 256 ? 1 : 2;
     const int64_t dict_bytes = (int64_t)Kp * C * 8;
     const int64_t stream = ib * (r1 - r0) + dict_bytes + 4 * Kp;
-    if (dict_bytes > (int64_t(16) << 20) || (double)stream > 0.5 * (double)other_bytes) return false;
+    // few long rows: one row per wave, the dictionary streamed (up to 256 MiB)
+    const bool lanes = r1 - r0 < SCS_LANES_ROWS && Kp >= 256;
+    if (lanes && !scs_lanes_enabled()) return false;
+    if (dict_bytes > (int64_t(lanes ? 256 : 16) << 20) || (double)stream > 0.5 * (double)other_bytes) return false;
     std::vector<double> dict((size_t)Kp * C, 0.0);
     for (int64_t c = 0; c < C; c++) {
         const int64_t i = rep[c];
@@ -287,6 +362,7 @@ bool build_scs(GpuCsr &m, const std::vector<int64_t> &rp, int64_t other_bytes) {
     m.scs_nclass = C;
     m.scs_ib = ib;
     m.scs_seg = seg;
+    m.scs_lanes = lanes;
     return true;
 }
 
@@ -297,8 +373,10 @@ void spmv_scs(const GpuCsr &m, const double *x, double *y, SpmvMode mode, const 
     if (r1 <= r0) return;
     ScsArgs a{m.scs_cls.get(), m.scs_dict.get(), m.scs_offs.get(), (int32_t)m.scs_k, (int32_t)m.scs_nclass,
               (int32_t)r0, (int32_t)r1, (int32_t)m.ncols, x, y, epi.b, epi.d, epi.dc, epi.dt};
-    const dim3 grid((unsigned)ceil_div(r1 - r0, 512)), block(256);
-#define FAMG_SCS2(M, IB) spmv_scs_kernel<M, IB><<<grid, block, 0, s>>>(a);
+    const dim3 grid((unsigned)ceil_div(r1 - r0, m.scs_lanes ? 4 : 512)), block(256);
+#define FAMG_SCS2(M, IB)                                                                           \
+    if (m.scs_lanes) spmv_scs_lanes_kernel<M, IB><<<grid, block, 0, s>>>(a);                       \
+    else spmv_scs_kernel<M, IB><<<grid, block, 0, s>>>(a);
 #define FAMG_SCS(IB)                                                                               \
     switch (mode) {                                                                                \
     case SPMV_SET: FAMG_SCS2(SPMV_SET, IB) break;                                                  \

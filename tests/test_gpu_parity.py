@@ -852,7 +852,7 @@ def test_vcycle_256_storage_mix(ctx):
     the bench times is what is checked: DIA codes on A_0, 4-bit-coded pattern
     SELL on R_0 (row bases, implicit columns), 4-bit SELL with u16 column deltas
     on P_0, 8-bit DIA codes in the 33-diagonal run pattern on A_1, stencil classes on A_2 (2197 classes),
-    16-bit codes on R_1/P_1, the fp64 pattern SELL (lanes per row) on A_3,
+    16-bit codes on R_1/P_1, stencil classes with one row per wave on A_3,
     the wave-per-row kernel on A_4.  One
     V-cycle to 1e-11 and 10 stationary cycles (rho_k) to 1e-8 (+ noise floor).
     The oracle runs its ParSpmmOp restatement on 16 threads (same per-row order
@@ -871,7 +871,7 @@ def test_vcycle_256_storage_mix(ctx):
     assert info[1][0]["kernel"] == "dia" and info[1][0]["value_bits"] == 8 and info[1][0]["dia_diagonals"] == 33
     assert info[2][0]["kernel"] == "classes" and info[2][0]["classes"] == 2197
     assert info[1][1]["value_bits"] == 16 and info[1][2]["value_bits"] == 16
-    assert info[3][0]["kernel"] == "sellp" and info[4][0]["kernel"] == "vector"
+    assert info[3][0]["kernel"] == "classes" and info[4][0]["kernel"] == "vector"
     levels = oracle_levels_from_gpu(mg, "jacobi")
     import sys
     sys.path.insert(0, GOLD)
