@@ -877,6 +877,39 @@ __global__ __launch_bounds__(256) void spmv_sell_kernel(SellArgs a) {
     }
 }
 
+// 16-bit codes with the table staged in LDS (dynamic, ntab doubles) by a
+// persistent grid: each workgroup stages once and walks virtual blocks v, v + G,
+// ... of the spmv_sell_kernel decomposition (the table reads become LDS reads
+// instead of dependent L2 gathers; per-block staging alone measured slower).
+template <int MODE>
+__global__ __launch_bounds__(256) void spmv_sell_t16_kernel(SellArgs a, int nvb) {
+    extern __shared__ double dtab[];
+    for (int i = threadIdx.x; i < a.ntab; i += 256) dtab[i] = a.vtab[i];
+    __syncthreads();
+    SellArgs b = a;
+    b.vtab = dtab;
+    constexpr int SPW = sell_slices_per_wave(16, MODE);
+    for (int v = blockIdx.x; v < nvb; v += gridDim.x) {
+        const int blk = xcd_remap(v, nvb);
+        const int wv = __builtin_amdgcn_readfirstlane(blk * 4 + (int)(threadIdx.x >> 6));
+        const int sl = wv * (SPW == 2 ? b.spw : 1);
+        if (sl < b.nslices) sell_wave<MODE, 16>(b, nullptr, sl);
+    }
+}
+
+// 16-bit-code SELL with its table in LDS for long rows (>= 32 entries on average:
+// R_1 of the 256^3 cycle, 87 entries per row, 40 -> 35 us; short rows such as P_1's
+// 11 pay more for the staging than they save: 47 -> 48 us with a persistent grid
+// of 2 workgroups per CU, 56 us with 4).  A/B switch FAMG_SELL_T16=0: off; N > 0:
+// also for short rows, at most N workgroups per CU.
+static int sell_t16_mode() {
+    static const int v = [] {
+        const char *e = getenv("FAMG_SELL_T16");
+        return e ? atoi(e) : -1;
+    }();
+    return v;
+}
+
 // Value-code SELL whose slices are all at most 4 steps wide with implicit or
 // u16 columns and pair up (equal width and column mode): P_0 of a box
 // hierarchy (4 entries per row).  Only the lockstep row-pair path of
@@ -2419,6 +2452,20 @@ void spmv(const GpuCsr &m, const double *x, double *y, SpmvMode mode, const Spmv
             FAMG_LAUNCH_MODES(spmv_sell_kernel, grid, block, s, a, FAMG_LAY4)
         } else if (m.sell_vbits == 8) {
             FAMG_LAUNCH_MODES(spmv_sell_kernel, grid, block, s, a, FAMG_LAY8)
+        } else if (m.sell_vbits == 16 && m.sell_ntab <= 8192 && mode != SPMV_SGS &&
+                   ((sell_t16_mode() < 0 && m.nnz >= 32 * m.nrows) || sell_t16_mode() > 0)) {
+            const int nvb = (int)grid.x;
+            const dim3 g2((unsigned)(sell_t16_mode() > 0 ? std::min(nvb, 256 * sell_t16_mode()) : nvb));
+            const size_t lds = (size_t)m.sell_ntab * sizeof(double);
+            switch (mode) {
+            case SPMV_SET: spmv_sell_t16_kernel<SPMV_SET><<<g2, block, lds, s>>>(a, nvb); break;
+            case SPMV_ADD: spmv_sell_t16_kernel<SPMV_ADD><<<g2, block, lds, s>>>(a, nvb); break;
+            case SPMV_RESID: spmv_sell_t16_kernel<SPMV_RESID><<<g2, block, lds, s>>>(a, nvb); break;
+            case SPMV_JACOBI: spmv_sell_t16_kernel<SPMV_JACOBI><<<g2, block, lds, s>>>(a, nvb); break;
+            case SPMV_RESID0: spmv_sell_t16_kernel<SPMV_RESID0><<<g2, block, lds, s>>>(a, nvb); break;
+            case SPMV_ADD0: spmv_sell_t16_kernel<SPMV_ADD0><<<g2, block, lds, s>>>(a, nvb); break;
+            default: break;
+            }
         } else if (m.sell_vbits == 16) {
             FAMG_LAUNCH_MODES(spmv_sell_kernel, grid, block, s, a, FAMG_LAY16)
         } else if (m.sell_paired) {
