@@ -403,12 +403,15 @@ void MultigridOp::ensure_workspace() {
 // Fused forms per smoother; the first step from x = 0 needs no SpMV.
 // v/t are the two buffers of the level; Jacobi ping-pongs between them.
 // FAMG_FOLD_DIA=1: fold the zero-guess step on DIA levels too (A/B switch)
-static bool fold_dia_enabled() {
-    static const bool on = [] {
+// FAMG_FOLD_DIA: unset -- fold on a DIA level whose P runs the short-slice
+// kernel (P_0 of a box hierarchy: its d*b epilogue streams dc and b instead of
+// v, the same bytes); 1 -- every DIA level; 0 -- none
+static int fold_dia_mode() {
+    static const int v = [] {
         const char *e = getenv("FAMG_FOLD_DIA");
-        return e && e[0] == '1';
+        return e ? (e[0] == '1' ? 1 : 0) : -1;
     }();
-    return on;
+    return v;
 }
 
 void MultigridOp::smooth(int64_t l, double *&v, double *&t, const double *f, bool v_zero) {
@@ -480,9 +483,10 @@ void MultigridOp::cycle(int64_t l, double *v, const double *f, bool v_zero, doub
     // values): value-code SELL and the wave-per-row kernel are latency-bound,
     // and gathering d beside x cost more there than the separate streaming
     // pass (measured on the 256^3 hierarchy).
-    // DIA storage folds only on request (FAMG_FOLD_DIA=1): the residual then
-    // gathers d beside x (139 us vs 105 + 49 for RESID + the d*f pass) but the
-    // correction's d*f epilogue on P_0 cost as much (153 vs 122 us).
+    // DIA storage folds where P runs the short-slice kernel (P_0 of the 256^3
+    // cycle): the residual gathers d beside x (115 us vs 91 + 51 for RESID + the
+    // d*f pass) and the correction's d*f epilogue costs 117 vs 99 us -- 9 us net.
+    // With the generic value-code SELL P (level 1) it lost: 58 + 49 vs 44 + 9 + 46.
     // Not where most slices carry 32-bit columns (unstructured operators): the
     // residual then gathers d as randomly as x, and that doubled gather cost more
     // than the pass it saves (Q1 elasticity 1.57M rows: 640 vs 388 + 15 us).
@@ -490,7 +494,9 @@ void MultigridOp::cycle(int64_t l, double *v, const double *f, bool v_zero, doub
     const bool fold = fold_zero_guess && v_zero && steps == 1 && A && D && P &&
                       ((A->m.kernel == SPMV_KERNEL_SELL && A->m.sell_vbits == 0 && gather_cheap) ||
                        A->m.kernel == SPMV_KERNEL_XS ||  // x-staged: d*x staged with x, no extra gather
-                       (A->m.kernel == SPMV_KERNEL_DIA && fold_dia_enabled()));
+                       (A->m.kernel == SPMV_KERNEL_DIA &&
+                        (fold_dia_mode() == 1 ||
+                         (fold_dia_mode() < 0 && P->m.kernel == SPMV_KERNEL_SELL && P->m.sell_short))));
     if (fold) {
         SpmvEpi epi;
         epi.b = f;
