@@ -501,6 +501,8 @@ void MultigridOp::cycle(int64_t l, double *v, const double *f, bool v_zero, doub
         SpmvEpi epi;
         epi.b = f;
         epi.d = D->d.get();
+        epi.dc = D->dcode.get();  // DIA: 1-B codes of d gathered instead of d
+        epi.dt = D->dtab.get();
         spmv(A->m, f, L.r.get(), SPMV_RESID0, epi, s);  // work = f - A (d f)
     } else {
         smooth(l, v, t, f, v_zero);

@@ -1024,6 +1024,28 @@ __device__ __forceinline__ void dia_codes2(const uint32_t *cp, uint32_t (&w0)[CW
 // The weighted-Jacobi epilogue with the 8-bit coded diagonal (d = dt[dc[i]],
 // dt padded to 256 entries and staged in LDS with the value table).
 constexpr int DIA_JACOBI_DC = 16;
+// The folded zero-guess residual y = b - A (d x) with the 8-bit coded diagonal:
+// the 7-point kernel gathers the 1-B codes of d beside x (dt staged in LDS)
+// instead of 8-B values of d: 17 MB instead of 134 MB more than a residual.
+constexpr int DIA_RESID0_DC = 17;
+
+// 8-bit codes at the positions dia_gx2 / dia_gx4 take their x operands from
+// (same clamps and selects)
+__device__ __forceinline__ void dia_gc2(const uint8_t *dc, int c, int ncols, uint32_t &k0, uint32_t &k1) {
+    const int cc = min(max(c, 0), ncols - 2);
+    const uint32_t a0 = dc[cc], a1 = dc[cc + 1];
+    k0 = c > ncols - 2 ? a1 : a0;
+    k1 = c < 0 ? a0 : a1;
+}
+__device__ __forceinline__ void dia_gc4(const uint8_t *dc, int c, int ncols, uint32_t (&k)[4]) {
+    const int p0 = min(max(c, 0), ncols - 2), p1 = min(max(c + 2, 0), ncols - 2);
+    const uint32_t a0 = dc[p0], a1 = dc[p0 + 1], b0 = dc[p1], b1 = dc[p1 + 1];
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+        const int t = c + j;
+        k[j] = t == p0 ? a0 : t == p0 + 1 ? a1 : t == p1 ? b0 : b1;
+    }
+}
 
 // Epilogue operands of a DIA row pair, loaded without divergence: one 16-B
 // load at i2 = min(row, row_end - 2) per vector; a tail row (row_end - 1)
@@ -1059,7 +1081,7 @@ template <int MODE, bool NT> struct DiaEpi {
             br = ldv(a.b);
         }
         if constexpr (MODE == SPMV_JACOBI) dr = ldv(a.d);
-        if constexpr (MODE == SPMV_RESID || MODE == SPMV_RESID0) br = ldv(a.b);
+        if constexpr (MODE == SPMV_RESID || MODE == SPMV_RESID0 || MODE == DIA_RESID0_DC) br = ldv(a.b);
         if constexpr (MODE == SPMV_ADD) yr = ldv(a.y);
         if constexpr (MODE == SPMV_ADD0) yr = ldv(a.d) * ldv(a.b);
     }
@@ -1069,7 +1091,7 @@ template <int MODE, bool NT> struct DiaEpi {
         if constexpr (MODE == DIA_JACOBI_DC) dr = dbl2_t{sdt[dc0], sdt[dc1]};
         if constexpr (MODE == SPMV_SET) out = acc;
         else if constexpr (MODE == SPMV_ADD || MODE == SPMV_ADD0) out = yr + acc;
-        else if constexpr (MODE == SPMV_RESID || MODE == SPMV_RESID0) out = br - acc;
+        else if constexpr (MODE == SPMV_RESID || MODE == SPMV_RESID0 || MODE == DIA_RESID0_DC) out = br - acc;
         else out = xr + dr * (br - acc);  // JACOBI
         if (l1) {
             if constexpr (NT) __builtin_nontemporal_store(out, reinterpret_cast<dbl2u_t *>(a.y + row));
@@ -1116,12 +1138,14 @@ __device__ __forceinline__ void dia_gx4(const Epi &e, int c, int ncols, double (
 template <int MODE, int VB, int CW, bool NT, int NR = 0>
 __global__ __launch_bounds__(256) void spmv_dia_kernel(DiaArgs a) {
     constexpr bool DC = MODE == DIA_JACOBI_DC;
-    constexpr int GM = DC ? SPMV_JACOBI : MODE;  // x operand of the row sums
+    constexpr bool RC = MODE == DIA_RESID0_DC && NR == -1;  // coded d gathered beside x
+    // x operand of the row sums (RC: plain x, multiplied by the decoded d after the barrier)
+    constexpr int GM = DC ? SPMV_JACOBI : RC ? SPMV_SET : MODE == DIA_RESID0_DC ? SPMV_RESID0 : MODE;
     __shared__ double stab[VB == 4 ? 16 : 256];
-    __shared__ double sdt[DC ? 256 : 1];
+    __shared__ double sdt[DC || RC ? 256 : 1];
     const double tv = (int)threadIdx.x < a.ntab ? a.vtab[threadIdx.x] : 0.0;
     double dv = 0.0;
-    if constexpr (DC) dv = a.e.dt[threadIdx.x];
+    if constexpr (DC || RC) dv = a.e.dt[threadIdx.x];
     int blk;
     if (a.band_bp > 0) {
         // 2.5-D order: XCD x takes band x (1/8 of the rows) of every plane in
@@ -1144,6 +1168,14 @@ __global__ __launch_bounds__(256) void spmv_dia_kernel(DiaArgs a) {
     ep.load(a.e, row, a.row_end);
     dia_codes2<CW>(a.codes + (int64_t)(min(row, a.row_end - 1) - a.code_row0) * CW, w0, w1);
     double xs7[4][2];  // NR == -1 (7-point): the four single diagonals
+    uint32_t ks7[4][2], kq[4];  // RC: their codes of d
+    if constexpr (RC) {
+        dia_gc2(a.e.dc, row + a.off[0], a.ncols, ks7[0][0], ks7[0][1]);
+        dia_gc2(a.e.dc, row + a.off[1], a.ncols, ks7[1][0], ks7[1][1]);
+        dia_gc4(a.e.dc, row + a.off[2], a.ncols, kq);
+        dia_gc2(a.e.dc, row + a.off[5], a.ncols, ks7[2][0], ks7[2][1]);
+        dia_gc2(a.e.dc, row + a.off[6], a.ncols, ks7[3][0], ks7[3][1]);
+    }
     if constexpr (NR > 0) {
 #pragma unroll
         for (int j = 0; j < NR; j++) dia_gx4<GM>(a.e, row + a.off[3 * j], a.ncols, xq[j]);
@@ -1158,11 +1190,19 @@ __global__ __launch_bounds__(256) void spmv_dia_kernel(DiaArgs a) {
         for (int k = 0; k < KMAX; k++) dia_gx2<GM>(a.e, row + a.off[k], a.ncols, x0[k], x1[k]);
     }
     if ((int)threadIdx.x < a.ntab) stab[threadIdx.x] = tv;
-    if constexpr (DC) sdt[threadIdx.x] = dv;
+    if constexpr (DC || RC) sdt[threadIdx.x] = dv;
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
     if (row >= a.row_end) return;
+    if constexpr (RC) {  // the zero-guess iterate d*x per column (vec_mul's product)
+#pragma unroll
+        for (int i = 0; i < 4; i++)
+#pragma unroll
+            for (int j = 0; j < 2; j++) xs7[i][j] = sdt[ks7[i][j]] * xs7[i][j];
+#pragma unroll
+        for (int j = 0; j < 4; j++) xq[0][j] = sdt[kq[j]] * xq[0][j];
+    }
     double acc0 = 0.0, acc1 = 0.0;
     if constexpr (NR == -1) {
 #pragma unroll
@@ -2249,6 +2289,15 @@ static bool dia_pat27() {
     return on;
 }
 
+// A/B switch FAMG_DIA_RC=0: the folded DIA residual gathers 8-B values of d
+static bool dia_rc_enabled() {
+    static const bool on = [] {
+        const char *e = getenv("FAMG_DIA_RC");
+        return !(e && e[0] == '0');
+    }();
+    return on;
+}
+
 // A/B switch FAMG_DIA_RUNS7=0: the 7-point DIA kernels load every diagonal's pair
 static bool dia_runs7() {
     static const bool on = [] {
@@ -2412,7 +2461,13 @@ void spmv(const GpuCsr &m, const double *x, double *y, SpmvMode mode, const Spmv
             FAMG_DIA2(SPMV_JACOBI, VB, CW)                                                        \
         }                                                                                         \
         break;                                                                                    \
-    case SPMV_RESID0: FAMG_DIA2(SPMV_RESID0, VB, CW) break;                                       \
+    case SPMV_RESID0:                                                                             \
+        if (e.dc && dia_rc_enabled()) {                                                           \
+            FAMG_DIA2(DIA_RESID0_DC, VB, CW)                                                      \
+        } else {                                                                                  \
+            FAMG_DIA2(SPMV_RESID0, VB, CW)                                                        \
+        }                                                                                         \
+        break;                                                                                    \
     case SPMV_ADD0: FAMG_DIA2(SPMV_ADD0, VB, CW) break;                                           \
     default: break;                                                                               \
     }
