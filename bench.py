@@ -139,6 +139,15 @@ def fa_block_to_csr(S):
     return fa.SparseMatOp(h, S.ctx)
 
 
+def cgroup_cpu_quota():
+    """CPUs this process's cgroup may use (cpu.max quota / period), None if unlimited."""
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        return None if q == "max" else round(int(q) / int(per), 2)
+    except (OSError, ValueError):
+        return None
+
+
 def _time_cycles(omg, b, budget_s, max_cycles=60, min_cycles=3):
     """Per-V-cycle wall times of the oracle (after one warm-up cycle)."""
     import numpy as np
@@ -176,12 +185,13 @@ def cpu_side(mg, A, b_host, z_gpu, args):
     OA = levels[0]["A"]
     log(f"oracle hierarchy import {time.perf_counter() - t_imp:.1f}s")
     nproc = os.cpu_count() or 1
-    all_threads = min(nproc, 64)
+    all_threads = nproc  # every host core ("all host cores", count from nproc)
     t16 = args.cpu_threads
 
-    # parity of one V-cycle (the bench's own z from the timed loop)
+    # parity of one V-cycle (the bench's own z from the timed loop); >= 50 cycles
+    # at 16 threads (median over >= 50 cycles)
     omg.set_parallel(t16)
-    ts16, zref = _time_cycles(omg, b_host, args.cpu_budget)
+    ts16, zref = _time_cycles(omg, b_host, args.cpu_budget, min_cycles=args.cpu_min_cycles)
     rel_err = float(np.linalg.norm(z_gpu - zref) / np.linalg.norm(zref))
     # residual history of 10 stationary cycles (simple_geometric.rs:117-158)
     K = 10
@@ -215,9 +225,11 @@ def cpu_side(mg, A, b_host, z_gpu, args):
            "fine_spmv_GBs_usize_layout": round((16 * nnz + 8 * (m + 1) + 8 * n + 8 * m) / spmv_t / 1e9, 2)}
     if all_threads != t16:
         omg.set_parallel(all_threads)
-        tsa, _ = _time_cycles(omg, b_host, args.cpu_budget / 2)
+        tsa, _ = _time_cycles(omg, b_host, args.cpu_budget / 2, min_cycles=3)
         res["all_cores"] = {"value": round(1.0 / float(np.median(tsa)), 4), "cores": all_threads,
-                            "nproc": nproc, "sample": f"median of {len(tsa)} V-cycles"}
+                            "nproc": nproc, "cpu_quota": cgroup_cpu_quota(),
+                            "sample": f"median of {len(tsa)} V-cycles at {all_threads} OpenMP threads"}
+        omg.set_parallel(t16)
     parity = {"vcycle_rel_err": rel_err, "tol": 1e-11, "ok": rel_err <= 1e-11,
               "rho_k_gpu": [float(v) for v in hist_gpu], "rho_k_cpu": [float(v) for v in hist_cpu],
               "rho_k_max_rel_diff": rho_rel,
@@ -249,7 +261,7 @@ def build_problem(fa, ctx, args, dims):
         bs = args.block_size
         nn = fa.constant_candidates(A.nrows, bs)
         mg = fa.smoothed_aggregation(A, nn, block_size=bs, candidate_dimension=bs, coarsest_dim=1000,
-                                     smoother=args.smoother)
+                                     smoother=args.smoother, strength_depth=args.strength_depth)
     return A, mg
 
 
@@ -262,66 +274,24 @@ def workload_name(args, dims):
            f"within {perm})"
            if args.problem == "elast" else f"Matrix Market {os.path.basename(args.mtx)}")
     return (f"SA V-cycle, {src}, block size {args.block_size}, {args.block_size} constant candidates, "
+            f"strength graph depth {args.strength_depth} (reference: 3, partitioners/mod.rs:290), "
             f"MIS aggregates, block-Jacobi P smoothing, {args.smoother} s=1 mu=1, Cholesky coarsest")
 
 
-def sgs_sweep_bytes(S, A, n, launches):
-    """Algorithmic bytes of `launches` color updates of a multicolor SGS sweep
-    (DESIGN.md 5): per launch over the n_c = n / C rows of one color, that
-    color's share of the sweep storage (DIA codes of the color-permuted copy,
-    or its SELL bytes), perm + d + b (20 B), x read and written (16 B) per row,
-    and the other colors' x entries the rows gather (8 (n - n_c))."""
-    import faer_amg_amd as fa
-    st = fa.sgs_info(S)
-    C = st["colors"]
-    if st["kernel"] == "dia":
-        cw = 1
-        while 32 * cw < st["diagonals"] * st["bits"]:
-            cw *= 2
-        sweep = 4 * cw * n
-    else:
-        sweep = A.spmv_info()["stream_bytes"]
-    nc = n / C
-    return launches * (sweep / C + 36 * nc + 8 * (n - nc)), C
-
-
-def vcycle_bytes(mg, csr=False, fold=True):
-    """Algorithmic bytes of one V-cycle (s = 1, mu = 1, zero initial guess) from the
-    per-kernel formulas of SURVEY.md 8(d); matrix bytes of the chosen storage
-    (csr=False) or of 32-bit CSR (csr=True).  fold: diagonal smoothers fold the
-    first smoothing step v = d f into the residual (reads f, d; writes r) and the
-    correction (reads d, f, P, v_c; writes v) -- no separate 24n pass.  SGS
-    levels count their 2C - 1 color launches per smoothing step (sgs_sweep_bytes)."""
-    def mat(M):
-        return 12 * M.nnz + 4 * (M.nrows + 1) if csr else M.spmv_info()["stream_bytes"]
-    tot = 0
-    nl = mg.levels()
-    fold_all = fold
-    for l in range(nl):
-        A, S, R, P = mg.level(l)
-        n = A.nrows
-        if l == nl - 1:
-            tot += 8 * n * n + 16 * n
-            continue
-        bA = mat(A)
-        nc = R.nrows
-        info = A.spmv_info()
-        tot += bA + 24 * n                             # residual
-        tot += mat(R) + 8 * n + 8 * nc                 # restrict
-        if S.kind == "sgs":
-            pre, C = sgs_sweep_bytes(S, A, n, 1)
-            post, _ = sgs_sweep_bytes(S, A, n, 2 * C - 1)
-            tot += 8 * n + (2 * C - 2) * pre + 28 * n / C  # e = 0, first color e = d r, 2C - 2 launches
-            tot += mat(P) + 8 * nc + 16 * n           # interpolate + add
-            tot += post                                # post-smoothing sweep on x
-            continue
-        # the library folds only diagonal smoothers on fp64-valued SELL storage
-        fold = (fold_all and S.kind == "diag" and info["kernel"] == "sell" and info["value_bits"] == 0
-                and 2 * info["slices_i32"] < info["slices"])
-        tot += 0 if fold else 24 * n                   # first smoothing step from 0
-        tot += mat(P) + 8 * nc + (24 if fold else 16) * n  # interpolate + add
-        tot += bA + 32 * n                             # post-smoothing Jacobi
-    return tot
+def plan_summary(plan):
+    """Per-level and whole-cycle algorithmic bytes from the library's own launch
+    plan of one V-cycle (amg_multigrid_cycle_plan: every launch the cycle makes,
+    with the bytes its storage streams and the vectors it moves)."""
+    lv = {}
+    for r in plan:
+        d = lv.setdefault(r["level"], {"launches": 0, "bytes": 0, "csr_bytes": 0, "kernels": []})
+        d["launches"] += 1
+        d["bytes"] += r["bytes"]
+        d["csr_bytes"] += r["csr_bytes"]
+        d["kernels"].append(f"{r['role']}:{r['name']}:{r['mode']}")
+    return {"launches": len(plan), "bytes": sum(r["bytes"] for r in plan),
+            "csr_bytes": sum(r["csr_bytes"] for r in plan),
+            "per_level": [dict(level=l, **lv[l]) for l in sorted(lv)]}
 
 
 def run_single(args):
@@ -352,11 +322,13 @@ def run_single(args):
         mg.apply(z, b)
     torch.cuda.synchronize()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    ctx.trace_mark(1)  # k_trace_mark<<<1>>> ... <<<2>>> bracket the timed cycles in a kernel trace
     t_wall0 = time.perf_counter()
     e0.record(stream)
     for _ in range(args.steps):
         mg.apply(z, b)
     e1.record(stream)
+    ctx.trace_mark(2)
     torch.cuda.synchronize()
     t_wall = time.perf_counter() - t_wall0
     ms_per_cycle = e0.elapsed_time(e1) / args.steps
@@ -414,8 +386,12 @@ def run_single(args):
     A.apply(r, z)
     torch.cuda.synchronize()
     rho1 = float(torch.linalg.norm(b - r) / torch.linalg.norm(b))
-    vbytes = vcycle_bytes(mg, fold=not args.no_fold)
-    vbytes_csr = vcycle_bytes(mg, csr=True, fold=not args.no_fold)
+    plan = mg.cycle_plan()
+    psum = plan_summary(plan)
+    vbytes, vbytes_csr = psum["bytes"], psum["csr_bytes"]
+    if args.plan_out:
+        with open(args.plan_out, "w") as fh:
+            json.dump({"steps": args.steps, "plan": plan}, fh)
 
     cpu, parity = None, None
     if not args.no_cpu_baseline:
@@ -448,6 +424,11 @@ def run_single(args):
                    "vcycle_algorithmic_GB": round(vbytes / 1e9, 3),
                    "vcycle_GBs": round(vbytes / (ms_per_cycle * 1e-3) / 1e9, 1),
                    "vcycle_csr_equivalent_GB": round(vbytes_csr / 1e9, 3),
+                   "vcycle_plan": {"launches": psum["launches"],
+                                   "source": "amg_multigrid_cycle_plan (the launches the library makes)",
+                                   "per_level_GB": [round(d["bytes"] / 1e9, 4) for d in psum["per_level"]],
+                                   "per_level_launches": [d["launches"] for d in psum["per_level"]],
+                                   "per_level_kernels": [d["kernels"] for d in psum["per_level"]]},
                    "rel_residual_after_1_cycle": rho1,
                    "parallelism": "single GPU"},
         "fine_spmv_gbs": round(achieved, 1),
@@ -567,7 +548,7 @@ def run_dist(args, world, rank, local_rank):
         "metric": METRIC,
         "value": round(cycles_per_s if strong else cycles_per_s * world, 3),
         "unit": "V-cycles/s",
-        "n_gpus": world,
+        "n_gpus": comm.nranks,
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": round(ms_per_cycle, 4),
@@ -588,6 +569,7 @@ def run_dist(args, world, rank, local_rank):
                    "agglomerate_rows": args.agglomerate,
                    "halo_overlap": not args.no_overlap,
                    "rccl": fa.rccl_library(),
+                   "rccl_ranks": comm.nranks,
                    "parallelism": f"row-block {'z-slabs' if args.problem in ('7pt', '27pt') else 'row ranges'} "
                                   f"x{world}, RCCL halo exchange"},
         "fine_spmv_gbs": round(float(ga[0]), 1),
@@ -655,6 +637,81 @@ def c4_single_gpu_rate(fa, ctx, args, stream, cycles=10):
     return 1000.0 / ms
 
 
+def visible_gpus():
+    """GPUs this process may use.  torch.cuda.device_count() counts devices
+    without creating a HIP context on this image, so the launcher stays
+    GPU-free and its children start on untouched devices."""
+    import torch
+    return torch.cuda.device_count()
+
+
+def free_port():
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(n):
+    """`python bench.py --gpus N` without an outer launcher: start N rank
+    processes (torch.distributed.run, one per GPU, rendezvous on 127.0.0.1)
+    as a child process, forward every rank's stderr and rank 0's JSON line,
+    and return the exit status (non-zero when fewer than N GPUs are visible,
+    a rank fails, or rank 0 printed no line)."""
+    import subprocess
+    if os.environ.get("FAMG_BENCH_LAUNCH_CHECK") != "1":
+        have = visible_gpus()
+        if have < n:
+            log(f"bench.py --gpus {n}: only {have} GPU(s) visible")
+            return 3
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(free_port()),
+           os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # dmabuf IPC (RCCL between processes)
+    env.setdefault("OMP_NUM_THREADS", "16")
+    log("launching: " + " ".join(cmd))
+    proc = subprocess.Popen(cmd, stdout=subprocess.PIPE, text=True, env=env)
+    lines = []
+    for line in proc.stdout:
+        s = line.strip()
+        if s.startswith("{"):
+            try:
+                d = json.loads(s)
+            except ValueError:
+                d = None
+            if isinstance(d, dict) and "metric" in d:
+                lines.append(s)
+                continue
+        sys.stderr.write(line)
+    rc = proc.wait()
+    if rc != 0:
+        log(f"rank processes exited with status {rc}")
+        return rc
+    if len(lines) != 1:
+        log(f"expected one JSON line from rank 0, got {len(lines)}")
+        return 4
+    print(lines[0], flush=True)
+    return 0
+
+
+def launch_check(world, rank):
+    """FAMG_BENCH_LAUNCH_CHECK=1: what a rank does instead of the GPU work when
+    the launcher is tested on a CPU-only machine -- join the process group
+    (gloo), agree on the world size with an all-reduce, rank 0 returns a line."""
+    import torch
+    import torch.distributed as dist
+    dist.init_process_group("gloo")
+    t = torch.tensor([1.0], dtype=torch.float64)
+    dist.all_reduce(t)
+    out = {"metric": METRIC, "value": None, "n_gpus": dist.get_world_size(), "ranks_counted": int(t[0]),
+           "launch_check": True}
+    dist.destroy_process_group()
+    return out if rank == 0 else None
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -672,6 +729,9 @@ def main():
                     help="elast: node numbering shuffled within windows of this many nodes (the locality "
                          "of a mesh numbering without stencil structure); 0 = over all nodes")
     ap.add_argument("--block-size", type=int, default=3, help="elast/mtx: dofs per node")
+    ap.add_argument("--strength-depth", type=int, default=1,
+                    help="elast/mtx: BFS depth of the strength graph (the reference hard-codes 3, "
+                         "partitioners/mod.rs:290; 1 by default here for memory, DESIGN.md 10)")
     ap.add_argument("--agglomerate", type=int, default=None,
                     help="levels with fewer global rows run redundantly on every rank "
                          "(default 16384 x world: a level is distributed while every rank owns "
@@ -679,6 +739,8 @@ def main():
                          "redundant cycle)")
     ap.add_argument("--cpu-threads", type=int, default=int(os.environ.get("OMP_NUM_THREADS", "16")))
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-min-cycles", type=int, default=50,
+                    help="CPU baseline: at least this many V-cycles at --cpu-threads")
     ap.add_argument("--cpu-budget", type=float, default=20.0,
                     help="seconds of CPU V-cycles at --cpu-threads (half that at all cores)")
     ap.add_argument("--no-graph", action="store_true")
@@ -693,6 +755,8 @@ def main():
                          "carries the C4 strong-scaling ratio) or c4 (512^3 fixed at every N, strong)")
     ap.add_argument("--no-c4-base", action="store_true",
                     help="skip the one-GPU 512^3 measurement behind the C4 ratio")
+    ap.add_argument("--plan-out", default=None,
+                    help="write the V-cycle launch plan (JSON) here, for scripts/prof_summary.py --plan")
     ap.add_argument("--dist", action="store_true",
                     help="distributed path even at world size 1 (1-rank RCCL; a check of run_dist)")
     args = ap.parse_args()
@@ -703,9 +767,20 @@ def main():
     if args.problem == "mtx" and not args.mtx:
         ap.error("--problem mtx needs --mtx PATH")
 
+    if (args.gpus > 1 or args.dist) and "WORLD_SIZE" not in os.environ:
+        # `python bench.py --gpus N` (or --dist): start the N rank processes
+        # ourselves (before anything touches the GPU) and forward rank 0's line
+        sys.exit(launch_ranks(args.gpus))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        log(f"note: WORLD_SIZE={world} but --gpus {args.gpus}; the job runs {world} ranks")
+    if os.environ.get("FAMG_BENCH_LAUNCH_CHECK") == "1":
+        out = launch_check(world, rank)  # CPU-only launcher check (tests/test_bench_launch.py)
+        if out is not None:
+            print(json.dumps(out), flush=True)
+        return
     if args.workload == "c4" and world == 1 and not args.dist:
         args.edge = 512  # C4 on one GPU: the base of the strong-scaling curve
     if world > 1 or args.dist:

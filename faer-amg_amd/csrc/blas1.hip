@@ -59,6 +59,7 @@ FAMG_EW_KERNEL(k_mul_coded, (double *o, const uint8_t *dc, const double *dt, con
 
 void vec_mul_coded(double *o, const uint8_t *dc, const double *dt, const double *a, int64_t n, hipStream_t s) {
     if (n <= 0) return;
+    log_launch("vec_mul_coded", -1, -1, n, 17 * n);
     const bool aligned = ((reinterpret_cast<uintptr_t>(o) | reinterpret_cast<uintptr_t>(a)) & 15) == 0;
     if (aligned && n >= 2) {
         const int64_t n2 = n / 2;
@@ -71,19 +72,24 @@ void vec_mul_coded(double *o, const uint8_t *dc, const double *dt, const double 
 }
 
 void vec_fill(double *x, double v, int64_t n, hipStream_t s) {
+    if (n > 0) log_launch("vec_fill", -1, -1, n, 8 * n);
     if (n > 0) hipLaunchKernelGGL(k_fill, dim3(ew_grid(n)), dim3(EW_BS), 0, s, x, v, n);
 }
 void vec_copy(double *dst, const double *src, int64_t n, hipStream_t s) {
+    if (n > 0) log_launch("vec_copy", -1, -1, n, 16 * n);
     if (n > 0) FAMG_CHECK_HIP(hipMemcpyAsync(dst, src, n * sizeof(double), hipMemcpyDeviceToDevice, s));
 }
 void vec_sub(double *o, const double *a, const double *b, int64_t n, hipStream_t s) {
+    if (n > 0) log_launch("vec_sub", -1, -1, n, 24 * n);
     if (n > 0) hipLaunchKernelGGL(k_sub, dim3(ew_grid(n)), dim3(EW_BS), 0, s, o, a, b, n);
 }
 void vec_add_inplace(double *x, const double *y, int64_t n, hipStream_t s) {
+    if (n > 0) log_launch("vec_add", -1, -1, n, 24 * n);
     if (n > 0) hipLaunchKernelGGL(k_add, dim3(ew_grid(n)), dim3(EW_BS), 0, s, x, y, n);
 }
 void vec_mul(double *o, const double *d, const double *a, int64_t n, hipStream_t s) {
     if (n <= 0) return;
+    log_launch("vec_mul", -1, -1, n, 24 * n);
     const bool aligned = ((reinterpret_cast<uintptr_t>(o) | reinterpret_cast<uintptr_t>(d) |
                            reinterpret_cast<uintptr_t>(a)) & 15) == 0;
     if (aligned && n >= 2) {
@@ -96,15 +102,19 @@ void vec_mul(double *o, const double *d, const double *a, int64_t n, hipStream_t
     }
 }
 void vec_axpy(double *y, double al, const double *x, int64_t n, hipStream_t s) {
+    if (n > 0) log_launch("vec_axpy", -1, -1, n, 24 * n);
     if (n > 0) hipLaunchKernelGGL(k_axpy, dim3(ew_grid(n)), dim3(EW_BS), 0, s, y, al, x, n);
 }
 void vec_xpay(double *y, double be, const double *x, int64_t n, hipStream_t s) {
+    if (n > 0) log_launch("vec_xpay", -1, -1, n, 24 * n);
     if (n > 0) hipLaunchKernelGGL(k_xpay, dim3(ew_grid(n)), dim3(EW_BS), 0, s, y, be, x, n);
 }
 void vec_scale(double *x, double al, int64_t n, hipStream_t s) {
+    if (n > 0) log_launch("vec_scale", -1, -1, n, 16 * n);
     if (n > 0) hipLaunchKernelGGL(k_scale, dim3(ew_grid(n)), dim3(EW_BS), 0, s, x, al, n);
 }
 void vec_nn_step(double *x, const double *d, const double *r, int64_t n, hipStream_t s) {
+    if (n > 0) log_launch("vec_nn_step", -1, -1, n, 32 * n);
     if (n > 0) hipLaunchKernelGGL(k_nn_step, dim3(ew_grid(n)), dim3(EW_BS), 0, s, x, d, r, n);
 }
 
@@ -144,6 +154,7 @@ __global__ __launch_bounds__(256) void k_dot_final(const double *partials, doubl
 
 void vec_dot_dev(const double *x, const double *y, int64_t n, double *res, Ctx &ctx) {
     if (ctx.red_partials.size() < (size_t)RED_GRID) ctx.red_partials.resize(RED_GRID);
+    log_launch("vec_dot", -1, -1, n, 16 * n);
     hipLaunchKernelGGL(k_dot_partial, dim3(RED_GRID), dim3(256), 0, ctx.stream, x, y, n,
                        ctx.red_partials.get());
     hipLaunchKernelGGL(k_dot_final, dim3(1), dim3(256), 0, ctx.stream, ctx.red_partials.get(), res);
@@ -176,6 +187,7 @@ __global__ __launch_bounds__(256) void k_gemv(const double *M, const double *x, 
 
 void dense_gemv(const double *M, const double *x, double *out, int64_t n, hipStream_t s) {
     if (n <= 0) return;
+    log_launch("gemv", -1, -1, n, 8 * n * n + 16 * n);
     hipLaunchKernelGGL(k_gemv, dim3((unsigned)ceil_div(n, 4)), dim3(256), 0, s, M, x, out, n);
     FAMG_CHECK_HIP(hipGetLastError());
 }

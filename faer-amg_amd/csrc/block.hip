@@ -53,6 +53,8 @@ __global__ __launch_bounds__(BLK_CHUNK) void k_block_apply(const int32_t *rows, 
 void BlockSmootherOp::apply(double *out, const double *rhs) {
     if (nchunks == 0) return;
     const size_t lds = sizeof(double) * std::max<int64_t>(BLK_CHUNK, max_block);
+    // inverses + rows/blk_of (8 B per row) + r gathered + out written
+    log_launch("block", -1, -1, nrows, 8 * (int64_t)inv.size() + 24 * nrows);
     hipLaunchKernelGGL(k_block_apply, dim3((unsigned)nchunks), dim3(BLK_CHUNK), lds, ctx->stream, rows.get(),
                        blk_of.get(), bptr.get(), ioff.get(), chunk.get(), inv.get(), rhs, out);
     FAMG_CHECK_HIP(hipGetLastError());

@@ -607,6 +607,38 @@ amg_status amg_multigrid_apply(amg_linop *mg, double *out, int64_t ld_out, const
     });
 }
 
+amg_status amg_multigrid_cycle_plan(amg_linop *mg, amg_launch_rec *recs, int64_t cap, int64_t *count) {
+    return guard([&] {
+        auto m = need_mg(mg);
+        FAMG_REQUIRE(count && cap >= 0, AMG_ERR_INVALID, "bad argument");
+        m->ctx->set_device();
+        const std::vector<LaunchRec> plan = m->cycle_plan();
+        *count = (int64_t)plan.size();
+        if (!recs) return;
+        for (int64_t i = 0; i < std::min<int64_t>(cap, (int64_t)plan.size()); i++) {
+            const LaunchRec &r = plan[i];
+            amg_launch_rec &o = recs[i];
+            o.level = r.level;
+            o.role = r.role;
+            o.kernel = r.kernel;
+            o.mode = r.mode;
+            o.rows = r.rows;
+            o.bytes = r.bytes;
+            o.csr_bytes = r.csr_bytes;
+            std::memset(o.name, 0, sizeof(o.name));
+            std::strncpy(o.name, r.name, sizeof(o.name) - 1);
+        }
+    });
+}
+
+amg_status amg_trace_mark(amg_ctx *ctx, int32_t tag) {
+    return guard([&] {
+        FAMG_REQUIRE(ctx, AMG_ERR_INVALID, "null context");
+        ctx->ctx.set_device();
+        trace_mark(ctx->ctx, tag);
+    });
+}
+
 amg_status amg_multigrid_get_level(const amg_linop *mg, int64_t level, amg_linop **A, amg_linop **S,
                                    amg_linop **R, amg_linop **P) {
     return guard([&] {

@@ -118,4 +118,33 @@ struct Ctx {
 
 inline int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
 
+// Launch plan (amg_multigrid_cycle_plan): while g_launch_log is set on this
+// thread, every kernel the V-cycle launches appends one record with the
+// algorithmic bytes of that launch (the bytes its storage streams
+// + the vectors it reads and writes) and its 32-bit-CSR equivalent.  The
+// records come from the code that issues the launches, so fold decisions,
+// SGS colour launches and storage choices are what actually ran.
+struct LaunchRec {
+    int32_t level, role, kernel, mode;
+    int64_t rows, bytes, csr_bytes;
+    const char *name;
+};
+struct LaunchLog {
+    std::vector<LaunchRec> recs;
+    int32_t level = 0, role = AMG_ROLE_OTHER;
+};
+extern thread_local LaunchLog *g_launch_log;
+inline void log_launch(const char *name, int32_t kernel, int32_t mode, int64_t rows, int64_t bytes,
+                       int64_t csr_bytes = -1) {
+    if (g_launch_log)
+        g_launch_log->recs.push_back({g_launch_log->level, g_launch_log->role, kernel, mode, rows, bytes,
+                                      csr_bytes < 0 ? bytes : csr_bytes, name});
+}
+inline void log_at(int64_t level, int32_t role) {
+    if (g_launch_log) {
+        g_launch_log->level = (int32_t)level;
+        g_launch_log->role = role;
+    }
+}
+
 }  // namespace famg

@@ -60,13 +60,23 @@ struct RcclApi {
     decltype(&ncclAllReduce) AllReduce = nullptr;
 };
 
+// The mapped object whose basename is librccl.so or librccl.so.<version> (not a
+// plugin such as librccl-net.so).
 static int find_mapped_rccl(struct dl_phdr_info *info, size_t, void *data) {
-    if (info->dlpi_name && std::strstr(info->dlpi_name, "librccl")) {
+    if (!info->dlpi_name) return 0;
+    const char *base = std::strrchr(info->dlpi_name, '/');
+    base = base ? base + 1 : info->dlpi_name;
+    if (std::strncmp(base, "librccl.so", 10) == 0 && (base[10] == '\0' || base[10] == '.')) {
         *static_cast<std::string *>(data) = info->dlpi_name;
         return 1;
     }
     return 0;
 }
+
+static const char *const RCCL_SYMS[] = {"ncclGetErrorString", "ncclGetUniqueId", "ncclCommInitRank",
+                                        "ncclCommDestroy",    "ncclGroupStart",  "ncclGroupEnd",
+                                        "ncclSend",           "ncclRecv",        "ncclAllGather",
+                                        "ncclAllReduce"};
 
 static RcclApi load_rccl() {
     RcclApi a;
@@ -77,15 +87,29 @@ static RcclApi load_rccl() {
     if (const char *e = getenv("FAMG_RCCL_PATH")) cands.push_back({e, RTLD_NOW});
     cands.push_back({"librccl.so.1", RTLD_NOW});
     cands.push_back({"/opt/rocm/lib/librccl.so.1", RTLD_NOW});
+    // first candidate that loads and exports every entry point; a candidate
+    // lacking one is closed and the next one tried
+    std::string tried;
     for (auto &c : cands) {
-        a.h = dlopen(c.first.c_str(), c.second);
-        if (a.h) {
-            a.path = c.first;
-            break;
+        void *h = dlopen(c.first.c_str(), c.second);
+        if (!h) {
+            tried += " " + c.first + " (not loadable)";
+            continue;
         }
+        const char *missing = nullptr;
+        for (const char *name : RCCL_SYMS)
+            if (!dlsym(h, name)) { missing = name; break; }
+        if (missing) {
+            tried += " " + c.first + " (lacks " + missing + ")";
+            dlclose(h);
+            continue;
+        }
+        a.h = h;
+        a.path = c.first;
+        break;
     }
     if (!a.h) {
-        a.error = "cannot load librccl (tried the mapped one, $FAMG_RCCL_PATH, librccl.so.1, /opt/rocm/lib)";
+        a.error = "cannot load librccl:" + tried;
         return a;
     }
     auto sym = [&](const char *name) {

@@ -242,6 +242,9 @@ void vec_nn_step(double *x, const double *d, const double *r, int64_t n, hipStre
 void vec_dot_dev(const double *x, const double *y, int64_t n, double *res, Ctx &ctx);
 double vec_dot(const double *x, const double *y, int64_t n, Ctx &ctx);  // syncs
 
+// marker kernel for rocprofv3 traces (amg_trace_mark)
+void trace_mark(Ctx &ctx, int32_t tag);
+
 // dense row-major GEMV: out = M * x (M n x n)
 void dense_gemv(const double *M, const double *x, double *out, int64_t n, hipStream_t s);
 
@@ -370,6 +373,8 @@ struct MultigridOp : LinOp {
     // V-cycle building blocks (also used by the distributed multigrid)
     void cycle(int64_t l, double *v, const double *f, bool v_zero, double *out_final);
     void smooth(int64_t l, double *&v, double *&t, const double *f, bool v_zero);
+    // launch records of one V-cycle (eager, recorder on)
+    std::vector<LaunchRec> cycle_plan();
 
   private:
     struct GraphEntry {

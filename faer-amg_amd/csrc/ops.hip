@@ -256,6 +256,7 @@ void SgsOp::sweep(double *e, const double *r) {
     if (!n) return;
     vec_fill(e, 0.0, n, s);
     const int64_t p0 = color_ptr[0], p1 = color_ptr[1];
+    if (p1 > p0) log_launch("sgs_first", -1, -1, p1 - p0, 28 * (p1 - p0));
     if (p1 > p0)
         hipLaunchKernelGGL(k_sgs_first, dim3((unsigned)ceil_div(p1 - p0, 256)), dim3(256), 0, s,
                            perm.get(), dinv.get(), r, e, p0, p1);
@@ -421,6 +422,7 @@ void MultigridOp::smooth(int64_t l, double *&v, double *&t, const double *f, boo
     auto *A = dynamic_cast<CsrOp *>(L.A.get());
     auto *D = dynamic_cast<DiagOp *>(L.S.get());
     auto *G = dynamic_cast<SgsOp *>(L.S.get());
+    log_at(l, AMG_ROLE_SMOOTH);
     for (int64_t it = 0; it < steps; it++) {
         const bool zero = v_zero && it == 0;
         if (A && D) {
@@ -468,6 +470,7 @@ void MultigridOp::cycle(int64_t l, double *v, const double *f, bool v_zero, doub
     hipStream_t s = ctx->stream;
     const int64_t n = L.A->nrows;
     if (l == (int64_t)levels.size() - 1) {
+        log_at(l, AMG_ROLE_COARSE);
         L.S->apply(v, f);  // smoother.apply(v, f) (:291)
         return;
     }
@@ -498,6 +501,7 @@ void MultigridOp::cycle(int64_t l, double *v, const double *f, bool v_zero, doub
                         (fold_dia_mode() == 1 ||
                          (fold_dia_mode() < 0 && P->m.kernel == SPMV_KERNEL_SELL && P->m.sell_short))));
     if (fold) {
+        log_at(l, AMG_ROLE_RESID);
         SpmvEpi epi;
         epi.b = f;
         epi.d = D->d.get();
@@ -506,6 +510,7 @@ void MultigridOp::cycle(int64_t l, double *v, const double *f, bool v_zero, doub
         spmv(A->m, f, L.r.get(), SPMV_RESID0, epi, s);  // work = f - A (d f)
     } else {
         smooth(l, v, t, f, v_zero);
+        log_at(l, AMG_ROLE_RESID);
         if (A) {
             SpmvEpi epi;
             epi.b = f;
@@ -516,8 +521,10 @@ void MultigridOp::cycle(int64_t l, double *v, const double *f, bool v_zero, doub
         }
     }
     MgLevel &C = levels[l + 1];
+    log_at(l, AMG_ROLE_RESTRICT);
     L.R->apply(C.f.get(), L.r.get());  // f_c = R work (:343)
     for (int64_t k = 0; k < mu; k++) cycle(l + 1, C.v.get(), C.f.get(), k == 0, nullptr);
+    log_at(l, AMG_ROLE_INTERP);
     if (fold) {
         SpmvEpi epi;
         epi.b = f;
@@ -533,6 +540,7 @@ void MultigridOp::cycle(int64_t l, double *v, const double *f, bool v_zero, doub
         vec_add_inplace(v, L.r.get(), n, s);
     }
     smooth(l, v, t, f, false);  // post-smoothing (:361-369)
+    log_at(l, AMG_ROLE_OTHER);
     if (v != v0) vec_copy(v0, v, n, s);
 }
 
@@ -575,6 +583,36 @@ void MultigridOp::apply(double *out, const double *rhs) {
     }
     graphs_.push_back({out, rhs, exec});
     FAMG_CHECK_HIP(hipGraphLaunch(exec, s));
+}
+
+// Launch plan of one V-cycle (amg_multigrid_cycle_plan): one eager cycle on
+// scratch vectors (b = 1) with the launch recorder on.
+std::vector<LaunchRec> MultigridOp::cycle_plan() {
+    std::lock_guard<std::mutex> lk(mtx);
+    FAMG_REQUIRE(!levels.empty(), AMG_ERR_INVALID, "empty multigrid");
+    ensure_workspace();
+    const int64_t n = levels[0].A->nrows;
+    DevBuf<double> b(std::max<int64_t>(1, n)), z(std::max<int64_t>(1, n));
+    vec_fill(b.get(), 1.0, n, ctx->stream);
+    LaunchLog log;
+    g_launch_log = &log;
+    try {
+        cycle(0, z.get(), b.get(), true, z.get());
+    } catch (...) {
+        g_launch_log = nullptr;
+        throw;
+    }
+    g_launch_log = nullptr;
+    FAMG_CHECK_HIP(hipStreamSynchronize(ctx->stream));
+    return log.recs;
+}
+
+// empty: only its name and grid (1 block per tag unit) show in a kernel trace
+__global__ void k_trace_mark() {}
+
+void trace_mark(Ctx &ctx, int32_t tag) {
+    hipLaunchKernelGGL(k_trace_mark, dim3((unsigned)std::max<int32_t>(1, tag)), dim3(64), 0, ctx.stream);
+    FAMG_CHECK_HIP(hipGetLastError());
 }
 
 // ------------------------------------------------------------------- setup

@@ -28,6 +28,7 @@
 // Determinism rules the reference leaves to unstable sorts are fixed here:
 // ties in strength are broken by column, ties in MIS degree by node index.
 #include <algorithm>
+#include <atomic>
 #include <cmath>
 #include <cstring>
 #include <numeric>
@@ -357,11 +358,11 @@ CsrPtr sa_tentative_block(Ctx *ctx, int64_t nnodes, int64_t bs, const int64_t *a
     std::vector<int64_t> rp(n + 1), col(n * cd);
     std::vector<double> val(n * cd);
     for (int64_t i = 0; i <= n; i++) rp[i] = i * cd;
-    bool ok = true;
+    std::atomic<bool> ok{true};  // written by the OpenMP threads
 #pragma omp parallel for schedule(dynamic, 64)
     for (int64_t a = 0; a < naggs; a++) {
         const int64_t na = aptr[a + 1] - aptr[a], rows = na * bs;
-        if (rows < cd) { ok = false; continue; }  // the reference asserts (:757-762)
+        if (rows < cd) { ok.store(false, std::memory_order_relaxed); continue; }  // the reference asserts (:757-762)
         std::vector<double> M(rows * k), U, s, V;
         for (int64_t li = 0; li < na; li++) {
             const int64_t node = anodes[aptr[a] + li];
@@ -506,11 +507,14 @@ CsrPtr block_jacobi_smooth(CsrOp &A, const CsrOp &P, int64_t bs, double omega) {
     const int64_t nb = n / bs;
     std::vector<int64_t> rp(n + 1), col(n * bs);
     std::vector<double> val(n * bs);
-    bool ok = true;
+    std::atomic<bool> ok{true};  // written by the OpenMP threads
 #pragma omp parallel for schedule(static)
     for (int64_t b = 0; b < nb; b++) {
         std::vector<double> inv(bs * bs);
-        if (!block_inverse_eig(bs, hb.data() + b * bs * bs, inv.data())) { ok = false; continue; }
+        if (!block_inverse_eig(bs, hb.data() + b * bs * bs, inv.data())) {
+            ok.store(false, std::memory_order_relaxed);
+            continue;
+        }
         for (int64_t i = 0; i < bs; i++)
             for (int64_t j = 0; j < bs; j++) {
                 col[(b * bs + i) * bs + j] = b * bs + j;

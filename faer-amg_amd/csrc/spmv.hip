@@ -2339,11 +2339,77 @@ static bool dia_runs7() {
     return on;
 }
 
+thread_local LaunchLog *g_launch_log = nullptr;
+
+// Launch-plan record of one spmv() call (amg_multigrid_cycle_plan): the storage
+// the dispatch below takes, the bytes that storage streams for the launched rows,
+// x read once, and the epilogue's vector traffic per mode.
+static void log_spmv(const GpuCsr &m, SpmvMode mode, const SpmvEpi &epi, int64_t seg) {
+    const int64_t r0 = seg < 0 ? 0 : m.seg_rows[seg], r1 = seg < 0 ? m.nrows : m.seg_rows[seg + 1];
+    const int64_t r = r1 - r0;
+    if (r <= 0 || m.nrows <= 0) return;
+    const double frac = (double)r / (double)m.nrows;
+    auto part = [&](int64_t whole) { return seg < 0 ? whole : (int64_t)std::llround((double)whole * frac); };
+    int kernel = m.kernel;
+    const char *name = "csr-stream";
+    int64_t mat = 0;
+    const int64_t csr_mat = part(m.index_bytes());
+    const int64_t dia_bytes = 4 * (int64_t)m.dia_cw * r + 8 * m.dia_ntab;
+    if (m.kernel == SPMV_KERNEL_BSR) {
+        name = "bsr3";
+        mat = part(m.stream_bytes());
+    } else if (m.kernel == SPMV_KERNEL_SCS || (m.has_scs() && seg >= 0 && seg == m.scs_seg && mode != SPMV_SGS)) {
+        kernel = SPMV_KERNEL_SCS;
+        name = m.scs_lanes ? "scs_lanes" : "scs";
+        mat = m.scs_ib * r + 8 * m.scs_k * m.scs_nclass + 4 * m.scs_k;
+    } else if (m.kernel == SPMV_KERNEL_XS && seg < 0 && xs_supports(mode)) {
+        name = "xsell";
+        mat = m.stream_bytes();
+    } else if (m.kernel == SPMV_KERNEL_SELLP) {
+        name = "sellp";
+        mat = part(m.stream_bytes());
+    } else if (mode == SPMV_SGS && m.has_dia() && m.dia_rowid) {
+        kernel = SPMV_KERNEL_DIA;
+        name = "dia_sgs";
+        mat = dia_bytes;
+    } else if (m.kernel == SPMV_KERNEL_DIA || (m.has_dia() && !m.dia_rowid && seg >= 0 && seg == m.dia_seg)) {
+        kernel = SPMV_KERNEL_DIA;
+        name = (m.dia_pat || (m.dia_k == 27 && dia_runs() && dia_pat27())) ? "dia_pat" : "dia";
+        mat = dia_bytes;
+    } else if (m.kernel == SPMV_KERNEL_SELL) {
+        name = (m.sell_short && seg < 0 && mode != SPMV_SGS && mode != SPMV_RESID0 && sell_short_enabled())
+                   ? "sell_short" : "sell";
+        mat = part(m.stream_bytes());
+    } else if (m.kernel == SPMV_KERNEL_VECTOR) {
+        name = "vector";
+        mat = part(m.stream_bytes());
+    } else {
+        kernel = SPMV_KERNEL_STREAM;
+        mat = csr_mat;
+    }
+    const int64_t xcols = part(m.ncols);
+    const int64_t db = (epi.dc ? 1 : 8);  // bytes per diagonal entry (8-bit codes or fp64)
+    int64_t vec = 8 * xcols;              // x read once
+    switch (mode) {
+    case SPMV_SET: vec += 8 * r; break;                  // y written
+    case SPMV_ADD: vec += 16 * r; break;                 // y read + written
+    case SPMV_RESID: vec += 16 * r; break;               // b read, y written
+    case SPMV_JACOBI: vec += 16 * r + db * r; break;     // b, d read, y written
+    case SPMV_SGS: vec += 28 * r; break;                 // perm, d, b read, x written
+    case SPMV_RESID0:  // x = b; d gathered beside x (1-B codes only in the DIA kernel); y written
+        vec += 8 * r + ((kernel == SPMV_KERNEL_DIA && epi.dc && dia_rc_enabled()) ? 1 : 8) * xcols;
+        break;
+    case SPMV_ADD0: vec += 16 * r + db * r; break;       // b, d read, y written
+    }
+    log_launch(name, kernel, mode, r, mat + vec, csr_mat + vec);
+}
+
 void spmv(const GpuCsr &m, const double *x, double *y, SpmvMode mode, const SpmvEpi &epi,
           hipStream_t s, int64_t seg) {
     FAMG_REQUIRE(m.spmv_ready(), AMG_ERR_UNSUPPORTED, "SpMV needs nnz < 2^31 (32-bit row pointers)");
     FAMG_REQUIRE(seg < (int64_t)m.seg_rows.size() - 1, AMG_ERR_INVALID, "SpMV segment out of range");
     FAMG_REQUIRE(mode != SPMV_SGS || epi.perm, AMG_ERR_INVALID, "SGS mode needs a permutation");
+    if (g_launch_log) log_spmv(m, mode, epi, seg);
     Epi e{x, y, epi.b, epi.d, epi.perm, epi.dc, epi.dt};
     const dim3 block(256);
     if (m.kernel == SPMV_KERNEL_BSR) {

@@ -142,12 +142,24 @@ SIGNATURES = {
     "amg_nn_postprocess": (i32, [vp, i64, vp, i64, i64]),
     "amg_gen_elasticity_q1": (i32, [i64, i64, i64, dbl, dbl, C.c_uint64, i32, P(vp)]),
     "amg_dist_pcg_solve": (i32, [vp, i32, vp, vp, i64, dbl, dbl, vp, P(i64)]),
+    "amg_multigrid_cycle_plan": (i32, [vp, vp, i64, P(i64)]),
+    "amg_trace_mark": (i32, [vp, i32]),
 }
 
 for _name, (_res, _args) in SIGNATURES.items():
     _f = getattr(_lib, _name)
     _f.restype = _res
     _f.argtypes = _args
+
+
+class LaunchRec(C.Structure):
+    """amg_launch_rec (include/amg.h)."""
+    _fields_ = [("level", i32), ("role", i32), ("kernel", i32), ("mode", i32), ("rows", i64),
+                ("bytes", i64), ("csr_bytes", i64), ("name", C.c_char * 32)]
+
+
+ROLES = {0: "smooth", 1: "resid", 2: "restrict", 3: "interp", 4: "coarse", 5: "other"}
+MODES = {-1: "-", 0: "SET", 1: "ADD", 2: "RESID", 3: "JACOBI", 4: "SGS", 5: "RESID0", 6: "ADD0"}
 
 
 class AmgError(RuntimeError):
@@ -239,6 +251,10 @@ class Context:
 
     def synchronize(self):
         _ck(_lib.amg_ctx_synchronize(self.h))
+
+    def trace_mark(self, tag):
+        """Launch k_trace_mark with `tag` blocks (brackets a region of a kernel trace)."""
+        _ck(_lib.amg_trace_mark(self.h, tag))
 
     @property
     def stream(self):
@@ -534,6 +550,17 @@ class Multigrid(LinOp):
         v = i64()
         _ck(_lib.amg_multigrid_levels(self.h, C.byref(v)))
         return v.value
+
+    def cycle_plan(self):
+        """The launches of one V-cycle in order (amg_multigrid_cycle_plan): list of
+        dicts {level, role, kernel, mode, name, rows, bytes, csr_bytes}."""
+        n = i64()
+        _ck(_lib.amg_multigrid_cycle_plan(self.h, None, 0, C.byref(n)))
+        recs = (LaunchRec * max(1, n.value))()
+        _ck(_lib.amg_multigrid_cycle_plan(self.h, recs, n.value, C.byref(n)))
+        return [{"level": r.level, "role": ROLES.get(r.role, "?"), "kernel": r.kernel,
+                 "mode": MODES.get(r.mode, "?"), "name": r.name.decode(), "rows": r.rows,
+                 "bytes": r.bytes, "csr_bytes": r.csr_bytes} for r in recs[:n.value]]
 
     def level(self, l):
         """(A, S, R, P) handles of level l (R, P None on the coarsest)."""

@@ -80,10 +80,17 @@ amg_status amg_ctx_stream(amg_ctx *ctx, void **hip_stream);
  * the context stream.  Event-based, no host synchronisation. */
 amg_status amg_ctx_join_stream(amg_ctx *ctx, void *other, int32_t ctx_waits);
 /* SpMV storage policy for matrices built after the call (process-wide):
- * 0 auto (SELL-64 for short regular rows, wave-per-row for rows averaging >= 48
- * entries, CSR-stream otherwise), 1 CSR-stream only, 2 SELL-64 whenever rows are
- * <= 256 long, 3 wave-per-row for every matrix.  Results agree to the summation
- * order of the rows (bitwise for rows summed by one lane). */
+ * 0 auto -- per matrix the cheapest of: DIA codes (square, <= 32 diagonals or a
+ * known run pattern, >= 80 % filled, <= 256 distinct values), 3x3 block storage
+ * (block operators), stencil classes (structured Galerkin operators, >= 64
+ * offsets), pattern SELL (structured operators incl. rectangular R/P), x-staged
+ * SELL (gather-heavy fp64 SELL whose x footprint per 4096 rows fits LDS),
+ * SELL-64 with compressed columns and value codes (short regular rows),
+ * wave-per-row (rows averaging >= 256 entries), CSR-stream otherwise
+ * (DESIGN.md 2); 1 CSR-stream only, 2 SELL-64 whenever rows are <= 256 long,
+ * 3 wave-per-row for every matrix.  Results agree to the summation order of the
+ * rows (bitwise for rows summed by one lane, which every storage but the
+ * long-row CSR-stream / wave-per-row paths does). */
 amg_status amg_set_spmv_format(int32_t policy);
 /* Value storage of SELL-64 matrices built after the call (process-wide):
  * 1 (default) stores a 4 / 8 / 16-bit code per entry into a per-matrix table of
@@ -229,12 +236,44 @@ amg_status amg_multigrid_set_graph(amg_linop *mg, int32_t enable);
  * residual form of smooth() (multigrid.rs:418-423: r = f - A x; x += SGS(r))
  * instead of the fused in-place sweep on x (default 0: fused, one SpMV fewer);
  * 2 = fold the first Jacobi step from v = 0 (v = d f, s = 1) into the residual
- * and correction SpMVs instead of storing it, on levels whose operator is SELL
- * storage with fp64 values (default 1; bitwise identical). */
+ * and correction SpMVs instead of storing it (default 1; bitwise identical), on
+ * levels whose operator is fp64 SELL with mostly short columns, x-staged SELL,
+ * or DIA codes whose P runs the short-slice kernel; amg_multigrid_cycle_plan
+ * reports which levels fold (RESID0 / ADD0 launches). */
 amg_status amg_multigrid_set_option(amg_linop *mg, int32_t option, int64_t value);
 /* Multigrid::apply == amg_linop_apply on a multigrid handle. */
 amg_status amg_multigrid_apply(amg_linop *mg, double *out, int64_t ld_out, const double *rhs,
                                int64_t ld_rhs, int64_t k, amg_mem mem);
+
+/* Launch plan of one V-cycle: the kernels the library launches for one
+ * amg_multigrid_apply, in launch order, each with the algorithmic bytes of
+ * that launch (the bytes its storage streams + the vectors it reads and
+ * writes) and the same launch priced with 32-bit CSR matrix bytes
+ * (SURVEY.md 8(d)).  Recorded by running one eager (non-graph) cycle on
+ * scratch vectors with the recorder on, so fold decisions, SGS colour launches
+ * and storage choices are the ones the cycle makes.  recs may be NULL (count
+ * only); at most cap records are written, *count = records of the cycle. */
+typedef enum amg_role {
+    AMG_ROLE_SMOOTH = 0,   /* pre/post smoothing (smooth, multigrid.rs:407-424) */
+    AMG_ROLE_RESID = 1,    /* r = f - A v (:341-342), incl. a folded zero-guess step */
+    AMG_ROLE_RESTRICT = 2, /* f_c = R r (:343) */
+    AMG_ROLE_INTERP = 3,   /* v += P v_c (:349-350), incl. a folded d*f */
+    AMG_ROLE_COARSE = 4,   /* coarsest solve (:291) */
+    AMG_ROLE_OTHER = 5
+} amg_role;
+typedef struct amg_launch_rec {
+    int32_t level, role, kernel, mode; /* kernel as amg_csr_spmv_info (-1: vector op); mode: SET 0,
+                                          ADD 1, RESID 2, JACOBI 3, SGS 4, RESID0 5, ADD0 6 (-1) */
+    int64_t rows;                      /* rows this launch updates */
+    int64_t bytes;                     /* algorithmic bytes */
+    int64_t csr_bytes;                 /* with 12 nnz + 4 (m+1) matrix bytes (= bytes for vector ops) */
+    char name[32];                     /* storage kernel ("dia", "sell_short", "dia_sgs", "vec_mul" ...) */
+} amg_launch_rec;
+amg_status amg_multigrid_cycle_plan(amg_linop *mg, amg_launch_rec *recs, int64_t cap, int64_t *count);
+/* Launch the marker kernel k_trace_mark(tag) on the context stream: brackets a
+ * region of a rocprofv3 kernel trace (bench.py marks its timed V-cycles, and
+ * scripts/prof_summary.py keeps the dispatches between the marks). */
+amg_status amg_trace_mark(amg_ctx *ctx, int32_t tag);
 
 /* ---- Galerkin setup kernels (interpolation/mod.rs:716-720, 824-828, 927-946) - */
 

@@ -29,6 +29,22 @@ for s in "$@"; do
         profelast) export TMPDIR=/tmp; R=$(pwd)
               step profelast 600 rocprofv3 --kernel-trace --stats -d "$R/gpurun_out/profelast" -o run \
                   --output-format csv -- python3 "$R/bench.py" --problem elast --steps 20 --warmup 3 --no-cpu-baseline ;;
+        plantest) step plantest 300 python -u -m pytest tests/test_gpu_parity.py -m gpu -v --timeout 120 \
+                  --timeout-method thread -k "cycle_plan" ;;
+        launch1) step launch1 600 python bench.py --gpus 1 --dist --steps 20 --warmup 3 ;;
+        launch1c4) step launch1c4 600 python bench.py --gpus 1 --dist --workload c4 --steps 5 --warmup 1 ;;
+        profp) export TMPDIR=/tmp; R=$(pwd)
+              step profp 600 rocprofv3 --kernel-trace --stats -d "$R/gpurun_out/profp" -o run \
+                  --output-format csv -- python3 "$R/bench.py" --steps 20 --warmup 3 --no-cpu-baseline --no-general \
+                  --plan-out "$R/gpurun_out/plan_c2.json" ;;
+        profp27) export TMPDIR=/tmp; R=$(pwd)
+              step profp27 600 rocprofv3 --kernel-trace --stats -d "$R/gpurun_out/profp27" -o run \
+                  --output-format csv -- python3 "$R/bench.py" --problem 27pt --steps 10 --warmup 2 --no-cpu-baseline \
+                  --no-general --plan-out "$R/gpurun_out/plan_c3.json" ;;
+        profpel) export TMPDIR=/tmp; R=$(pwd)
+              step profpel 600 rocprofv3 --kernel-trace --stats -d "$R/gpurun_out/profpel" -o run \
+                  --output-format csv -- python3 "$R/bench.py" --problem elast --steps 20 --warmup 3 --no-cpu-baseline \
+                  --plan-out "$R/gpurun_out/plan_c5.json" ;;
         smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
         bench) step bench 600 python bench.py --steps 20 --warmup 3 ;;
         benchq) step bench 400 python bench.py --steps 20 --warmup 3 --no-cpu-baseline --ab ;;

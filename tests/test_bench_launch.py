@@ -1,0 +1,45 @@
+"""bench.py --gpus N starts its own N rank processes (verdict r02 item 1).
+
+The driver runs `python bench.py --gpus N` (and, for N > 1, possibly under an
+outer torch.distributed.run).  Without WORLD_SIZE in the environment the
+script must launch the ranks itself, before touching a GPU, and forward
+exactly one JSON line from rank 0.  FAMG_BENCH_LAUNCH_CHECK=1 replaces each
+rank's GPU work with a gloo all-reduce so the launcher runs on this CPU-only
+machine."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def run_bench(args, env_extra, timeout=240):
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env.update(env_extra)
+    return subprocess.run([sys.executable, os.path.join(ROOT, "bench.py")] + args, env=env,
+                          capture_output=True, text=True, timeout=timeout, cwd=ROOT)
+
+
+@pytest.mark.parametrize("n", [2, 3])
+def test_launcher_spawns_n_ranks_and_forwards_one_line(n):
+    p = run_bench(["--gpus", str(n), "--steps", "2", "--warmup", "1"], {"FAMG_BENCH_LAUNCH_CHECK": "1"})
+    assert p.returncode == 0, p.stderr[-3000:]
+    lines = [l for l in p.stdout.splitlines() if l.strip()]
+    assert len(lines) == 1, p.stdout
+    d = json.loads(lines[0])
+    assert d["launch_check"] is True
+    assert d["n_gpus"] == n and d["ranks_counted"] == n
+    assert "torch.distributed.run" in p.stderr  # the launcher logged its child command
+
+
+def test_launcher_refuses_without_enough_gpus():
+    import torch
+    if torch.cuda.device_count() >= 64:
+        pytest.skip("machine has many GPUs")
+    p = run_bench(["--gpus", "64", "--steps", "1", "--warmup", "0"], {}, timeout=120)
+    assert p.returncode == 3, (p.returncode, p.stderr[-2000:])
+    assert p.stdout.strip() == ""
+    assert "GPU(s) visible" in p.stderr

@@ -1112,3 +1112,64 @@ def test_stencil_classes(ctx):
     zref = O.Multigrid(oracle_levels_from_gpu(mg, "jacobi")).apply(b)
     z = apply_dev(ctx, mg, b, A.nrows)
     assert np.linalg.norm(z - zref) <= 1e-11 * np.linalg.norm(zref)
+
+
+def test_cycle_plan_accounts_for_every_launch(ctx):
+    """amg_multigrid_cycle_plan: the launches of one V-cycle as the library makes
+    them.  On the 7-pt box hierarchy the fine level folds its zero-guess step
+    (RESID0 + ADD0, no separate d*f pass) when the fine operator is DIA and P_0
+    runs the short-slice kernel; with the fold off the level issues the d*f pass,
+    RESID and ADD instead.  The coarsest level is one GEMV of 8 n^2 + 16 n bytes.
+    The plan's launch count equals the dispatches of a replayed cycle (the bench
+    checks the same against the rocprofv3 trace)."""
+    dims = (64, 64, 64)
+    A = fa().SparseMatOp.laplace3d_7pt(ctx, *dims)
+    mg = fa().sa_build_box(A, dims, (2, 2, 2), coarsest_dim=100)
+    plan = mg.cycle_plan()
+    nl = mg.levels()
+    assert {p["level"] for p in plan} == set(range(nl))
+    coarse = [p for p in plan if p["role"] == "coarse"]
+    n_c = mg.level(nl - 1)[0].nrows
+    assert len(coarse) == 1 and coarse[0]["name"] == "gemv" and coarse[0]["bytes"] == 8 * n_c * n_c + 16 * n_c
+    for p in plan:
+        assert p["bytes"] > 0 and p["csr_bytes"] >= p["bytes"] or p["kernel"] in (-1, 4, 7)
+    f0 = [p for p in plan if p["level"] == 0]
+    modes0 = [p["mode"] for p in f0]
+    info = A.spmv_info()
+    n = A.nrows
+    if "RESID0" in modes0:
+        # folded: RESID0 (f - A d f), R, ADD0 (d f + P v_c), post-smoothing Jacobi
+        assert modes0 == ["RESID0", "SET", "ADD0", "JACOBI"], f0
+        if info["kernel"] == "dia":  # 17 n: f read, 1-B codes of d gathered, r written
+            assert f0[0]["bytes"] == info["stream_bytes"] + 17 * n, f0[0]
+    else:
+        # d*f pass, residual, restriction, interpolate-add, post-smoothing Jacobi
+        assert modes0 == ["-", "RESID", "SET", "ADD", "JACOBI"], f0
+        assert f0[1]["bytes"] == info["stream_bytes"] + 24 * n, f0[1]
+    mg.set_fold_zero_guess(False)
+    plan2 = mg.cycle_plan()
+    modes_nf = [p["mode"] for p in plan2 if p["level"] == 0]
+    assert "RESID0" not in modes_nf and "ADD0" not in modes_nf
+    assert modes_nf[0] == "-" and modes_nf[1] == "RESID"  # d*f pass, then the residual
+    # results are unchanged by recording
+    import torch
+    b = T(np.random.default_rng(0).uniform(-1, 1, A.nrows))
+    z1, z2 = torch.empty_like(b), torch.empty_like(b)
+    mg.apply(z1, b)
+    mg.cycle_plan()
+    mg.apply(z2, b)
+    ctx.synchronize()
+    assert torch.equal(z1, z2)
+
+
+def test_cycle_plan_sgs_counts_colour_launches(ctx):
+    """SGS levels: 1 + (C - 1) + (C - 1) launches for the pre-smoothing from zero
+    (first colour pass, forward, backward) and 2 C - 1 for the fused post sweep."""
+    dims = (32, 32, 32)
+    A = fa().SparseMatOp.aniso27(ctx, *dims, 1.0, 1.0, 0.01)
+    mg = fa().sa_build_box(A, dims, (2, 2, 2), coarsest_dim=100, smoother="sgs")
+    plan = mg.cycle_plan()
+    S0 = mg.level(0)[1]
+    C = fa().sgs_info(S0)["colors"]
+    sweeps = [p for p in plan if p["level"] == 0 and p["mode"] == "SGS"]
+    assert len(sweeps) == (C - 1) + (C - 1) + (2 * C - 1), (len(sweeps), C)
