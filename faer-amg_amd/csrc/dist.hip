@@ -31,6 +31,7 @@
 #include <string>
 
 #include "handles.hpp"
+#include "plan.hpp"
 #include "solve.hpp"
 
 using namespace famg;
@@ -313,22 +314,20 @@ static unsigned g1(int64_t n) { return (unsigned)std::max<int64_t>(1, ceil_div(n
 
 // -------------------------------------------------------- vector spaces
 
+// A level's vector space on this rank: the host plan (plan.hpp: ghost set,
+// requests, send lists, neighbours) plus its device buffers.
 struct Space {
     bool redundant = false;
+    HaloPlan plan;
     int64_t n_glob = 0, r0 = 0, r1 = 0, n_own = 0, n_ghost = 0;
-    std::vector<int64_t> splits;          // nranks+1
     DevBuf<int64_t> mark, scan;           // setup only (global length)
-    std::vector<int64_t> ghost_ids;
-    // halo plan
+    // halo plan (copied from `plan`)
     std::vector<int> nbr;
     std::vector<int64_t> soff, scnt, roff, rcnt;
     DevBuf<int32_t> send_idx;
     DevBuf<double> sendbuf;
     std::vector<Peer> peers;              // rebuilt per vector (rbuf differs)
     int64_t nsend = 0;
-    int owner(int64_t g) const {
-        return int(std::upper_bound(splits.begin(), splits.end(), g) - splits.begin()) - 1;
-    }
 };
 
 // Local copy of rows [r0, r1) of M with global column ids.
@@ -355,27 +354,26 @@ static void space_mark(Space &sp, const GpuCsr &local, Ctx *ctx) {
     FAMG_CHECK_HIP(hipGetLastError());
 }
 
-// After all matrices of the space are marked: ghost list, halo plan (request
-// exchange through the transport), scan kept for the column remap.
+// After all matrices of the space are marked: the ghost list (device compaction
+// of the marks, the same set plan_add_columns computes on the host), then the
+// host plan (plan.hpp) with its two request exchanges over the transport.
 static void space_plan(Space &sp, Transport &tr, Ctx *ctx) {
     hipStream_t s = ctx->stream;
     sp.scan.resize(sp.n_glob + 1);
-    sp.n_ghost = scan_counts(sp.mark.get(), sp.scan.get(), sp.n_glob, *ctx);
-    DevBuf<int64_t> ids(sp.n_ghost);
+    const int64_t ng = scan_counts(sp.mark.get(), sp.scan.get(), sp.n_glob, *ctx);
+    DevBuf<int64_t> ids(ng);
     hipLaunchKernelGGL(k_compact_ghost, dim3(g1(sp.n_glob)), dim3(256), 0, s, sp.mark.get(), sp.scan.get(),
                        sp.n_glob, ids.get());
-    sp.ghost_ids.resize(sp.n_ghost);
-    if (sp.n_ghost)
-        FAMG_CHECK_HIP(hipMemcpyAsync(sp.ghost_ids.data(), ids.get(), sp.n_ghost * sizeof(int64_t), hipMemcpyDeviceToHost, s));
+    std::vector<int64_t> ghost_ids(ng);
+    if (ng) FAMG_CHECK_HIP(hipMemcpyAsync(ghost_ids.data(), ids.get(), ng * sizeof(int64_t), hipMemcpyDeviceToHost, s));
     FAMG_CHECK_HIP(hipStreamSynchronize(s));
+    HaloPlan &pl = sp.plan;
+    plan_set_ghosts(pl, std::move(ghost_ids));
+    sp.n_ghost = pl.n_ghost();
     const int P = tr.nranks;
-    // requests per owner
-    std::vector<int64_t> req_cnt(P, 0), req_off(P + 1, 0);
-    for (int64_t g : sp.ghost_ids) req_cnt[sp.owner(g)]++;
-    for (int q = 0; q < P; q++) req_off[q + 1] = req_off[q] + req_cnt[q];
-    // all-to-all counts
+    // all-to-all request counts
     DevBuf<int64_t> dsend(P), drecv(P);
-    FAMG_CHECK_HIP(hipMemcpyAsync(dsend.get(), req_cnt.data(), P * sizeof(int64_t), hipMemcpyHostToDevice, s));
+    FAMG_CHECK_HIP(hipMemcpyAsync(dsend.get(), pl.req_cnt.data(), P * sizeof(int64_t), hipMemcpyHostToDevice, s));
     FAMG_CHECK_HIP(hipMemsetAsync(drecv.get(), 0, P * sizeof(int64_t), s));
     std::vector<Peer> cp;
     for (int q = 0; q < P; q++)
@@ -390,36 +388,30 @@ static void space_plan(Space &sp, Transport &tr, Ctx *ctx) {
     // exchange the requested ids
     DevBuf<int64_t> req_ids(std::max<int64_t>(1, sp.n_ghost)), in_ids(std::max<int64_t>(1, got_off[P]));
     if (sp.n_ghost)
-        FAMG_CHECK_HIP(hipMemcpyAsync(req_ids.get(), sp.ghost_ids.data(), sp.n_ghost * sizeof(int64_t), hipMemcpyHostToDevice, s));
+        FAMG_CHECK_HIP(hipMemcpyAsync(req_ids.get(), pl.ghost_ids.data(), sp.n_ghost * sizeof(int64_t),
+                                      hipMemcpyHostToDevice, s));
     std::vector<Peer> ip;
     for (int q = 0; q < P; q++) {
-        if (q == tr.rank || (req_cnt[q] == 0 && got[q] == 0)) continue;
-        ip.push_back({q, req_ids.get() + req_off[q], req_cnt[q] * 8, in_ids.get() + got_off[q], got[q] * 8});
+        if (q == tr.rank || (pl.req_cnt[q] == 0 && got[q] == 0)) continue;
+        ip.push_back({q, req_ids.get() + pl.req_off[q], pl.req_cnt[q] * 8, in_ids.get() + got_off[q], got[q] * 8});
     }
     tr.exchange(ip, s);
     std::vector<int64_t> inh(got_off[P]);
     if (got_off[P])
         FAMG_CHECK_HIP(hipMemcpyAsync(inh.data(), in_ids.get(), got_off[P] * sizeof(int64_t), hipMemcpyDeviceToHost, s));
     FAMG_CHECK_HIP(hipStreamSynchronize(s));
-    std::vector<int32_t> sidx(got_off[P]);
-    for (int64_t k = 0; k < got_off[P]; k++) {
-        FAMG_REQUIRE(inh[k] >= sp.r0 && inh[k] < sp.r1, AMG_ERR_INVALID, "halo request for a row not owned");
-        sidx[k] = (int32_t)(inh[k] - sp.r0);
-    }
-    sp.nsend = got_off[P];
+    plan_set_incoming(pl, got.data(), inh.data());
+    sp.nsend = (int64_t)pl.send_idx.size();
     sp.send_idx.resize(std::max<int64_t>(1, sp.nsend));
     sp.sendbuf.resize(std::max<int64_t>(1, sp.nsend));
     if (sp.nsend)
-        FAMG_CHECK_HIP(hipMemcpyAsync(sp.send_idx.get(), sidx.data(), sp.nsend * sizeof(int32_t), hipMemcpyHostToDevice, s));
-    sp.nbr.clear(); sp.soff.clear(); sp.scnt.clear(); sp.roff.clear(); sp.rcnt.clear();
-    for (int q = 0; q < P; q++) {
-        if (q == tr.rank || (req_cnt[q] == 0 && got[q] == 0)) continue;
-        sp.nbr.push_back(q);
-        sp.soff.push_back(got_off[q]);
-        sp.scnt.push_back(got[q]);
-        sp.roff.push_back(req_off[q]);
-        sp.rcnt.push_back(req_cnt[q]);
-    }
+        FAMG_CHECK_HIP(hipMemcpyAsync(sp.send_idx.get(), pl.send_idx.data(), sp.nsend * sizeof(int32_t),
+                                      hipMemcpyHostToDevice, s));
+    sp.nbr = pl.nbr;
+    sp.soff = pl.soff;
+    sp.scnt = pl.scnt;
+    sp.roff = pl.roff;
+    sp.rcnt = pl.rcnt;
     FAMG_CHECK_HIP(hipStreamSynchronize(s));
 }
 
@@ -456,14 +448,7 @@ static void space_remap(const Space &sp, GpuCsr &local, Ctx *ctx) {
     FAMG_CHECK_HIP(hipMemcpyAsync(flag.data(), dflag.get(), n, hipMemcpyDeviceToHost, s));
     FAMG_CHECK_HIP(hipStreamSynchronize(s));
     int64_t lo = 0, hi = 0;
-    for (int64_t i = 0; i < n;) {
-        if (flag[i]) { i++; continue; }
-        int64_t j = i;
-        while (j < n && !flag[j]) j++;
-        if (j - i > hi - lo) { lo = i; hi = j; }
-        i = j;
-    }
-    if (hi == lo) lo = hi = n;
+    interior_segment(flag.data(), n, lo, hi);
     const std::vector<int64_t> segs{0, lo, hi, n};
     csr_finalize(local, &segs);
 }
@@ -702,9 +687,11 @@ static std::shared_ptr<DistMultigridOp> build_dist(amg_comm *comm, const Multigr
     d->mu = g.mu;
     d->steps = g.steps;
     d->nlevels = (int64_t)g.levels.size();
-    d->La = d->nlevels - 1;  // the coarsest level is always redundant
-    for (int64_t l = 0; l < d->nlevels - 1; l++)
-        if (g.levels[l].A->nrows < agglo) { d->La = l; break; }
+    {
+        std::vector<int64_t> rows(d->nlevels);
+        for (int64_t l = 0; l < d->nlevels; l++) rows[l] = g.levels[l].A->nrows;
+        d->La = first_redundant_level(rows.data(), d->nlevels, agglo);
+    }
     auto sp_of = [&](int64_t l) {
         std::vector<int64_t> s(splits + l * (P + 1), splits + (l + 1) * (P + 1));
         FAMG_REQUIRE(s[0] == 0 && s[P] == g.levels[l].A->nrows, AMG_ERR_DIM, "level splits must cover the level");
@@ -720,11 +707,12 @@ static std::shared_ptr<DistMultigridOp> build_dist(amg_comm *comm, const Multigr
         auto *S = dynamic_cast<DiagOp *>(g.levels[l].S.get());
         FAMG_REQUIRE(A && R && Pm, AMG_ERR_UNSUPPORTED, "distributed levels need CSR operators");
         FAMG_REQUIRE(S, AMG_ERR_UNSUPPORTED, "distributed levels need a diagonal (Jacobi/L1/L2) smoother");
-        D.sp.splits = sp_of(l);
+        const std::vector<int64_t> spl = sp_of(l);
+        plan_init(D.sp.plan, P, me, spl.data());
         D.sp.n_glob = A->nrows;
-        D.sp.r0 = D.sp.splits[me];
-        D.sp.r1 = D.sp.splits[me + 1];
-        D.sp.n_own = D.sp.r1 - D.sp.r0;
+        D.sp.r0 = D.sp.plan.r0;
+        D.sp.r1 = D.sp.plan.r1;
+        D.sp.n_own = D.sp.plan.n_own;
     }
     // local matrices with global columns
     for (int64_t l = 0; l < d->La; l++) {

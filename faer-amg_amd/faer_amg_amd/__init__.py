@@ -143,6 +143,17 @@ SIGNATURES = {
     "amg_gen_elasticity_q1": (i32, [i64, i64, i64, dbl, dbl, C.c_uint64, i32, P(vp)]),
     "amg_dist_pcg_solve": (i32, [vp, i32, vp, vp, i64, dbl, dbl, vp, P(i64)]),
     "amg_multigrid_cycle_plan": (i32, [vp, vp, i64, P(i64)]),
+    "amg_halo_plan_create": (i32, [i32, i32, vp, P(vp)]),
+    "amg_halo_plan_destroy": (i32, [vp]),
+    "amg_halo_plan_add_columns": (i32, [vp, i64, vp]),
+    "amg_halo_plan_requests": (i32, [vp, vp, P(i64)]),
+    "amg_halo_plan_ghost_ids": (i32, [vp, vp]),
+    "amg_halo_plan_set_incoming": (i32, [vp, vp, vp]),
+    "amg_halo_plan_info": (i32, [vp, vp]),
+    "amg_halo_plan_neighbors": (i32, [vp, vp, vp, vp, vp, vp]),
+    "amg_halo_plan_send_indices": (i32, [vp, vp]),
+    "amg_halo_plan_remap": (i32, [vp, i64, vp, vp, vp, P(i64), P(i64)]),
+    "amg_dist_first_redundant_level": (i32, [i64, vp, i64, P(i64)]),
     "amg_trace_mark": (i32, [vp, i32]),
 }
 
@@ -929,6 +940,90 @@ class DistMultigrid(LinOp):
                                                max_iter, rel_tol, hist.ctypes.data_as(vp),
                                                C.byref(it)))
         return it.value, hist[:it.value]
+
+
+def _i64(a):
+    return np.ascontiguousarray(a, np.int64)
+
+
+class HaloPlan:
+    """Host-side halo plan of one level on one rank (amg_halo_plan_*; no device):
+    the library's own planner, driven step by step so any process layout (a gloo
+    test, a custom launcher) can exchange the requests itself."""
+
+    def __init__(self, nranks, rank, splits):
+        sp_ = _i64(splits)
+        if len(sp_) != nranks + 1:
+            raise ValueError("splits must have nranks + 1 entries")
+        h = vp()
+        _ck(_lib.amg_halo_plan_create(nranks, rank, sp_.ctypes.data_as(vp), C.byref(h)))
+        self.h, self.nranks, self.rank = h, nranks, rank
+
+    def __del__(self, _destroy=_lib.amg_halo_plan_destroy):
+        if getattr(self, "h", None):
+            _destroy(self.h)
+            self.h = None
+
+    def add_columns(self, cols):
+        c = _i64(cols)
+        _ck(_lib.amg_halo_plan_add_columns(self.h, len(c), c.ctypes.data_as(vp)))
+
+    def requests(self):
+        """(ghost ids sorted, ids to request from each rank as a list of arrays)."""
+        cnt = np.zeros(self.nranks, np.int64)
+        ng = i64()
+        _ck(_lib.amg_halo_plan_requests(self.h, cnt.ctypes.data_as(vp), C.byref(ng)))
+        ids = np.zeros(max(1, ng.value), np.int64)
+        _ck(_lib.amg_halo_plan_ghost_ids(self.h, ids.ctypes.data_as(vp)))
+        ids = ids[:ng.value]
+        off = np.concatenate([[0], np.cumsum(cnt)])
+        return ids, [ids[off[q]:off[q + 1]] for q in range(self.nranks)]
+
+    def set_incoming(self, per_rank_ids):
+        cnt = _i64([len(x) for x in per_rank_ids])
+        ids = _i64(np.concatenate([np.asarray(x, np.int64) for x in per_rank_ids] + [np.zeros(0, np.int64)]))
+        _ck(_lib.amg_halo_plan_set_incoming(self.h, cnt.ctypes.data_as(vp),
+                                            ids.ctypes.data_as(vp) if len(ids) else None))
+
+    def info(self):
+        v = np.zeros(6, np.int64)
+        _ck(_lib.amg_halo_plan_info(self.h, v.ctypes.data_as(vp)))
+        return dict(zip(("n_own", "n_ghost", "neighbors", "nsend", "nrecv", "r0"), (int(x) for x in v)))
+
+    def neighbors(self):
+        k = self.info()["neighbors"]
+        nbr = np.zeros(max(1, k), np.int32)
+        arrs = [np.zeros(max(1, k), np.int64) for _ in range(4)]
+        _ck(_lib.amg_halo_plan_neighbors(self.h, nbr.ctypes.data_as(vp), *[a.ctypes.data_as(vp) for a in arrs]))
+        return {"nbr": nbr[:k], "soff": arrs[0][:k], "scnt": arrs[1][:k], "roff": arrs[2][:k], "rcnt": arrs[3][:k]}
+
+    def send_indices(self):
+        n = self.info()["nsend"]
+        idx = np.zeros(max(1, n), np.int32)
+        _ck(_lib.amg_halo_plan_send_indices(self.h, idx.ctypes.data_as(vp)))
+        return idx[:n]
+
+    def remap(self, M):
+        """scipy CSR with global columns -> (CSR with [owned | ghost] columns, lo, hi)."""
+        import scipy.sparse as sps
+        M = M.tocsr()
+        rp, ci = _i64(M.indptr), _i64(M.indices)
+        out = np.zeros(max(1, len(ci)), np.int32)
+        lo, hi = i64(), i64()
+        _ck(_lib.amg_halo_plan_remap(self.h, M.shape[0], rp.ctypes.data_as(vp), ci.ctypes.data_as(vp),
+                                     out.ctypes.data_as(vp), C.byref(lo), C.byref(hi)))
+        inf = self.info()
+        L = sps.csr_matrix((M.data.copy(), out[:len(ci)].astype(np.int64), rp.copy()),
+                           shape=(M.shape[0], inf["n_own"] + inf["n_ghost"]))
+        return L, lo.value, hi.value
+
+
+def first_redundant_level(level_rows, agglomerate_rows):
+    """The first level the distributed multigrid gathers and cycles redundantly."""
+    r = _i64(level_rows)
+    v = i64()
+    _ck(_lib.amg_dist_first_redundant_level(len(r), r.ctypes.data_as(vp), agglomerate_rows, C.byref(v)))
+    return v.value
 
 
 def slab_splits(level_dims, nranks):

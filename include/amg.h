@@ -458,6 +458,41 @@ amg_status amg_dist_pcg_solve(amg_linop *dist_mg, int32_t precondition, const do
                               int64_t max_iter, double rel_tol, double abs_tol, double *hist,
                               int64_t *iters);
 
+/* ---- host-side distributed planning (no device; faer-amg_amd/csrc/plan.hpp) --
+ * The planner amg_dist_multigrid_create runs per level, exported so it can be
+ * driven (and tested) from any process layout: rank p owns rows
+ * [splits[p], splits[p+1]); add the global column ids of every local matrix
+ * that reads the level's vector (A_l, R_l rows and P_{l-1} rows owned here);
+ * amg_halo_plan_requests finalises the ghost set (sorted global ids, grouped by
+ * owner) and returns how many ids go to each rank; after the ranks have
+ * exchanged their request lists, amg_halo_plan_set_incoming builds the send
+ * lists (in_ids: the ids every rank requested from this one, concatenated in
+ * rank order) and the neighbour table.  amg_halo_plan_remap renumbers a local
+ * matrix's columns into [owned | ghost] and returns the interior row segment
+ * [lo, hi) (the longest run of rows reading owned entries only). */
+typedef struct amg_halo_plan amg_halo_plan;
+amg_status amg_halo_plan_create(int32_t nranks, int32_t rank, const int64_t *splits, amg_halo_plan **out);
+amg_status amg_halo_plan_destroy(amg_halo_plan *plan);
+amg_status amg_halo_plan_add_columns(amg_halo_plan *plan, int64_t nnz, const int64_t *cols);
+/* req_counts: nranks entries (may be NULL); *n_ghost: ghost entries. */
+amg_status amg_halo_plan_requests(amg_halo_plan *plan, int64_t *req_counts, int64_t *n_ghost);
+amg_status amg_halo_plan_ghost_ids(const amg_halo_plan *plan, int64_t *ids);
+amg_status amg_halo_plan_set_incoming(amg_halo_plan *plan, const int64_t *in_counts, const int64_t *in_ids);
+/* info6 = {n_own, n_ghost, neighbours, entries sent per refresh, entries received, first owned row} */
+amg_status amg_halo_plan_info(const amg_halo_plan *plan, int64_t *info6);
+/* Per neighbour (rank order): send offset/count into the send list, receive
+ * offset/count into the ghost region.  Arrays of `neighbours` entries (any may be NULL). */
+amg_status amg_halo_plan_neighbors(const amg_halo_plan *plan, int32_t *nbr, int64_t *soff, int64_t *scnt,
+                                   int64_t *roff, int64_t *rcnt);
+/* The owned local indices packed for the neighbours (entries sent per refresh). */
+amg_status amg_halo_plan_send_indices(const amg_halo_plan *plan, int32_t *idx);
+amg_status amg_halo_plan_remap(const amg_halo_plan *plan, int64_t nrows, const int64_t *rowptr, const int64_t *cols,
+                               int32_t *local_cols, int64_t *lo, int64_t *hi);
+/* The first level cycled redundantly (agglomerated): the first l < nlevels-1
+ * with level_rows[l] < agglomerate_rows, else the coarsest. */
+amg_status amg_dist_first_redundant_level(int64_t nlevels, const int64_t *level_rows, int64_t agglomerate_rows,
+                                          int64_t *level);
+
 /* ---- Dataset loaders (utils.rs:269-534) -------------------
  * Host-side; no device needed.  Matrix Market: sparse coordinate files
  * (real/integer/pattern, general/symmetric), 1-based indices, explicit 0.0
