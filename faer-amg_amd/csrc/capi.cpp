@@ -165,6 +165,22 @@ amg_status amg_set_value_codes(int32_t enable) {
     });
 }
 
+amg_status amg_set_sgs_fused(int32_t enable) {
+    return guard([&] {
+        FAMG_REQUIRE(enable == 0 || enable == 1, AMG_ERR_INVALID, "enable must be 0 or 1");
+        g_sgs_fused = enable;
+    });
+}
+
+amg_status amg_sgs_fused(const amg_linop *op, int32_t *fused) {
+    return guard([&] {
+        FAMG_REQUIRE(fused, AMG_ERR_INVALID, "null output");
+        auto p = std::dynamic_pointer_cast<SgsOp>(need(op).shared_from_this());
+        FAMG_REQUIRE(p, AMG_ERR_INVALID, "operator is not an SGS smoother");
+        *fused = p->fused27 ? 1 : 0;
+    });
+}
+
 amg_status amg_set_spmv_format(int32_t policy) {
     return guard([&] {
         FAMG_REQUIRE(policy >= 0 && policy <= 3, AMG_ERR_INVALID, "policy must be 0..3");

@@ -330,6 +330,13 @@ struct SgsOp : LinOp {
     std::vector<int32_t> host_colors;
     int64_t ncolors = 0;
     DevBuf<double> e_;     // scratch correction
+    // fused plane-parity sweeps on a 27-point grid operator (sgs27.hip)
+    bool fused27 = false;
+    int nx27 = 0, ny27 = 0, nz27 = 0;
+    std::vector<uint32_t> icode27;  // interior row's code group (8 words, unused = ~0)
+    std::vector<double> icoef27;    // and its 27 coefficients
+    std::vector<uint32_t> fmask27;  // 6 x 8 words: code bits of the entries leaving each grid face
+    DevBuf<double> fused_tmp, fused_zero;
     Kind kind() const override { return Kind::Sgs; }
     bool is_precond() const override { return true; }
     // e = SGS(r) from e = 0 (device pointers, e != r)
@@ -399,6 +406,13 @@ std::shared_ptr<DiagOp> make_jacobi(CsrOp &A, double omega);
 std::shared_ptr<DiagOp> make_l1(CsrOp &A);
 std::shared_ptr<DiagOp> make_l2(CsrOp &A);
 std::shared_ptr<SgsOp> make_sgs(const CsrPtr &A, const int32_t *colors, bool validate = true);
+// fused SGS phases for a 27-point grid operator stored as DIA codes (sgs27.hip)
+// SgsOps built afterwards use the fused phases where they apply (default 1,
+// FAMG_SGS_FUSED=0 sets 0; amg_set_sgs_fused)
+extern int g_sgs_fused;
+void sgs27_setup(SgsOp &S);
+bool sgs27_applies(const SgsOp &S, const double *x, const double *b);  // fused and 16-B aligned vectors
+void sgs27_sweep(SgsOp &S, double *x, const double *b, bool zero);
 std::shared_ptr<CoarseCholOp> make_coarse_chol(CsrOp &A);
 
 // SA setup pieces

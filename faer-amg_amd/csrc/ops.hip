@@ -246,6 +246,7 @@ std::shared_ptr<SgsOp> make_sgs(const CsrPtr &A, const int32_t *colors, bool val
     FAMG_REQUIRE(op->Ap.spmv_ready(), AMG_ERR_UNSUPPORTED, "sgs: nnz must be < 2^31");
     build_dia_sgs(op->Ap, op->perm.get());  // constant-stencil operators: DIA codes for the sweeps
     op->e_.resize(n);
+    sgs27_setup(*op);  // 27-point grid operators: fused plane-parity phases
     return op;
 }
 
@@ -254,6 +255,10 @@ void SgsOp::sweep(double *e, const double *r) {
     hipStream_t s = ctx->stream;
     const int64_t n = nrows;
     if (!n) return;
+    if (sgs27_applies(*this, e, r)) {
+        sgs27_sweep(*this, e, r, true);
+        return;
+    }
     vec_fill(e, 0.0, n, s);
     const int64_t p0 = color_ptr[0], p1 = color_ptr[1];
     if (p1 > p0) log_launch("sgs_first", -1, -1, p1 - p0, 28 * (p1 - p0));
@@ -274,6 +279,10 @@ void SgsOp::sweep(double *e, const double *r) {
 void SgsOp::sweep_x(double *x, const double *b) {
     hipStream_t s = ctx->stream;
     if (!nrows) return;
+    if (sgs27_applies(*this, x, b)) {
+        sgs27_sweep(*this, x, b, false);
+        return;
+    }
     SpmvEpi epi;
     epi.b = b;
     epi.d = dinv.get();

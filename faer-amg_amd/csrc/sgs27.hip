@@ -1,0 +1,446 @@
+// sgs27.hip -- multicolor SGS sweeps on a 3-D 27-point grid operator, fused
+// into plane-parity phases.
+//
+// The colour sweeps of SgsOp (ops.hip) update one colour per launch; each
+// launch updates 1/8 of the rows but gathers from the whole x, so an SGS step
+// (15 launches) streams x about 15 times.  On a structured nx x ny x nz grid
+// whose greedy colouring is the parity colouring c = (x&1) + 2 (y&1) + 4 (z&1)
+// (what greedy first-fit in row order gives for the 27-point stencil) the
+// sweep has plane structure:
+//   forward  colours 0..3 touch even planes only and read the odd planes'
+//            old values; colours 4..7 touch odd planes and read the even
+//            planes' new values;
+//   backward colours 6,5,4 (odd planes), then 3,2,1,0 (even planes).
+// So an SGS step is four phases (even fwd, odd fwd, odd bwd, even bwd); in a
+// phase every plane of one parity runs its 3-4 in-plane colours in order while
+// the other parity is read-only.  One workgroup owns TY rows of one plane: it
+// loads those rows plus nst rows of halo on each side into LDS, runs the
+// colours on shrinking halos (colour s is recomputed up to nst-1-s rows out,
+// so its neighbours are final when the next colour reads them), and writes its
+// TY rows to the phase's target buffer.  Each phase reads its planes from one
+// buffer and writes them to another (no workgroup reads what another writes
+// in the same launch); the other parity is read from where it currently lives.
+//
+// Arithmetic is the colour launches' exactly: row i of colour c sums
+// fma(a_ik, x_k, acc) over its 27 diagonals in ascending column order with
+// the latest values of lower colours and the old values of higher ones, then
+// x_i + (1/a_ii) (b_i - acc) -- bitwise equal to spmv_dia_sgs_kernel.  The
+// coefficients are the operator's own DIA codes (A's storage, original row
+// order); positions outside the grid carry the +0.0 code and read 0.0.
+#include <algorithm>
+#include <cstring>
+
+#include "famg.hpp"
+
+namespace famg {
+
+struct Sgs27Args {
+    const uint32_t *codes;  // A's DIA codes (original rows), CW words per row
+    const double *vtab;
+    int ntab;
+    int nx, ny, nz;
+    int pz;     // plane parity of this phase
+    int nst;    // in-plane colours applied, in order
+    int px[4], py[4];
+    const double *S;  // this parity's values before the phase
+    const double *O;  // the other parity's values (read-only in the phase)
+    double *T;        // this parity's values after the phase
+    const double *b;
+    int own_zero, other_zero;  // values known to be zero (sweep from e = 0): not read
+    int ntiles;
+    int ty;
+    uint32_t icode[8];     // code group of an interior row (all 27 entries present)
+    uint32_t fmask[6][8];  // code bits of the 9 entries leaving the grid at each face (x-,x+,y-,y+,z-,z+)
+    double icoef[27];      // the interior row's coefficients (table values of icode)
+    double idinv;          // 1 / icoef[13]
+    const double *zero;    // >= nx zeros (rows outside the grid)
+    int dbg;               // timing experiments (FAMG_SGS27_DEBUG): 0 = normal
+};
+
+
+typedef double sgs_dbl2_t __attribute__((ext_vector_type(2)));
+typedef uint32_t sgs_u32x4_t __attribute__((ext_vector_type(4)));
+
+// One colour stage of a workgroup.  Work is split into wave tasks: a task is
+// 64 consecutive points of the colour in one grid row y (x = PX + 2k, k =
+// 64 seg + lane), so y -- and with it every row address the 27-point stencil
+// needs (3 LDS rows of the own plane, 6 rows of the other parity's planes
+// z +- 1, or a zero row where the row leaves the grid) -- is wave-uniform and
+// lives in scalar registers; a lane only adds its x offset.  The three values
+// x-1, x, x+1 of a row come from two 16-B pair loads; the only lanes whose
+// window leaves the row are x = 0 (PX = 0, k = 0) and x = nx-1 (PX = 1,
+// k = nk-1), which clamp the pair address and select 0.0.  U tasks per trip
+// with all loads issued before the sums.  (Sharing one pair load per lane
+// through DPP wave shifts measured slower: each shift waits for its load.)
+//
+// A lane whose row carries the interior code group -- with the entries that
+// leave the grid at its faces cleared to the +0.0 code, i.e. a constant
+// stencil truncated at the boundary -- may use the interior coefficients from
+// the kernel arguments instead of decoding 27 codes through the LDS table;
+// when all lanes of the wave can, the wave does.  A replaced entry multiplies
+// an x operand of 0.0 on both paths; the product (+-0.0) added to an
+// accumulator that starts at +0.0 and can never become -0.0 leaves it
+// unchanged, so the sums are bitwise the same.
+template <int VB, int CW, int PX, int U>
+__device__ __forceinline__ void sgs27_stage(const Sgs27Args &a, double *lds, const double *stab, const double *scoef,
+                                            int z, int r0, int ys0, int ys1, int py, bool first_zero) {
+    constexpr uint32_t MASK = (1u << VB) - 1;
+    constexpr int MT = 4;  // tasks per chunk: their code groups and b prefetched together
+    const int nx = a.nx, ny = a.ny, nz = a.nz;
+    const int64_t plane = (int64_t)nx * ny;
+    const int yfirst = ys0 + ((ys0 & 1) != py ? 1 : 0);
+    const int nrow = yfirst < ys1 ? (ys1 - yfirst + 1) / 2 : 0;
+    const int nk = nx / 2;  // points of each x parity per row (nx even)
+    const int nseg = (nk + 63) >> 6;
+    const int ntask = nrow * nseg;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    const bool zlo = z == 0, zhi = z == nz - 1;
+    for (int c0 = wave; c0 < ntask; c0 += 4 * MT) {
+        // the chunk's code groups and right-hand sides: HBM streams, all in flight at once
+        uint32_t cwp[MT][CW];
+        double bp[MT];
+#pragma unroll
+        for (int i = 0; i < MT; i++) {
+            const int t = min(c0 + 4 * i, ntask - 1);  // wave-uniform
+            const int yr = t / nseg, sg = t - yr * nseg;
+            const int y = yfirst + 2 * yr;
+            const int x = PX + 2 * min((sg << 6) + lane, nk - 1);
+            const int64_t gi = (int64_t)z * plane + (int64_t)y * nx + x;
+            if (a.dbg == 3) {
+#pragma unroll
+                for (int q = 0; q < CW; q++) cwp[i][q] = a.icode[q];
+            } else {
+#pragma unroll
+                for (int q = 0; q < CW / 4; q++) {
+                    const sgs_u32x4_t c =
+                        __builtin_nontemporal_load(reinterpret_cast<const sgs_u32x4_t *>(a.codes + gi * CW) + q);
+#pragma unroll
+                    for (int e = 0; e < 4; e++) cwp[i][4 * q + e] = c[e];
+                }
+            }
+            bp[i] = __builtin_nontemporal_load(a.b + gi);
+        }
+#pragma unroll
+        for (int i = 0; i < MT; i++) {
+            const int t = c0 + 4 * i;
+            if (t >= ntask) break;  // wave-uniform
+            const int yr = t / nseg, sg = t - yr * nseg;
+            const int y = yfirst + 2 * yr;
+            const int k = (sg << 6) + lane;
+            const bool live = k < nk;
+            const int x = PX + 2 * min(k, nk - 1);
+            const bool lo = PX == 0 && x == 0, hi = PX == 1 && x == nx - 1;
+            // pair offsets: A = [x-2+PX, x-1+PX], B = A + 2 (clamped into the row at the edges)
+            const int offA = max(x - 2 + PX, 0), offB = min(x + PX, nx - 2);
+            const int64_t rowg = (int64_t)z * plane + (int64_t)y * nx;
+            double w[9][3];
+#pragma unroll
+            for (int j = 0; j < 9; j++) {
+                const int dz = j / 3 - 1, dy = j % 3 - 1;
+                const int yy = y + dy, zz = z + dz;
+                const bool rowok = yy >= 0 && yy < ny && zz >= 0 && zz < nz;  // wave-uniform
+                const double *row;
+                if (dz == 0) row = lds + (rowok && a.dbg != 4 ? (yy - r0 + 1) * nx : 0);  // LDS row 0: zeros
+                else if (a.other_zero || !rowok) row = a.zero;
+                else row = a.O + rowg + (int64_t)dz * plane + (int64_t)dy * nx;
+                const sgs_dbl2_t pa = *reinterpret_cast<const sgs_dbl2_t *>(row + offA);
+                const sgs_dbl2_t pb = *reinterpret_cast<const sgs_dbl2_t *>(row + offB);
+                if (PX == 0) {
+                    w[j][0] = lo ? 0.0 : pa.y;
+                    w[j][1] = pb.x;
+                    w[j][2] = pb.y;
+                } else {
+                    w[j][0] = pa.x;
+                    w[j][1] = pa.y;
+                    w[j][2] = hi ? 0.0 : pb.x;
+                }
+            }
+            // the interior group with the entries leaving the grid cleared
+            const bool ylo = y == 0, yhi = y == ny - 1;
+            bool inter = true;
+#pragma unroll
+            for (int q = 0; q < CW; q++) {
+                const uint32_t clr = (lo ? a.fmask[0][q] : 0u) | (hi ? a.fmask[1][q] : 0u) |
+                                     (ylo ? a.fmask[2][q] : 0u) | (yhi ? a.fmask[3][q] : 0u) |
+                                     (zlo ? a.fmask[4][q] : 0u) | (zhi ? a.fmask[5][q] : 0u);
+                inter = inter && cwp[i][q] == (a.icode[q] & ~clr);
+            }
+            double acc = 0.0, dr;
+            if (a.dbg == 2) {
+                acc = w[0][0] + w[8][2];
+                dr = 0.5;
+            } else if (__all(inter)) {
+#pragma unroll
+                for (int kk = 0; kk < 27; kk++) acc = fma(scoef[kk], w[kk / 3][kk % 3], acc);  // LDS broadcast
+                dr = scoef[27];
+            } else {
+#pragma unroll
+                for (int kk = 0; kk < 27; kk++)
+                    acc = fma(stab[(cwp[i][(kk * VB) >> 5] >> ((kk * VB) & 31)) & MASK], w[kk / 3][kk % 3], acc);
+                dr = 1.0 / stab[(cwp[i][(13 * VB) >> 5] >> ((13 * VB) & 31)) & MASK];
+            }
+            const double xr = w[4][1];  // the point's own old value
+            if (live) lds[(y - r0 + 1) * nx + x] = first_zero ? dr * bp[i] : xr + dr * (bp[i] - acc);
+        }
+    }
+}
+
+template <int VB, int CW, int U>
+__global__ __launch_bounds__(256) void k_sgs27_phase(Sgs27Args a) {
+    extern __shared__ sgs_dbl2_t lds_pairs[];  // 16-B aligned: rows are read as pairs
+    double *lds = reinterpret_cast<double *>(lds_pairs);  // row 0: zeros; row 1 + (y - r0): grid row y
+    __shared__ double stab[VB == 4 ? 16 : 256];
+    __shared__ double scoef[28];  // interior coefficients + 1/a_ii (uniform reads: LDS broadcast, no SGPR pressure)
+    const int tid = threadIdx.x;
+    const int w = xcd_remap(blockIdx.x, gridDim.x);
+    if (tid < 27) scoef[tid] = a.icoef[tid];
+    if (tid == 27) scoef[27] = a.idinv;
+    const int zp = w / a.ntiles, tile = w - zp * a.ntiles;
+    const int z = 2 * zp + a.pz;
+    const int nx = a.nx, ny = a.ny;
+    const int y0 = tile * a.ty, y1 = min(y0 + a.ty, ny);
+    const int r0 = max(y0 - a.nst, 0), r1 = min(y1 + a.nst, ny);
+    const int64_t zoff = (int64_t)z * nx * ny;
+    for (int q = tid; q < a.ntab; q += 256) stab[q] = a.vtab[q];
+    const int nx2 = nx / 2;
+    const int nload2 = (r1 - r0) * nx2;  // nx even: whole rows of 16-B pairs
+    sgs_dbl2_t *l2 = reinterpret_cast<sgs_dbl2_t *>(lds);
+    for (int q = tid; q < nx2; q += 256) l2[q] = sgs_dbl2_t{0.0, 0.0};
+    if (a.own_zero) {
+        for (int q = tid; q < nload2; q += 256) l2[nx2 + q] = sgs_dbl2_t{0.0, 0.0};
+    } else {
+        // all of a lane's loads issued before its LDS writes (a load-wait-write
+        // loop serialises ~13 memory latencies per workgroup)
+        const sgs_dbl2_t *src = reinterpret_cast<const sgs_dbl2_t *>(a.S + zoff + (int64_t)r0 * nx);
+        constexpr int PF = 8;
+        for (int q0 = tid; q0 < nload2; q0 += 256 * PF) {
+            sgs_dbl2_t v[PF];
+#pragma unroll
+            for (int u = 0; u < PF; u++) v[u] = src[min(q0 + 256 * u, nload2 - 1)];
+#pragma unroll
+            for (int u = 0; u < PF; u++)
+                if (q0 + 256 * u < nload2) l2[nx2 + q0 + 256 * u] = v[u];
+        }
+    }
+    __syncthreads();
+    const int nst_run = a.dbg == 5 ? 0 : a.dbg == 6 ? 1 : a.nst;
+    for (int s = 0; s < nst_run; s++) {
+        const int h = a.nst - 1 - s;
+        const int ys0 = max(y0 - h, 0), ys1 = min(y1 + h, ny);
+        const bool first_zero = a.own_zero && a.other_zero && s == 0;
+        if (a.px[s] == 0) sgs27_stage<VB, CW, 0, U>(a, lds, stab, scoef, z, r0, ys0, ys1, a.py[s], first_zero);
+        else sgs27_stage<VB, CW, 1, U>(a, lds, stab, scoef, z, r0, ys0, ys1, a.py[s], first_zero);
+        __syncthreads();
+    }
+    sgs_dbl2_t *dst = reinterpret_cast<sgs_dbl2_t *>(a.T + zoff + (int64_t)y0 * nx);
+    const sgs_dbl2_t *srcl = reinterpret_cast<const sgs_dbl2_t *>(lds + (y0 - r0 + 1) * nx);
+    for (int q = tid; q < (y1 - y0) * nx2; q += 256) dst[q] = srcl[q];
+}
+
+// FAMG_SGS_FUSED=0 (or amg_set_sgs_fused(0)): colour launches instead of the fused phases
+int g_sgs_fused = [] {
+    const char *e = getenv("FAMG_SGS_FUSED");
+    return (e && e[0] == '0') ? 0 : 1;
+}();
+static bool sgs_fused_enabled() { return g_sgs_fused != 0; }
+
+// rows per workgroup and independent points per lane (A/B switches
+// FAMG_SGS27_TY, FAMG_SGS27_U)
+static int sgs27_ty() {
+    static const int v = [] {
+        const char *e = getenv("FAMG_SGS27_TY");
+        const int t = e ? atoi(e) : 0;
+        return t >= 2 && t <= 64 ? t : 16;
+    }();
+    return v;
+}
+static int sgs27_u() {
+    static const int v = [] {
+        const char *e = getenv("FAMG_SGS27_U");
+        return (e && e[0] == '1') ? 1 : 2;
+    }();
+    return v;
+}
+constexpr int SGS27_MAX_NX = 512;  // LDS: (TY + 8) rows of nx doubles (TY = 16: 96 KB at nx = 512)
+
+__global__ void k_sgs27_check(const uint32_t *codes, int cw, int vb, int zcode, int nx, int ny, int nz,
+                              int *bad) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    const int64_t n = (int64_t)nx * ny * nz;
+    if (i >= n) return;
+    const int x = (int)(i % nx), y = (int)((i / nx) % ny), z = (int)(i / ((int64_t)nx * ny));
+    const uint32_t mask = (1u << vb) - 1;
+    for (int k = 0; k < 27; k++) {
+        const int dx = k % 3 - 1, dy = (k / 3) % 3 - 1, dz = k / 9 - 1;
+        const bool in = x + dx >= 0 && x + dx < nx && y + dy >= 0 && y + dy < ny && z + dz >= 0 && z + dz < nz;
+        const uint32_t c = (codes[i * cw + ((k * vb) >> 5)] >> ((k * vb) & 31)) & mask;
+        if (!in && (int)c != zcode) bad[0] = 1;
+    }
+}
+
+// Decide whether S's sweeps can run as fused plane-parity phases: A is stored
+// as DIA codes (whole matrix) with the 27 offsets of an nx x ny x nz grid, the
+// colouring is the parity colouring, and every entry that would leave the grid
+// carries the +0.0 code.
+void sgs27_setup(SgsOp &S) {
+    S.fused27 = false;
+    if (!sgs_fused_enabled() || !S.A) return;
+    const GpuCsr &m = S.A->m;
+    if (m.kernel != SPMV_KERNEL_DIA || !m.has_dia() || m.dia_rowid || m.dia_r0 != 0 || m.dia_r1 != m.nrows ||
+        m.dia_k != 27 || m.nrows != m.ncols)
+        return;
+    if (!((m.dia_vbits == 4 && m.dia_cw == 4) || (m.dia_vbits == 8 && m.dia_cw == 8))) return;
+    const std::vector<int> &off = m.dia_off;
+    const int nx = off[16];       // diagonal (dz, dy, dx) = (0, +1, 0)
+    if (nx < 2 || nx > SGS27_MAX_NX || (nx & 1)) return;  // even rows: aligned 16-B pairs
+    const int64_t pl = off[22];   // diagonal (+1, 0, 0): nx * ny
+    if (pl <= 0 || pl % nx != 0 || m.nrows % pl != 0) return;
+    const int ny = (int)(pl / nx), nz = (int)(m.nrows / pl);
+    for (int k = 0; k < 27; k++) {
+        const int dx = k % 3 - 1, dy = (k / 3) % 3 - 1, dz = k / 9 - 1;
+        if (off[k] != (int64_t)dz * pl + (int64_t)dy * nx + dx) return;
+    }
+    if ((int64_t)S.host_colors.size() != m.nrows) return;
+    for (int64_t i = 0; i < m.nrows; i++) {
+        const int x = (int)(i % nx), y = (int)((i / nx) % ny), z = (int)(i / pl);
+        if (S.host_colors[i] != (x & 1) + 2 * (y & 1) + 4 * (z & 1)) return;
+    }
+    // the +0.0 code: the table is sorted by bit pattern and holds +0.0
+    std::vector<double> tab(m.dia_ntab);
+    hipStream_t s = S.ctx->stream;
+    FAMG_CHECK_HIP(hipMemcpyAsync(tab.data(), m.dia_vtab.get(), tab.size() * 8, hipMemcpyDeviceToHost, s));
+    FAMG_CHECK_HIP(hipStreamSynchronize(s));
+    int zcode = -1;
+    for (size_t q = 0; q < tab.size(); q++) {
+        uint64_t bits;
+        std::memcpy(&bits, &tab[q], 8);
+        if (bits == 0) zcode = (int)q;
+    }
+    if (zcode < 0) return;
+    DevBuf<int> bad(1);
+    FAMG_CHECK_HIP(hipMemsetAsync(bad.get(), 0, sizeof(int), s));
+    hipLaunchKernelGGL(k_sgs27_check, dim3((unsigned)ceil_div(m.nrows, 256)), dim3(256), 0, s, m.dia_codes.get(),
+                       m.dia_cw, m.dia_vbits, zcode, nx, ny, nz, bad.get());
+    FAMG_CHECK_HIP(hipGetLastError());
+    int hbad = 1;
+    FAMG_CHECK_HIP(hipMemcpyAsync(&hbad, bad.get(), sizeof(int), hipMemcpyDeviceToHost, s));
+    FAMG_CHECK_HIP(hipStreamSynchronize(s));
+    if (hbad) return;
+    // code group of an interior row (the grid centre) and its coefficients
+    {
+        const int64_t ic = ((int64_t)(nz / 2) * ny + ny / 2) * nx + nx / 2;
+        std::vector<uint32_t> w(m.dia_cw);
+        FAMG_CHECK_HIP(hipMemcpyAsync(w.data(), m.dia_codes.get() + ic * m.dia_cw, m.dia_cw * 4,
+                                      hipMemcpyDeviceToHost, s));
+        FAMG_CHECK_HIP(hipStreamSynchronize(s));
+        S.icode27.assign(8, 0xffffffffu);
+        for (int q = 0; q < m.dia_cw; q++) S.icode27[q] = w[q];
+        S.icoef27.assign(27, 0.0);
+        const uint32_t mask = (1u << m.dia_vbits) - 1;
+        for (int k = 0; k < 27; k++)
+            S.icoef27[k] = tab[(w[(k * m.dia_vbits) >> 5] >> ((k * m.dia_vbits) & 31)) & mask];
+        // face masks: code bits of the entries with dx = -1 / +1, dy = -1 / +1, dz = -1 / +1
+        S.fmask27.assign(6 * 8, 0u);
+        for (int k = 0; k < 27; k++) {
+            const int dx = k % 3 - 1, dy = (k / 3) % 3 - 1, dz = k / 9 - 1;
+            const uint32_t bits = mask << ((k * m.dia_vbits) & 31);
+            const int q = (k * m.dia_vbits) >> 5;
+            if (dx < 0) S.fmask27[0 * 8 + q] |= bits;
+            if (dx > 0) S.fmask27[1 * 8 + q] |= bits;
+            if (dy < 0) S.fmask27[2 * 8 + q] |= bits;
+            if (dy > 0) S.fmask27[3 * 8 + q] |= bits;
+            if (dz < 0) S.fmask27[4 * 8 + q] |= bits;
+            if (dz > 0) S.fmask27[5 * 8 + q] |= bits;
+        }
+        if (zcode != 0) S.icode27.assign(8, 0xffffffffu);  // cleared entries would not read code 0: no fast path
+    }
+    S.nx27 = nx;
+    S.ny27 = ny;
+    S.nz27 = nz;
+    S.fused_tmp.resize(m.nrows);
+    S.fused_zero.resize(nx + 8);
+    FAMG_CHECK_HIP(hipMemsetAsync(S.fused_zero.get(), 0, (nx + 8) * sizeof(double), s));
+    S.fused27 = true;
+}
+
+// One phase: the planes of parity pz run the in-plane colours (px, py)[0..nst).
+static void sgs27_phase(const SgsOp &S, int pz, int nst, const int *px, const int *py, const double *src,
+                        const double *other, double *dst, const double *b, bool own_zero, bool other_zero,
+                        hipStream_t s) {
+    const GpuCsr &m = S.A->m;
+    const int nplanes = (S.nz27 - pz + 1) / 2;
+    if (nplanes <= 0) return;
+    Sgs27Args a{};
+    a.codes = m.dia_codes.get();
+    a.vtab = m.dia_vtab.get();
+    a.ntab = (int)m.dia_ntab;
+    a.nx = S.nx27;
+    a.ny = S.ny27;
+    a.nz = S.nz27;
+    a.pz = pz;
+    a.nst = nst;
+    for (int q = 0; q < nst; q++) {
+        a.px[q] = px[q];
+        a.py[q] = py[q];
+    }
+    a.S = src;
+    a.O = other;
+    a.T = dst;
+    a.b = b;
+    a.own_zero = own_zero;
+    a.other_zero = other_zero;
+    {  // timing experiments only (wrong results): FAMG_SGS27_DEBUG=1 skips the z +- 1 plane loads
+        static const int dbg = [] {
+            const char *e = getenv("FAMG_SGS27_DEBUG");
+            return e ? atoi(e) : 0;
+        }();
+        if (dbg == 1) a.other_zero = 1;
+        a.dbg = dbg;
+    }
+    a.ty = sgs27_ty();
+    for (int q = 0; q < 8; q++) a.icode[q] = S.icode27[q];
+    for (int f = 0; f < 6; f++)
+        for (int q = 0; q < 8; q++) a.fmask[f][q] = S.fmask27[f * 8 + q];
+    for (int k = 0; k < 27; k++) a.icoef[k] = S.icoef27[k];
+    a.idinv = 1.0 / S.icoef27[13];
+    a.zero = S.fused_zero.get();
+    a.ntiles = (int)ceil_div(S.ny27, a.ty);
+    const int64_t rows = (int64_t)nplanes * S.ny27 * S.nx27;
+    // algorithmic bytes: the parity's x read + written, its codes and b, the
+    // other parity's x read once
+    if (g_launch_log)
+        log_launch("sgs27_phase", SPMV_KERNEL_DIA, SPMV_SGS, rows,
+                   rows * (16 + 4 * (int64_t)m.dia_cw + 8) + (other_zero ? 0 : (int64_t)(m.nrows - rows) * 8));
+    const dim3 grid((unsigned)(nplanes * a.ntiles)), block(256);
+    const size_t lds = (size_t)(a.ty + 2 * nst + 1) * S.nx27 * sizeof(double);
+    const bool u2 = sgs27_u() == 2;
+    if (m.dia_vbits == 4) {
+        if (u2) k_sgs27_phase<4, 4, 2><<<grid, block, lds, s>>>(a);
+        else k_sgs27_phase<4, 4, 1><<<grid, block, lds, s>>>(a);
+    } else {
+        if (u2) k_sgs27_phase<8, 8, 2><<<grid, block, lds, s>>>(a);
+        else k_sgs27_phase<8, 8, 1><<<grid, block, lds, s>>>(a);
+    }
+    FAMG_CHECK_HIP(hipGetLastError());
+}
+
+// x <- SGS step (forward colours 0..7, backward 6..0) as four phases; zero:
+// x starts at 0 (sweep from e = 0: nothing of x is read).
+bool sgs27_applies(const SgsOp &S, const double *x, const double *b) {
+    return S.fused27 && ((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(b)) & 15) == 0;
+}
+
+void sgs27_sweep(SgsOp &S, double *x, const double *b, bool zero) {
+    hipStream_t s = S.ctx->stream;
+    double *t1 = S.fused_tmp.get();
+    static const int fpx[4] = {0, 1, 0, 1}, fpy[4] = {0, 0, 1, 1};  // colours 0,1,2,3 / 4,5,6,7
+    static const int bopx[3] = {0, 1, 0}, bopy[3] = {1, 0, 0};       // colours 6,5,4
+    static const int bepx[4] = {1, 0, 1, 0}, bepy[4] = {1, 1, 0, 0}; // colours 3,2,1,0
+    sgs27_phase(S, 0, 4, fpx, fpy, x, x, t1, b, zero, zero, s);      // even planes -> t1
+    sgs27_phase(S, 1, 4, fpx, fpy, x, t1, t1, b, zero, false, s);    // odd planes -> t1
+    sgs27_phase(S, 1, 3, bopx, bopy, t1, t1, x, b, false, false, s); // odd planes -> x
+    sgs27_phase(S, 0, 4, bepx, bepy, t1, x, x, b, false, false, s);  // even planes -> x
+}
+
+}  // namespace famg

@@ -143,6 +143,8 @@ SIGNATURES = {
     "amg_gen_elasticity_q1": (i32, [i64, i64, i64, dbl, dbl, C.c_uint64, i32, P(vp)]),
     "amg_dist_pcg_solve": (i32, [vp, i32, vp, vp, i64, dbl, dbl, vp, P(i64)]),
     "amg_multigrid_cycle_plan": (i32, [vp, vp, i64, P(i64)]),
+    "amg_set_sgs_fused": (i32, [i32]),
+    "amg_sgs_fused": (i32, [vp, P(i32)]),
     "amg_halo_plan_create": (i32, [i32, i32, vp, P(vp)]),
     "amg_halo_plan_destroy": (i32, [vp]),
     "amg_halo_plan_add_columns": (i32, [vp, i64, vp]),
@@ -506,6 +508,17 @@ def sgs_info(S):
     _ck(_lib.amg_sgs_info(S.h, info.ctypes.data_as(vp)))
     return {"colors": int(info[0]), "kernel": ("csr-stream", "sell", "vector", "dia", "bsr", "sellp")[int(info[1])],
             "diagonals": int(info[2]), "bits": int(info[3])}
+
+
+def set_sgs_fused(enable):
+    """SGS smoothers built afterwards use the fused plane-parity phases where they apply."""
+    _ck(_lib.amg_set_sgs_fused(1 if enable else 0))
+
+
+def sgs_fused(S):
+    v = i32()
+    _ck(_lib.amg_sgs_fused(S.h, C.byref(v)))
+    return bool(v.value)
 
 
 def CoarseCholesky(A):

@@ -208,6 +208,13 @@ amg_status amg_diag_create(amg_ctx *ctx, int64_t n, const double *d, amg_linop *
  * colors: host array of nrows colors in [0, ncolors) or NULL for greedy
  * first-fit coloring in row order. */
 amg_status amg_sgs_create(const amg_linop *A, const int32_t *colors, amg_linop **out);
+/* SGS smoothers built after the call run their sweeps as four fused
+ * plane-parity phases (sgs27.hip) where that applies -- a 27-point grid operator
+ * stored as DIA codes with the parity colouring -- instead of one launch per
+ * colour (default 1; FAMG_SGS_FUSED=0 sets 0).  Bitwise the same results. */
+amg_status amg_set_sgs_fused(int32_t enable);
+/* *fused = 1 if this SGS smoother runs the fused phases. */
+amg_status amg_sgs_fused(const amg_linop *op, int32_t *fused);
 /* Number of colors of an SGS smoother. */
 amg_status amg_sgs_ncolors(const amg_linop *op, int64_t *ncolors);
 /* Storage of the color sweeps: info4 = {colors, kernel (as amg_csr_spmv_info:

@@ -1173,3 +1173,38 @@ def test_cycle_plan_sgs_counts_colour_launches(ctx):
     C = fa().sgs_info(S0)["colors"]
     sweeps = [p for p in plan if p["level"] == 0 and p["mode"] == "SGS"]
     assert len(sweeps) == (C - 1) + (C - 1) + (2 * C - 1), (len(sweeps), C)
+
+
+@pytest.mark.parametrize("dims", [(48, 48, 32), (50, 45, 37), (64, 40, 33)])
+def test_sgs27_fused_phases_bitwise(ctx, dims):
+    """The fused plane-parity SGS phases (sgs27.hip: four launches per SGS step,
+    in-plane colours on shrinking LDS halos) against the colour launches
+    (fifteen per step): bitwise equal for the step from e = 0 (the smoother's
+    apply) and inside the V-cycle (pre-smoothing from zero, post-smoothing on
+    x), odd and even extents; and within 1e-11 of the oracle's V-cycle."""
+    OA = O.aniso27(*dims)
+    A = fa().SparseMatOp.aniso27(ctx, *dims, 1.0, 1.0, 0.01)
+    if A.spmv_info()["kernel"] != "dia":
+        pytest.skip("operator not stored as DIA codes")
+    S1 = fa().SymGaussSeidel(A)
+    fa().set_sgs_fused(False)
+    try:
+        S0 = fa().SymGaussSeidel(A)
+        mg0 = fa().sa_build_box(A, dims, (2, 2, 2), coarsest_dim=500, smoother="sgs")
+    finally:
+        fa().set_sgs_fused(True)
+    mg1 = fa().sa_build_box(A, dims, (2, 2, 2), coarsest_dim=500, smoother="sgs")
+    assert fa().sgs_fused(S1) and not fa().sgs_fused(S0)
+    assert fa().sgs_fused(mg1.level(0)[1]) and not fa().sgs_fused(mg0.level(0)[1])
+    r = np.random.default_rng(8).standard_normal(OA.nrows)
+    e1 = apply_dev(ctx, S1, r, OA.nrows)
+    e0 = apply_dev(ctx, S0, r, OA.nrows)
+    assert np.array_equal(e1, e0)
+    b = np.random.default_rng(9).uniform(-1, 1, OA.nrows)
+    z1 = apply_dev(ctx, mg1, b, OA.nrows)
+    z0 = apply_dev(ctx, mg0, b, OA.nrows)
+    assert np.array_equal(z1, z0)
+    zref = O.Multigrid(oracle_levels_from_gpu(mg1, "sgs")).apply(b)
+    assert np.linalg.norm(z1 - zref) <= 1e-11 * np.linalg.norm(zref)
+    plan = mg1.cycle_plan()
+    assert sum(1 for p in plan if p["name"] == "sgs27_phase") == 8  # two SGS steps x four phases
