@@ -212,6 +212,9 @@ struct SpmvEpi {
 // Y = A X for k columns (column-major, leading dimensions ldx/ldy): SELL
 // matrices stream once per 8 columns; bitwise equal to k SpMVs.
 void spmm(const GpuCsr &m, const double *x, int64_t ldx, double *y, int64_t ldy, int64_t k, hipStream_t s);
+// the same for DIA-code, stencil-class and 3x3-block storage; false if m has none of them
+bool spmm_compressed(const GpuCsr &m, const double *x, int64_t ldx, double *y, int64_t ldy, int64_t k,
+                     hipStream_t s);
 void spmv(const GpuCsr &m, const double *x, double *y, SpmvMode mode, const SpmvEpi &epi,
           hipStream_t s, int64_t seg = -1);
 void spmv_bsr(const GpuCsr &m, const double *x, double *y, SpmvMode mode, const SpmvEpi &epi, hipStream_t s,

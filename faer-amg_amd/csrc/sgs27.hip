@@ -54,7 +54,6 @@ struct Sgs27Args {
     double icoef[27];      // the interior row's coefficients (table values of icode)
     double idinv;          // 1 / icoef[13]
     const double *zero;    // >= nx zeros (rows outside the grid)
-    int dbg;               // timing experiments (FAMG_SGS27_DEBUG): 0 = normal
 };
 
 
@@ -67,8 +66,8 @@ typedef uint32_t sgs_u32x4_t __attribute__((ext_vector_type(4)));
 // needs (3 LDS rows of the own plane, 6 rows of the other parity's planes
 // z +- 1, or a zero row where the row leaves the grid) -- is wave-uniform and
 // lives in scalar registers; a lane only adds its x offset.  The three values
-// x-1, x, x+1 of a row come from two 16-B pair loads; the only lanes whose
-// window leaves the row are x = 0 (PX = 0, k = 0) and x = nx-1 (PX = 1,
+// x-1, x, x+1 of a row come from two aligned 16-B pair loads; the only lanes
+// whose window leaves the row are x = 0 (PX = 0, k = 0) and x = nx-1 (PX = 1,
 // k = nk-1), which clamp the pair address and select 0.0.  U tasks per trip
 // with all loads issued before the sums.  (Sharing one pair load per lane
 // through DPP wave shifts measured slower: each shift waits for its load.)
@@ -85,7 +84,6 @@ template <int VB, int CW, int PX, int U>
 __device__ __forceinline__ void sgs27_stage(const Sgs27Args &a, double *lds, const double *stab, const double *scoef,
                                             int z, int r0, int ys0, int ys1, int py, bool first_zero) {
     constexpr uint32_t MASK = (1u << VB) - 1;
-    constexpr int MT = 4;  // tasks per chunk: their code groups and b prefetched together
     const int nx = a.nx, ny = a.ny, nz = a.nz;
     const int64_t plane = (int64_t)nx * ny;
     const int yfirst = ys0 + ((ys0 & 1) != py ? 1 : 0);
@@ -96,92 +94,88 @@ __device__ __forceinline__ void sgs27_stage(const Sgs27Args &a, double *lds, con
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
     const bool zlo = z == 0, zhi = z == nz - 1;
-    for (int c0 = wave; c0 < ntask; c0 += 4 * MT) {
-        // the chunk's code groups and right-hand sides: HBM streams, all in flight at once
-        uint32_t cwp[MT][CW];
-        double bp[MT];
+    for (int t0 = wave; t0 < ntask; t0 += 4 * U) {
+        double w[U][9][3];
+        uint32_t cw[U][CW];
+        double br[U];
+        int li[U];
+        bool live[U], inter = true;
 #pragma unroll
-        for (int i = 0; i < MT; i++) {
-            const int t = min(c0 + 4 * i, ntask - 1);  // wave-uniform
-            const int yr = t / nseg, sg = t - yr * nseg;
-            const int y = yfirst + 2 * yr;
-            const int x = PX + 2 * min((sg << 6) + lane, nk - 1);
-            const int64_t gi = (int64_t)z * plane + (int64_t)y * nx + x;
-            if (a.dbg == 3) {
-#pragma unroll
-                for (int q = 0; q < CW; q++) cwp[i][q] = a.icode[q];
-            } else {
-#pragma unroll
-                for (int q = 0; q < CW / 4; q++) {
-                    const sgs_u32x4_t c =
-                        __builtin_nontemporal_load(reinterpret_cast<const sgs_u32x4_t *>(a.codes + gi * CW) + q);
-#pragma unroll
-                    for (int e = 0; e < 4; e++) cwp[i][4 * q + e] = c[e];
-                }
-            }
-            bp[i] = __builtin_nontemporal_load(a.b + gi);
-        }
-#pragma unroll
-        for (int i = 0; i < MT; i++) {
-            const int t = c0 + 4 * i;
-            if (t >= ntask) break;  // wave-uniform
+        for (int u = 0; u < U; u++) {
+            const int t = min(t0 + 4 * u, ntask - 1);  // wave-uniform
             const int yr = t / nseg, sg = t - yr * nseg;
             const int y = yfirst + 2 * yr;
             const int k = (sg << 6) + lane;
-            const bool live = k < nk;
+            live[u] = t0 + 4 * u < ntask && k < nk;
             const int x = PX + 2 * min(k, nk - 1);
             const bool lo = PX == 0 && x == 0, hi = PX == 1 && x == nx - 1;
             // pair offsets: A = [x-2+PX, x-1+PX], B = A + 2 (clamped into the row at the edges)
             const int offA = max(x - 2 + PX, 0), offB = min(x + PX, nx - 2);
             const int64_t rowg = (int64_t)z * plane + (int64_t)y * nx;
-            double w[9][3];
+            const int64_t gi = rowg + x;
+            li[u] = (y - r0 + 1) * nx + x;
+#pragma unroll
+            for (int q = 0; q < CW / 4; q++) {
+                const sgs_u32x4_t c =
+                    __builtin_nontemporal_load(reinterpret_cast<const sgs_u32x4_t *>(a.codes + gi * CW) + q);
+#pragma unroll
+                for (int e = 0; e < 4; e++) cw[u][4 * q + e] = c[e];
+            }
+            br[u] = a.b[gi];
 #pragma unroll
             for (int j = 0; j < 9; j++) {
                 const int dz = j / 3 - 1, dy = j % 3 - 1;
                 const int yy = y + dy, zz = z + dz;
                 const bool rowok = yy >= 0 && yy < ny && zz >= 0 && zz < nz;  // wave-uniform
                 const double *row;
-                if (dz == 0) row = lds + (rowok && a.dbg != 4 ? (yy - r0 + 1) * nx : 0);  // LDS row 0: zeros
+                if (dz == 0) row = lds + (rowok ? (yy - r0 + 1) * nx : 0);  // LDS row 0: zeros
                 else if (a.other_zero || !rowok) row = a.zero;
                 else row = a.O + rowg + (int64_t)dz * plane + (int64_t)dy * nx;
                 const sgs_dbl2_t pa = *reinterpret_cast<const sgs_dbl2_t *>(row + offA);
                 const sgs_dbl2_t pb = *reinterpret_cast<const sgs_dbl2_t *>(row + offB);
                 if (PX == 0) {
-                    w[j][0] = lo ? 0.0 : pa.y;
-                    w[j][1] = pb.x;
-                    w[j][2] = pb.y;
+                    w[u][j][0] = lo ? 0.0 : pa.y;
+                    w[u][j][1] = pb.x;
+                    w[u][j][2] = pb.y;
                 } else {
-                    w[j][0] = pa.x;
-                    w[j][1] = pa.y;
-                    w[j][2] = hi ? 0.0 : pb.x;
+                    w[u][j][0] = pa.x;
+                    w[u][j][1] = pa.y;
+                    w[u][j][2] = hi ? 0.0 : pb.x;
                 }
             }
             // the interior group with the entries leaving the grid cleared
             const bool ylo = y == 0, yhi = y == ny - 1;
-            bool inter = true;
 #pragma unroll
             for (int q = 0; q < CW; q++) {
                 const uint32_t clr = (lo ? a.fmask[0][q] : 0u) | (hi ? a.fmask[1][q] : 0u) |
                                      (ylo ? a.fmask[2][q] : 0u) | (yhi ? a.fmask[3][q] : 0u) |
                                      (zlo ? a.fmask[4][q] : 0u) | (zhi ? a.fmask[5][q] : 0u);
-                inter = inter && cwp[i][q] == (a.icode[q] & ~clr);
+                inter = inter && cw[u][q] == (a.icode[q] & ~clr);
             }
-            double acc = 0.0, dr;
-            if (a.dbg == 2) {
-                acc = w[0][0] + w[8][2];
-                dr = 0.5;
-            } else if (__all(inter)) {
+        }
+        double acc[U], dr[U];
+        if (__all(inter)) {
 #pragma unroll
-                for (int kk = 0; kk < 27; kk++) acc = fma(scoef[kk], w[kk / 3][kk % 3], acc);  // LDS broadcast
-                dr = scoef[27];
-            } else {
+            for (int u = 0; u < U; u++) {
+                acc[u] = 0.0;
 #pragma unroll
-                for (int kk = 0; kk < 27; kk++)
-                    acc = fma(stab[(cwp[i][(kk * VB) >> 5] >> ((kk * VB) & 31)) & MASK], w[kk / 3][kk % 3], acc);
-                dr = 1.0 / stab[(cwp[i][(13 * VB) >> 5] >> ((13 * VB) & 31)) & MASK];
+                for (int k = 0; k < 27; k++) acc[u] = fma(scoef[k], w[u][k / 3][k % 3], acc[u]);  // LDS broadcast
+                dr[u] = scoef[27];
             }
-            const double xr = w[4][1];  // the point's own old value
-            if (live) lds[(y - r0 + 1) * nx + x] = first_zero ? dr * bp[i] : xr + dr * (bp[i] - acc);
+        } else {
+#pragma unroll
+            for (int u = 0; u < U; u++) {
+                acc[u] = 0.0;
+#pragma unroll
+                for (int k = 0; k < 27; k++)
+                    acc[u] = fma(stab[(cw[u][(k * VB) >> 5] >> ((k * VB) & 31)) & MASK], w[u][k / 3][k % 3], acc[u]);
+                dr[u] = 1.0 / stab[(cw[u][(13 * VB) >> 5] >> ((13 * VB) & 31)) & MASK];
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            const double xr = w[u][4][1];  // the point's own old value
+            if (live[u]) lds[li[u]] = first_zero ? dr[u] * br[u] : xr + dr[u] * (br[u] - acc[u]);
         }
     }
 }
@@ -224,8 +218,7 @@ __global__ __launch_bounds__(256) void k_sgs27_phase(Sgs27Args a) {
         }
     }
     __syncthreads();
-    const int nst_run = a.dbg == 5 ? 0 : a.dbg == 6 ? 1 : a.nst;
-    for (int s = 0; s < nst_run; s++) {
+    for (int s = 0; s < a.nst; s++) {
         const int h = a.nst - 1 - s;
         const int ys0 = max(y0 - h, 0), ys1 = min(y1 + h, ny);
         const bool first_zero = a.own_zero && a.other_zero && s == 0;
@@ -258,7 +251,7 @@ static int sgs27_ty() {
 static int sgs27_u() {
     static const int v = [] {
         const char *e = getenv("FAMG_SGS27_U");
-        return (e && e[0] == '1') ? 1 : 2;
+        return (e && e[0] == '2') ? 2 : 1;
     }();
     return v;
 }
@@ -390,14 +383,7 @@ static void sgs27_phase(const SgsOp &S, int pz, int nst, const int *px, const in
     a.b = b;
     a.own_zero = own_zero;
     a.other_zero = other_zero;
-    {  // timing experiments only (wrong results): FAMG_SGS27_DEBUG=1 skips the z +- 1 plane loads
-        static const int dbg = [] {
-            const char *e = getenv("FAMG_SGS27_DEBUG");
-            return e ? atoi(e) : 0;
-        }();
-        if (dbg == 1) a.other_zero = 1;
-        a.dbg = dbg;
-    }
+
     a.ty = sgs27_ty();
     for (int q = 0; q < 8; q++) a.icode[q] = S.icode27[q];
     for (int f = 0; f < 6; f++)

@@ -2250,6 +2250,7 @@ void choose_kernel(GpuCsr &m) {
 #define FAMG_LAY16 , 16
 
 void spmm(const GpuCsr &m, const double *x, int64_t ldx, double *y, int64_t ldy, int64_t k, hipStream_t s) {
+    if (spmm_compressed(m, x, ldx, y, ldy, k, s)) return;  // DIA codes, stencil classes, 3x3 blocks (spmm.hip)
     if (m.kernel != SPMV_KERNEL_SELL || m.sell_vbits) {  // other storages: one SpMV per column
         for (int64_t c = 0; c < k; c++) spmv(m, x + c * ldx, y + c * ldy, SPMV_SET, SpmvEpi{}, s);
         return;

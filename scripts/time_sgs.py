@@ -34,6 +34,6 @@ for fused in (True, False):
     res[fused] = ((time.perf_counter() - t0) / 20 * 1e3, e.cpu().numpy())
     del S
 fa.set_sgs_fused(True)
-print(f"TY={os.environ.get('FAMG_SGS27_TY', '16')} U={os.environ.get('FAMG_SGS27_U', '2')}: "
+print(f"TY={os.environ.get('FAMG_SGS27_TY', '16')} U={os.environ.get('FAMG_SGS27_U', '1')}: "
       f"fused {res[True][0]:.3f} ms/step, colour launches {res[False][0]:.3f} ms/step, "
       f"bitwise {np.array_equal(res[True][1], res[False][1])}", flush=True)

@@ -1208,3 +1208,43 @@ def test_sgs27_fused_phases_bitwise(ctx, dims):
     assert np.linalg.norm(z1 - zref) <= 1e-11 * np.linalg.norm(zref)
     plan = mg1.cycle_plan()
     assert sum(1 for p in plan if p["name"] == "sgs27_phase") == 8  # two SGS steps x four phases
+
+
+def _spmm_vs_spmv(ctx, A, ks=(1, 3, 8, 32), seed=0):
+    """Y = A X (k columns, leading dimensions > n) against k single-vector applies: bitwise."""
+    import torch
+    m, n = A.dims()
+    rng = np.random.default_rng(seed)
+    for k in ks:
+        X = _colmajor(rng, n, k, 3)
+        Y = _colmajor(rng, m, k, 5)
+        A.apply(Y, X)
+        ctx.synchronize()
+        for c in range(k):
+            y1 = torch.empty(m, dtype=torch.float64, device="cuda:0")
+            A.apply(y1, X[:, c].contiguous())
+            ctx.synchronize()
+            assert torch.equal(Y[:, c], y1), (A.spmv_info()["kernel"], k, c)
+
+
+def test_spmm_compressed_storages(ctx):
+    """f2 (adaptivity.rs:168-244,307-390): k-wide applies on the storages the
+    hierarchies use -- DIA codes (7 diagonals; the 33-diagonal run pattern of A_1;
+    the 27-point stencil), stencil classes (one row per lane on A_2, one row per
+    wave on A_3) and 3x3 blocks (elasticity) -- each column bitwise equal to the
+    single-vector kernel, k in {1, 3, 8, 32} (column groups of 8)."""
+    seen = set()
+    A7 = fa().SparseMatOp.laplace3d_7pt(ctx, 64, 64, 64)
+    A27 = fa().SparseMatOp.aniso27(ctx, 48, 48, 32, 1.0, 1.0, 0.01)
+    dims = (128, 128, 128)
+    A = fa().SparseMatOp.laplace3d_7pt(ctx, *dims)
+    mg = fa().sa_build_box(A, dims, (2, 2, 2), coarsest_dim=500)
+    mats = [A7, A27] + [mg.level(l)[0] for l in range(1, mg.levels() - 1)]
+    H = fa().elasticity_q1((12, 10, 10), seed=3)
+    mats.append(H.upload(ctx))
+    for M in mats:
+        info = M.spmv_info()
+        seen.add((info["kernel"], info.get("classes", 0) > 0))
+        _spmm_vs_spmv(ctx, M, ks=(1, 3, 8, 32) if M.nrows < 2_000_000 else (3, 8))
+    kinds = {k for k, _ in seen}
+    assert {"dia", "bsr"} <= kinds, seen
