@@ -414,6 +414,8 @@ def run_single(args):
         "ms_per_step": round(ms_per_cycle, 4),
         "higher_is_better": True,
         "scaling": "weak",
+        "scaling_note": "single GPU: the N = 1 base of bench.py's default weak series "
+                        "(256^3 rows per GPU fixed as N grows; --workload c4 gives the strong series)",
         "vs_baseline": None,
         "dtype": "f64",
         "data": "synthetic (device-generated operator, splitmix64 rhs seed 42)",

@@ -160,14 +160,14 @@ amg_status amg_set_alloc_policy(int32_t policy) {
 
 amg_status amg_set_value_codes(int32_t enable) {
     return guard([&] {
-        FAMG_REQUIRE(enable == 0 || enable == 1, AMG_ERR_INVALID, "enable must be 0 or 1");
+        FAMG_REQUIRE(enable >= 0 && enable <= 2, AMG_ERR_INVALID, "enable must be 0, 1 or 2");
         g_value_codes = enable;
     });
 }
 
 amg_status amg_set_sgs_fused(int32_t enable) {
     return guard([&] {
-        FAMG_REQUIRE(enable == 0 || enable == 1, AMG_ERR_INVALID, "enable must be 0 or 1");
+        FAMG_REQUIRE(enable >= 0 && enable <= 2, AMG_ERR_INVALID, "enable must be 0, 1 or 2");
         g_sgs_fused = enable;
     });
 }
@@ -292,6 +292,34 @@ amg_status amg_csr_class_info(const amg_linop *op, int64_t *info4) {
     });
 }
 
+amg_status amg_csr_set_grid(amg_linop *op, int64_t nx, int64_t ny, int64_t nz) {
+    return guard([&] {
+        auto p = need_csr(op);
+        FAMG_REQUIRE(nx >= 0 && ny >= 0 && nz >= 0, AMG_ERR_INVALID, "grid dims must be >= 0");
+        FAMG_REQUIRE((nx == 0 && ny == 0 && nz == 0) || (p->m.nrows == p->m.ncols && nx * ny * nz == p->m.nrows),
+                     AMG_ERR_DIM, "grid dims do not match the square matrix");
+        p->m.grid[0] = nx;
+        p->m.grid[1] = ny;
+        p->m.grid[2] = nz;
+        csr_finalize(p->m, &p->m.seg_rows);
+    });
+}
+
+amg_status amg_csr_grid_info(const amg_linop *op, int64_t *info12) {
+    return guard([&] {
+        FAMG_REQUIRE(info12, AMG_ERR_INVALID, "null argument");
+        const GpuCsr &m = need_csr(op)->m;
+        for (int q = 0; q < 12; q++) info12[q] = 0;
+        for (int q = 0; q < 3; q++) info12[q] = m.grid[q];
+        const bool on = m.has_scs() && m.xscs;
+        info12[3] = on ? 1 : 0;
+        for (int q = 0; q < 3; q++) {
+            info12[4 + q] = on ? m.xscs_t[q] : 0;
+            info12[7 + q] = on ? m.xscs_r[q] : 0;
+        }
+    });
+}
+
 amg_status amg_csr_dia_range(const amg_linop *op, int64_t *info4) {
     return guard([&] {
         FAMG_REQUIRE(info4, AMG_ERR_INVALID, "null argument");
@@ -301,6 +329,21 @@ amg_status amg_csr_dia_range(const amg_linop *op, int64_t *info4) {
         info4[1] = on ? m.dia_r1 : 0;
         info4[2] = on ? m.dia_k : 0;
         info4[3] = on ? m.dia_vbits : 0;
+    });
+}
+
+amg_status amg_csr_spmv_epilogue(const amg_linop *op, int32_t mode, const double *x, double *y, const double *b,
+                                 const double *d) {
+    return guard([&] {
+        auto p = need_csr(op);
+        FAMG_REQUIRE(mode >= SPMV_SET && mode <= SPMV_JACOBI, AMG_ERR_INVALID, "mode must be SET, ADD, RESID or JACOBI");
+        FAMG_REQUIRE(x && y && x != y, AMG_ERR_INVALID, "x and y must be distinct device vectors");
+        FAMG_REQUIRE((mode != SPMV_RESID && mode != SPMV_JACOBI) || b, AMG_ERR_INVALID, "b required");
+        FAMG_REQUIRE(mode != SPMV_JACOBI || d, AMG_ERR_INVALID, "d required");
+        SpmvEpi e;
+        e.b = b;
+        e.d = d;
+        spmv(p->m, x, y, (SpmvMode)mode, e, p->ctx->stream);
     });
 }
 

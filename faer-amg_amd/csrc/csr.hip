@@ -42,6 +42,7 @@ void csr_clone(const GpuCsr &src, GpuCsr &dst) {
         FAMG_CHECK_HIP(hipMemcpyAsync(dst.val.get(), src.val.get(), src.nnz * sizeof(double), hipMemcpyDeviceToDevice, s));
     }
     FAMG_CHECK_HIP(hipStreamSynchronize(s));
+    for (int q = 0; q < 3; q++) dst.grid[q] = src.grid[q];
 }
 
 __global__ void k_narrow_rp(const int64_t *rp64, int32_t *rp32, int64_t n1) {
@@ -421,6 +422,7 @@ void gen_stencil(GpuCsr &m, Ctx *ctx, int64_t nx, int64_t ny, int64_t nz, const 
     hipLaunchKernelGGL(k_sten_fill, dim3(g), dim3(256), 0, s, st, nx, ny, nz, m.rp64.get(),
                        m.col.get(), m.val.get());
     FAMG_CHECK_HIP(hipGetLastError());
+    m.grid[0] = nx; m.grid[1] = ny; m.grid[2] = nz;
     csr_finalize(m);
 }
 

@@ -111,6 +111,15 @@ struct GpuCsr {
     int64_t scs_seg = -1;  // >= 0: only this row segment (a distributed level's halo interior) beside SELL
     int scs_ib = 0;
     bool scs_lanes = false;  // one row per wave (few long rows: spmv_scs_lanes_kernel)
+    // x-staged stencil classes on a 3-D grid (scs.hip, spmv_xscs_kernel): per tile
+    // of tx x ty x tz grid points its x window (tile + halo rx/ry/rz) in LDS;
+    // xscs_lo[k] = the window offset of stencil offset k
+    bool xscs = false;
+    int xscs_t[3] = {0, 0, 0}, xscs_r[3] = {0, 0, 0};
+    DevBuf<int32_t> xscs_lo;
+    // grid hint: the rows are the points of an nx x ny x nz grid, x fastest (0 = none);
+    // set by the stencil generators, the box hierarchy and amg_csr_set_grid
+    int64_t grid[3] = {0, 0, 0};
     // x-staged SELL (xsell.hip): per group of 4096 rows the x chunks staged in LDS,
     // per slice fp64 values + 16-bit LDS indices (or 32-bit columns: escape slices)
     DevBuf<char> xs_data;
@@ -422,7 +431,9 @@ std::shared_ptr<CoarseCholOp> make_coarse_chol(CsrOp &A);
 CsrPtr sa_tentative(Ctx *ctx, int64_t n, const int64_t *agg_of, int64_t naggs,
                     const double *nn, double *coarse_nn);
 CsrPtr smooth_interpolation(CsrOp &A, const CsrOp &P, double omega);
-CsrPtr galerkin_rap(const CsrOp &R, const CsrOp &A, const CsrOp &P);
+// Galerkin A_c = R (A P); grid: the coarse grid dims (hint for the x-staged
+// stencil kernels) or null
+CsrPtr galerkin_rap(const CsrOp &R, const CsrOp &A, const CsrOp &P, const int64_t *grid = nullptr);
 CsrPtr transpose_op(const CsrOp &P);
 CsrPtr spgemm_op(const CsrOp &A, const CsrOp &B);
 void nn_stationary_l1(CsrOp &A, int64_t iters, double *x_host);

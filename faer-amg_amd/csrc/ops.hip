@@ -684,12 +684,15 @@ CsrPtr smooth_interpolation(CsrOp &A, const CsrOp &P, double omega) {
 }
 
 // A_c = R (A P) (interpolation/mod.rs:828)
-CsrPtr galerkin_rap(const CsrOp &R, const CsrOp &A, const CsrOp &P) {
+CsrPtr galerkin_rap(const CsrOp &R, const CsrOp &A, const CsrOp &P, const int64_t *grid) {
     FAMG_REQUIRE(R.ncols == A.nrows && A.ncols == P.nrows && R.nrows == P.ncols, AMG_ERR_DIM,
                  "galerkin_rap dims");
     GpuCsr AP, C;
     spgemm(A.m, P.m, AP, false);
-    spgemm(R.m, AP, C);
+    spgemm(R.m, AP, C, false);
+    if (grid)
+        for (int q = 0; q < 3; q++) C.grid[q] = grid[q];
+    csr_finalize(C);
     return wrap(A.ctx, std::move(C));
 }
 
@@ -826,7 +829,8 @@ std::shared_ptr<MultigridOp> sa_build_box(const CsrPtr &A, int64_t nx, int64_t n
         CsrPtr P = smooth_interpolation(*cur, *Pt, omega);
         Pt.reset();
         CsrPtr R = transpose_op(*P);
-        CsrPtr Ac = galerkin_rap(*R, *cur, *P);
+        const int64_t cgrid[3] = {ncx, ncy, ncz};  // the coarse grid (x-staged stencil kernels)
+        CsrPtr Ac = galerkin_rap(*R, *cur, *P, cgrid);
         nn_stationary_l1_dev(*Ac, 3, cnn.get());
         if (smoother == 3) {
             std::vector<int32_t> a32(n);

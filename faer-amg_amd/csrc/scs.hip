@@ -21,6 +21,7 @@
 // matrix or for the halo-interior row segment of a distributed level (rows that
 // read owned columns only; the boundary segments keep SELL-64).
 #include <algorithm>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <unordered_map>
@@ -181,6 +182,153 @@ __global__ __launch_bounds__(256) void spmv_scs_lanes_kernel(ScsArgs a) {
     }
 }
 
+// x-staged stencil classes on a 3-D grid (the rows are the points of an
+// nx x ny x nz grid, x fastest, and every nonzero's offset maps to a grid
+// neighbour within radii rx, ry, rz).  One workgroup per tile of tx x ty x tz
+// points: it stages the tile's x window -- the tile plus the halo, 0.0 outside
+// the grid -- in LDS (one read of each x value from L2/HBM per window instead of
+// one cache gather per entry), then each lane walks the K offsets of its RL rows
+// in ascending order reading x from LDS at its window position + lo[k].  A
+// wave whose rows share a class (interior tiles) reads the dictionary through
+// scalar loads.  Arithmetic is spmv_scs_kernel's: fma over the K offsets in
+// ascending order, absent entries +0.0 times a finite value (an x entry or the
+// halo's 0.0), so the row sums are bitwise the oracle's CSR sums.
+struct XscsArgs {
+    const void *cls;
+    const double *dict;
+    const int32_t *lo;
+    int32_t k;
+    int nx, ny, nz, tx, ty, tz, rx, ry, rz, wx, wy, wz, ntx, nty;
+    const double *x;
+    double *y;
+    const double *b;
+    const double *d;
+    const uint8_t *dc;
+    const double *dt;
+};
+
+template <int MODE, int IB, int RL>
+__global__ __launch_bounds__(256) void spmv_xscs_kernel(XscsArgs a) {
+    extern __shared__ double win[];
+    const int tid = threadIdx.x;
+    const int t = xcd_remap(blockIdx.x, gridDim.x);
+    const int tix = t % a.ntx, tiy = (t / a.ntx) % a.nty, tiz = t / (a.ntx * a.nty);
+    const int x0 = tix * a.tx, y0 = tiy * a.ty, z0 = tiz * a.tz;
+    const int T = a.tx * a.ty * a.tz;
+    const int64_t plane = (int64_t)a.nx * a.ny;
+    auto cls_of = [&](int64_t r) {
+        return IB == 1 ? (int)static_cast<const uint8_t *>(a.cls)[r] : (int)static_cast<const uint16_t *>(a.cls)[r];
+    };
+    // the rows' class ids and epilogue operands first: their loads overlap the staging
+    int wb[RL], c[RL];
+    int64_t gi[RL];
+    bool live[RL];
+    double br[RL], xr[RL], dr[RL], yr[RL];
+#pragma unroll
+    for (int j = 0; j < RL; j++) {
+        const int lt = tid + 256 * j;
+        const int lx = lt % a.tx, ly = (lt / a.tx) % a.ty, lz = lt / (a.tx * a.ty);
+        const int gx = x0 + lx, gy = y0 + ly, gz = z0 + lz;
+        live[j] = lt < T && gx < a.nx && gy < a.ny && gz < a.nz;
+        gi[j] = live[j] ? (int64_t)gz * plane + (int64_t)gy * a.nx + gx
+                        : (int64_t)z0 * plane + (int64_t)y0 * a.nx + x0;  // the tile's first point
+        wb[j] = live[j] ? ((lz + a.rz) * a.wy + ly + a.ry) * a.wx + lx + a.rx
+                        : (a.rz * a.wy + a.ry) * a.wx + a.rx;
+        c[j] = cls_of(gi[j]);
+        br[j] = xr[j] = dr[j] = yr[j] = 0.0;
+        if (live[j]) {
+            if constexpr (MODE == SPMV_RESID) br[j] = a.b[gi[j]];
+            if constexpr (MODE == SPMV_ADD) yr[j] = a.y[gi[j]];
+            if constexpr (MODE == SPMV_JACOBI) {
+                xr[j] = a.x[gi[j]];
+                br[j] = a.b[gi[j]];
+                dr[j] = a.dc ? a.dt[a.dc[gi[j]]] : a.d[gi[j]];
+            }
+        }
+    }
+    // stage the window: rows of wx consecutive x values, 0.0 outside the grid
+    const int W = a.wx * a.wy * a.wz;
+    constexpr int PF = 8;
+    for (int p0 = tid; p0 < W; p0 += 256 * PF) {
+        double v[PF];
+#pragma unroll
+        for (int u = 0; u < PF; u++) {
+            const int p = p0 + 256 * u;
+            const int px = p % a.wx, q = p / a.wx;
+            const int py = q % a.wy, pz = q / a.wy;
+            const int gx = x0 - a.rx + px, gy = y0 - a.ry + py, gz = z0 - a.rz + pz;
+            const bool in = p < W && (unsigned)gx < (unsigned)a.nx && (unsigned)gy < (unsigned)a.ny &&
+                            (unsigned)gz < (unsigned)a.nz;
+            v[u] = in ? a.x[(int64_t)gz * plane + (int64_t)gy * a.nx + gx] : 0.0;
+        }
+#pragma unroll
+        for (int u = 0; u < PF; u++)
+            if (p0 + 256 * u < W) win[p0 + 256 * u] = v[u];
+    }
+    __syncthreads();
+    bool uni = true;
+    int cu[RL];
+#pragma unroll
+    for (int j = 0; j < RL; j++) {
+        cu[j] = __builtin_amdgcn_readfirstlane(c[j]);
+        uni = uni && __all(c[j] == cu[j]);
+    }
+    double acc[RL];
+#pragma unroll
+    for (int j = 0; j < RL; j++) acc[j] = 0.0;
+    if (uni) {  // wave-uniform classes: dictionary values through scalar loads
+        for (int k0 = 0; k0 < a.k; k0 += SCS_U) {
+            int l[SCS_U];
+#pragma unroll
+            for (int u = 0; u < SCS_U; u++) l[u] = a.lo[k0 + u];
+            double xv[RL][SCS_U], v[RL][SCS_U];
+#pragma unroll
+            for (int j = 0; j < RL; j++)
+#pragma unroll
+                for (int u = 0; u < SCS_U; u++) {
+                    xv[j][u] = win[wb[j] + l[u]];
+                    v[j][u] = a.dict[(int64_t)cu[j] * a.k + k0 + u];
+                }
+#pragma unroll
+            for (int j = 0; j < RL; j++)
+#pragma unroll
+                for (int u = 0; u < SCS_U; u++) acc[j] = fma(v[j][u], xv[j][u], acc[j]);
+        }
+    } else {
+        for (int k0 = 0; k0 < a.k; k0 += SCS_U) {
+            int l[SCS_U];
+#pragma unroll
+            for (int u = 0; u < SCS_U; u++) l[u] = a.lo[k0 + u];
+            double xv[RL][SCS_U], v[RL][SCS_U];
+#pragma unroll
+            for (int j = 0; j < RL; j++) {
+                const double *dj = a.dict + (int64_t)c[j] * a.k + k0;
+#pragma unroll
+                for (int u = 0; u < SCS_U; u += 2) {
+                    const scs_dbl2a_t pv = *reinterpret_cast<const scs_dbl2a_t *>(dj + u);
+                    v[j][u] = pv.x;
+                    v[j][u + 1] = pv.y;
+                }
+#pragma unroll
+                for (int u = 0; u < SCS_U; u++) xv[j][u] = win[wb[j] + l[u]];
+            }
+#pragma unroll
+            for (int j = 0; j < RL; j++)
+#pragma unroll
+                for (int u = 0; u < SCS_U; u++) acc[j] = fma(v[j][u], xv[j][u], acc[j]);
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < RL; j++) {
+        if (!live[j]) continue;
+        const int64_t i = gi[j];
+        if constexpr (MODE == SPMV_SET) a.y[i] = acc[j];
+        else if constexpr (MODE == SPMV_ADD) a.y[i] = yr[j] + acc[j];
+        else if constexpr (MODE == SPMV_RESID) a.y[i] = br[j] - acc[j];
+        else a.y[i] = xr[j] + dr[j] * (br[j] - acc[j]);  // JACOBI
+    }
+}
+
 // the lanes-per-row kernel for row ranges of < SCS_LANES_ROWS rows with >= 256
 // offsets (A/B switch FAMG_SCS_LANES=0: no stencil classes for them)
 constexpr int64_t SCS_LANES_ROWS = 131072;
@@ -207,6 +355,114 @@ void scs_release(GpuCsr &m) {
     m.scs_k = m.scs_nclass = m.scs_ib = 0;
     m.scs_seg = -1;
     m.scs_lanes = false;
+    m.xscs = false;
+    m.xscs_lo.release();
+}
+
+// A/B switch FAMG_XSCS=0: no x-staged stencil classes; FAMG_XSCS_TILE=tx,ty,tz
+// forces the tile
+static bool xscs_enabled() {
+    static const bool on = [] {
+        const char *e = getenv("FAMG_XSCS");
+        return !(e && e[0] == '0');
+    }();
+    return on;
+}
+
+// The grid hint applies to the whole square matrix.
+static bool grid_applies(const GpuCsr &m) {
+    return xscs_enabled() && m.grid[0] > 0 && m.grid[1] > 0 && m.grid[2] > 0 && m.nrows == m.ncols &&
+           m.grid[0] * m.grid[1] * m.grid[2] == m.nrows && m.nrows < (int64_t(1) << 31);
+}
+
+// Decompose the offsets into grid steps (dx, dy, dz) (centred residues), check
+// that every nonzero entry's step stays inside the grid, pick the tile and store
+// the window offsets: m.xscs on success.
+static bool xscs_setup(GpuCsr &m, const std::vector<int32_t> &offs, int Kp, const std::vector<int64_t> &rp,
+                       const std::vector<int32_t> &col, const std::vector<double> &val) {
+    const int64_t nx = m.grid[0], ny = m.grid[1], nz = m.grid[2], pl = nx * ny, n = m.nrows;
+    const int K = (int)offs.size();
+    std::vector<int> dx(K), dy(K), dz(K);
+    int rx = 0, ry = 0, rz = 0;
+    for (int k = 0; k < K; k++) {
+        const int64_t o = offs[k];
+        int64_t ex = ((o % nx) + nx) % nx;
+        if (ex > nx / 2) ex -= nx;
+        const int64_t q = (o - ex) / nx;
+        int64_t ey = ((q % ny) + ny) % ny;
+        if (ey > ny / 2) ey -= ny;
+        const int64_t ez = (q - ey) / ny;
+        dx[k] = (int)ex;
+        dy[k] = (int)ey;
+        dz[k] = (int)ez;
+        rx = std::max(rx, std::abs(dx[k]));
+        ry = std::max(ry, std::abs(dy[k]));
+        rz = std::max<int>(rz, (int)std::min<int64_t>(std::abs(ez), INT32_MAX / 4));
+    }
+    if (rx > 16 || ry > 16 || rz > 16) return false;
+    bool ok = true;
+#pragma omp parallel for schedule(static) reduction(&& : ok)
+    for (int64_t i = 0; i < n; i++) {
+        const int64_t x = i % nx, y = (i / nx) % ny, z = i / pl;
+        for (int64_t e = rp[i]; e < rp[i + 1]; e++) {
+            if (val[e] == 0.0) continue;
+            const int32_t o = (int32_t)((int64_t)col[e] - i);
+            const int k = (int)(std::lower_bound(offs.begin(), offs.end(), o) - offs.begin());
+            const int64_t X = x + dx[k], Y = y + dy[k], Z = z + dz[k];
+            if (X < 0 || X >= nx || Y < 0 || Y >= ny || Z < 0 || Z >= nz) ok = false;
+        }
+    }
+    if (!ok) return false;
+    // tile: smallest modelled time -- per CU, ds_read_b64 at 2 clk per wave and
+    // offset plus the window staged at ~64 B/clk, in rounds of 256 workgroups,
+    // plus a latency per round of resident workgroups
+    int best[3] = {0, 0, 0};
+    double best_cost = 1e300;
+    auto cands = [](int64_t ext, bool z) {
+        std::vector<int> c;
+        for (int t : {1, 2, 4, 8, 16, 32, 64})
+            if ((z || t >= 4) && t <= ext) c.push_back(t);
+        if (ext < 64 && (c.empty() || c.back() != ext)) c.push_back((int)ext);
+        return c;
+    };
+    for (int tx : cands(nx, false))
+        for (int ty : cands(ny, false))
+            for (int tz : cands(nz, true)) {
+                const int64_t T = (int64_t)tx * ty * tz;
+                const int64_t W = (int64_t)(tx + 2 * rx) * (ty + 2 * ry) * (tz + 2 * rz);
+                if (T > 1024 || T < std::min<int64_t>(64, n) || W * 8 > 64 * 1024) continue;
+                const int64_t ntiles = ceil_div(nx, tx) * ceil_div(ny, ty) * ceil_div(nz, tz);
+                const double occ = std::min(4.0, std::floor(160.0 * 1024 / (W * 8.0)));
+                const double rounds = std::ceil(ntiles / 256.0);
+                const double cost = rounds * ((double)std::max<int64_t>(T, 64) * Kp / 32.0 + W / 8.0) +
+                                    1500.0 * std::ceil(ntiles / (256.0 * occ));
+                if (cost < best_cost) {
+                    best_cost = cost;
+                    best[0] = tx; best[1] = ty; best[2] = tz;
+                }
+            }
+    if (const char *e = getenv("FAMG_XSCS_TILE")) {
+        int t0, t1, t2;
+        if (sscanf(e, "%d,%d,%d", &t0, &t1, &t2) == 3 && t0 > 0 && t1 > 0 && t2 > 0 && t0 * t1 * t2 <= 1024 &&
+            (int64_t)(t0 + 2 * rx) * (t1 + 2 * ry) * (t2 + 2 * rz) * 8 <= 64 * 1024) {
+            best[0] = t0; best[1] = t1; best[2] = t2;
+        }
+    }
+    if (!best[0]) return false;
+    const int wx = best[0] + 2 * rx, wy = best[1] + 2 * ry;
+    std::vector<int32_t> lo(Kp, (rz * wy + ry) * wx + rx);  // padding offsets: the row itself
+    for (int k = 0; k < K; k++) lo[k] = ((dz[k] + rz) * wy + dy[k] + ry) * wx + dx[k] + rx;
+    // lo is relative to the window origin; the kernel adds the row's position
+    // (its window base includes the halo), so subtract the centre
+    const int ctr = (rz * wy + ry) * wx + rx;
+    for (int k = 0; k < Kp; k++) lo[k] -= ctr;
+    m.xscs_lo.resize(Kp);
+    FAMG_CHECK_HIP(hipMemcpyAsync(m.xscs_lo.get(), lo.data(), Kp * 4, hipMemcpyHostToDevice, m.ctx->stream));
+    FAMG_CHECK_HIP(hipStreamSynchronize(m.ctx->stream));
+    m.xscs_t[0] = best[0]; m.xscs_t[1] = best[1]; m.xscs_t[2] = best[2];
+    m.xscs_r[0] = rx; m.xscs_r[1] = ry; m.xscs_r[2] = rz;
+    m.xscs = true;
+    return true;
 }
 
 // Class of every row of [r0, r1): rows with the same (col - base[i], value bits) list share
@@ -306,16 +562,21 @@ bool build_scs(GpuCsr &m, const std::vector<int64_t> &rp, int64_t other_bytes) {
         }
     const int K = (int)offs.size();
     if (K == 0 || (double)K * (double)(r1 - r0) > 2.0 * (double)(rp[r1] - rp[r0])) return false;  // mostly padding
-    // short stencils stay on SELL-64: A_1 of the 256^3 cycle (33 offsets, 8-bit
-    // codes) ran 47 vs 44 us here; A_2 (179 offsets, 16-bit codes) 31-46 vs 55 us
-    if (K < SCS_KMIN) return false;
+    // on a grid the x-staged kernel may take the operator (checked below);
+    // otherwise short stencils stay on SELL-64: A_1 of the 256^3 cycle (33
+    // offsets, 8-bit codes) ran 47 vs 44 us here; A_2 (179 offsets, 16-bit
+    // codes) 31-46 vs 55 us
+    const bool on_grid = seg < 0 && grid_applies(m);
+    if (K < (on_grid ? 8 : SCS_KMIN)) return false;
     // operators with a <= 256-entry value table keep SELL-64, whose codes decode
     // from an LDS table: A_1 of the 27-pt cycle (125 offsets, 8-bit codes) ran
     // 135 vs 121 us here (two dictionary loads per step per row pair)
+    bool small_table = false;
     {
         std::vector<unsigned long long> tab;
         const int vb = csr_value_table(m, tab);
-        if (vb == 4 || vb == 8) return false;
+        small_table = vb == 4 || vb == 8;
+        if (small_table && !on_grid) return false;
     }
     std::vector<double> val(m.nnz);
     FAMG_CHECK_HIP(hipMemcpyAsync(val.data(), m.val.get(), m.nnz * sizeof(double), hipMemcpyDeviceToHost, st));
@@ -330,10 +591,15 @@ bool build_scs(GpuCsr &m, const std::vector<int64_t> &rp, int64_t other_bytes) {
     const int ib = C <= 256 ? 1 : 2;
     const int64_t dict_bytes = (int64_t)Kp * C * 8;
     const int64_t stream = ib * (r1 - r0) + dict_bytes + 4 * Kp;
+    // x staged per grid tile when the offsets are grid steps within the grid
+    const bool xs3 = on_grid && dict_bytes <= (int64_t(256) << 20) && (double)stream <= 0.5 * (double)other_bytes &&
+                     xscs_setup(m, offs, Kp, rp, col, val);
+    if (!xs3 && (K < SCS_KMIN || small_table)) return false;
     // few long rows: one row per wave, the dictionary streamed (up to 256 MiB)
-    const bool lanes = r1 - r0 < SCS_LANES_ROWS && Kp >= 256;
-    if (lanes && !scs_lanes_enabled()) return false;
-    if (dict_bytes > (int64_t(lanes ? 256 : 16) << 20) || (double)stream > 0.5 * (double)other_bytes) return false;
+    const bool lanes = !xs3 && r1 - r0 < SCS_LANES_ROWS && Kp >= 256;
+    if (lanes && !scs_lanes_enabled()) { scs_release(m); return false; }
+    if (!xs3 && (dict_bytes > (int64_t(lanes ? 256 : 16) << 20) || (double)stream > 0.5 * (double)other_bytes))
+        return false;
     std::vector<double> dict((size_t)Kp * C, 0.0);
     for (int64_t c = 0; c < C; c++) {
         const int64_t i = rep[c];
@@ -366,11 +632,52 @@ bool build_scs(GpuCsr &m, const std::vector<int64_t> &rp, int64_t other_bytes) {
     return true;
 }
 
+static void spmv_xscs(const GpuCsr &m, const double *x, double *y, SpmvMode mode, const SpmvEpi &epi,
+                      hipStream_t s) {
+    XscsArgs a{};
+    a.cls = m.scs_cls.get();
+    a.dict = m.scs_dict.get();
+    a.lo = m.xscs_lo.get();
+    a.k = (int32_t)m.scs_k;
+    a.nx = (int)m.grid[0]; a.ny = (int)m.grid[1]; a.nz = (int)m.grid[2];
+    a.tx = m.xscs_t[0]; a.ty = m.xscs_t[1]; a.tz = m.xscs_t[2];
+    a.rx = m.xscs_r[0]; a.ry = m.xscs_r[1]; a.rz = m.xscs_r[2];
+    a.wx = a.tx + 2 * a.rx; a.wy = a.ty + 2 * a.ry; a.wz = a.tz + 2 * a.rz;
+    a.ntx = (int)ceil_div(a.nx, a.tx); a.nty = (int)ceil_div(a.ny, a.ty);
+    const int ntz = (int)ceil_div(a.nz, a.tz);
+    a.x = x; a.y = y; a.b = epi.b; a.d = epi.d; a.dc = epi.dc; a.dt = epi.dt;
+    const int T = a.tx * a.ty * a.tz;
+    const int rl = T <= 256 ? 1 : T <= 512 ? 2 : 4;
+    const size_t lds = (size_t)a.wx * a.wy * a.wz * sizeof(double);
+    const dim3 grid((unsigned)((int64_t)a.ntx * a.nty * ntz)), block(256);
+#define FAMG_XS3(M, IB)                                                                            \
+    if (rl == 1) spmv_xscs_kernel<M, IB, 1><<<grid, block, lds, s>>>(a);                           \
+    else if (rl == 2) spmv_xscs_kernel<M, IB, 2><<<grid, block, lds, s>>>(a);                      \
+    else spmv_xscs_kernel<M, IB, 4><<<grid, block, lds, s>>>(a);
+#define FAMG_XS3M(IB)                                                                              \
+    switch (mode) {                                                                                \
+    case SPMV_SET: FAMG_XS3(SPMV_SET, IB) break;                                                   \
+    case SPMV_ADD: FAMG_XS3(SPMV_ADD, IB) break;                                                   \
+    case SPMV_RESID: FAMG_XS3(SPMV_RESID, IB) break;                                               \
+    case SPMV_JACOBI: FAMG_XS3(SPMV_JACOBI, IB) break;                                             \
+    default: fail(AMG_ERR_UNSUPPORTED, "stencil-class storage: unsupported SpMV epilogue");        \
+    }
+    if (m.scs_ib == 1) { FAMG_XS3M(1) }
+    else { FAMG_XS3M(2) }
+#undef FAMG_XS3M
+#undef FAMG_XS3
+    FAMG_CHECK_HIP(hipGetLastError());
+}
+
 void spmv_scs(const GpuCsr &m, const double *x, double *y, SpmvMode mode, const SpmvEpi &epi, hipStream_t s,
               int64_t seg) {
     const int64_t r0 = seg < 0 ? 0 : m.seg_rows[seg];
     const int64_t r1 = seg < 0 ? m.nrows : m.seg_rows[seg + 1];
     if (r1 <= r0) return;
+    if (m.xscs && seg < 0) {
+        spmv_xscs(m, x, y, mode, epi, s);
+        return;
+    }
     ScsArgs a{m.scs_cls.get(), m.scs_dict.get(), m.scs_offs.get(), (int32_t)m.scs_k, (int32_t)m.scs_nclass,
               (int32_t)r0, (int32_t)r1, (int32_t)m.ncols, x, y, epi.b, epi.d, epi.dc, epi.dt};
     const dim3 grid((unsigned)ceil_div(r1 - r0, m.scs_lanes ? 4 : 512)), block(256);

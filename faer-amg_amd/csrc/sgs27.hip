@@ -40,8 +40,8 @@ struct Sgs27Args {
     int ntab;
     int nx, ny, nz;
     int pz;     // plane parity of this phase
-    int nst;    // in-plane colours applied, in order
-    int px[4], py[4];
+    int nst;    // in-plane colours applied, in order (<= 8)
+    int px[8], py[8];
     const double *S;  // this parity's values before the phase
     const double *O;  // the other parity's values (read-only in the phase)
     double *T;        // this parity's values after the phase
@@ -54,6 +54,8 @@ struct Sgs27Args {
     double icoef[27];      // the interior row's coefficients (table values of icode)
     double idinv;          // 1 / icoef[13]
     const double *zero;    // >= nx zeros (rows outside the grid)
+    const double *cpy_src; // optional: the tile's rows of plane z + 1 copied from cpy_src to cpy_dst
+    double *cpy_dst;
 };
 
 
@@ -80,7 +82,7 @@ typedef uint32_t sgs_u32x4_t __attribute__((ext_vector_type(4)));
 // an x operand of 0.0 on both paths; the product (+-0.0) added to an
 // accumulator that starts at +0.0 and can never become -0.0 leaves it
 // unchanged, so the sums are bitwise the same.
-template <int VB, int CW, int PX, int U>
+template <int VB, int CW, int PX, int U, int NW>
 __device__ __forceinline__ void sgs27_stage(const Sgs27Args &a, double *lds, const double *stab, const double *scoef,
                                             int z, int r0, int ys0, int ys1, int py, bool first_zero) {
     constexpr uint32_t MASK = (1u << VB) - 1;
@@ -94,7 +96,7 @@ __device__ __forceinline__ void sgs27_stage(const Sgs27Args &a, double *lds, con
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
     const bool zlo = z == 0, zhi = z == nz - 1;
-    for (int t0 = wave; t0 < ntask; t0 += 4 * U) {
+    for (int t0 = wave; t0 < ntask; t0 += NW * U) {
         double w[U][9][3];
         uint32_t cw[U][CW];
         double br[U];
@@ -102,11 +104,11 @@ __device__ __forceinline__ void sgs27_stage(const Sgs27Args &a, double *lds, con
         bool live[U], inter = true;
 #pragma unroll
         for (int u = 0; u < U; u++) {
-            const int t = min(t0 + 4 * u, ntask - 1);  // wave-uniform
+            const int t = min(t0 + NW * u, ntask - 1);  // wave-uniform
             const int yr = t / nseg, sg = t - yr * nseg;
             const int y = yfirst + 2 * yr;
             const int k = (sg << 6) + lane;
-            live[u] = t0 + 4 * u < ntask && k < nk;
+            live[u] = t0 + NW * u < ntask && k < nk;
             const int x = PX + 2 * min(k, nk - 1);
             const bool lo = PX == 0 && x == 0, hi = PX == 1 && x == nx - 1;
             // pair offsets: A = [x-2+PX, x-1+PX], B = A + 2 (clamped into the row at the edges)
@@ -180,8 +182,9 @@ __device__ __forceinline__ void sgs27_stage(const Sgs27Args &a, double *lds, con
     }
 }
 
-template <int VB, int CW, int U>
-__global__ __launch_bounds__(256) void k_sgs27_phase(Sgs27Args a) {
+template <int VB, int CW, int U, int NW>
+__global__ __launch_bounds__(64 * NW) void k_sgs27_phase(Sgs27Args a) {
+    constexpr int NT = 64 * NW;
     extern __shared__ sgs_dbl2_t lds_pairs[];  // 16-B aligned: rows are read as pairs
     double *lds = reinterpret_cast<double *>(lds_pairs);  // row 0: zeros; row 1 + (y - r0): grid row y
     __shared__ double stab[VB == 4 ? 16 : 256];
@@ -196,25 +199,25 @@ __global__ __launch_bounds__(256) void k_sgs27_phase(Sgs27Args a) {
     const int y0 = tile * a.ty, y1 = min(y0 + a.ty, ny);
     const int r0 = max(y0 - a.nst, 0), r1 = min(y1 + a.nst, ny);
     const int64_t zoff = (int64_t)z * nx * ny;
-    for (int q = tid; q < a.ntab; q += 256) stab[q] = a.vtab[q];
+    for (int q = tid; q < a.ntab; q += NT) stab[q] = a.vtab[q];
     const int nx2 = nx / 2;
     const int nload2 = (r1 - r0) * nx2;  // nx even: whole rows of 16-B pairs
     sgs_dbl2_t *l2 = reinterpret_cast<sgs_dbl2_t *>(lds);
-    for (int q = tid; q < nx2; q += 256) l2[q] = sgs_dbl2_t{0.0, 0.0};
+    for (int q = tid; q < nx2; q += NT) l2[q] = sgs_dbl2_t{0.0, 0.0};
     if (a.own_zero) {
-        for (int q = tid; q < nload2; q += 256) l2[nx2 + q] = sgs_dbl2_t{0.0, 0.0};
+        for (int q = tid; q < nload2; q += NT) l2[nx2 + q] = sgs_dbl2_t{0.0, 0.0};
     } else {
         // all of a lane's loads issued before its LDS writes (a load-wait-write
         // loop serialises ~13 memory latencies per workgroup)
         const sgs_dbl2_t *src = reinterpret_cast<const sgs_dbl2_t *>(a.S + zoff + (int64_t)r0 * nx);
         constexpr int PF = 8;
-        for (int q0 = tid; q0 < nload2; q0 += 256 * PF) {
+        for (int q0 = tid; q0 < nload2; q0 += NT * PF) {
             sgs_dbl2_t v[PF];
 #pragma unroll
-            for (int u = 0; u < PF; u++) v[u] = src[min(q0 + 256 * u, nload2 - 1)];
+            for (int u = 0; u < PF; u++) v[u] = src[min(q0 + NT * u, nload2 - 1)];
 #pragma unroll
             for (int u = 0; u < PF; u++)
-                if (q0 + 256 * u < nload2) l2[nx2 + q0 + 256 * u] = v[u];
+                if (q0 + NT * u < nload2) l2[nx2 + q0 + NT * u] = v[u];
         }
     }
     __syncthreads();
@@ -222,19 +225,26 @@ __global__ __launch_bounds__(256) void k_sgs27_phase(Sgs27Args a) {
         const int h = a.nst - 1 - s;
         const int ys0 = max(y0 - h, 0), ys1 = min(y1 + h, ny);
         const bool first_zero = a.own_zero && a.other_zero && s == 0;
-        if (a.px[s] == 0) sgs27_stage<VB, CW, 0, U>(a, lds, stab, scoef, z, r0, ys0, ys1, a.py[s], first_zero);
-        else sgs27_stage<VB, CW, 1, U>(a, lds, stab, scoef, z, r0, ys0, ys1, a.py[s], first_zero);
+        if (a.px[s] == 0) sgs27_stage<VB, CW, 0, U, NW>(a, lds, stab, scoef, z, r0, ys0, ys1, a.py[s], first_zero);
+        else sgs27_stage<VB, CW, 1, U, NW>(a, lds, stab, scoef, z, r0, ys0, ys1, a.py[s], first_zero);
         __syncthreads();
     }
     sgs_dbl2_t *dst = reinterpret_cast<sgs_dbl2_t *>(a.T + zoff + (int64_t)y0 * nx);
     const sgs_dbl2_t *srcl = reinterpret_cast<const sgs_dbl2_t *>(lds + (y0 - r0 + 1) * nx);
-    for (int q = tid; q < (y1 - y0) * nx2; q += 256) dst[q] = srcl[q];
+    for (int q = tid; q < (y1 - y0) * nx2; q += NT) dst[q] = srcl[q];
+    if (a.cpy_src && z + 1 < a.nz) {  // plane z + 1 (the other parity) carried to the next phase's source
+        const int64_t o = zoff + (int64_t)nx * ny + (int64_t)y0 * nx;
+        const sgs_dbl2_t *cs = reinterpret_cast<const sgs_dbl2_t *>(a.cpy_src + o);
+        sgs_dbl2_t *cd = reinterpret_cast<sgs_dbl2_t *>(a.cpy_dst + o);
+        for (int q = tid; q < (y1 - y0) * nx2; q += NT) cd[q] = cs[q];
+    }
 }
 
-// FAMG_SGS_FUSED=0 (or amg_set_sgs_fused(0)): colour launches instead of the fused phases
+// FAMG_SGS_FUSED=0 (or amg_set_sgs_fused(0)): colour launches instead of the
+// fused phases; 2: four phases per step instead of three (A/B, tests)
 int g_sgs_fused = [] {
     const char *e = getenv("FAMG_SGS_FUSED");
-    return (e && e[0] == '0') ? 0 : 1;
+    return (e && e[0] == '0') ? 0 : (e && e[0] == '2') ? 2 : 1;
 }();
 static bool sgs_fused_enabled() { return g_sgs_fused != 0; }
 
@@ -255,6 +265,16 @@ static int sgs27_u() {
     }();
     return v;
 }
+// waves per workgroup (FAMG_SGS27_NW: 4 or 8)
+static int sgs27_nw() {
+    static const int v = [] {
+        const char *e = getenv("FAMG_SGS27_NW");
+        return (e && e[0] == '8') ? 8 : 4;
+    }();
+    return v;
+}
+// odd planes' forward and backward colours in one phase (g_sgs_fused == 2: two)
+static int sgs27_p23() { return g_sgs_fused != 2; }
 constexpr int SGS27_MAX_NX = 512;  // LDS: (TY + 8) rows of nx doubles (TY = 16: 96 KB at nx = 512)
 
 __global__ void k_sgs27_check(const uint32_t *codes, int cw, int vb, int zcode, int nx, int ny, int nz,
@@ -357,10 +377,11 @@ void sgs27_setup(SgsOp &S) {
     S.fused27 = true;
 }
 
-// One phase: the planes of parity pz run the in-plane colours (px, py)[0..nst).
+// One phase: the planes of parity pz run the in-plane colours (px, py)[0..nst);
+// cpy_src/cpy_dst (optional): each workgroup also copies its rows of plane z + 1.
 static void sgs27_phase(const SgsOp &S, int pz, int nst, const int *px, const int *py, const double *src,
                         const double *other, double *dst, const double *b, bool own_zero, bool other_zero,
-                        hipStream_t s) {
+                        hipStream_t s, const double *cpy_src = nullptr, double *cpy_dst = nullptr) {
     const GpuCsr &m = S.A->m;
     const int nplanes = (S.nz27 - pz + 1) / 2;
     if (nplanes <= 0) return;
@@ -383,7 +404,8 @@ static void sgs27_phase(const SgsOp &S, int pz, int nst, const int *px, const in
     a.b = b;
     a.own_zero = own_zero;
     a.other_zero = other_zero;
-
+    a.cpy_src = cpy_src;
+    a.cpy_dst = cpy_dst;
     a.ty = sgs27_ty();
     for (int q = 0; q < 8; q++) a.icode[q] = S.icode27[q];
     for (int f = 0; f < 6; f++)
@@ -393,26 +415,31 @@ static void sgs27_phase(const SgsOp &S, int pz, int nst, const int *px, const in
     a.zero = S.fused_zero.get();
     a.ntiles = (int)ceil_div(S.ny27, a.ty);
     const int64_t rows = (int64_t)nplanes * S.ny27 * S.nx27;
-    // algorithmic bytes: the parity's x read + written, its codes and b, the
-    // other parity's x read once
+    // algorithmic bytes: the parity's x read (unless zero) + written, its codes
+    // and b, the other parity's x read once (unless zero), the copied planes
     if (g_launch_log)
         log_launch("sgs27_phase", SPMV_KERNEL_DIA, SPMV_SGS, rows,
-                   rows * (16 + 4 * (int64_t)m.dia_cw + 8) + (other_zero ? 0 : (int64_t)(m.nrows - rows) * 8));
-    const dim3 grid((unsigned)(nplanes * a.ntiles)), block(256);
+                   rows * (8 + 4 * (int64_t)m.dia_cw + 8) + (own_zero ? 0 : rows * 8) +
+                       (other_zero ? 0 : (int64_t)(m.nrows - rows) * 8) +
+                       (cpy_src ? (int64_t)(m.nrows - rows) * 16 : 0));
+    const dim3 grid((unsigned)(nplanes * a.ntiles));
     const size_t lds = (size_t)(a.ty + 2 * nst + 1) * S.nx27 * sizeof(double);
     const bool u2 = sgs27_u() == 2;
+    const int nw = sgs27_nw();
+#define FAMG_SGS27_LAUNCH(VB, CW, U, NW) k_sgs27_phase<VB, CW, U, NW><<<grid, dim3(64 * NW), lds, s>>>(a)
     if (m.dia_vbits == 4) {
-        if (u2) k_sgs27_phase<4, 4, 2><<<grid, block, lds, s>>>(a);
-        else k_sgs27_phase<4, 4, 1><<<grid, block, lds, s>>>(a);
+        if (nw == 8) { if (u2) FAMG_SGS27_LAUNCH(4, 4, 2, 8); else FAMG_SGS27_LAUNCH(4, 4, 1, 8); }
+        else { if (u2) FAMG_SGS27_LAUNCH(4, 4, 2, 4); else FAMG_SGS27_LAUNCH(4, 4, 1, 4); }
     } else {
-        if (u2) k_sgs27_phase<8, 8, 2><<<grid, block, lds, s>>>(a);
-        else k_sgs27_phase<8, 8, 1><<<grid, block, lds, s>>>(a);
+        if (nw == 8) { if (u2) FAMG_SGS27_LAUNCH(8, 8, 2, 8); else FAMG_SGS27_LAUNCH(8, 8, 1, 8); }
+        else { if (u2) FAMG_SGS27_LAUNCH(8, 8, 2, 4); else FAMG_SGS27_LAUNCH(8, 8, 1, 4); }
     }
+#undef FAMG_SGS27_LAUNCH
     FAMG_CHECK_HIP(hipGetLastError());
 }
 
-// x <- SGS step (forward colours 0..7, backward 6..0) as four phases; zero:
-// x starts at 0 (sweep from e = 0: nothing of x is read).
+// x <- SGS step (forward colours 0..7, backward 6..0) as plane-parity phases;
+// zero: x starts at 0 (sweep from e = 0: nothing of x is read).
 bool sgs27_applies(const SgsOp &S, const double *x, const double *b) {
     return S.fused27 && ((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(b)) & 15) == 0;
 }
@@ -423,6 +450,16 @@ void sgs27_sweep(SgsOp &S, double *x, const double *b, bool zero) {
     static const int fpx[4] = {0, 1, 0, 1}, fpy[4] = {0, 0, 1, 1};  // colours 0,1,2,3 / 4,5,6,7
     static const int bopx[3] = {0, 1, 0}, bopy[3] = {1, 0, 0};       // colours 6,5,4
     static const int bepx[4] = {1, 0, 1, 0}, bepy[4] = {1, 1, 0, 0}; // colours 3,2,1,0
+    static const int opx[7] = {0, 1, 0, 1, 0, 1, 0}, opy[7] = {0, 0, 1, 1, 1, 0, 0};  // 4,5,6,7,6,5,4
+    if (sgs27_p23() && (size_t)(sgs27_ty() + 15) * S.nx27 * sizeof(double) <= 150 * 1024) {
+        // three phases: the odd planes run forward and backward colours in one
+        // launch; reading its source from t1 and writing x, it needs the odd
+        // planes' old values in t1 -- the even phase copies them (none when zero)
+        sgs27_phase(S, 0, 4, fpx, fpy, x, x, t1, b, zero, zero, s, zero ? nullptr : x, zero ? nullptr : t1);
+        sgs27_phase(S, 1, 7, opx, opy, t1, t1, x, b, zero, false, s);   // odd planes -> x
+        sgs27_phase(S, 0, 4, bepx, bepy, t1, x, x, b, false, false, s); // even planes -> x
+        return;
+    }
     sgs27_phase(S, 0, 4, fpx, fpy, x, x, t1, b, zero, zero, s);      // even planes -> t1
     sgs27_phase(S, 1, 4, fpx, fpy, x, t1, t1, b, zero, false, s);    // odd planes -> t1
     sgs27_phase(S, 1, 3, bopx, bopy, t1, t1, x, b, false, false, s); // odd planes -> x

@@ -60,6 +60,9 @@ SIGNATURES = {
     "amg_csr_download": (i32, [vp, vp, vp, vp]),
     "amg_csr_dia_range": (i32, [vp, vp]),
     "amg_csr_class_info": (i32, [vp, vp]),
+    "amg_csr_set_grid": (i32, [vp, i64, i64, i64]),
+    "amg_csr_spmv_epilogue": (i32, [vp, i32, vp, vp, vp, vp]),
+    "amg_csr_grid_info": (i32, [vp, vp]),
     "amg_gen_laplace3d_7pt": (i32, [vp, i64, i64, i64, P(vp)]),
     "amg_gen_aniso27": (i32, [vp, i64, i64, i64, dbl, dbl, dbl, P(vp)]),
     "amg_gen_random_7pt": (i32, [vp, i64, i64, i64, C.c_uint64, i64, P(vp)]),
@@ -435,7 +438,24 @@ class SparseMatOp(LinOp):
         ci = np.zeros(4, np.int64)
         _ck(_lib.amg_csr_class_info(self.h, ci.ctypes.data_as(vp)))
         d["classes"], d["class_offsets"], d["class_id_bits"] = int(ci[0]), int(ci[1]), int(ci[2])
+        g = np.zeros(12, np.int64)
+        _ck(_lib.amg_csr_grid_info(self.h, g.ctypes.data_as(vp)))
+        d["grid"] = tuple(int(v) for v in g[:3])
+        d["xstaged"] = bool(g[3])
+        if d["xstaged"]:
+            d["tile"], d["halo"] = tuple(int(v) for v in g[4:7]), tuple(int(v) for v in g[7:10])
         return d
+
+    def spmv_epilogue(self, mode, x, y, b=None, d=None):
+        """amg_csr_spmv_epilogue on device tensors: mode "set" y = A x, "add" y += A x,
+        "resid" y = b - A x, "jacobi" y = x + d (b - A x)."""
+        m = {"set": 0, "add": 1, "resid": 2, "jacobi": 3}[mode]
+        ptr = lambda t: None if t is None else vp(t.data_ptr())  # noqa: E731
+        _ck(_lib.amg_csr_spmv_epilogue(self.h, m, ptr(x), ptr(y), ptr(b), ptr(d)))
+
+    def set_grid(self, nx, ny, nz):
+        """Grid hint (amg_csr_set_grid): the rows are an nx x ny x nz grid; re-finalizes the storage."""
+        _ck(_lib.amg_csr_set_grid(self.h, nx, ny, nz))
 
     def arrays(self):
         m, n = self.dims()
@@ -511,8 +531,9 @@ def sgs_info(S):
 
 
 def set_sgs_fused(enable):
-    """SGS smoothers built afterwards use the fused plane-parity phases where they apply."""
-    _ck(_lib.amg_set_sgs_fused(1 if enable else 0))
+    """SGS smoothers built afterwards use the fused plane-parity phases where they
+    apply (True / 1: three phases per step, 2: four phases, False / 0: colour launches)."""
+    _ck(_lib.amg_set_sgs_fused(int(enable)))
 
 
 def sgs_fused(S):

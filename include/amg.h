@@ -114,6 +114,24 @@ amg_status amg_set_alloc_policy(int32_t policy);
  * to 8), class-id bits, dictionary bytes}; zeros when the operator uses another
  * storage. */
 amg_status amg_csr_class_info(const amg_linop *op, int64_t *info4);
+/* Grid hint (no reference counterpart: the reference's SparseMatOp has no
+ * geometry): the rows of the square operator are the points of an nx x ny x nz
+ * grid, x fastest.  Stencil-class operators whose nonzero offsets are grid steps
+ * that stay inside the grid then run x-staged per grid tile (scs.hip,
+ * bitwise the same sums).  Re-finalizes the SpMV storage: call before the
+ * operator is used (graphs captured earlier would read released storage).  The
+ * stencil generators and amg_sa_build_box set it for the levels they make;
+ * 0,0,0 clears it. */
+amg_status amg_csr_set_grid(amg_linop *op, int64_t nx, int64_t ny, int64_t nz);
+/* The fused SpMV epilogues the V-cycle runs (multigrid.rs:337-369, 407-424),
+ * on device vectors, asynchronous on the context stream: mode 0 y = A x, 1
+ * y += A x, 2 y = b - A x, 3 y = x + d (b - A x) (weighted Jacobi step; d the
+ * scaled inverse diagonal).  x != y. */
+amg_status amg_csr_spmv_epilogue(const amg_linop *op, int32_t mode, const double *x, double *y,
+                                 const double *b, const double *d);
+/* info12 = {nx, ny, nz (0: no hint), x-staged (0/1), tile tx, ty, tz, halo
+ * rx, ry, rz, 0, 0}. */
+amg_status amg_csr_grid_info(const amg_linop *op, int64_t *info12);
 
 /* Copy a host CSR with usize-compatible (int64) row pointers and column indices
  * and fp64 values to the device.  Columns must be sorted ascending within each
@@ -208,10 +226,11 @@ amg_status amg_diag_create(amg_ctx *ctx, int64_t n, const double *d, amg_linop *
  * colors: host array of nrows colors in [0, ncolors) or NULL for greedy
  * first-fit coloring in row order. */
 amg_status amg_sgs_create(const amg_linop *A, const int32_t *colors, amg_linop **out);
-/* SGS smoothers built after the call run their sweeps as four fused
- * plane-parity phases (sgs27.hip) where that applies -- a 27-point grid operator
- * stored as DIA codes with the parity colouring -- instead of one launch per
- * colour (default 1; FAMG_SGS_FUSED=0 sets 0).  Bitwise the same results. */
+/* SGS smoothers built after the call run their sweeps as fused plane-parity
+ * phases (sgs27.hip) where that applies -- a 27-point grid operator stored as
+ * DIA codes with the parity colouring -- instead of one launch per colour:
+ * enable 1 (default) three phases per SGS step, 2 four phases, 0 colour
+ * launches (FAMG_SGS_FUSED=0/2 sets the default).  Bitwise the same results. */
 amg_status amg_set_sgs_fused(int32_t enable);
 /* *fused = 1 if this SGS smoother runs the fused phases. */
 amg_status amg_sgs_fused(const amg_linop *op, int32_t *fused);

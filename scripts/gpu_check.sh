@@ -45,6 +45,9 @@ for s in "$@"; do
               step profpel 600 rocprofv3 --kernel-trace --stats -d "$R/gpurun_out/profpel" -o run \
                   --output-format csv -- python3 "$R/bench.py" --problem elast --steps 20 --warmup 3 --no-cpu-baseline \
                   --plan-out "$R/gpurun_out/plan_c5.json" ;;
+        ptk) step ptk 600 python -u -m pytest tests -m gpu -v --timeout 120 --timeout-method thread -k "$PTK" ;;
+        absgs) step absgs 900 bash scripts/ab_sgs27.sh ;;
+        bench27g) step bench27g 600 python bench.py --problem 27pt --smoother sgs --steps 10 --warmup 2 --no-cpu-baseline --no-general ;;
         smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
         bench) step bench 600 python bench.py --steps 20 --warmup 3 ;;
         benchq) step bench 400 python bench.py --steps 20 --warmup 3 --no-cpu-baseline --ab ;;

@@ -1114,6 +1114,59 @@ def test_stencil_classes(ctx):
     assert np.linalg.norm(z - zref) <= 1e-11 * np.linalg.norm(zref)
 
 
+def _epilogues_bitwise(ctx, M, seed):
+    """The four SpMV epilogues of M (amg_csr_spmv_epilogue) against the oracle's
+    row sums: y = A x, y += A x, y = b - A x, y = x + d (b - A x), bitwise."""
+    OM = O.Csr.from_arrays(*M.dims(), *M.arrays())
+    rng = np.random.default_rng(seed)
+    m, n = M.dims()
+    x, y0, b, d = rng.standard_normal(n), rng.standard_normal(m), rng.standard_normal(m), rng.uniform(0.1, 1, m)
+    ax = OM.spmv(x)
+    want = {"set": ax, "add": y0 + ax, "resid": b - ax, "jacobi": x + d * (b - ax)}
+    for mode, ref in want.items():
+        yd = T(y0)
+        M.spmv_epilogue(mode, T(x), yd, T(b), T(d))
+        assert np.array_equal(H(yd), ref), (mode, M.spmv_info())
+
+
+def test_xstaged_stencil_classes(ctx):
+    """x-staged stencil classes (scs.hip spmv_xscs_kernel): the coarse operators
+    of box hierarchies on a grid (7-pt 128^3: A_2 = 32^3 with 13^3 classes and
+    A_3; 27-pt 64^3: A_1 = 32^3 with 125 offsets and 8-bit values) carry the
+    grid hint and run one workgroup per grid tile with the tile's x window in
+    LDS.  All four SpMV epilogues bitwise equal to the oracle's row sums; a
+    wrong grid hint (nonzeros that would leave the grid) is refused and the
+    storage falls back; the V-cycle within 1e-11 of the oracle."""
+    seen = 0
+    for gen, dims, smoother in (("laplace3d_7pt", (128, 128, 128), "jacobi"), ("aniso27", (64, 64, 64), "jacobi")):
+        A = (fa().SparseMatOp.laplace3d_7pt(ctx, *dims) if gen == "laplace3d_7pt"
+             else fa().SparseMatOp.aniso27(ctx, *dims, 1.0, 1.0, 0.01))
+        mg = fa().sa_build_box(A, dims, (2, 2, 2), coarsest_dim=100)
+        for l in range(1, mg.levels() - 1):
+            Al = mg.level(l)[0]
+            info = Al.spmv_info()
+            g = tuple(-(-d // 2 ** l) for d in dims)
+            assert info["grid"] == g, (l, info)
+            if info["xstaged"]:
+                seen += 1
+                _epilogues_bitwise(ctx, Al, 100 + l)
+        b = np.random.default_rng(42).uniform(-1, 1, A.nrows)
+        zref = O.Multigrid(oracle_levels_from_gpu(mg, smoother)).apply(b)
+        z = apply_dev(ctx, mg, b, A.nrows)
+        assert np.linalg.norm(z - zref) <= 1e-11 * np.linalg.norm(zref)
+    assert seen >= 3, seen
+    # a grid hint the operator does not fit (nonzeros leave the grid): refused
+    A = fa().SparseMatOp.laplace3d_7pt(ctx, 64, 64, 64)
+    mg = fa().sa_build_box(A, (64, 64, 64), (2, 2, 2), coarsest_dim=100)
+    A1 = mg.level(2)[0]  # 16^3
+    assert A1.spmv_info()["xstaged"]
+    A1.set_grid(8, 32, 16)
+    assert not A1.spmv_info()["xstaged"]
+    _epilogues_bitwise(ctx, A1, 7) if A1.spmv_info()["kernel"] != "classes" else None
+    A1.set_grid(0, 0, 0)
+    assert A1.spmv_info()["grid"] == (0, 0, 0) and not A1.spmv_info()["xstaged"]
+
+
 def test_cycle_plan_accounts_for_every_launch(ctx):
     """amg_multigrid_cycle_plan: the launches of one V-cycle as the library makes
     them.  On the 7-pt box hierarchy the fine level folds its zero-guess step
@@ -1177,11 +1230,12 @@ def test_cycle_plan_sgs_counts_colour_launches(ctx):
 
 @pytest.mark.parametrize("dims", [(48, 48, 32), (50, 45, 37), (64, 40, 33)])
 def test_sgs27_fused_phases_bitwise(ctx, dims):
-    """The fused plane-parity SGS phases (sgs27.hip: four launches per SGS step,
-    in-plane colours on shrinking LDS halos) against the colour launches
-    (fifteen per step): bitwise equal for the step from e = 0 (the smoother's
-    apply) and inside the V-cycle (pre-smoothing from zero, post-smoothing on
-    x), odd and even extents; and within 1e-11 of the oracle's V-cycle."""
+    """The fused plane-parity SGS phases (sgs27.hip: three launches per SGS step
+    -- the odd planes' forward and backward colours in one -- or four, in-plane
+    colours on shrinking LDS halos) against the colour launches (fifteen per
+    step): bitwise equal for the step from e = 0 (the smoother's apply) and
+    inside the V-cycle (pre-smoothing from zero, post-smoothing on x), odd and
+    even extents; and within 1e-11 of the oracle's V-cycle."""
     OA = O.aniso27(*dims)
     A = fa().SparseMatOp.aniso27(ctx, *dims, 1.0, 1.0, 0.01)
     if A.spmv_info()["kernel"] != "dia":
@@ -1191,6 +1245,14 @@ def test_sgs27_fused_phases_bitwise(ctx, dims):
     try:
         S0 = fa().SymGaussSeidel(A)
         mg0 = fa().sa_build_box(A, dims, (2, 2, 2), coarsest_dim=500, smoother="sgs")
+        fa().set_sgs_fused(2)
+        S2 = fa().SymGaussSeidel(A)
+        mg2 = fa().sa_build_box(A, dims, (2, 2, 2), coarsest_dim=500, smoother="sgs")
+        r2 = np.random.default_rng(8).standard_normal(OA.nrows)
+        e2 = apply_dev(ctx, S2, r2, OA.nrows)
+        b2 = np.random.default_rng(9).uniform(-1, 1, OA.nrows)
+        z2 = apply_dev(ctx, mg2, b2, OA.nrows)
+        plan2 = mg2.cycle_plan()
     finally:
         fa().set_sgs_fused(True)
     mg1 = fa().sa_build_box(A, dims, (2, 2, 2), coarsest_dim=500, smoother="sgs")
@@ -1204,10 +1266,12 @@ def test_sgs27_fused_phases_bitwise(ctx, dims):
     z1 = apply_dev(ctx, mg1, b, OA.nrows)
     z0 = apply_dev(ctx, mg0, b, OA.nrows)
     assert np.array_equal(z1, z0)
+    assert np.array_equal(e2, e0) and np.array_equal(z2, z0)
     zref = O.Multigrid(oracle_levels_from_gpu(mg1, "sgs")).apply(b)
     assert np.linalg.norm(z1 - zref) <= 1e-11 * np.linalg.norm(zref)
     plan = mg1.cycle_plan()
-    assert sum(1 for p in plan if p["name"] == "sgs27_phase") == 8  # two SGS steps x four phases
+    assert sum(1 for p in plan if p["name"] == "sgs27_phase") == 6  # two SGS steps x three phases
+    assert sum(1 for p in plan2 if p["name"] == "sgs27_phase") == 8  # two SGS steps x four phases
 
 
 def _spmm_vs_spmv(ctx, A, ks=(1, 3, 8, 32), seed=0):
