@@ -651,6 +651,7 @@ amg_status amg_multigrid_set_option(amg_linop *mg, int32_t option, int64_t value
         case 0: m->use_graph = value != 0; break;
         case 1: m->sgs_residual_form = value != 0; break;
         case 2: m->fold_zero_guess = value != 0; break;
+        case 3: m->fuse_transfers = value != 0; m->invalidate_graphs(); m->fuse_reset(); break;
         default: fail(AMG_ERR_INVALID, "unknown multigrid option");
         }
         m->invalidate_graphs();

@@ -366,10 +366,13 @@ struct CoarseCholOp : LinOp {
     void apply(double *out, const double *rhs) override;
 };
 
+struct TransferFuse;  // fuse.hip
 struct MgLevel {
     LinOpPtr A, S, R, P;  // R, P: transfer to the next-coarser level (null on the coarsest)
     // device workspaces (allocated lazily at first apply)
     DevBuf<double> v, f, t, r;
+    // fused residual->restriction and interpolation->Jacobi launches (fuse.hip)
+    std::shared_ptr<TransferFuse> fuse;
 };
 
 struct MultigridOp : LinOp {
@@ -380,6 +383,9 @@ struct MultigridOp : LinOp {
     // s = 1 Jacobi levels: fold the first smoothing step from v = 0 (v = d*f)
     // into the residual (RESID0) and the correction (ADD0) instead of storing it
     bool fold_zero_guess = true;
+    // grid levels: residual + restriction and interpolation + post-smoothing
+    // Jacobi as one launch each (fuse.hip)
+    bool fuse_transfers = true;
     std::mutex mtx;
     Kind kind() const override { return Kind::Multigrid; }
     bool is_precond() const override { return true; }
@@ -387,6 +393,7 @@ struct MultigridOp : LinOp {
     void add_level(LinOpPtr A, LinOpPtr S, LinOpPtr R, LinOpPtr P);
     void ensure_workspace();
     void invalidate_graphs();
+    void fuse_reset() { fuse_ready_ = false; }  // fused transfers re-decided at the next apply
     ~MultigridOp() override;
 
     // V-cycle building blocks (also used by the distributed multigrid)
@@ -403,7 +410,18 @@ struct MultigridOp : LinOp {
     };
     std::vector<GraphEntry> graphs_;
     bool workspace_ready_ = false;
+    bool fuse_ready_ = false;
 };
+
+// fused grid transfers (fuse.hip); FAMG_FUSE=0 disables them process-wide
+extern int g_fuse_transfers;
+void fuse_setup(MultigridOp &mg, size_t l);
+bool fuse_has_pre(const MgLevel &L);
+bool fuse_has_post(const MgLevel &L);
+void fuse_resid_restrict(const TransferFuse &F, const GpuCsr &m, const double *f, const double *x,
+                         const DiagOp *D, double *fc, hipStream_t s);
+void fuse_interp_jacobi(const TransferFuse &F, const GpuCsr &m, const double *vc, const double *f, const double *x,
+                        const DiagOp &D, double *out, hipStream_t s);
 
 // ---------------------------------------------------------------- factories
 

@@ -591,6 +591,11 @@ class Multigrid(LinOp):
         """Fold the zero-guess Jacobi step into the residual/correction SpMVs (default on)."""
         _ck(_lib.amg_multigrid_set_option(self.h, 2, 1 if enable else 0))
 
+    def set_fuse_transfers(self, enable):
+        """Grid levels: residual + restriction and interpolation + post-smoothing Jacobi
+        as one launch each (fuse.hip; default on, FAMG_FUSE=0 disables process-wide)."""
+        _ck(_lib.amg_multigrid_set_option(self.h, 3, 1 if enable else 0))
+
     def levels(self):
         v = i64()
         _ck(_lib.amg_multigrid_levels(self.h, C.byref(v)))

@@ -265,7 +265,13 @@ amg_status amg_multigrid_set_graph(amg_linop *mg, int32_t enable);
  * and correction SpMVs instead of storing it (default 1; bitwise identical), on
  * levels whose operator is fp64 SELL with mostly short columns, x-staged SELL,
  * or DIA codes whose P runs the short-slice kernel; amg_multigrid_cycle_plan
- * reports which levels fold (RESID0 / ADD0 launches). */
+ * reports which levels fold (RESID0 / ADD0 launches); 3 = fused grid transfers
+ * (default 1; FAMG_FUSE=0 sets 0 process-wide): on a level whose operator is
+ * DIA codes on a grid (amg_csr_set_grid) with steps in {-1,0,1}^3 and whose
+ * next level is its 2x2x2-box grid, the residual and the restriction run as
+ * one launch (fuse_resid_restrict), and the interpolation with one Jacobi
+ * post-smoothing step as another (fuse_interp_jacobi); R and P are read as
+ * grid-transfer classes (8-bit class per row).  Bitwise identical. */
 amg_status amg_multigrid_set_option(amg_linop *mg, int32_t option, int64_t value);
 /* Multigrid::apply == amg_linop_apply on a multigrid handle. */
 amg_status amg_multigrid_apply(amg_linop *mg, double *out, int64_t ld_out, const double *rhs,

@@ -1167,6 +1167,42 @@ def test_xstaged_stencil_classes(ctx):
     assert A1.spmv_info()["grid"] == (0, 0, 0) and not A1.spmv_info()["xstaged"]
 
 
+@pytest.mark.parametrize("case", ["7pt-fold", "7pt-odd", "7pt-nofold", "7pt-s2", "27pt-sgs", "7pt-l1"])
+def test_fused_grid_transfers_bitwise(ctx, case):
+    """fuse.hip: on grid levels the residual + restriction and the interpolation
+    + post-smoothing Jacobi step run as one launch each, R/P read as
+    grid-transfer classes.  The V-cycle is bitwise equal to the unfused
+    launches: folded zero-guess step (RESID0/ADD0), odd extents (partial tiles
+    and boxes), fold off (x = v), two smoothing steps (restriction fused only),
+    27-point operator with SGS (restriction fused after the sweep), L1
+    smoother; and within 1e-11 of the oracle."""
+    dims = {"7pt-odd": (37, 29, 23), "27pt-sgs": (48, 40, 36)}.get(case, (64, 48, 40))
+    smoother = "sgs" if case == "27pt-sgs" else "l1" if case == "7pt-l1" else "jacobi"
+    A = (fa().SparseMatOp.aniso27(ctx, *dims, 1.0, 1.0, 0.01) if case == "27pt-sgs"
+         else fa().SparseMatOp.laplace3d_7pt(ctx, *dims))
+    mg = fa().sa_build_box(A, dims, (2, 2, 2), coarsest_dim=100, smoother=smoother)
+    if case == "7pt-nofold":
+        mg.set_fold_zero_guess(False)
+    if case == "7pt-s2":
+        mg.with_smoothing_steps(2)
+    b = np.random.default_rng(11).uniform(-1, 1, A.nrows)
+    plan = mg.cycle_plan()
+    names = [p["name"] for p in plan if p["level"] == 0]
+    assert "fuse_resid_restrict" in names, names
+    assert ("fuse_interp_jacobi" in names) == (case not in ("7pt-s2", "27pt-sgs")), names
+    z1 = apply_dev(ctx, mg, b, A.nrows)
+    mg.set_fuse_transfers(False)
+    names0 = [p["name"] for p in mg.cycle_plan() if p["level"] == 0]
+    assert not any(n.startswith("fuse_") for n in names0), names0
+    z0 = apply_dev(ctx, mg, b, A.nrows)
+    assert np.array_equal(z1, z0)
+    mg.set_fuse_transfers(True)
+    z2 = apply_dev(ctx, mg, b, A.nrows)
+    assert np.array_equal(z2, z0)
+    zref = O.Multigrid(oracle_levels_from_gpu(mg, smoother), mu=1, steps=2 if case == "7pt-s2" else 1).apply(b)
+    assert np.linalg.norm(z1 - zref) <= 1e-11 * np.linalg.norm(zref)
+
+
 def test_cycle_plan_accounts_for_every_launch(ctx):
     """amg_multigrid_cycle_plan: the launches of one V-cycle as the library makes
     them.  On the 7-pt box hierarchy the fine level folds its zero-guess step
