@@ -658,6 +658,29 @@ amg_status amg_multigrid_set_option(amg_linop *mg, int32_t option, int64_t value
     });
 }
 
+amg_status amg_multigrid_fused_transfer(amg_linop *mg, int64_t level, int32_t which, const double *a,
+                                       const double *b, const double *x, double *out, int32_t *applied) {
+    return guard([&] {
+        auto m = need_mg(mg);
+        FAMG_REQUIRE(applied, AMG_ERR_INVALID, "null output");
+        std::lock_guard<std::mutex> lk(m->mtx);
+        FAMG_REQUIRE(level >= 0 && level + 1 < (int64_t)m->levels.size(), AMG_ERR_INVALID, "level out of range");
+        m->ensure_workspace();
+        MgLevel &L = m->levels[level];
+        auto *A = dynamic_cast<CsrOp *>(L.A.get());
+        auto *D = dynamic_cast<DiagOp *>(L.S.get());
+        *applied = 0;
+        if (which == 0 && fuse_has_pre(L)) {
+            FAMG_REQUIRE(x || D, AMG_ERR_INVALID, "folded restriction needs a diagonal smoother");
+            fuse_resid_restrict(*L.fuse, A->m, a, x, D, out, m->ctx->stream);
+            *applied = 1;
+        } else if (which == 1 && fuse_has_post(L) && D) {
+            fuse_interp_jacobi(*L.fuse, A->m, a, b, x, *D, out, m->ctx->stream);
+            *applied = 1;
+        }
+    });
+}
+
 amg_status amg_multigrid_apply(amg_linop *mg, double *out, int64_t ld_out, const double *rhs,
                                int64_t ld_rhs, int64_t k, amg_mem mem) {
     return guard([&] {

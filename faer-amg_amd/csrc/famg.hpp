@@ -367,6 +367,8 @@ struct CoarseCholOp : LinOp {
 };
 
 struct TransferFuse;  // fuse.hip
+// default of MultigridOp::fuse_transfers (FAMG_FUSE=1: on)
+extern int g_fuse_transfers;
 struct MgLevel {
     LinOpPtr A, S, R, P;  // R, P: transfer to the next-coarser level (null on the coarsest)
     // device workspaces (allocated lazily at first apply)
@@ -385,7 +387,7 @@ struct MultigridOp : LinOp {
     bool fold_zero_guess = true;
     // grid levels: residual + restriction and interpolation + post-smoothing
     // Jacobi as one launch each (fuse.hip)
-    bool fuse_transfers = true;
+    bool fuse_transfers = g_fuse_transfers != 0;
     std::mutex mtx;
     Kind kind() const override { return Kind::Multigrid; }
     bool is_precond() const override { return true; }
@@ -413,8 +415,7 @@ struct MultigridOp : LinOp {
     bool fuse_ready_ = false;
 };
 
-// fused grid transfers (fuse.hip); FAMG_FUSE=0 disables them process-wide
-extern int g_fuse_transfers;
+// fused grid transfers (fuse.hip)
 void fuse_setup(MultigridOp &mg, size_t l);
 bool fuse_has_pre(const MgLevel &L);
 bool fuse_has_post(const MgLevel &L);

@@ -41,16 +41,19 @@
 
 namespace famg {
 
+// FAMG_FUSE=1 enables the fused transfers process-wide (default off: measured
+// slower than the separate launches so far)
 int g_fuse_transfers = [] {
     const char *e = getenv("FAMG_FUSE");
-    return (e && e[0] == '0') ? 0 : 1;
+    return (e && e[0] == '1') ? 1 : 0;
 }();
 
 struct TransferFuse {
     int fx = 0, fy = 0, fz = 0, cx = 0, cy = 0, cz = 0;
     int K = 0;
     int8_t adx[32] = {}, ady[32] = {}, adz[32] = {};
-    DevBuf<uint8_t> pcls, pslot, rcls, rslot;
+    DevBuf<uint8_t> pcls, rcls;
+    DevBuf<int16_t> poff, roff;  // per class entry: its position in the kernel's LDS layout (below)
     DevBuf<double> pval, rval;
     int pke = 0, rke = 0, pnc = 0, rnc = 0;
     bool pre = false, post = false;
@@ -64,6 +67,12 @@ constexpr int FR_XX = FR_RX + 2, FR_XY = FR_RY + 2;          // x-operand region
 constexpr int FI_TX = 32, FI_TY = 16;                       // fine tile of the interpolation
 constexpr int FI_VX = FI_TX + 2, FI_VY = FI_TY + 2;          // corrected-v region 34 x 18
 constexpr int FI_WX = FI_TX / 2 + 4, FI_WY = FI_TY / 2 + 4;  // v_c window 20 x 12 (x 3 planes)
+constexpr int F_DMAX = 1024;  // class entries staged in LDS (nclass * ke)
+// R entry at step (dx, dy, dz) from the box's first fine point: (dz + 1) << 12 |
+// (dy * FR_RX + dx + 2048), relative to that point's position in a residual plane
+__host__ __device__ constexpr int fr_pack(int dx, int dy, int dz) { return ((dz + 1) << 12) | (dy * FR_RX + dx + 2048); }
+// P entry at coarse step (dx, dy, dz) from the anchor: its offset in the v_c window
+__host__ __device__ constexpr int fi_pack(int dx, int dy, int dz) { return (dz * FI_WY + dy) * FI_WX + dx; }
 
 struct FuseArgs {
     const uint32_t *codes;
@@ -76,9 +85,9 @@ struct FuseArgs {
     const double *dt;
     const double *d;
     const uint8_t *cls;   // R (restriction) or P (interpolation) classes
-    const double *cval;
-    const uint8_t *cslot;
-    int ke;
+    const double *cval;   // class entries: values and LDS positions, ke per class
+    const int16_t *coff;
+    int ke, nce;          // entries per class (a multiple of 8 / 4), nclass * ke
     const double *vc;     // interpolation: the coarse correction
     double *out;          // restriction: f_c; interpolation: the smoothed v
     int fx, fy, fz, cx, cy, cz;
@@ -96,7 +105,13 @@ __global__ __launch_bounds__(256) void k_fuse_resid_restrict(FuseArgs a) {
     __shared__ double rr[4][RPL];
     __shared__ double stab[VB == 4 ? 16 : 256];
     __shared__ double sdt[XM == 1 ? 256 : 1];
+    __shared__ double sval[F_DMAX];
+    __shared__ int16_t soff[F_DMAX];
     const int tid = threadIdx.x;
+    for (int q = tid; q < a.nce; q += 256) {
+        sval[q] = a.cval[q];
+        soff[q] = a.coff[q];
+    }
     const int t = xcd_remap(blockIdx.x, gridDim.x);
     const int tix = t % a.ntx, tiy = (t / a.ntx) % a.nty, tiz = t / (a.ntx * a.nty);
     const int X0 = tix * FR_CTX, Y0 = tiy * FR_CTY, Z0 = tiz * a.zchunk, Z1 = min(Z0 + a.zchunk, a.cz);
@@ -169,14 +184,19 @@ __global__ __launch_bounds__(256) void k_fuse_resid_restrict(FuseArgs a) {
         const int lx = tid % FR_CTX, ly = tid / FR_CTX, X = X0 + lx, Y = Y0 + ly;
         if (X >= a.cx || Y >= a.cy) return;
         const int64_t J = ((int64_t)Z * a.cy + Y) * a.cx + X;
-        const int c = a.cls[J];
-        const double *cv = a.cval + (int64_t)c * a.ke;
-        const uint8_t *cs = a.cslot + (int64_t)c * a.ke;
+        const int c0 = a.cls[J] * a.ke;
+        const int base = (2 * ly + 1) * FR_RX + 2 * lx + 1 - 2048;
         double acc = 0.0;
-        for (int e = 0; e < a.ke; e++) {
-            const int s = cs[e];
-            const int dx = (s & 3) - 1, dy = ((s >> 2) & 3) - 1, dz = (s >> 4) - 1;
-            acc = fma(cv[e], rr[(2 * Z + dz + 4) & 3][(2 * ly + 1 + dy) * FR_RX + 2 * lx + 1 + dx], acc);
+        for (int e0 = 0; e0 < a.ke; e0 += 8) {
+            double cv[8], rv[8];
+#pragma unroll
+            for (int u = 0; u < 8; u++) {
+                const int o = soff[c0 + e0 + u];
+                cv[u] = sval[c0 + e0 + u];
+                rv[u] = rr[(2 * Z + (o >> 12) - 1 + 4) & 3][base + (o & 4095)];
+            }
+#pragma unroll
+            for (int u = 0; u < 8; u++) acc = fma(cv[u], rv[u], acc);
         }
         a.out[J] = acc;
     };
@@ -218,7 +238,13 @@ __global__ __launch_bounds__(256) void k_fuse_interp_jacobi(FuseArgs a) {
     __shared__ double cw[3 * WPL];
     __shared__ double stab[VB == 4 ? 16 : 256];
     __shared__ double sdt[DC ? 256 : 1];
+    __shared__ double sval[F_DMAX];
+    __shared__ int16_t soff[F_DMAX];
     const int tid = threadIdx.x;
+    for (int q = tid; q < a.nce; q += 256) {
+        sval[q] = a.cval[q];
+        soff[q] = a.coff[q];
+    }
     const int t = xcd_remap(blockIdx.x, gridDim.x);
     const int tix = t % a.ntx, tiy = (t / a.ntx) % a.nty, tiz = t / (a.ntx * a.nty);
     const int x0 = tix * FI_TX, y0 = tiy * FI_TY, z0 = tiz * a.zchunk, z1 = min(z0 + a.zchunk, a.fz);
@@ -277,14 +303,18 @@ __global__ __launch_bounds__(256) void k_fuse_interp_jacobi(FuseArgs a) {
             double out = 0.0;
             if (L.cl[u] >= 0) {
                 const int gx = x0 - 1 + q % FI_VX, gy = y0 - 1 + q / FI_VX;
-                const int ax = (gx >> 1) - wx0, ay = (gy >> 1) - wy0;
-                const double *cv = a.cval + (int64_t)L.cl[u] * a.ke;
-                const uint8_t *cs = a.cslot + (int64_t)L.cl[u] * a.ke;
+                const int base = (FI_WY + (gy >> 1) - wy0) * FI_WX + (gx >> 1) - wx0;  // the anchor, window plane 1
+                const int c0 = L.cl[u] * a.ke;
                 double acc = 0.0;
-                for (int e = 0; e < a.ke; e++) {
-                    const int s = cs[e];
-                    const int dx = s % 3 - 1, dy = (s / 3) % 3 - 1, dz = s / 9;  // dz + 1: window plane
-                    acc = fma(cv[e], cw[(dz * FI_WY + ay + dy) * FI_WX + ax + dx], acc);
+                for (int e0 = 0; e0 < a.ke; e0 += 4) {
+                    double cv[4], wv[4];
+#pragma unroll
+                    for (int e = 0; e < 4; e++) {
+                        cv[e] = sval[c0 + e0 + e];
+                        wv[e] = cw[base + soff[c0 + e0 + e]];
+                    }
+#pragma unroll
+                    for (int e = 0; e < 4; e++) acc = fma(cv[e], wv[e], acc);
                 }
                 out = L.base[u] + acc;
             }
@@ -367,7 +397,7 @@ __global__ void k_fuse_check_dia(const uint32_t *codes, int cw, int vb, int K, c
 // on the coarse grid) for 2 x 2 x 2 boxes; false if an entry is not at such a
 // step, the columns are not ascending, or there are more than 256 classes.
 static bool build_gtc(const GpuCsr &M, bool is_r, const TransferFuse &F, DevBuf<uint8_t> &dcls,
-                      DevBuf<double> &dval, DevBuf<uint8_t> &dslot, int &ke_out, int &nc_out) {
+                      DevBuf<double> &dval, DevBuf<int16_t> &doff, int &ke_out, int &nc_out) {
     const int64_t n = M.nrows, nnz = M.nnz;
     if (n <= 0 || nnz <= 0) return false;
     std::vector<int64_t> rp(n + 1);
@@ -447,24 +477,31 @@ static bool build_gtc(const GpuCsr &M, bool is_r, const TransferFuse &F, DevBuf<
     const int C = (int)rep.size();
     int ke = 1;
     for (int c = 0; c < C; c++) ke = std::max<int>(ke, (int)(rp[rep[c] + 1] - rp[rep[c]]));
-    const uint8_t centre = is_r ? (uint8_t)(16 + 4 + 1) : (uint8_t)(9 + 3 + 1);
-    std::vector<double> hv((size_t)C * ke, 0.0);   // padding: +0.0 at the anchor itself
-    std::vector<uint8_t> hs((size_t)C * ke, centre);
+    const int gran = is_r ? 8 : 4;  // the kernels' load groups
+    ke = (ke + gran - 1) / gran * gran;
+    if ((int64_t)C * ke > F_DMAX) return false;
+    // entries as the kernels' LDS positions; padding: +0.0 at the anchor itself
+    // (after the row's entries: a +0.0 term leaves the accumulator unchanged)
+    auto pack = [&](int sl) {
+        if (is_r) return fr_pack(sl % 4 - 1, (sl / 4) % 4 - 1, sl / 16 - 1);
+        return fi_pack(sl % 3 - 1, (sl / 3) % 3 - 1, sl / 9 - 1);
+    };
+    const int16_t centre = (int16_t)(is_r ? fr_pack(0, 0, 0) : fi_pack(0, 0, 0));
+    std::vector<double> hv((size_t)C * ke, 0.0);
+    std::vector<int16_t> ho((size_t)C * ke, centre);
     for (int c = 0; c < C; c++) {
         const int64_t i = rep[c];
         for (int64_t e = rp[i]; e < rp[i + 1]; e++) {
             hv[(size_t)c * ke + (e - rp[i])] = val[e];
-            hs[(size_t)c * ke + (e - rp[i])] = slots[e];
+            ho[(size_t)c * ke + (e - rp[i])] = (int16_t)pack(slots[e]);
         }
     }
-    // padding must come after the row's entries in ascending order: a +0.0 term
-    // leaves the accumulator unchanged wherever it is added (finite operands)
     dcls.resize(n);
     dval.resize(hv.size());
-    dslot.resize(hs.size());
+    doff.resize(ho.size());
     FAMG_CHECK_HIP(hipMemcpyAsync(dcls.get(), cls.data(), n, hipMemcpyHostToDevice, s));
     FAMG_CHECK_HIP(hipMemcpyAsync(dval.get(), hv.data(), hv.size() * 8, hipMemcpyHostToDevice, s));
-    FAMG_CHECK_HIP(hipMemcpyAsync(dslot.get(), hs.data(), hs.size(), hipMemcpyHostToDevice, s));
+    FAMG_CHECK_HIP(hipMemcpyAsync(doff.get(), ho.data(), ho.size() * 2, hipMemcpyHostToDevice, s));
     FAMG_CHECK_HIP(hipStreamSynchronize(s));
     ke_out = ke;
     nc_out = C;
@@ -481,7 +518,7 @@ static bool fuse_kernel_shape(const GpuCsr &m) {
 void fuse_setup(MultigridOp &mg, size_t l) {
     MgLevel &L = mg.levels[l];
     L.fuse.reset();
-    if (!g_fuse_transfers || l + 1 >= mg.levels.size()) return;
+    if (!mg.fuse_transfers || l + 1 >= mg.levels.size()) return;
     auto *A = dynamic_cast<CsrOp *>(L.A.get());
     auto *R = dynamic_cast<CsrOp *>(L.R.get());
     auto *P = dynamic_cast<CsrOp *>(L.P.get());
@@ -539,9 +576,9 @@ void fuse_setup(MultigridOp &mg, size_t l) {
         FAMG_CHECK_HIP(hipStreamSynchronize(s));
         if (hbad) return;
     }
-    F->pre = build_gtc(R->m, true, *F, F->rcls, F->rval, F->rslot, F->rke, F->rnc);
+    F->pre = build_gtc(R->m, true, *F, F->rcls, F->rval, F->roff, F->rke, F->rnc);
     auto *D = dynamic_cast<DiagOp *>(L.S.get());
-    F->post = D && build_gtc(P->m, false, *F, F->pcls, F->pval, F->pslot, F->pke, F->pnc);
+    F->post = D && build_gtc(P->m, false, *F, F->pcls, F->pval, F->poff, F->pke, F->pnc);
     if (F->pre || F->post) L.fuse = F;
 }
 
@@ -576,8 +613,9 @@ void fuse_resid_restrict(const TransferFuse &F, const GpuCsr &m, const double *f
     }
     a.cls = F.rcls.get();
     a.cval = F.rval.get();
-    a.cslot = F.rslot.get();
+    a.coff = F.roff.get();
     a.ke = F.rke;
+    a.nce = F.rke * F.rnc;
     a.out = fc;
     a.ntx = (int)ceil_div(F.cx, FR_CTX);
     a.nty = (int)ceil_div(F.cy, FR_CTY);
@@ -615,8 +653,9 @@ void fuse_interp_jacobi(const TransferFuse &F, const GpuCsr &m, const double *vc
     a.d = D.d.get();
     a.cls = F.pcls.get();
     a.cval = F.pval.get();
-    a.cslot = F.pslot.get();
+    a.coff = F.poff.get();
     a.ke = F.pke;
+    a.nce = F.pke * F.pnc;
     a.vc = vc;
     a.out = out;
     a.ntx = (int)ceil_div(F.fx, FI_TX);

@@ -431,6 +431,11 @@ static bool xscs_setup(GpuCsr &m, const std::vector<int32_t> &offs, int Kp, cons
                 const int64_t T = (int64_t)tx * ty * tz;
                 const int64_t W = (int64_t)(tx + 2 * rx) * (ty + 2 * ry) * (tz + 2 * rz);
                 if (T > 1024 || T < std::min<int64_t>(64, n) || W * 8 > 64 * 1024) continue;
+                // one row per lane wherever the grid gives >= 1024 such tiles: the
+                // walk is latency-bound, so resident waves matter more than halo
+                // bytes (A_2 of the 256^3 cycle: 1024-row tiles, one wave per SIMD,
+                // ran 51 us against 40 on the cache-gathering kernel)
+                if (T > 256 && n >= 1024 * 256) continue;
                 const int64_t ntiles = ceil_div(nx, tx) * ceil_div(ny, ty) * ceil_div(nz, tz);
                 const double occ = std::min(4.0, std::floor(160.0 * 1024 / (W * 8.0)));
                 const double rounds = std::ceil(ntiles / 256.0);
