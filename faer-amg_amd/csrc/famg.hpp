@@ -117,6 +117,7 @@ struct GpuCsr {
     bool xscs = false;
     int xscs_t[3] = {0, 0, 0}, xscs_r[3] = {0, 0, 0};
     DevBuf<int32_t> xscs_lo;
+    std::vector<int> xscs_steps;  // (dx, dy, dz) of each of the scs_k offsets
     // grid hint: the rows are the points of an nx x ny x nz grid, x fastest (0 = none);
     // set by the stencil generators, the box hierarchy and amg_csr_set_grid
     int64_t grid[3] = {0, 0, 0};
@@ -344,6 +345,7 @@ struct SgsOp : LinOp {
     DevBuf<double> e_;     // scratch correction
     // fused plane-parity sweeps on a 27-point grid operator (sgs27.hip)
     bool fused27 = false;
+    bool const27 = false;  // every row the interior stencil truncated at the faces: no codes loaded
     int nx27 = 0, ny27 = 0, nz27 = 0;
     std::vector<uint32_t> icode27;  // interior row's code group (8 words, unused = ~0)
     std::vector<double> icoef27;    // and its 27 coefficients

@@ -21,6 +21,7 @@
 // matrix or for the halo-interior row segment of a distributed level (rows that
 // read owned columns only; the boundary segments keep SELL-64).
 #include <algorithm>
+#include <array>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -375,6 +376,21 @@ static bool grid_applies(const GpuCsr &m) {
            m.grid[0] * m.grid[1] * m.grid[2] == m.nrows && m.nrows < (int64_t(1) << 31);
 }
 
+// Tile t for m's x-staged kernel: the window offset of every stencil offset,
+// relative to the row's own window position.
+static void xscs_set_tile(GpuCsr &m, const int *t) {
+    const int rx = m.xscs_r[0], ry = m.xscs_r[1];
+    const int wx = t[0] + 2 * rx, wy = t[1] + 2 * ry;
+    const int Kp = (int)(m.xscs_steps.size() / 3);
+    std::vector<int32_t> lo(Kp);
+    for (int k = 0; k < Kp; k++)
+        lo[k] = (m.xscs_steps[3 * k + 2] * wy + m.xscs_steps[3 * k + 1]) * wx + m.xscs_steps[3 * k];
+    m.xscs_lo.resize(Kp);
+    FAMG_CHECK_HIP(hipMemcpyAsync(m.xscs_lo.get(), lo.data(), Kp * 4, hipMemcpyHostToDevice, m.ctx->stream));
+    FAMG_CHECK_HIP(hipStreamSynchronize(m.ctx->stream));
+    for (int q = 0; q < 3; q++) m.xscs_t[q] = t[q];
+}
+
 // Decompose the offsets into grid steps (dx, dy, dz) (centred residues), check
 // that every nonzero entry's step stays inside the grid, pick the tile and store
 // the window offsets: m.xscs on success.
@@ -454,19 +470,15 @@ static bool xscs_setup(GpuCsr &m, const std::vector<int32_t> &offs, int Kp, cons
         }
     }
     if (!best[0]) return false;
-    const int wx = best[0] + 2 * rx, wy = best[1] + 2 * ry;
-    std::vector<int32_t> lo(Kp, (rz * wy + ry) * wx + rx);  // padding offsets: the row itself
-    for (int k = 0; k < K; k++) lo[k] = ((dz[k] + rz) * wy + dy[k] + ry) * wx + dx[k] + rx;
-    // lo is relative to the window origin; the kernel adds the row's position
-    // (its window base includes the halo), so subtract the centre
-    const int ctr = (rz * wy + ry) * wx + rx;
-    for (int k = 0; k < Kp; k++) lo[k] -= ctr;
-    m.xscs_lo.resize(Kp);
-    FAMG_CHECK_HIP(hipMemcpyAsync(m.xscs_lo.get(), lo.data(), Kp * 4, hipMemcpyHostToDevice, m.ctx->stream));
-    FAMG_CHECK_HIP(hipStreamSynchronize(m.ctx->stream));
-    m.xscs_t[0] = best[0]; m.xscs_t[1] = best[1]; m.xscs_t[2] = best[2];
+    m.xscs_steps.assign(3 * Kp, 0);  // padding offsets: the row itself
+    for (int k = 0; k < K; k++) {
+        m.xscs_steps[3 * k] = dx[k];
+        m.xscs_steps[3 * k + 1] = dy[k];
+        m.xscs_steps[3 * k + 2] = dz[k];
+    }
     m.xscs_r[0] = rx; m.xscs_r[1] = ry; m.xscs_r[2] = rz;
     m.xscs = true;
+    xscs_set_tile(m, best);
     return true;
 }
 
@@ -516,6 +528,57 @@ static int64_t row_classes(const std::vector<int64_t> &rp, const std::vector<int
         cls[i] = (uint16_t)c;
     }
     return (int64_t)rep.size();
+}
+
+static void spmv_xscs(const GpuCsr &m, const double *x, double *y, SpmvMode mode, const SpmvEpi &epi,
+                      hipStream_t s);
+
+// Pick the tile by timing the candidates on the device (a few SET launches each
+// on scratch vectors): the modelled choice missed by up to 1.6x -- wide x rows
+// stage with fewer, longer loads, but a tile whose waves straddle boundary
+// classes reads the dictionary per lane (profiles/r03/ab_xscs_*.log).  The
+// tile changes no result (same sums in the same order).
+static void xscs_autotune(GpuCsr &m) {
+    if (getenv("FAMG_XSCS_TILE")) return;
+    const int64_t nx = m.grid[0], ny = m.grid[1], nz = m.grid[2], n = m.nrows;
+    const int rx = m.xscs_r[0], ry = m.xscs_r[1], rz = m.xscs_r[2];
+    std::vector<std::array<int, 3>> cands;
+    for (int tx : {4, 8, 16, 32, 64})
+        for (int ty : {1, 2, 4, 8, 16})
+            for (int tz : {1, 2, 4, 8}) {
+                if (tx > nx || ty > ny || tz > nz) continue;
+                const int64_t T = (int64_t)tx * ty * tz;
+                const int64_t W = (int64_t)(tx + 2 * rx) * (ty + 2 * ry) * (tz + 2 * rz);
+                if (T < std::min<int64_t>(64, n) || T > (n >= 1024 * 256 ? 256 : 1024) || W * 8 > 64 * 1024) continue;
+                if (T < 128 && n >= 1024 * 256) continue;
+                cands.push_back({tx, ty, tz});
+            }
+    if (cands.size() < 2) return;
+    hipStream_t s = m.ctx->stream;
+    DevBuf<double> x(m.ncols), y(m.nrows);
+    FAMG_CHECK_HIP(hipMemsetAsync(x.get(), 0, m.ncols * sizeof(double), s));
+    hipEvent_t e0, e1;
+    FAMG_CHECK_HIP(hipEventCreate(&e0));
+    FAMG_CHECK_HIP(hipEventCreate(&e1));
+    int best[3] = {m.xscs_t[0], m.xscs_t[1], m.xscs_t[2]};
+    float best_ms = 1e30f;
+    for (const auto &c : cands) {
+        xscs_set_tile(m, c.data());
+        spmv_xscs(m, x.get(), y.get(), SPMV_SET, SpmvEpi{}, s);
+        FAMG_CHECK_HIP(hipEventRecord(e0, s));
+        for (int r = 0; r < 3; r++) spmv_xscs(m, x.get(), y.get(), SPMV_SET, SpmvEpi{}, s);
+        FAMG_CHECK_HIP(hipEventRecord(e1, s));
+        FAMG_CHECK_HIP(hipEventSynchronize(e1));
+        float ms = 0.f;
+        FAMG_CHECK_HIP(hipEventElapsedTime(&ms, e0, e1));
+        if (ms < best_ms) {
+            best_ms = ms;
+            best[0] = c[0]; best[1] = c[1]; best[2] = c[2];
+        }
+    }
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+    xscs_set_tile(m, best);
 }
 
 bool build_scs(GpuCsr &m, const std::vector<int64_t> &rp, int64_t other_bytes) {
@@ -634,6 +697,7 @@ bool build_scs(GpuCsr &m, const std::vector<int64_t> &rp, int64_t other_bytes) {
     m.scs_ib = ib;
     m.scs_seg = seg;
     m.scs_lanes = lanes;
+    if (m.xscs) xscs_autotune(m);
     return true;
 }
 

@@ -82,9 +82,14 @@ typedef uint32_t sgs_u32x4_t __attribute__((ext_vector_type(4)));
 // an x operand of 0.0 on both paths; the product (+-0.0) added to an
 // accumulator that starts at +0.0 and can never become -0.0 leaves it
 // unchanged, so the sums are bitwise the same.
-template <int VB, int CW, int PX, int U, int NW>
+// CST: every row is the interior stencil truncated at the grid faces (checked
+// at setup), so no row's codes are loaded: the interior coefficients always.
+// OL: the other parity's rows z -+ 1 come from an LDS copy (olds: orw rows per
+// plane from grid row r0 - 1) instead of global memory.
+template <int VB, int CW, int PX, int U, int NW, bool CST, bool OL>
 __device__ __forceinline__ void sgs27_stage(const Sgs27Args &a, double *lds, const double *stab, const double *scoef,
-                                            int z, int r0, int ys0, int ys1, int py, bool first_zero) {
+                                            int z, int r0, int ys0, int ys1, int py, bool first_zero,
+                                            const double *olds, int orw) {
     constexpr uint32_t MASK = (1u << VB) - 1;
     const int nx = a.nx, ny = a.ny, nz = a.nz;
     const int64_t plane = (int64_t)nx * ny;
@@ -117,7 +122,7 @@ __device__ __forceinline__ void sgs27_stage(const Sgs27Args &a, double *lds, con
             const int64_t gi = rowg + x;
             li[u] = (y - r0 + 1) * nx + x;
 #pragma unroll
-            for (int q = 0; q < CW / 4; q++) {
+            for (int q = 0; q < (CST ? 0 : CW / 4); q++) {
                 const sgs_u32x4_t c =
                     __builtin_nontemporal_load(reinterpret_cast<const sgs_u32x4_t *>(a.codes + gi * CW) + q);
 #pragma unroll
@@ -131,7 +136,8 @@ __device__ __forceinline__ void sgs27_stage(const Sgs27Args &a, double *lds, con
                 const bool rowok = yy >= 0 && yy < ny && zz >= 0 && zz < nz;  // wave-uniform
                 const double *row;
                 if (dz == 0) row = lds + (rowok ? (yy - r0 + 1) * nx : 0);  // LDS row 0: zeros
-                else if (a.other_zero || !rowok) row = a.zero;
+                else if (a.other_zero || !rowok) row = OL ? lds : a.zero;
+                else if (OL) row = olds + ((dz > 0 ? orw : 0) + (yy - r0 + 1)) * nx;
                 else row = a.O + rowg + (int64_t)dz * plane + (int64_t)dy * nx;
                 const sgs_dbl2_t pa = *reinterpret_cast<const sgs_dbl2_t *>(row + offA);
                 const sgs_dbl2_t pb = *reinterpret_cast<const sgs_dbl2_t *>(row + offB);
@@ -148,7 +154,7 @@ __device__ __forceinline__ void sgs27_stage(const Sgs27Args &a, double *lds, con
             // the interior group with the entries leaving the grid cleared
             const bool ylo = y == 0, yhi = y == ny - 1;
 #pragma unroll
-            for (int q = 0; q < CW; q++) {
+            for (int q = 0; q < (CST ? 0 : CW); q++) {
                 const uint32_t clr = (lo ? a.fmask[0][q] : 0u) | (hi ? a.fmask[1][q] : 0u) |
                                      (ylo ? a.fmask[2][q] : 0u) | (yhi ? a.fmask[3][q] : 0u) |
                                      (zlo ? a.fmask[4][q] : 0u) | (zhi ? a.fmask[5][q] : 0u);
@@ -156,7 +162,7 @@ __device__ __forceinline__ void sgs27_stage(const Sgs27Args &a, double *lds, con
             }
         }
         double acc[U], dr[U];
-        if (__all(inter)) {
+        if (CST || __all(inter)) {
 #pragma unroll
             for (int u = 0; u < U; u++) {
                 acc[u] = 0.0;
@@ -182,7 +188,7 @@ __device__ __forceinline__ void sgs27_stage(const Sgs27Args &a, double *lds, con
     }
 }
 
-template <int VB, int CW, int U, int NW>
+template <int VB, int CW, int U, int NW, bool CST, bool OL>
 __global__ __launch_bounds__(64 * NW) void k_sgs27_phase(Sgs27Args a) {
     constexpr int NT = 64 * NW;
     extern __shared__ sgs_dbl2_t lds_pairs[];  // 16-B aligned: rows are read as pairs
@@ -220,13 +226,44 @@ __global__ __launch_bounds__(64 * NW) void k_sgs27_phase(Sgs27Args a) {
                 if (q0 + NT * u < nload2) l2[nx2 + q0 + NT * u] = v[u];
         }
     }
+    // OL: rows r0-1 .. r1 of planes z-1 and z+1 (zeros outside the grid)
+    const int orw = a.ty + 2 * a.nst + 2;
+    double *olds = lds + (int64_t)(1 + a.ty + 2 * a.nst) * nx;
+    if (OL && !a.other_zero) {
+        const int nrow_o = r1 - r0 + 2;
+        const int nload_o = 2 * nrow_o * nx2;
+        sgs_dbl2_t *o2 = reinterpret_cast<sgs_dbl2_t *>(olds);
+        constexpr int PF = 4;
+        for (int q0 = tid; q0 < nload_o; q0 += NT * PF) {
+            sgs_dbl2_t v[PF];
+#pragma unroll
+            for (int u = 0; u < PF; u++) {
+                const int q = q0 + NT * u;
+                const int pr = q / nx2, c = q - pr * nx2;      // pr: plane-row index
+                const int pi = pr >= nrow_o ? 1 : 0, j = pr - pi * nrow_o;
+                const int yy = r0 - 1 + j, zz = z + (pi ? 1 : -1);
+                const bool ok = q < nload_o && yy >= 0 && yy < ny && zz >= 0 && zz < a.nz;
+                v[u] = ok ? reinterpret_cast<const sgs_dbl2_t *>(a.O + (int64_t)zz * nx * ny + (int64_t)yy * nx)[c]
+                          : sgs_dbl2_t{0.0, 0.0};
+            }
+#pragma unroll
+            for (int u = 0; u < PF; u++) {
+                const int q = q0 + NT * u;
+                if (q < nload_o) {
+                    const int pr = q / nx2, c = q - pr * nx2;
+                    const int pi = pr >= nrow_o ? 1 : 0, j = pr - pi * nrow_o;
+                    o2[(pi * orw + j) * nx2 + c] = v[u];
+                }
+            }
+        }
+    }
     __syncthreads();
     for (int s = 0; s < a.nst; s++) {
         const int h = a.nst - 1 - s;
         const int ys0 = max(y0 - h, 0), ys1 = min(y1 + h, ny);
         const bool first_zero = a.own_zero && a.other_zero && s == 0;
-        if (a.px[s] == 0) sgs27_stage<VB, CW, 0, U, NW>(a, lds, stab, scoef, z, r0, ys0, ys1, a.py[s], first_zero);
-        else sgs27_stage<VB, CW, 1, U, NW>(a, lds, stab, scoef, z, r0, ys0, ys1, a.py[s], first_zero);
+        if (a.px[s] == 0) sgs27_stage<VB, CW, 0, U, NW, CST, OL>(a, lds, stab, scoef, z, r0, ys0, ys1, a.py[s], first_zero, olds, orw);
+        else sgs27_stage<VB, CW, 1, U, NW, CST, OL>(a, lds, stab, scoef, z, r0, ys0, ys1, a.py[s], first_zero, olds, orw);
         __syncthreads();
     }
     sgs_dbl2_t *dst = reinterpret_cast<sgs_dbl2_t *>(a.T + zoff + (int64_t)y0 * nx);
@@ -273,6 +310,27 @@ static int sgs27_nw() {
     }();
     return v;
 }
+// FAMG_SGS27_CST=0: load every row's codes even for a constant stencil (A/B)
+static bool sgs27_cst() {
+    static const bool on = [] {
+        const char *e = getenv("FAMG_SGS27_CST");
+        return !(e && e[0] == '0');
+    }();
+    return on;
+}
+// The other parity's rows in LDS too (1024-thread workgroups, one per CU):
+// rows of TY + 2 nst (own) + 2 (TY + 2 nst + 2) (planes z -+ 1) doubles of nx
+// within 160 KB.  Returns the TY used, 0 if it does not fit or FAMG_SGS27_OL=0.
+static int sgs27_ol_ty(int nx, int nst) {
+    static const bool on = [] {
+        const char *e = getenv("FAMG_SGS27_OL");
+        return !(e && e[0] == '0');
+    }();
+    if (!on) return 0;
+    for (int ty : {16, 12, 8, 4})
+        if ((size_t)(ty + 2 * nst + 1 + 2 * (ty + 2 * nst + 2)) * nx * sizeof(double) <= 160 * 1024) return ty;
+    return 0;
+}
 // odd planes' forward and backward colours in one phase (g_sgs_fused == 2: two)
 static int sgs27_p23() { return g_sgs_fused != 2; }
 constexpr int SGS27_MAX_NX = 512;  // LDS: (TY + 8) rows of nx doubles (TY = 16: 96 KB at nx = 512)
@@ -289,6 +347,23 @@ __global__ void k_sgs27_check(const uint32_t *codes, int cw, int vb, int zcode, 
         const bool in = x + dx >= 0 && x + dx < nx && y + dy >= 0 && y + dy < ny && z + dz >= 0 && z + dz < nz;
         const uint32_t c = (codes[i * cw + ((k * vb) >> 5)] >> ((k * vb) & 31)) & mask;
         if (!in && (int)c != zcode) bad[0] = 1;
+    }
+}
+
+struct Sgs27Const {
+    uint32_t icode[8], fmask[6][8];
+};
+// every row equals the interior code group with the entries leaving the grid cleared
+__global__ void k_sgs27_const(const uint32_t *codes, int cw, Sgs27Const c, int nx, int ny, int nz, int *bad) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    const int64_t n = (int64_t)nx * ny * nz;
+    if (i >= n) return;
+    const int x = (int)(i % nx), y = (int)((i / nx) % ny), z = (int)(i / ((int64_t)nx * ny));
+    for (int q = 0; q < cw; q++) {
+        const uint32_t clr = (x == 0 ? c.fmask[0][q] : 0u) | (x == nx - 1 ? c.fmask[1][q] : 0u) |
+                             (y == 0 ? c.fmask[2][q] : 0u) | (y == ny - 1 ? c.fmask[3][q] : 0u) |
+                             (z == 0 ? c.fmask[4][q] : 0u) | (z == nz - 1 ? c.fmask[5][q] : 0u);
+        if (codes[i * cw + q] != (c.icode[q] & ~clr)) bad[0] = 1;
     }
 }
 
@@ -368,6 +443,22 @@ void sgs27_setup(SgsOp &S) {
         }
         if (zcode != 0) S.icode27.assign(8, 0xffffffffu);  // cleared entries would not read code 0: no fast path
     }
+    // a constant stencil truncated at the faces: the phases load no codes
+    S.const27 = false;
+    if (zcode == 0) {
+        Sgs27Const c;
+        for (int q = 0; q < 8; q++) c.icode[q] = S.icode27[q];
+        for (int f = 0; f < 6; f++)
+            for (int q = 0; q < 8; q++) c.fmask[f][q] = S.fmask27[f * 8 + q];
+        FAMG_CHECK_HIP(hipMemsetAsync(bad.get(), 0, sizeof(int), s));
+        hipLaunchKernelGGL(k_sgs27_const, dim3((unsigned)ceil_div(m.nrows, 256)), dim3(256), 0, s,
+                           m.dia_codes.get(), m.dia_cw, c, nx, ny, nz, bad.get());
+        FAMG_CHECK_HIP(hipGetLastError());
+        int hb = 1;
+        FAMG_CHECK_HIP(hipMemcpyAsync(&hb, bad.get(), sizeof(int), hipMemcpyDeviceToHost, s));
+        FAMG_CHECK_HIP(hipStreamSynchronize(s));
+        S.const27 = hb == 0 && sgs27_cst();
+    }
     S.nx27 = nx;
     S.ny27 = ny;
     S.nz27 = nz;
@@ -406,7 +497,8 @@ static void sgs27_phase(const SgsOp &S, int pz, int nst, const int *px, const in
     a.other_zero = other_zero;
     a.cpy_src = cpy_src;
     a.cpy_dst = cpy_dst;
-    a.ty = sgs27_ty();
+    const bool ol = sgs27_ol_ty(S.nx27, nst) > 0;
+    a.ty = ol ? sgs27_ol_ty(S.nx27, nst) : sgs27_ty();
     for (int q = 0; q < 8; q++) a.icode[q] = S.icode27[q];
     for (int f = 0; f < 6; f++)
         for (int q = 0; q < 8; q++) a.fmask[f][q] = S.fmask27[f * 8 + q];
@@ -419,15 +511,25 @@ static void sgs27_phase(const SgsOp &S, int pz, int nst, const int *px, const in
     // and b, the other parity's x read once (unless zero), the copied planes
     if (g_launch_log)
         log_launch("sgs27_phase", SPMV_KERNEL_DIA, SPMV_SGS, rows,
-                   rows * (8 + 4 * (int64_t)m.dia_cw + 8) + (own_zero ? 0 : rows * 8) +
+                   rows * (8 + (S.const27 ? 0 : 4 * (int64_t)m.dia_cw) + 8) + (own_zero ? 0 : rows * 8) +
                        (other_zero ? 0 : (int64_t)(m.nrows - rows) * 8) +
                        (cpy_src ? (int64_t)(m.nrows - rows) * 16 : 0));
     const dim3 grid((unsigned)(nplanes * a.ntiles));
-    const size_t lds = (size_t)(a.ty + 2 * nst + 1) * S.nx27 * sizeof(double);
+    const size_t lds = (size_t)(a.ty + 2 * nst + 1 + (ol ? 2 * (a.ty + 2 * nst + 2) : 0)) * S.nx27 * sizeof(double);
     const bool u2 = sgs27_u() == 2;
     const int nw = sgs27_nw();
-#define FAMG_SGS27_LAUNCH(VB, CW, U, NW) k_sgs27_phase<VB, CW, U, NW><<<grid, dim3(64 * NW), lds, s>>>(a)
-    if (m.dia_vbits == 4) {
+#define FAMG_SGS27_LAUNCH(VB, CW, U, NW)                                                           \
+    if (S.const27) k_sgs27_phase<VB, CW, U, NW, true, false><<<grid, dim3(64 * NW), lds, s>>>(a);   \
+    else k_sgs27_phase<VB, CW, U, NW, false, false><<<grid, dim3(64 * NW), lds, s>>>(a)
+    if (ol) {
+        if (m.dia_vbits == 4) {
+            if (S.const27) k_sgs27_phase<4, 4, 1, 16, true, true><<<grid, dim3(1024), lds, s>>>(a);
+            else k_sgs27_phase<4, 4, 1, 16, false, true><<<grid, dim3(1024), lds, s>>>(a);
+        } else {
+            if (S.const27) k_sgs27_phase<8, 8, 1, 16, true, true><<<grid, dim3(1024), lds, s>>>(a);
+            else k_sgs27_phase<8, 8, 1, 16, false, true><<<grid, dim3(1024), lds, s>>>(a);
+        }
+    } else if (m.dia_vbits == 4) {
         if (nw == 8) { if (u2) FAMG_SGS27_LAUNCH(4, 4, 2, 8); else FAMG_SGS27_LAUNCH(4, 4, 1, 8); }
         else { if (u2) FAMG_SGS27_LAUNCH(4, 4, 2, 4); else FAMG_SGS27_LAUNCH(4, 4, 1, 4); }
     } else {
@@ -451,7 +553,7 @@ void sgs27_sweep(SgsOp &S, double *x, const double *b, bool zero) {
     static const int bopx[3] = {0, 1, 0}, bopy[3] = {1, 0, 0};       // colours 6,5,4
     static const int bepx[4] = {1, 0, 1, 0}, bepy[4] = {1, 1, 0, 0}; // colours 3,2,1,0
     static const int opx[7] = {0, 1, 0, 1, 0, 1, 0}, opy[7] = {0, 0, 1, 1, 1, 0, 0};  // 4,5,6,7,6,5,4
-    if (sgs27_p23() && (size_t)(sgs27_ty() + 15) * S.nx27 * sizeof(double) <= 150 * 1024) {
+    if (sgs27_p23() && sgs27_ol_ty(S.nx27, 4) == 0 && (size_t)(sgs27_ty() + 15) * S.nx27 * sizeof(double) <= 150 * 1024) {
         // three phases: the odd planes run forward and backward colours in one
         // launch; reading its source from t1 and writing x, it needs the odd
         // planes' old values in t1 -- the even phase copies them (none when zero)
