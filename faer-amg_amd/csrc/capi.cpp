@@ -257,6 +257,10 @@ amg_status amg_csr_spmv_info(const amg_linop *op, int64_t *info8) {
             info8[6] = info8[3] - m.xs_escape_slices;
             info8[7] = m.xs_escape_slices;
         }
+        if (m.gtc_on) {  // the grid-transfer overlay (its modes; the storage above serves the rest)
+            info8[0] = SPMV_KERNEL_GTC;
+            info8[1] = m.nrows + 2 * (int64_t)m.gtc_nce + 8 * (int64_t)m.gtc_ntab;
+        }
     });
 }
 

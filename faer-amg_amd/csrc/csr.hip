@@ -122,6 +122,7 @@ void csr_finalize(GpuCsr &m, const std::vector<int64_t> *segments) {
     FAMG_CHECK_HIP(hipStreamSynchronize(ctx.stream));
     scs_release(m);
     sellp_release(m);
+    gtc_release(m);
     build_sell(m, rp);
     const bool dia_all = m.has_dia() && m.dia_r0 == 0 && m.dia_r1 == m.nrows;
     const int64_t sell_b = m.sell_bytes + 12 * (m.nslices + 1) + 4 * m.sell_steps + 8 * m.sell_ntab;

@@ -118,6 +118,14 @@ struct GpuCsr {
     int xscs_t[3] = {0, 0, 0}, xscs_r[3] = {0, 0, 0};
     DevBuf<int32_t> xscs_lo;
     std::vector<int> xscs_steps;  // (dx, dy, dz) of each of the scs_k offsets
+    // grid-transfer classes (gtc.hip) for R/P of a 2x2x2-box hierarchy: an overlay
+    // on the finalized storage used for the modes it supports (gtc_supports)
+    bool gtc_on = false, gtc_r = false;
+    DevBuf<uint8_t> gtc_cls;
+    DevBuf<uint16_t> gtc_dict;
+    DevBuf<double> gtc_vtab;
+    int gtc_ke = 0, gtc_nce = 0, gtc_ntab = 0;
+    int64_t gtc_fg[3] = {0, 0, 0}, gtc_cg[3] = {0, 0, 0};
     // grid hint: the rows are the points of an nx x ny x nz grid, x fastest (0 = none);
     // set by the stencil generators, the box hierarchy and amg_csr_set_grid
     int64_t grid[3] = {0, 0, 0};
@@ -167,8 +175,15 @@ extern int g_spmv_format_policy;
 extern int g_value_codes;
 enum SpmvKernel : int {
     SPMV_KERNEL_STREAM = 0, SPMV_KERNEL_SELL = 1, SPMV_KERNEL_VECTOR = 2, SPMV_KERNEL_DIA = 3, SPMV_KERNEL_BSR = 4,
-    SPMV_KERNEL_SELLP = 5, SPMV_KERNEL_SCS = 6, SPMV_KERNEL_XS = 7
+    SPMV_KERNEL_SELLP = 5, SPMV_KERNEL_SCS = 6, SPMV_KERNEL_XS = 7, SPMV_KERNEL_GTC = 8
 };
+// grid-transfer classes (gtc.hip): fg/cg the fine/coarse grids of a 2x2x2-box
+// level; the row classes of P (fine rows) or R (coarse rows) as (slot, value)
+// lists; gtc_attach builds the overlay storage (true if it applies)
+bool gtc_classes(const GpuCsr &M, bool is_r, const int64_t *fg, const int64_t *cg, std::vector<uint8_t> &cls,
+                 std::vector<std::vector<std::pair<uint8_t, double>>> &dict);
+bool gtc_attach(GpuCsr &m, const int64_t *fg, const int64_t *cg);
+void gtc_release(GpuCsr &m);
 // stencil-class storage for structured operators whose rows repeat up to a
 // shift; true if built (scs.hip)
 bool build_scs(GpuCsr &m, const std::vector<int64_t> &rp, int64_t other_bytes);
@@ -232,6 +247,8 @@ void spmv_bsr(const GpuCsr &m, const double *x, double *y, SpmvMode mode, const 
 void spmv_scs(const GpuCsr &m, const double *x, double *y, SpmvMode mode, const SpmvEpi &epi, hipStream_t s,
               int64_t seg);
 bool xs_supports(SpmvMode mode);
+bool gtc_supports(const GpuCsr &m, SpmvMode mode);
+void spmv_gtc(const GpuCsr &m, const double *x, double *y, SpmvMode mode, const SpmvEpi &epi, hipStream_t s);
 void spmv_xs(const GpuCsr &m, const double *x, double *y, SpmvMode mode, const SpmvEpi &epi, hipStream_t s);
 void spmv_sellp(const GpuCsr &m, const double *x, double *y, SpmvMode mode, const SpmvEpi &epi, hipStream_t s,
                 int64_t seg);

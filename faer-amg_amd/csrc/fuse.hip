@@ -398,85 +398,15 @@ __global__ void k_fuse_check_dia(const uint32_t *codes, int cw, int vb, int K, c
 // step, the columns are not ascending, or there are more than 256 classes.
 static bool build_gtc(const GpuCsr &M, bool is_r, const TransferFuse &F, DevBuf<uint8_t> &dcls,
                       DevBuf<double> &dval, DevBuf<int16_t> &doff, int &ke_out, int &nc_out) {
-    const int64_t n = M.nrows, nnz = M.nnz;
-    if (n <= 0 || nnz <= 0) return false;
-    std::vector<int64_t> rp(n + 1);
-    std::vector<int32_t> col(nnz);
-    std::vector<double> val(nnz);
+    const int64_t fg[3] = {F.fx, F.fy, F.fz}, cg[3] = {F.cx, F.cy, F.cz};
+    std::vector<uint8_t> cls;
+    std::vector<std::vector<std::pair<uint8_t, double>>> dict;
+    if (!gtc_classes(M, is_r, fg, cg, cls, dict)) return false;
+    const int64_t n = M.nrows;
     hipStream_t s = M.ctx->stream;
-    FAMG_CHECK_HIP(hipMemcpyAsync(rp.data(), M.rp64.get(), (n + 1) * 8, hipMemcpyDeviceToHost, s));
-    FAMG_CHECK_HIP(hipMemcpyAsync(col.data(), M.col.get(), nnz * 4, hipMemcpyDeviceToHost, s));
-    FAMG_CHECK_HIP(hipMemcpyAsync(val.data(), M.val.get(), nnz * 8, hipMemcpyDeviceToHost, s));
-    FAMG_CHECK_HIP(hipStreamSynchronize(s));
-    const int64_t rx = is_r ? F.cx : F.fx, ry = is_r ? F.cy : F.fy;   // row grid
-    const int64_t kx = is_r ? F.fx : F.cx, ky = is_r ? F.fy : F.cy;   // column grid
-    const int KEMAX = is_r ? 64 : 27;
-    std::vector<uint8_t> slots(nnz);
-    std::vector<uint64_t> h(n);
-    bool ok = true;
-#pragma omp parallel for schedule(static) reduction(&& : ok)
-    for (int64_t i = 0; i < n; i++) {
-        const int64_t x = i % rx, y = (i / rx) % ry, z = i / (rx * ry);
-        // anchor in the column grid
-        const int64_t ax = is_r ? 2 * x : x / 2, ay = is_r ? 2 * y : y / 2, az = is_r ? 2 * z : z / 2;
-        uint64_t hh = 0x9E3779B97F4A7C15ull ^ (uint64_t)(rp[i + 1] - rp[i]);
-        int prev = -1;
-        if (rp[i + 1] - rp[i] > KEMAX) ok = false;
-        for (int64_t e = rp[i]; e < rp[i + 1]; e++) {
-            const int64_t j = col[e];
-            const int64_t dx = j % kx - ax, dy = (j / kx) % ky - ay, dz = j / (kx * ky) - az;
-            int sl;
-            if (is_r) {
-                if (dx < -1 || dx > 2 || dy < -1 || dy > 2 || dz < -1 || dz > 2) { ok = false; sl = 0; }
-                else sl = (int)((dz + 1) * 16 + (dy + 1) * 4 + dx + 1);
-            } else {
-                if (dx < -1 || dx > 1 || dy < -1 || dy > 1 || dz < -1 || dz > 1) { ok = false; sl = 0; }
-                else sl = (int)((dz + 1) * 9 + (dy + 1) * 3 + dx + 1);
-            }
-            if (sl <= prev) ok = false;
-            prev = sl;
-            slots[e] = (uint8_t)sl;
-            uint64_t bits;
-            std::memcpy(&bits, &val[e], 8);
-            hh = (hh ^ (uint64_t)sl) * 0x100000001B3ull;
-            hh = (hh ^ bits) * 0xFF51AFD7ED558CCDull;
-            hh ^= hh >> 29;
-        }
-        h[i] = hh;
-    }
-    if (!ok) return false;
-    auto same = [&](int64_t i, int64_t j) {
-        if (rp[i + 1] - rp[i] != rp[j + 1] - rp[j]) return false;
-        for (int64_t a = rp[i], b = rp[j]; a < rp[i + 1]; a++, b++)
-            if (slots[a] != slots[b] || std::memcmp(&val[a], &val[b], 8) != 0) return false;
-        return true;
-    };
-    std::unordered_map<uint64_t, std::vector<int>> by_hash;
-    std::vector<int64_t> rep;
-    std::vector<uint8_t> cls(n);
-    int64_t last_i = -1;
-    int last_c = -1;
-    for (int64_t i = 0; i < n; i++) {
-        int c = -1;
-        if (last_c >= 0 && h[i] == h[last_i] && same(last_i, i)) c = last_c;  // runs of equal rows
-        if (c < 0) {
-            auto &cands = by_hash[h[i]];
-            for (int q : cands)
-                if (same(rep[q], i)) { c = q; break; }
-            if (c < 0) {
-                c = (int)rep.size();
-                if (c >= 256) return false;
-                rep.push_back(i);
-                cands.push_back(c);
-            }
-        }
-        cls[i] = (uint8_t)c;
-        last_i = i;
-        last_c = c;
-    }
-    const int C = (int)rep.size();
+    const int C = (int)dict.size();
     int ke = 1;
-    for (int c = 0; c < C; c++) ke = std::max<int>(ke, (int)(rp[rep[c] + 1] - rp[rep[c]]));
+    for (int c = 0; c < C; c++) ke = std::max<int>(ke, (int)dict[c].size());
     const int gran = is_r ? 8 : 4;  // the kernels' load groups
     ke = (ke + gran - 1) / gran * gran;
     if ((int64_t)C * ke > F_DMAX) return false;
@@ -489,13 +419,11 @@ static bool build_gtc(const GpuCsr &M, bool is_r, const TransferFuse &F, DevBuf<
     const int16_t centre = (int16_t)(is_r ? fr_pack(0, 0, 0) : fi_pack(0, 0, 0));
     std::vector<double> hv((size_t)C * ke, 0.0);
     std::vector<int16_t> ho((size_t)C * ke, centre);
-    for (int c = 0; c < C; c++) {
-        const int64_t i = rep[c];
-        for (int64_t e = rp[i]; e < rp[i + 1]; e++) {
-            hv[(size_t)c * ke + (e - rp[i])] = val[e];
-            ho[(size_t)c * ke + (e - rp[i])] = (int16_t)pack(slots[e]);
+    for (int c = 0; c < C; c++)
+        for (size_t k = 0; k < dict[c].size(); k++) {
+            hv[(size_t)c * ke + k] = dict[c][k].second;
+            ho[(size_t)c * ke + k] = (int16_t)pack(dict[c][k].first);
         }
-    }
     dcls.resize(n);
     dval.resize(hv.size());
     doff.resize(ho.size());

@@ -1,0 +1,374 @@
+// gtc.hip -- grid-transfer classes: SpMV storage for the transfer operators of
+// a 2 x 2 x 2 box-aggregation hierarchy on a structured grid.
+//
+// P (fine rows, coarse columns; interpolation/mod.rs:716-720 smoothed) and
+// R = P^T (coarse rows, fine columns) have rows whose entries sit at a few
+// fixed grid steps from an anchor: P's row (x, y, z) reads coarse points
+// (x/2, y/2, z/2) + {-1,0,1}^3, R's row (X, Y, Z) reads fine points
+// (2X, 2Y, 2Z) + {-1,..,2}^3.  Away from the boundary the rows repeat with the
+// parity of (x, y, z) (P) or not at all (R), so a row is one 8-bit class id
+// into a dictionary of (step, value) lists.  P_0 of the 256^3 7-point
+// hierarchy: 1 B per row instead of 12.5 B of value-code SELL; 27-point: 1 B
+// instead of ~25 B.  Dictionary entries are 16 bits: the value's index in a
+// table of the operator's distinct values (<= 256) and the step's slot.
+//
+// Kernels: one workgroup per grid tile stages the tile's column-grid window
+// (the coarse v_c for P, the fine vector for R; 0.0 outside the grid) in LDS,
+// then each lane sums its rows' entries in stored (ascending column) order
+// with fma from the window -- bitwise the oracle's CSR row sums; epilogues
+// SET, ADD (y += P v_c), ADD0 (y = d*b + P v_c, the folded zero-guess step).
+#include <algorithm>
+#include <cstring>
+#include <unordered_map>
+
+#include "famg.hpp"
+
+namespace famg {
+
+// ------------------------------------------------------------ host classes
+
+bool gtc_classes(const GpuCsr &M, bool is_r, const int64_t *fg, const int64_t *cg, std::vector<uint8_t> &cls,
+                 std::vector<std::vector<std::pair<uint8_t, double>>> &dict) {
+    const int64_t n = M.nrows, nnz = M.nnz;
+    if (n <= 0 || nnz <= 0) return false;
+    const int64_t rx = is_r ? cg[0] : fg[0], ry = is_r ? cg[1] : fg[1], rz = is_r ? cg[2] : fg[2];  // row grid
+    const int64_t kx = is_r ? fg[0] : cg[0], ky = is_r ? fg[1] : cg[1], kz = is_r ? fg[2] : cg[2];  // column grid
+    if (rx * ry * rz != n || kx * ky * kz != M.ncols) return false;
+    if (cg[0] != (fg[0] + 1) / 2 || cg[1] != (fg[1] + 1) / 2 || cg[2] != (fg[2] + 1) / 2) return false;
+    std::vector<int64_t> rp(n + 1);
+    std::vector<int32_t> col(nnz);
+    std::vector<double> val(nnz);
+    hipStream_t s = M.ctx->stream;
+    FAMG_CHECK_HIP(hipMemcpyAsync(rp.data(), M.rp64.get(), (n + 1) * 8, hipMemcpyDeviceToHost, s));
+    FAMG_CHECK_HIP(hipMemcpyAsync(col.data(), M.col.get(), nnz * 4, hipMemcpyDeviceToHost, s));
+    FAMG_CHECK_HIP(hipMemcpyAsync(val.data(), M.val.get(), nnz * 8, hipMemcpyDeviceToHost, s));
+    FAMG_CHECK_HIP(hipStreamSynchronize(s));
+    const int KEMAX = is_r ? 64 : 27;
+    std::vector<uint8_t> slots(nnz);
+    std::vector<uint64_t> h(n);
+    bool ok = true;
+#pragma omp parallel for schedule(static) reduction(&& : ok)
+    for (int64_t i = 0; i < n; i++) {
+        const int64_t x = i % rx, y = (i / rx) % ry, z = i / (rx * ry);
+        const int64_t ax = is_r ? 2 * x : x / 2, ay = is_r ? 2 * y : y / 2, az = is_r ? 2 * z : z / 2;  // anchor
+        uint64_t hh = 0x9E3779B97F4A7C15ull ^ (uint64_t)(rp[i + 1] - rp[i]);
+        int prev = -1;
+        if (rp[i + 1] - rp[i] > KEMAX) ok = false;
+        for (int64_t e = rp[i]; e < rp[i + 1]; e++) {
+            const int64_t j = col[e];
+            const int64_t dx = j % kx - ax, dy = (j / kx) % ky - ay, dz = j / (kx * ky) - az;
+            int sl = 0;
+            if (is_r) {
+                if (dx < -1 || dx > 2 || dy < -1 || dy > 2 || dz < -1 || dz > 2) ok = false;
+                else sl = (int)((dz + 1) * 16 + (dy + 1) * 4 + dx + 1);
+            } else {
+                if (dx < -1 || dx > 1 || dy < -1 || dy > 1 || dz < -1 || dz > 1) ok = false;
+                else sl = (int)((dz + 1) * 9 + (dy + 1) * 3 + dx + 1);
+            }
+            if (sl <= prev) ok = false;  // ascending columns = ascending slots
+            prev = sl;
+            slots[e] = (uint8_t)sl;
+            uint64_t bits;
+            std::memcpy(&bits, &val[e], 8);
+            hh = (hh ^ (uint64_t)sl) * 0x100000001B3ull;
+            hh = (hh ^ bits) * 0xFF51AFD7ED558CCDull;
+            hh ^= hh >> 29;
+        }
+        h[i] = hh;
+    }
+    if (!ok) return false;
+    auto same = [&](int64_t i, int64_t j) {
+        if (rp[i + 1] - rp[i] != rp[j + 1] - rp[j]) return false;
+        for (int64_t a = rp[i], b = rp[j]; a < rp[i + 1]; a++, b++)
+            if (slots[a] != slots[b] || std::memcmp(&val[a], &val[b], 8) != 0) return false;
+        return true;
+    };
+    std::unordered_map<uint64_t, std::vector<int>> by_hash;
+    std::vector<int64_t> rep;
+    cls.assign(n, 0);
+    int64_t last_i = -1;
+    int last_c = -1;
+    for (int64_t i = 0; i < n; i++) {
+        int c = -1;
+        if (last_c >= 0 && h[i] == h[last_i] && same(last_i, i)) c = last_c;  // runs of equal rows
+        if (c < 0) {
+            auto &cands = by_hash[h[i]];
+            for (int q : cands)
+                if (same(rep[q], i)) { c = q; break; }
+            if (c < 0) {
+                c = (int)rep.size();
+                if (c >= 256) return false;
+                rep.push_back(i);
+                cands.push_back(c);
+            }
+        }
+        cls[i] = (uint8_t)c;
+        last_i = i;
+        last_c = c;
+    }
+    dict.assign(rep.size(), {});
+    for (size_t c = 0; c < rep.size(); c++)
+        for (int64_t e = rp[rep[c]]; e < rp[rep[c] + 1]; e++) dict[c].push_back({slots[e], val[e]});
+    return true;
+}
+
+// ------------------------------------------------------------ kernels
+
+constexpr int GP_TX = 32, GP_TY = 8, GP_TZ = 4;                  // P: fine tile (4 rows per lane along z)
+constexpr int GP_WX = GP_TX / 2 + 2, GP_WY = GP_TY / 2 + 2, GP_WZ = GP_TZ / 2 + 2;  // coarse window 18 x 6 x 4
+constexpr int GR_TX = 16, GR_TY = 8, GR_TZ = 2;                  // R: coarse tile (one row per lane)
+constexpr int GR_WX = 2 * GR_TX + 2, GR_WY = 2 * GR_TY + 2, GR_WZ = 2 * GR_TZ + 2;  // fine window 34 x 18 x 6
+constexpr int G_DMAX = 2048;                                      // dictionary entries (nclass * ke)
+
+struct GtcArgs {
+    const uint8_t *cls;
+    const uint16_t *dict;  // nclass x ke entries: value index << 8 | slot
+    const double *vtab;    // distinct values
+    int ke, nce, ntab;
+    int rx, ry, rz;        // row grid
+    int kx, ky, kz;        // column grid
+    int ntx, nty;
+    const double *x;
+    double *y;
+    const double *b;
+    const double *d;
+    const uint8_t *dc;
+    const double *dt;
+};
+
+// P v_c over a fine tile of 32 x 8 x 4 points: lane (x, y) of the tile takes
+// its four points along z; the coarse window 18 x 6 x 4 around them in LDS.
+template <int MODE>
+__global__ __launch_bounds__(256) void k_gtc_interp(GtcArgs a) {
+    __shared__ double win[GP_WX * GP_WY * GP_WZ];
+    __shared__ uint16_t sd[G_DMAX];
+    __shared__ double st[256];
+    __shared__ int16_t lut[27];
+    const int tid = threadIdx.x;
+    const int t = xcd_remap(blockIdx.x, gridDim.x);
+    const int tix = t % a.ntx, tiy = (t / a.ntx) % a.nty, tiz = t / (a.ntx * a.nty);
+    const int x0 = tix * GP_TX, y0 = tiy * GP_TY, z0 = tiz * GP_TZ;
+    const int wx0 = x0 / 2 - 1, wy0 = y0 / 2 - 1, wz0 = z0 / 2 - 1;  // window origin (coarse)
+    const int64_t fplane = (int64_t)a.rx * a.ry, cplane = (int64_t)a.kx * a.ky;
+    // the rows' class ids and epilogue operands first
+    const int lx = tid % GP_TX, ly = tid / GP_TX, gx = x0 + lx, gy = y0 + ly;
+    int cl[GP_TZ];
+    double yb[GP_TZ];
+    bool live[GP_TZ];
+#pragma unroll
+    for (int j = 0; j < GP_TZ; j++) {
+        const int gz = z0 + j;
+        live[j] = gx < a.rx && gy < a.ry && gz < a.rz;
+        const int64_t i = live[j] ? (int64_t)gz * fplane + (int64_t)gy * a.rx + gx : 0;
+        cl[j] = a.cls[i];
+        yb[j] = 0.0;
+        if (live[j]) {
+            if constexpr (MODE == SPMV_ADD) yb[j] = a.y[i];
+            if constexpr (MODE == SPMV_ADD0) yb[j] = (a.dc ? a.dt[a.dc[i]] : a.d[i]) * a.b[i];  // d*b
+        }
+    }
+    for (int q = tid; q < GP_WX * GP_WY * GP_WZ; q += 256) {
+        const int X = wx0 + q % GP_WX, Y = wy0 + (q / GP_WX) % GP_WY, Z = wz0 + q / (GP_WX * GP_WY);
+        const bool in = (unsigned)X < (unsigned)a.kx && (unsigned)Y < (unsigned)a.ky && (unsigned)Z < (unsigned)a.kz;
+        win[q] = in ? a.x[(int64_t)Z * cplane + (int64_t)Y * a.kx + X] : 0.0;
+    }
+    for (int q = tid; q < a.nce; q += 256) sd[q] = a.dict[q];
+    if (tid < a.ntab) st[tid] = a.vtab[tid];
+    if (tid < 27) lut[tid] = (int16_t)(((tid / 9 - 1) * GP_WY + (tid / 3) % 3 - 1) * GP_WX + tid % 3 - 1);
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < GP_TZ; j++) {
+        if (!live[j]) continue;
+        const int gz = z0 + j;
+        const int base = (((gz >> 1) - wz0) * GP_WY + (gy >> 1) - wy0) * GP_WX + (gx >> 1) - wx0;
+        const uint16_t *e = sd + cl[j] * a.ke;
+        double acc = 0.0;
+        for (int k = 0; k < a.ke; k += 4) {
+            double v[4], w[4];
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                const uint16_t c = e[k + u];
+                v[u] = st[c >> 8];
+                w[u] = win[base + lut[c & 255]];
+            }
+#pragma unroll
+            for (int u = 0; u < 4; u++) acc = fma(v[u], w[u], acc);
+        }
+        const int64_t i = (int64_t)gz * fplane + (int64_t)gy * a.rx + gx;
+        if constexpr (MODE == SPMV_SET) a.y[i] = acc;
+        else a.y[i] = yb[j] + acc;  // ADD, ADD0
+    }
+}
+
+// R r over a coarse tile of 16 x 8 x 2 points, one per lane; the fine window
+// 34 x 18 x 6 around their boxes in LDS.
+__global__ __launch_bounds__(256) void k_gtc_restrict(GtcArgs a) {
+    __shared__ double win[GR_WX * GR_WY * GR_WZ];
+    __shared__ uint16_t sd[G_DMAX];
+    __shared__ double st[256];
+    __shared__ int16_t lut[64];
+    const int tid = threadIdx.x;
+    const int t = xcd_remap(blockIdx.x, gridDim.x);
+    const int tix = t % a.ntx, tiy = (t / a.ntx) % a.nty, tiz = t / (a.ntx * a.nty);
+    const int X0 = tix * GR_TX, Y0 = tiy * GR_TY, Z0 = tiz * GR_TZ;
+    const int wx0 = 2 * X0 - 1, wy0 = 2 * Y0 - 1, wz0 = 2 * Z0 - 1;  // window origin (fine)
+    const int64_t cplane = (int64_t)a.rx * a.ry, fplane = (int64_t)a.kx * a.ky;
+    const int lx = tid % GR_TX, ly = (tid / GR_TX) % GR_TY, lz = tid / (GR_TX * GR_TY);
+    const int X = X0 + lx, Y = Y0 + ly, Z = Z0 + lz;
+    const bool live = X < a.rx && Y < a.ry && Z < a.rz;
+    const int64_t J = live ? (int64_t)Z * cplane + (int64_t)Y * a.rx + X : 0;
+    const int c = a.cls[J];
+    constexpr int W = GR_WX * GR_WY * GR_WZ, PF = (W + 255) / 256;
+    double v[PF];
+#pragma unroll
+    for (int u = 0; u < PF; u++) {  // all of a lane's window loads before its LDS stores
+        const int q = tid + 256 * u;
+        const int x = wx0 + q % GR_WX, y = wy0 + (q / GR_WX) % GR_WY, z = wz0 + q / (GR_WX * GR_WY);
+        const bool in = q < W && (unsigned)x < (unsigned)a.kx && (unsigned)y < (unsigned)a.ky && (unsigned)z < (unsigned)a.kz;
+        v[u] = in ? a.x[(int64_t)z * fplane + (int64_t)y * a.kx + x] : 0.0;
+    }
+#pragma unroll
+    for (int u = 0; u < PF; u++)
+        if (tid + 256 * u < W) win[tid + 256 * u] = v[u];
+    for (int q = tid; q < a.nce; q += 256) sd[q] = a.dict[q];
+    if (tid < a.ntab) st[tid] = a.vtab[tid];
+    if (tid < 64) lut[tid] = (int16_t)(((tid / 16 - 1) * GR_WY + (tid / 4) % 4 - 1) * GR_WX + tid % 4 - 1);
+    __syncthreads();
+    if (!live) return;
+    const int base = ((2 * lz + 1) * GR_WY + 2 * ly + 1) * GR_WX + 2 * lx + 1;
+    const uint16_t *e = sd + c * a.ke;
+    double acc = 0.0;
+    for (int k = 0; k < a.ke; k += 8) {
+        double cv[8], w[8];
+#pragma unroll
+        for (int u = 0; u < 8; u++) {
+            const uint16_t q = e[k + u];
+            cv[u] = st[q >> 8];
+            w[u] = win[base + lut[q & 255]];
+        }
+#pragma unroll
+        for (int u = 0; u < 8; u++) acc = fma(cv[u], w[u], acc);
+    }
+    a.y[J] = acc;
+}
+
+// ------------------------------------------------------------ build / dispatch
+
+void gtc_release(GpuCsr &m) {
+    m.gtc_cls.release();
+    m.gtc_dict.release();
+    m.gtc_vtab.release();
+    m.gtc_ke = m.gtc_nce = m.gtc_ntab = 0;
+    m.gtc_r = m.gtc_on = false;
+}
+
+// FAMG_GTC=0: keep the finalize-time storage for R and P
+static bool gtc_enabled() {
+    static const bool on = [] {
+        const char *e = getenv("FAMG_GTC");
+        return !(e && e[0] == '0');
+    }();
+    return on;
+}
+
+bool gtc_attach(GpuCsr &m, const int64_t *fg, const int64_t *cg) {
+    gtc_release(m);
+    if (!gtc_enabled() || m.nnz >= (int64_t(1) << 31)) return false;
+    const bool is_r = m.nrows < m.ncols;
+    std::vector<uint8_t> cls;
+    std::vector<std::vector<std::pair<uint8_t, double>>> dict;
+    if (!gtc_classes(m, is_r, fg, cg, cls, dict)) return false;
+    // distinct values (bit patterns), <= 256
+    std::vector<uint64_t> vals;
+    for (const auto &d : dict)
+        for (const auto &e : d) {
+            uint64_t b;
+            std::memcpy(&b, &e.second, 8);
+            vals.push_back(b);
+        }
+    vals.push_back(0);  // +0.0 for the padding entries
+    std::sort(vals.begin(), vals.end());
+    vals.erase(std::unique(vals.begin(), vals.end()), vals.end());
+    if (vals.size() > 256) return false;
+    const int gran = is_r ? 8 : 4;
+    size_t ke = 1;
+    for (const auto &d : dict) ke = std::max(ke, d.size());
+    ke = (ke + gran - 1) / gran * gran;
+    if (dict.size() * ke > (size_t)G_DMAX) return false;
+    const uint16_t zero_idx = (uint16_t)(std::lower_bound(vals.begin(), vals.end(), 0ull) - vals.begin());
+    const uint16_t centre = is_r ? (uint16_t)(16 + 4 + 1) : (uint16_t)(9 + 3 + 1);
+    // padding: +0.0 at the anchor (after the row's entries: a +0.0 term leaves
+    // the accumulator unchanged)
+    std::vector<uint16_t> hd(dict.size() * ke, (uint16_t)(zero_idx << 8 | centre));
+    for (size_t c = 0; c < dict.size(); c++)
+        for (size_t k = 0; k < dict[c].size(); k++) {
+            uint64_t b;
+            std::memcpy(&b, &dict[c][k].second, 8);
+            const uint16_t vi = (uint16_t)(std::lower_bound(vals.begin(), vals.end(), b) - vals.begin());
+            hd[c * ke + k] = (uint16_t)(vi << 8 | dict[c][k].first);
+        }
+    std::vector<double> vt(vals.size());
+    for (size_t q = 0; q < vals.size(); q++) std::memcpy(&vt[q], &vals[q], 8);
+    hipStream_t s = m.ctx->stream;
+    m.gtc_cls.resize(cls.size());
+    m.gtc_dict.resize(hd.size());
+    m.gtc_vtab.resize(vt.size());
+    FAMG_CHECK_HIP(hipMemcpyAsync(m.gtc_cls.get(), cls.data(), cls.size(), hipMemcpyHostToDevice, s));
+    FAMG_CHECK_HIP(hipMemcpyAsync(m.gtc_dict.get(), hd.data(), hd.size() * 2, hipMemcpyHostToDevice, s));
+    FAMG_CHECK_HIP(hipMemcpyAsync(m.gtc_vtab.get(), vt.data(), vt.size() * 8, hipMemcpyHostToDevice, s));
+    FAMG_CHECK_HIP(hipStreamSynchronize(s));
+    m.gtc_ke = (int)ke;
+    m.gtc_nce = (int)(dict.size() * ke);
+    m.gtc_ntab = (int)vt.size();
+    m.gtc_r = is_r;
+    for (int q = 0; q < 3; q++) {
+        m.gtc_fg[q] = fg[q];
+        m.gtc_cg[q] = cg[q];
+    }
+    m.gtc_on = true;
+    return true;
+}
+
+bool gtc_supports(const GpuCsr &m, SpmvMode mode) {
+    return m.gtc_r ? mode == SPMV_SET : (mode == SPMV_SET || mode == SPMV_ADD || mode == SPMV_ADD0);
+}
+
+void spmv_gtc(const GpuCsr &m, const double *x, double *y, SpmvMode mode, const SpmvEpi &epi, hipStream_t s) {
+    GtcArgs a{};
+    a.cls = m.gtc_cls.get();
+    a.dict = m.gtc_dict.get();
+    a.vtab = m.gtc_vtab.get();
+    a.ke = m.gtc_ke;
+    a.nce = m.gtc_nce;
+    a.ntab = m.gtc_ntab;
+    const int64_t *rg = m.gtc_r ? m.gtc_cg : m.gtc_fg, *kg = m.gtc_r ? m.gtc_fg : m.gtc_cg;
+    a.rx = (int)rg[0]; a.ry = (int)rg[1]; a.rz = (int)rg[2];
+    a.kx = (int)kg[0]; a.ky = (int)kg[1]; a.kz = (int)kg[2];
+    a.x = x;
+    a.y = y;
+    a.b = epi.b;
+    a.d = epi.d;
+    a.dc = epi.dc;
+    a.dt = epi.dt;
+    if (m.gtc_r) {
+        FAMG_REQUIRE(mode == SPMV_SET, AMG_ERR_UNSUPPORTED, "grid-transfer R: SET only");
+        a.ntx = (int)ceil_div(a.rx, GR_TX);
+        a.nty = (int)ceil_div(a.ry, GR_TY);
+        const int ntz = (int)ceil_div(a.rz, GR_TZ);
+        hipLaunchKernelGGL(k_gtc_restrict, dim3((unsigned)((int64_t)a.ntx * a.nty * ntz)), dim3(256), 0, s, a);
+    } else {
+        a.ntx = (int)ceil_div(a.rx, GP_TX);
+        a.nty = (int)ceil_div(a.ry, GP_TY);
+        const int ntz = (int)ceil_div(a.rz, GP_TZ);
+        const dim3 grid((unsigned)((int64_t)a.ntx * a.nty * ntz)), block(256);
+        switch (mode) {
+        case SPMV_SET: k_gtc_interp<SPMV_SET><<<grid, block, 0, s>>>(a); break;
+        case SPMV_ADD: k_gtc_interp<SPMV_ADD><<<grid, block, 0, s>>>(a); break;
+        case SPMV_ADD0: k_gtc_interp<SPMV_ADD0><<<grid, block, 0, s>>>(a); break;
+        default: fail(AMG_ERR_UNSUPPORTED, "grid-transfer P: unsupported SpMV epilogue");
+        }
+    }
+    FAMG_CHECK_HIP(hipGetLastError());
+}
+
+}  // namespace famg

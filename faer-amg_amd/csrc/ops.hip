@@ -522,7 +522,8 @@ void MultigridOp::cycle(int64_t l, double *v, const double *f, bool v_zero, doub
                        A->m.kernel == SPMV_KERNEL_XS ||  // x-staged: d*x staged with x, no extra gather
                        (A->m.kernel == SPMV_KERNEL_DIA &&
                         (fold_dia_mode() == 1 ||
-                         (fold_dia_mode() < 0 && P->m.kernel == SPMV_KERNEL_SELL && P->m.sell_short))));
+                         (fold_dia_mode() < 0 &&
+                          ((P->m.kernel == SPMV_KERNEL_SELL && P->m.sell_short) || P->m.gtc_on)))));
     MgLevel &C = levels[l + 1];
     // grid levels: residual and restriction in one launch (fuse.hip), r never stored
     const bool fuse_pre = fuse_transfers && A && fuse_has_pre(L) && (!fold || D);
@@ -866,6 +867,13 @@ std::shared_ptr<MultigridOp> sa_build_box(const CsrPtr &A, int64_t nx, int64_t n
         CsrPtr P = smooth_interpolation(*cur, *Pt, omega);
         Pt.reset();
         CsrPtr R = transpose_op(*P);
+        {  // R and P as grid-transfer classes (1 B per row) where their rows fit the boxes
+            const int64_t fg[3] = {cx, cy, cz}, cg[3] = {ncx, ncy, ncz};
+            if (bx == 2 && by == 2 && bz == 2) {
+                gtc_attach(P->m, fg, cg);
+                gtc_attach(R->m, fg, cg);
+            }
+        }
         const int64_t cgrid[3] = {ncx, ncy, ncz};  // the coarse grid (x-staged stencil kernels)
         CsrPtr Ac = galerkin_rap(*R, *cur, *P, cgrid);
         nn_stationary_l1_dev(*Ac, 3, cnn.get());

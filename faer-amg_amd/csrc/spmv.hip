@@ -2356,7 +2356,11 @@ static void log_spmv(const GpuCsr &m, SpmvMode mode, const SpmvEpi &epi, int64_t
     int64_t mat = 0;
     const int64_t csr_mat = part(m.index_bytes());
     const int64_t dia_bytes = 4 * (int64_t)m.dia_cw * r + 8 * m.dia_ntab;
-    if (m.kernel == SPMV_KERNEL_BSR) {
+    if (m.gtc_on && seg < 0 && gtc_supports(m, mode)) {
+        kernel = SPMV_KERNEL_GTC;
+        name = "gtc";
+        mat = m.nrows + 2 * (int64_t)m.gtc_nce + 8 * (int64_t)m.gtc_ntab;
+    } else if (m.kernel == SPMV_KERNEL_BSR) {
         name = "bsr3";
         mat = part(m.stream_bytes());
     } else if (m.kernel == SPMV_KERNEL_SCS || (m.has_scs() && seg >= 0 && seg == m.scs_seg && mode != SPMV_SGS)) {
@@ -2413,6 +2417,10 @@ void spmv(const GpuCsr &m, const double *x, double *y, SpmvMode mode, const Spmv
     if (g_launch_log) log_spmv(m, mode, epi, seg);
     Epi e{x, y, epi.b, epi.d, epi.perm, epi.dc, epi.dt};
     const dim3 block(256);
+    if (m.gtc_on && seg < 0 && gtc_supports(m, mode)) {
+        spmv_gtc(m, x, y, mode, epi, s);
+        return;
+    }
     if (m.kernel == SPMV_KERNEL_BSR) {
         FAMG_REQUIRE(mode != SPMV_SGS, AMG_ERR_UNSUPPORTED, "block storage has no SGS sweep");
         spmv_bsr(m, x, y, mode, epi, s, seg);

@@ -428,7 +428,7 @@ class SparseMatOp(LinOp):
         keys = ("kernel", "stream_bytes", "csr_bytes", "slices", "stored_entries",
                 "slices_implicit", "slices_u16", "slices_i32")
         d = dict(zip(keys, (int(v) for v in info)))
-        d["kernel"] = ("csr-stream", "sell", "vector", "dia", "bsr", "sellp", "classes", "xsell")[d["kernel"]]
+        d["kernel"] = ("csr-stream", "sell", "vector", "dia", "bsr", "sellp", "classes", "xsell", "gtc")[d["kernel"]]
         vc = np.zeros(2, np.int64)
         _ck(_lib.amg_csr_value_codes(self.h, vc.ctypes.data_as(vp)))
         d["value_bits"], d["value_table"] = int(vc[0]), int(vc[1])

@@ -28,8 +28,10 @@ def sell_values(path, counter, kernel="spmv_sell_kernel"):
 
 
 def main(fetch_csv, write_csv, known_json, out_json):
+    global N
     known = json.load(open(known_json))
-    kern = "spmv_%s_kernel" % known["fine"]["kernel"]
+    N = known.get("n", N)
+    kern = known.get("kernel", "spmv_%s_kernel" % known["fine"]["kernel"])
     assert known["cal"]["kernel"] == known["fine"]["kernel"], known
     cal_f, fine_f = sell_values(fetch_csv, "FETCH_SIZE", kern)
     cal_w, fine_w = sell_values(write_csv, "WRITE_SIZE", kern)
@@ -38,7 +40,7 @@ def main(fetch_csv, write_csv, known_json, out_json):
     read = statistics.median(fine_f) * factor
     write = statistics.median(fine_w)
     out = {
-        "kernel": kern + "<SET> on A_0 (7-pt 256^3)",
+        "kernel": kern + "<SET> on " + known.get("workload", "A_0 (7-pt 256^3)"),
         "storage": known["fine"],
         "algorithmic_bytes_per_launch": known["fine"]["stream_bytes"] + 16 * N,
         "fetch_correction_factor": round(factor, 4),

@@ -1242,6 +1242,41 @@ def test_fused_grid_transfers(ctx, case):
     del torch
 
 
+@pytest.mark.parametrize("gen,dims", [("7pt", (64, 48, 40)), ("7pt", (67, 45, 39)), ("27pt", (48, 40, 36))])
+def test_grid_transfer_classes(ctx, gen, dims):
+    """gtc.hip: R and P of a 2x2x2-box hierarchy stored as grid-transfer classes
+    (one 8-bit class per row, the coarse / fine window of a grid tile in LDS):
+    y = P v_c, y += P v_c and f_c = R r bitwise equal to the oracle's row sums on
+    every level that takes the storage, odd extents included; the V-cycle (which
+    folds the zero-guess step into P's d*f + P v_c epilogue on the fine level)
+    within 1e-11 of the oracle."""
+    A = (fa().SparseMatOp.laplace3d_7pt(ctx, *dims) if gen == "7pt"
+         else fa().SparseMatOp.aniso27(ctx, *dims, 1.0, 1.0, 0.01))
+    mg = fa().sa_build_box(A, dims, (2, 2, 2), coarsest_dim=100)
+    seen = 0
+    rng = np.random.default_rng(3)
+    for l in range(mg.levels() - 1):
+        _, _, R, P = mg.level(l)
+        for M in (R, P):
+            if M.spmv_info()["kernel"] != "gtc":
+                continue
+            seen += 1
+            OM = O.Csr.from_arrays(*M.dims(), *M.arrays())
+            m, n = M.dims()
+            x, y0 = rng.standard_normal(n), rng.standard_normal(m)
+            assert np.array_equal(apply_dev(ctx, M, x, m), OM.spmv(x)), (l, M.dims())
+            if m > n:  # P: the interpolate-add epilogue
+                yd = T(y0)
+                M.spmv_epilogue("add", T(x), yd)
+                assert np.array_equal(H(yd), y0 + OM.spmv(x))
+    assert seen >= 2, seen
+    assert mg.level(0)[3].spmv_info()["kernel"] == "gtc"
+    b = np.random.default_rng(42).uniform(-1, 1, A.nrows)
+    zref = O.Multigrid(oracle_levels_from_gpu(mg, "jacobi")).apply(b)
+    z = apply_dev(ctx, mg, b, A.nrows)
+    assert np.linalg.norm(z - zref) <= 1e-11 * np.linalg.norm(zref)
+
+
 def test_cycle_plan_accounts_for_every_launch(ctx):
     """amg_multigrid_cycle_plan: the launches of one V-cycle as the library makes
     them.  On the 7-pt box hierarchy the fine level folds its zero-guess step
