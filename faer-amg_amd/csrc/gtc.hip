@@ -9,8 +9,8 @@
 // parity of (x, y, z) (P) or not at all (R), so a row is one 8-bit class id
 // into a dictionary of (step, value) lists.  P_0 of the 256^3 7-point
 // hierarchy: 1 B per row instead of 12.5 B of value-code SELL; 27-point: 1 B
-// instead of ~25 B.  Dictionary entries are 16 bits: the value's index in a
-// table of the operator's distinct values (<= 256) and the step's slot.
+// instead of ~25 B.  Dictionary entries: the value and the step's offset in the
+// kernel's LDS window.
 //
 // Kernels: one workgroup per grid tile stages the tile's column-grid window
 // (the coarse v_c for P, the fine vector for R; 0.0 outside the grid) in LDS,
@@ -122,9 +122,9 @@ constexpr int G_DMAX = 2048;                                      // dictionary 
 
 struct GtcArgs {
     const uint8_t *cls;
-    const uint16_t *dict;  // nclass x ke entries: value index << 8 | slot
-    const double *vtab;    // distinct values
-    int ke, nce, ntab;
+    const double *dval;    // nclass x ke entries: values
+    const int16_t *doff;   //   and window offsets from the row's anchor
+    int ke, nce;
     int rx, ry, rz;        // row grid
     int kx, ky, kz;        // column grid
     int ntx, nty;
@@ -141,9 +141,8 @@ struct GtcArgs {
 template <int MODE>
 __global__ __launch_bounds__(256) void k_gtc_interp(GtcArgs a) {
     __shared__ double win[GP_WX * GP_WY * GP_WZ];
-    __shared__ uint16_t sd[G_DMAX];
-    __shared__ double st[256];
-    __shared__ int16_t lut[27];
+    __shared__ double sv[G_DMAX];
+    __shared__ int16_t so[G_DMAX];
     const int tid = threadIdx.x;
     const int t = xcd_remap(blockIdx.x, gridDim.x);
     const int tix = t % a.ntx, tiy = (t / a.ntx) % a.nty, tiz = t / (a.ntx * a.nty);
@@ -172,24 +171,24 @@ __global__ __launch_bounds__(256) void k_gtc_interp(GtcArgs a) {
         const bool in = (unsigned)X < (unsigned)a.kx && (unsigned)Y < (unsigned)a.ky && (unsigned)Z < (unsigned)a.kz;
         win[q] = in ? a.x[(int64_t)Z * cplane + (int64_t)Y * a.kx + X] : 0.0;
     }
-    for (int q = tid; q < a.nce; q += 256) sd[q] = a.dict[q];
-    if (tid < a.ntab) st[tid] = a.vtab[tid];
-    if (tid < 27) lut[tid] = (int16_t)(((tid / 9 - 1) * GP_WY + (tid / 3) % 3 - 1) * GP_WX + tid % 3 - 1);
+    for (int q = tid; q < a.nce; q += 256) {
+        sv[q] = a.dval[q];
+        so[q] = a.doff[q];
+    }
     __syncthreads();
 #pragma unroll
     for (int j = 0; j < GP_TZ; j++) {
         if (!live[j]) continue;
         const int gz = z0 + j;
         const int base = (((gz >> 1) - wz0) * GP_WY + (gy >> 1) - wy0) * GP_WX + (gx >> 1) - wx0;
-        const uint16_t *e = sd + cl[j] * a.ke;
+        const int e = cl[j] * a.ke;
         double acc = 0.0;
         for (int k = 0; k < a.ke; k += 4) {
             double v[4], w[4];
 #pragma unroll
             for (int u = 0; u < 4; u++) {
-                const uint16_t c = e[k + u];
-                v[u] = st[c >> 8];
-                w[u] = win[base + lut[c & 255]];
+                v[u] = sv[e + k + u];
+                w[u] = win[base + so[e + k + u]];
             }
 #pragma unroll
             for (int u = 0; u < 4; u++) acc = fma(v[u], w[u], acc);
@@ -204,9 +203,8 @@ __global__ __launch_bounds__(256) void k_gtc_interp(GtcArgs a) {
 // 34 x 18 x 6 around their boxes in LDS.
 __global__ __launch_bounds__(256) void k_gtc_restrict(GtcArgs a) {
     __shared__ double win[GR_WX * GR_WY * GR_WZ];
-    __shared__ uint16_t sd[G_DMAX];
-    __shared__ double st[256];
-    __shared__ int16_t lut[64];
+    __shared__ double sv[G_DMAX];
+    __shared__ int16_t so[G_DMAX];
     const int tid = threadIdx.x;
     const int t = xcd_remap(blockIdx.x, gridDim.x);
     const int tix = t % a.ntx, tiy = (t / a.ntx) % a.nty, tiz = t / (a.ntx * a.nty);
@@ -230,21 +228,21 @@ __global__ __launch_bounds__(256) void k_gtc_restrict(GtcArgs a) {
 #pragma unroll
     for (int u = 0; u < PF; u++)
         if (tid + 256 * u < W) win[tid + 256 * u] = v[u];
-    for (int q = tid; q < a.nce; q += 256) sd[q] = a.dict[q];
-    if (tid < a.ntab) st[tid] = a.vtab[tid];
-    if (tid < 64) lut[tid] = (int16_t)(((tid / 16 - 1) * GR_WY + (tid / 4) % 4 - 1) * GR_WX + tid % 4 - 1);
+    for (int q = tid; q < a.nce; q += 256) {
+        sv[q] = a.dval[q];
+        so[q] = a.doff[q];
+    }
     __syncthreads();
     if (!live) return;
     const int base = ((2 * lz + 1) * GR_WY + 2 * ly + 1) * GR_WX + 2 * lx + 1;
-    const uint16_t *e = sd + c * a.ke;
+    const int e = c * a.ke;
     double acc = 0.0;
     for (int k = 0; k < a.ke; k += 8) {
         double cv[8], w[8];
 #pragma unroll
         for (int u = 0; u < 8; u++) {
-            const uint16_t q = e[k + u];
-            cv[u] = st[q >> 8];
-            w[u] = win[base + lut[q & 255]];
+            cv[u] = sv[e + k + u];
+            w[u] = win[base + so[e + k + u]];
         }
 #pragma unroll
         for (int u = 0; u < 8; u++) acc = fma(cv[u], w[u], acc);
@@ -256,9 +254,9 @@ __global__ __launch_bounds__(256) void k_gtc_restrict(GtcArgs a) {
 
 void gtc_release(GpuCsr &m) {
     m.gtc_cls.release();
-    m.gtc_dict.release();
-    m.gtc_vtab.release();
-    m.gtc_ke = m.gtc_nce = m.gtc_ntab = 0;
+    m.gtc_val.release();
+    m.gtc_off.release();
+    m.gtc_ke = m.gtc_nce = 0;
     m.gtc_r = m.gtc_on = false;
 }
 
@@ -278,48 +276,35 @@ bool gtc_attach(GpuCsr &m, const int64_t *fg, const int64_t *cg) {
     std::vector<uint8_t> cls;
     std::vector<std::vector<std::pair<uint8_t, double>>> dict;
     if (!gtc_classes(m, is_r, fg, cg, cls, dict)) return false;
-    // distinct values (bit patterns), <= 256
-    std::vector<uint64_t> vals;
-    for (const auto &d : dict)
-        for (const auto &e : d) {
-            uint64_t b;
-            std::memcpy(&b, &e.second, 8);
-            vals.push_back(b);
-        }
-    vals.push_back(0);  // +0.0 for the padding entries
-    std::sort(vals.begin(), vals.end());
-    vals.erase(std::unique(vals.begin(), vals.end()), vals.end());
-    if (vals.size() > 256) return false;
     const int gran = is_r ? 8 : 4;
     size_t ke = 1;
     for (const auto &d : dict) ke = std::max(ke, d.size());
     ke = (ke + gran - 1) / gran * gran;
     if (dict.size() * ke > (size_t)G_DMAX) return false;
-    const uint16_t zero_idx = (uint16_t)(std::lower_bound(vals.begin(), vals.end(), 0ull) - vals.begin());
-    const uint16_t centre = is_r ? (uint16_t)(16 + 4 + 1) : (uint16_t)(9 + 3 + 1);
-    // padding: +0.0 at the anchor (after the row's entries: a +0.0 term leaves
-    // the accumulator unchanged)
-    std::vector<uint16_t> hd(dict.size() * ke, (uint16_t)(zero_idx << 8 | centre));
+    // entries: value and window offset from the anchor (the kernels' window
+    // shapes); padding: +0.0 at the anchor (after the row's entries: a +0.0
+    // term leaves the accumulator unchanged)
+    auto off = [&](int sl) {
+        if (is_r) return ((sl / 16 - 1) * GR_WY + (sl / 4) % 4 - 1) * GR_WX + sl % 4 - 1;
+        return ((sl / 9 - 1) * GP_WY + (sl / 3) % 3 - 1) * GP_WX + sl % 3 - 1;
+    };
+    std::vector<double> hv(dict.size() * ke, 0.0);
+    std::vector<int16_t> ho(dict.size() * ke, 0);
     for (size_t c = 0; c < dict.size(); c++)
         for (size_t k = 0; k < dict[c].size(); k++) {
-            uint64_t b;
-            std::memcpy(&b, &dict[c][k].second, 8);
-            const uint16_t vi = (uint16_t)(std::lower_bound(vals.begin(), vals.end(), b) - vals.begin());
-            hd[c * ke + k] = (uint16_t)(vi << 8 | dict[c][k].first);
+            hv[c * ke + k] = dict[c][k].second;
+            ho[c * ke + k] = (int16_t)off(dict[c][k].first);
         }
-    std::vector<double> vt(vals.size());
-    for (size_t q = 0; q < vals.size(); q++) std::memcpy(&vt[q], &vals[q], 8);
     hipStream_t s = m.ctx->stream;
     m.gtc_cls.resize(cls.size());
-    m.gtc_dict.resize(hd.size());
-    m.gtc_vtab.resize(vt.size());
+    m.gtc_val.resize(hv.size());
+    m.gtc_off.resize(ho.size());
     FAMG_CHECK_HIP(hipMemcpyAsync(m.gtc_cls.get(), cls.data(), cls.size(), hipMemcpyHostToDevice, s));
-    FAMG_CHECK_HIP(hipMemcpyAsync(m.gtc_dict.get(), hd.data(), hd.size() * 2, hipMemcpyHostToDevice, s));
-    FAMG_CHECK_HIP(hipMemcpyAsync(m.gtc_vtab.get(), vt.data(), vt.size() * 8, hipMemcpyHostToDevice, s));
+    FAMG_CHECK_HIP(hipMemcpyAsync(m.gtc_val.get(), hv.data(), hv.size() * 8, hipMemcpyHostToDevice, s));
+    FAMG_CHECK_HIP(hipMemcpyAsync(m.gtc_off.get(), ho.data(), ho.size() * 2, hipMemcpyHostToDevice, s));
     FAMG_CHECK_HIP(hipStreamSynchronize(s));
     m.gtc_ke = (int)ke;
     m.gtc_nce = (int)(dict.size() * ke);
-    m.gtc_ntab = (int)vt.size();
     m.gtc_r = is_r;
     for (int q = 0; q < 3; q++) {
         m.gtc_fg[q] = fg[q];
@@ -336,11 +321,10 @@ bool gtc_supports(const GpuCsr &m, SpmvMode mode) {
 void spmv_gtc(const GpuCsr &m, const double *x, double *y, SpmvMode mode, const SpmvEpi &epi, hipStream_t s) {
     GtcArgs a{};
     a.cls = m.gtc_cls.get();
-    a.dict = m.gtc_dict.get();
-    a.vtab = m.gtc_vtab.get();
+    a.dval = m.gtc_val.get();
+    a.doff = m.gtc_off.get();
     a.ke = m.gtc_ke;
     a.nce = m.gtc_nce;
-    a.ntab = m.gtc_ntab;
     const int64_t *rg = m.gtc_r ? m.gtc_cg : m.gtc_fg, *kg = m.gtc_r ? m.gtc_fg : m.gtc_cg;
     a.rx = (int)rg[0]; a.ry = (int)rg[1]; a.rz = (int)rg[2];
     a.kx = (int)kg[0]; a.ky = (int)kg[1]; a.kz = (int)kg[2];

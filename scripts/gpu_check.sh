@@ -48,6 +48,11 @@ for s in "$@"; do
         ptk) step ptk 600 python -u -m pytest tests -m gpu -v --timeout 120 --timeout-method thread -k "$PTK" ;;
         absgs) step absgs 900 bash scripts/ab_sgs27.sh ;;
         bench27g) step bench27g 600 python bench.py --problem 27pt --smoother sgs --steps 10 --warmup 2 --no-cpu-baseline --no-general ;;
+        pmcbsr) export TMPDIR=/tmp; R=$(pwd)
+              step pmcbsr_fetch 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d "$R/gpurun_out/pmcbsr_fetch" -o run \
+                  --output-format csv -- python3 "$R/scripts/pmc_bsr.py"
+              step pmcbsr_write 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d "$R/gpurun_out/pmcbsr_write" -o run \
+                  --output-format csv -- python3 "$R/scripts/pmc_bsr.py" ;;
         smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
         bench) step bench 600 python bench.py --steps 20 --warmup 3 ;;
         benchq) step bench 400 python bench.py --steps 20 --warmup 3 --no-cpu-baseline --ab ;;

@@ -28,7 +28,7 @@ n = A.nrows
 nodes = n // 3
 rp = np.arange(0, 9 * nodes + 1, 3, dtype=np.int64)
 ci = np.repeat(np.arange(n, dtype=np.int64).reshape(nodes, 3), 3, axis=0).reshape(-1)
-va = np.tile(np.array([4.0, 1.0, 0.5, 1.0, 4.0, 1.0, 0.5, 1.0, 4.0]), nodes)
+va = np.random.default_rng(1).uniform(0.5, 1.5, 9 * nodes)  # > 65536 distinct values: no value codes
 B = fa.SparseMatOp.from_arrays(ctx, n, n, rp, ci, va)
 assert B.spmv_info()["kernel"] == "bsr" and A.spmv_info()["kernel"] == "bsr", (B.spmv_info(), A.spmv_info())
 x = torch.as_tensor(np.random.default_rng(0).uniform(-1, 1, n), device="cuda:0")
