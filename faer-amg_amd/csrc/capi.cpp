@@ -259,7 +259,7 @@ amg_status amg_csr_spmv_info(const amg_linop *op, int64_t *info8) {
         }
         if (m.gtc_on) {  // the grid-transfer overlay (its modes; the storage above serves the rest)
             info8[0] = SPMV_KERNEL_GTC;
-            info8[1] = m.nrows + 10 * (int64_t)m.gtc_nce;
+            info8[1] = m.nrows + 2 * (int64_t)m.gtc_nce + 8 * (int64_t)m.gtc_ntab;
         }
     });
 }

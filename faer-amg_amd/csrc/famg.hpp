@@ -122,9 +122,9 @@ struct GpuCsr {
     // on the finalized storage used for the modes it supports (gtc_supports)
     bool gtc_on = false, gtc_r = false;
     DevBuf<uint8_t> gtc_cls;
-    DevBuf<double> gtc_val;
-    DevBuf<int16_t> gtc_off;
-    int gtc_ke = 0, gtc_nce = 0;
+    DevBuf<uint16_t> gtc_dict;  // nclass x ke entries: value index << 8 | step slot
+    DevBuf<double> gtc_vtab;    // the distinct values (<= 256)
+    int gtc_ke = 0, gtc_nce = 0, gtc_ntab = 0;
     int64_t gtc_fg[3] = {0, 0, 0}, gtc_cg[3] = {0, 0, 0};
     // grid hint: the rows are the points of an nx x ny x nz grid, x fastest (0 = none);
     // set by the stencil generators, the box hierarchy and amg_csr_set_grid

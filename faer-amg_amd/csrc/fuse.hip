@@ -108,9 +108,22 @@ __global__ __launch_bounds__(256) void k_fuse_resid_restrict(FuseArgs a) {
     __shared__ double sval[F_DMAX];
     __shared__ int16_t soff[F_DMAX];
     const int tid = threadIdx.x;
-    for (int q = tid; q < a.nce; q += 256) {
-        sval[q] = a.cval[q];
-        soff[q] = a.coff[q];
+    {  // class dictionary: all loads of a lane before its stores
+        constexpr int PF = F_DMAX / 256;
+        double v[PF];
+        int16_t o[PF];
+#pragma unroll
+        for (int u = 0; u < PF; u++) {
+            const int q = min(tid + 256 * u, a.nce - 1);
+            v[u] = a.cval[q];
+            o[u] = a.coff[q];
+        }
+#pragma unroll
+        for (int u = 0; u < PF; u++)
+            if (tid + 256 * u < a.nce) {
+                sval[tid + 256 * u] = v[u];
+                soff[tid + 256 * u] = o[u];
+            }
     }
     const int t = xcd_remap(blockIdx.x, gridDim.x);
     const int tix = t % a.ntx, tiy = (t / a.ntx) % a.nty, tiz = t / (a.ntx * a.nty);
@@ -241,9 +254,22 @@ __global__ __launch_bounds__(256) void k_fuse_interp_jacobi(FuseArgs a) {
     __shared__ double sval[F_DMAX];
     __shared__ int16_t soff[F_DMAX];
     const int tid = threadIdx.x;
-    for (int q = tid; q < a.nce; q += 256) {
-        sval[q] = a.cval[q];
-        soff[q] = a.coff[q];
+    {  // class dictionary: all loads of a lane before its stores
+        constexpr int PF = F_DMAX / 256;
+        double v[PF];
+        int16_t o[PF];
+#pragma unroll
+        for (int u = 0; u < PF; u++) {
+            const int q = min(tid + 256 * u, a.nce - 1);
+            v[u] = a.cval[q];
+            o[u] = a.coff[q];
+        }
+#pragma unroll
+        for (int u = 0; u < PF; u++)
+            if (tid + 256 * u < a.nce) {
+                sval[tid + 256 * u] = v[u];
+                soff[tid + 256 * u] = o[u];
+            }
     }
     const int t = xcd_remap(blockIdx.x, gridDim.x);
     const int tix = t % a.ntx, tiy = (t / a.ntx) % a.nty, tiz = t / (a.ntx * a.nty);

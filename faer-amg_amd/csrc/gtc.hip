@@ -9,8 +9,8 @@
 // parity of (x, y, z) (P) or not at all (R), so a row is one 8-bit class id
 // into a dictionary of (step, value) lists.  P_0 of the 256^3 7-point
 // hierarchy: 1 B per row instead of 12.5 B of value-code SELL; 27-point: 1 B
-// instead of ~25 B.  Dictionary entries: the value and the step's offset in the
-// kernel's LDS window.
+// instead of ~25 B.  Dictionary entries are 16 bits: the value's index in a
+// table of the operator's distinct values (<= 256) and the step's slot.
 //
 // Kernels: one workgroup per grid tile stages the tile's column-grid window
 // (the coarse v_c for P, the fine vector for R; 0.0 outside the grid) in LDS,
@@ -114,17 +114,17 @@ bool gtc_classes(const GpuCsr &M, bool is_r, const int64_t *fg, const int64_t *c
 
 // ------------------------------------------------------------ kernels
 
-constexpr int GP_TX = 32, GP_TY = 8, GP_TZ = 4;                  // P: fine tile (4 rows per lane along z)
-constexpr int GP_WX = GP_TX / 2 + 2, GP_WY = GP_TY / 2 + 2, GP_WZ = GP_TZ / 2 + 2;  // coarse window 18 x 6 x 4
+constexpr int GP_TX = 32, GP_TY = 8;                             // P: fine tile (TZ rows per lane along z)
+constexpr int GP_WX = GP_TX / 2 + 2, GP_WY = GP_TY / 2 + 2;      // coarse window 18 x 6 x (TZ/2 + 2)
 constexpr int GR_TX = 16, GR_TY = 8, GR_TZ = 2;                  // R: coarse tile (one row per lane)
 constexpr int GR_WX = 2 * GR_TX + 2, GR_WY = 2 * GR_TY + 2, GR_WZ = 2 * GR_TZ + 2;  // fine window 34 x 18 x 6
 constexpr int G_DMAX = 2048;                                      // dictionary entries (nclass * ke)
 
 struct GtcArgs {
     const uint8_t *cls;
-    const double *dval;    // nclass x ke entries: values
-    const int16_t *doff;   //   and window offsets from the row's anchor
-    int ke, nce;
+    const uint16_t *dict;  // nclass x ke entries: value index << 8 | slot
+    const double *vtab;    // distinct values
+    int ke, nce, ntab;
     int rx, ry, rz;        // row grid
     int kx, ky, kz;        // column grid
     int ntx, nty;
@@ -136,13 +136,30 @@ struct GtcArgs {
     const double *dt;
 };
 
+// The class dictionary and value table into LDS: every load of a lane issued
+// before its stores (a load-wait-store loop serialises one memory latency per
+// trip: 4 trips cost P_0 of the 256^3 cycle ~20 us)
+__device__ __forceinline__ void gtc_stage_dict(const GtcArgs &a, uint16_t *sd, double *st) {
+    constexpr int PF = G_DMAX / 256;
+    uint16_t v[PF];
+#pragma unroll
+    for (int u = 0; u < PF; u++) v[u] = a.dict[min((int)threadIdx.x + 256 * u, a.nce - 1)];
+    const double t = a.vtab[min((int)threadIdx.x, a.ntab - 1)];
+#pragma unroll
+    for (int u = 0; u < PF; u++)
+        if ((int)threadIdx.x + 256 * u < a.nce) sd[threadIdx.x + 256 * u] = v[u];
+    if ((int)threadIdx.x < a.ntab) st[threadIdx.x] = t;
+}
+
 // P v_c over a fine tile of 32 x 8 x 4 points: lane (x, y) of the tile takes
 // its four points along z; the coarse window 18 x 6 x 4 around them in LDS.
-template <int MODE>
+template <int MODE, int GP_TZ>
 __global__ __launch_bounds__(256) void k_gtc_interp(GtcArgs a) {
+    constexpr int GP_WZ = GP_TZ / 2 + 2;
     __shared__ double win[GP_WX * GP_WY * GP_WZ];
-    __shared__ double sv[G_DMAX];
-    __shared__ int16_t so[G_DMAX];
+    __shared__ uint16_t sd[G_DMAX];
+    __shared__ double st[256];
+    __shared__ int16_t lut[27];
     const int tid = threadIdx.x;
     const int t = xcd_remap(blockIdx.x, gridDim.x);
     const int tix = t % a.ntx, tiy = (t / a.ntx) % a.nty, tiz = t / (a.ntx * a.nty);
@@ -151,9 +168,12 @@ __global__ __launch_bounds__(256) void k_gtc_interp(GtcArgs a) {
     const int64_t fplane = (int64_t)a.rx * a.ry, cplane = (int64_t)a.kx * a.ky;
     // the rows' class ids and epilogue operands first
     const int lx = tid % GP_TX, ly = tid / GP_TX, gx = x0 + lx, gy = y0 + ly;
-    int cl[GP_TZ];
+    __shared__ double sdt[256];  // the coded Jacobi diagonal's table (ADD0)
+    int cl[GP_TZ], dci[GP_TZ];
     double yb[GP_TZ];
     bool live[GP_TZ];
+    if constexpr (MODE == SPMV_ADD0)
+        if (a.dc) sdt[tid] = a.dt[tid];
 #pragma unroll
     for (int j = 0; j < GP_TZ; j++) {
         const int gz = z0 + j;
@@ -163,7 +183,11 @@ __global__ __launch_bounds__(256) void k_gtc_interp(GtcArgs a) {
         yb[j] = 0.0;
         if (live[j]) {
             if constexpr (MODE == SPMV_ADD) yb[j] = a.y[i];
-            if constexpr (MODE == SPMV_ADD0) yb[j] = (a.dc ? a.dt[a.dc[i]] : a.d[i]) * a.b[i];  // d*b
+            if constexpr (MODE == SPMV_ADD0) {
+                yb[j] = a.b[i];
+                if (a.dc) dci[j] = a.dc[i];
+                else yb[j] = a.d[i] * yb[j];  // d*b
+            }
         }
     }
     for (int q = tid; q < GP_WX * GP_WY * GP_WZ; q += 256) {
@@ -171,24 +195,25 @@ __global__ __launch_bounds__(256) void k_gtc_interp(GtcArgs a) {
         const bool in = (unsigned)X < (unsigned)a.kx && (unsigned)Y < (unsigned)a.ky && (unsigned)Z < (unsigned)a.kz;
         win[q] = in ? a.x[(int64_t)Z * cplane + (int64_t)Y * a.kx + X] : 0.0;
     }
-    for (int q = tid; q < a.nce; q += 256) {
-        sv[q] = a.dval[q];
-        so[q] = a.doff[q];
-    }
+    gtc_stage_dict(a, sd, st);
+    if (tid < 27) lut[tid] = (int16_t)(((tid / 9 - 1) * GP_WY + (tid / 3) % 3 - 1) * GP_WX + tid % 3 - 1);
     __syncthreads();
 #pragma unroll
     for (int j = 0; j < GP_TZ; j++) {
         if (!live[j]) continue;
+        if constexpr (MODE == SPMV_ADD0)
+            if (a.dc) yb[j] = sdt[dci[j]] * yb[j];  // d*b, d decoded after the barrier
         const int gz = z0 + j;
         const int base = (((gz >> 1) - wz0) * GP_WY + (gy >> 1) - wy0) * GP_WX + (gx >> 1) - wx0;
-        const int e = cl[j] * a.ke;
+        const uint16_t *e = sd + cl[j] * a.ke;
         double acc = 0.0;
         for (int k = 0; k < a.ke; k += 4) {
             double v[4], w[4];
 #pragma unroll
             for (int u = 0; u < 4; u++) {
-                v[u] = sv[e + k + u];
-                w[u] = win[base + so[e + k + u]];
+                const uint16_t c = e[k + u];
+                v[u] = st[c >> 8];
+                w[u] = win[base + lut[c & 255]];
             }
 #pragma unroll
             for (int u = 0; u < 4; u++) acc = fma(v[u], w[u], acc);
@@ -203,8 +228,9 @@ __global__ __launch_bounds__(256) void k_gtc_interp(GtcArgs a) {
 // 34 x 18 x 6 around their boxes in LDS.
 __global__ __launch_bounds__(256) void k_gtc_restrict(GtcArgs a) {
     __shared__ double win[GR_WX * GR_WY * GR_WZ];
-    __shared__ double sv[G_DMAX];
-    __shared__ int16_t so[G_DMAX];
+    __shared__ uint16_t sd[G_DMAX];
+    __shared__ double st[256];
+    __shared__ int16_t lut[64];
     const int tid = threadIdx.x;
     const int t = xcd_remap(blockIdx.x, gridDim.x);
     const int tix = t % a.ntx, tiy = (t / a.ntx) % a.nty, tiz = t / (a.ntx * a.nty);
@@ -228,21 +254,20 @@ __global__ __launch_bounds__(256) void k_gtc_restrict(GtcArgs a) {
 #pragma unroll
     for (int u = 0; u < PF; u++)
         if (tid + 256 * u < W) win[tid + 256 * u] = v[u];
-    for (int q = tid; q < a.nce; q += 256) {
-        sv[q] = a.dval[q];
-        so[q] = a.doff[q];
-    }
+    gtc_stage_dict(a, sd, st);
+    if (tid < 64) lut[tid] = (int16_t)(((tid / 16 - 1) * GR_WY + (tid / 4) % 4 - 1) * GR_WX + tid % 4 - 1);
     __syncthreads();
     if (!live) return;
     const int base = ((2 * lz + 1) * GR_WY + 2 * ly + 1) * GR_WX + 2 * lx + 1;
-    const int e = c * a.ke;
+    const uint16_t *e = sd + c * a.ke;
     double acc = 0.0;
     for (int k = 0; k < a.ke; k += 8) {
         double cv[8], w[8];
 #pragma unroll
         for (int u = 0; u < 8; u++) {
-            cv[u] = sv[e + k + u];
-            w[u] = win[base + so[e + k + u]];
+            const uint16_t q = e[k + u];
+            cv[u] = st[q >> 8];
+            w[u] = win[base + lut[q & 255]];
         }
 #pragma unroll
         for (int u = 0; u < 8; u++) acc = fma(cv[u], w[u], acc);
@@ -254,9 +279,9 @@ __global__ __launch_bounds__(256) void k_gtc_restrict(GtcArgs a) {
 
 void gtc_release(GpuCsr &m) {
     m.gtc_cls.release();
-    m.gtc_val.release();
-    m.gtc_off.release();
-    m.gtc_ke = m.gtc_nce = 0;
+    m.gtc_dict.release();
+    m.gtc_vtab.release();
+    m.gtc_ke = m.gtc_nce = m.gtc_ntab = 0;
     m.gtc_r = m.gtc_on = false;
 }
 
@@ -276,35 +301,48 @@ bool gtc_attach(GpuCsr &m, const int64_t *fg, const int64_t *cg) {
     std::vector<uint8_t> cls;
     std::vector<std::vector<std::pair<uint8_t, double>>> dict;
     if (!gtc_classes(m, is_r, fg, cg, cls, dict)) return false;
+    // distinct values (bit patterns), <= 256
+    std::vector<uint64_t> vals;
+    for (const auto &d : dict)
+        for (const auto &e : d) {
+            uint64_t b;
+            std::memcpy(&b, &e.second, 8);
+            vals.push_back(b);
+        }
+    vals.push_back(0);  // +0.0 for the padding entries
+    std::sort(vals.begin(), vals.end());
+    vals.erase(std::unique(vals.begin(), vals.end()), vals.end());
+    if (vals.size() > 256) return false;
     const int gran = is_r ? 8 : 4;
     size_t ke = 1;
     for (const auto &d : dict) ke = std::max(ke, d.size());
     ke = (ke + gran - 1) / gran * gran;
     if (dict.size() * ke > (size_t)G_DMAX) return false;
-    // entries: value and window offset from the anchor (the kernels' window
-    // shapes); padding: +0.0 at the anchor (after the row's entries: a +0.0
-    // term leaves the accumulator unchanged)
-    auto off = [&](int sl) {
-        if (is_r) return ((sl / 16 - 1) * GR_WY + (sl / 4) % 4 - 1) * GR_WX + sl % 4 - 1;
-        return ((sl / 9 - 1) * GP_WY + (sl / 3) % 3 - 1) * GP_WX + sl % 3 - 1;
-    };
-    std::vector<double> hv(dict.size() * ke, 0.0);
-    std::vector<int16_t> ho(dict.size() * ke, 0);
+    const uint16_t zero_idx = (uint16_t)(std::lower_bound(vals.begin(), vals.end(), 0ull) - vals.begin());
+    const uint16_t centre = is_r ? (uint16_t)(16 + 4 + 1) : (uint16_t)(9 + 3 + 1);
+    // padding: +0.0 at the anchor (after the row's entries: a +0.0 term leaves
+    // the accumulator unchanged)
+    std::vector<uint16_t> hd(dict.size() * ke, (uint16_t)(zero_idx << 8 | centre));
     for (size_t c = 0; c < dict.size(); c++)
         for (size_t k = 0; k < dict[c].size(); k++) {
-            hv[c * ke + k] = dict[c][k].second;
-            ho[c * ke + k] = (int16_t)off(dict[c][k].first);
+            uint64_t b;
+            std::memcpy(&b, &dict[c][k].second, 8);
+            const uint16_t vi = (uint16_t)(std::lower_bound(vals.begin(), vals.end(), b) - vals.begin());
+            hd[c * ke + k] = (uint16_t)(vi << 8 | dict[c][k].first);
         }
+    std::vector<double> vt(vals.size());
+    for (size_t q = 0; q < vals.size(); q++) std::memcpy(&vt[q], &vals[q], 8);
     hipStream_t s = m.ctx->stream;
     m.gtc_cls.resize(cls.size());
-    m.gtc_val.resize(hv.size());
-    m.gtc_off.resize(ho.size());
+    m.gtc_dict.resize(hd.size());
+    m.gtc_vtab.resize(vt.size());
     FAMG_CHECK_HIP(hipMemcpyAsync(m.gtc_cls.get(), cls.data(), cls.size(), hipMemcpyHostToDevice, s));
-    FAMG_CHECK_HIP(hipMemcpyAsync(m.gtc_val.get(), hv.data(), hv.size() * 8, hipMemcpyHostToDevice, s));
-    FAMG_CHECK_HIP(hipMemcpyAsync(m.gtc_off.get(), ho.data(), ho.size() * 2, hipMemcpyHostToDevice, s));
+    FAMG_CHECK_HIP(hipMemcpyAsync(m.gtc_dict.get(), hd.data(), hd.size() * 2, hipMemcpyHostToDevice, s));
+    FAMG_CHECK_HIP(hipMemcpyAsync(m.gtc_vtab.get(), vt.data(), vt.size() * 8, hipMemcpyHostToDevice, s));
     FAMG_CHECK_HIP(hipStreamSynchronize(s));
     m.gtc_ke = (int)ke;
     m.gtc_nce = (int)(dict.size() * ke);
+    m.gtc_ntab = (int)vt.size();
     m.gtc_r = is_r;
     for (int q = 0; q < 3; q++) {
         m.gtc_fg[q] = fg[q];
@@ -314,6 +352,15 @@ bool gtc_attach(GpuCsr &m, const int64_t *fg, const int64_t *cg) {
     return true;
 }
 
+// fine points per lane along z in the P kernel (FAMG_GTC_TZ=8: eight)
+static int gtc_tz() {
+    static const int v = [] {
+        const char *e = getenv("FAMG_GTC_TZ");
+        return (e && e[0] == '8') ? 8 : 4;
+    }();
+    return v;
+}
+
 bool gtc_supports(const GpuCsr &m, SpmvMode mode) {
     return m.gtc_r ? mode == SPMV_SET : (mode == SPMV_SET || mode == SPMV_ADD || mode == SPMV_ADD0);
 }
@@ -321,10 +368,11 @@ bool gtc_supports(const GpuCsr &m, SpmvMode mode) {
 void spmv_gtc(const GpuCsr &m, const double *x, double *y, SpmvMode mode, const SpmvEpi &epi, hipStream_t s) {
     GtcArgs a{};
     a.cls = m.gtc_cls.get();
-    a.dval = m.gtc_val.get();
-    a.doff = m.gtc_off.get();
+    a.dict = m.gtc_dict.get();
+    a.vtab = m.gtc_vtab.get();
     a.ke = m.gtc_ke;
     a.nce = m.gtc_nce;
+    a.ntab = m.gtc_ntab;
     const int64_t *rg = m.gtc_r ? m.gtc_cg : m.gtc_fg, *kg = m.gtc_r ? m.gtc_fg : m.gtc_cg;
     a.rx = (int)rg[0]; a.ry = (int)rg[1]; a.rz = (int)rg[2];
     a.kx = (int)kg[0]; a.ky = (int)kg[1]; a.kz = (int)kg[2];
@@ -343,14 +391,19 @@ void spmv_gtc(const GpuCsr &m, const double *x, double *y, SpmvMode mode, const 
     } else {
         a.ntx = (int)ceil_div(a.rx, GP_TX);
         a.nty = (int)ceil_div(a.ry, GP_TY);
-        const int ntz = (int)ceil_div(a.rz, GP_TZ);
+        const int tz = gtc_tz();
+        const int ntz = (int)ceil_div(a.rz, tz);
         const dim3 grid((unsigned)((int64_t)a.ntx * a.nty * ntz)), block(256);
-        switch (mode) {
-        case SPMV_SET: k_gtc_interp<SPMV_SET><<<grid, block, 0, s>>>(a); break;
-        case SPMV_ADD: k_gtc_interp<SPMV_ADD><<<grid, block, 0, s>>>(a); break;
-        case SPMV_ADD0: k_gtc_interp<SPMV_ADD0><<<grid, block, 0, s>>>(a); break;
-        default: fail(AMG_ERR_UNSUPPORTED, "grid-transfer P: unsupported SpMV epilogue");
-        }
+#define FAMG_GTCI(TZ)                                                                              \
+    switch (mode) {                                                                                \
+    case SPMV_SET: k_gtc_interp<SPMV_SET, TZ><<<grid, block, 0, s>>>(a); break;                    \
+    case SPMV_ADD: k_gtc_interp<SPMV_ADD, TZ><<<grid, block, 0, s>>>(a); break;                    \
+    case SPMV_ADD0: k_gtc_interp<SPMV_ADD0, TZ><<<grid, block, 0, s>>>(a); break;                  \
+    default: fail(AMG_ERR_UNSUPPORTED, "grid-transfer P: unsupported SpMV epilogue");              \
+    }
+        if (tz == 8) { FAMG_GTCI(8) }
+        else { FAMG_GTCI(4) }
+#undef FAMG_GTCI
     }
     FAMG_CHECK_HIP(hipGetLastError());
 }

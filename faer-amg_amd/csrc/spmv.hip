@@ -2359,7 +2359,7 @@ static void log_spmv(const GpuCsr &m, SpmvMode mode, const SpmvEpi &epi, int64_t
     if (m.gtc_on && seg < 0 && gtc_supports(m, mode)) {
         kernel = SPMV_KERNEL_GTC;
         name = "gtc";
-        mat = m.nrows + 10 * (int64_t)m.gtc_nce;
+        mat = m.nrows + 2 * (int64_t)m.gtc_nce + 8 * (int64_t)m.gtc_ntab;
     } else if (m.kernel == SPMV_KERNEL_BSR) {
         name = "bsr3";
         mat = part(m.stream_bytes());

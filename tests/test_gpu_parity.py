@@ -849,11 +849,11 @@ def test_dia_pattern33(ctx):
 def test_vcycle_256_storage_mix(ctx):
     """The benchmark configuration itself (C2: 7-pt 256^3, SA 2^3 boxes, Jacobi,
     6 levels) against the oracle on the same hierarchy, so the exact storage mix
-    the bench times is what is checked: DIA codes on A_0, 4-bit-coded pattern
-    SELL on R_0 (row bases, implicit columns), 4-bit SELL with u16 column deltas
-    on P_0, 8-bit DIA codes in the 33-diagonal run pattern on A_1, stencil classes on A_2 (2197 classes),
-    16-bit codes on R_1/P_1, stencil classes with one row per wave on A_3,
-    the wave-per-row kernel on A_4.  One
+    the bench times is what is checked: DIA codes on A_0, grid-transfer classes
+    on R_0 and P_0 (one 8-bit class per row; the folded d*f + P v_c epilogue),
+    8-bit DIA codes in the 33-diagonal run pattern on A_1, x-staged stencil
+    classes on A_2 (2197 classes) and A_3, 16-bit codes on R_1/P_1, the
+    wave-per-row kernel on A_4.  One
     V-cycle to 1e-11 and 10 stationary cycles (rho_k) to 1e-8 (+ noise floor).
     The oracle runs its ParSpmmOp restatement on 16 threads (same per-row order
     as the sequential CSR)."""
@@ -866,12 +866,11 @@ def test_vcycle_256_storage_mix(ctx):
              mg.level(l)[3].spmv_info() if l < 5 else None) for l in range(6)]
     a0, r0, p0 = info[0]
     assert a0["kernel"] == "dia" and a0["value_bits"] == 4
-    assert r0["kernel"] == "sellp" and r0["value_bits"] == 4
-    assert p0["kernel"] == "sell" and p0["value_bits"] == 4 and p0["slices_u16"] > 0
+    assert r0["kernel"] == "gtc" and p0["kernel"] == "gtc"
     assert info[1][0]["kernel"] == "dia" and info[1][0]["value_bits"] == 8 and info[1][0]["dia_diagonals"] == 33
-    assert info[2][0]["kernel"] == "classes" and info[2][0]["classes"] == 2197
+    assert info[2][0]["kernel"] == "classes" and info[2][0]["classes"] == 2197 and info[2][0]["xstaged"]
     assert info[1][1]["value_bits"] == 16 and info[1][2]["value_bits"] == 16
-    assert info[3][0]["kernel"] == "classes" and info[4][0]["kernel"] == "vector"
+    assert info[3][0]["kernel"] == "classes" and info[3][0]["xstaged"] and info[4][0]["kernel"] == "vector"
     levels = oracle_levels_from_gpu(mg, "jacobi")
     import sys
     sys.path.insert(0, GOLD)
