@@ -90,6 +90,33 @@ static void storage_check(GpuCsr &m) {
             (long)m.ncols, (long)m.nnz, (int)k, (long)bad, (long)first);
 }
 
+// Time y = A x (SET) on scratch vectors with m's DIA codes and with its x-staged
+// stencil classes (3 launches each after one warm-up); true if the classes win.
+// Both sum every row in the same order: the choice changes no result.
+static bool xscs_beats_dia(GpuCsr &m) {
+    if (const char *e = getenv("FAMG_XSCS_VS_DIA")) return e[0] == '1';
+    hipStream_t s = m.ctx->stream;
+    DevBuf<double> x(m.ncols), y(m.nrows);
+    FAMG_CHECK_HIP(hipMemsetAsync(x.get(), 0, m.ncols * sizeof(double), s));
+    hipEvent_t e0, e1;
+    FAMG_CHECK_HIP(hipEventCreate(&e0));
+    FAMG_CHECK_HIP(hipEventCreate(&e1));
+    float ms[2] = {0.f, 0.f};
+    const int kinds[2] = {SPMV_KERNEL_DIA, SPMV_KERNEL_SCS};
+    for (int k = 0; k < 2; k++) {
+        m.kernel = kinds[k];
+        spmv(m, x.get(), y.get(), SPMV_SET, SpmvEpi{}, s);
+        FAMG_CHECK_HIP(hipEventRecord(e0, s));
+        for (int r = 0; r < 3; r++) spmv(m, x.get(), y.get(), SPMV_SET, SpmvEpi{}, s);
+        FAMG_CHECK_HIP(hipEventRecord(e1, s));
+        FAMG_CHECK_HIP(hipEventSynchronize(e1));
+        FAMG_CHECK_HIP(hipEventElapsedTime(&ms[k], e0, e1));
+    }
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+    return ms[1] < ms[0];
+}
+
 void csr_finalize(GpuCsr &m, const std::vector<int64_t> *segments) {
     Ctx &ctx = *m.ctx;
     if (segments) {
@@ -137,7 +164,22 @@ void csr_finalize(GpuCsr &m, const std::vector<int64_t> *segments) {
     // structured operators: stencil classes, else the pattern SELL, replace
     // SELL-64 / wave-per-row
     const int64_t other_b = m.has_sell() ? sell_b : 10 * m.nnz + 4 * (m.nrows + 1);
-    const bool scs = !dia_all && !m.has_bsr() && build_scs(m, rp, other_b);
+    // long DIA run patterns (> 27 diagonals: A_1 of the 7-point box hierarchy) on a
+    // grid may run faster as x-staged stencil classes: both are built and timed
+    const bool dia_vs_xscs = dia_all && m.dia_k > 27 && m.grid[0] > 0;
+    const bool scs = (!dia_all || dia_vs_xscs) && !m.has_bsr() && build_scs(m, rp, other_b);
+    if (dia_vs_xscs && scs) {
+        if (m.xscs && xscs_beats_dia(m)) {
+            m.dia_codes.release();
+            m.dia_vtab.release();
+            m.dia_ntab = 0;
+            m.dia_k = m.dia_cw = m.dia_vbits = m.dia_pat = 0;
+            m.dia_r0 = m.dia_r1 = m.dia_seg = 0;
+            m.dia_off.clear();
+        } else {
+            scs_release(m);
+        }
+    }
     const bool scs_all = scs && m.scs_seg < 0;  // else a row segment beside SELL-64
     if (!dia_all && !m.has_bsr() && (scs_all || (!scs && build_sellp(m, rp, other_b)))) {
         m.sell_row0.release(); m.sell_soff.release(); m.sell_desc.release(); m.sell_base.release();

@@ -83,7 +83,10 @@ amg_status amg_ctx_join_stream(amg_ctx *ctx, void *other, int32_t ctx_waits);
  * 0 auto -- per matrix the cheapest of: DIA codes (square, <= 32 diagonals or a
  * known run pattern, >= 80 % filled, <= 256 distinct values), 3x3 block storage
  * (block operators), stencil classes (structured Galerkin operators, >= 64
- * offsets), pattern SELL (structured operators incl. rectangular R/P), x-staged
+ * offsets; with a grid hint x-staged per grid tile, also for shorter stencils and
+ * instead of a > 27-diagonal DIA pattern when that times faster at setup), pattern
+ * SELL (structured operators incl. rectangular R/P; the R/P of amg_sa_build_box
+ * get the grid-transfer-class overlay, one 8-bit class per row), x-staged
  * SELL (gather-heavy fp64 SELL whose x footprint per 4096 rows fits LDS),
  * SELL-64 with compressed columns and value codes (short regular rows),
  * wave-per-row (rows averaging >= 256 entries), CSR-stream otherwise
