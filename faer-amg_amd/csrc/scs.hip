@@ -549,8 +549,9 @@ static void xscs_autotune(GpuCsr &m) {
                 if (tx > nx || ty > ny || tz > nz) continue;
                 const int64_t T = (int64_t)tx * ty * tz;
                 const int64_t W = (int64_t)(tx + 2 * rx) * (ty + 2 * ry) * (tz + 2 * rz);
-                if (T < std::min<int64_t>(64, n) || T > (n >= 1024 * 256 ? 256 : 1024) || W * 8 > 64 * 1024) continue;
+                if (T < std::min<int64_t>(64, n) || T > 1024 || W * 8 > 64 * 1024) continue;
                 if (T < 128 && n >= 1024 * 256) continue;
+                if (tx < 8 && nx >= 8) continue;  // short x rows stage poorly (ab_xscs)
                 cands.push_back({tx, ty, tz});
             }
     if (cands.size() < 2) return;
