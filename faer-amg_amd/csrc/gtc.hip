@@ -118,7 +118,8 @@ constexpr int GP_TX = 32, GP_TY = 8;                             // P: fine tile
 constexpr int GP_WX = GP_TX / 2 + 2, GP_WY = GP_TY / 2 + 2;      // coarse window 18 x 6 x (TZ/2 + 2)
 constexpr int GR_TX = 16, GR_TY = 8, GR_TZ = 2;                  // R: coarse tile (one row per lane)
 constexpr int GR_WX = 2 * GR_TX + 2, GR_WY = 2 * GR_TY + 2, GR_WZ = 2 * GR_TZ + 2;  // fine window 34 x 18 x 6
-constexpr int G_DMAX = 2048;                                      // dictionary entries (nclass * ke)
+constexpr int G_DMAX = 2048;   // P: dictionary entries (nclass * ke) staged in LDS
+constexpr int G_RMAX = 8192;   // R: more boundary classes of 64 entries (R_1 of a radius-2 A_1)
 
 struct GtcArgs {
     const uint8_t *cls;
@@ -139,15 +140,18 @@ struct GtcArgs {
 // The class dictionary and value table into LDS: every load of a lane issued
 // before its stores (a load-wait-store loop serialises one memory latency per
 // trip: 4 trips cost P_0 of the 256^3 cycle ~20 us)
+template <int DMAX>
 __device__ __forceinline__ void gtc_stage_dict(const GtcArgs &a, uint16_t *sd, double *st) {
-    constexpr int PF = G_DMAX / 256;
-    uint16_t v[PF];
-#pragma unroll
-    for (int u = 0; u < PF; u++) v[u] = a.dict[min((int)threadIdx.x + 256 * u, a.nce - 1)];
+    constexpr int PF = 8;
     const double t = a.vtab[min((int)threadIdx.x, a.ntab - 1)];
+    for (int b = 0; b < a.nce; b += 256 * PF) {  // one trip per 2048 entries
+        uint16_t v[PF];
 #pragma unroll
-    for (int u = 0; u < PF; u++)
-        if ((int)threadIdx.x + 256 * u < a.nce) sd[threadIdx.x + 256 * u] = v[u];
+        for (int u = 0; u < PF; u++) v[u] = a.dict[min(b + (int)threadIdx.x + 256 * u, a.nce - 1)];
+#pragma unroll
+        for (int u = 0; u < PF; u++)
+            if (b + (int)threadIdx.x + 256 * u < a.nce) sd[b + threadIdx.x + 256 * u] = v[u];
+    }
     if ((int)threadIdx.x < a.ntab) st[threadIdx.x] = t;
 }
 
@@ -195,7 +199,7 @@ __global__ __launch_bounds__(256) void k_gtc_interp(GtcArgs a) {
         const bool in = (unsigned)X < (unsigned)a.kx && (unsigned)Y < (unsigned)a.ky && (unsigned)Z < (unsigned)a.kz;
         win[q] = in ? a.x[(int64_t)Z * cplane + (int64_t)Y * a.kx + X] : 0.0;
     }
-    gtc_stage_dict(a, sd, st);
+    gtc_stage_dict<G_DMAX>(a, sd, st);
     if (tid < 27) lut[tid] = (int16_t)(((tid / 9 - 1) * GP_WY + (tid / 3) % 3 - 1) * GP_WX + tid % 3 - 1);
     __syncthreads();
 #pragma unroll
@@ -228,7 +232,7 @@ __global__ __launch_bounds__(256) void k_gtc_interp(GtcArgs a) {
 // 34 x 18 x 6 around their boxes in LDS.
 __global__ __launch_bounds__(256) void k_gtc_restrict(GtcArgs a) {
     __shared__ double win[GR_WX * GR_WY * GR_WZ];
-    __shared__ uint16_t sd[G_DMAX];
+    __shared__ uint16_t sd[G_RMAX];
     __shared__ double st[256];
     __shared__ int16_t lut[64];
     const int tid = threadIdx.x;
@@ -254,7 +258,7 @@ __global__ __launch_bounds__(256) void k_gtc_restrict(GtcArgs a) {
 #pragma unroll
     for (int u = 0; u < PF; u++)
         if (tid + 256 * u < W) win[tid + 256 * u] = v[u];
-    gtc_stage_dict(a, sd, st);
+    gtc_stage_dict<G_RMAX>(a, sd, st);
     if (tid < 64) lut[tid] = (int16_t)(((tid / 16 - 1) * GR_WY + (tid / 4) % 4 - 1) * GR_WX + tid % 4 - 1);
     __syncthreads();
     if (!live) return;
@@ -317,7 +321,7 @@ bool gtc_attach(GpuCsr &m, const int64_t *fg, const int64_t *cg) {
     size_t ke = 1;
     for (const auto &d : dict) ke = std::max(ke, d.size());
     ke = (ke + gran - 1) / gran * gran;
-    if (dict.size() * ke > (size_t)G_DMAX) return false;
+    if (dict.size() * ke > (size_t)(is_r ? G_RMAX : G_DMAX)) return false;
     const uint16_t zero_idx = (uint16_t)(std::lower_bound(vals.begin(), vals.end(), 0ull) - vals.begin());
     const uint16_t centre = is_r ? (uint16_t)(16 + 4 + 1) : (uint16_t)(9 + 3 + 1);
     // padding: +0.0 at the anchor (after the row's entries: a +0.0 term leaves
