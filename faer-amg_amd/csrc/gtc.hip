@@ -116,8 +116,8 @@ bool gtc_classes(const GpuCsr &M, bool is_r, const int64_t *fg, const int64_t *c
 
 constexpr int GP_TX = 32, GP_TY = 8;                             // P: fine tile (TZ rows per lane along z)
 constexpr int GP_WX = GP_TX / 2 + 2, GP_WY = GP_TY / 2 + 2;      // coarse window 18 x 6 x (TZ/2 + 2)
-constexpr int GR_TX = 16, GR_TY = 8, GR_TZ = 2;                  // R: coarse tile (one row per lane)
-constexpr int GR_WX = 2 * GR_TX + 2, GR_WY = 2 * GR_TY + 2, GR_WZ = 2 * GR_TZ + 2;  // fine window 34 x 18 x 6
+constexpr int GR_TX = 16, GR_TY = 8;                             // R: coarse tile (TZ rows per lane along z)
+constexpr int GR_WX = 2 * GR_TX + 2, GR_WY = 2 * GR_TY + 2;      // fine window 34 x 18 x (2 TZ + 2)
 constexpr int G_DMAX = 2048;   // P: dictionary entries (nclass * ke) staged in LDS
 constexpr int G_RMAX = 8192;   // R: more boundary classes of 64 entries (R_1 of a radius-2 A_1)
 
@@ -228,11 +228,14 @@ __global__ __launch_bounds__(256) void k_gtc_interp(GtcArgs a) {
     }
 }
 
-// R r over a coarse tile of 16 x 8 x 2 points, one per lane; the fine window
-// 34 x 18 x 6 around their boxes in LDS.
+// R r over a coarse tile of 16 x 8 x GR_TZ points (GR_TZ / 2 rows per lane,
+// along z); the fine window 34 x 18 x (2 GR_TZ + 2) around their boxes in LDS,
+// the dictionary in dynamic LDS (nce entries).
+template <int GR_TZ>
 __global__ __launch_bounds__(256) void k_gtc_restrict(GtcArgs a) {
+    constexpr int GR_WZ = 2 * GR_TZ + 2, RL = GR_TZ / 2;
     __shared__ double win[GR_WX * GR_WY * GR_WZ];
-    __shared__ uint16_t sd[G_RMAX];
+    extern __shared__ uint16_t sd[];
     __shared__ double st[256];
     __shared__ int16_t lut[64];
     const int tid = threadIdx.x;
@@ -241,11 +244,17 @@ __global__ __launch_bounds__(256) void k_gtc_restrict(GtcArgs a) {
     const int X0 = tix * GR_TX, Y0 = tiy * GR_TY, Z0 = tiz * GR_TZ;
     const int wx0 = 2 * X0 - 1, wy0 = 2 * Y0 - 1, wz0 = 2 * Z0 - 1;  // window origin (fine)
     const int64_t cplane = (int64_t)a.rx * a.ry, fplane = (int64_t)a.kx * a.ky;
-    const int lx = tid % GR_TX, ly = (tid / GR_TX) % GR_TY, lz = tid / (GR_TX * GR_TY);
-    const int X = X0 + lx, Y = Y0 + ly, Z = Z0 + lz;
-    const bool live = X < a.rx && Y < a.ry && Z < a.rz;
-    const int64_t J = live ? (int64_t)Z * cplane + (int64_t)Y * a.rx + X : 0;
-    const int c = a.cls[J];
+    const int lx = tid % GR_TX, ly = (tid / GR_TX) % GR_TY, lz0 = tid / (GR_TX * GR_TY);  // lz0 in {0, 1}
+    bool live[RL];
+    int64_t J[RL];
+    int c[RL];
+#pragma unroll
+    for (int j = 0; j < RL; j++) {
+        const int X = X0 + lx, Y = Y0 + ly, Z = Z0 + lz0 + 2 * j;
+        live[j] = X < a.rx && Y < a.ry && Z < a.rz;
+        J[j] = live[j] ? (int64_t)Z * cplane + (int64_t)Y * a.rx + X : 0;
+        c[j] = a.cls[J[j]];
+    }
     constexpr int W = GR_WX * GR_WY * GR_WZ, PF = (W + 255) / 256;
     double v[PF];
 #pragma unroll
@@ -261,22 +270,26 @@ __global__ __launch_bounds__(256) void k_gtc_restrict(GtcArgs a) {
     gtc_stage_dict<G_RMAX>(a, sd, st);
     if (tid < 64) lut[tid] = (int16_t)(((tid / 16 - 1) * GR_WY + (tid / 4) % 4 - 1) * GR_WX + tid % 4 - 1);
     __syncthreads();
-    if (!live) return;
-    const int base = ((2 * lz + 1) * GR_WY + 2 * ly + 1) * GR_WX + 2 * lx + 1;
-    const uint16_t *e = sd + c * a.ke;
-    double acc = 0.0;
-    for (int k = 0; k < a.ke; k += 8) {
-        double cv[8], w[8];
 #pragma unroll
-        for (int u = 0; u < 8; u++) {
-            const uint16_t q = e[k + u];
-            cv[u] = st[q >> 8];
-            w[u] = win[base + lut[q & 255]];
+    for (int j = 0; j < RL; j++) {
+        if (!live[j]) continue;
+        const int lz = lz0 + 2 * j;
+        const int base = ((2 * lz + 1) * GR_WY + 2 * ly + 1) * GR_WX + 2 * lx + 1;
+        const uint16_t *e = sd + c[j] * a.ke;
+        double acc = 0.0;
+        for (int k = 0; k < a.ke; k += 8) {
+            double cv[8], w[8];
+#pragma unroll
+            for (int u = 0; u < 8; u++) {
+                const uint16_t q = e[k + u];
+                cv[u] = st[q >> 8];
+                w[u] = win[base + lut[q & 255]];
+            }
+#pragma unroll
+            for (int u = 0; u < 8; u++) acc = fma(cv[u], w[u], acc);
         }
-#pragma unroll
-        for (int u = 0; u < 8; u++) acc = fma(cv[u], w[u], acc);
+        a.y[J[j]] = acc;
     }
-    a.y[J] = acc;
 }
 
 // ------------------------------------------------------------ build / dispatch
@@ -365,6 +378,15 @@ static int gtc_tz() {
     return v;
 }
 
+// coarse planes per R tile (FAMG_GTC_RTZ=4: four, two rows per lane)
+static int gtc_rtz() {
+    static const int v = [] {
+        const char *e = getenv("FAMG_GTC_RTZ");
+        return (e && e[0] == '4') ? 4 : 2;
+    }();
+    return v;
+}
+
 bool gtc_supports(const GpuCsr &m, SpmvMode mode) {
     return m.gtc_r ? mode == SPMV_SET : (mode == SPMV_SET || mode == SPMV_ADD || mode == SPMV_ADD0);
 }
@@ -390,8 +412,12 @@ void spmv_gtc(const GpuCsr &m, const double *x, double *y, SpmvMode mode, const 
         FAMG_REQUIRE(mode == SPMV_SET, AMG_ERR_UNSUPPORTED, "grid-transfer R: SET only");
         a.ntx = (int)ceil_div(a.rx, GR_TX);
         a.nty = (int)ceil_div(a.ry, GR_TY);
-        const int ntz = (int)ceil_div(a.rz, GR_TZ);
-        hipLaunchKernelGGL(k_gtc_restrict, dim3((unsigned)((int64_t)a.ntx * a.nty * ntz)), dim3(256), 0, s, a);
+        const int rtz = gtc_rtz();  // coarse planes per tile
+        const int ntz = (int)ceil_div(a.rz, rtz);
+        const size_t dyn = (size_t)a.nce * sizeof(uint16_t);
+        const dim3 grid((unsigned)((int64_t)a.ntx * a.nty * ntz));
+        if (rtz == 4) k_gtc_restrict<4><<<grid, dim3(256), dyn, s>>>(a);
+        else k_gtc_restrict<2><<<grid, dim3(256), dyn, s>>>(a);
     } else {
         a.ntx = (int)ceil_div(a.rx, GP_TX);
         a.nty = (int)ceil_div(a.ry, GP_TY);
