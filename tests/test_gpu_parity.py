@@ -829,7 +829,12 @@ def test_dia_pattern33(ctx):
     within 1e-11 of the restatement, fold on and off."""
     dims = (97, 85, 73)  # level 1: 49 x 43 x 37 = 77959 rows (odd, > 65536)
     A = fa().SparseMatOp.laplace3d_7pt(ctx, *dims)
-    mg = fa().sa_build_box(A, dims, (2, 2, 2), coarsest_dim=1000)
+    # keep the DIA pattern (setup would otherwise time it against x-staged classes)
+    os.environ["FAMG_XSCS_VS_DIA"] = "0"
+    try:
+        mg = fa().sa_build_box(A, dims, (2, 2, 2), coarsest_dim=1000)
+    finally:
+        del os.environ["FAMG_XSCS_VS_DIA"]
     A1 = mg.level(1)[0]
     info = A1.spmv_info()
     assert info["kernel"] == "dia" and info["dia_diagonals"] == 33 and info["value_bits"] in (4, 8), info
