@@ -481,7 +481,8 @@ struct DLevel {
     Space sp;
     CsrPtr A, R, P;  // local: A rows own(l) cols space l; R rows own(l+1) cols space l;
                      // P rows own(l) cols space l+1 (global ids when l+1 is redundant)
-    std::shared_ptr<DiagOp> S;
+    std::shared_ptr<DiagOp> S;  // diagonal smoother slice, or
+    std::shared_ptr<SgsOp> G;   // SGS over the owned rows (global colors)
     DevBuf<double> v, t, f, r;
 };
 
@@ -529,10 +530,57 @@ struct DistMultigridOp : LinOp {
         spmv(m, x, y, mode, epi, s, 2);
     }
 
+    // Multicolor SGS on a distributed level: the global smoother's color sweeps
+    // (SgsOp::sweep / sweep_x) with the ghosts refreshed before every color, so
+    // each color reads the values the previous colors wrote on every rank.
+    // zero: e = SGS(b) from e = 0 (ghosts of e filled with 0 first); otherwise
+    // x <- x + SGS(b - A x) in place.  Rows of one color do not couple, and a
+    // row's entries keep their stored order, so every rank's rows get exactly
+    // the single-GPU sweep's values.
+    void sgs_sweep(DLevel &D, double *x, const double *b, bool zero) {
+        SgsOp &G = *D.G;
+        hipStream_t s = ctx->stream;
+        const int64_t C = G.ncolors;
+        SpmvEpi epi;
+        epi.b = b;
+        epi.d = G.dinv.get();
+        epi.perm = G.perm.get();
+        int64_t c0 = 0;
+        if (zero) {
+            vec_fill(x, 0.0, D.sp.n_own + D.sp.n_ghost, s);
+            if (D.sp.n_own) G.first_color(x, b);
+            c0 = 1;
+        }
+        for (int64_t c = c0; c < C; c++) {
+            halo(D.sp, x, *tr, s);
+            if (D.sp.n_own) spmv(G.Ap, x, x, SPMV_SGS, epi, s, c);
+        }
+        for (int64_t c = C - 2; c >= 0; c--) {
+            halo(D.sp, x, *tr, s);
+            if (D.sp.n_own) spmv(G.Ap, x, x, SPMV_SGS, epi, s, c);
+        }
+    }
+
     // last_out: the final step writes there (owned rows only) instead of t
     void smooth(int64_t l, double *&v, double *&t, const double *f, bool zero, double *last_out = nullptr) {
         DLevel &D = L[l];
         hipStream_t s = ctx->stream;
+        if (D.G) {  // in place on v; the residual form as MultigridOp::smooth
+            for (int64_t it = 0; it < steps; it++) {
+                if (zero && it == 0) {
+                    sgs_sweep(D, v, f, true);
+                } else if (tail->sgs_residual_form) {
+                    SpmvEpi epi;
+                    epi.b = f;
+                    halo_spmv(D.sp, v, D.A->m, D.r.get(), SPMV_RESID, epi);
+                    sgs_sweep(D, t, D.r.get(), true);
+                    vec_add_inplace(v, t, D.sp.n_own, s);
+                } else {
+                    sgs_sweep(D, v, f, false);
+                }
+            }
+            return;
+        }
         for (int64_t it = 0; it < steps; it++) {
             if (last_out && it + 1 == steps) t = last_out;
             if (zero && it == 0) {
@@ -587,7 +635,7 @@ struct DistMultigridOp : LinOp {
             for (int64_t k = 0; k < mu; k++) tail->cycle(0, vc_full.get(), fc_full.get(), k == 0, nullptr);
             spmv(D.P->m, vc_full.get(), v, SPMV_ADD, SpmvEpi{}, s);
         }
-        const bool direct = out && steps >= 1 && D.S;
+        const bool direct = out && steps >= 1 && D.S && !D.G;
         smooth(l, v, t, f, false, direct ? out : nullptr);
         if (direct) return;
         if (v != v0) vec_copy(v0, v, D.sp.n_own, s);
@@ -705,8 +753,10 @@ static std::shared_ptr<DistMultigridOp> build_dist(amg_comm *comm, const Multigr
         auto *R = dynamic_cast<CsrOp *>(g.levels[l].R.get());
         auto *Pm = dynamic_cast<CsrOp *>(g.levels[l].P.get());
         auto *S = dynamic_cast<DiagOp *>(g.levels[l].S.get());
+        auto *G = dynamic_cast<SgsOp *>(g.levels[l].S.get());
         FAMG_REQUIRE(A && R && Pm, AMG_ERR_UNSUPPORTED, "distributed levels need CSR operators");
-        FAMG_REQUIRE(S, AMG_ERR_UNSUPPORTED, "distributed levels need a diagonal (Jacobi/L1/L2) smoother");
+        FAMG_REQUIRE(S || G, AMG_ERR_UNSUPPORTED,
+                     "distributed levels need a diagonal (Jacobi/L1/L2) or multicolor SGS smoother");
         const std::vector<int64_t> spl = sp_of(l);
         plan_init(D.sp.plan, P, me, spl.data());
         D.sp.n_glob = A->nrows;
@@ -734,8 +784,9 @@ static std::shared_ptr<DistMultigridOp> build_dist(amg_comm *comm, const Multigr
         } else {
             extract_rows(R->m, cr0, cr1, D.R->m, ctx);
         }
-        // smoother slice
+        // smoother slice (SGS: built on the remapped local A below)
         auto *S = dynamic_cast<DiagOp *>(g.levels[l].S.get());
+        if (!S) continue;
         D.S = std::make_shared<DiagOp>();
         D.S->ctx = ctx;
         D.S->nrows = D.S->ncols = D.sp.n_own;
@@ -762,6 +813,15 @@ static std::shared_ptr<DistMultigridOp> build_dist(amg_comm *comm, const Multigr
             op->nrows = op->m.nrows;
             op->ncols = op->m.ncols;
         }
+    }
+    // SGS slices: the owned rows of the remapped local A (columns [owned | ghost],
+    // owned row i = column i) under the global coloring
+    for (int64_t l = 0; l < d->La; l++) {
+        auto *G = dynamic_cast<SgsOp *>(g.levels[l].S.get());
+        if (!G) continue;
+        DLevel &D = d->L[l];
+        FAMG_REQUIRE((int64_t)G->host_colors.size() == D.sp.n_glob, AMG_ERR_INVALID, "sgs: coloring size");
+        D.G = make_sgs_slice(D.A, G->host_colors.data() + D.sp.r0, G->ncolors);
     }
     // the last distributed level's P references the replicated level La by global id
     if (d->La > 0) {
@@ -871,6 +931,9 @@ amg_status amg_comm_create(amg_ctx *ctx, int32_t nranks, int32_t rank, const voi
         ncclUniqueId u;
         std::memcpy(&u, id, sizeof(u));
         FAMG_CHECK_NCCL(rccl().CommInitRank(&t->comm, nranks, u, rank));
+        // RCCL's device probing may leave a stale per-thread HIP error that the
+        // next hipGetLastError() check would report as ours
+        (void)hipGetLastError();
         *out = new amg_comm{c, t};
     });
 }

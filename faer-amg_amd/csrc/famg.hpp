@@ -208,7 +208,9 @@ void csr_from_host(GpuCsr &m, Ctx *ctx, int64_t nrows, int64_t ncols, const int6
                    const int64_t *col, const double *val);
 void csr_to_host(const GpuCsr &m, int64_t *rowptr, int64_t *col, double *val);
 // Diagonal a_ii per row (device, n); throws if a diagonal entry is missing.
-void csr_diagonal(const GpuCsr &m, double *d_out);
+// a_ii per row; wide: m may have more columns than rows (the owned rows of a
+// distributed level over [owned | ghost] columns: row i's diagonal is column i)
+void csr_diagonal(const GpuCsr &m, double *d_out, bool wide = false);
 void csr_abs_row_sums(const GpuCsr &m, double *d_out);
 
 // ------------------------------------------------------------------ kernels
@@ -374,6 +376,8 @@ struct SgsOp : LinOp {
     void sweep(double *e, const double *r);
     // x <- x + SGS(b - A x), in place on x
     void sweep_x(double *x, const double *b);
+    // e_i = dinv_i r_i on the rows of color 0 (the first forward color from e = 0)
+    void first_color(double *e, const double *r);
     void apply(double *out, const double *rhs) override;
     void apply_in_place(double *rhs) override;
 };
@@ -456,6 +460,10 @@ std::shared_ptr<DiagOp> make_jacobi(CsrOp &A, double omega);
 std::shared_ptr<DiagOp> make_l1(CsrOp &A);
 std::shared_ptr<DiagOp> make_l2(CsrOp &A);
 std::shared_ptr<SgsOp> make_sgs(const CsrPtr &A, const int32_t *colors, bool validate = true);
+// SGS over the owned rows of a distributed level (A: owned rows x [owned | ghost]
+// columns, row i's diagonal at column i); colors: the global smoother's colors of
+// those rows, ncolors the global count (every rank sweeps the same colors)
+std::shared_ptr<SgsOp> make_sgs_slice(const CsrPtr &A, const int32_t *colors, int64_t ncolors);
 // fused SGS phases for a 27-point grid operator stored as DIA codes (sgs27.hip)
 // SgsOps built afterwards use the fused phases where they apply (default 1,
 // FAMG_SGS_FUSED=0 sets 0; amg_set_sgs_fused)

@@ -186,10 +186,81 @@ __global__ void k_sgs_first(const int32_t *perm, const double *dinv, const doubl
     }
 }
 
+// The color-permuted copy Ap (rows grouped by color, stable within a color),
+// perm and 1/a_ii of op->A for the coloring op->host_colors / op->ncolors.
+// A may be rectangular (the owned rows of a distributed level over the
+// [owned | ghost] columns): row i's diagonal is column i.
+static void sgs_permuted_copy(SgsOp &op) {
+    const CsrPtr &A = op.A;
+    Ctx *ctx = A->ctx;
+    hipStream_t s = ctx->stream;
+    const int64_t n = A->nrows;
+    const std::vector<int32_t> &color = op.host_colors;
+    // stable counting sort of rows by color
+    op.color_ptr.assign(op.ncolors + 1, 0);
+    for (int64_t i = 0; i < n; i++) op.color_ptr[color[i] + 1]++;
+    for (int64_t c = 0; c < op.ncolors; c++) op.color_ptr[c + 1] += op.color_ptr[c];
+    std::vector<int32_t> perm(n);
+    {
+        std::vector<int64_t> pos(op.color_ptr.begin(), op.color_ptr.end() - 1);
+        for (int64_t i = 0; i < n; i++) perm[pos[color[i]]++] = (int32_t)i;
+    }
+    op.perm.resize(std::max<int64_t>(1, n));
+    if (n) FAMG_CHECK_HIP(hipMemcpyAsync(op.perm.get(), perm.data(), n * sizeof(int32_t), hipMemcpyHostToDevice, s));
+    DevBuf<int64_t> cnt(std::max<int64_t>(1, n));
+    const unsigned g = (unsigned)std::max<int64_t>(1, ceil_div(n, 256));
+    if (n) hipLaunchKernelGGL(k_perm_counts, dim3(g), dim3(256), 0, s, A->m.rp64.get(), op.perm.get(), n, cnt.get());
+    DevBuf<int64_t> prp(n + 1);
+    const int64_t nnz = scan_counts(cnt.get(), prp.get(), n, *ctx);
+    csr_alloc(op.Ap, ctx, n, A->ncols, nnz);
+    op.Ap.rp64 = std::move(prp);
+    op.Ap.no_bsr = true;  // swept in SGS mode only
+    op.Ap.no_sellp = true;
+    op.dinv.resize(std::max<int64_t>(1, n));
+    DevBuf<double> wide_diag;
+    const double *aii = nullptr;
+    if (A->nrows == A->ncols) {
+        aii = A->diagonal();
+    } else if (n) {
+        wide_diag.resize(n);
+        csr_diagonal(A->m, wide_diag.get(), true);
+        aii = wide_diag.get();
+    }
+    if (n)
+        hipLaunchKernelGGL(k_perm_rows, dim3(g), dim3(256), 0, s, A->m.rp64.get(), A->m.col.get(),
+                           A->m.val.get(), op.perm.get(), n, op.Ap.rp64.get(), op.Ap.col.get(),
+                           op.Ap.val.get(), aii, op.dinv.get());
+    FAMG_CHECK_HIP(hipGetLastError());
+    csr_finalize(op.Ap, &op.color_ptr);  // one row segment per color
+    FAMG_REQUIRE(op.Ap.spmv_ready(), AMG_ERR_UNSUPPORTED, "sgs: nnz must be < 2^31");
+}
+
+std::shared_ptr<SgsOp> make_sgs_slice(const CsrPtr &A, const int32_t *colors, int64_t ncolors) {
+    FAMG_REQUIRE(A->nrows <= A->ncols, AMG_ERR_DIM, "sgs slice: more rows than columns");
+    auto op = std::make_shared<SgsOp>();
+    op->ctx = A->ctx;
+    op->A = A;
+    op->nrows = op->ncols = A->nrows;
+    op->ncolors = ncolors;
+    op->host_colors.assign(colors, colors + A->nrows);
+    for (int32_t c : op->host_colors)
+        FAMG_REQUIRE(c >= 0 && c < ncolors, AMG_ERR_INVALID, "sgs slice: color out of range");
+    sgs_permuted_copy(*op);
+    return op;
+}
+
+void SgsOp::first_color(double *e, const double *r) {
+    const int64_t p0 = color_ptr[0], p1 = color_ptr[1];
+    if (p1 > p0) log_launch("sgs_first", -1, -1, p1 - p0, 28 * (p1 - p0));
+    if (p1 > p0)
+        hipLaunchKernelGGL(k_sgs_first, dim3((unsigned)ceil_div(p1 - p0, 256)), dim3(256), 0, ctx->stream,
+                           perm.get(), dinv.get(), r, e, p0, p1);
+    FAMG_CHECK_HIP(hipGetLastError());
+}
+
 std::shared_ptr<SgsOp> make_sgs(const CsrPtr &A, const int32_t *colors, bool validate) {
     FAMG_REQUIRE(A->nrows == A->ncols, AMG_ERR_DIM, "sgs: matrix must be square");
     Ctx *ctx = A->ctx;
-    hipStream_t s = ctx->stream;
     auto op = std::make_shared<SgsOp>();
     op->ctx = ctx;
     op->A = A;
@@ -215,35 +286,8 @@ std::shared_ptr<SgsOp> make_sgs(const CsrPtr &A, const int32_t *colors, bool val
     } else {
         op->ncolors = greedy_coloring(A->m, color);
     }
-    op->host_colors = color;
-    // stable counting sort of rows by color
-    op->color_ptr.assign(op->ncolors + 1, 0);
-    for (int64_t i = 0; i < n; i++) op->color_ptr[color[i] + 1]++;
-    for (int64_t c = 0; c < op->ncolors; c++) op->color_ptr[c + 1] += op->color_ptr[c];
-    std::vector<int32_t> perm(n);
-    {
-        std::vector<int64_t> pos(op->color_ptr.begin(), op->color_ptr.end() - 1);
-        for (int64_t i = 0; i < n; i++) perm[pos[color[i]]++] = (int32_t)i;
-    }
-    op->perm.resize(n);
-    FAMG_CHECK_HIP(hipMemcpyAsync(op->perm.get(), perm.data(), n * sizeof(int32_t), hipMemcpyHostToDevice, s));
-    DevBuf<int64_t> cnt(n);
-    const unsigned g = (unsigned)std::max<int64_t>(1, ceil_div(n, 256));
-    if (n) hipLaunchKernelGGL(k_perm_counts, dim3(g), dim3(256), 0, s, A->m.rp64.get(), op->perm.get(), n, cnt.get());
-    DevBuf<int64_t> prp(n + 1);
-    const int64_t nnz = scan_counts(cnt.get(), prp.get(), n, *ctx);
-    csr_alloc(op->Ap, ctx, n, n, nnz);
-    op->Ap.rp64 = std::move(prp);
-    op->Ap.no_bsr = true;  // swept in SGS mode only
-    op->Ap.no_sellp = true;
-    op->dinv.resize(n);
-    if (n)
-        hipLaunchKernelGGL(k_perm_rows, dim3(g), dim3(256), 0, s, A->m.rp64.get(), A->m.col.get(),
-                           A->m.val.get(), op->perm.get(), n, op->Ap.rp64.get(), op->Ap.col.get(),
-                           op->Ap.val.get(), A->diagonal(), op->dinv.get());
-    FAMG_CHECK_HIP(hipGetLastError());
-    csr_finalize(op->Ap, &op->color_ptr);  // one row segment per color
-    FAMG_REQUIRE(op->Ap.spmv_ready(), AMG_ERR_UNSUPPORTED, "sgs: nnz must be < 2^31");
+    op->host_colors = std::move(color);
+    sgs_permuted_copy(*op);
     build_dia_sgs(op->Ap, op->perm.get());  // constant-stencil operators: DIA codes for the sweeps
     op->e_.resize(n);
     sgs27_setup(*op);  // 27-point grid operators: fused plane-parity phases
@@ -260,11 +304,7 @@ void SgsOp::sweep(double *e, const double *r) {
         return;
     }
     vec_fill(e, 0.0, n, s);
-    const int64_t p0 = color_ptr[0], p1 = color_ptr[1];
-    if (p1 > p0) log_launch("sgs_first", -1, -1, p1 - p0, 28 * (p1 - p0));
-    if (p1 > p0)
-        hipLaunchKernelGGL(k_sgs_first, dim3((unsigned)ceil_div(p1 - p0, 256)), dim3(256), 0, s,
-                           perm.get(), dinv.get(), r, e, p0, p1);
+    first_color(e, r);
     SpmvEpi epi;
     epi.b = r;
     epi.d = dinv.get();
@@ -517,9 +557,16 @@ void MultigridOp::cycle(int64_t l, double *v, const double *f, bool v_zero, doub
     // residual then gathers d as randomly as x, and that doubled gather cost more
     // than the pass it saves (Q1 elasticity 1.57M rows: 640 vs 388 + 15 us).
     const bool gather_cheap = A && 2 * A->m.sell_mode_slices[2] < A->m.nslices;
+    // x-staged stencil classes (levels 1-3 of the box hierarchies): d*f is
+    // staged with the window (1-B codes of d per staged point), and the
+    // correction's d*f epilogue streams dc and f in place of v -- the 24n-byte
+    // d*f pass and its launch go away (FAMG_FOLD_XSCS=0: off, A/B).
+    static const bool fold_xscs = !getenv("FAMG_FOLD_XSCS") || getenv("FAMG_FOLD_XSCS")[0] != '0';
+    const bool p_add0 = P && (P->m.kernel == SPMV_KERNEL_SELL || P->m.kernel == SPMV_KERNEL_SELLP || P->m.gtc_on);
     const bool fold = fold_zero_guess && v_zero && steps == 1 && A && D && P &&
                       ((A->m.kernel == SPMV_KERNEL_SELL && A->m.sell_vbits == 0 && gather_cheap) ||
                        A->m.kernel == SPMV_KERNEL_XS ||  // x-staged: d*x staged with x, no extra gather
+                       (fold_xscs && A->m.kernel == SPMV_KERNEL_SCS && A->m.xscs && p_add0) ||
                        (A->m.kernel == SPMV_KERNEL_DIA &&
                         (fold_dia_mode() == 1 ||
                          (fold_dia_mode() < 0 &&

@@ -238,7 +238,7 @@ __global__ __launch_bounds__(256) void spmv_xscs_kernel(XscsArgs a) {
         c[j] = cls_of(gi[j]);
         br[j] = xr[j] = dr[j] = yr[j] = 0.0;
         if (live[j]) {
-            if constexpr (MODE == SPMV_RESID) br[j] = a.b[gi[j]];
+            if constexpr (MODE == SPMV_RESID || MODE == SPMV_RESID0) br[j] = a.b[gi[j]];
             if constexpr (MODE == SPMV_ADD) yr[j] = a.y[gi[j]];
             if constexpr (MODE == SPMV_JACOBI) {
                 xr[j] = a.x[gi[j]];
@@ -247,7 +247,10 @@ __global__ __launch_bounds__(256) void spmv_xscs_kernel(XscsArgs a) {
             }
         }
     }
-    // stage the window: rows of wx consecutive x values, 0.0 outside the grid
+    // stage the window: rows of wx consecutive x values, 0.0 outside the grid.
+    // RESID0 (the zero-guess step folded into the residual): the staged operand
+    // is the iterate d*x that vec_mul(_coded) would have stored, so the sums are
+    // the unfolded residual's bitwise
     const int W = a.wx * a.wy * a.wz;
     constexpr int PF = 8;
     for (int p0 = tid; p0 < W; p0 += 256 * PF) {
@@ -260,7 +263,9 @@ __global__ __launch_bounds__(256) void spmv_xscs_kernel(XscsArgs a) {
             const int gx = x0 - a.rx + px, gy = y0 - a.ry + py, gz = z0 - a.rz + pz;
             const bool in = p < W && (unsigned)gx < (unsigned)a.nx && (unsigned)gy < (unsigned)a.ny &&
                             (unsigned)gz < (unsigned)a.nz;
-            v[u] = in ? a.x[(int64_t)gz * plane + (int64_t)gy * a.nx + gx] : 0.0;
+            const int64_t g = (int64_t)gz * plane + (int64_t)gy * a.nx + gx;
+            if constexpr (MODE == SPMV_RESID0) v[u] = in ? (a.dc ? a.dt[a.dc[g]] : a.d[g]) * a.x[g] : 0.0;
+            else v[u] = in ? a.x[g] : 0.0;
         }
 #pragma unroll
         for (int u = 0; u < PF; u++)
@@ -325,7 +330,7 @@ __global__ __launch_bounds__(256) void spmv_xscs_kernel(XscsArgs a) {
         const int64_t i = gi[j];
         if constexpr (MODE == SPMV_SET) a.y[i] = acc[j];
         else if constexpr (MODE == SPMV_ADD) a.y[i] = yr[j] + acc[j];
-        else if constexpr (MODE == SPMV_RESID) a.y[i] = br[j] - acc[j];
+        else if constexpr (MODE == SPMV_RESID || MODE == SPMV_RESID0) a.y[i] = br[j] - acc[j];
         else a.y[i] = xr[j] + dr[j] * (br[j] - acc[j]);  // JACOBI
     }
 }
@@ -729,6 +734,7 @@ static void spmv_xscs(const GpuCsr &m, const double *x, double *y, SpmvMode mode
     case SPMV_SET: FAMG_XS3(SPMV_SET, IB) break;                                                   \
     case SPMV_ADD: FAMG_XS3(SPMV_ADD, IB) break;                                                   \
     case SPMV_RESID: FAMG_XS3(SPMV_RESID, IB) break;                                               \
+    case SPMV_RESID0: FAMG_XS3(SPMV_RESID0, IB) break;                                             \
     case SPMV_JACOBI: FAMG_XS3(SPMV_JACOBI, IB) break;                                             \
     default: fail(AMG_ERR_UNSUPPORTED, "stencil-class storage: unsupported SpMV epilogue");        \
     }

@@ -1574,37 +1574,59 @@ __device__ __forceinline__ void vec_entry(const VecArgs &a, int row, int k, doub
     else c = __builtin_nontemporal_load(a.col + k);
 }
 
-template <int MODE, int VB, bool O16>
+// WPR waves per row (1, 2, 4): a level with few long rows (A_4 of the box
+// hierarchies: 4096 rows of ~1400 entries, R_4: 512 rows) has too few waves
+// to keep the loads in flight with one wave per row; with WPR > 1 the row's
+// 64-entry chunks are dealt round-robin to its waves and the wave sums are
+// added in LDS (a different lane split: the sum is bounded, not bitwise).
+template <int MODE, int VB, bool O16, int WPR>
 __global__ __launch_bounds__(256) void spmv_vector_kernel(VecArgs a) {
+    __shared__ double part[4];
     const int blk = xcd_remap(blockIdx.x, gridDim.x);
-    const int w = blk * 4 + (threadIdx.x >> 6);
-    if (w >= a.nrows) return;
-    const int row = a.row_begin + w;
+    const int wv = threadIdx.x >> 6;
+    const int w = blk * (4 / WPR) + wv / WPR;
+    const int sub = wv % WPR;
+    if constexpr (WPR == 1)
+        if (w >= a.nrows) return;
+    const bool ok = w < a.nrows;
+    const int row = a.row_begin + (ok ? w : 0);
     const int lane = threadIdx.x & 63;
     EpiOps<MODE> ep;
-    if (lane == 0) ep.load(a.e, row);
-    const int e0 = a.rowptr[row], e1 = a.rowptr[row + 1];
+    if (ok && lane == 0 && sub == 0) ep.load(a.e, row);
+    const int e0 = ok ? a.rowptr[row] : 0, e1 = ok ? a.rowptr[row + 1] : 0;
+    constexpr int S = 64 * WPR;
     double acc = 0.0;
-    int k = e0 + lane;
-    for (; k + 3 * 64 < e1; k += 4 * 64) {
+    int k = e0 + sub * 64 + lane;
+    for (; k + 3 * S < e1; k += 4 * S) {
         double vv[4];
         int32_t cc[4];
 #pragma unroll
-        for (int u = 0; u < 4; u++) vec_entry<VB, O16>(a, row, k + 64 * u, vv[u], cc[u]);
+        for (int u = 0; u < 4; u++) vec_entry<VB, O16>(a, row, k + S * u, vv[u], cc[u]);
         double xx[4];
 #pragma unroll
         for (int u = 0; u < 4; u++) xx[u] = gx<MODE>(a.e, cc[u]);
 #pragma unroll
         for (int u = 0; u < 4; u++) acc = fma(vv[u], xx[u], acc);
     }
-    for (; k < e1; k += 64) {
+    for (; k < e1; k += S) {
         double v;
         int32_t c;
         vec_entry<VB, O16>(a, row, k, v, c);
         acc = fma(v, gx<MODE>(a.e, c), acc);
     }
     for (int off = 32; off > 0; off >>= 1) acc += __shfl_xor(acc, off);
-    if (lane == 0) ep.store(a.e, acc);
+    if constexpr (WPR == 1) {
+        if (lane == 0) ep.store(a.e, acc);
+    } else {
+        if (lane == 0) part[wv] = acc;
+        __syncthreads();
+        if (ok && lane == 0 && sub == 0) {
+            double t = part[wv];
+#pragma unroll
+            for (int j = 1; j < WPR; j++) t += part[wv + j];
+            ep.store(a.e, t);
+        }
+    }
 }
 
 // ------------------------------------------------------------ host: storage
@@ -2242,7 +2264,20 @@ void choose_kernel(GpuCsr &m) {
     case SPMV_RESID0: KERNEL<SPMV_RESID0 __VA_ARGS__><<<grid, block, 0, s>>>(args); break; \
     case SPMV_ADD0: KERNEL<SPMV_ADD0 __VA_ARGS__><<<grid, block, 0, s>>>(args); break;     \
     }
-#define FAMG_VEC(VB, O16) , VB, O16
+#define FAMG_VEC(VB, O16, W) , VB, O16, W
+
+// waves per row of the wave-per-row kernel: few long rows get 2 or 4 waves each
+// (FAMG_VEC_WPR=1/2/4 forces it; read per launch so tests can switch it)
+static int vec_waves_per_row(int64_t rows, int64_t nnz) {
+    if (const char *e = getenv("FAMG_VEC_WPR")) {
+        const int w = atoi(e);
+        if (w == 1 || w == 2 || w == 4) return w;
+    }
+    const int64_t avg = nnz / std::max<int64_t>(1, rows);
+    if (rows <= 16384 && avg >= 512) return 4;
+    if (rows <= 65536 && avg >= 256) return 2;
+    return 1;
+}
 #define FAMG_LAY0 , 0
 #define FAMG_LAY1 , 1
 #define FAMG_LAY4 , 4
@@ -2401,8 +2436,9 @@ static void log_spmv(const GpuCsr &m, SpmvMode mode, const SpmvEpi &epi, int64_t
     case SPMV_RESID: vec += 16 * r; break;               // b read, y written
     case SPMV_JACOBI: vec += 16 * r + db * r; break;     // b, d read, y written
     case SPMV_SGS: vec += 28 * r; break;                 // perm, d, b read, x written
-    case SPMV_RESID0:  // x = b; d gathered beside x (1-B codes only in the DIA kernel); y written
-        vec += 8 * r + ((kernel == SPMV_KERNEL_DIA && epi.dc && dia_rc_enabled()) ? 1 : 8) * xcols;
+    case SPMV_RESID0:  // x = b; d gathered beside x (1-B codes in the DIA and x-staged class kernels); y written
+        vec += 8 * r + (((kernel == SPMV_KERNEL_DIA && dia_rc_enabled()) || (kernel == SPMV_KERNEL_SCS && m.xscs))
+                            && epi.dc ? 1 : 8) * xcols;
         break;
     case SPMV_ADD0: vec += 16 * r + db * r; break;       // b, d read, y written
     }
@@ -2641,16 +2677,22 @@ void spmv(const GpuCsr &m, const double *x, double *y, SpmvMode mode, const Spmv
         if (r1 <= r0) return;
         VecArgs a{m.rp32.get(), m.col.get(), m.vec_off.get(), m.val.get(), m.vec_codes.get(), m.sell_vtab.get(),
                   (int32_t)r0, (int32_t)(r1 - r0), e};
-        const dim3 grid((unsigned)ceil_div(r1 - r0, 4));
+        const int wpr = vec_waves_per_row(r1 - r0, m.nnz * (r1 - r0) / std::max<int64_t>(1, m.nrows));
+        const dim3 grid((unsigned)ceil_div(r1 - r0, 4 / wpr));
         const int key = m.vec_vbits * 2 + (m.vec_o16 ? 1 : 0);
-        switch (key) {
-        case 0: FAMG_LAUNCH_MODES(spmv_vector_kernel, grid, block, s, a, FAMG_VEC(0, false)) break;
-        case 1: FAMG_LAUNCH_MODES(spmv_vector_kernel, grid, block, s, a, FAMG_VEC(0, true)) break;
-        case 16: FAMG_LAUNCH_MODES(spmv_vector_kernel, grid, block, s, a, FAMG_VEC(8, false)) break;
-        case 17: FAMG_LAUNCH_MODES(spmv_vector_kernel, grid, block, s, a, FAMG_VEC(8, true)) break;
-        case 32: FAMG_LAUNCH_MODES(spmv_vector_kernel, grid, block, s, a, FAMG_VEC(16, false)) break;
-        default: FAMG_LAUNCH_MODES(spmv_vector_kernel, grid, block, s, a, FAMG_VEC(16, true)) break;
+#define FAMG_VECW(W)                                                                                   \
+        switch (key) {                                                                                 \
+        case 0: FAMG_LAUNCH_MODES(spmv_vector_kernel, grid, block, s, a, FAMG_VEC(0, false, W)) break;  \
+        case 1: FAMG_LAUNCH_MODES(spmv_vector_kernel, grid, block, s, a, FAMG_VEC(0, true, W)) break;   \
+        case 16: FAMG_LAUNCH_MODES(spmv_vector_kernel, grid, block, s, a, FAMG_VEC(8, false, W)) break; \
+        case 17: FAMG_LAUNCH_MODES(spmv_vector_kernel, grid, block, s, a, FAMG_VEC(8, true, W)) break;  \
+        case 32: FAMG_LAUNCH_MODES(spmv_vector_kernel, grid, block, s, a, FAMG_VEC(16, false, W)) break;\
+        default: FAMG_LAUNCH_MODES(spmv_vector_kernel, grid, block, s, a, FAMG_VEC(16, true, W)) break; \
         }
+        if (wpr == 4) { FAMG_VECW(4) }
+        else if (wpr == 2) { FAMG_VECW(2) }
+        else { FAMG_VECW(1) }
+#undef FAMG_VECW
     } else {
         const int64_t b0 = seg < 0 ? 0 : m.seg_blk[seg];
         const int64_t b1 = seg < 0 ? m.nblocks : m.seg_blk[seg + 1];

@@ -468,8 +468,11 @@ amg_status amg_comm_allreduce_sum(amg_comm *comm, double *value);
  * nlevels x (nranks+1) row splits (row range of rank p at level l is
  * [s[l*(nranks+1)+p], s[l*(nranks+1)+p+1])).  Levels from the first one with
  * fewer than agglomerate_rows rows down are run redundantly on every rank.
- * Every distributed level must be smoothed by a diagonal smoother.  apply()
- * maps the rank's owned rows of rhs (n_own) to its owned rows of out. */
+ * Every distributed level must be smoothed by a diagonal (Jacobi/L1/L2) or a
+ * multicolor SGS smoother; SGS sweeps the global coloring restricted to the
+ * owned rows with one halo exchange before every color (the single-GPU sweep's
+ * values on every rank).  apply() maps the rank's owned rows of rhs (n_own) to
+ * its owned rows of out. */
 amg_status amg_dist_multigrid_create(amg_comm *comm, const amg_linop *mg_global,
                                      const int64_t *level_splits, int64_t agglomerate_rows,
                                      amg_linop **out);

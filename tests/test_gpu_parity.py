@@ -100,12 +100,17 @@ def test_spmv_irregular_golden(ctx):
     assert np.all(y[np.diff(g["rowptr"]) == 0] == 0)
 
 
-@pytest.mark.parametrize("fmt", ["csr", "sell", "vector"])
+@pytest.mark.parametrize("fmt", ["csr", "sell", "vector", "vector-w2", "vector-w4"])
 def test_spmv_formats(ctx, fmt):
     """Both storage paths (CSR-stream and SELL-64) on short, long, empty and
     rectangular rows.  SELL sums every row sequentially in one lane (bitwise
     equal to the oracle); CSR-stream does so when a block holds >= 128 rows
-    (rows of <= 16 entries) and splits longer rows over lanes (bounded)."""
+    (rows of <= 16 entries) and splits longer rows over lanes (bounded); the
+    wave-per-row kernel with 1, 2 or 4 waves per row (bounded; odd row counts
+    leave a workgroup's last row slots empty)."""
+    if fmt.startswith("vector-w"):
+        os.environ["FAMG_VEC_WPR"] = fmt[-1]
+        fmt = "vector"
     fa().set_spmv_format(fmt)
     try:
         OA = O.laplace3d_7pt(33, 17, 9)
@@ -133,6 +138,7 @@ def test_spmv_formats(ctx, fmt):
         assert np.all(np.abs(y - g5["y"]) <= spmv_bound(S, g5["x"]))
     finally:
         fa().set_spmv_format("auto")
+        os.environ.pop("FAMG_VEC_WPR", None)
 
 
 def _random_rows(rng, m, n, per_row, spread):
@@ -1174,6 +1180,32 @@ def test_xstaged_stencil_classes(ctx):
     assert np.max(np.abs(y - ref)) <= 1e-12 * np.max(np.abs(ref))
     A1.set_grid(0, 0, 0)
     assert A1.spmv_info()["grid"] == (0, 0, 0) and not A1.spmv_info()["xstaged"]
+
+
+def test_xstaged_classes_fold_zero_guess(ctx):
+    """The zero-guess smoothing step folded on x-staged stencil-class levels
+    (RESID0 stages d*f with the x window, ADD0 writes d*f + P v_c): the plan
+    shows RESID0/ADD0 and no d*f pass on those levels, the V-cycle is bitwise
+    the unfolded one (the staged products are vec_mul's) and within 1e-11 of
+    the oracle."""
+    dims = (128, 128, 128)
+    A = fa().SparseMatOp.laplace3d_7pt(ctx, *dims)
+    mg = fa().sa_build_box(A, dims, (2, 2, 2), coarsest_dim=100)
+    xs = [l for l in range(1, mg.levels() - 1) if mg.level(l)[0].spmv_info()["xstaged"]]
+    assert xs, "no x-staged level"
+    plan = mg.cycle_plan()
+    for l in xs:
+        modes = [p["mode"] for p in plan if p["level"] == l]
+        assert modes[0] == "RESID0" and "ADD0" in modes and "-" not in modes, (l, modes)
+    b = np.random.default_rng(21).uniform(-1, 1, A.nrows)
+    outs = {}
+    for fold in (True, False):
+        mg.set_fold_zero_guess(fold)
+        outs[fold] = apply_dev(ctx, mg, b, A.nrows)
+    mg.set_fold_zero_guess(True)
+    assert np.array_equal(outs[True].view(np.int64), outs[False].view(np.int64))
+    zref = O.Multigrid(oracle_levels_from_gpu(mg, "jacobi")).apply(b)
+    assert np.linalg.norm(outs[True] - zref) <= 1e-11 * np.linalg.norm(zref)
 
 
 def _smoother_diag(ctx, S, n):
