@@ -258,8 +258,8 @@ __global__ void k_diag(const int64_t *rp, const int32_t *col, const double *val,
     else { d[i] = 0.0; *missing = 1; }
 }
 
-void csr_diagonal(const GpuCsr &m, double *d_out, bool wide) {
-    FAMG_REQUIRE(m.nrows == m.ncols || (wide && m.nrows < m.ncols), AMG_ERR_DIM, "diagonal of a non-square matrix");
+void csr_diagonal(const GpuCsr &m, double *d_out) {
+    FAMG_REQUIRE(m.nrows == m.ncols, AMG_ERR_DIM, "diagonal of a non-square matrix");
     DevBuf<int> flag(1);
     hipStream_t s = m.ctx->stream;
     FAMG_CHECK_HIP(hipMemsetAsync(flag.get(), 0, sizeof(int), s));

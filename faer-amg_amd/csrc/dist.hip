@@ -639,6 +639,7 @@ struct DistMultigridOp : LinOp {
         smooth(l, v, t, f, false, direct ? out : nullptr);
         if (direct) return;
         if (v != v0) vec_copy(v0, v, D.sp.n_own, s);
+        if (out) vec_copy(out, v0, D.sp.n_own, s);  // SGS (in place on v) or no smoothing steps
     }
 
     // Allocation length of a level-0 vector that A_0 reads in place: the owned
@@ -821,7 +822,8 @@ static std::shared_ptr<DistMultigridOp> build_dist(amg_comm *comm, const Multigr
         if (!G) continue;
         DLevel &D = d->L[l];
         FAMG_REQUIRE((int64_t)G->host_colors.size() == D.sp.n_glob, AMG_ERR_INVALID, "sgs: coloring size");
-        D.G = make_sgs_slice(D.A, G->host_colors.data() + D.sp.r0, G->ncolors);
+        auto *Ag = dynamic_cast<CsrOp *>(g.levels[l].A.get());
+        D.G = make_sgs_slice(D.A, G->host_colors.data() + D.sp.r0, G->ncolors, Ag->diagonal() + D.sp.r0);
     }
     // the last distributed level's P references the replicated level La by global id
     if (d->La > 0) {

@@ -208,9 +208,7 @@ void csr_from_host(GpuCsr &m, Ctx *ctx, int64_t nrows, int64_t ncols, const int6
                    const int64_t *col, const double *val);
 void csr_to_host(const GpuCsr &m, int64_t *rowptr, int64_t *col, double *val);
 // Diagonal a_ii per row (device, n); throws if a diagonal entry is missing.
-// a_ii per row; wide: m may have more columns than rows (the owned rows of a
-// distributed level over [owned | ghost] columns: row i's diagonal is column i)
-void csr_diagonal(const GpuCsr &m, double *d_out, bool wide = false);
+void csr_diagonal(const GpuCsr &m, double *d_out);
 void csr_abs_row_sums(const GpuCsr &m, double *d_out);
 
 // ------------------------------------------------------------------ kernels
@@ -362,6 +360,7 @@ struct SgsOp : LinOp {
     std::vector<int32_t> host_colors;
     int64_t ncolors = 0;
     DevBuf<double> e_;     // scratch correction
+    const double *aii_ = nullptr;  // setup only: a_ii of a rectangular slice's rows
     // fused plane-parity sweeps on a 27-point grid operator (sgs27.hip)
     bool fused27 = false;
     bool const27 = false;  // every row the interior stencil truncated at the faces: no codes loaded
@@ -461,9 +460,10 @@ std::shared_ptr<DiagOp> make_l1(CsrOp &A);
 std::shared_ptr<DiagOp> make_l2(CsrOp &A);
 std::shared_ptr<SgsOp> make_sgs(const CsrPtr &A, const int32_t *colors, bool validate = true);
 // SGS over the owned rows of a distributed level (A: owned rows x [owned | ghost]
-// columns, row i's diagonal at column i); colors: the global smoother's colors of
-// those rows, ncolors the global count (every rank sweeps the same colors)
-std::shared_ptr<SgsOp> make_sgs_slice(const CsrPtr &A, const int32_t *colors, int64_t ncolors);
+// columns; a row's columns keep the global order, so they need not ascend);
+// colors: the global smoother's colors of those rows, ncolors the global count
+// (every rank sweeps the same colors); aii: their diagonal (device, owned rows)
+std::shared_ptr<SgsOp> make_sgs_slice(const CsrPtr &A, const int32_t *colors, int64_t ncolors, const double *aii);
 // fused SGS phases for a 27-point grid operator stored as DIA codes (sgs27.hip)
 // SgsOps built afterwards use the fused phases where they apply (default 1,
 // FAMG_SGS_FUSED=0 sets 0; amg_set_sgs_fused)

@@ -189,7 +189,7 @@ __global__ void k_sgs_first(const int32_t *perm, const double *dinv, const doubl
 // The color-permuted copy Ap (rows grouped by color, stable within a color),
 // perm and 1/a_ii of op->A for the coloring op->host_colors / op->ncolors.
 // A may be rectangular (the owned rows of a distributed level over the
-// [owned | ghost] columns): row i's diagonal is column i.
+// [owned | ghost] columns); its diagonal then comes from op.aii_.
 static void sgs_permuted_copy(SgsOp &op) {
     const CsrPtr &A = op.A;
     Ctx *ctx = A->ctx;
@@ -217,15 +217,7 @@ static void sgs_permuted_copy(SgsOp &op) {
     op.Ap.no_bsr = true;  // swept in SGS mode only
     op.Ap.no_sellp = true;
     op.dinv.resize(std::max<int64_t>(1, n));
-    DevBuf<double> wide_diag;
-    const double *aii = nullptr;
-    if (A->nrows == A->ncols) {
-        aii = A->diagonal();
-    } else if (n) {
-        wide_diag.resize(n);
-        csr_diagonal(A->m, wide_diag.get(), true);
-        aii = wide_diag.get();
-    }
+    const double *aii = op.aii_ ? op.aii_ : A->diagonal();
     if (n)
         hipLaunchKernelGGL(k_perm_rows, dim3(g), dim3(256), 0, s, A->m.rp64.get(), A->m.col.get(),
                            A->m.val.get(), op.perm.get(), n, op.Ap.rp64.get(), op.Ap.col.get(),
@@ -235,7 +227,7 @@ static void sgs_permuted_copy(SgsOp &op) {
     FAMG_REQUIRE(op.Ap.spmv_ready(), AMG_ERR_UNSUPPORTED, "sgs: nnz must be < 2^31");
 }
 
-std::shared_ptr<SgsOp> make_sgs_slice(const CsrPtr &A, const int32_t *colors, int64_t ncolors) {
+std::shared_ptr<SgsOp> make_sgs_slice(const CsrPtr &A, const int32_t *colors, int64_t ncolors, const double *aii) {
     FAMG_REQUIRE(A->nrows <= A->ncols, AMG_ERR_DIM, "sgs slice: more rows than columns");
     auto op = std::make_shared<SgsOp>();
     op->ctx = A->ctx;
@@ -245,7 +237,9 @@ std::shared_ptr<SgsOp> make_sgs_slice(const CsrPtr &A, const int32_t *colors, in
     op->host_colors.assign(colors, colors + A->nrows);
     for (int32_t c : op->host_colors)
         FAMG_REQUIRE(c >= 0 && c < ncolors, AMG_ERR_INVALID, "sgs slice: color out of range");
+    op->aii_ = aii;
     sgs_permuted_copy(*op);
+    op->aii_ = nullptr;
     return op;
 }
 
@@ -557,16 +551,25 @@ void MultigridOp::cycle(int64_t l, double *v, const double *f, bool v_zero, doub
     // residual then gathers d as randomly as x, and that doubled gather cost more
     // than the pass it saves (Q1 elasticity 1.57M rows: 640 vs 388 + 15 us).
     const bool gather_cheap = A && 2 * A->m.sell_mode_slices[2] < A->m.nslices;
-    // x-staged stencil classes (levels 1-3 of the box hierarchies): d*f is
-    // staged with the window (1-B codes of d per staged point), and the
-    // correction's d*f epilogue streams dc and f in place of v -- the 24n-byte
-    // d*f pass and its launch go away (FAMG_FOLD_XSCS=0: off, A/B).
-    static const bool fold_xscs = !getenv("FAMG_FOLD_XSCS") || getenv("FAMG_FOLD_XSCS")[0] != '0';
-    const bool p_add0 = P && (P->m.kernel == SPMV_KERNEL_SELL || P->m.kernel == SPMV_KERNEL_SELLP || P->m.gtc_on);
+    // x-staged stencil classes (levels 1-3 of the box hierarchies): d*f can be
+    // staged with the window (1-B codes of d per staged point) and the
+    // correction's d*f epilogue streams dc and f in place of v, saving the
+    // 24n-byte d*f pass and its launch.  Measured a net loss on the C2 cycle
+    // (profiles/r03/ab_fold_xscs_{on,off_wpr1}.txt: dependent code -> table loads lengthen
+    // the staging, RESID0 44.4 vs 33.3 + 8.5 us on A_1; ADD0 on P_1 49.5 vs
+    // 46.5 us), so off by default; FAMG_FOLD_XSCS=1 turns it on (also for the
+    // small wave-per-row levels below, which lose 0.6 us the same way).
+    const char *fx = getenv("FAMG_FOLD_XSCS");  // read per cycle build (host only; graphs replay)
+    const bool fold_xscs = fx && fx[0] == '1';
+    const bool p_add0 = P && (P->m.kernel == SPMV_KERNEL_SELL || P->m.kernel == SPMV_KERNEL_SELLP ||
+                              P->m.kernel == SPMV_KERNEL_STREAM || P->m.kernel == SPMV_KERNEL_VECTOR || P->m.gtc_on);
     const bool fold = fold_zero_guess && v_zero && steps == 1 && A && D && P &&
                       ((A->m.kernel == SPMV_KERNEL_SELL && A->m.sell_vbits == 0 && gather_cheap) ||
                        A->m.kernel == SPMV_KERNEL_XS ||  // x-staged: d*x staged with x, no extra gather
                        (fold_xscs && A->m.kernel == SPMV_KERNEL_SCS && A->m.xscs && p_add0) ||
+                       // wave-per-row levels small enough that x and d stay in L2 (A_4 of the
+                       // box hierarchies: 4096 rows): d gathered beside x costs no HBM bytes
+                       (fold_xscs && A->m.kernel == SPMV_KERNEL_VECTOR && A->m.ncols <= 65536 && p_add0) ||
                        (A->m.kernel == SPMV_KERNEL_DIA &&
                         (fold_dia_mode() == 1 ||
                          (fold_dia_mode() < 0 &&
