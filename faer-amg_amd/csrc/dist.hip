@@ -592,6 +592,7 @@ struct DistMultigridOp : LinOp {
                 epi.d = D.S->d.get();
                 epi.dc = D.S->dcode.get();
                 epi.dt = D.S->dtab.get();
+                epi.dk = D.S->dconst;
                 halo_spmv(D.sp, v, D.A->m, t, SPMV_JACOBI, epi);
             }
             std::swap(v, t);
@@ -793,7 +794,7 @@ static std::shared_ptr<DistMultigridOp> build_dist(amg_comm *comm, const Multigr
         D.S->nrows = D.S->ncols = D.sp.n_own;
         D.S->d.resize(D.sp.n_own);
         if (D.sp.n_own) vec_copy(D.S->d.get(), S->d.get() + D.sp.r0, D.sp.n_own, ctx->stream);
-        array_codes_u8(D.S->d.get(), D.sp.n_own, *ctx, D.S->dcode, D.S->dtab);  // 1 B per row when few values
+        array_codes_u8(D.S->d.get(), D.sp.n_own, *ctx, D.S->dcode, D.S->dtab, &D.S->dconst);  // 1 B per row when few values
         D.S->codes_tried = true;
     }
     // ghost sets: space l collects A_l, R_l (fine columns) and P_{l-1} (coarse columns)

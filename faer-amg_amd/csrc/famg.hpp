@@ -230,6 +230,7 @@ struct SpmvEpi {
     const int32_t *perm = nullptr;
     const uint8_t *dc = nullptr;  // JACOBI only: 8-bit codes of d into dt
     const double *dt = nullptr;
+    double dk = 0.0;              // d when every entry is this one value (0: not constant)
 };
 
 // y = epilogue(A x) over all rows (seg < 0) or over row segment `seg`, with the
@@ -262,7 +263,9 @@ void vec_mul(double *out, const double *d, const double *a, int64_t n, hipStream
 // out = dt[dc] * a (8-bit codes of the diagonal)
 void vec_mul_coded(double *out, const uint8_t *dc, const double *dt, const double *a, int64_t n, hipStream_t s);
 // 8-bit codes of v (<= 256 distinct values): returns the table size, 0 if none built
-int64_t array_codes_u8(const double *v, int64_t n, Ctx &ctx, DevBuf<uint8_t> &code, DevBuf<double> &table);
+// dconst (optional): set to the value when v holds one distinct nonzero value, else 0
+int64_t array_codes_u8(const double *v, int64_t n, Ctx &ctx, DevBuf<uint8_t> &code, DevBuf<double> &table,
+                       double *dconst = nullptr);
 void vec_axpy(double *y, double alpha, const double *x, int64_t n, hipStream_t s);      // y+=a x
 void vec_xpay(double *y, double beta, const double *x, int64_t n, hipStream_t s);       // y=x+b y
 void vec_scale(double *x, double alpha, int64_t n, hipStream_t s);                      // x*=a
@@ -344,6 +347,7 @@ struct DiagOp : LinOp {
     // values; the V-cycle's Jacobi steps then read 1 B per row instead of 8)
     DevBuf<uint8_t> dcode;
     DevBuf<double> dtab;
+    double dconst = 0.0;  // d when it is one value (set with the codes), else 0
     bool codes_tried = false;
     Kind kind() const override { return Kind::Diag; }
     bool is_precond() const override { return true; }

@@ -135,6 +135,8 @@ struct GtcArgs {
     const double *d;
     const uint8_t *dc;
     const double *dt;
+    int dconst;  // ADD0 with coded d of one value: d = dk, no codes read
+    double dk;
 };
 
 // The class dictionary and value table into LDS: every load of a lane issued
@@ -177,7 +179,10 @@ __global__ __launch_bounds__(256) void k_gtc_interp(GtcArgs a) {
     double yb[GP_TZ];
     bool live[GP_TZ];
     if constexpr (MODE == SPMV_ADD0)
-        if (a.dc) sdt[tid] = a.dt[tid];
+        if (a.dc && !a.dconst) sdt[tid] = a.dt[tid];
+    double dk = 0.0;
+    if constexpr (MODE == SPMV_ADD0)
+        if (a.dconst) dk = a.dk;
 #pragma unroll
     for (int j = 0; j < GP_TZ; j++) {
         const int gz = z0 + j;
@@ -189,8 +194,9 @@ __global__ __launch_bounds__(256) void k_gtc_interp(GtcArgs a) {
             if constexpr (MODE == SPMV_ADD) yb[j] = a.y[i];
             if constexpr (MODE == SPMV_ADD0) {
                 yb[j] = a.b[i];
-                if (a.dc) dci[j] = a.dc[i];
-                else yb[j] = a.d[i] * yb[j];  // d*b
+                if (a.dconst) yb[j] = dk * yb[j];  // d*b (vec_mul's product)
+                else if (a.dc) dci[j] = a.dc[i];
+                else yb[j] = a.d[i] * yb[j];
             }
         }
     }
@@ -206,7 +212,7 @@ __global__ __launch_bounds__(256) void k_gtc_interp(GtcArgs a) {
     for (int j = 0; j < GP_TZ; j++) {
         if (!live[j]) continue;
         if constexpr (MODE == SPMV_ADD0)
-            if (a.dc) yb[j] = sdt[dci[j]] * yb[j];  // d*b, d decoded after the barrier
+            if (a.dc && !a.dconst) yb[j] = sdt[dci[j]] * yb[j];  // d*b, d decoded after the barrier
         const int gz = z0 + j;
         const int base = (((gz >> 1) - wz0) * GP_WY + (gy >> 1) - wy0) * GP_WX + (gx >> 1) - wx0;
         const uint16_t *e = sd + cl[j] * a.ke;
@@ -391,6 +397,12 @@ bool gtc_supports(const GpuCsr &m, SpmvMode mode) {
     return m.gtc_r ? mode == SPMV_SET : (mode == SPMV_SET || mode == SPMV_ADD || mode == SPMV_ADD0);
 }
 
+// A/B switch FAMG_DIA_DK=0 (shared with the DIA kernels): a constant coded d is read per row
+static bool gtc_dk_enabled() {
+    const char *e = getenv("FAMG_DIA_DK");
+    return !(e && e[0] == '0');
+}
+
 void spmv_gtc(const GpuCsr &m, const double *x, double *y, SpmvMode mode, const SpmvEpi &epi, hipStream_t s) {
     GtcArgs a{};
     a.cls = m.gtc_cls.get();
@@ -408,6 +420,8 @@ void spmv_gtc(const GpuCsr &m, const double *x, double *y, SpmvMode mode, const 
     a.d = epi.d;
     a.dc = epi.dc;
     a.dt = epi.dt;
+    a.dconst = epi.dc && epi.dk != 0.0 && gtc_dk_enabled();
+    a.dk = epi.dk;
     if (m.gtc_r) {
         FAMG_REQUIRE(mode == SPMV_SET, AMG_ERR_UNSUPPORTED, "grid-transfer R: SET only");
         a.ntx = (int)ceil_div(a.rx, GR_TX);

@@ -445,7 +445,7 @@ void MultigridOp::ensure_workspace() {
     for (auto &L : levels) {
         auto *D = dynamic_cast<DiagOp *>(L.S.get());
         if (D && !D->codes_tried) {
-            array_codes_u8(D->d.get(), D->nrows, *ctx, D->dcode, D->dtab);
+            array_codes_u8(D->d.get(), D->nrows, *ctx, D->dcode, D->dtab, &D->dconst);
             D->codes_tried = true;
         }
     }
@@ -492,6 +492,7 @@ void MultigridOp::smooth(int64_t l, double *&v, double *&t, const double *f, boo
                 epi.d = D->d.get();
                 epi.dc = D->dcode.get();
                 epi.dt = D->dtab.get();
+                epi.dk = D->dconst;
                 spmv(A->m, v, t, SPMV_JACOBI, epi, s);
             }
             std::swap(v, t);
@@ -587,6 +588,7 @@ void MultigridOp::cycle(int64_t l, double *v, const double *f, bool v_zero, doub
             epi.d = D->d.get();
             epi.dc = D->dcode.get();  // DIA: 1-B codes of d gathered instead of d
             epi.dt = D->dtab.get();
+            epi.dk = D->dconst;
             spmv(A->m, f, L.r.get(), SPMV_RESID0, epi, s);  // work = f - A (d f)
         }
     } else {
@@ -628,6 +630,7 @@ void MultigridOp::cycle(int64_t l, double *v, const double *f, bool v_zero, doub
         epi.d = D->d.get();
         epi.dc = D->dcode.get();
         epi.dt = D->dtab.get();
+        epi.dk = D->dconst;
         spmv(P->m, C.v.get(), t, SPMV_ADD0, epi, s);  // v = d f + P v_c
         std::swap(v, t);                               // (where smooth() would have left v)
     } else if (P) {

@@ -26,6 +26,8 @@
 
 #include "famg.hpp"
 
+#include <cstring>
+
 namespace famg {
 
 typedef double dbl2_t __attribute__((ext_vector_type(2)));
@@ -83,6 +85,7 @@ struct Epi {
     const int32_t *perm;
     const uint8_t *dc;  // JACOBI: d[i] = dt[dc[i]] when set (8-bit codes of the diagonal)
     const double *dt;
+    double dk;          // d when it is one value (the constant-diagonal epilogues)
 };
 
 // Operands of the epilogue that do not depend on the row sum are fetched
@@ -1060,6 +1063,11 @@ constexpr int DIA_JACOBI_DC = 16;
 // the 7-point kernel gathers the 1-B codes of d beside x (dt staged in LDS)
 // instead of 8-B values of d: 17 MB instead of 134 MB more than a residual.
 constexpr int DIA_RESID0_DC = 17;
+// The same two epilogues when the coded diagonal is one value (Epi::dk: the 7-point
+// Laplacian's a_ii = 6 everywhere): d is one scalar load, no per-row or gathered
+// codes (the 7-point run kernel only)
+constexpr int DIA_JACOBI_DK = 18;
+constexpr int DIA_RESID0_DK = 19;
 
 // 8-bit codes at the positions dia_gx2 / dia_gx4 take their x operands from
 // (same clamps and selects)
@@ -1106,14 +1114,15 @@ template <int MODE, bool NT> struct DiaEpi {
         i2 = min(r, row_end - 2);
         l0 = r < row_end;
         l1 = r + 1 < row_end;
-        if constexpr (MODE == SPMV_JACOBI || MODE == DIA_JACOBI_DC) {
+        if constexpr (MODE == SPMV_JACOBI || MODE == DIA_JACOBI_DC || MODE == DIA_JACOBI_DK) {
             const dbl2u_t *q = reinterpret_cast<const dbl2u_t *>(a.x + i2);  // x is gathered: cached
             xr = *q;
             if (row != i2) xr.x = xr.y;
             br = ldv(a.b);
         }
         if constexpr (MODE == SPMV_JACOBI) dr = ldv(a.d);
-        if constexpr (MODE == SPMV_RESID || MODE == SPMV_RESID0 || MODE == DIA_RESID0_DC) br = ldv(a.b);
+        if constexpr (MODE == SPMV_RESID || MODE == SPMV_RESID0 || MODE == DIA_RESID0_DC || MODE == DIA_RESID0_DK)
+            br = ldv(a.b);
         if constexpr (MODE == SPMV_ADD) yr = ldv(a.y);
         if constexpr (MODE == SPMV_ADD0) yr = ldv(a.d) * ldv(a.b);
     }
@@ -1123,7 +1132,8 @@ template <int MODE, bool NT> struct DiaEpi {
         if constexpr (MODE == DIA_JACOBI_DC) dr = dbl2_t{sdt[dc0], sdt[dc1]};
         if constexpr (MODE == SPMV_SET) out = acc;
         else if constexpr (MODE == SPMV_ADD || MODE == SPMV_ADD0) out = yr + acc;
-        else if constexpr (MODE == SPMV_RESID || MODE == SPMV_RESID0 || MODE == DIA_RESID0_DC) out = br - acc;
+        else if constexpr (MODE == SPMV_RESID || MODE == SPMV_RESID0 || MODE == DIA_RESID0_DC || MODE == DIA_RESID0_DK)
+            out = br - acc;
         else out = xr + dr * (br - acc);  // JACOBI
         if (l1) {
             if constexpr (NT) __builtin_nontemporal_store(out, reinterpret_cast<dbl2u_t *>(a.y + row));
@@ -1171,8 +1181,12 @@ template <int MODE, int VB, int CW, bool NT, int NR = 0>
 __global__ __launch_bounds__(256) void spmv_dia_kernel(DiaArgs a) {
     constexpr bool DC = MODE == DIA_JACOBI_DC;
     constexpr bool RC = MODE == DIA_RESID0_DC && NR == -1;  // coded d gathered beside x
-    // x operand of the row sums (RC: plain x, multiplied by the decoded d after the barrier)
-    constexpr int GM = DC ? SPMV_JACOBI : RC ? SPMV_SET : MODE == DIA_RESID0_DC ? SPMV_RESID0 : MODE;
+    constexpr bool JK = MODE == DIA_JACOBI_DK, RK = MODE == DIA_RESID0_DK;  // d = dt[0]
+    static_assert(!(JK || RK) || NR == -1, "constant-d epilogues: 7-point run kernel only");
+    // x operand of the row sums (RC, RK: plain x, multiplied by d after the loads)
+    constexpr int GM = DC || JK ? SPMV_JACOBI : RC || RK ? SPMV_SET : MODE == DIA_RESID0_DC ? SPMV_RESID0 : MODE;
+    double dk = 0.0;
+    if constexpr (JK || RK) dk = a.e.dk;
     __shared__ double stab[VB == 4 ? 16 : 256];
     __shared__ double sdt[DC || RC ? 256 : 1];
     const double tv = (int)threadIdx.x < a.ntab ? a.vtab[threadIdx.x] : 0.0;
@@ -1235,6 +1249,15 @@ __global__ __launch_bounds__(256) void spmv_dia_kernel(DiaArgs a) {
 #pragma unroll
         for (int j = 0; j < 4; j++) xq[0][j] = sdt[kq[j]] * xq[0][j];
     }
+    if constexpr (RK) {  // the same product with the one value of d
+#pragma unroll
+        for (int i = 0; i < 4; i++)
+#pragma unroll
+            for (int j = 0; j < 2; j++) xs7[i][j] = dk * xs7[i][j];
+#pragma unroll
+        for (int j = 0; j < 4; j++) xq[0][j] = dk * xq[0][j];
+    }
+    if constexpr (JK) ep.dr = dbl2_t{dk, dk};
     double acc0 = 0.0, acc1 = 0.0;
     if constexpr (NR == -1) {
 #pragma unroll
@@ -1741,7 +1764,8 @@ __global__ __launch_bounds__(256) void k_value_set(const double *val, int64_t nn
 
 // Code width for m's values (0 = keep fp64, 4, 8 or 16) and the table: the
 // distinct bit patterns, +0.0 (padding) included, ascending as unsigned.
-static int value_table_of(const double *val, int64_t nnz, hipStream_t s, std::vector<unsigned long long> &tab);
+static int value_table_of(const double *val, int64_t nnz, hipStream_t s, std::vector<unsigned long long> &tab,
+                          unsigned *found = nullptr);
 
 int csr_value_table(const GpuCsr &m, std::vector<unsigned long long> &tab);
 static int value_table(const GpuCsr &m, std::vector<unsigned long long> &tab) { return csr_value_table(m, tab); }
@@ -1751,7 +1775,8 @@ int csr_value_table(const GpuCsr &m, std::vector<unsigned long long> &tab) {
     return value_table_of(m.val.get(), m.nnz, m.ctx->stream, tab);
 }
 
-static int value_table_of(const double *val, int64_t nnz, hipStream_t s, std::vector<unsigned long long> &tab) {
+static int value_table_of(const double *val, int64_t nnz, hipStream_t s, std::vector<unsigned long long> &tab,
+                          unsigned *found) {
     tab.clear();
     DevBuf<unsigned long long> slots(VT_SLOTS);
     DevBuf<unsigned int> cnt(1);
@@ -1766,6 +1791,7 @@ static int value_table_of(const double *val, int64_t nnz, hipStream_t s, std::ve
                                   hipMemcpyDeviceToHost, s));
     FAMG_CHECK_HIP(hipMemcpyAsync(&c, cnt.get(), sizeof(c), hipMemcpyDeviceToHost, s));
     FAMG_CHECK_HIP(hipStreamSynchronize(s));
+    if (found) *found = c;  // distinct values present (the table adds 0.0)
     if (c > (unsigned)VT_MAX) return 0;
     for (unsigned long long b : h)
         if (b != VT_EMPTY) tab.push_back(b);
@@ -1868,13 +1894,19 @@ __global__ __launch_bounds__(256) void k_array_codes(const double *v, int64_t n,
     code[i] = (uint8_t)lo;
 }
 
-int64_t array_codes_u8(const double *v, int64_t n, Ctx &ctx, DevBuf<uint8_t> &code, DevBuf<double> &table) {
+int64_t array_codes_u8(const double *v, int64_t n, Ctx &ctx, DevBuf<uint8_t> &code, DevBuf<double> &table,
+                       double *dconst) {
     code.release();
     table.release();
+    if (dconst) *dconst = 0.0;
     if (!g_value_codes || n == 0) return 0;
     std::vector<unsigned long long> tab;
-    const int vb = value_table_of(v, n, ctx.stream, tab);
+    unsigned found = 0;
+    const int vb = value_table_of(v, n, ctx.stream, tab, &found);
     if (vb != 4 && vb != 8) return 0;
+    if (dconst && found == 1)  // one value present (the table's other entry is the added 0.0)
+        for (unsigned long long bits : tab)
+            if (bits != 0ull) std::memcpy(dconst, &bits, 8);
     table.resize(256);  // padded: kernels stage all 256 entries without a bound
     FAMG_CHECK_HIP(hipMemsetAsync(table.get(), 0, 256 * sizeof(double), ctx.stream));
     code.resize(n + 2);
@@ -2314,6 +2346,15 @@ void spmm(const GpuCsr &m, const double *x, int64_t ldx, double *y, int64_t ldy,
 
 template <int M, int VB, int CW>
 static void launch_dia(int runs, bool nt, dim3 grid, dim3 block, hipStream_t s, const DiaArgs &a) {
+    if constexpr (M == DIA_JACOBI_DK || M == DIA_RESID0_DK) {  // chosen only for the 7-point run kernel
+        if constexpr (CW * 32 / VB >= 7) {
+            if (runs == -1) {
+                spmv_dia_kernel<M, VB, CW, false, -1><<<grid, block, 0, s>>>(a);
+                return;
+            }
+        }
+        fail(AMG_ERR_INVALID, "DIA: constant-diagonal epilogue outside the 7-point run kernel");
+    } else {
     if constexpr (CW * 32 / VB >= 27) {
         if (runs == 9) {
             spmv_dia_kernel<M, VB, CW, false, 9><<<grid, block, 0, s>>>(a);
@@ -2328,6 +2369,7 @@ static void launch_dia(int runs, bool nt, dim3 grid, dim3 block, hipStream_t s, 
     }
     if (nt) spmv_dia_kernel<M, VB, CW, true><<<grid, block, 0, s>>>(a);
     else spmv_dia_kernel<M, VB, CW, false><<<grid, block, 0, s>>>(a);
+    }
 }
 
 // A/B switch FAMG_DIA_RUNS=0: the 27-point DIA kernels load every diagonal's pair
@@ -2373,6 +2415,23 @@ static bool dia_runs7() {
         return !(e && e[0] == '0');
     }();
     return on;
+}
+
+// A/B switch FAMG_DIA_DK=0: a constant coded diagonal is still read per row
+static bool dia_dk_enabled() {  // read per launch (host only; graphs replay), so tests can switch it
+    const char *e = getenv("FAMG_DIA_DK");
+    return !(e && e[0] == '0');
+}
+
+// The 7-point run pattern of the DIA kernel (NR = -1)
+static bool dia_run7(const GpuCsr &m) {
+    return m.dia_k == 7 && dia_runs7() && m.dia_off[3] == m.dia_off[2] + 1 && m.dia_off[4] == m.dia_off[2] + 2;
+}
+
+// JACOBI / RESID0 with a coded diagonal of one value on the 7-point DIA kernel:
+// d is dt[0], no codes are read
+static bool dia_dk(const GpuCsr &m, const SpmvEpi &epi) {
+    return epi.dc && epi.dk != 0.0 && dia_dk_enabled() && !m.dia_pat && dia_run7(m);
 }
 
 thread_local LaunchLog *g_launch_log = nullptr;
@@ -2428,7 +2487,9 @@ static void log_spmv(const GpuCsr &m, SpmvMode mode, const SpmvEpi &epi, int64_t
         mat = csr_mat;
     }
     const int64_t xcols = part(m.ncols);
-    const int64_t db = (epi.dc ? 1 : 8);  // bytes per diagonal entry (8-bit codes or fp64)
+    const bool dk = (kernel == SPMV_KERNEL_DIA && dia_dk(m, epi)) ||  // one value of d: no codes read
+                    (kernel == SPMV_KERNEL_GTC && mode == SPMV_ADD0 && epi.dc && epi.dk != 0.0 && dia_dk_enabled());
+    const int64_t db = dk ? 0 : (epi.dc ? 1 : 8);  // bytes per diagonal entry (8-bit codes or fp64)
     int64_t vec = 8 * xcols;              // x read once
     switch (mode) {
     case SPMV_SET: vec += 8 * r; break;                  // y written
@@ -2437,8 +2498,8 @@ static void log_spmv(const GpuCsr &m, SpmvMode mode, const SpmvEpi &epi, int64_t
     case SPMV_JACOBI: vec += 16 * r + db * r; break;     // b, d read, y written
     case SPMV_SGS: vec += 28 * r; break;                 // perm, d, b read, x written
     case SPMV_RESID0:  // x = b; d gathered beside x (1-B codes in the DIA and x-staged class kernels); y written
-        vec += 8 * r + (((kernel == SPMV_KERNEL_DIA && dia_rc_enabled()) || (kernel == SPMV_KERNEL_SCS && m.xscs))
-                            && epi.dc ? 1 : 8) * xcols;
+        vec += 8 * r + (dk ? 0 : (((kernel == SPMV_KERNEL_DIA && dia_rc_enabled()) || (kernel == SPMV_KERNEL_SCS && m.xscs))
+                                   && epi.dc ? 1 : 8)) * xcols;
         break;
     case SPMV_ADD0: vec += 16 * r + db * r; break;       // b, d read, y written
     }
@@ -2451,7 +2512,7 @@ void spmv(const GpuCsr &m, const double *x, double *y, SpmvMode mode, const Spmv
     FAMG_REQUIRE(seg < (int64_t)m.seg_rows.size() - 1, AMG_ERR_INVALID, "SpMV segment out of range");
     FAMG_REQUIRE(mode != SPMV_SGS || epi.perm, AMG_ERR_INVALID, "SGS mode needs a permutation");
     if (g_launch_log) log_spmv(m, mode, epi, seg);
-    Epi e{x, y, epi.b, epi.d, epi.perm, epi.dc, epi.dt};
+    Epi e{x, y, epi.b, epi.d, epi.perm, epi.dc, epi.dt, epi.dk};
     const dim3 block(256);
     if (m.gtc_on && seg < 0 && gtc_supports(m, mode)) {
         spmv_gtc(m, x, y, mode, epi, s);
@@ -2552,8 +2613,8 @@ void spmv(const GpuCsr &m, const double *x, double *y, SpmvMode mode, const Spmv
         bool runs9 = m.dia_k == 27 && dia_runs();
         for (int j = 0; runs9 && j < 9; j++)
             runs9 = m.dia_off[3 * j + 1] == m.dia_off[3 * j] + 1 && m.dia_off[3 * j + 2] == m.dia_off[3 * j] + 2;
-        const bool run7 = m.dia_k == 7 && dia_runs7() && m.dia_off[3] == m.dia_off[2] + 1 &&
-                          m.dia_off[4] == m.dia_off[2] + 2;
+        const bool run7 = dia_run7(m);
+        const bool dk = dia_dk(m, epi);
         const int runs9i = runs9 ? 9 : run7 ? -1 : 0;
         const int pat = m.dia_pat ? m.dia_pat : runs9 && dia_pat27() && (key == 4 * 16 + 4 || key == 8 * 16 + 8) ? 27 : 0;
         if (pat) {
@@ -2598,14 +2659,18 @@ void spmv(const GpuCsr &m, const double *x, double *y, SpmvMode mode, const Spmv
     case SPMV_ADD: FAMG_DIA2(SPMV_ADD, VB, CW) break;                                             \
     case SPMV_RESID: FAMG_DIA2(SPMV_RESID, VB, CW) break;                                         \
     case SPMV_JACOBI:                                                                             \
-        if (e.dc) {                                                                               \
+        if (dk) {                                                                                 \
+            FAMG_DIA2(DIA_JACOBI_DK, VB, CW)                                                      \
+        } else if (e.dc) {                                                                        \
             FAMG_DIA2(DIA_JACOBI_DC, VB, CW)                                                      \
         } else {                                                                                  \
             FAMG_DIA2(SPMV_JACOBI, VB, CW)                                                        \
         }                                                                                         \
         break;                                                                                    \
     case SPMV_RESID0:                                                                             \
-        if (e.dc && dia_rc_enabled()) {                                                           \
+        if (dk) {                                                                                 \
+            FAMG_DIA2(DIA_RESID0_DK, VB, CW)                                                      \
+        } else if (e.dc && dia_rc_enabled()) {                                                    \
             FAMG_DIA2(DIA_RESID0_DC, VB, CW)                                                      \
         } else {                                                                                  \
             FAMG_DIA2(SPMV_RESID0, VB, CW)                                                        \

@@ -1320,6 +1320,38 @@ def test_grid_transfer_classes(ctx, gen, dims):
     assert np.linalg.norm(z - zref) <= 1e-11 * np.linalg.norm(zref)
 
 
+def test_constant_diagonal_epilogues_bitwise(ctx):
+    """The 7-point Laplacian's Jacobi diagonal is one value (a_ii = 6): the DIA
+    JACOBI / folded RESID0 epilogues and the grid-transfer ADD0 read it as one
+    scalar (dt[0]) instead of 1-B codes per row / per gathered column.  The
+    V-cycle is bitwise the coded path's (FAMG_DIA_DK=0) and the plan charges
+    no code bytes on the fine level (RESID0 16 n + format, JACOBI 24 n +
+    format)."""
+    import torch
+    dims = (64, 64, 64)
+    b = T(np.random.default_rng(3).uniform(-1, 1, int(np.prod(dims))))
+    outs, plans = {}, {}
+    for dk in ("1", "0"):
+        os.environ["FAMG_DIA_DK"] = dk
+        try:
+            A = fa().SparseMatOp.laplace3d_7pt(ctx, *dims)
+            mg = fa().sa_build_box(A, dims, (2, 2, 2), coarsest_dim=100)
+            mg.set_graph(False)
+            z = torch.empty_like(b)
+            mg.apply(z, b)
+            ctx.synchronize()
+            outs[dk] = H(z)
+            plans[dk] = [p for p in mg.cycle_plan() if p["level"] == 0]
+        finally:
+            os.environ.pop("FAMG_DIA_DK", None)
+    assert np.array_equal(outs["1"].view(np.int64), outs["0"].view(np.int64))
+    n = int(np.prod(dims))
+    by = {p["mode"]: p["bytes"] for p in plans["1"]}
+    by0 = {p["mode"]: p["bytes"] for p in plans["0"]}
+    if "RESID0" in by and A.spmv_info()["kernel"] == "dia":
+        assert by0["RESID0"] - by["RESID0"] == n and by0["JACOBI"] - by["JACOBI"] == n, (by, by0)
+
+
 def test_cycle_plan_accounts_for_every_launch(ctx):
     """amg_multigrid_cycle_plan: the launches of one V-cycle as the library makes
     them.  On the 7-pt box hierarchy the fine level folds its zero-guess step
@@ -1346,8 +1378,8 @@ def test_cycle_plan_accounts_for_every_launch(ctx):
     if "RESID0" in modes0:
         # folded: RESID0 (f - A d f), R, ADD0 (d f + P v_c), post-smoothing Jacobi
         assert modes0 == ["RESID0", "SET", "ADD0", "JACOBI"], f0
-        if info["kernel"] == "dia":  # 17 n: f read, 1-B codes of d gathered, r written
-            assert f0[0]["bytes"] == info["stream_bytes"] + 17 * n, f0[0]
+        if info["kernel"] == "dia":  # 16 n: f read, r written; d = 6/omega everywhere is one scalar
+            assert f0[0]["bytes"] == info["stream_bytes"] + 16 * n, f0[0]
     else:
         # d*f pass, residual, restriction, interpolate-add, post-smoothing Jacobi
         assert modes0 == ["-", "RESID", "SET", "ADD", "JACOBI"], f0
