@@ -482,6 +482,8 @@ def run_dist(args, world, rank, local_rank):
     dist.broadcast_object_list(obj, src=0)
     comm = fa.Comm(ctx, nranks=world, rank=rank, uid=obj[0])
     dm = fa.DistMultigrid(comm, mg, splits, agglomerate_rows=args.agglomerate).set_overlap(not args.no_overlap)
+    if args.dist_graph:
+        dm.set_graph(True)
     infos = [dm.level_info(l) for l in range(nl)]
     n_glob = A.nrows
     del mg, A  # global fine levels are no longer needed on this rank
@@ -570,6 +572,7 @@ def run_dist(args, world, rank, local_rank):
                    "rel_residual_after_1_cycle": float(hist[1]) if len(hist) > 1 else None,
                    "agglomerate_rows": args.agglomerate,
                    "halo_overlap": not args.no_overlap,
+                   "dist_graph": bool(args.dist_graph),
                    "rccl": fa.rccl_library(),
                    "rccl_ranks": comm.nranks,
                    "parallelism": f"row-block {'z-slabs' if args.problem in ('7pt', '27pt') else 'row ranges'} "
@@ -746,6 +749,8 @@ def main():
     ap.add_argument("--cpu-budget", type=float, default=20.0,
                     help="seconds of CPU V-cycles at --cpu-threads (half that at all cores)")
     ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--dist-graph", action="store_true",
+                    help="replay the distributed cycle as a captured hipGraph (RCCL p2p + all-gather captured)")
     ap.add_argument("--no-overlap", action="store_true",
                     help="distributed: exchange halos before the SpMV instead of under its interior rows")
     ap.add_argument("--ab", action="store_true", help="A/B the SpMV storage formats (stderr)")

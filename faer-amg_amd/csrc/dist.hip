@@ -501,9 +501,24 @@ struct DistMultigridOp : LinOp {
     bool overlap = true;
     hipStream_t comm_stream = nullptr;
     hipEvent_t ev_pack = nullptr, ev_halo = nullptr;
+    // hipGraph replay of the cycle (option 1, off by default): RCCL transport only
+    // -- its grouped send/recv and all-gather are stream-ordered and capturable,
+    // the loopback transport synchronises on the host
+    bool use_graph = false;
+    struct Graph {
+        double *out;
+        const double *rhs;
+        hipGraphExec_t exec;
+    };
+    std::vector<Graph> graphs_;
+    void drop_graphs() {
+        for (auto &g : graphs_) (void)hipGraphExecDestroy(g.exec);
+        graphs_.clear();
+    }
     Kind kind() const override { return Kind::DistMultigrid; }
     bool is_precond() const override { return true; }
     ~DistMultigridOp() override {
+        drop_graphs();
         if (ev_pack) (void)hipEventDestroy(ev_pack);
         if (ev_halo) (void)hipEventDestroy(ev_halo);
         if (comm_stream) (void)hipStreamDestroy(comm_stream);
@@ -688,6 +703,39 @@ struct DistMultigridOp : LinOp {
         std::lock_guard<std::mutex> lk(mtx);
         hipStream_t s = ctx->stream;
         tail->ensure_workspace();
+        if (!use_graph || !dynamic_cast<RcclTransport *>(tr.get())) {
+            apply_eager(out, rhs);
+            return;
+        }
+        for (auto &g : graphs_)
+            if (g.out == out && g.rhs == rhs) {
+                FAMG_CHECK_HIP(hipGraphLaunch(g.exec, s));
+                return;
+            }
+        hipGraph_t graph = nullptr;
+        FAMG_CHECK_HIP(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
+        try {
+            apply_eager(out, rhs);
+        } catch (...) {
+            (void)hipStreamEndCapture(s, &graph);
+            if (graph) (void)hipGraphDestroy(graph);
+            throw;
+        }
+        FAMG_CHECK_HIP(hipStreamEndCapture(s, &graph));
+        hipGraphExec_t exec = nullptr;
+        FAMG_CHECK_HIP(hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0));
+        (void)hipGraphDestroy(graph);
+        if (graphs_.size() >= 8) {
+            (void)hipGraphExecDestroy(graphs_.front().exec);
+            graphs_.erase(graphs_.begin());
+        }
+        graphs_.push_back({out, rhs, exec});
+        FAMG_CHECK_HIP(hipGraphLaunch(exec, s));
+    }
+
+    // one cycle issued on the stream (workspaces allocated beforehand)
+    void apply_eager(double *out, const double *rhs) {
+        hipStream_t s = ctx->stream;
         if (La == 0) {
             gather_tail(rhs);
             tail->cycle(0, vc_full.get(), fc_full.get(), true, nullptr);
@@ -1082,7 +1130,8 @@ amg_status amg_dist_set_option(amg_linop *dist, int32_t option, int64_t value) {
         auto d = need_dist(dist);
         std::lock_guard<std::mutex> lk(d->mtx);
         switch (option) {
-        case 0: d->overlap = value != 0; break;
+        case 0: d->overlap = value != 0; d->drop_graphs(); break;
+        case 1: d->use_graph = value != 0; d->drop_graphs(); break;
         default: fail(AMG_ERR_INVALID, "unknown distributed multigrid option");
         }
     });

@@ -972,6 +972,11 @@ class DistMultigrid(LinOp):
         _ck(_lib.amg_dist_set_option(self.h, 0, 1 if on else 0))
         return self
 
+    def set_graph(self, on=True):
+        """hipGraph replay of the distributed cycle (RCCL communicators only; default off)."""
+        _ck(_lib.amg_dist_set_option(self.h, 1, 1 if on else 0))
+        return self
+
     def pcg_solve(self, b, x, max_iter=1000, rel_tol=1e-8, abs_tol=0.0, precondition=True):
         """Distributed PCG (dots all-reduced), one distributed V-cycle per iteration."""
         hist = np.zeros(max(max_iter, 1))

@@ -488,7 +488,9 @@ amg_status amg_dist_level_operator(const amg_linop *dist, int64_t level, amg_lin
 amg_status amg_dist_level_matrix(const amg_linop *dist, int64_t level, int32_t which,
                                  amg_linop **out);
 /* Options of a distributed multigrid: 0 = overlap each halo exchange with the
- * interior rows of the SpMV that consumes it (default 1; 0 exchanges first). */
+ * interior rows of the SpMV that consumes it (default 1; 0 exchanges first);
+ * 1 = replay apply() as a captured hipGraph per (out, rhs) pair (default 0;
+ * RCCL communicators only -- the loopback transport always runs eagerly). */
 amg_status amg_dist_set_option(amg_linop *dist, int32_t option, int64_t value);
 /* Distributed stationary solve (dots all-reduced over ranks): local vectors. */
 amg_status amg_dist_stationary_solve(amg_linop *dist_mg, const double *b, double *x,

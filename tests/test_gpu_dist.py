@@ -195,6 +195,16 @@ def test_rccl_single_rank():
     ctx.synchronize()
     assert torch.allclose(z1, z2, rtol=1e-13, atol=0)
     assert torch.equal(z1, z3)
+    # hipGraph replay of the distributed cycle (RCCL all-gather of the tail captured):
+    # bitwise the eager cycle, replayed twice with the same buffers
+    dm.set_graph(True)
+    z4, z5 = torch.empty_like(b), torch.empty_like(b)
+    dm.apply(z4, b)
+    dm.apply(z4, b)
+    dm.apply(z5, b)
+    ctx.synchronize()
+    assert torch.equal(z1, z4) and torch.equal(z1, z5)
+    dm.set_graph(False)
 
 
 @pytest.mark.parametrize("split_kind", ["slab", "equal"])
