@@ -195,8 +195,23 @@ def test_rccl_single_rank():
     ctx.synchronize()
     assert torch.allclose(z1, z2, rtol=1e-13, atol=0)
     assert torch.equal(z1, z3)
-    # hipGraph replay of the distributed cycle (RCCL all-gather of the tail captured):
-    # bitwise the eager cycle, replayed twice with the same buffers
+
+
+def test_rccl_single_rank_graph():
+    """hipGraph replay of the distributed cycle (amg_dist_set_option 1; the RCCL
+    all-gather of the agglomerated tail captured with the kernels): bitwise the
+    eager cycle, replayed with the same and with other buffers."""
+    import torch
+    ctx = fa().Context(0)
+    comm = fa().Comm(ctx, nranks=1, rank=0, uid=fa().unique_id())
+    dims = (12, 12, 12)
+    A = fa().SparseMatOp.laplace3d_7pt(ctx, *dims)
+    mg = fa().sa_build_box(A, dims, (2, 2, 2), coarsest_dim=60)
+    splits = fa().slab_splits(fa().box_level_dims(dims, (2, 2, 2), mg.levels()), 1)
+    dm = fa().DistMultigrid(comm, mg, splits, agglomerate_rows=100)
+    b = torch.as_tensor(np.random.default_rng(1).uniform(-1, 1, 1728), device="cuda:0")
+    z1 = torch.empty_like(b)
+    dm.apply(z1, b)
     dm.set_graph(True)
     z4, z5 = torch.empty_like(b), torch.empty_like(b)
     dm.apply(z4, b)
