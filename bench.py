@@ -185,7 +185,10 @@ def cpu_side(mg, A, b_host, z_gpu, args):
     OA = levels[0]["A"]
     log(f"oracle hierarchy import {time.perf_counter() - t_imp:.1f}s")
     nproc = os.cpu_count() or 1
-    all_threads = nproc  # every host core ("all host cores", count from nproc)
+    quota = cgroup_cpu_quota()
+    # every host core this process may run on: nproc capped by the cgroup CPU
+    # quota (256 threads inside a 16-CPU quota measured oversubscription)
+    all_threads = max(1, min(nproc, int(quota))) if quota else nproc
     t16 = args.cpu_threads
 
     # parity of one V-cycle (the bench's own z from the timed loop); >= 50 cycles
@@ -227,7 +230,7 @@ def cpu_side(mg, A, b_host, z_gpu, args):
         omg.set_parallel(all_threads)
         tsa, _ = _time_cycles(omg, b_host, args.cpu_budget / 2, min_cycles=3)
         res["all_cores"] = {"value": round(1.0 / float(np.median(tsa)), 4), "cores": all_threads,
-                            "nproc": nproc, "cpu_quota": cgroup_cpu_quota(),
+                            "nproc": nproc, "cpu_quota": quota,
                             "sample": f"median of {len(tsa)} V-cycles at {all_threads} OpenMP threads"}
         omg.set_parallel(t16)
     parity = {"vcycle_rel_err": rel_err, "tol": 1e-11, "ok": rel_err <= 1e-11,
@@ -294,6 +297,71 @@ def plan_summary(plan):
             "per_level": [dict(level=l, **lv[l]) for l in sorted(lv)]}
 
 
+def abi_ingest(fa, ctx, mg, b, z_ref, stream, args):
+    """The drop-in path's rate (what a Rust caller of INTEGRATION.md does): the
+    hierarchy's arrays downloaded to the host and handed back level by level
+    through amg_csr_create (no grid hints), new_jacobi / CoarseCholesky, then
+    Multigrid::new + add_level (multigrid.rs:190-239, core.rs:56-74).  The same
+    cycle is timed; z must equal the headline's bit for bit."""
+    import numpy as np
+    import torch
+    t0 = time.perf_counter()
+    nl = mg.levels()
+    keep = []
+    mg2 = None
+    for l in range(nl):
+        Al, Sl, Rl, Pl = mg.level(l)
+        A2 = fa.SparseMatOp.from_arrays(ctx, *Al.dims(), *Al.arrays())
+        if l == nl - 1:
+            S2 = fa.CoarseCholesky(A2)
+        elif Sl.kind == "sgs":
+            S2 = fa.SymGaussSeidel(A2)
+        elif Sl.kind == "diag" and args.smoother == "jacobi":
+            S2 = fa.new_jacobi(A2, 0.66)
+        elif Sl.kind == "diag" and args.smoother == "l1":
+            S2 = fa.new_l1(A2)
+        else:
+            return {"skipped": f"no drop-in construction for the {Sl.kind} smoother"}
+        if l == 0:
+            mg2 = fa.Multigrid(A2, S2)
+        else:
+            R2 = fa.SparseMatOp.from_arrays(ctx, *Rp.dims(), *Rp.arrays())
+            P2 = fa.SparseMatOp.from_arrays(ctx, *Pp.dims(), *Pp.arrays())
+            mg2.add_level(A2, S2, R2, P2)
+            keep += [R2, P2]
+        keep += [A2, S2]
+        Rp, Pp = Rl, Pl
+    mg2.set_graph(not args.no_graph)
+    mg2.set_fold_zero_guess(not args.no_fold)
+    torch.cuda.synchronize()
+    setup_s = time.perf_counter() - t0
+    z2 = torch.empty_like(b)
+    for _ in range(max(1, args.warmup)):
+        mg2.apply(z2, b)
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(stream)
+    for _ in range(args.steps):
+        mg2.apply(z2, b)
+    e1.record(stream)
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / args.steps
+    same = bool(torch.equal(z2, z_ref))
+    rel = float(torch.linalg.norm(z2 - z_ref) / torch.linalg.norm(z_ref))
+    p1 = plan_summary(mg.cycle_plan())["per_level"]
+    p2 = plan_summary(mg2.cycle_plan())["per_level"]
+    kinds = [d["kernels"] for d in p2]
+    grids = [mg2.level(l)[0].spmv_info()["grid_source"] for l in range(nl)]
+    del mg2, keep
+    torch.cuda.synchronize()
+    return {"vcycles_per_s": round(1000.0 / ms, 3), "ms_per_step": round(ms, 4), "setup_s": round(setup_s, 2),
+            "bitwise_equal_to_headline": same, "rel_diff": rel,
+            "same_launch_plan": [d["kernels"] for d in p1] == kinds,
+            "grid_hints": grids, "per_level_kernels": kinds,
+            "what": "hierarchy arrays re-ingested through amg_csr_create + amg_multigrid_create/add_level "
+                    "(no grid hints: inferred), same timed cycle as the headline"}
+
+
 def run_single(args):
     import numpy as np
     import torch
@@ -355,7 +423,8 @@ def run_single(args):
         A64.apply(y, x)
     spmv64_ms = time_kernel(lambda: A64.apply(y, x), 25, stream)  # 28 launches: apart from the cycle's in a trace
     bytes64 = spmv_bytes_fmt(A64)
-    fp64_values = {"kernel": "spmv_sell_kernel<SET> on A_0, fp64 values", "ms_per_launch": round(spmv64_ms, 5),
+    k64 = A64.spmv_info()["kernel"].replace("-", "_")
+    fp64_values = {"kernel": f"spmv_{k64}_kernel<SET> on A_0, fp64 values", "ms_per_launch": round(spmv64_ms, 5),
                    "bytes_per_launch": bytes64,
                    "achieved": round(bytes64 / (spmv64_ms * 1e-3) / 1e9, 1),
                    "frac": round(bytes64 / (spmv64_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
@@ -381,6 +450,15 @@ def run_single(args):
             log(f"A/B fine SpMV {fmt}: median {np.median(v)*1e3:.1f} us  min {min(v)*1e3:.1f} us  "
                 f"-> {spmv_bytes_fmt(ops[fmt]) / (min(v) * 1e-3) / 1e9:.0f} GB/s")
         del ops
+
+    abi = None
+    if not args.no_abi and args.problem in ("7pt", "27pt"):
+        try:
+            abi = abi_ingest(fa, ctx, mg, b, z, stream, args)
+            log("abi ingest: " + json.dumps({k: v for k, v in abi.items() if k != "per_level_kernels"}))
+        except Exception as e:  # reported, never fatal to the headline
+            abi = {"error": repr(e)}
+            log(f"abi ingest failed: {e!r}")
 
     r = torch.empty_like(b)
     A.apply(r, z)
@@ -413,7 +491,7 @@ def run_single(args):
         "warmup": args.warmup,
         "ms_per_step": round(ms_per_cycle, 4),
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "none",
         "scaling_note": "single GPU: the N = 1 base of bench.py's default weak series "
                         "(256^3 rows per GPU fixed as N grows; --workload c4 gives the strong series)",
         "vs_baseline": None,
@@ -432,6 +510,7 @@ def run_single(args):
                                    "per_level_launches": [d["launches"] for d in psum["per_level"]],
                                    "per_level_kernels": [d["kernels"] for d in psum["per_level"]]},
                    "rel_residual_after_1_cycle": rho1,
+                   "abi_ingest": abi,
                    "parallelism": "single GPU"},
         "fine_spmv_gbs": round(achieved, 1),
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
@@ -643,11 +722,23 @@ def c4_single_gpu_rate(fa, ctx, args, stream, cycles=10):
 
 
 def visible_gpus():
-    """GPUs this process may use.  torch.cuda.device_count() counts devices
-    without creating a HIP context on this image, so the launcher stays
-    GPU-free and its children start on untouched devices."""
-    import torch
-    return torch.cuda.device_count()
+    """GPUs this process may use, counted without torch or HIP (the launcher
+    stays provably GPU-free, so its children start on untouched devices): the
+    *_VISIBLE_DEVICES lists when set, else the KFD topology's GPU nodes."""
+    for var in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        v = os.environ.get(var)
+        if v is not None:
+            return len([t for t in v.split(",") if t.strip() and t.strip() != "-1"])
+    import glob
+    n = 0
+    for props in glob.glob("/sys/class/kfd/kfd/topology/nodes/*/properties"):
+        try:
+            kv = dict(line.split()[:2] for line in open(props) if len(line.split()) >= 2)
+        except OSError:
+            continue
+        if int(kv.get("simd_count", "0")) > 0:  # CPU nodes have no SIMDs
+            n += 1
+    return n
 
 
 def free_port():
@@ -755,6 +846,8 @@ def main():
                     help="distributed: exchange halos before the SpMV instead of under its interior rows")
     ap.add_argument("--ab", action="store_true", help="A/B the SpMV storage formats (stderr)")
     ap.add_argument("--no-general", action="store_true", help="skip roofline.general (random 7-pt)")
+    ap.add_argument("--no-abi", action="store_true",
+                    help="skip config.abi_ingest (the hierarchy re-ingested through the C ABI, timed)")
     ap.add_argument("--no-fold", action="store_true",
                     help="store the zero-guess smoothing step instead of folding it into the residual")
     ap.add_argument("--workload", default="weak", choices=["weak", "c4"],

@@ -2,6 +2,7 @@
 // exceptions to amg_status + a thread-local message; handles are thin boxes
 // around shared_ptr<LinOp> so operators keep what they reference alive (the
 // reference's Arc<dyn LinOp> ownership, core.rs:9-17).
+#include <atomic>
 #include <cmath>
 #include <cstring>
 #include <string>
@@ -75,6 +76,24 @@ void for_columns(LinOp &op, double *out, int64_t ld_out, const double *rhs, int6
 }
 
 }  // namespace
+
+namespace famg {
+static std::atomic<int64_t> g_flag_val[FLAG_COUNT] = {
+    {[] { const char *e = getenv("FAMG_FOLD_XSCS"); return (int64_t)(e && e[0] == '1'); }()},
+    {[] { const char *e = getenv("FAMG_DIA_DK"); return (int64_t)!(e && e[0] == '0'); }()},
+    {[] {
+        const char *e = getenv("FAMG_VEC_WPR");
+        const int w = e ? atoi(e) : 0;
+        return (int64_t)((w == 1 || w == 2 || w == 4) ? w : 0);
+    }()}};
+static std::atomic<uint64_t> g_flag_gen{0};
+int64_t flag(FlagId f) { return g_flag_val[f].load(std::memory_order_relaxed); }
+void set_flag(FlagId f, int64_t v) {
+    g_flag_val[f].store(v);
+    g_flag_gen.fetch_add(1);
+}
+uint64_t flags_generation() { return g_flag_gen.load(); }
+}  // namespace famg
 
 extern "C" {
 
@@ -305,7 +324,35 @@ amg_status amg_csr_set_grid(amg_linop *op, int64_t nx, int64_t ny, int64_t nz) {
         p->m.grid[0] = nx;
         p->m.grid[1] = ny;
         p->m.grid[2] = nz;
+        p->m.grid_src = 1;  // also a cleared hint: nothing is inferred then
         csr_finalize(p->m, &p->m.seg_rows);
+    });
+}
+
+
+amg_status amg_set_flag(int32_t which, int64_t value) {
+    return guard([&] {
+        FAMG_REQUIRE(which >= 0 && which < FLAG_COUNT, AMG_ERR_INVALID, "unknown flag");
+        if (which == FLAG_VEC_WPR)
+            FAMG_REQUIRE(value == 0 || value == 1 || value == 2 || value == 4, AMG_ERR_INVALID,
+                         "waves per row must be 0 (auto), 1, 2 or 4");
+        set_flag((FlagId)which, value);
+    });
+}
+
+amg_status amg_get_flag(int32_t which, int64_t *value) {
+    return guard([&] {
+        FAMG_REQUIRE(which >= 0 && which < FLAG_COUNT && value, AMG_ERR_INVALID, "bad argument");
+        *value = flag((FlagId)which);
+    });
+}
+
+amg_status amg_grid_from_offsets(const int64_t *offs, int64_t k, int64_t n, int64_t *grid3, int32_t *found) {
+    return guard([&] {
+        FAMG_REQUIRE((offs || k == 0) && grid3 && found && k >= 0 && n >= 0, AMG_ERR_INVALID, "bad argument");
+        std::vector<int64_t> o(offs, offs + k);
+        grid3[0] = grid3[1] = grid3[2] = 0;
+        *found = grid_from_offsets(o, n, grid3) ? 1 : 0;
     });
 }
 
@@ -315,6 +362,7 @@ amg_status amg_csr_grid_info(const amg_linop *op, int64_t *info12) {
         const GpuCsr &m = need_csr(op)->m;
         for (int q = 0; q < 12; q++) info12[q] = 0;
         for (int q = 0; q < 3; q++) info12[q] = m.grid[q];
+        info12[10] = m.grid_src;
         const bool on = m.has_scs() && m.xscs;
         info12[3] = on ? 1 : 0;
         for (int q = 0; q < 3; q++) {

@@ -118,6 +118,16 @@ struct Ctx {
 
 inline int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
 
+// Run-time A/B switches that change which kernels a cycle launches (bitwise
+// neutral).  Read once from the environment (FAMG_FOLD_XSCS, FAMG_DIA_DK,
+// FAMG_VEC_WPR) into these flags; amg_set_flag changes one and bumps
+// g_flags_gen, which makes every multigrid drop the hipGraphs it captured under
+// the old value (a graph replays the launches it recorded).
+enum FlagId : int { FLAG_FOLD_XSCS = 0, FLAG_DIA_DK = 1, FLAG_VEC_WPR = 2, FLAG_COUNT = 3 };
+int64_t flag(FlagId f);
+void set_flag(FlagId f, int64_t v);
+uint64_t flags_generation();
+
 // Launch plan (amg_multigrid_cycle_plan): while g_launch_log is set on this
 // thread, every kernel the V-cycle launches appends one record with the
 // algorithmic bytes of that launch (the bytes its storage streams

@@ -43,6 +43,7 @@ void csr_clone(const GpuCsr &src, GpuCsr &dst) {
     }
     FAMG_CHECK_HIP(hipStreamSynchronize(s));
     for (int q = 0; q < 3; q++) dst.grid[q] = src.grid[q];
+    dst.grid_src = src.grid_src;
 }
 
 __global__ void k_narrow_rp(const int64_t *rp64, int32_t *rp32, int64_t n1) {
@@ -117,6 +118,135 @@ static bool xscs_beats_dia(GpuCsr &m) {
     return ms[1] < ms[0];
 }
 
+// ---- grid hint inference (the drop-in path: matrices handed over through
+// amg_csr_create carry no hint, but the x-staged stencil classes and the
+// grid-transfer classes need one)
+
+// centred residue of o mod q, in (-q/2, q/2]
+static int64_t cres(int64_t o, int64_t q) {
+    int64_t r = ((o % q) + q) % q;
+    if (r > q / 2) r -= q;
+    return r;
+}
+
+bool grid_from_offsets(const std::vector<int64_t> &offs_in, int64_t n, int64_t *g) {
+    std::vector<int64_t> O(offs_in);
+    std::sort(O.begin(), O.end());
+    O.erase(std::unique(O.begin(), O.end()), O.end());
+    auto has = [](const std::vector<int64_t> &v, int64_t x) { return std::binary_search(v.begin(), v.end(), x); };
+    // the x radius: offsets 1..rx all present
+    int64_t rx = 0;
+    while (rx < 16 && has(O, rx + 1)) rx++;
+    if (rx == 0 || n <= 2 * rx) return false;
+    int64_t maxabs = 0;
+    for (int64_t o : O) maxabs = std::max<int64_t>(maxabs, std::abs(o));
+    if (maxabs <= rx) {  // 1-D
+        g[0] = n; g[1] = 1; g[2] = 1;
+        return true;
+    }
+    int64_t o1 = INT64_MAX;  // smallest offset past the x run: nx - r' (0 <= r' <= rx)
+    for (int64_t o : O)
+        if (o > rx) { o1 = o; break; }
+    // every (nx, ny) consistent with the offsets; the most compact one (fewest
+    // distinct steps per axis) wins.  The consumers verify every entry against it.
+    int best_score = INT32_MAX;
+    bool found = false;
+    for (int64_t nx = o1; nx <= o1 + rx; nx++) {
+        if (nx <= 2 * rx || n % nx) continue;
+        std::vector<int64_t> dxs, Q;
+        bool ok = true;
+        for (int64_t o : O) {
+            const int64_t dx = cres(o, nx);
+            if (std::abs(dx) > rx) { ok = false; break; }
+            dxs.push_back(dx);
+            Q.push_back((o - dx) / nx);
+        }
+        if (!ok) continue;
+        auto distinct = [](std::vector<int64_t> v) {
+            std::sort(v.begin(), v.end());
+            return (int)(std::unique(v.begin(), v.end()) - v.begin());
+        };
+        std::vector<int64_t> Qs(Q);
+        std::sort(Qs.begin(), Qs.end());
+        Qs.erase(std::unique(Qs.begin(), Qs.end()), Qs.end());
+        int64_t ry = 0;
+        while (ry < 16 && has(Qs, ry + 1)) ry++;
+        const int64_t nyz = n / nx;
+        int64_t maxq = 0;
+        for (int64_t q : Qs) maxq = std::max<int64_t>(maxq, std::abs(q));
+        if (maxq <= ry) {  // 2-D
+            if (ry == 0 || nyz <= 2 * ry) continue;
+            const int score = distinct(dxs) + distinct(Q) + 1;
+            if (score < best_score) {
+                best_score = score;
+                g[0] = nx; g[1] = nyz; g[2] = 1;
+                found = true;
+            }
+            continue;
+        }
+        if (ry == 0) continue;
+        int64_t q1 = INT64_MAX;
+        for (int64_t q : Qs)
+            if (q > ry) { q1 = q; break; }
+        for (int64_t ny = q1; ny <= q1 + ry; ny++) {
+            if (ny <= 2 * ry || nyz % ny) continue;
+            const int64_t nz = nyz / ny;
+            std::vector<int64_t> dys, dzs;
+            bool ok2 = true;
+            for (int64_t q : Q) {
+                const int64_t dy = cres(q, ny);
+                const int64_t dz = (q - dy) / ny;
+                if (std::abs(dy) > ry || std::abs(dz) > 16 || std::abs(dz) >= nz) { ok2 = false; break; }
+                dys.push_back(dy);
+                dzs.push_back(dz);
+            }
+            if (!ok2) continue;
+            const int score = distinct(dxs) + distinct(dys) + distinct(dzs);
+            if (score < best_score) {
+                best_score = score;
+                g[0] = nx; g[1] = ny; g[2] = nz;
+                found = true;
+            }
+        }
+    }
+    return found;
+}
+
+// FAMG_INFER_GRID=0: only explicit grid hints (generators, box hierarchy, amg_csr_set_grid)
+static bool infer_grid_enabled() {
+    static const bool on = [] {
+        const char *e = getenv("FAMG_INFER_GRID");
+        return !(e && e[0] == '0');
+    }();
+    return on;
+}
+
+// The stencil of 64 rows spread over the matrix (their col - row union) through
+// grid_from_offsets.  A wrong guess costs nothing but time: the x-staged classes
+// and the grid-transfer classes check every entry against the hint they get.
+static void infer_grid(GpuCsr &m, const std::vector<int64_t> &rp) {
+    const int64_t n = m.nrows;
+    if (!infer_grid_enabled() || m.grid_src != 0 || n != m.ncols || n < 64 || m.nnz == 0 || m.no_sellp) return;
+    constexpr int NS = 64, MAXLEN = 1024;
+    std::vector<int64_t> offs;
+    std::vector<int32_t> c(MAXLEN);
+    hipStream_t s = m.ctx->stream;
+    for (int k = 0; k < NS; k++) {
+        const int64_t i = ((2 * k + 1) * n) / (2 * NS);
+        const int64_t len = rp[i + 1] - rp[i];
+        if (len > MAXLEN) return;
+        if (len == 0) continue;
+        FAMG_CHECK_HIP(hipMemcpyAsync(c.data(), m.col.get() + rp[i], len * sizeof(int32_t), hipMemcpyDeviceToHost, s));
+        FAMG_CHECK_HIP(hipStreamSynchronize(s));
+        for (int64_t e = 0; e < len; e++) offs.push_back((int64_t)c[e] - i);
+    }
+    int64_t g[3];
+    if (grid_from_offsets(offs, n, g)) {
+        for (int q = 0; q < 3; q++) m.grid[q] = g[q];
+        m.grid_src = 2;
+    }
+}
+
 void csr_finalize(GpuCsr &m, const std::vector<int64_t> *segments) {
     Ctx &ctx = *m.ctx;
     if (segments) {
@@ -147,9 +277,11 @@ void csr_finalize(GpuCsr &m, const std::vector<int64_t> *segments) {
     FAMG_CHECK_HIP(hipMemcpyAsync(m.sched.get(), sched.data(), sched.size() * sizeof(int32_t),
                                   hipMemcpyHostToDevice, ctx.stream));
     FAMG_CHECK_HIP(hipStreamSynchronize(ctx.stream));
+    infer_grid(m, rp);
     scs_release(m);
     sellp_release(m);
     gtc_release(m);
+    m.gtc_tried = false;
     build_sell(m, rp);
     const bool dia_all = m.has_dia() && m.dia_r0 == 0 && m.dia_r1 == m.nrows;
     const int64_t sell_b = m.sell_bytes + 12 * (m.nslices + 1) + 4 * m.sell_steps + 8 * m.sell_ntab;
@@ -466,6 +598,7 @@ void gen_stencil(GpuCsr &m, Ctx *ctx, int64_t nx, int64_t ny, int64_t nz, const 
                        m.col.get(), m.val.get());
     FAMG_CHECK_HIP(hipGetLastError());
     m.grid[0] = nx; m.grid[1] = ny; m.grid[2] = nz;
+    m.grid_src = 1;
     csr_finalize(m);
 }
 

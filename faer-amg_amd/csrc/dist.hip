@@ -511,6 +511,7 @@ struct DistMultigridOp : LinOp {
         hipGraphExec_t exec;
     };
     std::vector<Graph> graphs_;
+    uint64_t flags_gen_ = 0;
     void drop_graphs() {
         for (auto &g : graphs_) (void)hipGraphExecDestroy(g.exec);
         graphs_.clear();
@@ -703,6 +704,10 @@ struct DistMultigridOp : LinOp {
         std::lock_guard<std::mutex> lk(mtx);
         hipStream_t s = ctx->stream;
         tail->ensure_workspace();
+        if (flags_gen_ != flags_generation()) {  // a switch changed: graphs recorded the old launches
+            drop_graphs();
+            flags_gen_ = flags_generation();
+        }
         if (!use_graph || !dynamic_cast<RcclTransport *>(tr.get())) {
             apply_eager(out, rhs);
             return;
@@ -859,6 +864,15 @@ static std::shared_ptr<DistMultigridOp> build_dist(amg_comm *comm, const Multigr
         if (l > 0) space_remap(sp, d->L[l - 1].P->m, ctx);
         sp.mark.release();
         sp.scan.release();
+        // a wave-per-row local matrix splits its rows like the global one (same
+        // waves per row: the same sums)
+        {
+            auto *Ag = dynamic_cast<CsrOp *>(g.levels[l].A.get());
+            auto *Rg = dynamic_cast<CsrOp *>(g.levels[l].R.get());
+            d->L[l].A->m.vec_wpr = Ag->m.vec_wpr;
+            d->L[l].R->m.vec_wpr = Rg->m.vec_wpr;
+            if (l > 0) d->L[l - 1].P->m.vec_wpr = dynamic_cast<CsrOp *>(g.levels[l - 1].P.get())->m.vec_wpr;
+        }
         for (auto *op : {d->L[l].A.get(), d->L[l].R.get()}) {
             op->nrows = op->m.nrows;
             op->ncols = op->m.ncols;

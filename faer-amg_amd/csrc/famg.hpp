@@ -85,6 +85,7 @@ struct GpuCsr {
     DevBuf<int16_t> vec_off;
     int vec_vbits = 0;
     bool vec_o16 = false;
+    int vec_wpr = 1;  // waves per row, chosen once for the whole matrix (flag FLAG_VEC_WPR overrides)
     // 3x3 block storage (bsr.hip): node-row slices, one 4864-B unit per block step
     DevBuf<char> bsr_data;
     DevBuf<int32_t> bsr_row0, bsr_soff;
@@ -121,6 +122,7 @@ struct GpuCsr {
     // grid-transfer classes (gtc.hip) for R/P of a 2x2x2-box hierarchy: an overlay
     // on the finalized storage used for the modes it supports (gtc_supports)
     bool gtc_on = false, gtc_r = false;
+    bool gtc_tried = false;  // gtc_attach ran since the last finalize (attach_box_transfers retries nothing)
     DevBuf<uint8_t> gtc_cls;
     DevBuf<uint16_t> gtc_dict;  // nclass x ke entries: value index << 8 | step slot
     DevBuf<double> gtc_vtab;    // the distinct values (<= 256)
@@ -128,7 +130,9 @@ struct GpuCsr {
     int64_t gtc_fg[3] = {0, 0, 0}, gtc_cg[3] = {0, 0, 0};
     // grid hint: the rows are the points of an nx x ny x nz grid, x fastest (0 = none);
     // set by the stencil generators, the box hierarchy and amg_csr_set_grid
+    // (grid_src 1), else inferred at finalize from the stencil offsets (grid_src 2)
     int64_t grid[3] = {0, 0, 0};
+    int grid_src = 0;
     // x-staged SELL (xsell.hip): per group of 4096 rows the x chunks staged in LDS,
     // per slice fp64 values + 16-bit LDS indices (or 32-bit columns: escape slices)
     DevBuf<char> xs_data;
@@ -157,6 +161,12 @@ struct GpuCsr {
     }
 };
 
+// Grid dims (nx, ny, nz) of a square operator of n rows whose stencil has the
+// offsets offs (col - row over some rows); false if no grid explains them.
+bool grid_from_offsets(const std::vector<int64_t> &offs, int64_t n, int64_t *g);
+// R and P of a 2x2x2-box level as grid-transfer classes when the fine and coarse
+// operators carry grid hints of that relation (Multigrid::add_level)
+void attach_box_transfers(const GpuCsr &Af, const GpuCsr &Ac, GpuCsr &R, GpuCsr &P);
 // Allocate a CSR with the given shape/nnz (arrays uninitialised).
 void csr_alloc(GpuCsr &m, Ctx *ctx, int64_t nrows, int64_t ncols, int64_t nnz);
 // Device copy of the CSR arrays (rp64/col/val) of src into dst; dst is not
@@ -437,6 +447,7 @@ struct MultigridOp : LinOp {
         hipGraphExec_t exec;
     };
     std::vector<GraphEntry> graphs_;
+    uint64_t flags_gen_ = 0;  // flags_generation() the graphs were captured under
     bool workspace_ready_ = false;
     bool fuse_ready_ = false;
 };

@@ -319,6 +319,7 @@ static bool gtc_enabled() {
 
 bool gtc_attach(GpuCsr &m, const int64_t *fg, const int64_t *cg) {
     gtc_release(m);
+    m.gtc_tried = true;
     if (!gtc_enabled() || m.nnz >= (int64_t(1) << 31)) return false;
     const bool is_r = m.nrows < m.ncols;
     std::vector<uint8_t> cls;
@@ -375,6 +376,16 @@ bool gtc_attach(GpuCsr &m, const int64_t *fg, const int64_t *cg) {
     return true;
 }
 
+void attach_box_transfers(const GpuCsr &Af, const GpuCsr &Ac, GpuCsr &R, GpuCsr &P) {
+    const int64_t *fg = Af.grid, *cg = Ac.grid;
+    for (int q = 0; q < 3; q++)
+        if (fg[q] <= 0 || cg[q] != (fg[q] + 1) / 2) return;
+    if (fg[0] * fg[1] * fg[2] != Af.nrows || cg[0] * cg[1] * cg[2] != Ac.nrows) return;
+    if (P.nrows != Af.nrows || P.ncols != Ac.nrows || R.nrows != Ac.nrows || R.ncols != Af.nrows) return;
+    if (!P.gtc_on && !P.gtc_tried) gtc_attach(P, fg, cg);
+    if (!R.gtc_on && !R.gtc_tried) gtc_attach(R, fg, cg);
+}
+
 // fine points per lane along z in the P kernel (FAMG_GTC_TZ=8: eight)
 static int gtc_tz() {
     static const int v = [] {
@@ -398,10 +409,7 @@ bool gtc_supports(const GpuCsr &m, SpmvMode mode) {
 }
 
 // A/B switch FAMG_DIA_DK=0 (shared with the DIA kernels): a constant coded d is read per row
-static bool gtc_dk_enabled() {
-    const char *e = getenv("FAMG_DIA_DK");
-    return !(e && e[0] == '0');
-}
+static bool gtc_dk_enabled() { return flag(FLAG_DIA_DK) != 0; }
 
 void spmv_gtc(const GpuCsr &m, const double *x, double *y, SpmvMode mode, const SpmvEpi &epi, hipStream_t s) {
     GtcArgs a{};

@@ -413,6 +413,16 @@ void MultigridOp::add_level(LinOpPtr A, LinOpPtr S, LinOpPtr R, LinOpPtr P) {
     FAMG_REQUIRE(S->nrows == nc && S->ncols == nc, AMG_ERR_DIM, "add_level: smoother size != op size");
     FAMG_REQUIRE(P->nrows == nf && P->ncols == nc, AMG_ERR_DIM, "add_level: p must be n_fine x n_coarse");
     FAMG_REQUIRE(R->nrows == nc && R->ncols == nf, AMG_ERR_DIM, "add_level: r must be n_coarse x n_fine");
+    // the drop-in path (amg_csr_create per level, then add_level) gets the same
+    // grid-transfer storage as sa_build_box: attached when A_l and A_{l+1} carry
+    // grid hints of a 2x2x2 box relation (inferred at finalize), rows verified
+    {
+        auto *Af = dynamic_cast<CsrOp *>(levels.back().A.get());
+        auto *Ac = dynamic_cast<CsrOp *>(A.get());
+        auto *Rc = dynamic_cast<CsrOp *>(R.get());
+        auto *Pc = dynamic_cast<CsrOp *>(P.get());
+        if (Af && Ac && Rc && Pc) attach_box_transfers(Af->m, Ac->m, Rc->m, Pc->m);
+    }
     levels.back().R = R;
     levels.back().P = P;
     MgLevel L;
@@ -560,8 +570,7 @@ void MultigridOp::cycle(int64_t l, double *v, const double *f, bool v_zero, doub
     // the staging, RESID0 44.4 vs 33.3 + 8.5 us on A_1; ADD0 on P_1 49.5 vs
     // 46.5 us), so off by default; FAMG_FOLD_XSCS=1 turns it on (also for the
     // small wave-per-row levels below, which lose 0.6 us the same way).
-    const char *fx = getenv("FAMG_FOLD_XSCS");  // read per cycle build (host only; graphs replay)
-    const bool fold_xscs = fx && fx[0] == '1';
+    const bool fold_xscs = flag(FLAG_FOLD_XSCS) != 0;
     const bool p_add0 = P && (P->m.kernel == SPMV_KERNEL_SELL || P->m.kernel == SPMV_KERNEL_SELLP ||
                               P->m.kernel == SPMV_KERNEL_STREAM || P->m.kernel == SPMV_KERNEL_VECTOR || P->m.gtc_on);
     const bool fold = fold_zero_guess && v_zero && steps == 1 && A && D && P &&
@@ -653,6 +662,10 @@ void MultigridOp::apply(double *out, const double *rhs) {
     for (size_t l = 0; l + 1 < levels.size(); l++)
         FAMG_REQUIRE(levels[l].R && levels[l].P, AMG_ERR_INVALID, "multigrid level without R/P");
     ensure_workspace();
+    if (flags_gen_ != flags_generation()) {  // a switch changed: graphs recorded the old launches
+        invalidate_graphs();
+        flags_gen_ = flags_generation();
+    }
     hipStream_t s = ctx->stream;
     auto run = [&]() { cycle(0, out, rhs, true, out); };
     if (!use_graph || s == nullptr) {
@@ -783,6 +796,7 @@ CsrPtr galerkin_rap(const CsrOp &R, const CsrOp &A, const CsrOp &P, const int64_
     spgemm(R.m, AP, C, false);
     if (grid)
         for (int q = 0; q < 3; q++) C.grid[q] = grid[q];
+    if (grid) C.grid_src = 1;
     csr_finalize(C);
     return wrap(A.ctx, std::move(C));
 }

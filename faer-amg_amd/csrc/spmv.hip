@@ -2267,6 +2267,8 @@ static void build_vec_codes(GpuCsr &m) {
     m.sell_ntab = vb ? (int64_t)tab.size() : 0;
 }
 
+static int vec_waves_per_row(int64_t rows, int64_t nnz);
+
 void choose_kernel(GpuCsr &m) {
     if (m.has_dia() && !m.dia_rowid && m.dia_r0 == 0 && m.dia_r1 == m.nrows) m.kernel = SPMV_KERNEL_DIA;
     else if (m.has_bsr()) m.kernel = SPMV_KERNEL_BSR;
@@ -2277,6 +2279,7 @@ void choose_kernel(GpuCsr &m) {
     else if (g_spmv_format_policy == 3 ||
              (g_spmv_format_policy == 0 && m.nrows > 0 && m.nnz >= vec_min_avg() * m.nrows)) {
         m.kernel = SPMV_KERNEL_VECTOR;
+        m.vec_wpr = vec_waves_per_row(m.nrows, m.nnz);
         build_vec_codes(m);
     }
     else m.kernel = SPMV_KERNEL_STREAM;
@@ -2298,13 +2301,11 @@ void choose_kernel(GpuCsr &m) {
     }
 #define FAMG_VEC(VB, O16, W) , VB, O16, W
 
-// waves per row of the wave-per-row kernel: few long rows get 2 or 4 waves each
-// (FAMG_VEC_WPR=1/2/4 forces it; read per launch so tests can switch it)
+// waves per row of the wave-per-row kernel: few long rows get 2 or 4 waves each.
+// Chosen once per matrix at finalize from all of its rows, so every row segment
+// (halo interior / boundary launches, rank-local copies) splits its rows the
+// same way; flag FLAG_VEC_WPR (FAMG_VEC_WPR, amg_set_flag) forces 1/2/4.
 static int vec_waves_per_row(int64_t rows, int64_t nnz) {
-    if (const char *e = getenv("FAMG_VEC_WPR")) {
-        const int w = atoi(e);
-        if (w == 1 || w == 2 || w == 4) return w;
-    }
     const int64_t avg = nnz / std::max<int64_t>(1, rows);
     if (rows <= 16384 && avg >= 512) return 4;
     if (rows <= 65536 && avg >= 256) return 2;
@@ -2417,11 +2418,8 @@ static bool dia_runs7() {
     return on;
 }
 
-// A/B switch FAMG_DIA_DK=0: a constant coded diagonal is still read per row
-static bool dia_dk_enabled() {  // read per launch (host only; graphs replay), so tests can switch it
-    const char *e = getenv("FAMG_DIA_DK");
-    return !(e && e[0] == '0');
-}
+// A/B switch FAMG_DIA_DK=0 / amg_set_flag(1, 0): a constant coded diagonal is still read per row
+static bool dia_dk_enabled() { return flag(FLAG_DIA_DK) != 0; }
 
 // The 7-point run pattern of the DIA kernel (NR = -1)
 static bool dia_run7(const GpuCsr &m) {
@@ -2742,7 +2740,7 @@ void spmv(const GpuCsr &m, const double *x, double *y, SpmvMode mode, const Spmv
         if (r1 <= r0) return;
         VecArgs a{m.rp32.get(), m.col.get(), m.vec_off.get(), m.val.get(), m.vec_codes.get(), m.sell_vtab.get(),
                   (int32_t)r0, (int32_t)(r1 - r0), e};
-        const int wpr = vec_waves_per_row(r1 - r0, m.nnz * (r1 - r0) / std::max<int64_t>(1, m.nrows));
+        const int wpr = flag(FLAG_VEC_WPR) ? (int)flag(FLAG_VEC_WPR) : m.vec_wpr;
         const dim3 grid((unsigned)ceil_div(r1 - r0, 4 / wpr));
         const int key = m.vec_vbits * 2 + (m.vec_o16 ? 1 : 0);
 #define FAMG_VECW(W)                                                                                   \

@@ -64,6 +64,9 @@ SIGNATURES = {
     "amg_multigrid_fused_transfer": (i32, [vp, i64, i32, vp, vp, vp, vp, P(i32)]),
     "amg_csr_spmv_epilogue": (i32, [vp, i32, vp, vp, vp, vp]),
     "amg_csr_grid_info": (i32, [vp, vp]),
+    "amg_grid_from_offsets": (i32, [vp, i64, i64, vp, P(i32)]),
+    "amg_set_flag": (i32, [i32, i64]),
+    "amg_get_flag": (i32, [i32, P(i64)]),
     "amg_gen_laplace3d_7pt": (i32, [vp, i64, i64, i64, P(vp)]),
     "amg_gen_aniso27": (i32, [vp, i64, i64, i64, dbl, dbl, dbl, P(vp)]),
     "amg_gen_random_7pt": (i32, [vp, i64, i64, i64, C.c_uint64, i64, P(vp)]),
@@ -442,6 +445,7 @@ class SparseMatOp(LinOp):
         g = np.zeros(12, np.int64)
         _ck(_lib.amg_csr_grid_info(self.h, g.ctypes.data_as(vp)))
         d["grid"] = tuple(int(v) for v in g[:3])
+        d["grid_source"] = ("none", "given", "inferred")[int(g[10])]
         d["xstaged"] = bool(g[3])
         if d["xstaged"]:
             d["tile"], d["halo"] = tuple(int(v) for v in g[4:7]), tuple(int(v) for v in g[7:10])
@@ -472,6 +476,31 @@ class SparseMatOp(LinOp):
         import scipy.sparse as sp
         rp, ci, va = self.arrays()
         return sp.csr_matrix((va, ci, rp), shape=self.dims())
+
+
+FLAGS = {"fold_xscs": 0, "dia_dk": 1, "vec_wpr": 2}
+
+
+def set_flag(name, value):
+    """amg_set_flag: a run-time A/B switch (bitwise neutral); multigrids re-capture
+    their graphs at the next apply."""
+    _ck(_lib.amg_set_flag(FLAGS[name], int(value)))
+
+
+def get_flag(name):
+    v = i64()
+    _ck(_lib.amg_get_flag(FLAGS[name], C.byref(v)))
+    return v.value
+
+
+def grid_from_offsets(offsets, n):
+    """amg_grid_from_offsets (host only): the (nx, ny, nz) grid the library infers
+    for an n-row square operator whose stencil has these col - row offsets, or None."""
+    o = np.ascontiguousarray(np.asarray(offsets, dtype=np.int64))
+    g = np.zeros(3, np.int64)
+    found = C.c_int32(0)
+    _ck(_lib.amg_grid_from_offsets(o.ctypes.data_as(vp), len(o), int(n), g.ctypes.data_as(vp), C.byref(found)))
+    return tuple(int(v) for v in g) if found.value else None
 
 
 def _wrap(h, ctx, cls=LinOp, refs=()):

@@ -111,6 +111,15 @@ amg_status amg_set_alloc_policy(int32_t policy);
  *      par_spmm.rs:31-96, and the SparseRowMat<usize,f64> LinOp used at
  *      multigrid.rs:137-158) -------------------------------------------------- */
 
+/* Run-time switches (no reference counterpart; measured A/B paths, every
+ * setting bitwise neutral): 0 = fold the zero-guess step on x-staged class
+ * levels (default 0, env FAMG_FOLD_XSCS), 1 = read a constant coded Jacobi
+ * diagonal as one scalar (default 1, env FAMG_DIA_DK), 2 = waves per row of the
+ * wave-per-row kernel (0 auto = chosen per matrix at finalize, 1/2/4; env
+ * FAMG_VEC_WPR).  Setting one makes every multigrid re-capture its hipGraph at
+ * its next apply.  amg_get_flag reads the current value. */
+amg_status amg_set_flag(int32_t which, int64_t value);
+amg_status amg_get_flag(int32_t which, int64_t *value);
 /* Stencil-class storage of a CSR operator (structured Galerkin operators whose
  * rows repeat up to a shift; replaces the value/column streams of
  * interpolation/mod.rs:828's A_c in SpMV): info4 = {classes, offsets K (padded
@@ -124,8 +133,17 @@ amg_status amg_csr_class_info(const amg_linop *op, int64_t *info4);
  * bitwise the same sums).  Re-finalizes the SpMV storage: call before the
  * operator is used (graphs captured earlier would read released storage).  The
  * stencil generators and amg_sa_build_box set it for the levels they make;
- * 0,0,0 clears it. */
+ * 0,0,0 clears it (and stops the inference below).  A square operator created
+ * without a hint (amg_csr_create: the drop-in path, multigrid.rs:190-239 /
+ * core.rs:56-74 callers) gets one inferred at finalize from the stencil of 64
+ * sample rows (amg_grid_from_offsets); every consumer of the hint (x-staged
+ * classes, grid-transfer classes in amg_multigrid_add_level, fused SGS phases)
+ * checks every entry against it.  FAMG_INFER_GRID=0 turns the inference off. */
 amg_status amg_csr_set_grid(amg_linop *op, int64_t nx, int64_t ny, int64_t nz);
+/* The grid inference on its own (host only, no device): grid3 = (nx, ny, nz) of
+ * an n-row square operator whose stencil has the k offsets offs (col - row,
+ * any order, repeats allowed); *found = 0 when no grid explains them. */
+amg_status amg_grid_from_offsets(const int64_t *offs, int64_t k, int64_t n, int64_t *grid3, int32_t *found);
 /* The fused SpMV epilogues the V-cycle runs (multigrid.rs:337-369, 407-424),
  * on device vectors, asynchronous on the context stream: mode 0 y = A x, 1
  * y += A x, 2 y = b - A x, 3 y = x + d (b - A x) (weighted Jacobi step; d the
@@ -133,7 +151,7 @@ amg_status amg_csr_set_grid(amg_linop *op, int64_t nx, int64_t ny, int64_t nz);
 amg_status amg_csr_spmv_epilogue(const amg_linop *op, int32_t mode, const double *x, double *y,
                                  const double *b, const double *d);
 /* info12 = {nx, ny, nz (0: no hint), x-staged (0/1), tile tx, ty, tz, halo
- * rx, ry, rz, 0, 0}. */
+ * rx, ry, rz, hint source (0 none, 1 given, 2 inferred), 0}. */
 amg_status amg_csr_grid_info(const amg_linop *op, int64_t *info12);
 
 /* Copy a host CSR with usize-compatible (int64) row pointers and column indices

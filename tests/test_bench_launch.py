@@ -43,3 +43,15 @@ def test_launcher_refuses_without_enough_gpus():
     assert p.returncode == 3, (p.returncode, p.stderr[-2000:])
     assert p.stdout.strip() == ""
     assert "GPU(s) visible" in p.stderr
+
+
+def test_launcher_counts_gpus_without_torch():
+    """The launcher counts GPUs from *_VISIBLE_DEVICES / the KFD topology, never
+    through torch or HIP (verdict r03: the parent must stay GPU-free)."""
+    p = run_bench(["--gpus", "3", "--steps", "1", "--warmup", "0"],
+                  {"HIP_VISIBLE_DEVICES": "0,1", "ROCR_VISIBLE_DEVICES": "0,1"}, timeout=120)
+    assert p.returncode == 3, (p.returncode, p.stderr[-2000:])
+    assert "only 2 GPU(s) visible" in p.stderr
+    import bench
+    src = __import__("inspect").getsource(bench.visible_gpus)
+    assert "torch" not in src.split('"""')[2]

@@ -70,3 +70,46 @@ def test_no_gpu_context_fails_loudly():
     import faer_amg_amd as fa
     with pytest.raises(fa.AmgError):
         fa.Context(0)
+
+
+def _stencil(nx, ny, r, rz=None):
+    import itertools
+    rz = r if rz is None else rz
+    return [dz * nx * ny + dy * nx + dx
+            for dz, dy, dx in itertools.product(range(-rz, rz + 1), range(-r, r + 1), range(-r, r + 1))]
+
+
+@pytest.mark.parametrize("dims,kind", [((256, 256, 256), "7"), ((10, 12, 14), "27"), ((9, 10, 11), "7"),
+                                       ((33, 17, 9), "125"), ((128, 128, 128), "a1"), ((30, 30, 1), "5"),
+                                       ((100, 1, 1), "3"), ((7, 7, 7), "27")])
+def test_grid_inference_from_stencil_offsets(dims, kind):
+    """The drop-in path infers the grid hint a generator would have set
+    (amg_grid_from_offsets, host only)."""
+    import faer_amg_amd as fa
+    nx, ny, nz = dims
+    n = nx * ny * nz
+    pl = nx * ny
+    if kind == "7":
+        offs = [0, 1, -1, nx, -nx, pl, -pl]
+    elif kind == "27":
+        offs = _stencil(nx, ny, 1)
+    elif kind == "125":
+        offs = _stencil(nx, ny, 2)
+    elif kind == "a1":  # A_1 of the 7-point box hierarchy (33 diagonals, radius 2)
+        offs = ([-2 * pl, 2 * pl, -2 * nx, 2 * nx] + [d for d in range(-2, 3)] +
+                [s * pl + dy * nx + dx for s in (-1, 1) for dy in (-1, 0, 1) for dx in (-1, 0, 1)] +
+                [dy * nx + dx for dy in (-1, 1) for dx in (-1, 0, 1)])
+    elif kind == "5":
+        offs = [0, 1, -1, nx, -nx]
+    else:
+        offs = [0, 1, -1]
+    rng = __import__("random").Random(7)
+    rng.shuffle(offs)
+    assert fa.grid_from_offsets(offs + offs[:3], n) == dims
+
+
+def test_grid_inference_rejects_unstructured_offsets():
+    import faer_amg_amd as fa
+    assert fa.grid_from_offsets([0, 5, 17, -5, -17], 900) is None  # no x coupling
+    assert fa.grid_from_offsets([0, 1, -1, 37, -41, 1000], 4096) is None
+    assert fa.grid_from_offsets([], 100) is None

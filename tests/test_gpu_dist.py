@@ -154,10 +154,12 @@ def test_dist_sgs_27pt(nranks, split_kind, steps, resid_form):
     color sweep; the reference's SGS is the stub smoothers.rs:26-27, semantics
     DESIGN.md 5): the global greedy coloring restricted to each rank's rows, the
     ghosts refreshed before every color.  Rows of one color never couple, so the
-    distributed sweep gives the single-GPU sweep's values: the cycle equals the
-    single-GPU cycle bitwise in the direct form (1e-13 in the residual form,
-    whose residual rows are summed by the local storage) and the oracle within
-    1e-11."""
+    distributed sweep gives the single-GPU sweep's values.  Under the auto
+    storage policy the cycle is within 1e-13 of the single-GPU cycle (a
+    rank-local CSR-stream matrix of a coarse level may split its long rows over
+    lanes differently) and within 1e-11 of the oracle; with every level in
+    one-lane-per-row SELL storage the direct form is bitwise the single-GPU
+    cycle."""
     dims = (14, 12, 16)
     b = np.random.default_rng(5 + nranks).uniform(-1, 1, int(np.prod(dims)))
     zg, zref, _ = global_reference(dims, 60, b, problem="27pt", smoother="sgs", steps=steps)
@@ -168,6 +170,15 @@ def test_dist_sgs_27pt(nranks, split_kind, steps, resid_form):
     assert np.linalg.norm(z - zref) <= 1e-11 * np.linalg.norm(zref)
     h0 = res[0][4]
     assert h0[-1] < h0[0]
+    if not resid_form:
+        fa().set_spmv_format("sell")
+        try:
+            zg2, _, _ = global_reference(dims, 60, b, problem="27pt", smoother="sgs", steps=steps)
+            z2, _ = dist_apply(nranks, dims, 60, b, 100, split_kind, problem="27pt", smoother="sgs", steps=steps,
+                               resid_form=resid_form)
+        finally:
+            fa().set_spmv_format("auto")
+        assert np.array_equal(z2.view(np.int64), zg2.view(np.int64))
 
 
 def test_rccl_single_rank():

@@ -109,7 +109,7 @@ def test_spmv_formats(ctx, fmt):
     wave-per-row kernel with 1, 2 or 4 waves per row (bounded; odd row counts
     leave a workgroup's last row slots empty)."""
     if fmt.startswith("vector-w"):
-        os.environ["FAMG_VEC_WPR"] = fmt[-1]
+        fa().set_flag("vec_wpr", int(fmt[-1]))
         fmt = "vector"
     fa().set_spmv_format(fmt)
     try:
@@ -138,7 +138,7 @@ def test_spmv_formats(ctx, fmt):
         assert np.all(np.abs(y - g5["y"]) <= spmv_bound(S, g5["x"]))
     finally:
         fa().set_spmv_format("auto")
-        os.environ.pop("FAMG_VEC_WPR", None)
+        fa().set_flag("vec_wpr", 0)
 
 
 def _random_rows(rng, m, n, per_row, spread):
@@ -1188,11 +1188,11 @@ def test_xstaged_classes_fold_zero_guess(ctx):
     shows RESID0/ADD0 and no d*f pass on those levels, the V-cycle is bitwise
     the unfolded one (the staged products are vec_mul's) and within 1e-11 of
     the oracle.  (Off by default -- measured slower on the C2 cycle -- so the
-    test switches it on; the library reads FAMG_FOLD_XSCS whenever it lays
-    out a cycle.)"""
+    test switches it on with amg_set_flag, read whenever the library lays out
+    a cycle.)"""
     dims = (128, 128, 128)
     A = fa().SparseMatOp.laplace3d_7pt(ctx, *dims)
-    os.environ["FAMG_FOLD_XSCS"] = "1"  # off by default (measured slower)
+    fa().set_flag("fold_xscs", 1)  # off by default (measured slower)
     mg = fa().sa_build_box(A, dims, (2, 2, 2), coarsest_dim=100)
     xs = [l for l in range(1, mg.levels() - 1) if mg.level(l)[0].spmv_info()["xstaged"]]
     assert xs, "no x-staged level"
@@ -1206,7 +1206,7 @@ def test_xstaged_classes_fold_zero_guess(ctx):
         mg.set_fold_zero_guess(fold)
         outs[fold] = apply_dev(ctx, mg, b, A.nrows)
     mg.set_fold_zero_guess(True)
-    os.environ.pop("FAMG_FOLD_XSCS", None)
+    fa().set_flag("fold_xscs", 0)
     assert np.array_equal(outs[True].view(np.int64), outs[False].view(np.int64))
     zref = O.Multigrid(oracle_levels_from_gpu(mg, "jacobi")).apply(b)
     assert np.linalg.norm(outs[True] - zref) <= 1e-11 * np.linalg.norm(zref)
@@ -1332,7 +1332,7 @@ def test_constant_diagonal_epilogues_bitwise(ctx):
     b = T(np.random.default_rng(3).uniform(-1, 1, int(np.prod(dims))))
     outs, plans = {}, {}
     for dk in ("1", "0"):
-        os.environ["FAMG_DIA_DK"] = dk
+        fa().set_flag("dia_dk", int(dk))
         try:
             A = fa().SparseMatOp.laplace3d_7pt(ctx, *dims)
             mg = fa().sa_build_box(A, dims, (2, 2, 2), coarsest_dim=100)
@@ -1343,7 +1343,7 @@ def test_constant_diagonal_epilogues_bitwise(ctx):
             outs[dk] = H(z)
             plans[dk] = [p for p in mg.cycle_plan() if p["level"] == 0]
         finally:
-            os.environ.pop("FAMG_DIA_DK", None)
+            fa().set_flag("dia_dk", 1)
     assert np.array_equal(outs["1"].view(np.int64), outs["0"].view(np.int64))
     n = int(np.prod(dims))
     by = {p["mode"]: p["bytes"] for p in plans["1"]}
