@@ -561,17 +561,49 @@ def run_dist(args, world, rank, local_rank):
     dist.broadcast_object_list(obj, src=0)
     comm = fa.Comm(ctx, nranks=world, rank=rank, uid=obj[0])
     dm = fa.DistMultigrid(comm, mg, splits, agglomerate_rows=args.agglomerate).set_overlap(not args.no_overlap)
-    if args.dist_graph:
-        dm.set_graph(True)
     infos = [dm.level_info(l) for l in range(nl)]
+    La = sum(1 for i in infos if i["redundant"] == 0)
+
+    def kind(M):
+        i = M.spmv_info()
+        k = "xscs" if i["kernel"] == "classes" and i["xstaged"] else i["kernel"]
+        return k + ("+gtc" if i["gtc"] != "none" else "")
+    storages = [{w: kind(dm.level_matrix(l, w)) for w in ("A", "R", "P")} for l in range(La)]
     n_glob = A.nrows
     del mg, A  # global fine levels are no longer needed on this rank
     torch.cuda.synchronize()
     setup_s = time.perf_counter() - t0
-    log(f"rank {rank}: setup {setup_s:.1f}s, RCCL {fa.rccl_library()}")
+    log(f"rank {rank}: setup {setup_s:.1f}s, RCCL {fa.rccl_library()}, local storages {storages}")
     r0, r1 = dm.local_rows()
     b = torch.as_tensor(splitmix_uniform(n_glob, 42)[r0:r1].copy(), device=f"cuda:{local_rank}")
     z = torch.empty_like(b)
+    plan = plan_summary(dm.cycle_plan())  # collective: one eager cycle with the launch recorder on
+    # hipGraph replay of the whole distributed cycle (RCCL p2p + all-gather
+    # captured), checked bitwise against the eager cycle on every rank before it
+    # is used; any difference or error falls back to the eager cycle
+    graph = "off (--no-dist-graph)"
+    if not args.no_dist_graph:
+        ok, why = 1.0, ""
+        try:
+            ze, zg = torch.empty_like(b), torch.empty_like(b)
+            dm.set_graph(False)
+            dm.apply(ze, b)
+            dm.set_graph(True)
+            dm.apply(zg, b)  # capture + first replay
+            dm.apply(zg, b)  # replay
+            torch.cuda.synchronize()
+            if not torch.equal(ze, zg):
+                ok, why = 0.0, "replay differs from the eager cycle"
+        except Exception as e:  # noqa: BLE001 -- reported in the line
+            ok, why = 0.0, f"capture failed: {e!r}"
+        t = torch.tensor([ok], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MIN)
+        if float(t[0]) == 1.0:
+            graph = "on (replay bitwise equal to the eager cycle on every rank)"
+        else:
+            dm.set_graph(False)
+            graph = "eager fallback: " + (why or "another rank's replay check failed")
+        log(f"rank {rank}: dist graph {graph}")
     for _ in range(args.warmup):
         dm.apply(z, b)
     torch.cuda.synchronize()
@@ -636,7 +668,7 @@ def run_dist(args, world, rank, local_rank):
         "warmup": args.warmup,
         "ms_per_step": round(ms_per_cycle, 4),
         "higher_is_better": True,
-        "scaling": "strong" if strong else "weak",
+        "scaling": "strong" if strong else ("weak" if world > 1 else "none"),
         "vs_baseline": None,
         "dtype": "f64",
         "data": "synthetic (device-generated operator, splitmix64 rhs seed 42)",
@@ -651,7 +683,12 @@ def run_dist(args, world, rank, local_rank):
                    "rel_residual_after_1_cycle": float(hist[1]) if len(hist) > 1 else None,
                    "agglomerate_rows": args.agglomerate,
                    "halo_overlap": not args.no_overlap,
-                   "dist_graph": bool(args.dist_graph),
+                   "dist_graph": graph,
+                   "local_storages_rank0": storages,
+                   "vcycle_plan_rank0": {"launches": plan["launches"],
+                                         "source": "amg_dist_cycle_plan (the launches this rank makes)",
+                                         "per_level_GB": [round(d["bytes"] / 1e9, 4) for d in plan["per_level"]],
+                                         "per_level_kernels": [d["kernels"] for d in plan["per_level"]]},
                    "rccl": fa.rccl_library(),
                    "rccl_ranks": comm.nranks,
                    "parallelism": f"row-block {'z-slabs' if args.problem in ('7pt', '27pt') else 'row ranges'} "
@@ -840,8 +877,10 @@ def main():
     ap.add_argument("--cpu-budget", type=float, default=20.0,
                     help="seconds of CPU V-cycles at --cpu-threads (half that at all cores)")
     ap.add_argument("--no-graph", action="store_true")
-    ap.add_argument("--dist-graph", action="store_true",
-                    help="replay the distributed cycle as a captured hipGraph (RCCL p2p + all-gather captured)")
+    ap.add_argument("--no-dist-graph", action="store_true",
+                    help="distributed: run the cycle eagerly instead of replaying it as a captured hipGraph "
+                         "(RCCL p2p + all-gather captured; by default used after a bitwise check against the "
+                         "eager cycle on every rank)")
     ap.add_argument("--no-overlap", action="store_true",
                     help="distributed: exchange halos before the SpMV instead of under its interior rows")
     ap.add_argument("--ab", action="store_true", help="A/B the SpMV storage formats (stderr)")

@@ -78,6 +78,26 @@ void for_columns(LinOp &op, double *out, int64_t ld_out, const double *rhs, int6
 }  // namespace
 
 namespace famg {
+void export_plan(const std::vector<LaunchRec> &plan, amg_launch_rec *recs, int64_t cap, int64_t *count) {
+    *count = (int64_t)plan.size();
+    if (!recs) return;
+    for (int64_t i = 0; i < std::min<int64_t>(cap, (int64_t)plan.size()); i++) {
+        const LaunchRec &r = plan[i];
+        amg_launch_rec &o = recs[i];
+        o.level = r.level;
+        o.role = r.role;
+        o.kernel = r.kernel;
+        o.mode = r.mode;
+        o.rows = r.rows;
+        o.bytes = r.bytes;
+        o.csr_bytes = r.csr_bytes;
+        std::memset(o.name, 0, sizeof(o.name));
+        std::strncpy(o.name, r.name, sizeof(o.name) - 1);
+    }
+}
+}  // namespace famg
+
+namespace famg {
 static std::atomic<int64_t> g_flag_val[FLAG_COUNT] = {
     {[] { const char *e = getenv("FAMG_FOLD_XSCS"); return (int64_t)(e && e[0] == '1'); }()},
     {[] { const char *e = getenv("FAMG_DIA_DK"); return (int64_t)!(e && e[0] == '0'); }()},
@@ -363,6 +383,7 @@ amg_status amg_csr_grid_info(const amg_linop *op, int64_t *info12) {
         for (int q = 0; q < 12; q++) info12[q] = 0;
         for (int q = 0; q < 3; q++) info12[q] = m.grid[q];
         info12[10] = m.grid_src;
+        info12[11] = m.gtc_on ? (m.gtc_r ? 2 : 1) : 0;
         const bool on = m.has_scs() && m.xscs;
         info12[3] = on ? 1 : 0;
         for (int q = 0; q < 3; q++) {
@@ -747,22 +768,7 @@ amg_status amg_multigrid_cycle_plan(amg_linop *mg, amg_launch_rec *recs, int64_t
         auto m = need_mg(mg);
         FAMG_REQUIRE(count && cap >= 0, AMG_ERR_INVALID, "bad argument");
         m->ctx->set_device();
-        const std::vector<LaunchRec> plan = m->cycle_plan();
-        *count = (int64_t)plan.size();
-        if (!recs) return;
-        for (int64_t i = 0; i < std::min<int64_t>(cap, (int64_t)plan.size()); i++) {
-            const LaunchRec &r = plan[i];
-            amg_launch_rec &o = recs[i];
-            o.level = r.level;
-            o.role = r.role;
-            o.kernel = r.kernel;
-            o.mode = r.mode;
-            o.rows = r.rows;
-            o.bytes = r.bytes;
-            o.csr_bytes = r.csr_bytes;
-            std::memset(o.name, 0, sizeof(o.name));
-            std::strncpy(o.name, r.name, sizeof(o.name) - 1);
-        }
+        export_plan(m->cycle_plan(), recs, cap, count);
     });
 }
 

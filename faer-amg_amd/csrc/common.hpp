@@ -142,6 +142,7 @@ struct LaunchRec {
 struct LaunchLog {
     std::vector<LaunchRec> recs;
     int32_t level = 0, role = AMG_ROLE_OTHER;
+    int32_t level_base = 0;  // added to log_at's level (a distributed cycle's redundant tail)
 };
 extern thread_local LaunchLog *g_launch_log;
 inline void log_launch(const char *name, int32_t kernel, int32_t mode, int64_t rows, int64_t bytes,
@@ -152,7 +153,7 @@ inline void log_launch(const char *name, int32_t kernel, int32_t mode, int64_t r
 }
 inline void log_at(int64_t level, int32_t role) {
     if (g_launch_log) {
-        g_launch_log->level = (int32_t)level;
+        g_launch_log->level = g_launch_log->level_base + (int32_t)level;
         g_launch_log->role = role;
     }
 }

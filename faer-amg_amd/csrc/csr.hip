@@ -313,6 +313,14 @@ void csr_finalize(GpuCsr &m, const std::vector<int64_t> *segments) {
         }
     }
     const bool scs_all = scs && m.scs_seg < 0;  // else a row segment beside SELL-64
+    if (scs_all && m.has_dia() && !dia_all) {  // the classes take every row: no segment DIA beside them
+        m.dia_codes.release();
+        m.dia_vtab.release();
+        m.dia_ntab = 0;
+        m.dia_k = m.dia_cw = m.dia_vbits = m.dia_pat = 0;
+        m.dia_r0 = m.dia_r1 = m.dia_seg = 0;
+        m.dia_off.clear();
+    }
     if (!dia_all && !m.has_bsr() && (scs_all || (!scs && build_sellp(m, rp, other_b)))) {
         m.sell_row0.release(); m.sell_soff.release(); m.sell_desc.release(); m.sell_base.release();
         m.sell_data.release(); m.sell_vtab.release();

@@ -305,6 +305,19 @@ __global__ void k_remap_cols(int32_t *col, int64_t nnz, int64_t c0, int64_t c1, 
     }
 }
 
+// the lowest marked column below r0 and the highest at or above r1
+__global__ void k_ghost_extent(const int64_t *mark, int64_t n, int64_t r0, int64_t r1, unsigned long long *ext) {
+    const int64_t c = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (c >= n || !mark[c]) return;
+    if (c < r0) atomicMin(&ext[0], (unsigned long long)c);
+    else if (c >= r1) atomicMax(&ext[1], (unsigned long long)c);
+}
+
+__global__ void k_mark_range(int64_t *mark, int64_t c0, int64_t c1) {
+    const int64_t c = c0 + (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (c < c1) mark[c] = 1;
+}
+
 __global__ void k_gather_idx(const double *x, const int32_t *idx, int64_t n, double *out) {
     const int64_t k = (int64_t)blockIdx.x * 256 + threadIdx.x;
     if (k < n) out[k] = x[idx[k]];
@@ -320,6 +333,10 @@ struct Space {
     bool redundant = false;
     HaloPlan plan;
     int64_t n_glob = 0, r0 = 0, r1 = 0, n_own = 0, n_ghost = 0;
+    // a grid level split into whole planes: the ghost set is made of whole
+    // planes (below, then above the owned ones), so the local vector has the
+    // SlabFrame layout and the grid kernels run on the rank-local matrices
+    SlabFrame frame;
     DevBuf<int64_t> mark, scan;           // setup only (global length)
     // halo plan (copied from `plan`)
     std::vector<int> nbr;
@@ -357,6 +374,33 @@ static void space_mark(Space &sp, const GpuCsr &local, Ctx *ctx) {
 // After all matrices of the space are marked: the ghost list (device compaction
 // of the marks, the same set plan_add_columns computes on the host), then the
 // host plan (plan.hpp) with its two request exchanges over the transport.
+// Slab levels: extend the marked ghost columns to whole planes (the planes the
+// level's stencils reach below and above the owned ones), so the ghost region
+// is the frame's ghost planes.  Costs extra halo entries only where a plane was
+// referenced partly.
+static void space_mark_planes(Space &sp, Ctx *ctx) {
+    if (!sp.frame.on()) return;
+    hipStream_t s = ctx->stream;
+    const int64_t pl = sp.frame.pl();
+    DevBuf<unsigned long long> ext(2);
+    const unsigned long long init[2] = {~0ull, 0ull};
+    FAMG_CHECK_HIP(hipMemcpyAsync(ext.get(), init, sizeof(init), hipMemcpyHostToDevice, s));
+    hipLaunchKernelGGL(k_ghost_extent, dim3(g1(sp.n_glob)), dim3(256), 0, s, sp.mark.get(), sp.n_glob, sp.r0, sp.r1,
+                       ext.get());
+    unsigned long long h[2];
+    FAMG_CHECK_HIP(hipMemcpyAsync(h, ext.get(), sizeof(h), hipMemcpyDeviceToHost, s));
+    FAMG_CHECK_HIP(hipStreamSynchronize(s));
+    if (h[0] != ~0ull) {
+        const int64_t c0 = (int64_t)h[0] / pl * pl;
+        hipLaunchKernelGGL(k_mark_range, dim3(g1(sp.r0 - c0)), dim3(256), 0, s, sp.mark.get(), c0, sp.r0);
+    }
+    if (h[1] >= (unsigned long long)sp.r1) {
+        const int64_t c1 = std::min<int64_t>(sp.n_glob, ((int64_t)h[1] / pl + 1) * pl);
+        hipLaunchKernelGGL(k_mark_range, dim3(g1(c1 - sp.r1)), dim3(256), 0, s, sp.mark.get(), sp.r1, c1);
+    }
+    FAMG_CHECK_HIP(hipGetLastError());
+}
+
 static void space_plan(Space &sp, Transport &tr, Ctx *ctx) {
     hipStream_t s = ctx->stream;
     sp.scan.resize(sp.n_glob + 1);
@@ -367,6 +411,17 @@ static void space_plan(Space &sp, Transport &tr, Ctx *ctx) {
     std::vector<int64_t> ghost_ids(ng);
     if (ng) FAMG_CHECK_HIP(hipMemcpyAsync(ghost_ids.data(), ids.get(), ng * sizeof(int64_t), hipMemcpyDeviceToHost, s));
     FAMG_CHECK_HIP(hipStreamSynchronize(s));
+    if (sp.frame.on()) {  // ghost planes below / above (whole planes: space_mark_planes)
+        const int64_t P = sp.frame.pl();
+        int64_t below = 0;
+        while (below < ng && ghost_ids[below] < sp.r0) below++;
+        sp.frame.gl = below / P;
+        sp.frame.gh = (ng - below) / P;
+        const bool whole = below % P == 0 && (ng - below) % P == 0 &&
+                           (below == 0 || ghost_ids[0] == sp.r0 - below) &&
+                           (ng == below || ghost_ids[ng - 1] == sp.r1 + (ng - below) - 1);
+        if (!whole) sp.frame = SlabFrame{};
+    }
     HaloPlan &pl = sp.plan;
     plan_set_ghosts(pl, std::move(ghost_ids));
     sp.n_ghost = pl.n_ghost();
@@ -581,6 +636,7 @@ struct DistMultigridOp : LinOp {
     void smooth(int64_t l, double *&v, double *&t, const double *f, bool zero, double *last_out = nullptr) {
         DLevel &D = L[l];
         hipStream_t s = ctx->stream;
+        log_at(l, AMG_ROLE_SMOOTH);
         if (D.G) {  // in place on v; the residual form as MultigridOp::smooth
             for (int64_t it = 0; it < steps; it++) {
                 if (zero && it == 0) {
@@ -635,22 +691,56 @@ struct DistMultigridOp : LinOp {
         hipStream_t s = ctx->stream;
         double *v0 = v;
         double *t = (v == D.t.get()) ? D.v.get() : D.t.get();
-        smooth(l, v, t, f, zero);
+        // the single-GPU cycle's zero-guess fold (fold_level) where the level's
+        // residual needs no halo (a rank that owns the whole level): RESID0 reads
+        // f and d at every column, which a ghost region of f would have to carry
+        const bool fold = zero && !D.G && D.sp.nbr.empty() && D.sp.n_ghost == 0 &&
+                          fold_level(D.A.get(), D.S.get(), D.P.get(), tail->fold_zero_guess, true, steps);
         SpmvEpi epi;
         epi.b = f;
-        halo_spmv(D.sp, v, D.A->m, D.r.get(), SPMV_RESID, epi);
+        SpmvEpi epi0 = epi;  // the folded epilogues' d*f
+        if (D.S) {
+            epi0.d = D.S->d.get();
+            epi0.dc = D.S->dcode.get();
+            epi0.dt = D.S->dtab.get();
+            epi0.dk = D.S->dconst;
+        }
+        if (fold) {
+            log_at(l, AMG_ROLE_RESID);
+            spmv(D.A->m, f, D.r.get(), SPMV_RESID0, epi0, s);  // f - A (d f)
+        } else {
+            smooth(l, v, t, f, zero);
+            log_at(l, AMG_ROLE_RESID);
+            halo_spmv(D.sp, v, D.A->m, D.r.get(), SPMV_RESID, epi);
+        }
         if (l + 1 < La) {
             DLevel &C = L[l + 1];
+            log_at(l, AMG_ROLE_RESTRICT);
             halo_spmv(D.sp, D.r.get(), D.R->m, C.f.get(), SPMV_SET, SpmvEpi{});
             for (int64_t k = 0; k < mu; k++) cycle(l + 1, C.v.get(), C.f.get(), k == 0);
-            halo_spmv(C.sp, C.v.get(), D.P->m, v, SPMV_ADD, SpmvEpi{});
+            log_at(l, AMG_ROLE_INTERP);
+            if (fold) {
+                halo_spmv(C.sp, C.v.get(), D.P->m, t, SPMV_ADD0, epi0);  // v = d f + P v_c
+                std::swap(v, t);
+            } else {
+                halo_spmv(C.sp, C.v.get(), D.P->m, v, SPMV_ADD, SpmvEpi{});
+            }
         } else {
             const int64_t cnt = tail_splits[tr->rank + 1] - tail_splits[tr->rank];
+            log_at(l, AMG_ROLE_RESTRICT);
             if (cnt) halo_spmv(D.sp, D.r.get(), D.R->m, gather.get() + tr->rank * tail_max, SPMV_SET, SpmvEpi{});
             else halo(D.sp, D.r.get(), *tr, s);
             gather_tail(gather.get() + tr->rank * tail_max);
+            if (g_launch_log) g_launch_log->level_base = (int32_t)La;
             for (int64_t k = 0; k < mu; k++) tail->cycle(0, vc_full.get(), fc_full.get(), k == 0, nullptr);
-            spmv(D.P->m, vc_full.get(), v, SPMV_ADD, SpmvEpi{}, s);
+            if (g_launch_log) g_launch_log->level_base = 0;
+            log_at(l, AMG_ROLE_INTERP);
+            if (fold) {
+                spmv(D.P->m, vc_full.get(), t, SPMV_ADD0, epi0, s);
+                std::swap(v, t);
+            } else {
+                spmv(D.P->m, vc_full.get(), v, SPMV_ADD, SpmvEpi{}, s);
+            }
         }
         const bool direct = out && steps >= 1 && D.S && !D.G;
         smooth(l, v, t, f, false, direct ? out : nullptr);
@@ -738,6 +828,25 @@ struct DistMultigridOp : LinOp {
         FAMG_CHECK_HIP(hipGraphLaunch(exec, s));
     }
 
+    // launch records of one eager cycle on scratch vectors (amg_dist_cycle_plan)
+    std::vector<LaunchRec> cycle_plan() {
+        std::lock_guard<std::mutex> lk(mtx);
+        tail->ensure_workspace();
+        DevBuf<double> b(std::max<int64_t>(1, nrows)), z(std::max<int64_t>(1, nrows));
+        vec_fill(b.get(), 1.0, nrows, ctx->stream);
+        LaunchLog log;
+        g_launch_log = &log;
+        try {
+            apply_eager(z.get(), b.get());
+        } catch (...) {
+            g_launch_log = nullptr;
+            throw;
+        }
+        g_launch_log = nullptr;
+        FAMG_CHECK_HIP(hipStreamSynchronize(ctx->stream));
+        return log.recs;
+    }
+
     // one cycle issued on the stream (workspaces allocated beforehand)
     void apply_eager(double *out, const double *rhs) {
         hipStream_t s = ctx->stream;
@@ -775,6 +884,40 @@ struct DistLevelOp : LinOp {
         mg->halo_spmv(D.sp, x.get(), D.A->m, out, SPMV_SET, SpmvEpi{});
     }
 };
+
+// The owned planes [r0, r1) of a grid operator as a frame (no ghosts yet), or
+// off when the operator has no grid hint or the split cuts a plane.
+static SlabFrame owned_frame(const GpuCsr &A, int64_t r0, int64_t r1) {
+    SlabFrame f;
+    const int64_t *g = A.grid;
+    if (g[0] <= 0 || g[1] <= 0 || g[2] <= 0 || g[0] * g[1] * g[2] != A.nrows || r1 <= r0) return f;
+    const int64_t pl = g[0] * g[1];
+    if (r0 % pl || r1 % pl) return f;
+    f.nx = g[0]; f.ny = g[1]; f.gz = g[2];
+    f.z0 = r0 / pl;
+    f.nz = (r1 - r0) / pl;
+    return f;
+}
+
+// A rank-local matrix with slab frames: its rows are rf's owned planes, its
+// columns cf's vector (both must be on for the grid kernels to take it)
+static void set_frames(GpuCsr &m, const SlabFrame &rf, const SlabFrame &cf, bool square) {
+    auto whole = [](const SlabFrame &f) { return f.on() && f.z0 == 0 && f.nz == f.gz && f.gl == 0 && f.gh == 0; };
+    if (whole(rf) && whole(cf)) {  // a rank that owns the whole level: the global matrix, unframed
+        m.rframe = m.cframe = SlabFrame{};
+        if (square) {
+            m.grid[0] = rf.nx; m.grid[1] = rf.ny; m.grid[2] = rf.gz;
+            m.grid_src = 1;
+        }
+        return;
+    }
+    m.rframe = rf;
+    m.cframe = cf;
+    if (square && rf.on() && cf.on()) {  // the owned grid: the x-staged classes' row grid
+        m.grid[0] = rf.nx; m.grid[1] = rf.ny; m.grid[2] = rf.nz;
+        m.grid_src = 1;
+    }
+}
 
 static std::shared_ptr<DistMultigridOp> build_dist(amg_comm *comm, const MultigridOp &g,
                                                    const int64_t *splits, int64_t agglo) {
@@ -818,6 +961,13 @@ static std::shared_ptr<DistMultigridOp> build_dist(amg_comm *comm, const Multigr
         D.sp.r0 = D.sp.plan.r0;
         D.sp.r1 = D.sp.plan.r1;
         D.sp.n_own = D.sp.plan.n_own;
+        D.sp.frame = owned_frame(A->m, D.sp.r0, D.sp.r1);
+    }
+    int64_t tail_r0 = 0, tail_r1 = 0;  // this rank's rows of the first redundant level
+    if (d->La < d->nlevels) {
+        const std::vector<int64_t> ts = sp_of(d->La);
+        tail_r0 = ts[me];
+        tail_r1 = ts[me + 1];
     }
     // local matrices with global columns
     for (int64_t l = 0; l < d->La; l++) {
@@ -858,7 +1008,16 @@ static std::shared_ptr<DistMultigridOp> build_dist(amg_comm *comm, const Multigr
         space_mark(sp, d->L[l].A->m, ctx);
         space_mark(sp, d->L[l].R->m, ctx);
         if (l > 0) space_mark(sp, d->L[l - 1].P->m, ctx);
+        space_mark_planes(sp, ctx);
         space_plan(sp, tr, ctx);
+        {  // slab frames of the local A_l, R_l (rows: level l+1) and P_{l-1} (columns: space l)
+            const SlabFrame rows_next =
+                owned_frame(dynamic_cast<CsrOp *>(g.levels[l + 1].A.get())->m, l + 1 < d->La ? d->L[l + 1].sp.r0 : tail_r0,
+                            l + 1 < d->La ? d->L[l + 1].sp.r1 : tail_r1);
+            set_frames(d->L[l].A->m, sp.frame, sp.frame, true);
+            set_frames(d->L[l].R->m, rows_next, sp.frame, false);
+            if (l > 0) set_frames(d->L[l - 1].P->m, d->L[l - 1].sp.frame, sp.frame, false);
+        }
         space_remap(sp, d->L[l].A->m, ctx);
         space_remap(sp, d->L[l].R->m, ctx);
         if (l > 0) space_remap(sp, d->L[l - 1].P->m, ctx);
@@ -891,7 +1050,21 @@ static std::shared_ptr<DistMultigridOp> build_dist(amg_comm *comm, const Multigr
     // the last distributed level's P references the replicated level La by global id
     if (d->La > 0) {
         DLevel &D = d->L[d->La - 1];
+        const GpuCsr &Ag = dynamic_cast<CsrOp *>(g.levels[d->La].A.get())->m;
+        set_frames(D.P->m, D.sp.frame, owned_frame(Ag, 0, Ag.nrows), false);
         csr_finalize(D.P->m);
+    }
+    // R_l / P_l of a 2x2x2-box level as grid-transfer classes through the slab
+    // frames (the classes of their global rows; every entry checked)
+    for (int64_t l = 0; l < d->La; l++) {
+        const GpuCsr &Af = dynamic_cast<CsrOp *>(g.levels[l].A.get())->m;
+        const GpuCsr &Ac = dynamic_cast<CsrOp *>(g.levels[l + 1].A.get())->m;
+        bool box = true;
+        for (int q = 0; q < 3; q++) box = box && Af.grid[q] > 0 && Ac.grid[q] == (Af.grid[q] + 1) / 2;
+        if (!box) continue;
+        GpuCsr &R = d->L[l].R->m, &Pm = d->L[l].P->m;
+        if (R.nrows > 0) gtc_attach(R, Af.grid, Ac.grid, 1);  // gtc_classes checks the frames / grids first
+        if (Pm.nrows > 0) gtc_attach(Pm, Af.grid, Ac.grid, 0);
     }
     for (int64_t l = 0; l < d->La; l++) {
         d->L[l].P->nrows = d->L[l].P->m.nrows;
@@ -1136,6 +1309,15 @@ amg_status amg_dist_level_matrix(const amg_linop *dist, int64_t level, int32_t w
                      "level must be distributed, which in {0,1,2}");
         const DLevel &D = d->L[level];
         *out = new amg_linop{which == 0 ? D.A : which == 1 ? D.R : D.P};
+    });
+}
+
+amg_status amg_dist_cycle_plan(amg_linop *dist, amg_launch_rec *recs, int64_t cap, int64_t *count) {
+    return dguard([&] {
+        auto d = need_dist(dist);
+        FAMG_REQUIRE(count && cap >= 0, AMG_ERR_INVALID, "bad argument");
+        d->ctx->set_device();
+        export_plan(d->cycle_plan(), recs, cap, count);
     });
 }
 

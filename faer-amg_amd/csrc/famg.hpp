@@ -31,6 +31,35 @@ __device__ __forceinline__ int xcd_remap(int b, int nb) {
 
 // ------------------------------------------------------------------ CSR data
 
+// Plane layout of a rank-local vector of a distributed grid level (dist.hip,
+// DESIGN.md 6): the rank owns planes [z0, z0 + nz) of an nx x ny x gz grid
+// (local entries [0, nz * pl)), then its ghost planes -- gl whole planes below z0,
+// then gh above z0 + nz.  Local plane z in [-gl, nz + gh) starts at entry
+// z * pl + (z < 0 ? nz * pl + gl * pl : z >= nz ? gl * pl : 0).
+// Off (nx == 0) for single-GPU matrices; a redundant (all-gathered) level is
+// the frame with z0 = 0, nz = gz and no ghosts.
+struct SlabFrame {
+    int64_t nx = 0, ny = 0, gz = 0;  // the global grid
+    int64_t z0 = 0, nz = 0;          // owned planes
+    int64_t gl = 0, gh = 0;          // ghost planes below / above
+    bool on() const { return nx > 0; }
+    int64_t pl() const { return nx * ny; }
+    int64_t n_own() const { return nz * nx * ny; }
+    int64_t add_lo() const { return (nz + gl) * nx * ny; }  // added to z * pl for z < 0
+    int64_t add_hi() const { return gl * nx * ny; }         // ... for z >= nz
+    // global grid plane of a local entry (ghosts included)
+    int64_t plane_of(int64_t c) const {
+        const int64_t p = pl(), own = n_own();
+        if (c < own) return z0 + c / p;
+        const int64_t g = c - own;
+        return g < gl * p ? z0 - gl + g / p : z0 + nz + (g - gl * p) / p;
+    }
+    int64_t in_plane(int64_t c) const {
+        const int64_t p = pl(), own = n_own();
+        return c < own ? c % p : (c - own) % p;
+    }
+};
+
 // A CSR matrix resident on the device.  rp64 (int64 row pointers) always
 // exists and is what setup kernels (SpGEMM, transpose, extraction) read;
 // rp32 + the stream schedule exist when nnz < 2^31 and are what SpMV reads
@@ -133,6 +162,12 @@ struct GpuCsr {
     // (grid_src 1), else inferred at finalize from the stencil offsets (grid_src 2)
     int64_t grid[3] = {0, 0, 0};
     int grid_src = 0;
+    // rank-local matrix of a distributed grid level (dist.hip): its rows are the
+    // owned planes of rframe, its columns the local vector of cframe.  The
+    // x-staged classes and grid-transfer classes then stage ghost planes through
+    // the frame, and their launches split into interior / boundary z-tile ranges
+    // (segments 1 / 0, 2) so the interior runs while the halo is in flight.
+    SlabFrame rframe, cframe;
     // x-staged SELL (xsell.hip): per group of 4096 rows the x chunks staged in LDS,
     // per slice fp64 values + 16-bit LDS indices (or 32-bit columns: escape slices)
     DevBuf<char> xs_data;
@@ -192,7 +227,8 @@ enum SpmvKernel : int {
 // lists; gtc_attach builds the overlay storage (true if it applies)
 bool gtc_classes(const GpuCsr &M, bool is_r, const int64_t *fg, const int64_t *cg, std::vector<uint8_t> &cls,
                  std::vector<std::vector<std::pair<uint8_t, double>>> &dict);
-bool gtc_attach(GpuCsr &m, const int64_t *fg, const int64_t *cg);
+// which: 1 = R (coarse rows), 0 = P (fine rows), -1 = R if it has fewer rows than columns
+bool gtc_attach(GpuCsr &m, const int64_t *fg, const int64_t *cg, int which = -1);
 void gtc_release(GpuCsr &m);
 // stencil-class storage for structured operators whose rows repeat up to a
 // shift; true if built (scs.hip)
@@ -259,7 +295,10 @@ void spmv_scs(const GpuCsr &m, const double *x, double *y, SpmvMode mode, const 
               int64_t seg);
 bool xs_supports(SpmvMode mode);
 bool gtc_supports(const GpuCsr &m, SpmvMode mode);
-void spmv_gtc(const GpuCsr &m, const double *x, double *y, SpmvMode mode, const SpmvEpi &epi, hipStream_t s);
+// seg < 0: every tile; a rank-local matrix (rframe on) also takes segments 1
+// (interior z-tiles: no ghost reads) and 0 / 2 (the tiles before / after)
+void spmv_gtc(const GpuCsr &m, const double *x, double *y, SpmvMode mode, const SpmvEpi &epi, hipStream_t s,
+              int64_t seg = -1);
 void spmv_xs(const GpuCsr &m, const double *x, double *y, SpmvMode mode, const SpmvEpi &epi, hipStream_t s);
 void spmv_sellp(const GpuCsr &m, const double *x, double *y, SpmvMode mode, const SpmvEpi &epi, hipStream_t s,
                 int64_t seg);
@@ -451,6 +490,9 @@ struct MultigridOp : LinOp {
     bool workspace_ready_ = false;
     bool fuse_ready_ = false;
 };
+
+// the zero-guess fold decision of one level (RESID0 + ADD0 instead of v = d*f)
+bool fold_level(const CsrOp *A, const DiagOp *D, const CsrOp *P, bool fold_zero_guess, bool v_zero, int64_t steps);
 
 // fused grid transfers (fuse.hip)
 void fuse_setup(MultigridOp &mg, size_t l);

@@ -33,8 +33,19 @@ bool gtc_classes(const GpuCsr &M, bool is_r, const int64_t *fg, const int64_t *c
     if (n <= 0 || nnz <= 0) return false;
     const int64_t rx = is_r ? cg[0] : fg[0], ry = is_r ? cg[1] : fg[1], rz = is_r ? cg[2] : fg[2];  // row grid
     const int64_t kx = is_r ? fg[0] : cg[0], ky = is_r ? fg[1] : cg[1], kz = is_r ? fg[2] : cg[2];  // column grid
-    if (rx * ry * rz != n || kx * ky * kz != M.ncols) return false;
     if (cg[0] != (fg[0] + 1) / 2 || cg[1] != (fg[1] + 1) / 2 || cg[2] != (fg[2] + 1) / 2) return false;
+    // rows / columns: the whole grids, or (a rank-local matrix of a distributed
+    // level) the owned planes of rframe over the [owned | ghost planes] vector of
+    // cframe; classes and steps are taken in global grid coordinates, so a
+    // local row gets its global row's class
+    const SlabFrame &RF = M.rframe, &CF = M.cframe;
+    if (RF.on() != CF.on()) return false;
+    if (RF.on()) {
+        if (RF.nx != rx || RF.ny != ry || RF.gz != rz || CF.nx != kx || CF.ny != ky || CF.gz != kz) return false;
+        if (RF.n_own() != n || CF.n_own() + (CF.gl + CF.gh) * CF.pl() != M.ncols) return false;
+    } else if (rx * ry * rz != n || kx * ky * kz != M.ncols) {
+        return false;
+    }
     std::vector<int64_t> rp(n + 1);
     std::vector<int32_t> col(nnz);
     std::vector<double> val(nnz);
@@ -49,14 +60,16 @@ bool gtc_classes(const GpuCsr &M, bool is_r, const int64_t *fg, const int64_t *c
     bool ok = true;
 #pragma omp parallel for schedule(static) reduction(&& : ok)
     for (int64_t i = 0; i < n; i++) {
-        const int64_t x = i % rx, y = (i / rx) % ry, z = i / (rx * ry);
+        const int64_t x = i % rx, y = (i / rx) % ry, z = i / (rx * ry) + (RF.on() ? RF.z0 : 0);
         const int64_t ax = is_r ? 2 * x : x / 2, ay = is_r ? 2 * y : y / 2, az = is_r ? 2 * z : z / 2;  // anchor
         uint64_t hh = 0x9E3779B97F4A7C15ull ^ (uint64_t)(rp[i + 1] - rp[i]);
         int prev = -1;
         if (rp[i + 1] - rp[i] > KEMAX) ok = false;
         for (int64_t e = rp[i]; e < rp[i + 1]; e++) {
             const int64_t j = col[e];
-            const int64_t dx = j % kx - ax, dy = (j / kx) % ky - ay, dz = j / (kx * ky) - az;
+            const int64_t jp = CF.on() ? CF.in_plane(j) : j % (kx * ky);
+            const int64_t jz = CF.on() ? CF.plane_of(j) : j / (kx * ky);
+            const int64_t dx = jp % kx - ax, dy = jp / kx - ay, dz = jz - az;
             int sl = 0;
             if (is_r) {
                 if (dx < -1 || dx > 2 || dy < -1 || dy > 2 || dz < -1 || dz > 2) ok = false;
@@ -126,9 +139,15 @@ struct GtcArgs {
     const uint16_t *dict;  // nclass x ke entries: value index << 8 | slot
     const double *vtab;    // distinct values
     int ke, nce, ntab;
-    int rx, ry, rz;        // row grid
-    int kx, ky, kz;        // column grid
+    int rx, ry, rz;        // row grid (rz: the owned row planes of a rank-local matrix)
+    int kx, ky, kz;        // column grid (kz: owned column planes)
     int ntx, nty;
+    int tile0;             // first tile of this launch (z-tile range of a segment)
+    // column planes: local plane Z is loadable for kz_lo <= Z < kz_hi (else 0.0) and
+    // starts at Z * plane + (Z < 0 ? add_lo : Z >= kz ? add_hi : 0); rz0 / kz0 =
+    // the global grid plane of local row / column plane 0 (single GPU: 0, 0, kz, 0, 0)
+    int kz_lo, kz_hi, rz0, kz0;
+    int64_t add_lo, add_hi;
     const double *x;
     double *y;
     const double *b;
@@ -167,10 +186,12 @@ __global__ __launch_bounds__(256) void k_gtc_interp(GtcArgs a) {
     __shared__ double st[256];
     __shared__ int16_t lut[27];
     const int tid = threadIdx.x;
-    const int t = xcd_remap(blockIdx.x, gridDim.x);
+    const int t = a.tile0 + xcd_remap(blockIdx.x, gridDim.x);
     const int tix = t % a.ntx, tiy = (t / a.ntx) % a.nty, tiz = t / (a.ntx * a.nty);
     const int x0 = tix * GP_TX, y0 = tiy * GP_TY, z0 = tiz * GP_TZ;
-    const int wx0 = x0 / 2 - 1, wy0 = y0 / 2 - 1, wz0 = z0 / 2 - 1;  // window origin (coarse)
+    // window origin (local coarse planes; rz0 is even, so the tile's four fine
+    // planes map to two coarse planes)
+    const int wx0 = x0 / 2 - 1, wy0 = y0 / 2 - 1, wz0 = ((a.rz0 + z0) >> 1) - 1 - a.kz0;
     const int64_t fplane = (int64_t)a.rx * a.ry, cplane = (int64_t)a.kx * a.ky;
     // the rows' class ids and epilogue operands first
     const int lx = tid % GP_TX, ly = tid / GP_TX, gx = x0 + lx, gy = y0 + ly;
@@ -202,8 +223,9 @@ __global__ __launch_bounds__(256) void k_gtc_interp(GtcArgs a) {
     }
     for (int q = tid; q < GP_WX * GP_WY * GP_WZ; q += 256) {
         const int X = wx0 + q % GP_WX, Y = wy0 + (q / GP_WX) % GP_WY, Z = wz0 + q / (GP_WX * GP_WY);
-        const bool in = (unsigned)X < (unsigned)a.kx && (unsigned)Y < (unsigned)a.ky && (unsigned)Z < (unsigned)a.kz;
-        win[q] = in ? a.x[(int64_t)Z * cplane + (int64_t)Y * a.kx + X] : 0.0;
+        const bool in = (unsigned)X < (unsigned)a.kx && (unsigned)Y < (unsigned)a.ky && Z >= a.kz_lo && Z < a.kz_hi;
+        const int64_t zb = (int64_t)Z * cplane + (Z < 0 ? a.add_lo : Z >= a.kz ? a.add_hi : 0);
+        win[q] = in ? a.x[zb + (int64_t)Y * a.kx + X] : 0.0;
     }
     gtc_stage_dict<G_DMAX>(a, sd, st);
     if (tid < 27) lut[tid] = (int16_t)(((tid / 9 - 1) * GP_WY + (tid / 3) % 3 - 1) * GP_WX + tid % 3 - 1);
@@ -214,7 +236,7 @@ __global__ __launch_bounds__(256) void k_gtc_interp(GtcArgs a) {
         if constexpr (MODE == SPMV_ADD0)
             if (a.dc && !a.dconst) yb[j] = sdt[dci[j]] * yb[j];  // d*b, d decoded after the barrier
         const int gz = z0 + j;
-        const int base = (((gz >> 1) - wz0) * GP_WY + (gy >> 1) - wy0) * GP_WX + (gx >> 1) - wx0;
+        const int base = ((((a.rz0 + gz) >> 1) - a.kz0 - wz0) * GP_WY + (gy >> 1) - wy0) * GP_WX + (gx >> 1) - wx0;
         const uint16_t *e = sd + cl[j] * a.ke;
         double acc = 0.0;
         for (int k = 0; k < a.ke; k += 4) {
@@ -245,10 +267,10 @@ __global__ __launch_bounds__(256) void k_gtc_restrict(GtcArgs a) {
     __shared__ double st[256];
     __shared__ int16_t lut[64];
     const int tid = threadIdx.x;
-    const int t = xcd_remap(blockIdx.x, gridDim.x);
+    const int t = a.tile0 + xcd_remap(blockIdx.x, gridDim.x);
     const int tix = t % a.ntx, tiy = (t / a.ntx) % a.nty, tiz = t / (a.ntx * a.nty);
     const int X0 = tix * GR_TX, Y0 = tiy * GR_TY, Z0 = tiz * GR_TZ;
-    const int wx0 = 2 * X0 - 1, wy0 = 2 * Y0 - 1, wz0 = 2 * Z0 - 1;  // window origin (fine)
+    const int wx0 = 2 * X0 - 1, wy0 = 2 * Y0 - 1, wz0 = 2 * (a.rz0 + Z0) - 1 - a.kz0;  // window origin (local fine)
     const int64_t cplane = (int64_t)a.rx * a.ry, fplane = (int64_t)a.kx * a.ky;
     const int lx = tid % GR_TX, ly = (tid / GR_TX) % GR_TY, lz0 = tid / (GR_TX * GR_TY);  // lz0 in {0, 1}
     bool live[RL];
@@ -267,8 +289,10 @@ __global__ __launch_bounds__(256) void k_gtc_restrict(GtcArgs a) {
     for (int u = 0; u < PF; u++) {  // all of a lane's window loads before its LDS stores
         const int q = tid + 256 * u;
         const int x = wx0 + q % GR_WX, y = wy0 + (q / GR_WX) % GR_WY, z = wz0 + q / (GR_WX * GR_WY);
-        const bool in = q < W && (unsigned)x < (unsigned)a.kx && (unsigned)y < (unsigned)a.ky && (unsigned)z < (unsigned)a.kz;
-        v[u] = in ? a.x[(int64_t)z * fplane + (int64_t)y * a.kx + x] : 0.0;
+        const bool in = q < W && (unsigned)x < (unsigned)a.kx && (unsigned)y < (unsigned)a.ky && z >= a.kz_lo &&
+                        z < a.kz_hi;
+        const int64_t zb = (int64_t)z * fplane + (z < 0 ? a.add_lo : z >= a.kz ? a.add_hi : 0);
+        v[u] = in ? a.x[zb + (int64_t)y * a.kx + x] : 0.0;
     }
 #pragma unroll
     for (int u = 0; u < PF; u++)
@@ -317,11 +341,14 @@ static bool gtc_enabled() {
     return on;
 }
 
-bool gtc_attach(GpuCsr &m, const int64_t *fg, const int64_t *cg) {
+bool gtc_attach(GpuCsr &m, const int64_t *fg, const int64_t *cg, int which) {
     gtc_release(m);
     m.gtc_tried = true;
     if (!gtc_enabled() || m.nnz >= (int64_t(1) << 31)) return false;
-    const bool is_r = m.nrows < m.ncols;
+    const bool is_r = which < 0 ? m.nrows < m.ncols : which == 1;
+    // a rank-local P starts at an even fine plane (its tiles' four fine planes
+    // then map onto two coarse planes of the staged window)
+    if (!is_r && m.rframe.on() && (m.rframe.z0 & 1)) return false;
     std::vector<uint8_t> cls;
     std::vector<std::vector<std::pair<uint8_t, double>>> dict;
     if (!gtc_classes(m, is_r, fg, cg, cls, dict)) return false;
@@ -411,7 +438,18 @@ bool gtc_supports(const GpuCsr &m, SpmvMode mode) {
 // A/B switch FAMG_DIA_DK=0 (shared with the DIA kernels): a constant coded d is read per row
 static bool gtc_dk_enabled() { return flag(FLAG_DIA_DK) != 0; }
 
-void spmv_gtc(const GpuCsr &m, const double *x, double *y, SpmvMode mode, const SpmvEpi &epi, hipStream_t s) {
+// The z-tiles [ta, tb) of a launch whose column windows [w0(t), w0(t) + wz) lie
+// in the owned column planes [0, kz_own): they read no ghost entry.
+template <typename F>
+static void interior_tiles(int ntz, int wz, int kz_own, F w0, int &ta, int &tb) {
+    ta = 0;
+    while (ta < ntz && w0(ta) < 0) ta++;
+    tb = ta;
+    while (tb < ntz && w0(tb) >= 0 && w0(tb) + wz <= kz_own) tb++;
+}
+
+void spmv_gtc(const GpuCsr &m, const double *x, double *y, SpmvMode mode, const SpmvEpi &epi, hipStream_t s,
+              int64_t seg) {
     GtcArgs a{};
     a.cls = m.gtc_cls.get();
     a.dict = m.gtc_dict.get();
@@ -422,6 +460,17 @@ void spmv_gtc(const GpuCsr &m, const double *x, double *y, SpmvMode mode, const 
     const int64_t *rg = m.gtc_r ? m.gtc_cg : m.gtc_fg, *kg = m.gtc_r ? m.gtc_fg : m.gtc_cg;
     a.rx = (int)rg[0]; a.ry = (int)rg[1]; a.rz = (int)rg[2];
     a.kx = (int)kg[0]; a.ky = (int)kg[1]; a.kz = (int)kg[2];
+    a.kz_lo = 0; a.kz_hi = a.kz; a.rz0 = 0; a.kz0 = 0; a.add_lo = a.add_hi = 0;
+    if (m.rframe.on()) {  // rank-local: owned row planes, [owned | ghost planes] columns
+        a.rz = (int)m.rframe.nz;
+        a.rz0 = (int)m.rframe.z0;
+        a.kz = (int)m.cframe.nz;
+        a.kz0 = (int)m.cframe.z0;
+        a.kz_lo = (int)-m.cframe.gl;
+        a.kz_hi = (int)(m.cframe.nz + m.cframe.gh);
+        a.add_lo = m.cframe.add_lo();
+        a.add_hi = m.cframe.add_hi();
+    }
     a.x = x;
     a.y = y;
     a.b = epi.b;
@@ -430,14 +479,26 @@ void spmv_gtc(const GpuCsr &m, const double *x, double *y, SpmvMode mode, const 
     a.dt = epi.dt;
     a.dconst = epi.dc && epi.dk != 0.0 && gtc_dk_enabled();
     a.dk = epi.dk;
+    // the launch's z-tile range: all tiles, or (segments of a rank-local matrix)
+    // 1 = the tiles that read owned columns only, 0 / 2 = those before / after
+    auto range = [&](int ntz, int ta, int tb, int &z0, int &z1) {
+        z0 = seg < 0 || seg == 0 ? 0 : seg == 1 ? ta : tb;
+        z1 = seg < 0 || seg == 2 ? ntz : seg == 1 ? tb : ta;
+    };
     if (m.gtc_r) {
         FAMG_REQUIRE(mode == SPMV_SET, AMG_ERR_UNSUPPORTED, "grid-transfer R: SET only");
         a.ntx = (int)ceil_div(a.rx, GR_TX);
         a.nty = (int)ceil_div(a.ry, GR_TY);
         const int rtz = gtc_rtz();  // coarse planes per tile
         const int ntz = (int)ceil_div(a.rz, rtz);
+        int ta = 0, tb = ntz, z0, z1;
+        if (seg >= 0)
+            interior_tiles(ntz, 2 * rtz + 2, a.kz, [&](int t) { return 2 * (a.rz0 + t * rtz) - 1 - a.kz0; }, ta, tb);
+        range(ntz, ta, tb, z0, z1);
+        if (z1 <= z0) return;
+        a.tile0 = a.ntx * a.nty * z0;
         const size_t dyn = (size_t)a.nce * sizeof(uint16_t);
-        const dim3 grid((unsigned)((int64_t)a.ntx * a.nty * ntz));
+        const dim3 grid((unsigned)((int64_t)a.ntx * a.nty * (z1 - z0)));
         if (rtz == 4) k_gtc_restrict<4><<<grid, dim3(256), dyn, s>>>(a);
         else k_gtc_restrict<2><<<grid, dim3(256), dyn, s>>>(a);
     } else {
@@ -445,7 +506,13 @@ void spmv_gtc(const GpuCsr &m, const double *x, double *y, SpmvMode mode, const 
         a.nty = (int)ceil_div(a.ry, GP_TY);
         const int tz = gtc_tz();
         const int ntz = (int)ceil_div(a.rz, tz);
-        const dim3 grid((unsigned)((int64_t)a.ntx * a.nty * ntz)), block(256);
+        int ta = 0, tb = ntz, z0, z1;
+        if (seg >= 0)
+            interior_tiles(ntz, tz / 2 + 2, a.kz, [&](int t) { return ((a.rz0 + t * tz) >> 1) - 1 - a.kz0; }, ta, tb);
+        range(ntz, ta, tb, z0, z1);
+        if (z1 <= z0) return;
+        a.tile0 = a.ntx * a.nty * z0;
+        const dim3 grid((unsigned)((int64_t)a.ntx * a.nty * (z1 - z0))), block(256);
 #define FAMG_GTCI(TZ)                                                                              \
     switch (mode) {                                                                                \
     case SPMV_SET: k_gtc_interp<SPMV_SET, TZ><<<grid, block, 0, s>>>(a); break;                    \

@@ -28,6 +28,9 @@ namespace famg {
 // record the thread-local message returned by amg_last_error(); returns s
 amg_status set_last_error(amg_status s, const char *msg);
 
+// copy launch records into the caller's amg_launch_rec array (cycle plans)
+void export_plan(const std::vector<LaunchRec> &plan, amg_launch_rec *recs, int64_t cap, int64_t *count);
+
 template <typename F> amg_status guard(F &&f) {
     try {
         f();

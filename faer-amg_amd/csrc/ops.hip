@@ -531,6 +531,37 @@ void MultigridOp::smooth(int64_t l, double *&v, double *&t, const double *f, boo
     }
 }
 
+// One Jacobi step from v = 0 gives v = d*f; with s = 1 nothing else reads v
+// before the correction, so the residual gathers d*f on the fly (RESID0) and the
+// correction writes d*f + P v_c (ADD0): the same rounded values, 16n bytes and
+// one launch fewer per level.  Where that pays (measured per storage, below) --
+// the decision of MultigridOp::cycle and of the distributed cycle's levels.
+bool fold_level(const CsrOp *A, const DiagOp *D, const CsrOp *P, bool fold_zero_guess, bool v_zero, int64_t steps) {
+    const bool gather_cheap = A && 2 * A->m.sell_mode_slices[2] < A->m.nslices;
+    // x-staged stencil classes (levels 1-3 of the box hierarchies): d*f can be
+    // staged with the window (1-B codes of d per staged point) and the
+    // correction's d*f epilogue streams dc and f in place of v, saving the
+    // 24n-byte d*f pass and its launch.  Measured a net loss on the C2 cycle
+    // (profiles/r03/ab_fold_xscs_{on,off_wpr1}.txt: dependent code -> table loads lengthen
+    // the staging, RESID0 44.4 vs 33.3 + 8.5 us on A_1; ADD0 on P_1 49.5 vs
+    // 46.5 us), so off by default; FAMG_FOLD_XSCS=1 turns it on (also for the
+    // small wave-per-row levels below, which lose 0.6 us the same way).
+    const bool fold_xscs = flag(FLAG_FOLD_XSCS) != 0;
+    const bool p_add0 = P && (P->m.kernel == SPMV_KERNEL_SELL || P->m.kernel == SPMV_KERNEL_SELLP ||
+                              P->m.kernel == SPMV_KERNEL_STREAM || P->m.kernel == SPMV_KERNEL_VECTOR || P->m.gtc_on);
+    return fold_zero_guess && v_zero && steps == 1 && A && D && P &&
+                      ((A->m.kernel == SPMV_KERNEL_SELL && A->m.sell_vbits == 0 && gather_cheap) ||
+                       A->m.kernel == SPMV_KERNEL_XS ||  // x-staged: d*x staged with x, no extra gather
+                       (fold_xscs && A->m.kernel == SPMV_KERNEL_SCS && A->m.xscs && p_add0) ||
+                       // wave-per-row levels small enough that x and d stay in L2 (A_4 of the
+                       // box hierarchies: 4096 rows): d gathered beside x costs no HBM bytes
+                       (fold_xscs && A->m.kernel == SPMV_KERNEL_VECTOR && A->m.ncols <= 65536 && p_add0) ||
+                       (A->m.kernel == SPMV_KERNEL_DIA &&
+                        (fold_dia_mode() == 1 ||
+                         (fold_dia_mode() < 0 &&
+                          ((P->m.kernel == SPMV_KERNEL_SELL && P->m.sell_short) || P->m.gtc_on)))));
+}
+
 // cycle (multigrid.rs:269-380).  The result ends in the buffer v points to on
 // entry (Jacobi ping-pong flips an even number of times: 2*steps).
 void MultigridOp::cycle(int64_t l, double *v, const double *f, bool v_zero, double *) {
@@ -561,29 +592,7 @@ void MultigridOp::cycle(int64_t l, double *v, const double *f, bool v_zero, doub
     // Not where most slices carry 32-bit columns (unstructured operators): the
     // residual then gathers d as randomly as x, and that doubled gather cost more
     // than the pass it saves (Q1 elasticity 1.57M rows: 640 vs 388 + 15 us).
-    const bool gather_cheap = A && 2 * A->m.sell_mode_slices[2] < A->m.nslices;
-    // x-staged stencil classes (levels 1-3 of the box hierarchies): d*f can be
-    // staged with the window (1-B codes of d per staged point) and the
-    // correction's d*f epilogue streams dc and f in place of v, saving the
-    // 24n-byte d*f pass and its launch.  Measured a net loss on the C2 cycle
-    // (profiles/r03/ab_fold_xscs_{on,off_wpr1}.txt: dependent code -> table loads lengthen
-    // the staging, RESID0 44.4 vs 33.3 + 8.5 us on A_1; ADD0 on P_1 49.5 vs
-    // 46.5 us), so off by default; FAMG_FOLD_XSCS=1 turns it on (also for the
-    // small wave-per-row levels below, which lose 0.6 us the same way).
-    const bool fold_xscs = flag(FLAG_FOLD_XSCS) != 0;
-    const bool p_add0 = P && (P->m.kernel == SPMV_KERNEL_SELL || P->m.kernel == SPMV_KERNEL_SELLP ||
-                              P->m.kernel == SPMV_KERNEL_STREAM || P->m.kernel == SPMV_KERNEL_VECTOR || P->m.gtc_on);
-    const bool fold = fold_zero_guess && v_zero && steps == 1 && A && D && P &&
-                      ((A->m.kernel == SPMV_KERNEL_SELL && A->m.sell_vbits == 0 && gather_cheap) ||
-                       A->m.kernel == SPMV_KERNEL_XS ||  // x-staged: d*x staged with x, no extra gather
-                       (fold_xscs && A->m.kernel == SPMV_KERNEL_SCS && A->m.xscs && p_add0) ||
-                       // wave-per-row levels small enough that x and d stay in L2 (A_4 of the
-                       // box hierarchies: 4096 rows): d gathered beside x costs no HBM bytes
-                       (fold_xscs && A->m.kernel == SPMV_KERNEL_VECTOR && A->m.ncols <= 65536 && p_add0) ||
-                       (A->m.kernel == SPMV_KERNEL_DIA &&
-                        (fold_dia_mode() == 1 ||
-                         (fold_dia_mode() < 0 &&
-                          ((P->m.kernel == SPMV_KERNEL_SELL && P->m.sell_short) || P->m.gtc_on)))));
+    const bool fold = fold_level(A, D, P, fold_zero_guess, v_zero, steps);
     MgLevel &C = levels[l + 1];
     // grid levels: residual and restriction in one launch (fuse.hip), r never stored
     const bool fuse_pre = fuse_transfers && A && fuse_has_pre(L) && (!fold || D);

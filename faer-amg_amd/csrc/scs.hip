@@ -200,6 +200,11 @@ struct XscsArgs {
     const int32_t *lo;
     int32_t k;
     int nx, ny, nz, tx, ty, tz, rx, ry, rz, wx, wy, wz, ntx, nty;
+    // staged planes: local plane z is loadable for zlo <= z < zhi (else 0.0) and
+    // starts at z * plane + (z < 0 ? add_lo : z >= nz ? add_hi : 0) -- a rank-local
+    // matrix's ghost planes (SlabFrame); single GPU: 0, nz, 0, 0
+    int zlo, zhi, tile0;
+    int64_t add_lo, add_hi;
     const double *x;
     double *y;
     const double *b;
@@ -212,7 +217,7 @@ template <int MODE, int IB, int RL>
 __global__ __launch_bounds__(256) void spmv_xscs_kernel(XscsArgs a) {
     extern __shared__ double win[];
     const int tid = threadIdx.x;
-    const int t = xcd_remap(blockIdx.x, gridDim.x);
+    const int t = a.tile0 + xcd_remap(blockIdx.x, gridDim.x);
     const int tix = t % a.ntx, tiy = (t / a.ntx) % a.nty, tiz = t / (a.ntx * a.nty);
     const int x0 = tix * a.tx, y0 = tiy * a.ty, z0 = tiz * a.tz;
     const int T = a.tx * a.ty * a.tz;
@@ -261,9 +266,10 @@ __global__ __launch_bounds__(256) void spmv_xscs_kernel(XscsArgs a) {
             const int px = p % a.wx, q = p / a.wx;
             const int py = q % a.wy, pz = q / a.wy;
             const int gx = x0 - a.rx + px, gy = y0 - a.ry + py, gz = z0 - a.rz + pz;
-            const bool in = p < W && (unsigned)gx < (unsigned)a.nx && (unsigned)gy < (unsigned)a.ny &&
-                            (unsigned)gz < (unsigned)a.nz;
-            const int64_t g = (int64_t)gz * plane + (int64_t)gy * a.nx + gx;
+            const bool in = p < W && (unsigned)gx < (unsigned)a.nx && (unsigned)gy < (unsigned)a.ny && gz >= a.zlo &&
+                            gz < a.zhi;
+            const int64_t g = (int64_t)gz * plane + (gz < 0 ? a.add_lo : gz >= a.nz ? a.add_hi : 0) +
+                              (int64_t)gy * a.nx + gx;
             if constexpr (MODE == SPMV_RESID0) v[u] = in ? (a.dc ? a.dt[a.dc[g]] : a.d[g]) * a.x[g] : 0.0;
             else v[u] = in ? a.x[g] : 0.0;
         }
@@ -421,6 +427,8 @@ static bool xscs_setup(GpuCsr &m, const std::vector<int32_t> &offs, int Kp, cons
         rz = std::max<int>(rz, (int)std::min<int64_t>(std::abs(ez), INT32_MAX / 4));
     }
     if (rx > 16 || ry > 16 || rz > 16) return false;
+    // planes a nonzero may reach: the grid, or a rank-local matrix's owned + ghost planes
+    const int64_t zlo = m.cframe.on() ? -m.cframe.gl : 0, zhi = m.cframe.on() ? nz + m.cframe.gh : nz;
     bool ok = true;
 #pragma omp parallel for schedule(static) reduction(&& : ok)
     for (int64_t i = 0; i < n; i++) {
@@ -430,7 +438,7 @@ static bool xscs_setup(GpuCsr &m, const std::vector<int32_t> &offs, int Kp, cons
             const int32_t o = (int32_t)((int64_t)col[e] - i);
             const int k = (int)(std::lower_bound(offs.begin(), offs.end(), o) - offs.begin());
             const int64_t X = x + dx[k], Y = y + dy[k], Z = z + dz[k];
-            if (X < 0 || X >= nx || Y < 0 || Y >= ny || Z < 0 || Z >= nz) ok = false;
+            if (X < 0 || X >= nx || Y < 0 || Y >= ny || Z < zlo || Z >= zhi) ok = false;
         }
     }
     if (!ok) return false;
@@ -536,7 +544,7 @@ static int64_t row_classes(const std::vector<int64_t> &rp, const std::vector<int
 }
 
 static void spmv_xscs(const GpuCsr &m, const double *x, double *y, SpmvMode mode, const SpmvEpi &epi,
-                      hipStream_t s);
+                      hipStream_t s, int64_t seg = -1);
 
 // Pick the tile by timing the candidates on the device (a few SET launches each
 // on scratch vectors): the modelled choice missed by up to 1.6x -- wide x rows
@@ -593,10 +601,19 @@ bool build_scs(GpuCsr &m, const std::vector<int64_t> &rp, int64_t other_bytes) {
         m.ncols < m.nrows)
         return false;
     const int64_t n = m.nrows;
+    // a rank-local matrix of a distributed grid level with its slab frames: its
+    // columns map to grid planes (ghost planes included), so the whole matrix
+    // can run x-staged through the frame -- and only that way
+    const SlabFrame &F = m.cframe;
+    const bool framed = F.on() && m.rframe.on();
+    if (framed && (m.rframe.nx != F.nx || m.rframe.ny != F.ny || m.rframe.z0 != F.z0 || m.rframe.nz != F.nz ||
+                   n != F.n_own() || m.ncols != F.n_own() + (F.gl + F.gh) * F.pl() ||
+                   m.grid[0] != F.nx || m.grid[1] != F.ny || m.grid[2] != F.nz))
+        return false;
     // the whole matrix (square), or the longest row segment of a [owned | ghost]
     // distributed level when its rows read owned columns only (the halo interior)
     int64_t r0 = 0, r1 = n, seg = -1;
-    if (m.nrows != m.ncols) {
+    if (m.nrows != m.ncols && !framed) {
         if (m.seg_rows.size() < 3) return false;
         seg = 0;
         for (size_t g = 1; g + 1 < m.seg_rows.size(); g++)
@@ -613,6 +630,14 @@ bool build_scs(GpuCsr &m, const std::vector<int64_t> &rp, int64_t other_bytes) {
     if (seg >= 0)
         for (int64_t e = rp[r0]; e < rp[r1]; e++)
             if (col[e] >= n) return false;  // a ghost column
+    if (framed) {  // local column -> position in the contiguous plane frame (ghosts below negative)
+        const int64_t own = F.n_own(), below = F.gl * F.pl();
+#pragma omp parallel for schedule(static)
+        for (int64_t e = 0; e < m.nnz; e++) {
+            const int64_t c = col[e];
+            col[e] = (int32_t)(c < own ? c : c - own < below ? c - own - below : c - below);
+        }
+    }
     // union of the offsets: bounded first (K <= SCS_KMAX), then a bitmap over the span
     int64_t omin = INT64_MAX, omax = INT64_MIN;
 #pragma omp parallel for reduction(min : omin) reduction(max : omax) schedule(static)
@@ -640,7 +665,7 @@ bool build_scs(GpuCsr &m, const std::vector<int64_t> &rp, int64_t other_bytes) {
     // otherwise short stencils stay on SELL-64: A_1 of the 256^3 cycle (33
     // offsets, 8-bit codes) ran 47 vs 44 us here; A_2 (179 offsets, 16-bit
     // codes) 31-46 vs 55 us
-    const bool on_grid = seg < 0 && grid_applies(m);
+    const bool on_grid = framed ? xscs_enabled() : seg < 0 && grid_applies(m);
     if (K < (on_grid ? 8 : SCS_KMIN)) return false;
     // operators with a <= 256-entry value table keep SELL-64, whose codes decode
     // from an LDS table: A_1 of the 27-pt cycle (125 offsets, 8-bit codes) ran
@@ -666,9 +691,9 @@ bool build_scs(GpuCsr &m, const std::vector<int64_t> &rp, int64_t other_bytes) {
     const int64_t dict_bytes = (int64_t)Kp * C * 8;
     const int64_t stream = ib * (r1 - r0) + dict_bytes + 4 * Kp;
     // x staged per grid tile when the offsets are grid steps within the grid
-    const bool xs3 = on_grid && dict_bytes <= (int64_t(256) << 20) && (double)stream <= 0.5 * (double)other_bytes &&
-                     xscs_setup(m, offs, Kp, rp, col, val);
-    if (!xs3 && (K < SCS_KMIN || small_table)) return false;
+    const bool xs3 = on_grid && dict_bytes <= (int64_t(256) << 20) &&
+                     (framed || (double)stream <= 0.5 * (double)other_bytes) && xscs_setup(m, offs, Kp, rp, col, val);
+    if (!xs3 && (K < SCS_KMIN || small_table || framed)) return false;
     // few long rows: one row per wave, the dictionary streamed (up to 256 MiB)
     const bool lanes = !xs3 && r1 - r0 < SCS_LANES_ROWS && Kp >= 256;
     if (lanes && !scs_lanes_enabled()) { scs_release(m); return false; }
@@ -708,7 +733,7 @@ bool build_scs(GpuCsr &m, const std::vector<int64_t> &rp, int64_t other_bytes) {
 }
 
 static void spmv_xscs(const GpuCsr &m, const double *x, double *y, SpmvMode mode, const SpmvEpi &epi,
-                      hipStream_t s) {
+                      hipStream_t s, int64_t seg) {
     XscsArgs a{};
     a.cls = m.scs_cls.get();
     a.dict = m.scs_dict.get();
@@ -720,11 +745,34 @@ static void spmv_xscs(const GpuCsr &m, const double *x, double *y, SpmvMode mode
     a.wx = a.tx + 2 * a.rx; a.wy = a.ty + 2 * a.ry; a.wz = a.tz + 2 * a.rz;
     a.ntx = (int)ceil_div(a.nx, a.tx); a.nty = (int)ceil_div(a.ny, a.ty);
     const int ntz = (int)ceil_div(a.nz, a.tz);
+    a.zlo = 0; a.zhi = a.nz; a.add_lo = a.add_hi = 0;
+    const SlabFrame &F = m.cframe;
+    if (F.on()) {  // rank-local: the ghost planes below / above the owned ones
+        a.zlo = (int)-F.gl;
+        a.zhi = (int)(F.nz + F.gh);
+        a.add_lo = F.add_lo();
+        a.add_hi = F.add_hi();
+        FAMG_REQUIRE(mode != SPMV_RESID0 || F.gl + F.gh == 0, AMG_ERR_UNSUPPORTED,
+                     "x-staged classes: the folded residual needs d on the ghost planes");
+    }
+    // z-tiles of this launch: all, or (segments of a rank-local matrix) 1 = the
+    // tiles whose window lies in the owned planes, 0 / 2 = those before / after
+    int tz0 = 0, tz1 = ntz;
+    if (seg >= 0 && F.on()) {
+        int ta = 0;
+        while (ta < ntz && ta * a.tz - a.rz < 0) ta++;
+        int tb = ta;
+        while (tb < ntz && (tb + 1) * a.tz + a.rz <= a.nz) tb++;
+        tz0 = seg == 0 ? 0 : seg == 1 ? ta : tb;
+        tz1 = seg == 0 ? ta : seg == 1 ? tb : ntz;
+    }
+    if (tz1 <= tz0) return;
+    a.tile0 = a.ntx * a.nty * tz0;
     a.x = x; a.y = y; a.b = epi.b; a.d = epi.d; a.dc = epi.dc; a.dt = epi.dt;
     const int T = a.tx * a.ty * a.tz;
     const int rl = T <= 256 ? 1 : T <= 512 ? 2 : 4;
     const size_t lds = (size_t)a.wx * a.wy * a.wz * sizeof(double);
-    const dim3 grid((unsigned)((int64_t)a.ntx * a.nty * ntz)), block(256);
+    const dim3 grid((unsigned)((int64_t)a.ntx * a.nty * (tz1 - tz0))), block(256);
 #define FAMG_XS3(M, IB)                                                                            \
     if (rl == 1) spmv_xscs_kernel<M, IB, 1><<<grid, block, lds, s>>>(a);                           \
     else if (rl == 2) spmv_xscs_kernel<M, IB, 2><<<grid, block, lds, s>>>(a);                      \
@@ -750,8 +798,8 @@ void spmv_scs(const GpuCsr &m, const double *x, double *y, SpmvMode mode, const 
     const int64_t r0 = seg < 0 ? 0 : m.seg_rows[seg];
     const int64_t r1 = seg < 0 ? m.nrows : m.seg_rows[seg + 1];
     if (r1 <= r0) return;
-    if (m.xscs && seg < 0) {
-        spmv_xscs(m, x, y, mode, epi, s);
+    if (m.xscs && (seg < 0 || m.cframe.on())) {
+        spmv_xscs(m, x, y, mode, epi, s, seg);
         return;
     }
     ScsArgs a{m.scs_cls.get(), m.scs_dict.get(), m.scs_offs.get(), (int32_t)m.scs_k, (int32_t)m.scs_nclass,

@@ -2448,10 +2448,10 @@ static void log_spmv(const GpuCsr &m, SpmvMode mode, const SpmvEpi &epi, int64_t
     int64_t mat = 0;
     const int64_t csr_mat = part(m.index_bytes());
     const int64_t dia_bytes = 4 * (int64_t)m.dia_cw * r + 8 * m.dia_ntab;
-    if (m.gtc_on && seg < 0 && gtc_supports(m, mode)) {
+    if (m.gtc_on && (seg < 0 || m.rframe.on()) && gtc_supports(m, mode)) {
         kernel = SPMV_KERNEL_GTC;
         name = "gtc";
-        mat = m.nrows + 2 * (int64_t)m.gtc_nce + 8 * (int64_t)m.gtc_ntab;
+        mat = part(m.nrows) + 2 * (int64_t)m.gtc_nce + 8 * (int64_t)m.gtc_ntab;
     } else if (m.kernel == SPMV_KERNEL_BSR) {
         name = "bsr3";
         mat = part(m.stream_bytes());
@@ -2512,8 +2512,8 @@ void spmv(const GpuCsr &m, const double *x, double *y, SpmvMode mode, const Spmv
     if (g_launch_log) log_spmv(m, mode, epi, seg);
     Epi e{x, y, epi.b, epi.d, epi.perm, epi.dc, epi.dt, epi.dk};
     const dim3 block(256);
-    if (m.gtc_on && seg < 0 && gtc_supports(m, mode)) {
-        spmv_gtc(m, x, y, mode, epi, s);
+    if (m.gtc_on && (seg < 0 || m.rframe.on()) && gtc_supports(m, mode)) {
+        spmv_gtc(m, x, y, mode, epi, s, seg);
         return;
     }
     if (m.kernel == SPMV_KERNEL_BSR) {

@@ -150,6 +150,7 @@ SIGNATURES = {
     "amg_gen_elasticity_q1": (i32, [i64, i64, i64, dbl, dbl, C.c_uint64, i32, P(vp)]),
     "amg_dist_pcg_solve": (i32, [vp, i32, vp, vp, i64, dbl, dbl, vp, P(i64)]),
     "amg_multigrid_cycle_plan": (i32, [vp, vp, i64, P(i64)]),
+    "amg_dist_cycle_plan": (i32, [vp, vp, i64, P(i64)]),
     "amg_set_sgs_fused": (i32, [i32]),
     "amg_sgs_fused": (i32, [vp, P(i32)]),
     "amg_halo_plan_create": (i32, [i32, i32, vp, P(vp)]),
@@ -446,6 +447,7 @@ class SparseMatOp(LinOp):
         _ck(_lib.amg_csr_grid_info(self.h, g.ctypes.data_as(vp)))
         d["grid"] = tuple(int(v) for v in g[:3])
         d["grid_source"] = ("none", "given", "inferred")[int(g[10])]
+        d["gtc"] = ("none", "P", "R")[int(g[11])]
         d["xstaged"] = bool(g[3])
         if d["xstaged"]:
             d["tile"], d["halo"] = tuple(int(v) for v in g[4:7]), tuple(int(v) for v in g[7:10])
@@ -1000,6 +1002,16 @@ class DistMultigrid(LinOp):
         """Overlap halo exchanges with the interior rows of their SpMV (default on)."""
         _ck(_lib.amg_dist_set_option(self.h, 0, 1 if on else 0))
         return self
+
+    def cycle_plan(self, cap=4096):
+        """The launches of one distributed V-cycle on this rank (amg_dist_cycle_plan;
+        collective: every rank calls it), as Multigrid.cycle_plan."""
+        n = i64()
+        recs = (LaunchRec * cap)()
+        _ck(_lib.amg_dist_cycle_plan(self.h, recs, cap, C.byref(n)))
+        return [{"level": r.level, "role": ROLES.get(r.role, "?"), "kernel": r.kernel,
+                 "mode": MODES.get(r.mode, "?"), "name": r.name.decode(), "rows": r.rows,
+                 "bytes": r.bytes, "csr_bytes": r.csr_bytes} for r in recs[:min(cap, n.value)]]
 
     def set_graph(self, on=True):
         """hipGraph replay of the distributed cycle (RCCL communicators only; default off)."""

@@ -151,7 +151,8 @@ amg_status amg_grid_from_offsets(const int64_t *offs, int64_t k, int64_t n, int6
 amg_status amg_csr_spmv_epilogue(const amg_linop *op, int32_t mode, const double *x, double *y,
                                  const double *b, const double *d);
 /* info12 = {nx, ny, nz (0: no hint), x-staged (0/1), tile tx, ty, tz, halo
- * rx, ry, rz, hint source (0 none, 1 given, 2 inferred), 0}. */
+ * rx, ry, rz, hint source (0 none, 1 given, 2 inferred), grid-transfer classes
+ * (0 none, 1 as P, 2 as R)}. */
 amg_status amg_csr_grid_info(const amg_linop *op, int64_t *info12);
 
 /* Copy a host CSR with usize-compatible (int64) row pointers and column indices
@@ -329,6 +330,11 @@ typedef struct amg_launch_rec {
     char name[32];                     /* storage kernel ("dia", "sell_short", "dia_sgs", "vec_mul" ...) */
 } amg_launch_rec;
 amg_status amg_multigrid_cycle_plan(amg_linop *mg, amg_launch_rec *recs, int64_t cap, int64_t *count);
+/* The same for a distributed multigrid: one eager cycle (halo exchanges
+ * included: collective, every rank calls it) on this rank's scratch vectors;
+ * level = global level index (the redundant tail's levels after the
+ * distributed ones), rows = this rank's rows. */
+amg_status amg_dist_cycle_plan(amg_linop *dist, amg_launch_rec *recs, int64_t cap, int64_t *count);
 /* Launch the marker kernel k_trace_mark(tag) on the context stream: brackets a
  * region of a rocprofv3 kernel trace (bench.py marks its timed V-cycles, and
  * scripts/prof_summary.py keeps the dispatches between the marks). */
