@@ -728,9 +728,13 @@ struct DistMultigridOp : LinOp {
         } else {
             const int64_t cnt = tail_splits[tr->rank + 1] - tail_splits[tr->rank];
             log_at(l, AMG_ROLE_RESTRICT);
-            if (cnt) halo_spmv(D.sp, D.r.get(), D.R->m, gather.get() + tr->rank * tail_max, SPMV_SET, SpmvEpi{});
-            else halo(D.sp, D.r.get(), *tr, s);
-            gather_tail(gather.get() + tr->rank * tail_max);
+            if (tr->nranks == 1) {  // nothing to gather: restrict into the tail's input
+                halo_spmv(D.sp, D.r.get(), D.R->m, fc_full.get(), SPMV_SET, SpmvEpi{});
+            } else {
+                if (cnt) halo_spmv(D.sp, D.r.get(), D.R->m, gather.get() + tr->rank * tail_max, SPMV_SET, SpmvEpi{});
+                else halo(D.sp, D.r.get(), *tr, s);
+                gather_tail(gather.get() + tr->rank * tail_max);
+            }
             if (g_launch_log) g_launch_log->level_base = (int32_t)La;
             for (int64_t k = 0; k < mu; k++) tail->cycle(0, vc_full.get(), fc_full.get(), k == 0, nullptr);
             if (g_launch_log) g_launch_log->level_base = 0;

@@ -438,14 +438,15 @@ bool gtc_supports(const GpuCsr &m, SpmvMode mode) {
 // A/B switch FAMG_DIA_DK=0 (shared with the DIA kernels): a constant coded d is read per row
 static bool gtc_dk_enabled() { return flag(FLAG_DIA_DK) != 0; }
 
-// The z-tiles [ta, tb) of a launch whose column windows [w0(t), w0(t) + wz) lie
-// in the owned column planes [0, kz_own): they read no ghost entry.
+// The z-tiles [ta, tb) of a launch whose column windows [w0(t), w0(t) + wz) read
+// no ghost plane (planes [kz_lo, 0) and [kz_own, kz_hi)): they can run while the
+// halo is in flight.
 template <typename F>
-static void interior_tiles(int ntz, int wz, int kz_own, F w0, int &ta, int &tb) {
+static void interior_tiles(int ntz, int wz, int kz_own, int kz_lo, int kz_hi, F w0, int &ta, int &tb) {
     ta = 0;
-    while (ta < ntz && w0(ta) < 0) ta++;
+    while (ta < ntz && w0(ta) < 0 && kz_lo < 0) ta++;
     tb = ta;
-    while (tb < ntz && w0(tb) >= 0 && w0(tb) + wz <= kz_own) tb++;
+    while (tb < ntz && !(w0(tb) + wz > kz_own && kz_hi > kz_own)) tb++;
 }
 
 void spmv_gtc(const GpuCsr &m, const double *x, double *y, SpmvMode mode, const SpmvEpi &epi, hipStream_t s,
@@ -493,7 +494,7 @@ void spmv_gtc(const GpuCsr &m, const double *x, double *y, SpmvMode mode, const 
         const int ntz = (int)ceil_div(a.rz, rtz);
         int ta = 0, tb = ntz, z0, z1;
         if (seg >= 0)
-            interior_tiles(ntz, 2 * rtz + 2, a.kz, [&](int t) { return 2 * (a.rz0 + t * rtz) - 1 - a.kz0; }, ta, tb);
+            interior_tiles(ntz, 2 * rtz + 2, a.kz, a.kz_lo, a.kz_hi, [&](int t) { return 2 * (a.rz0 + t * rtz) - 1 - a.kz0; }, ta, tb);
         range(ntz, ta, tb, z0, z1);
         if (z1 <= z0) return;
         a.tile0 = a.ntx * a.nty * z0;
@@ -508,7 +509,7 @@ void spmv_gtc(const GpuCsr &m, const double *x, double *y, SpmvMode mode, const 
         const int ntz = (int)ceil_div(a.rz, tz);
         int ta = 0, tb = ntz, z0, z1;
         if (seg >= 0)
-            interior_tiles(ntz, tz / 2 + 2, a.kz, [&](int t) { return ((a.rz0 + t * tz) >> 1) - 1 - a.kz0; }, ta, tb);
+            interior_tiles(ntz, tz / 2 + 2, a.kz, a.kz_lo, a.kz_hi, [&](int t) { return ((a.rz0 + t * tz) >> 1) - 1 - a.kz0; }, ta, tb);
         range(ntz, ta, tb, z0, z1);
         if (z1 <= z0) return;
         a.tile0 = a.ntx * a.nty * z0;

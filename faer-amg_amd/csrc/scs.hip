@@ -758,11 +758,13 @@ static void spmv_xscs(const GpuCsr &m, const double *x, double *y, SpmvMode mode
     // z-tiles of this launch: all, or (segments of a rank-local matrix) 1 = the
     // tiles whose window lies in the owned planes, 0 / 2 = those before / after
     int tz0 = 0, tz1 = ntz;
-    if (seg >= 0 && F.on()) {
+    if (seg >= 0 && F.on()) {  // a window reads ghosts only where it crosses into a ghost plane
+        auto below = [&](int t) { return t * a.tz - a.rz < 0 && F.gl > 0; };
+        auto above = [&](int t) { return (t + 1) * a.tz + a.rz > a.nz && F.gh > 0; };
         int ta = 0;
-        while (ta < ntz && ta * a.tz - a.rz < 0) ta++;
+        while (ta < ntz && below(ta)) ta++;
         int tb = ta;
-        while (tb < ntz && (tb + 1) * a.tz + a.rz <= a.nz) tb++;
+        while (tb < ntz && !above(tb)) tb++;
         tz0 = seg == 0 ? 0 : seg == 1 ? ta : tb;
         tz1 = seg == 0 ? ta : seg == 1 ? tb : ntz;
     }
@@ -795,13 +797,13 @@ static void spmv_xscs(const GpuCsr &m, const double *x, double *y, SpmvMode mode
 
 void spmv_scs(const GpuCsr &m, const double *x, double *y, SpmvMode mode, const SpmvEpi &epi, hipStream_t s,
               int64_t seg) {
-    const int64_t r0 = seg < 0 ? 0 : m.seg_rows[seg];
-    const int64_t r1 = seg < 0 ? m.nrows : m.seg_rows[seg + 1];
-    if (r1 <= r0) return;
-    if (m.xscs && (seg < 0 || m.cframe.on())) {
+    if (m.xscs && (seg < 0 || m.cframe.on())) {  // a framed matrix: segments are z-tile ranges, not row ranges
         spmv_xscs(m, x, y, mode, epi, s, seg);
         return;
     }
+    const int64_t r0 = seg < 0 ? 0 : m.seg_rows[seg];
+    const int64_t r1 = seg < 0 ? m.nrows : m.seg_rows[seg + 1];
+    if (r1 <= r0) return;
     ScsArgs a{m.scs_cls.get(), m.scs_dict.get(), m.scs_offs.get(), (int32_t)m.scs_k, (int32_t)m.scs_nclass,
               (int32_t)r0, (int32_t)r1, (int32_t)m.ncols, x, y, epi.b, epi.d, epi.dc, epi.dt};
     const dim3 grid((unsigned)ceil_div(r1 - r0, m.scs_lanes ? 4 : 512)), block(256);

@@ -2457,7 +2457,7 @@ static void log_spmv(const GpuCsr &m, SpmvMode mode, const SpmvEpi &epi, int64_t
         mat = part(m.stream_bytes());
     } else if (m.kernel == SPMV_KERNEL_SCS || (m.has_scs() && seg >= 0 && seg == m.scs_seg && mode != SPMV_SGS)) {
         kernel = SPMV_KERNEL_SCS;
-        name = (m.xscs && seg < 0) ? "xscs" : m.scs_lanes ? "scs_lanes" : "scs";
+        name = (m.xscs && (seg < 0 || m.cframe.on())) ? "xscs" : m.scs_lanes ? "scs_lanes" : "scs";
         mat = m.scs_ib * r + 8 * m.scs_k * m.scs_nclass + 4 * m.scs_k;
     } else if (m.kernel == SPMV_KERNEL_XS && seg < 0 && xs_supports(mode)) {
         name = "xsell";
