@@ -577,7 +577,11 @@ def run_dist(args, world, rank, local_rank):
     r0, r1 = dm.local_rows()
     b = torch.as_tensor(splitmix_uniform(n_glob, 42)[r0:r1].copy(), device=f"cuda:{local_rank}")
     z = torch.empty_like(b)
-    plan = plan_summary(dm.cycle_plan())  # collective: one eager cycle with the launch recorder on
+    raw_plan = dm.cycle_plan()  # collective: one eager cycle with the launch recorder on
+    plan = plan_summary(raw_plan)
+    if args.plan_out and rank == 0:
+        with open(args.plan_out, "w") as fh:
+            json.dump({"steps": args.steps, "plan": raw_plan}, fh)
     # hipGraph replay of the whole distributed cycle (RCCL p2p + all-gather
     # captured), checked bitwise against the eager cycle on every rank before it
     # is used; any difference or error falls back to the eager cycle
@@ -608,11 +612,13 @@ def run_dist(args, world, rank, local_rank):
         dm.apply(z, b)
     torch.cuda.synchronize()
     dist.barrier()
+    ctx.trace_mark(1)  # brackets the timed cycles in a kernel trace (scripts/prof_summary.py)
     t_start = time.perf_counter()
     for _ in range(args.steps):
         dm.apply(z, b)
     torch.cuda.synchronize()
     el = time.perf_counter() - t_start
+    ctx.trace_mark(2)
     dist.barrier()
     tmax = torch.tensor([el], dtype=torch.float64)
     dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
