@@ -904,6 +904,42 @@ def test_vcycle_256_storage_mix(ctx):
     assert np.all(np.abs(hist - hist_o) <= 1e-8 * hist_o + floor), (hist, hist_o)
 
 
+@pytest.mark.timeout(900)
+def test_vcycle_256_27pt_sgs(ctx):
+    """Config C3 itself (27-pt anisotropic 256^3, SA 2^3 boxes, multicolour SGS
+    on the fine level -- the fused plane-parity phases of sgs27.hip -- L1 on the
+    Galerkin levels, Cholesky coarsest) against the oracle on the same
+    hierarchy (verdict r03 item 2): one V-cycle to 1e-11 and 10 stationary
+    cycles (rho_k) to 1e-8 (+ the fp64 noise floor of a computed residual)."""
+    import sys
+    import torch
+    dims = (256, 256, 256)
+    A = fa().SparseMatOp.aniso27(ctx, *dims, 1.0, 1.0, 0.01)
+    mg = fa().sa_build_box(A, dims, (2, 2, 2), coarsest_dim=1000, smoother="sgs")
+    S0 = mg.level(0)[1]
+    assert S0.kind == "sgs" and fa().sgs_fused(S0)  # the fused phases are what runs
+    assert sum(1 for p in mg.cycle_plan() if p["name"] == "sgs27_phase") in (6, 8)
+    levels = oracle_levels_from_gpu(mg, "sgs")
+    assert levels[0]["smoother"] == "sgs"
+    sys.path.insert(0, GOLD)
+    from make_golden import splitmix_uniform
+    b = splitmix_uniform(A.nrows, 42)
+    omg = O.Multigrid(levels)
+    omg.set_parallel(16)
+    zref = omg.apply(b)
+    z = apply_dev(ctx, mg, b, A.nrows)
+    assert np.linalg.norm(z - zref) <= 1e-11 * np.linalg.norm(zref)
+    x = torch.zeros(A.nrows, dtype=torch.float64, device="cuda:0")
+    it, hist = fa().stationary_solve(A, mg, T(b), x, max_iter=11, rel_tol=1e-300)
+    OA = levels[0]["A"]
+    _, it_o, hist_o = O.stationary_solve(OA, omg, b, max_iter=11, rel_tol=1e-300)
+    assert it == it_o == 11
+    rp, _, val = A.arrays()
+    a_inf = float(np.max(np.add.reduceat(np.abs(val), rp[:-1])))
+    floor = EPS * a_inf * np.max(np.abs(H(x))) / np.max(np.abs(b))
+    assert np.all(np.abs(hist - hist_o) <= 1e-8 * hist_o + floor), (hist, hist_o)
+
+
 @pytest.mark.parametrize("window", [-1, 0, 64])
 def test_random_7pt_generator_and_spmv(ctx, window):
     """The general operator of roofline.general (random coefficients, symmetric
@@ -1413,19 +1449,31 @@ def test_cycle_plan_sgs_counts_colour_launches(ctx):
     assert len(sweeps) == (C - 1) + (C - 1) + (2 * C - 1), (len(sweeps), C)
 
 
-@pytest.mark.parametrize("dims", [(48, 48, 32), (50, 45, 37), (64, 40, 33)])
+@pytest.mark.parametrize("dims", [(48, 48, 32), (50, 45, 37), (64, 40, 33), (49, 40, 32), (33, 35, 37)])
 def test_sgs27_fused_phases_bitwise(ctx, dims):
     """The fused plane-parity SGS phases (sgs27.hip: three launches per SGS step
     -- the odd planes' forward and backward colours in one -- or four, in-plane
     colours on shrinking LDS halos) against the colour launches (fifteen per
     step): bitwise equal for the step from e = 0 (the smoother's apply) and
     inside the V-cycle (pre-smoothing from zero, post-smoothing on x), odd and
-    even extents; and within 1e-11 of the oracle's V-cycle."""
+    even y/z extents; and within 1e-11 of the oracle's V-cycle.  An odd x
+    extent (rows not 16-B aligned pairs) takes the colour launches: the test
+    asserts that fallback and the same oracle bound."""
     OA = O.aniso27(*dims)
     A = fa().SparseMatOp.aniso27(ctx, *dims, 1.0, 1.0, 0.01)
     if A.spmv_info()["kernel"] != "dia":
         pytest.skip("operator not stored as DIA codes")
     S1 = fa().SymGaussSeidel(A)
+    if dims[0] % 2:
+        assert not fa().sgs_fused(S1)
+        mg1 = fa().sa_build_box(A, dims, (2, 2, 2), coarsest_dim=500, smoother="sgs")
+        assert not fa().sgs_fused(mg1.level(0)[1])
+        assert sum(1 for p in mg1.cycle_plan() if p["name"] == "sgs27_phase") == 0
+        b = np.random.default_rng(9).uniform(-1, 1, OA.nrows)
+        z1 = apply_dev(ctx, mg1, b, OA.nrows)
+        zref = O.Multigrid(oracle_levels_from_gpu(mg1, "sgs")).apply(b)
+        assert np.linalg.norm(z1 - zref) <= 1e-11 * np.linalg.norm(zref)
+        return
     fa().set_sgs_fused(False)
     try:
         S0 = fa().SymGaussSeidel(A)
