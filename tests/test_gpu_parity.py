@@ -1449,7 +1449,7 @@ def test_cycle_plan_sgs_counts_colour_launches(ctx):
     assert len(sweeps) == (C - 1) + (C - 1) + (2 * C - 1), (len(sweeps), C)
 
 
-@pytest.mark.parametrize("dims", [(48, 48, 32), (50, 45, 37), (64, 40, 33), (49, 40, 32), (33, 35, 37)])
+@pytest.mark.parametrize("dims", [(48, 48, 32), (50, 45, 37), (64, 40, 33), (49, 48, 32), (65, 40, 33)])
 def test_sgs27_fused_phases_bitwise(ctx, dims):
     """The fused plane-parity SGS phases (sgs27.hip: three launches per SGS step
     -- the odd planes' forward and backward colours in one -- or four, in-plane
