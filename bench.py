@@ -57,6 +57,13 @@ def measured_traffic(edge, problem):
     if edge != 256 or problem != "7pt":
         return None, None
     import glob
+    # the latest round's cycle-wide passes (scripts/pmc_cycle.sh: the roofline
+    # kernel -- DIA SET on A_0 -- and every launch of the cycle), else the
+    # older fine-SpMV-only passes
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "c2_cycle_traffic.json")))
+    if files:
+        d = json.load(open(files[-1]))
+        return d["fine_set"]["hbm_bytes_per_launch"], os.path.relpath(files[-1], ROOT)
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "fine_spmv_traffic.json")))
     if not files:
         return None, None

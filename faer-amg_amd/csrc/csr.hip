@@ -281,7 +281,8 @@ void csr_finalize(GpuCsr &m, const std::vector<int64_t> *segments) {
     scs_release(m);
     sellp_release(m);
     gtc_release(m);
-    m.gtc_tried = false;
+    gtx_release(m);
+    m.gtc_tried = m.gtx_tried = false;
     build_sell(m, rp);
     const bool dia_all = m.has_dia() && m.dia_r0 == 0 && m.dia_r1 == m.nrows;
     const int64_t sell_b = m.sell_bytes + 12 * (m.nslices + 1) + 4 * m.sell_steps + 8 * m.sell_ntab;

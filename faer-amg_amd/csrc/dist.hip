@@ -1069,6 +1069,8 @@ static std::shared_ptr<DistMultigridOp> build_dist(amg_comm *comm, const Multigr
         GpuCsr &R = d->L[l].R->m, &Pm = d->L[l].P->m;
         if (R.nrows > 0) gtc_attach(R, Af.grid, Ac.grid, 1);  // gtc_classes checks the frames / grids first
         if (Pm.nrows > 0) gtc_attach(Pm, Af.grid, Ac.grid, 0);
+        if (R.nrows > 0 && (!R.gtc_on || gtx_mode() == 2)) gtx_attach(R, Af.grid, Ac.grid, 1);
+        if (Pm.nrows > 0 && (!Pm.gtc_on || gtx_mode() == 2)) gtx_attach(Pm, Af.grid, Ac.grid, 0);
     }
     for (int64_t l = 0; l < d->La; l++) {
         d->L[l].P->nrows = d->L[l].P->m.nrows;

@@ -157,6 +157,15 @@ struct GpuCsr {
     DevBuf<double> gtc_vtab;    // the distinct values (<= 256)
     int gtc_ke = 0, gtc_nce = 0, gtc_ntab = 0;
     int64_t gtc_fg[3] = {0, 0, 0}, gtc_cg[3] = {0, 0, 0};
+    // wide grid-transfer classes (gtx.hip): 16-bit class per row, dictionary of
+    // (window offset, fp64 value) entries in global memory -- every box level
+    bool gtx_on = false, gtx_r = false, gtx_tried = false;
+    DevBuf<uint16_t> gtx_cls, gtx_doff;
+    DevBuf<int32_t> gtx_dptr, gtx_dlen;
+    DevBuf<double> gtx_dval;
+    int64_t gtx_nclass = 0, gtx_nent = 0;
+    int gtx_tile[3] = {0, 0, 0}, gtx_win[3] = {0, 0, 0}, gtx_lo[3] = {0, 0, 0};
+    int64_t gtx_fg[3] = {0, 0, 0}, gtx_cg[3] = {0, 0, 0};
     // grid hint: the rows are the points of an nx x ny x nz grid, x fastest (0 = none);
     // set by the stencil generators, the box hierarchy and amg_csr_set_grid
     // (grid_src 1), else inferred at finalize from the stencil offsets (grid_src 2)
@@ -267,7 +276,10 @@ enum SpmvMode : int {
     SPMV_SGS = 4,    // e[perm p] = e[perm p] + d_p (b[perm p] - (A e)_p)
     // the zero-guess Jacobi step v = d*b folded into its consumers (never stored):
     SPMV_RESID0 = 5, // y = b - A (d*b)   (x == b; d gathered with x)
-    SPMV_ADD0 = 6    // y = d*b + A x
+    SPMV_ADD0 = 6,   // y = d*b + A x
+    // restriction that also takes the next level's first Jacobi step from zero:
+    // y = A x, y2 = d*y (wide grid-transfer classes only, gtx.hip)
+    SPMV_SETDF = 7
 };
 
 struct SpmvEpi {
@@ -277,6 +289,7 @@ struct SpmvEpi {
     const uint8_t *dc = nullptr;  // JACOBI only: 8-bit codes of d into dt
     const double *dt = nullptr;
     double dk = 0.0;              // d when every entry is this one value (0: not constant)
+    double *y2 = nullptr;         // SETDF: the second output d*y
 };
 
 // y = epilogue(A x) over all rows (seg < 0) or over row segment `seg`, with the
@@ -295,6 +308,13 @@ void spmv_scs(const GpuCsr &m, const double *x, double *y, SpmvMode mode, const 
               int64_t seg);
 bool xs_supports(SpmvMode mode);
 bool gtc_supports(const GpuCsr &m, SpmvMode mode);
+// wide grid-transfer classes (gtx.hip); which as gtc_attach
+bool gtx_attach(GpuCsr &m, const int64_t *fg, const int64_t *cg, int which = -1);
+void gtx_release(GpuCsr &m);
+bool gtx_supports(const GpuCsr &m, SpmvMode mode);
+int gtx_mode();
+void spmv_gtx(const GpuCsr &m, const double *x, double *y, SpmvMode mode, const SpmvEpi &epi, hipStream_t s,
+              int64_t seg = -1);
 // seg < 0: every tile; a rank-local matrix (rframe on) also takes segments 1
 // (interior z-tiles: no ghost reads) and 0 / 2 (the tiles before / after)
 void spmv_gtc(const GpuCsr &m, const double *x, double *y, SpmvMode mode, const SpmvEpi &epi, hipStream_t s,
@@ -474,8 +494,10 @@ struct MultigridOp : LinOp {
     ~MultigridOp() override;
 
     // V-cycle building blocks (also used by the distributed multigrid)
-    void cycle(int64_t l, double *v, const double *f, bool v_zero, double *out_final);
-    void smooth(int64_t l, double *&v, double *&t, const double *f, bool v_zero);
+    // pre_df: the restriction that produced f already wrote the first Jacobi
+    // step from zero (d*f, SPMV_SETDF) into the level's t buffer
+    void cycle(int64_t l, double *v, const double *f, bool v_zero, double *out_final, bool pre_df = false);
+    void smooth(int64_t l, double *&v, double *&t, const double *f, bool v_zero, bool pre_df = false);
     // launch records of one V-cycle (eager, recorder on)
     std::vector<LaunchRec> cycle_plan();
 

@@ -409,8 +409,10 @@ void attach_box_transfers(const GpuCsr &Af, const GpuCsr &Ac, GpuCsr &R, GpuCsr 
         if (fg[q] <= 0 || cg[q] != (fg[q] + 1) / 2) return;
     if (fg[0] * fg[1] * fg[2] != Af.nrows || cg[0] * cg[1] * cg[2] != Ac.nrows) return;
     if (P.nrows != Af.nrows || P.ncols != Ac.nrows || R.nrows != Ac.nrows || R.ncols != Af.nrows) return;
-    if (!P.gtc_on && !P.gtc_tried) gtc_attach(P, fg, cg);
-    if (!R.gtc_on && !R.gtc_tried) gtc_attach(R, fg, cg);
+    if (!P.gtc_on && !P.gtc_tried) gtc_attach(P, fg, cg, 0);
+    if (!R.gtc_on && !R.gtc_tried) gtc_attach(R, fg, cg, 1);
+    if ((!P.gtc_on || gtx_mode() == 2) && !P.gtx_on && !P.gtx_tried) gtx_attach(P, fg, cg, 0);
+    if ((!R.gtc_on || gtx_mode() == 2) && !R.gtx_on && !R.gtx_tried) gtx_attach(R, fg, cg, 1);
 }
 
 // fine points per lane along z in the P kernel (FAMG_GTC_TZ=8: eight)

@@ -2298,6 +2298,7 @@ void choose_kernel(GpuCsr &m) {
     case SPMV_SGS: KERNEL<SPMV_SGS __VA_ARGS__><<<grid, block, 0, s>>>(args); break;       \
     case SPMV_RESID0: KERNEL<SPMV_RESID0 __VA_ARGS__><<<grid, block, 0, s>>>(args); break; \
     case SPMV_ADD0: KERNEL<SPMV_ADD0 __VA_ARGS__><<<grid, block, 0, s>>>(args); break;     \
+    default: break;                                                                     \
     }
 #define FAMG_VEC(VB, O16, W) , VB, O16, W
 
@@ -2448,7 +2449,11 @@ static void log_spmv(const GpuCsr &m, SpmvMode mode, const SpmvEpi &epi, int64_t
     int64_t mat = 0;
     const int64_t csr_mat = part(m.index_bytes());
     const int64_t dia_bytes = 4 * (int64_t)m.dia_cw * r + 8 * m.dia_ntab;
-    if (m.gtc_on && (seg < 0 || m.rframe.on()) && gtc_supports(m, mode)) {
+    if (m.gtx_on && (seg < 0 || m.rframe.on()) && gtx_supports(m, mode)) {
+        kernel = SPMV_KERNEL_GTC;
+        name = "gtx";
+        mat = 2 * part(m.nrows) + 10 * m.gtx_nent + 8 * m.gtx_nclass;
+    } else if (m.gtc_on && (seg < 0 || m.rframe.on()) && gtc_supports(m, mode)) {
         kernel = SPMV_KERNEL_GTC;
         name = "gtc";
         mat = part(m.nrows) + 2 * (int64_t)m.gtc_nce + 8 * (int64_t)m.gtc_ntab;
@@ -2500,6 +2505,7 @@ static void log_spmv(const GpuCsr &m, SpmvMode mode, const SpmvEpi &epi, int64_t
                                    && epi.dc ? 1 : 8)) * xcols;
         break;
     case SPMV_ADD0: vec += 16 * r + db * r; break;       // b, d read, y written
+    case SPMV_SETDF: vec += 16 * r + db * r; break;      // y and d*y written, d read
     }
     log_launch(name, kernel, mode, r, mat + vec, csr_mat + vec);
 }
@@ -2512,6 +2518,11 @@ void spmv(const GpuCsr &m, const double *x, double *y, SpmvMode mode, const Spmv
     if (g_launch_log) log_spmv(m, mode, epi, seg);
     Epi e{x, y, epi.b, epi.d, epi.perm, epi.dc, epi.dt, epi.dk};
     const dim3 block(256);
+    if (m.gtx_on && (seg < 0 || m.rframe.on()) && gtx_supports(m, mode)) {
+        spmv_gtx(m, x, y, mode, epi, s, seg);
+        return;
+    }
+    FAMG_REQUIRE(mode != SPMV_SETDF, AMG_ERR_UNSUPPORTED, "SETDF needs wide grid-transfer classes");
     if (m.gtc_on && (seg < 0 || m.rframe.on()) && gtc_supports(m, mode)) {
         spmv_gtc(m, x, y, mode, epi, s, seg);
         return;

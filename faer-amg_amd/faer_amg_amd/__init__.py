@@ -180,7 +180,7 @@ class LaunchRec(C.Structure):
 
 
 ROLES = {0: "smooth", 1: "resid", 2: "restrict", 3: "interp", 4: "coarse", 5: "other"}
-MODES = {-1: "-", 0: "SET", 1: "ADD", 2: "RESID", 3: "JACOBI", 4: "SGS", 5: "RESID0", 6: "ADD0"}
+MODES = {-1: "-", 0: "SET", 1: "ADD", 2: "RESID", 3: "JACOBI", 4: "SGS", 5: "RESID0", 6: "ADD0", 7: "SETDF"}
 
 
 class AmgError(RuntimeError):
@@ -447,7 +447,8 @@ class SparseMatOp(LinOp):
         _ck(_lib.amg_csr_grid_info(self.h, g.ctypes.data_as(vp)))
         d["grid"] = tuple(int(v) for v in g[:3])
         d["grid_source"] = ("none", "given", "inferred")[int(g[10])]
-        d["gtc"] = ("none", "P", "R")[int(g[11])]
+        d["gtc"] = ("none", "P", "R", "P", "R")[int(g[11])]
+        d["gtc_kind"] = ("none", "gtc", "gtc", "gtx", "gtx")[int(g[11])]
         d["xstaged"] = bool(g[3])
         if d["xstaged"]:
             d["tile"], d["halo"] = tuple(int(v) for v in g[4:7]), tuple(int(v) for v in g[7:10])

@@ -152,7 +152,7 @@ amg_status amg_csr_spmv_epilogue(const amg_linop *op, int32_t mode, const double
                                  const double *b, const double *d);
 /* info12 = {nx, ny, nz (0: no hint), x-staged (0/1), tile tx, ty, tz, halo
  * rx, ry, rz, hint source (0 none, 1 given, 2 inferred), grid-transfer classes
- * (0 none, 1 as P, 2 as R)}. */
+ * (0 none, 1 as P, 2 as R: 8-bit gtc.hip; 3 as P, 4 as R: 16-bit gtx.hip)}. */
 amg_status amg_csr_grid_info(const amg_linop *op, int64_t *info12);
 
 /* Copy a host CSR with usize-compatible (int64) row pointers and column indices
@@ -323,7 +323,8 @@ typedef enum amg_role {
 } amg_role;
 typedef struct amg_launch_rec {
     int32_t level, role, kernel, mode; /* kernel as amg_csr_spmv_info (-1: vector op); mode: SET 0,
-                                          ADD 1, RESID 2, JACOBI 3, SGS 4, RESID0 5, ADD0 6 (-1) */
+                                          ADD 1, RESID 2, JACOBI 3, SGS 4, RESID0 5, ADD0 6,
+                                          SETDF 7 = SET + d*y (-1) */
     int64_t rows;                      /* rows this launch updates */
     int64_t bytes;                     /* algorithmic bytes */
     int64_t csr_bytes;                 /* with 12 nnz + 4 (m+1) matrix bytes (= bytes for vector ops) */
