@@ -296,7 +296,10 @@ amg_status amg_csr_spmv_info(const amg_linop *op, int64_t *info8) {
             info8[6] = info8[3] - m.xs_escape_slices;
             info8[7] = m.xs_escape_slices;
         }
-        if (m.gtc_on) {  // the grid-transfer overlay (its modes; the storage above serves the rest)
+        if (m.gtx_on) {  // the wide grid-transfer overlay (gtx.hip; served first)
+            info8[0] = SPMV_KERNEL_GTC;
+            info8[1] = 2 * m.nrows + 10 * m.gtx_nent + 8 * m.gtx_nclass;
+        } else if (m.gtc_on) {  // the grid-transfer overlay (its modes; the storage above serves the rest)
             info8[0] = SPMV_KERNEL_GTC;
             info8[1] = m.nrows + 2 * (int64_t)m.gtc_nce + 8 * (int64_t)m.gtc_ntab;
         }
@@ -725,6 +728,7 @@ amg_status amg_multigrid_set_option(amg_linop *mg, int32_t option, int64_t value
         case 1: m->sgs_residual_form = value != 0; break;
         case 2: m->fold_zero_guess = value != 0; break;
         case 3: m->fuse_transfers = value != 0; m->invalidate_graphs(); m->fuse_reset(); break;
+        case 4: m->restrict_df = value != 0; break;
         default: fail(AMG_ERR_INVALID, "unknown multigrid option");
         }
         m->invalidate_graphs();

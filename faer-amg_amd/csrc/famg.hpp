@@ -483,6 +483,9 @@ struct MultigridOp : LinOp {
     // grid levels: residual + restriction and interpolation + post-smoothing
     // Jacobi as one launch each (fuse.hip)
     bool fuse_transfers = g_fuse_transfers != 0;
+    // R on wide grid-transfer classes writes the next level's first Jacobi step
+    // from zero beside f_c (SPMV_SETDF) instead of a separate d*f pass
+    bool restrict_df = true;
     std::mutex mtx;
     Kind kind() const override { return Kind::Multigrid; }
     bool is_precond() const override { return true; }

@@ -638,7 +638,7 @@ void MultigridOp::cycle(int64_t l, double *v, const double *f, bool v_zero, doub
     // step from zero (d_c * f_c, what smooth() would compute first) into the
     // buffer that step writes: one launch and 24 n_c bytes fewer, same values
     bool df = false;
-    if (!fuse_pre && l + 2 < (int64_t)levels.size() && setdf_enabled()) {
+    if (!fuse_pre && l + 2 < (int64_t)levels.size() && restrict_df && setdf_enabled()) {
         auto *Rc = dynamic_cast<CsrOp *>(L.R.get());
         auto *Ac = dynamic_cast<CsrOp *>(C.A.get());
         auto *Dc = dynamic_cast<DiagOp *>(C.S.get());

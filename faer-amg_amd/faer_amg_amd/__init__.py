@@ -634,6 +634,11 @@ class Multigrid(LinOp):
                                               ptr(x), ptr(out), C.byref(ok)))
         return bool(ok.value)
 
+    def set_restrict_df(self, enable):
+        """R on wide grid-transfer classes also writes the next level's first Jacobi step
+        from zero (SPMV_SETDF; default on; bitwise the separate d*f pass)."""
+        _ck(_lib.amg_multigrid_set_option(self.h, 4, 1 if enable else 0))
+
     def set_fuse_transfers(self, enable):
         """Grid levels: residual + restriction and interpolation + post-smoothing Jacobi
         as one launch each (fuse.hip; default off, FAMG_FUSE=1 turns it on for new multigrids)."""

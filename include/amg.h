@@ -293,7 +293,10 @@ amg_status amg_multigrid_set_graph(amg_linop *mg, int32_t enable);
  * next level is its 2x2x2-box grid, the residual and the restriction run as
  * one launch (fuse_resid_restrict), and the interpolation with one Jacobi
  * post-smoothing step as another (fuse_interp_jacobi); R and P are read as
- * grid-transfer classes (8-bit class per row).  Bitwise identical. */
+ * grid-transfer classes (8-bit class per row).  Bitwise identical.  4 = a
+ * restriction stored as wide grid-transfer classes (gtx.hip) also writes the
+ * next level's first Jacobi step from zero, d_c f_c, beside f_c (SPMV_SETDF)
+ * instead of a separate pass (default 1; bitwise identical). */
 amg_status amg_multigrid_set_option(amg_linop *mg, int32_t option, int64_t value);
 /* One fused grid transfer of level l on device vectors (test hook; *applied = 0
  * when the level has none): which 0 -- out (coarse) = R (a - A x), x = the

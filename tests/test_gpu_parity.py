@@ -1356,6 +1356,50 @@ def test_grid_transfer_classes(ctx, gen, dims):
     assert np.linalg.norm(z - zref) <= 1e-11 * np.linalg.norm(zref)
 
 
+@pytest.mark.parametrize("gen,dims", [("7pt", (64, 48, 40)), ("27pt", (40, 36, 33)), ("7pt", (45, 37, 29))])
+def test_wide_grid_transfer_classes(ctx, gen, dims):
+    """gtx.hip: R and P of the box levels the 8-bit classes cannot take (levels
+    >= 1: thousands of classes, steps up to {-5,..,6}^3) as 16-bit classes over a
+    global dictionary of (window offset, value) entries: y = P v_c, y += P v_c
+    and f_c = R r bitwise equal to the oracle's row sums on every such level,
+    odd extents included.  The restriction's SETDF epilogue (f_c and the next
+    level's first Jacobi step d f_c in one launch) leaves the V-cycle bitwise
+    the one with the separate d*f pass, and within 1e-11 of the oracle."""
+    A = (fa().SparseMatOp.laplace3d_7pt(ctx, *dims) if gen == "7pt"
+         else fa().SparseMatOp.aniso27(ctx, *dims, 1.0, 1.0, 0.01))
+    mg = fa().sa_build_box(A, dims, (2, 2, 2), coarsest_dim=60)
+    seen = set()
+    rng = np.random.default_rng(4)
+    for l in range(mg.levels() - 1):
+        _, _, R, P = mg.level(l)
+        for w, M in (("R", R), ("P", P)):
+            if M.spmv_info()["gtc_kind"] != "gtx":
+                continue
+            seen.add((l, w))
+            OM = O.Csr.from_arrays(*M.dims(), *M.arrays())
+            m, n = M.dims()
+            x, y0 = rng.standard_normal(n), rng.standard_normal(m)
+            assert np.array_equal(apply_dev(ctx, M, x, m), OM.spmv(x)), (l, w)
+            if w == "P":
+                yd = T(y0)
+                M.spmv_epilogue("add", T(x), yd)
+                assert np.array_equal(H(yd), y0 + OM.spmv(x)), (l, w)
+    assert (1, "R") in seen and (1, "P") in seen, seen
+    b = np.random.default_rng(43).uniform(-1, 1, A.nrows)
+    plan = mg.cycle_plan()
+    assert any(p["mode"] == "SETDF" for p in plan), [(p["level"], p["name"], p["mode"]) for p in plan]
+    z = apply_dev(ctx, mg, b, A.nrows)
+    mg.set_restrict_df(False)
+    z0 = apply_dev(ctx, mg, b, A.nrows)
+    plan0 = mg.cycle_plan()
+    mg.set_restrict_df(True)
+    assert not any(p["mode"] == "SETDF" for p in plan0)
+    assert len(plan0) > len(plan)  # the d*f passes the SETDF epilogue absorbed
+    assert np.array_equal(z.view(np.int64), z0.view(np.int64))
+    zref = O.Multigrid(oracle_levels_from_gpu(mg, "jacobi")).apply(b)
+    assert np.linalg.norm(z - zref) <= 1e-11 * np.linalg.norm(zref)
+
+
 def test_constant_diagonal_epilogues_bitwise(ctx):
     """The 7-point Laplacian's Jacobi diagonal is one value (a_ii = 6): the DIA
     JACOBI / folded RESID0 epilogues and the grid-transfer ADD0 read it as one
