@@ -79,40 +79,49 @@ __device__ __forceinline__ void gtx_stage(const GtxArgs &a, double *win, int wx0
     }
 }
 
-// The row's sum over its class's entries in stored order.  uni: the wave's
-// rows share class cu (dictionary through scalar loads).
-__device__ __forceinline__ double gtx_row(const GtxArgs &a, const double *win, int base, int c, bool uni, int cu) {
+// Row sums over a class's entries in stored order (fma, ascending columns).
+// gtx_rows_u: NB rows of one wave-uniform class cu -- each entry (offset, value)
+// is one scalar load shared by the NB rows, which run NB independent fma chains.
+// gtx_row_v: one row of a per-lane class (vector loads; boundary waves).
+template <int NB>
+__device__ __forceinline__ void gtx_rows_u(const GtxArgs &a, const double *win, const int *base, int cu,
+                                           double *acc) {
+    const int e0 = a.dptr[cu], n = a.dlen[cu];
+#pragma unroll
+    for (int r = 0; r < NB; r++) acc[r] = 0.0;
+    for (int k = 0; k < n; k += 4) {
+        int o[4];
+        double v[4], w[NB][4];
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            o[u] = a.doff[e0 + k + u];
+            v[u] = a.dval[e0 + k + u];
+        }
+#pragma unroll
+        for (int r = 0; r < NB; r++)
+#pragma unroll
+            for (int u = 0; u < 4; u++) w[r][u] = win[base[r] + o[u]];
+#pragma unroll
+        for (int r = 0; r < NB; r++)
+#pragma unroll
+            for (int u = 0; u < 4; u++) acc[r] = fma(v[u], w[r][u], acc[r]);
+    }
+}
+
+__device__ __forceinline__ double gtx_row_v(const GtxArgs &a, const double *win, int base, int e0, int n) {
     double acc = 0.0;
-    if (uni) {
-        const int e0 = a.dptr[cu], n = a.dlen[cu];
-        for (int k = 0; k < n; k += 4) {
-            int o[4];
-            double v[4], w[4];
+    for (int k = 0; k < n; k += 4) {
+        int o[4];
+        double v[4], w[4];
 #pragma unroll
-            for (int u = 0; u < 4; u++) {
-                o[u] = a.doff[e0 + k + u];
-                v[u] = a.dval[e0 + k + u];
-            }
-#pragma unroll
-            for (int u = 0; u < 4; u++) w[u] = win[base + o[u]];
-#pragma unroll
-            for (int u = 0; u < 4; u++) acc = fma(v[u], w[u], acc);
+        for (int u = 0; u < 4; u++) {
+            o[u] = a.doff[e0 + k + u];
+            v[u] = a.dval[e0 + k + u];
         }
-    } else {
-        const int e0 = a.dptr[c], n = a.dlen[c];
-        for (int k = 0; k < n; k += 4) {
-            int o[4];
-            double v[4], w[4];
 #pragma unroll
-            for (int u = 0; u < 4; u++) {
-                o[u] = a.doff[e0 + k + u];
-                v[u] = a.dval[e0 + k + u];
-            }
+        for (int u = 0; u < 4; u++) w[u] = win[base + o[u]];
 #pragma unroll
-            for (int u = 0; u < 4; u++) w[u] = win[base + o[u]];
-#pragma unroll
-            for (int u = 0; u < 4; u++) acc = fma(v[u], w[u], acc);
-        }
+        for (int u = 0; u < 4; u++) acc = fma(v[u], w[u], acc);
     }
     return acc;
 }
@@ -157,20 +166,51 @@ __global__ __launch_bounds__(256) void k_gtx_interp(GtxArgs a) {
             }
         }
     }
-    gtx_stage(a, win, (x0 >> 1) + a.lox, (y0 >> 1) + a.loy, az0 + a.loz);
-    __syncthreads();
+    // per-lane dictionary ranges (boundary waves), loaded under the staging
+    int e0[TZ], en[TZ];
 #pragma unroll
     for (int j = 0; j < TZ; j++) {
-        const int cu = __builtin_amdgcn_readfirstlane(cl[j]);
-        const bool uni = cu >= 0 && __all(cl[j] == cu);
+        e0[j] = live[j] ? a.dptr[cl[j]] : 0;
+        en[j] = live[j] ? a.dlen[cl[j]] : 0;
+    }
+    gtx_stage(a, win, (x0 >> 1) + a.lox, (y0 >> 1) + a.loy, az0 + a.loz);
+    __syncthreads();
+    int base[TZ];
+#pragma unroll
+    for (int j = 0; j < TZ; j++) base[j] = ((j >> 1) * a.wy + (ly >> 1)) * a.wx + (lx >> 1);
+    double acc[TZ];
+    // planes j and j + 2 share their z parity, hence (inside the grid) their class
+#pragma unroll
+    for (int j0 = 0; j0 < (TZ == 4 ? 2 : TZ); j0++) {
+        constexpr int NB = TZ == 4 ? 2 : 1;
+        const int cu = __builtin_amdgcn_readfirstlane(cl[j0]);
+        bool uni = cu >= 0;
+#pragma unroll
+        for (int r = 0; r < NB; r++) uni = uni && __all(cl[j0 + 2 * r] == cu);
+        if (uni) {
+            int bs[NB];
+            double ac[NB];
+#pragma unroll
+            for (int r = 0; r < NB; r++) bs[r] = base[j0 + 2 * r];
+            gtx_rows_u<NB>(a, win, bs, cu, ac);
+#pragma unroll
+            for (int r = 0; r < NB; r++) acc[j0 + 2 * r] = ac[r];
+        } else {
+#pragma unroll
+            for (int r = 0; r < NB; r++) {
+                const int j = j0 + 2 * r;
+                acc[j] = live[j] ? gtx_row_v(a, win, base[j], e0[j], en[j]) : 0.0;
+            }
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < TZ; j++) {
         if (!live[j]) continue;
         if constexpr (MODE == SPMV_ADD0)
             if (a.dc && !a.dconst) yb[j] = sdt[dci[j]] * yb[j];
-        const int base = (((j + (a.rz0 + z0 & 1)) >> 1) * a.wy + (ly >> 1)) * a.wx + (lx >> 1);
-        const double acc = gtx_row(a, win, base, cl[j], uni, cu);
         const int64_t i = (int64_t)(z0 + j) * fplane + (int64_t)gy * a.rx + gx;
-        if constexpr (MODE == SPMV_SET) a.y[i] = acc;
-        else a.y[i] = yb[j] + acc;  // ADD, ADD0
+        if constexpr (MODE == SPMV_SET) a.y[i] = acc[j];
+        else a.y[i] = yb[j] + acc[j];  // ADD, ADD0
     }
 }
 
@@ -201,18 +241,32 @@ __global__ __launch_bounds__(256) void k_gtx_restrict(GtxArgs a) {
         cl[j] = live[j] ? (int)a.cls[J[j]] : -1;
         base[j] = ((2 * lz) * a.wy + 2 * ly) * a.wx + 2 * lx;
     }
-    gtx_stage(a, win, 2 * X0 + a.lox, 2 * Y0 + a.loy, 2 * (a.rz0 + Z0) - a.kz0 + a.loz);
-    __syncthreads();
+    int e0[RL], en[RL];
 #pragma unroll
     for (int j = 0; j < RL; j++) {
-        const int cu = __builtin_amdgcn_readfirstlane(cl[j]);
-        const bool uni = cu >= 0 && __all(cl[j] == cu);
+        e0[j] = live[j] ? a.dptr[cl[j]] : 0;
+        en[j] = live[j] ? a.dlen[cl[j]] : 0;
+    }
+    gtx_stage(a, win, 2 * X0 + a.lox, 2 * Y0 + a.loy, 2 * (a.rz0 + Z0) - a.kz0 + a.loz);
+    __syncthreads();
+    double acc[RL];
+    const int cu = __builtin_amdgcn_readfirstlane(cl[0]);
+    bool uni = cu >= 0;
+#pragma unroll
+    for (int j = 0; j < RL; j++) uni = uni && __all(cl[j] == cu);
+    if (uni) {  // interior waves: one class for all their rows
+        gtx_rows_u<RL>(a, win, base, cu, acc);
+    } else {
+#pragma unroll
+        for (int j = 0; j < RL; j++) acc[j] = live[j] ? gtx_row_v(a, win, base[j], e0[j], en[j]) : 0.0;
+    }
+#pragma unroll
+    for (int j = 0; j < RL; j++) {
         if (!live[j]) continue;
-        const double acc = gtx_row(a, win, base[j], cl[j], uni, cu);
-        a.y[J[j]] = acc;
+        a.y[J[j]] = acc[j];
         if constexpr (MODE == SPMV_SETDF) {
             const double dd = a.dconst ? a.dk : a.dc ? sdt[a.dc[J[j]]] : a.d[J[j]];
-            a.y2[J[j]] = dd * acc;  // vec_mul(_coded)'s product
+            a.y2[J[j]] = dd * acc[j];  // vec_mul(_coded)'s product
         }
     }
 }
@@ -237,6 +291,39 @@ int gtx_mode() {
         return e ? atoi(e) : 1;
     }();
     return v;
+}
+
+// flag FLAG_GTX_TIME (FAMG_GTX_TIME=0, amg_set_flag(3, 0)): keep the classes
+// without timing them against the storage underneath
+static bool gtx_time_enabled() { return flag(FLAG_GTX_TIME) != 0; }
+
+static bool gtx_beats_storage(GpuCsr &m) {
+    if (!gtx_time_enabled() || gtx_mode() == 2) return true;
+    hipStream_t s = m.ctx->stream;
+    DevBuf<double> x(m.ncols), y(m.nrows), y2(m.nrows);
+    FAMG_CHECK_HIP(hipMemsetAsync(x.get(), 0, m.ncols * sizeof(double), s));
+    FAMG_CHECK_HIP(hipMemsetAsync(y.get(), 0, m.nrows * sizeof(double), s));
+    hipEvent_t e0, e1;
+    FAMG_CHECK_HIP(hipEventCreate(&e0));
+    FAMG_CHECK_HIP(hipEventCreate(&e1));
+    float ms[2] = {0.f, 0.f};
+    for (int k = 0; k < 2; k++) {
+        m.gtx_on = k == 1;
+        auto run = [&] {
+            spmv(m, x.get(), y.get(), SPMV_SET, SpmvEpi{}, s);
+            if (m.gtx_r && k == 0) vec_mul(y2.get(), y.get(), y.get(), m.nrows, s);  // the d*f pass SETDF saves
+        };
+        run();
+        FAMG_CHECK_HIP(hipEventRecord(e0, s));
+        for (int r = 0; r < 5; r++) run();
+        FAMG_CHECK_HIP(hipEventRecord(e1, s));
+        FAMG_CHECK_HIP(hipEventSynchronize(e1));
+        FAMG_CHECK_HIP(hipEventElapsedTime(&ms[k], e0, e1));
+    }
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+    m.gtx_on = true;
+    return ms[1] < 0.9f * ms[0];  // a clear win only (launch-bound small levels time noisily)
 }
 
 bool gtx_attach(GpuCsr &m, const int64_t *fg, const int64_t *cg, int which) {
@@ -319,7 +406,8 @@ bool gtx_attach(GpuCsr &m, const int64_t *fg, const int64_t *cg, int which) {
             }
         }
     } else {
-        static const int cands[][3] = {{16, 8, 2}, {16, 8, 1}, {16, 4, 1}, {8, 4, 1}, {8, 2, 1}, {4, 2, 1}};
+        static const int cands[][3] = {{16, 8, 4}, {16, 4, 4}, {16, 8, 2}, {16, 8, 1}, {16, 4, 1},
+                                       {8, 4, 1},  {8, 2, 1},  {4, 2, 1}};
         for (const auto &c : cands) {
             const int w0 = 2 * c[0] - 1 + hi[0] - lo[0], w1 = 2 * c[1] - 1 + hi[1] - lo[1],
                       w2 = 2 * c[2] - 1 + hi[2] - lo[2];
@@ -421,6 +509,14 @@ bool gtx_attach(GpuCsr &m, const int64_t *fg, const int64_t *cg, int which) {
     }
     m.gtx_r = is_r;
     m.gtx_on = true;
+    // keep the classes only where they beat the storage underneath (timed on
+    // scratch vectors; R is charged with the d*f pass its SETDF epilogue saves):
+    // the small Galerkin levels' long rows (R_3: ~490 entries, P_4 from a 16^3
+    // grid: 8 tiles) run a lane per row and lose to the lanes-per-row kernels
+    if (!gtx_beats_storage(m)) {
+        gtx_release(m);
+        return false;
+    }
     return true;
 }
 

@@ -116,8 +116,11 @@ amg_status amg_set_alloc_policy(int32_t policy);
  * levels (default 0, env FAMG_FOLD_XSCS), 1 = read a constant coded Jacobi
  * diagonal as one scalar (default 1, env FAMG_DIA_DK), 2 = waves per row of the
  * wave-per-row kernel (0 auto = chosen per matrix at finalize, 1/2/4; env
- * FAMG_VEC_WPR).  Setting one makes every multigrid re-capture its hipGraph at
- * its next apply.  amg_get_flag reads the current value. */
+ * FAMG_VEC_WPR), 3 = time the wide grid-transfer classes (gtx.hip) against a
+ * transfer operator's other storage at setup and keep them only where they win
+ * (default 1, env FAMG_GTX_TIME; 0 keeps them wherever they build).  Setting one
+ * makes every multigrid re-capture its hipGraph at its next apply.  amg_get_flag
+ * reads the current value. */
 amg_status amg_set_flag(int32_t which, int64_t value);
 amg_status amg_get_flag(int32_t which, int64_t *value);
 /* Stencil-class storage of a CSR operator (structured Galerkin operators whose
