@@ -299,7 +299,7 @@ amg_status amg_csr_spmv_info(const amg_linop *op, int64_t *info8) {
         }
         if (m.gtx_on) {  // the wide grid-transfer overlay (gtx.hip; served first)
             info8[0] = SPMV_KERNEL_GTC;
-            info8[1] = 2 * m.nrows + 10 * m.gtx_nent + 8 * m.gtx_nclass;
+            info8[1] = 2 * m.nrows + 12 * m.gtx_nent + 8 * m.gtx_nclass;
         } else if (m.gtc_on) {  // the grid-transfer overlay (its modes; the storage above serves the rest)
             info8[0] = SPMV_KERNEL_GTC;
             info8[1] = m.nrows + 2 * (int64_t)m.gtc_nce + 8 * (int64_t)m.gtc_ntab;

@@ -160,8 +160,8 @@ struct GpuCsr {
     // wide grid-transfer classes (gtx.hip): 16-bit class per row, dictionary of
     // (window offset, fp64 value) entries in global memory -- every box level
     bool gtx_on = false, gtx_r = false, gtx_tried = false;
-    DevBuf<uint16_t> gtx_cls, gtx_doff;
-    DevBuf<int32_t> gtx_dptr, gtx_dlen;
+    DevBuf<uint16_t> gtx_cls;
+    DevBuf<int32_t> gtx_dptr, gtx_dlen, gtx_doff;
     DevBuf<double> gtx_dval;
     int64_t gtx_nclass = 0, gtx_nent = 0;
     int gtx_tile[3] = {0, 0, 0}, gtx_win[3] = {0, 0, 0}, gtx_lo[3] = {0, 0, 0};

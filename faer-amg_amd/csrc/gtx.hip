@@ -11,7 +11,7 @@
 // {-5,..,6}^3 and 35428 values).  Here:
 //   * one 16-bit class id per row (2 B / row instead of 10-16 B of value-code
 //     SELL), the dictionary in global memory (L2-resident: <= 1 MB);
-//   * a dictionary entry is (uint16 window offset, fp64 value): the offset is
+//   * a dictionary entry is (int32 window offset, fp64 value): the offset is
 //     precomputed for the kernel's window at setup, so a term is one LDS read
 //     at row base + offset -- no slot -> lookup -> window chain;
 //   * waves cover points of one parity class (P: a wave holds x = px + 2i,
@@ -35,7 +35,7 @@ struct GtxArgs {
     const uint16_t *cls;    // class id per row
     const int32_t *dptr;    // per class: first dictionary entry
     const int32_t *dlen;    // per class: entries (a multiple of 4)
-    const uint16_t *doff;   // per entry: window offset from the row's base
+    const int32_t *doff;    // per entry: window offset from the row's base (32-bit: scalar loads)
     const double *dval;     // per entry: value
     int rx, ry, rz;         // row grid (rz: owned row planes)
     int kx, ky, kz;         // column grid (kz: owned column planes)
@@ -470,14 +470,14 @@ bool gtx_attach(GpuCsr &m, const int64_t *fg, const int64_t *cg, int which) {
     // a multiple of 4 with +0.0 at offset 0 (a +0.0 term leaves the sum unchanged)
     const int64_t C = (int64_t)rep.size();
     std::vector<int32_t> dptr(C), dlen(C);
-    std::vector<uint16_t> doff;
+    std::vector<int32_t> doff;
     std::vector<double> dval;
     for (int64_t c = 0; c < C; c++) {
         const int64_t i = rep[c];
         dptr[c] = (int32_t)doff.size();
         for (int64_t e = rp[i]; e < rp[i + 1]; e++) {
             const int off = ((st[3 * e + 2] - lo[2]) * wdim[1] + (st[3 * e + 1] - lo[1])) * wdim[0] + (st[3 * e] - lo[0]);
-            doff.push_back((uint16_t)off);
+            doff.push_back(off);
             dval.push_back(val[e]);
         }
         while ((doff.size() - dptr[c]) % 4) {
@@ -495,7 +495,7 @@ bool gtx_attach(GpuCsr &m, const int64_t *fg, const int64_t *cg, int which) {
     FAMG_CHECK_HIP(hipMemcpyAsync(m.gtx_cls.get(), cls.data(), n * 2, hipMemcpyHostToDevice, s));
     FAMG_CHECK_HIP(hipMemcpyAsync(m.gtx_dptr.get(), dptr.data(), C * 4, hipMemcpyHostToDevice, s));
     FAMG_CHECK_HIP(hipMemcpyAsync(m.gtx_dlen.get(), dlen.data(), C * 4, hipMemcpyHostToDevice, s));
-    FAMG_CHECK_HIP(hipMemcpyAsync(m.gtx_doff.get(), doff.data(), doff.size() * 2, hipMemcpyHostToDevice, s));
+    FAMG_CHECK_HIP(hipMemcpyAsync(m.gtx_doff.get(), doff.data(), doff.size() * 4, hipMemcpyHostToDevice, s));
     FAMG_CHECK_HIP(hipMemcpyAsync(m.gtx_dval.get(), dval.data(), dval.size() * 8, hipMemcpyHostToDevice, s));
     FAMG_CHECK_HIP(hipStreamSynchronize(s));
     m.gtx_nclass = C;

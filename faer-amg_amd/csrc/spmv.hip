@@ -2452,7 +2452,7 @@ static void log_spmv(const GpuCsr &m, SpmvMode mode, const SpmvEpi &epi, int64_t
     if (m.gtx_on && (seg < 0 || m.rframe.on()) && gtx_supports(m, mode)) {
         kernel = SPMV_KERNEL_GTC;
         name = "gtx";
-        mat = 2 * part(m.nrows) + 10 * m.gtx_nent + 8 * m.gtx_nclass;
+        mat = 2 * part(m.nrows) + 12 * m.gtx_nent + 8 * m.gtx_nclass;
     } else if (m.gtc_on && (seg < 0 || m.rframe.on()) && gtc_supports(m, mode)) {
         kernel = SPMV_KERNEL_GTC;
         name = "gtc";
