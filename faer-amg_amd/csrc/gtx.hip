@@ -31,6 +31,11 @@
 
 namespace famg {
 
+struct GtxArgs;
+// class peeling on mixed waves (scalar walks per distinct class) measured far slower than per-lane
+// dictionary loads: a boundary wave of the small Galerkin levels holds dozens of classes
+__device__ __forceinline__ constexpr bool gtx_peel() { return false; }
+
 struct GtxArgs {
     const uint16_t *cls;    // class id per row
     const int32_t *dptr;    // per class: first dictionary entry
@@ -57,11 +62,13 @@ struct GtxArgs {
 };
 
 // stage the column window [w0, w0 + w) into LDS (0.0 outside the grid / the
-// loadable planes), all of a lane's loads issued before its stores
+// loadable planes): every load of a lane issued before its stores -- PF is
+// chosen per matrix so one round covers the window (a round per memory latency
+// is what the staging costs; the gtc kernels' compile-time windows do the same)
+template <int PF>
 __device__ __forceinline__ void gtx_stage(const GtxArgs &a, double *win, int wx0, int wy0, int wz0) {
     const int W = a.wx * a.wy * a.wz;
     const int64_t cplane = (int64_t)a.kx * a.ky;
-    constexpr int PF = 8;
     for (int q0 = threadIdx.x; q0 < W; q0 += 256 * PF) {
         double v[PF];
 #pragma unroll
@@ -108,6 +115,28 @@ __device__ __forceinline__ void gtx_rows_u(const GtxArgs &a, const double *win, 
     }
 }
 
+// A row of a wave whose rows mix classes (boundary tiles): the wave peels
+// its classes one at a time -- the first pending lane's class cu is walked
+// with scalar dictionary loads by every lane of that class -- so boundary waves
+// also read the dictionary from SGPRs, once per distinct class.
+__device__ __forceinline__ double gtx_row_peel(const GtxArgs &a, const double *win, int base, int c, bool live) {
+    double acc = 0.0;
+    bool pending = live;
+    while (__any(pending)) {
+        if (pending) {
+            const int cu = __builtin_amdgcn_readfirstlane(c);
+            if (c == cu) {
+                double r[1];
+                const int b[1] = {base};
+                gtx_rows_u<1>(a, win, b, cu, r);
+                acc = r[0];
+                pending = false;
+            }
+        }
+    }
+    return acc;
+}
+
 __device__ __forceinline__ double gtx_row_v(const GtxArgs &a, const double *win, int base, int e0, int n) {
     double acc = 0.0;
     for (int k = 0; k < n; k += 4) {
@@ -130,7 +159,7 @@ __device__ __forceinline__ double gtx_row_v(const GtxArgs &a, const double *win,
 // y parity wv >> 1: lane l is the point (px + 2 (l & 15), py + 2 (l >> 4)),
 // and each lane walks TZ planes -- every wave of an interior tile is one class
 // per plane.
-template <int MODE, int TZ>
+template <int MODE, int TZ, int PF>
 __global__ __launch_bounds__(256) void k_gtx_interp(GtxArgs a) {
     extern __shared__ double win[];
     __shared__ double sdt[256];
@@ -173,7 +202,7 @@ __global__ __launch_bounds__(256) void k_gtx_interp(GtxArgs a) {
         e0[j] = live[j] ? a.dptr[cl[j]] : 0;
         en[j] = live[j] ? a.dlen[cl[j]] : 0;
     }
-    gtx_stage(a, win, (x0 >> 1) + a.lox, (y0 >> 1) + a.loy, az0 + a.loz);
+    gtx_stage<PF>(a, win, (x0 >> 1) + a.lox, (y0 >> 1) + a.loy, az0 + a.loz);
     __syncthreads();
     int base[TZ];
 #pragma unroll
@@ -199,7 +228,8 @@ __global__ __launch_bounds__(256) void k_gtx_interp(GtxArgs a) {
 #pragma unroll
             for (int r = 0; r < NB; r++) {
                 const int j = j0 + 2 * r;
-                acc[j] = live[j] ? gtx_row_v(a, win, base[j], e0[j], en[j]) : 0.0;
+                acc[j] = gtx_peel() ? gtx_row_peel(a, win, base[j], cl[j], live[j])
+                                    : (live[j] ? gtx_row_v(a, win, base[j], e0[j], en[j]) : 0.0);
             }
         }
     }
@@ -216,7 +246,7 @@ __global__ __launch_bounds__(256) void k_gtx_interp(GtxArgs a) {
 
 // R r over a coarse tile of tx x ty x tz rows (RL rows per lane); SETDF also
 // writes y2 = d * y (the next level's first Jacobi step from zero).
-template <int MODE, int RL>
+template <int MODE, int RL, int PF>
 __global__ __launch_bounds__(256) void k_gtx_restrict(GtxArgs a) {
     extern __shared__ double win[];
     __shared__ double sdt[256];
@@ -247,7 +277,7 @@ __global__ __launch_bounds__(256) void k_gtx_restrict(GtxArgs a) {
         e0[j] = live[j] ? a.dptr[cl[j]] : 0;
         en[j] = live[j] ? a.dlen[cl[j]] : 0;
     }
-    gtx_stage(a, win, 2 * X0 + a.lox, 2 * Y0 + a.loy, 2 * (a.rz0 + Z0) - a.kz0 + a.loz);
+    gtx_stage<PF>(a, win, 2 * X0 + a.lox, 2 * Y0 + a.loy, 2 * (a.rz0 + Z0) - a.kz0 + a.loz);
     __syncthreads();
     double acc[RL];
     const int cu = __builtin_amdgcn_readfirstlane(cl[0]);
@@ -258,7 +288,9 @@ __global__ __launch_bounds__(256) void k_gtx_restrict(GtxArgs a) {
         gtx_rows_u<RL>(a, win, base, cu, acc);
     } else {
 #pragma unroll
-        for (int j = 0; j < RL; j++) acc[j] = live[j] ? gtx_row_v(a, win, base[j], e0[j], en[j]) : 0.0;
+        for (int j = 0; j < RL; j++)
+            acc[j] = gtx_peel() ? gtx_row_peel(a, win, base[j], cl[j], live[j])
+                                : (live[j] ? gtx_row_v(a, win, base[j], e0[j], en[j]) : 0.0);
     }
 #pragma unroll
     for (int j = 0; j < RL; j++) {
@@ -299,6 +331,9 @@ static bool gtx_time_enabled() { return flag(FLAG_GTX_TIME) != 0; }
 
 static bool gtx_beats_storage(GpuCsr &m) {
     if (!gtx_time_enabled() || gtx_mode() == 2) return true;
+    // R of the small levels (<= 65536 coarse rows of hundreds of entries) loses in the cycle
+    // even where an isolated timing has it ahead (R_2 of the 256^3 cycle: 32.5 vs 21.9 + 4.6 us)
+    if (m.gtx_r && m.nrows <= 65536) return false;
     hipStream_t s = m.ctx->stream;
     DevBuf<double> x(m.ncols), y(m.nrows), y2(m.nrows);
     FAMG_CHECK_HIP(hipMemsetAsync(x.get(), 0, m.ncols * sizeof(double), s));
@@ -590,28 +625,40 @@ void spmv_gtx(const GpuCsr &m, const double *x, double *y, SpmvMode mode, const 
         const dim3 grid((unsigned)((int64_t)a.ntx * a.nty * (z1 - z0))), block(256);
         const int T = a.tx * a.ty * a.tz;
         const int rl = T <= 256 ? 1 : 2;
+        const int W = a.wx * a.wy * a.wz, pf = W <= 256 * 8 ? 8 : W <= 256 * 16 ? 16 : 32;
+#define FAMG_GTXR2(M, PF)                                                                          \
+    if (rl == 1) k_gtx_restrict<M, 1, PF><<<grid, block, lds, s>>>(a);                             \
+    else k_gtx_restrict<M, 2, PF><<<grid, block, lds, s>>>(a);
 #define FAMG_GTXR(M)                                                                               \
-    if (rl == 1) k_gtx_restrict<M, 1><<<grid, block, lds, s>>>(a);                                 \
-    else k_gtx_restrict<M, 2><<<grid, block, lds, s>>>(a);
+    if (pf == 8) { FAMG_GTXR2(M, 8) }                                                              \
+    else if (pf == 16) { FAMG_GTXR2(M, 16) }                                                       \
+    else { FAMG_GTXR2(M, 32) }
         if (mode == SPMV_SETDF) { FAMG_GTXR(SPMV_SETDF) }
         else { FAMG_GTXR(SPMV_SET) }
 #undef FAMG_GTXR
+#undef FAMG_GTXR2
     } else {
         gtx_tiles(ntz, seg, a.wz, a.kz, a.kz_lo, a.kz_hi,
                   [&](int t) { return ((a.rz0 + t * a.tz) >> 1) - a.kz0 + a.loz; }, z0, z1);
         if (z1 <= z0) return;
         a.tile0 = a.ntx * a.nty * z0;
         const dim3 grid((unsigned)((int64_t)a.ntx * a.nty * (z1 - z0))), block(256);
-#define FAMG_GTXP(TZ)                                                                              \
+        const int W = a.wx * a.wy * a.wz, pf = W <= 256 * 4 ? 4 : W <= 256 * 8 ? 8 : 16;
+#define FAMG_GTXP2(TZ, PF)                                                                         \
     switch (mode) {                                                                                \
-    case SPMV_SET: k_gtx_interp<SPMV_SET, TZ><<<grid, block, lds, s>>>(a); break;                  \
-    case SPMV_ADD: k_gtx_interp<SPMV_ADD, TZ><<<grid, block, lds, s>>>(a); break;                  \
-    case SPMV_ADD0: k_gtx_interp<SPMV_ADD0, TZ><<<grid, block, lds, s>>>(a); break;                \
+    case SPMV_SET: k_gtx_interp<SPMV_SET, TZ, PF><<<grid, block, lds, s>>>(a); break;              \
+    case SPMV_ADD: k_gtx_interp<SPMV_ADD, TZ, PF><<<grid, block, lds, s>>>(a); break;              \
+    case SPMV_ADD0: k_gtx_interp<SPMV_ADD0, TZ, PF><<<grid, block, lds, s>>>(a); break;            \
     default: break;                                                                                \
     }
+#define FAMG_GTXP(TZ)                                                                              \
+    if (pf == 4) { FAMG_GTXP2(TZ, 4) }                                                             \
+    else if (pf == 8) { FAMG_GTXP2(TZ, 8) }                                                        \
+    else { FAMG_GTXP2(TZ, 16) }
         if (a.tz == 4) { FAMG_GTXP(4) }
         else { FAMG_GTXP(2) }
 #undef FAMG_GTXP
+#undef FAMG_GTXP2
     }
     FAMG_CHECK_HIP(hipGetLastError());
 }
