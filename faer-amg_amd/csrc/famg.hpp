@@ -148,12 +148,6 @@ struct GpuCsr {
     int xscs_t[3] = {0, 0, 0}, xscs_r[3] = {0, 0, 0};
     DevBuf<int32_t> xscs_lo;
     std::vector<int> xscs_steps;  // (dx, dy, dz) of each of the scs_k offsets
-    // x-run variant (spmv_xscs_run_kernel): each lane sums xscs_rx consecutive x
-    // rows; the offsets walked as chunks of <= 4 consecutive window positions
-    // (x runs of the stencil), each chunk's window values loaded once for all rows
-    int xscs_rx = 0;                 // 0: the one-row-per-lane kernel
-    DevBuf<int32_t> xscs_chunks;     // per chunk: window offset | length << 24
-    int xscs_nchunks = 0;
     // grid-transfer classes (gtc.hip) for R/P of a 2x2x2-box hierarchy: an overlay
     // on the finalized storage used for the modes it supports (gtc_supports)
     bool gtc_on = false, gtc_r = false;

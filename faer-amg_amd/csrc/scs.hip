@@ -341,122 +341,6 @@ __global__ __launch_bounds__(256) void spmv_xscs_kernel(XscsArgs a) {
     }
 }
 
-// x-staged stencil classes, RX consecutive x rows per lane (the x-run variant):
-// the K offsets walked as chunks of <= 4 consecutive window positions (the
-// stencil's x runs: 25 runs of 5 for a 125-point stencil), a chunk's RX + 3
-// window values read once for the lane's RX rows -- (RX + 3) / (4 RX) of the
-// LDS reads of one row per lane, and on class-uniform waves one scalar
-// dictionary load per offset for all RX rows.  Each row still sums its K
-// offsets in ascending order (chunks in order, offsets within a chunk
-// ascending): bitwise spmv_xscs_kernel's sums.
-template <int MODE, int IB, int RX>
-__global__ __launch_bounds__(256) void spmv_xscs_run_kernel(XscsArgs a, const int32_t *chunks, int nchunks) {
-    extern __shared__ double win[];
-    const int tid = threadIdx.x;
-    const int t = a.tile0 + xcd_remap(blockIdx.x, gridDim.x);
-    const int tix = t % a.ntx, tiy = (t / a.ntx) % a.nty, tiz = t / (a.ntx * a.nty);
-    const int x0 = tix * a.tx, y0 = tiy * a.ty, z0 = tiz * a.tz;
-    const int tq = a.tx / RX, Q = tq * a.ty * a.tz;
-    const int64_t plane = (int64_t)a.nx * a.ny;
-    auto cls_of = [&](int64_t r) {
-        return IB == 1 ? (int)static_cast<const uint8_t *>(a.cls)[r] : (int)static_cast<const uint16_t *>(a.cls)[r];
-    };
-    const bool qlive = tid < Q;
-    const int qx = tid % tq, ly = (tid / tq) % a.ty, lz = tid / (tq * a.ty);
-    const int gy = y0 + ly, gz = z0 + lz;
-    int c[RX];
-    int64_t gi[RX];
-    bool live[RX];
-    double br[RX], xr[RX], dr[RX], yr[RX];
-#pragma unroll
-    for (int r = 0; r < RX; r++) {
-        const int gx = x0 + RX * qx + r;
-        live[r] = qlive && gx < a.nx && gy < a.ny && gz < a.nz;
-        gi[r] = live[r] ? (int64_t)gz * plane + (int64_t)gy * a.nx + gx
-                        : (int64_t)z0 * plane + (int64_t)y0 * a.nx + x0;  // the tile's first point
-        c[r] = cls_of(gi[r]);
-        br[r] = xr[r] = dr[r] = yr[r] = 0.0;
-        if (live[r]) {
-            if constexpr (MODE == SPMV_RESID || MODE == SPMV_RESID0) br[r] = a.b[gi[r]];
-            if constexpr (MODE == SPMV_ADD) yr[r] = a.y[gi[r]];
-            if constexpr (MODE == SPMV_JACOBI) {
-                xr[r] = a.x[gi[r]];
-                br[r] = a.b[gi[r]];
-                dr[r] = a.dc ? a.dt[a.dc[gi[r]]] : a.d[gi[r]];
-            }
-        }
-    }
-    const int wb = ((min(lz, a.tz - 1) + a.rz) * a.wy + min(ly, a.ty - 1) + a.ry) * a.wx + RX * min(qx, tq - 1) + a.rx;
-    // stage the window (as spmv_xscs_kernel)
-    const int W = a.wx * a.wy * a.wz;
-    constexpr int PF = 8;
-    for (int p0 = tid; p0 < W; p0 += 256 * PF) {
-        double v[PF];
-#pragma unroll
-        for (int u = 0; u < PF; u++) {
-            const int p = p0 + 256 * u;
-            const int px = p % a.wx, q = p / a.wx;
-            const int py = q % a.wy, pz = q / a.wy;
-            const int gx = x0 - a.rx + px, yy = y0 - a.ry + py, zz = z0 - a.rz + pz;
-            const bool in = p < W && (unsigned)gx < (unsigned)a.nx && (unsigned)yy < (unsigned)a.ny && zz >= a.zlo &&
-                            zz < a.zhi;
-            const int64_t g = (int64_t)zz * plane + (zz < 0 ? a.add_lo : zz >= a.nz ? a.add_hi : 0) +
-                              (int64_t)yy * a.nx + gx;
-            if constexpr (MODE == SPMV_RESID0) v[u] = in ? (a.dc ? a.dt[a.dc[g]] : a.d[g]) * a.x[g] : 0.0;
-            else v[u] = in ? a.x[g] : 0.0;
-        }
-#pragma unroll
-        for (int u = 0; u < PF; u++)
-            if (p0 + 256 * u < W) win[p0 + 256 * u] = v[u];
-    }
-    if (tid < 8) win[W + tid] = 0.0;  // a chunk of the tile's last quad may read up to RX + 2 past a row
-    __syncthreads();
-    bool uni = true;
-    const int cu = __builtin_amdgcn_readfirstlane(c[0]);
-#pragma unroll
-    for (int r = 0; r < RX; r++) uni = uni && __all(!live[r] || c[r] == cu);
-    double acc[RX];
-#pragma unroll
-    for (int r = 0; r < RX; r++) acc[r] = 0.0;
-    int k = 0;
-    for (int j = 0; j < nchunks; j++) {
-        const int32_t ch = chunks[j];  // wave-uniform: scalar load
-        const int lo = (ch & 0xffffff) - (1 << 20), len = ch >> 24;
-        double v[RX + 3];
-#pragma unroll
-        for (int i = 0; i < RX + 3; i++) v[i] = win[wb + lo + i];
-        double cf[RX][4];
-        if (uni) {
-#pragma unroll
-            for (int i = 0; i < 4; i++) {
-                const double w = i < len ? a.dict[(int64_t)cu * a.k + k + i] : 0.0;
-#pragma unroll
-                for (int r = 0; r < RX; r++) cf[r][i] = w;
-            }
-        } else {
-#pragma unroll
-            for (int r = 0; r < RX; r++)
-#pragma unroll
-                for (int i = 0; i < 4; i++) cf[r][i] = i < len ? a.dict[(int64_t)c[r] * a.k + k + i] : 0.0;
-        }
-#pragma unroll
-        for (int i = 0; i < 4; i++)
-            if (i < len)
-#pragma unroll
-                for (int r = 0; r < RX; r++) acc[r] = fma(cf[r][i], v[r + i], acc[r]);
-        k += len;
-    }
-#pragma unroll
-    for (int r = 0; r < RX; r++) {
-        if (!live[r]) continue;
-        const int64_t i = gi[r];
-        if constexpr (MODE == SPMV_SET) a.y[i] = acc[r];
-        else if constexpr (MODE == SPMV_ADD) a.y[i] = yr[r] + acc[r];
-        else if constexpr (MODE == SPMV_RESID || MODE == SPMV_RESID0) a.y[i] = br[r] - acc[r];
-        else a.y[i] = xr[r] + dr[r] * (br[r] - acc[r]);  // JACOBI
-    }
-}
-
 // the lanes-per-row kernel for row ranges of < SCS_LANES_ROWS rows with >= 256
 // offsets (A/B switch FAMG_SCS_LANES=0: no stencil classes for them)
 constexpr int64_t SCS_LANES_ROWS = 131072;
@@ -485,9 +369,6 @@ void scs_release(GpuCsr &m) {
     m.scs_lanes = false;
     m.xscs = false;
     m.xscs_lo.release();
-    m.xscs_rx = 0;
-    m.xscs_chunks.release();
-    m.xscs_nchunks = 0;
 }
 
 // A/B switch FAMG_XSCS=0: no x-staged stencil classes; FAMG_XSCS_TILE=tx,ty,tz
@@ -517,17 +398,6 @@ static void xscs_set_tile(GpuCsr &m, const int *t) {
         lo[k] = (m.xscs_steps[3 * k + 2] * wy + m.xscs_steps[3 * k + 1]) * wx + m.xscs_steps[3 * k];
     m.xscs_lo.resize(Kp);
     FAMG_CHECK_HIP(hipMemcpyAsync(m.xscs_lo.get(), lo.data(), Kp * 4, hipMemcpyHostToDevice, m.ctx->stream));
-    // x-run chunks: maximal runs of consecutive window positions, cut into <= 4
-    std::vector<int32_t> ch;
-    for (int k = 0; k < Kp;) {
-        int len = 1;
-        while (k + len < Kp && len < 4 && lo[k + len] == lo[k] + len) len++;
-        ch.push_back((int32_t)(((lo[k] + (1 << 20)) & 0xffffff) | (len << 24)));  // |lo| < 2^20
-        k += len;
-    }
-    m.xscs_chunks.resize(ch.size());
-    m.xscs_nchunks = (int)ch.size();
-    FAMG_CHECK_HIP(hipMemcpyAsync(m.xscs_chunks.get(), ch.data(), ch.size() * 4, hipMemcpyHostToDevice, m.ctx->stream));
     FAMG_CHECK_HIP(hipStreamSynchronize(m.ctx->stream));
     for (int q = 0; q < 3; q++) m.xscs_t[q] = t[q];
 }
@@ -681,12 +551,6 @@ static void spmv_xscs(const GpuCsr &m, const double *x, double *y, SpmvMode mode
 // stage with fewer, longer loads, but a tile whose waves straddle boundary
 // classes reads the dictionary per lane (profiles/r03/ab_xscs_*.log).  The
 // tile changes no result (same sums in the same order).
-// flag FLAG_XSCS_RUN (FAMG_XSCS_RUN, amg_set_flag(4, v)) for operators finalized
-// afterwards: 0 never the x-run variant, 1 (default) where it times faster, 2
-// wherever a tile allows it
-static int xscs_run_mode() { return (int)flag(FLAG_XSCS_RUN); }
-static bool xscs_run_enabled() { return xscs_run_mode() != 0; }
-
 static void xscs_autotune(GpuCsr &m) {
     if (getenv("FAMG_XSCS_TILE")) return;
     const int64_t nx = m.grid[0], ny = m.grid[1], nz = m.grid[2], n = m.nrows;
@@ -710,34 +574,25 @@ static void xscs_autotune(GpuCsr &m) {
     hipEvent_t e0, e1;
     FAMG_CHECK_HIP(hipEventCreate(&e0));
     FAMG_CHECK_HIP(hipEventCreate(&e1));
-    int best[3] = {m.xscs_t[0], m.xscs_t[1], m.xscs_t[2]}, best_rx = 0;
+    int best[3] = {m.xscs_t[0], m.xscs_t[1], m.xscs_t[2]};
     float best_ms = 1e30f;
     for (const auto &c : cands) {
         xscs_set_tile(m, c.data());
-        const int T = c[0] * c[1] * c[2];
-        for (int rx : {0, 4}) {
-            // the x-run variant: four x rows per lane, at least a wave of quads
-            if (rx && (!xscs_run_enabled() || c[0] % rx || T > 256 * rx || T < 64 * rx)) continue;
-            if (!rx && xscs_run_mode() == 2 && c[0] % 4 == 0 && T <= 1024 && T >= 256) continue;
-            m.xscs_rx = rx;
-            spmv_xscs(m, x.get(), y.get(), SPMV_SET, SpmvEpi{}, s);
-            FAMG_CHECK_HIP(hipEventRecord(e0, s));
-            for (int r = 0; r < 3; r++) spmv_xscs(m, x.get(), y.get(), SPMV_SET, SpmvEpi{}, s);
-            FAMG_CHECK_HIP(hipEventRecord(e1, s));
-            FAMG_CHECK_HIP(hipEventSynchronize(e1));
-            float ms = 0.f;
-            FAMG_CHECK_HIP(hipEventElapsedTime(&ms, e0, e1));
-            if (ms < best_ms) {
-                best_ms = ms;
-                best[0] = c[0]; best[1] = c[1]; best[2] = c[2];
-                best_rx = rx;
-            }
+        spmv_xscs(m, x.get(), y.get(), SPMV_SET, SpmvEpi{}, s);
+        FAMG_CHECK_HIP(hipEventRecord(e0, s));
+        for (int r = 0; r < 3; r++) spmv_xscs(m, x.get(), y.get(), SPMV_SET, SpmvEpi{}, s);
+        FAMG_CHECK_HIP(hipEventRecord(e1, s));
+        FAMG_CHECK_HIP(hipEventSynchronize(e1));
+        float ms = 0.f;
+        FAMG_CHECK_HIP(hipEventElapsedTime(&ms, e0, e1));
+        if (ms < best_ms) {
+            best_ms = ms;
+            best[0] = c[0]; best[1] = c[1]; best[2] = c[2];
         }
     }
     (void)hipEventDestroy(e0);
     (void)hipEventDestroy(e1);
     xscs_set_tile(m, best);
-    m.xscs_rx = best_rx;
 }
 
 bool build_scs(GpuCsr &m, const std::vector<int64_t> &rp, int64_t other_bytes) {
@@ -918,27 +773,8 @@ static void spmv_xscs(const GpuCsr &m, const double *x, double *y, SpmvMode mode
     a.x = x; a.y = y; a.b = epi.b; a.d = epi.d; a.dc = epi.dc; a.dt = epi.dt;
     const int T = a.tx * a.ty * a.tz;
     const int rl = T <= 256 ? 1 : T <= 512 ? 2 : 4;
-    const dim3 grid((unsigned)((int64_t)a.ntx * a.nty * (tz1 - tz0))), block(256);
-    if (m.xscs_rx == 4) {  // x-run variant: four consecutive x rows per lane
-        const size_t lds = ((size_t)a.wx * a.wy * a.wz + 8) * sizeof(double);
-#define FAMG_XR(M, IB) spmv_xscs_run_kernel<M, IB, 4><<<grid, block, lds, s>>>(a, m.xscs_chunks.get(), m.xscs_nchunks);
-#define FAMG_XRM(IB)                                                                               \
-    switch (mode) {                                                                                \
-    case SPMV_SET: FAMG_XR(SPMV_SET, IB) break;                                                    \
-    case SPMV_ADD: FAMG_XR(SPMV_ADD, IB) break;                                                    \
-    case SPMV_RESID: FAMG_XR(SPMV_RESID, IB) break;                                                \
-    case SPMV_RESID0: FAMG_XR(SPMV_RESID0, IB) break;                                              \
-    case SPMV_JACOBI: FAMG_XR(SPMV_JACOBI, IB) break;                                              \
-    default: fail(AMG_ERR_UNSUPPORTED, "stencil-class storage: unsupported SpMV epilogue");        \
-    }
-        if (m.scs_ib == 1) { FAMG_XRM(1) }
-        else { FAMG_XRM(2) }
-#undef FAMG_XRM
-#undef FAMG_XR
-        FAMG_CHECK_HIP(hipGetLastError());
-        return;
-    }
     const size_t lds = (size_t)a.wx * a.wy * a.wz * sizeof(double);
+    const dim3 grid((unsigned)((int64_t)a.ntx * a.nty * (tz1 - tz0))), block(256);
 #define FAMG_XS3(M, IB)                                                                            \
     if (rl == 1) spmv_xscs_kernel<M, IB, 1><<<grid, block, lds, s>>>(a);                           \
     else if (rl == 2) spmv_xscs_kernel<M, IB, 2><<<grid, block, lds, s>>>(a);                      \

@@ -118,11 +118,7 @@ amg_status amg_set_alloc_policy(int32_t policy);
  * wave-per-row kernel (0 auto = chosen per matrix at finalize, 1/2/4; env
  * FAMG_VEC_WPR), 3 = time the wide grid-transfer classes (gtx.hip) against a
  * transfer operator's other storage at setup and keep them only where they win
- * (default 1, env FAMG_GTX_TIME; 0 keeps them wherever they build), 4 = the
- * x-run variant of the x-staged stencil classes (four consecutive x rows per
- * lane, a stencil x run's window values read once for all four) for operators
- * finalized afterwards: 0 never, 1 (default, env FAMG_XSCS_RUN) where it times
- * faster at setup, 2 wherever the tile allows it.  Setting one
+ * (default 1, env FAMG_GTX_TIME; 0 keeps them wherever they build).  Setting one
  * makes every multigrid re-capture its hipGraph at its next apply.  amg_get_flag
  * reads the current value. */
 amg_status amg_set_flag(int32_t which, int64_t value);

@@ -1404,47 +1404,6 @@ def test_wide_grid_transfer_classes(ctx, gen, dims):
     assert np.linalg.norm(z - zref) <= 1e-11 * np.linalg.norm(zref)
 
 
-@pytest.mark.parametrize("gen,dims", [("27pt", (64, 48, 40)), ("7pt", (96, 64, 48)), ("27pt", (45, 37, 29))])
-def test_xstaged_classes_x_runs_bitwise(ctx, gen, dims):
-    """The x-run variant of the x-staged stencil classes (four consecutive x
-    rows per lane; the stencil's x runs read once per chunk of <= 4 offsets for
-    all four rows): every epilogue bitwise the one-row-per-lane kernel's on
-    each x-staged level, and the V-cycles bitwise equal."""
-    import torch
-    A = (fa().SparseMatOp.laplace3d_7pt(ctx, *dims) if gen == "7pt"
-         else fa().SparseMatOp.aniso27(ctx, *dims, 1.0, 1.0, 0.01))
-    mgs = {}
-    for mode in (0, 2):
-        fa().set_flag("xscs_run", mode)
-        try:
-            mgs[mode] = fa().sa_build_box(A, dims, (2, 2, 2), coarsest_dim=60)
-        finally:
-            fa().set_flag("xscs_run", 1)
-    seen = 0
-    rng = np.random.default_rng(5)
-    for l in range(1, mgs[0].levels() - 1):
-        A0, A2 = mgs[0].level(l)[0], mgs[2].level(l)[0]
-        if not (A0.spmv_info()["xstaged"] and A2.spmv_info()["xstaged"]):
-            continue
-        seen += 1
-        m, n = A0.dims()
-        x, b, y0 = (T(rng.standard_normal(m)) for _ in range(3))
-        d = T(rng.uniform(0.1, 1.0, m))
-        for mode in ("set", "add", "resid", "jacobi"):
-            outs = []
-            for M in (A0, A2):
-                y = y0.clone()
-                M.spmv_epilogue(mode, x, y, b, d)
-                ctx.synchronize()
-                outs.append(H(y))
-            assert np.array_equal(outs[0].view(np.int64), outs[1].view(np.int64)), (l, mode)
-    assert seen >= 1
-    b = np.random.default_rng(44).uniform(-1, 1, A.nrows)
-    z0 = apply_dev(ctx, mgs[0], b, A.nrows)
-    z2 = apply_dev(ctx, mgs[2], b, A.nrows)
-    assert np.array_equal(z0.view(np.int64), z2.view(np.int64))
-
-
 def test_constant_diagonal_epilogues_bitwise(ctx):
     """The 7-point Laplacian's Jacobi diagonal is one value (a_ii = 6): the DIA
     JACOBI / folded RESID0 epilogues and the grid-transfer ADD0 read it as one
