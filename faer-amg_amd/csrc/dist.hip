@@ -633,7 +633,9 @@ struct DistMultigridOp : LinOp {
     }
 
     // last_out: the final step writes there (owned rows only) instead of t
-    void smooth(int64_t l, double *&v, double *&t, const double *f, bool zero, double *last_out = nullptr) {
+    // pre_df: t = d*f (the first step from zero) was written by the restriction (SPMV_SETDF)
+    void smooth(int64_t l, double *&v, double *&t, const double *f, bool zero, double *last_out = nullptr,
+                bool pre_df = false) {
         DLevel &D = L[l];
         hipStream_t s = ctx->stream;
         log_at(l, AMG_ROLE_SMOOTH);
@@ -656,8 +658,13 @@ struct DistMultigridOp : LinOp {
         for (int64_t it = 0; it < steps; it++) {
             if (last_out && it + 1 == steps) t = last_out;
             if (zero && it == 0) {
-                if (D.S->dcode.get()) vec_mul_coded(t, D.S->dcode.get(), D.S->dtab.get(), f, D.sp.n_own, s);
-                else vec_mul(t, D.S->d.get(), f, D.sp.n_own, s);
+                if (pre_df) {
+                    // written by the restriction
+                } else if (D.S->dcode.get()) {
+                    vec_mul_coded(t, D.S->dcode.get(), D.S->dtab.get(), f, D.sp.n_own, s);
+                } else {
+                    vec_mul(t, D.S->d.get(), f, D.sp.n_own, s);
+                }
             } else {
                 SpmvEpi epi;
                 epi.b = f;
@@ -686,16 +693,45 @@ struct DistMultigridOp : LinOp {
 
     // out (level 0 only, may be null): the post-smoothing's last Jacobi step
     // writes the owned rows there directly, saving the final n_own copy
-    void cycle(int64_t l, double *v, const double *f, bool zero, double *out = nullptr) {
+    // the single-GPU cycle's zero-guess fold (fold_level) where the level's
+    // residual needs no halo (a rank that owns the whole level): RESID0 reads
+    // f and d at every column, which a ghost region of f would have to carry
+    bool folds(const DLevel &D, bool zero) const {
+        return zero && !D.G && D.sp.nbr.empty() && D.sp.n_ghost == 0 &&
+               fold_level(D.A.get(), D.S.get(), D.P.get(), tail->fold_zero_guess, true, steps);
+    }
+    // the restriction out of distributed level l writes level l + 1's first
+    // Jacobi step from zero (SPMV_SETDF), as MultigridOp::cycle does
+    bool restrict_df(int64_t l) const {
+        if (!tail->restrict_df || !setdf_enabled() || steps < 1 || !r_has_setdf(L[l].R.get())) return false;
+        if (l + 1 < La) {
+            const DLevel &C = L[l + 1];
+            return C.S && !C.G && !folds(C, true);
+        }
+        // into the tail: one rank restricts straight into the tail's input
+        if (tr->nranks != 1 || tail->levels.size() < 2) return false;
+        const MgLevel &T = tail->levels[0];
+        auto *Ac = dynamic_cast<const CsrOp *>(T.A.get());
+        auto *Dc = dynamic_cast<const DiagOp *>(T.S.get());
+        auto *Pc = dynamic_cast<const CsrOp *>(T.P.get());
+        return Ac && Dc && !fold_level(Ac, Dc, Pc, tail->fold_zero_guess, true, steps);
+    }
+    static SpmvEpi df_epi(const DiagOp &S, double *y2) {
+        SpmvEpi e;
+        e.d = S.d.get();
+        e.dc = S.dcode.get();
+        e.dt = S.dtab.get();
+        e.dk = S.dconst;
+        e.y2 = y2;
+        return e;
+    }
+
+    void cycle(int64_t l, double *v, const double *f, bool zero, double *out = nullptr, bool pre_df = false) {
         DLevel &D = L[l];
         hipStream_t s = ctx->stream;
         double *v0 = v;
         double *t = (v == D.t.get()) ? D.v.get() : D.t.get();
-        // the single-GPU cycle's zero-guess fold (fold_level) where the level's
-        // residual needs no halo (a rank that owns the whole level): RESID0 reads
-        // f and d at every column, which a ghost region of f would have to carry
-        const bool fold = zero && !D.G && D.sp.nbr.empty() && D.sp.n_ghost == 0 &&
-                          fold_level(D.A.get(), D.S.get(), D.P.get(), tail->fold_zero_guess, true, steps);
+        const bool fold = folds(D, zero);
         SpmvEpi epi;
         epi.b = f;
         SpmvEpi epi0 = epi;  // the folded epilogues' d*f
@@ -709,15 +745,17 @@ struct DistMultigridOp : LinOp {
             log_at(l, AMG_ROLE_RESID);
             spmv(D.A->m, f, D.r.get(), SPMV_RESID0, epi0, s);  // f - A (d f)
         } else {
-            smooth(l, v, t, f, zero);
+            smooth(l, v, t, f, zero, nullptr, pre_df);
             log_at(l, AMG_ROLE_RESID);
             halo_spmv(D.sp, v, D.A->m, D.r.get(), SPMV_RESID, epi);
         }
+        const bool df = restrict_df(l);
         if (l + 1 < La) {
             DLevel &C = L[l + 1];
             log_at(l, AMG_ROLE_RESTRICT);
-            halo_spmv(D.sp, D.r.get(), D.R->m, C.f.get(), SPMV_SET, SpmvEpi{});
-            for (int64_t k = 0; k < mu; k++) cycle(l + 1, C.v.get(), C.f.get(), k == 0);
+            if (df) halo_spmv(D.sp, D.r.get(), D.R->m, C.f.get(), SPMV_SETDF, df_epi(*C.S, C.t.get()));
+            else halo_spmv(D.sp, D.r.get(), D.R->m, C.f.get(), SPMV_SET, SpmvEpi{});
+            for (int64_t k = 0; k < mu; k++) cycle(l + 1, C.v.get(), C.f.get(), k == 0, nullptr, df && k == 0);
             log_at(l, AMG_ROLE_INTERP);
             if (fold) {
                 halo_spmv(C.sp, C.v.get(), D.P->m, t, SPMV_ADD0, epi0);  // v = d f + P v_c
@@ -729,14 +767,18 @@ struct DistMultigridOp : LinOp {
             const int64_t cnt = tail_splits[tr->rank + 1] - tail_splits[tr->rank];
             log_at(l, AMG_ROLE_RESTRICT);
             if (tr->nranks == 1) {  // nothing to gather: restrict into the tail's input
-                halo_spmv(D.sp, D.r.get(), D.R->m, fc_full.get(), SPMV_SET, SpmvEpi{});
+                if (df)
+                    halo_spmv(D.sp, D.r.get(), D.R->m, fc_full.get(), SPMV_SETDF,
+                              df_epi(*dynamic_cast<const DiagOp *>(tail->levels[0].S.get()), tail->levels[0].t.get()));
+                else
+                    halo_spmv(D.sp, D.r.get(), D.R->m, fc_full.get(), SPMV_SET, SpmvEpi{});
             } else {
                 if (cnt) halo_spmv(D.sp, D.r.get(), D.R->m, gather.get() + tr->rank * tail_max, SPMV_SET, SpmvEpi{});
                 else halo(D.sp, D.r.get(), *tr, s);
                 gather_tail(gather.get() + tr->rank * tail_max);
             }
             if (g_launch_log) g_launch_log->level_base = (int32_t)La;
-            for (int64_t k = 0; k < mu; k++) tail->cycle(0, vc_full.get(), fc_full.get(), k == 0, nullptr);
+            for (int64_t k = 0; k < mu; k++) tail->cycle(0, vc_full.get(), fc_full.get(), k == 0, nullptr, df && k == 0);
             if (g_launch_log) g_launch_log->level_base = 0;
             log_at(l, AMG_ROLE_INTERP);
             if (fold) {

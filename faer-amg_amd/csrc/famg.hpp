@@ -518,6 +518,13 @@ struct MultigridOp : LinOp {
 
 // the zero-guess fold decision of one level (RESID0 + ADD0 instead of v = d*f)
 bool fold_level(const CsrOp *A, const DiagOp *D, const CsrOp *P, bool fold_zero_guess, bool v_zero, int64_t steps);
+// the restriction into a level writes that level's first Jacobi step from zero
+// (SPMV_SETDF) -- false with FAMG_SETDF=0
+bool setdf_enabled();
+// R serves SPMV_SETDF (a grid-transfer overlay of either width)
+inline bool r_has_setdf(const CsrOp *R) {
+    return R && ((R->m.gtx_on && R->m.gtx_r) || (R->m.gtc_on && R->m.gtc_r));
+}
 
 // fused grid transfers (fuse.hip)
 void fuse_setup(MultigridOp &mg, size_t l);

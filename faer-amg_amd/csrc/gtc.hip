@@ -154,8 +154,9 @@ struct GtcArgs {
     const double *d;
     const uint8_t *dc;
     const double *dt;
-    int dconst;  // ADD0 with coded d of one value: d = dk, no codes read
+    int dconst;  // ADD0 / SETDF with coded d of one value: d = dk, no codes read
     double dk;
+    double *y2;  // restriction SETDF: y2 = d * y (the next level's first Jacobi step from zero)
 };
 
 // The class dictionary and value table into LDS: every load of a lane issued
@@ -258,8 +259,8 @@ __global__ __launch_bounds__(256) void k_gtc_interp(GtcArgs a) {
 
 // R r over a coarse tile of 16 x 8 x GR_TZ points (GR_TZ / 2 rows per lane,
 // along z); the fine window 34 x 18 x (2 GR_TZ + 2) around their boxes in LDS,
-// the dictionary in dynamic LDS (nce entries).
-template <int GR_TZ>
+// the dictionary in dynamic LDS (nce entries).  DF (SETDF): also y2 = d * y.
+template <int GR_TZ, bool DF>
 __global__ __launch_bounds__(256) void k_gtc_restrict(GtcArgs a) {
     constexpr int GR_WZ = 2 * GR_TZ + 2, RL = GR_TZ / 2;
     __shared__ double win[GR_WX * GR_WY * GR_WZ];
@@ -319,6 +320,10 @@ __global__ __launch_bounds__(256) void k_gtc_restrict(GtcArgs a) {
             for (int u = 0; u < 8; u++) acc = fma(cv[u], w[u], acc);
         }
         a.y[J[j]] = acc;
+        if constexpr (DF) {
+            const double dd = a.dconst ? a.dk : a.dc ? a.dt[a.dc[J[j]]] : a.d[J[j]];
+            a.y2[J[j]] = dd * acc;  // vec_mul(_coded)'s product
+        }
     }
 }
 
@@ -434,7 +439,7 @@ static int gtc_rtz() {
 }
 
 bool gtc_supports(const GpuCsr &m, SpmvMode mode) {
-    return m.gtc_r ? mode == SPMV_SET : (mode == SPMV_SET || mode == SPMV_ADD || mode == SPMV_ADD0);
+    return m.gtc_r ? (mode == SPMV_SET || mode == SPMV_SETDF) : (mode == SPMV_SET || mode == SPMV_ADD || mode == SPMV_ADD0);
 }
 
 // A/B switch FAMG_DIA_DK=0 (shared with the DIA kernels): a constant coded d is read per row
@@ -482,6 +487,7 @@ void spmv_gtc(const GpuCsr &m, const double *x, double *y, SpmvMode mode, const 
     a.dt = epi.dt;
     a.dconst = epi.dc && epi.dk != 0.0 && gtc_dk_enabled();
     a.dk = epi.dk;
+    a.y2 = epi.y2;
     // the launch's z-tile range: all tiles, or (segments of a rank-local matrix)
     // 1 = the tiles that read owned columns only, 0 / 2 = those before / after
     auto range = [&](int ntz, int ta, int tb, int &z0, int &z1) {
@@ -489,7 +495,9 @@ void spmv_gtc(const GpuCsr &m, const double *x, double *y, SpmvMode mode, const 
         z1 = seg < 0 || seg == 2 ? ntz : seg == 1 ? tb : ta;
     };
     if (m.gtc_r) {
-        FAMG_REQUIRE(mode == SPMV_SET, AMG_ERR_UNSUPPORTED, "grid-transfer R: SET only");
+        FAMG_REQUIRE(mode == SPMV_SET || mode == SPMV_SETDF, AMG_ERR_UNSUPPORTED, "grid-transfer R: SET / SETDF only");
+        FAMG_REQUIRE(mode != SPMV_SETDF || (epi.y2 && (epi.d || epi.dc || epi.dk != 0.0)), AMG_ERR_INVALID,
+                     "SETDF needs y2 and d");
         a.ntx = (int)ceil_div(a.rx, GR_TX);
         a.nty = (int)ceil_div(a.ry, GR_TY);
         const int rtz = gtc_rtz();  // coarse planes per tile
@@ -502,8 +510,14 @@ void spmv_gtc(const GpuCsr &m, const double *x, double *y, SpmvMode mode, const 
         a.tile0 = a.ntx * a.nty * z0;
         const size_t dyn = (size_t)a.nce * sizeof(uint16_t);
         const dim3 grid((unsigned)((int64_t)a.ntx * a.nty * (z1 - z0)));
-        if (rtz == 4) k_gtc_restrict<4><<<grid, dim3(256), dyn, s>>>(a);
-        else k_gtc_restrict<2><<<grid, dim3(256), dyn, s>>>(a);
+        const bool df = mode == SPMV_SETDF;
+        if (rtz == 4) {
+            if (df) k_gtc_restrict<4, true><<<grid, dim3(256), dyn, s>>>(a);
+            else k_gtc_restrict<4, false><<<grid, dim3(256), dyn, s>>>(a);
+        } else {
+            if (df) k_gtc_restrict<2, true><<<grid, dim3(256), dyn, s>>>(a);
+            else k_gtc_restrict<2, false><<<grid, dim3(256), dyn, s>>>(a);
+        }
     } else {
         a.ntx = (int)ceil_div(a.rx, GP_TX);
         a.nty = (int)ceil_div(a.ry, GP_TY);

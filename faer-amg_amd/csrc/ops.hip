@@ -567,7 +567,7 @@ bool fold_level(const CsrOp *A, const DiagOp *D, const CsrOp *P, bool fold_zero_
 // cycle (multigrid.rs:269-380).  The result ends in the buffer v points to on
 // entry (Jacobi ping-pong flips an even number of times: 2*steps).
 // FAMG_SETDF=0: the next level's first Jacobi step from zero as its own d*f pass
-static bool setdf_enabled() {
+bool setdf_enabled() {
     static const bool on = [] {
         const char *e = getenv("FAMG_SETDF");
         return !(e && e[0] == '0');
@@ -634,7 +634,7 @@ void MultigridOp::cycle(int64_t l, double *v, const double *f, bool v_zero, doub
             vec_sub(L.r.get(), f, L.r.get(), n, s);
         }
     }
-    // R on wide grid-transfer classes also writes the next level's first Jacobi
+    // R on grid-transfer classes (either width) also writes the next level's first Jacobi
     // step from zero (d_c * f_c, what smooth() would compute first) into the
     // buffer that step writes: one launch and 24 n_c bytes fewer, same values
     bool df = false;
@@ -643,7 +643,7 @@ void MultigridOp::cycle(int64_t l, double *v, const double *f, bool v_zero, doub
         auto *Ac = dynamic_cast<CsrOp *>(C.A.get());
         auto *Dc = dynamic_cast<DiagOp *>(C.S.get());
         auto *Pc = dynamic_cast<CsrOp *>(C.P.get());
-        df = Rc && Rc->m.gtx_on && Rc->m.gtx_r && Ac && Dc && steps >= 1 &&
+        df = r_has_setdf(Rc) && Ac && Dc && steps >= 1 &&
              !fold_level(Ac, Dc, Pc, fold_zero_guess, true, steps);
         if (df) {
             log_at(l, AMG_ROLE_RESTRICT);

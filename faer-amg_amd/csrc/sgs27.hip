@@ -56,6 +56,7 @@ struct Sgs27Args {
     const double *zero;    // >= nx zeros (rows outside the grid)
     const double *cpy_src; // optional: the tile's rows of plane z + 1 copied from cpy_src to cpy_dst
     double *cpy_dst;
+    int jper;  // march: planes of the parity per workgroup
 };
 
 
@@ -167,8 +168,8 @@ __device__ __forceinline__ void sgs27_stage(const Sgs27Args &a, double *lds, con
             for (int u = 0; u < U; u++) {
                 acc[u] = 0.0;
 #pragma unroll
-                for (int k = 0; k < 27; k++) acc[u] = fma(scoef[k], w[u][k / 3][k % 3], acc[u]);  // LDS broadcast
-                dr[u] = scoef[27];
+                for (int k = 0; k < 27; k++) acc[u] = fma(a.icoef[k], w[u][k / 3][k % 3], acc[u]);  // LDS broadcast
+                dr[u] = a.idinv;
             }
         } else {
 #pragma unroll
@@ -274,6 +275,161 @@ __global__ __launch_bounds__(64 * NW) void k_sgs27_phase(Sgs27Args a) {
         const sgs_dbl2_t *cs = reinterpret_cast<const sgs_dbl2_t *>(a.cpy_src + o);
         sgs_dbl2_t *cd = reinterpret_cast<sgs_dbl2_t *>(a.cpy_dst + o);
         for (int q = tid; q < (y1 - y0) * nx2; q += NT) cd[q] = cs[q];
+    }
+}
+
+
+// Marching phase (CST, nx <= 256): one workgroup per (grid-row tile, run of
+// jper planes of the parity).  Three LDS slots of rows r0 - 1 .. r1 (zero rows
+// outside the grid, so no row needs a range test): the own plane and the other
+// parity's planes z - 1 and z + 1.  While plane z runs its colours, registers
+// fetch plane z + 2's own rows and plane z + 3's rows; after z's rows are
+// written they go to the own slot and to the slot that held plane z - 1.  Each
+// plane of the other parity is staged once per tile column instead of twice,
+// and the staging overlaps the colour stages.  Per point the arithmetic is
+// sgs27_stage's (bitwise the colour launches).
+template <int NW, int PFS, int PFO>
+__device__ __forceinline__ void sgs27m_fetch(const Sgs27Args &a, int z, int zz, int r0, int nown2, int npl2,
+                                             bool own, sgs_dbl2_t (&vo)[PFS], sgs_dbl2_t (&vp)[PFO]) {
+    constexpr int NT = 64 * NW;
+    const int nx = a.nx, ny = a.ny, nx2 = nx / 2;
+    const int tid = threadIdx.x;
+    if (own) {
+        const sgs_dbl2_t *src = reinterpret_cast<const sgs_dbl2_t *>(a.S + ((int64_t)z * ny + r0) * nx);
+#pragma unroll
+        for (int u = 0; u < PFS; u++) vo[u] = src[min(tid + NT * u, nown2 - 1)];
+    }
+    const bool pok = !a.other_zero && zz >= 0 && zz < a.nz;
+    const sgs_dbl2_t *o2 = reinterpret_cast<const sgs_dbl2_t *>(a.O + (int64_t)zz * nx * ny);
+#pragma unroll
+    for (int u = 0; u < PFO; u++) {
+        const int q = min(tid + NT * u, npl2 - 1);
+        const int pr = q / nx2, c = q - pr * nx2;
+        const int yy = r0 - 1 + pr;
+        vp[u] = pok && yy >= 0 && yy < ny ? o2[(int64_t)yy * nx2 + c] : sgs_dbl2_t{0.0, 0.0};
+    }
+}
+
+// One colour of a marching phase.  Slot rows have a stride of nx + 4 doubles,
+// x at 2 + x, two zero columns on each side (never written), so the window
+// x - 1 .. x + 1 needs neither clamps nor selects: one 8-B and one 16-B read
+// per row.  Waves are split over the row's 64-point segments without a
+// division: wave w takes segment w % nseg of rows w / nseg, w / nseg + NW / nseg, ...
+template <int PX, int NW>
+__device__ __forceinline__ void sgs27m_stage(const Sgs27Args &a, double *own, const double *lo, const double *hi,
+                                             int z, int r0, int ys0, int ys1, int py, bool first_zero) {
+    const int nx = a.nx, ny = a.ny, rs = nx + 4;
+    const int yfirst = ys0 + ((ys0 & 1) != py ? 1 : 0);
+    const int nrow = yfirst < ys1 ? (ys1 - yfirst + 1) / 2 : 0;
+    const int nk = nx / 2;
+    const int nseg = (nk + 63) >> 6;  // 1 or 2 (nx <= 256): divides NW
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    const int sg = wave & (nseg - 1), wstep = NW / nseg;
+    const int k = (sg << 6) + lane;
+    const bool live = k < nk;
+    const int x = PX + 2 * min(k, nk - 1);
+    const int o16 = 2 + x - PX, o8 = PX == 0 ? 1 + x : 3 + x;  // [x - PX, x - PX + 1] and the third value
+    const double *planes[3] = {lo, own, hi};
+    for (int yr = wave / nseg; yr < nrow; yr += wstep) {
+        const int y = yfirst + 2 * yr;
+        const double br = a.b[((int64_t)z * ny + y) * nx + x];
+        double w[9][3];
+#pragma unroll
+        for (int j = 0; j < 9; j++) {
+            const double *row = planes[j / 3] + (y + j % 3 - r0) * rs;
+            const sgs_dbl2_t p = *reinterpret_cast<const sgs_dbl2_t *>(row + o16);
+            const double v = row[o8];
+            w[j][0] = PX == 0 ? v : p.x;
+            w[j][1] = PX == 0 ? p.x : p.y;
+            w[j][2] = PX == 0 ? p.y : v;
+        }
+        double acc = 0.0;
+#pragma unroll
+        for (int q = 0; q < 27; q++) acc = fma(a.icoef[q], w[q / 3][q % 3], acc);
+        const double xr = w[4][1];
+        if (live) own[(y - r0 + 1) * rs + 2 + x] = first_zero ? a.idinv * br : xr + a.idinv * (br - acc);
+    }
+}
+
+// pairs q of a row set (nx / 2 per row) -> LDS pair index in slot rows of nx + 4
+__device__ __forceinline__ int sgs27m_lpair(int q, int nx2) {
+    const int pr = q / nx2;
+    return pr * (nx2 + 2) + 1 + (q - pr * nx2);
+}
+
+template <int NW, int PFS, int PFO>
+__global__ __launch_bounds__(64 * NW) void k_sgs27_march(Sgs27Args a) {
+    constexpr int NT = 64 * NW;
+    extern __shared__ sgs_dbl2_t lds_pairs[];
+    double *lds = reinterpret_cast<double *>(lds_pairs);
+    const int tid = threadIdx.x;
+    const int w = xcd_remap(blockIdx.x, gridDim.x);
+    const int chunk = w / a.ntiles, tile = w - chunk * a.ntiles;
+    const int nplanes = (a.nz - a.pz + 1) / 2;
+    const int j0 = chunk * a.jper, j1 = min(j0 + a.jper, nplanes);
+    const int nx = a.nx, ny = a.ny, nx2 = nx / 2, rs = nx + 4;
+    const int y0 = tile * a.ty, y1 = min(y0 + a.ty, ny);
+    const int r0 = max(y0 - a.nst, 0), r1 = min(y1 + a.nst, ny);
+    const int nown2 = (r1 - r0) * nx2, npl2 = (r1 - r0 + 2) * nx2;
+    const int srw = a.ty + 2 * a.nst + 2;  // rows per slot
+    double *own = lds, *lo = lds + (int64_t)srw * rs, *hi = lo + (int64_t)srw * rs;
+    sgs_dbl2_t *ow2 = reinterpret_cast<sgs_dbl2_t *>(own);
+    // everything zero first: the pad columns and the own slot's rows r0 - 1 and r1
+    // are read where they leave the grid and never written
+    for (int q = tid; q < 3 * srw * (nx2 + 2); q += NT) lds_pairs[q] = sgs_dbl2_t{0.0, 0.0};
+    __syncthreads();
+    int z = 2 * j0 + a.pz;
+    {
+        sgs_dbl2_t vo[PFS], vp[PFO], vq[PFO];
+        sgs27m_fetch<NW, PFS, PFO>(a, z, z - 1, r0, nown2, npl2, !a.own_zero, vo, vp);
+        sgs_dbl2_t dummy[PFS];
+        sgs27m_fetch<NW, PFS, PFO>(a, z, z + 1, r0, nown2, npl2, false, dummy, vq);
+        if (!a.own_zero) {
+#pragma unroll
+            for (int u = 0; u < PFS; u++)
+                if (tid + NT * u < nown2) ow2[(nx2 + 2) + sgs27m_lpair(tid + NT * u, nx2)] = vo[u];
+        }
+        sgs_dbl2_t *s0 = reinterpret_cast<sgs_dbl2_t *>(lo), *s1 = reinterpret_cast<sgs_dbl2_t *>(hi);
+#pragma unroll
+        for (int u = 0; u < PFO; u++)
+            if (tid + NT * u < npl2) {
+                const int l = sgs27m_lpair(tid + NT * u, nx2);
+                s0[l] = vp[u];
+                s1[l] = vq[u];
+            }
+    }
+    __syncthreads();
+    for (int j = j0; j < j1; j++, z += 2) {
+        const bool more = j + 1 < j1;
+        sgs_dbl2_t vo[PFS], vp[PFO];
+        if (more) sgs27m_fetch<NW, PFS, PFO>(a, z + 2, z + 3, r0, nown2, npl2, !a.own_zero, vo, vp);
+        for (int s = 0; s < a.nst; s++) {
+            const int h = a.nst - 1 - s;
+            const int ys0 = max(y0 - h, 0), ys1 = min(y1 + h, ny);
+            const bool first_zero = a.own_zero && a.other_zero && s == 0;
+            if (a.px[s] == 0) sgs27m_stage<0, NW>(a, own, lo, hi, z, r0, ys0, ys1, a.py[s], first_zero);
+            else sgs27m_stage<1, NW>(a, own, lo, hi, z, r0, ys0, ys1, a.py[s], first_zero);
+            __syncthreads();
+        }
+        sgs_dbl2_t *dst = reinterpret_cast<sgs_dbl2_t *>(a.T + ((int64_t)z * ny + y0) * nx);
+        const sgs_dbl2_t *srcl = ow2 + (y0 - r0 + 1) * (nx2 + 2);
+        for (int q = tid; q < (y1 - y0) * nx2; q += NT) dst[q] = srcl[sgs27m_lpair(q, nx2)];
+        if (more) {
+            __syncthreads();
+#pragma unroll
+            for (int u = 0; u < PFS; u++)
+                if (tid + NT * u < nown2)
+                    ow2[(nx2 + 2) + sgs27m_lpair(tid + NT * u, nx2)] = a.own_zero ? sgs_dbl2_t{0.0, 0.0} : vo[u];
+            sgs_dbl2_t *sl = reinterpret_cast<sgs_dbl2_t *>(lo);
+#pragma unroll
+            for (int u = 0; u < PFO; u++)
+                if (tid + NT * u < npl2) sl[sgs27m_lpair(tid + NT * u, nx2)] = vp[u];
+            double *t = lo;
+            lo = hi;
+            hi = t;
+            __syncthreads();
+        }
     }
 }
 
@@ -514,6 +670,20 @@ static void sgs27_phase(const SgsOp &S, int pz, int nst, const int *px, const in
                    rows * (8 + (S.const27 ? 0 : 4 * (int64_t)m.dia_cw) + 8) + (own_zero ? 0 : rows * 8) +
                        (other_zero ? 0 : (int64_t)(m.nrows - rows) * 8) +
                        (cpy_src ? (int64_t)(m.nrows - rows) * 16 : 0));
+    constexpr int MPFS = 3, MPFO = 4;  // march: pairs per thread of a tile's own rows / a plane's rows
+    if (ol && S.const27 && S.nx27 <= 256 && nst <= 4 && flag(FLAG_SGS27_MARCH) > 0 && !cpy_src &&
+        (int64_t)(a.ty + 2 * nst) * (S.nx27 / 2) <= MPFS * 1024 && (int64_t)(a.ty + 2 * nst + 2) * (S.nx27 / 2) <= MPFO * 1024 &&
+        (size_t)3 * (a.ty + 2 * nst + 2) * (S.nx27 + 4) * sizeof(double) <= 160 * 1024) {
+        const int cus = std::max(S.ctx->num_cus, 1);
+        a.jper = flag(FLAG_SGS27_MARCH) > 1 ? (int)flag(FLAG_SGS27_MARCH) : (int)std::max<int64_t>(1, ceil_div((int64_t)nplanes * a.ntiles, cus));
+        const int64_t nchunks = ceil_div(nplanes, a.jper);
+        const size_t lds_m = (size_t)3 * (a.ty + 2 * nst + 2) * (S.nx27 + 4) * sizeof(double);
+        static const bool nw8 = getenv("FAMG_SGS27_MNW") && getenv("FAMG_SGS27_MNW")[0] == '8';
+        if (nw8) k_sgs27_march<8, 2 * MPFS, 2 * MPFO><<<dim3((unsigned)(nchunks * a.ntiles)), dim3(512), lds_m, s>>>(a);
+        else k_sgs27_march<16, MPFS, MPFO><<<dim3((unsigned)(nchunks * a.ntiles)), dim3(1024), lds_m, s>>>(a);
+        FAMG_CHECK_HIP(hipGetLastError());
+        return;
+    }
     const dim3 grid((unsigned)(nplanes * a.ntiles));
     const size_t lds = (size_t)(a.ty + 2 * nst + 1 + (ol ? 2 * (a.ty + 2 * nst + 2) : 0)) * S.nx27 * sizeof(double);
     const bool u2 = sgs27_u() == 2;

@@ -2491,7 +2491,8 @@ static void log_spmv(const GpuCsr &m, SpmvMode mode, const SpmvEpi &epi, int64_t
     }
     const int64_t xcols = part(m.ncols);
     const bool dk = (kernel == SPMV_KERNEL_DIA && dia_dk(m, epi)) ||  // one value of d: no codes read
-                    (kernel == SPMV_KERNEL_GTC && mode == SPMV_ADD0 && epi.dc && epi.dk != 0.0 && dia_dk_enabled());
+                    (kernel == SPMV_KERNEL_GTC && (mode == SPMV_ADD0 || mode == SPMV_SETDF) && epi.dc && epi.dk != 0.0 &&
+                     dia_dk_enabled());
     const int64_t db = dk ? 0 : (epi.dc ? 1 : 8);  // bytes per diagonal entry (8-bit codes or fp64)
     int64_t vec = 8 * xcols;              // x read once
     switch (mode) {
@@ -2522,11 +2523,11 @@ void spmv(const GpuCsr &m, const double *x, double *y, SpmvMode mode, const Spmv
         spmv_gtx(m, x, y, mode, epi, s, seg);
         return;
     }
-    FAMG_REQUIRE(mode != SPMV_SETDF, AMG_ERR_UNSUPPORTED, "SETDF needs wide grid-transfer classes");
     if (m.gtc_on && (seg < 0 || m.rframe.on()) && gtc_supports(m, mode)) {
         spmv_gtc(m, x, y, mode, epi, s, seg);
         return;
     }
+    FAMG_REQUIRE(mode != SPMV_SETDF, AMG_ERR_UNSUPPORTED, "SETDF needs a grid-transfer restriction");
     if (m.kernel == SPMV_KERNEL_BSR) {
         FAMG_REQUIRE(mode != SPMV_SGS, AMG_ERR_UNSUPPORTED, "block storage has no SGS sweep");
         spmv_bsr(m, x, y, mode, epi, s, seg);

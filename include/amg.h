@@ -118,7 +118,10 @@ amg_status amg_set_alloc_policy(int32_t policy);
  * wave-per-row kernel (0 auto = chosen per matrix at finalize, 1/2/4; env
  * FAMG_VEC_WPR), 3 = time the wide grid-transfer classes (gtx.hip) against a
  * transfer operator's other storage at setup and keep them only where they win
- * (default 1, env FAMG_GTX_TIME; 0 keeps them wherever they build).  Setting one
+ * (default 1, env FAMG_GTX_TIME; 0 keeps them wherever they build), 4 = marching
+ * 27-point SGS phases (sgs27.hip): 0 = one workgroup per tile and plane, 1 = auto
+ * (about one workgroup per CU), n >= 2 = n planes per workgroup (default 1, env
+ * FAMG_SGS27_MARCH).  Setting one
  * makes every multigrid re-capture its hipGraph at its next apply.  amg_get_flag
  * reads the current value. */
 amg_status amg_set_flag(int32_t which, int64_t value);

@@ -1404,6 +1404,35 @@ def test_wide_grid_transfer_classes(ctx, gen, dims):
     assert np.linalg.norm(z - zref) <= 1e-11 * np.linalg.norm(zref)
 
 
+@pytest.mark.parametrize("gen,dims,smoother", [("7pt", (64, 48, 40), "jacobi"), ("27pt", (48, 40, 33), "l1"),
+                                               ("27pt", (48, 40, 33), "sgs")])
+def test_gtc_restrict_setdf(ctx, gen, dims, smoother):
+    """The 8-bit grid-transfer restriction (R_0 of a box hierarchy) with the SETDF
+    epilogue: f_1 and level 1's first Jacobi-type step from zero d_1 f_1 in one
+    launch.  The cycle is bitwise the one with the separate d*f pass (coded,
+    constant and fp64 diagonals of the level-1 smoother), one launch shorter per
+    such level, and within 1e-11 of the oracle's cycle."""
+    A = (fa().SparseMatOp.laplace3d_7pt(ctx, *dims) if gen == "7pt"
+         else fa().SparseMatOp.aniso27(ctx, *dims, 1.0, 1.0, 0.01))
+    mg = fa().sa_build_box(A, dims, (2, 2, 2), coarsest_dim=60, smoother=smoother)
+    assert mg.level(0)[2].spmv_info()["gtc_kind"] == "gtc"
+    plan = mg.cycle_plan()
+    assert any(p["mode"] == "SETDF" and p["level"] == 0 for p in plan), [(p["level"], p["name"], p["mode"]) for p in plan]
+    b = np.random.default_rng(44).uniform(-1, 1, A.nrows)
+    z = apply_dev(ctx, mg, b, A.nrows)
+    mg.set_restrict_df(False)
+    try:
+        z0 = apply_dev(ctx, mg, b, A.nrows)
+        plan0 = mg.cycle_plan()
+    finally:
+        mg.set_restrict_df(True)
+    assert not any(p["mode"] == "SETDF" for p in plan0)
+    assert len(plan0) > len(plan)
+    assert np.array_equal(z.view(np.int64), z0.view(np.int64))
+    zref = O.Multigrid(oracle_levels_from_gpu(mg, smoother)).apply(b)
+    assert np.linalg.norm(z - zref) <= 1e-11 * np.linalg.norm(zref)
+
+
 def test_constant_diagonal_epilogues_bitwise(ctx):
     """The 7-point Laplacian's Jacobi diagonal is one value (a_ii = 6): the DIA
     JACOBI / folded RESID0 epilogues and the grid-transfer ADD0 read it as one
@@ -1554,6 +1583,38 @@ def test_sgs27_fused_phases_bitwise(ctx, dims):
     # two SGS steps x three phases (four where the LDS-staged phases take the level)
     assert sum(1 for p in plan if p["name"] == "sgs27_phase") in (6, 8)
     assert sum(1 for p in plan2 if p["name"] == "sgs27_phase") == 8  # two SGS steps x four phases
+
+
+@pytest.mark.parametrize("dims", [(64, 40, 33), (48, 48, 32), (96, 70, 29)])
+def test_sgs27_marching_phases_bitwise(ctx, dims):
+    """The marching SGS phases (sgs27.hip k_sgs27_march: a workgroup walks n
+    planes of one parity, the other parity's planes rotating through two LDS
+    slots, the next plane fetched into registers while the current one runs its
+    colours) against the colour launches: bitwise for the step from e = 0 and
+    inside the V-cycle, at 1 (no marching), 2, 3 and 5 planes per workgroup and
+    the automatic choice -- runs that do not divide the plane count included."""
+    A = fa().SparseMatOp.aniso27(ctx, *dims, 1.0, 1.0, 0.01)
+    if A.spmv_info()["kernel"] != "dia":
+        pytest.skip("operator not stored as DIA codes")
+    n = dims[0] * dims[1] * dims[2]
+    r = np.random.default_rng(8).standard_normal(n)
+    b = np.random.default_rng(9).uniform(-1, 1, n)
+    fa().set_sgs_fused(False)
+    try:
+        e0 = apply_dev(ctx, fa().SymGaussSeidel(A), r, n)
+        z0 = apply_dev(ctx, fa().sa_build_box(A, dims, (2, 2, 2), coarsest_dim=500, smoother="sgs"), b, n)
+    finally:
+        fa().set_sgs_fused(True)
+    S1 = fa().SymGaussSeidel(A)
+    mg1 = fa().sa_build_box(A, dims, (2, 2, 2), coarsest_dim=500, smoother="sgs")
+    assert fa().sgs_fused(S1)
+    try:
+        for v in (0, 2, 3, 5, 1):
+            fa().set_flag("sgs27_march", v)
+            assert np.array_equal(apply_dev(ctx, S1, r, n), e0), v
+            assert np.array_equal(apply_dev(ctx, mg1, b, n), z0), v
+    finally:
+        fa().set_flag("sgs27_march", 1)
 
 
 def _spmm_vs_spmv(ctx, A, ks=(1, 3, 8, 32), seed=0):
