@@ -26,7 +26,6 @@
 namespace famg {
 
 typedef double bsr_dbl2_t __attribute__((ext_vector_type(2)));
-typedef double bsr_dbl2u_t __attribute__((ext_vector_type(2), aligned(8)));  // x + 3J: 8-B aligned
 
 constexpr int BSR_B = 3;
 constexpr int BSR_C = 64;                                   // node rows per slice
@@ -70,9 +69,8 @@ template <int MODE> struct BsrRow {
     }
 };
 
-// U block steps: every load of the group is issued before the fmas.  X16: the
-// block's x operands 3J, 3J + 1 as one (dword-aligned) 16-B load + one 8-B load
-template <int U, bool X16>
+// U block steps: every load of the group is issued before the fmas
+template <int U>
 __device__ __forceinline__ void bsr_steps(const char *__restrict__ st, int lane, const double *__restrict__ x,
                                           double &a0, double &a1, double &a2) {
     double v[U][9], xx[U][3];
@@ -88,14 +86,8 @@ __device__ __forceinline__ void bsr_steps(const char *__restrict__ st, int lane,
         v[u][8] = __builtin_nontemporal_load(reinterpret_cast<const double *>(p + BSR_K8) + lane);
         const int J = __builtin_nontemporal_load(reinterpret_cast<const int32_t *>(p + BSR_COL) + lane);
         const double *xp = x + 3 * (int64_t)J;
-        if (X16) {
-            const bsr_dbl2u_t p01 = *reinterpret_cast<const bsr_dbl2u_t *>(xp);
-            xx[u][0] = p01.x;
-            xx[u][1] = p01.y;
-        } else {
-            xx[u][0] = xp[0];
-            xx[u][1] = xp[1];
-        }
+        xx[u][0] = xp[0];
+        xx[u][1] = xp[1];
         xx[u][2] = xp[2];
     }
 #pragma unroll
@@ -112,7 +104,7 @@ __device__ __forceinline__ void bsr_steps(const char *__restrict__ st, int lane,
     }
 }
 
-template <int MODE, bool X16>
+template <int MODE>
 __global__ __launch_bounds__(256) void spmv_bsr3_kernel(BsrArgs a) {
     const int blk = xcd_remap(blockIdx.x, gridDim.x);
     const int sl = __builtin_amdgcn_readfirstlane(blk * 4 + (int)(threadIdx.x >> 6));
@@ -131,11 +123,11 @@ __global__ __launch_bounds__(256) void spmv_bsr3_kernel(BsrArgs a) {
     const char *st = a.data + (int64_t)t0 * BSR_STEP;
     double a0 = 0.0, a1 = 0.0, a2 = 0.0;
     int t = 0;
-    for (; t + 4 <= w; t += 4) bsr_steps<4, X16>(st + (int64_t)t * BSR_STEP, lane, a.e.x, a0, a1, a2);
+    for (; t + 4 <= w; t += 4) bsr_steps<4>(st + (int64_t)t * BSR_STEP, lane, a.e.x, a0, a1, a2);
     switch (w - t) {
-    case 1: bsr_steps<1, X16>(st + (int64_t)t * BSR_STEP, lane, a.e.x, a0, a1, a2); break;
-    case 2: bsr_steps<2, X16>(st + (int64_t)t * BSR_STEP, lane, a.e.x, a0, a1, a2); break;
-    case 3: bsr_steps<3, X16>(st + (int64_t)t * BSR_STEP, lane, a.e.x, a0, a1, a2); break;
+    case 1: bsr_steps<1>(st + (int64_t)t * BSR_STEP, lane, a.e.x, a0, a1, a2); break;
+    case 2: bsr_steps<2>(st + (int64_t)t * BSR_STEP, lane, a.e.x, a0, a1, a2); break;
+    case 3: bsr_steps<3>(st + (int64_t)t * BSR_STEP, lane, a.e.x, a0, a1, a2); break;
     default: break;
     }
     if (live) {
@@ -286,20 +278,13 @@ void spmv_bsr(const GpuCsr &m, const double *x, double *y, SpmvMode mode, const 
     BsrArgs a{m.bsr_data.get(), m.bsr_row0.get(), m.bsr_soff.get(), (int32_t)s0, (int32_t)(s1 - s0),
               BsrEpi{x, y, epi.b, epi.d, epi.dc, epi.dt}};
     const dim3 grid((unsigned)ceil_div(s1 - s0, 4)), block(256);
-#define FAMG_BSR_LAUNCH(X16)                                                                        \
-    switch (mode) {                                                                                 \
-    case SPMV_SET: spmv_bsr3_kernel<SPMV_SET, X16><<<grid, block, 0, s>>>(a); break;                \
-    case SPMV_ADD: spmv_bsr3_kernel<SPMV_ADD, X16><<<grid, block, 0, s>>>(a); break;                \
-    case SPMV_RESID: spmv_bsr3_kernel<SPMV_RESID, X16><<<grid, block, 0, s>>>(a); break;            \
-    case SPMV_JACOBI: spmv_bsr3_kernel<SPMV_JACOBI, X16><<<grid, block, 0, s>>>(a); break;          \
-    default: fail(AMG_ERR_UNSUPPORTED, "block storage: unsupported SpMV epilogue");                 \
+    switch (mode) {
+    case SPMV_SET: spmv_bsr3_kernel<SPMV_SET><<<grid, block, 0, s>>>(a); break;
+    case SPMV_ADD: spmv_bsr3_kernel<SPMV_ADD><<<grid, block, 0, s>>>(a); break;
+    case SPMV_RESID: spmv_bsr3_kernel<SPMV_RESID><<<grid, block, 0, s>>>(a); break;
+    case SPMV_JACOBI: spmv_bsr3_kernel<SPMV_JACOBI><<<grid, block, 0, s>>>(a); break;
+    default: fail(AMG_ERR_UNSUPPORTED, "block storage: unsupported SpMV epilogue");
     }
-    static const bool x16 = [] {
-        const char *e = getenv("FAMG_BSR_X16");
-        return e && e[0] == '1';
-    }();
-    if (x16) { FAMG_BSR_LAUNCH(true) } else { FAMG_BSR_LAUNCH(false) }
-#undef FAMG_BSR_LAUNCH
     FAMG_CHECK_HIP(hipGetLastError());
 }
 

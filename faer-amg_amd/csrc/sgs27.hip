@@ -56,7 +56,8 @@ struct Sgs27Args {
     const double *zero;    // >= nx zeros (rows outside the grid)
     const double *cpy_src; // optional: the tile's rows of plane z + 1 copied from cpy_src to cpy_dst
     double *cpy_dst;
-    int jper;  // march: planes of the parity per workgroup
+    int jper;    // march: planes of the parity per workgroup
+    float rnx2;  // march: 1 / (nx / 2), rounded (q / (nx / 2) as (q + 0.5) * rnx2: exact for q < 2^14)
 };
 
 
@@ -304,7 +305,7 @@ __device__ __forceinline__ void sgs27m_fetch(const Sgs27Args &a, int z, int zz, 
 #pragma unroll
     for (int u = 0; u < PFO; u++) {
         const int q = min(tid + NT * u, npl2 - 1);
-        const int pr = q / nx2, c = q - pr * nx2;
+        const int pr = (int)(((float)q + 0.5f) * a.rnx2), c = q - pr * nx2;
         const int yy = r0 - 1 + pr;
         vp[u] = pok && yy >= 0 && yy < ny ? o2[(int64_t)yy * nx2 + c] : sgs_dbl2_t{0.0, 0.0};
     }
@@ -346,15 +347,15 @@ __device__ __forceinline__ void sgs27m_stage(const Sgs27Args &a, double *own, co
         }
         double acc = 0.0;
 #pragma unroll
-        for (int q = 0; q < 27; q++) acc = fma(a.icoef[q], w[q / 3][q % 3], acc);
+        for (int q = 0; q < 27; q++) acc = fma(a.icoef[q], w[q / 3][q % 3], acc);  // coefficients in SGPRs
         const double xr = w[4][1];
         if (live) own[(y - r0 + 1) * rs + 2 + x] = first_zero ? a.idinv * br : xr + a.idinv * (br - acc);
     }
 }
 
 // pairs q of a row set (nx / 2 per row) -> LDS pair index in slot rows of nx + 4
-__device__ __forceinline__ int sgs27m_lpair(int q, int nx2) {
-    const int pr = q / nx2;
+__device__ __forceinline__ int sgs27m_lpair(int q, int nx2, float rnx2) {
+    const int pr = (int)(((float)q + 0.5f) * rnx2);
     return pr * (nx2 + 2) + 1 + (q - pr * nx2);
 }
 
@@ -388,13 +389,13 @@ __global__ __launch_bounds__(64 * NW) void k_sgs27_march(Sgs27Args a) {
         if (!a.own_zero) {
 #pragma unroll
             for (int u = 0; u < PFS; u++)
-                if (tid + NT * u < nown2) ow2[(nx2 + 2) + sgs27m_lpair(tid + NT * u, nx2)] = vo[u];
+                if (tid + NT * u < nown2) ow2[(nx2 + 2) + sgs27m_lpair(tid + NT * u, nx2, a.rnx2)] = vo[u];
         }
         sgs_dbl2_t *s0 = reinterpret_cast<sgs_dbl2_t *>(lo), *s1 = reinterpret_cast<sgs_dbl2_t *>(hi);
 #pragma unroll
         for (int u = 0; u < PFO; u++)
             if (tid + NT * u < npl2) {
-                const int l = sgs27m_lpair(tid + NT * u, nx2);
+                const int l = sgs27m_lpair(tid + NT * u, nx2, a.rnx2);
                 s0[l] = vp[u];
                 s1[l] = vq[u];
             }
@@ -414,17 +415,17 @@ __global__ __launch_bounds__(64 * NW) void k_sgs27_march(Sgs27Args a) {
         }
         sgs_dbl2_t *dst = reinterpret_cast<sgs_dbl2_t *>(a.T + ((int64_t)z * ny + y0) * nx);
         const sgs_dbl2_t *srcl = ow2 + (y0 - r0 + 1) * (nx2 + 2);
-        for (int q = tid; q < (y1 - y0) * nx2; q += NT) dst[q] = srcl[sgs27m_lpair(q, nx2)];
+        for (int q = tid; q < (y1 - y0) * nx2; q += NT) dst[q] = srcl[sgs27m_lpair(q, nx2, a.rnx2)];
         if (more) {
             __syncthreads();
 #pragma unroll
             for (int u = 0; u < PFS; u++)
                 if (tid + NT * u < nown2)
-                    ow2[(nx2 + 2) + sgs27m_lpair(tid + NT * u, nx2)] = a.own_zero ? sgs_dbl2_t{0.0, 0.0} : vo[u];
+                    ow2[(nx2 + 2) + sgs27m_lpair(tid + NT * u, nx2, a.rnx2)] = a.own_zero ? sgs_dbl2_t{0.0, 0.0} : vo[u];
             sgs_dbl2_t *sl = reinterpret_cast<sgs_dbl2_t *>(lo);
 #pragma unroll
             for (int u = 0; u < PFO; u++)
-                if (tid + NT * u < npl2) sl[sgs27m_lpair(tid + NT * u, nx2)] = vp[u];
+                if (tid + NT * u < npl2) sl[sgs27m_lpair(tid + NT * u, nx2, a.rnx2)] = vp[u];
             double *t = lo;
             lo = hi;
             hi = t;
@@ -675,12 +676,11 @@ static void sgs27_phase(const SgsOp &S, int pz, int nst, const int *px, const in
         (int64_t)(a.ty + 2 * nst) * (S.nx27 / 2) <= MPFS * 1024 && (int64_t)(a.ty + 2 * nst + 2) * (S.nx27 / 2) <= MPFO * 1024 &&
         (size_t)3 * (a.ty + 2 * nst + 2) * (S.nx27 + 4) * sizeof(double) <= 160 * 1024) {
         const int cus = std::max(S.ctx->num_cus, 1);
+        a.rnx2 = 1.0f / (float)(S.nx27 / 2);
         a.jper = flag(FLAG_SGS27_MARCH) > 1 ? (int)flag(FLAG_SGS27_MARCH) : (int)std::max<int64_t>(1, ceil_div((int64_t)nplanes * a.ntiles, cus));
         const int64_t nchunks = ceil_div(nplanes, a.jper);
         const size_t lds_m = (size_t)3 * (a.ty + 2 * nst + 2) * (S.nx27 + 4) * sizeof(double);
-        static const bool nw8 = getenv("FAMG_SGS27_MNW") && getenv("FAMG_SGS27_MNW")[0] == '8';
-        if (nw8) k_sgs27_march<8, 2 * MPFS, 2 * MPFO><<<dim3((unsigned)(nchunks * a.ntiles)), dim3(512), lds_m, s>>>(a);
-        else k_sgs27_march<16, MPFS, MPFO><<<dim3((unsigned)(nchunks * a.ntiles)), dim3(1024), lds_m, s>>>(a);
+        k_sgs27_march<16, MPFS, MPFO><<<dim3((unsigned)(nchunks * a.ntiles)), dim3(1024), lds_m, s>>>(a);
         FAMG_CHECK_HIP(hipGetLastError());
         return;
     }

@@ -517,7 +517,14 @@ def slab_run(nranks, dims, coarsest, agglo, b, overlap=True):
         ctx.synchronize()
         return r0, r1, zl.cpu().numpy(), local, glob, plan, gplan, zg.cpu().numpy(), La
 
-    res = run_ranks(nranks, rank_fn)
+    # wide grid-transfer classes wherever they build: the setup-time timing that
+    # keeps them only where they win would decide per matrix (global vs local, per
+    # rank) on noise, and these tests compare storages
+    fa().set_flag("gtx_time", 0)
+    try:
+        res = run_ranks(nranks, rank_fn)
+    finally:
+        fa().set_flag("gtx_time", 1)
     z = np.zeros(len(b))
     for r in res:
         z[r[0]:r[1]] = r[2]

@@ -1488,14 +1488,16 @@ def test_cycle_plan_accounts_for_every_launch(ctx):
     modes0 = [p["mode"] for p in f0]
     info = A.spmv_info()
     n = A.nrows
+    # the restriction is SETDF where it also writes level 1's first step d_1 f_1
+    rmode = "SETDF" if any(p["mode"] == "SETDF" for p in f0) else "SET"
     if "RESID0" in modes0:
         # folded: RESID0 (f - A d f), R, ADD0 (d f + P v_c), post-smoothing Jacobi
-        assert modes0 == ["RESID0", "SET", "ADD0", "JACOBI"], f0
+        assert modes0 == ["RESID0", rmode, "ADD0", "JACOBI"], f0
         if info["kernel"] == "dia":  # 16 n: f read, r written; d = 6/omega everywhere is one scalar
             assert f0[0]["bytes"] == info["stream_bytes"] + 16 * n, f0[0]
     else:
         # d*f pass, residual, restriction, interpolate-add, post-smoothing Jacobi
-        assert modes0 == ["-", "RESID", "SET", "ADD", "JACOBI"], f0
+        assert modes0 == ["-", "RESID", rmode, "ADD", "JACOBI"], f0
         assert f0[1]["bytes"] == info["stream_bytes"] + 24 * n, f0[1]
     mg.set_fold_zero_guess(False)
     plan2 = mg.cycle_plan()
