@@ -267,6 +267,7 @@ __global__ __launch_bounds__(256) void k_gtc_restrict(GtcArgs a) {
     extern __shared__ uint16_t sd[];
     __shared__ double st[256];
     __shared__ int16_t lut[64];
+    __shared__ double sdt[DF ? 256 : 1];  // SETDF: the coded diagonal's table
     const int tid = threadIdx.x;
     const int t = a.tile0 + xcd_remap(blockIdx.x, gridDim.x);
     const int tix = t % a.ntx, tiy = (t / a.ntx) % a.nty, tiz = t / (a.ntx * a.nty);
@@ -283,6 +284,14 @@ __global__ __launch_bounds__(256) void k_gtc_restrict(GtcArgs a) {
         live[j] = X < a.rx && Y < a.ry && Z < a.rz;
         J[j] = live[j] ? (int64_t)Z * cplane + (int64_t)Y * a.rx + X : 0;
         c[j] = a.cls[J[j]];
+    }
+    int dci[RL];  // SETDF with coded d: the rows' codes loaded with the class ids
+    if constexpr (DF) {
+        if (a.dc && !a.dconst) {
+            sdt[tid] = a.dt[tid];
+#pragma unroll
+            for (int j = 0; j < RL; j++) dci[j] = a.dc[J[j]];
+        }
     }
     constexpr int W = GR_WX * GR_WY * GR_WZ, PF = (W + 255) / 256;
     double v[PF];
@@ -321,7 +330,7 @@ __global__ __launch_bounds__(256) void k_gtc_restrict(GtcArgs a) {
         }
         a.y[J[j]] = acc;
         if constexpr (DF) {
-            const double dd = a.dconst ? a.dk : a.dc ? a.dt[a.dc[J[j]]] : a.d[J[j]];
+            const double dd = a.dconst ? a.dk : a.dc ? sdt[dci[j]] : a.d[J[j]];
             a.y2[J[j]] = dd * acc;  // vec_mul(_coded)'s product
         }
     }

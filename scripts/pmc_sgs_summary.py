@@ -14,7 +14,7 @@ out_dir = sys.argv[1]
 per = {}
 for f in sorted(glob.glob(os.path.join(out_dir, "pmc_sgs*", "**", "*counter_collection.csv"), recursive=True)):
     for r in csv.DictReader(open(f)):
-        if "sgs27_phase" not in r["Kernel_Name"]:
+        if "k_sgs27_phase" not in r["Kernel_Name"] and "k_sgs27_march" not in r["Kernel_Name"]:
             continue
         key = (os.path.dirname(f), int(r["Dispatch_Id"]))
         per.setdefault(r["Counter_Name"], {}).setdefault(key, [r["Kernel_Name"], 0.0])[1] += float(r["Counter_Value"])
