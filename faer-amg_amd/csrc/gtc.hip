@@ -19,6 +19,7 @@
 // SET, ADD (y += P v_c), ADD0 (y = d*b + P v_c, the folded zero-guess step).
 #include <algorithm>
 #include <cstring>
+#include <mutex>
 #include <unordered_map>
 
 #include "famg.hpp"
@@ -157,6 +158,7 @@ struct GtcArgs {
     int dconst;  // ADD0 / SETDF with coded d of one value: d = dk, no codes read
     double dk;
     double *y2;  // restriction SETDF: y2 = d * y (the next level's first Jacobi step from zero)
+    int mz0, mz1, jper;  // marching R: coarse planes [mz0, mz1) of the launch, planes per workgroup
 };
 
 // The class dictionary and value table into LDS: every load of a lane issued
@@ -179,7 +181,8 @@ __device__ __forceinline__ void gtc_stage_dict(const GtcArgs &a, uint16_t *sd, d
 
 // P v_c over a fine tile of 32 x 8 x 4 points: lane (x, y) of the tile takes
 // its four points along z; the coarse window 18 x 6 x 4 around them in LDS.
-template <int MODE, int GP_TZ>
+// NT: the fine-vector streams (b / y read, y written) non-temporal
+template <int MODE, int GP_TZ, bool NT>
 __global__ __launch_bounds__(256) void k_gtc_interp(GtcArgs a) {
     constexpr int GP_WZ = GP_TZ / 2 + 2;
     __shared__ double win[GP_WX * GP_WY * GP_WZ];
@@ -213,9 +216,9 @@ __global__ __launch_bounds__(256) void k_gtc_interp(GtcArgs a) {
         cl[j] = a.cls[i];
         yb[j] = 0.0;
         if (live[j]) {
-            if constexpr (MODE == SPMV_ADD) yb[j] = a.y[i];
+            if constexpr (MODE == SPMV_ADD) yb[j] = NT ? __builtin_nontemporal_load(a.y + i) : a.y[i];
             if constexpr (MODE == SPMV_ADD0) {
-                yb[j] = a.b[i];
+                yb[j] = NT ? __builtin_nontemporal_load(a.b + i) : a.b[i];
                 if (a.dconst) yb[j] = dk * yb[j];  // d*b (vec_mul's product)
                 else if (a.dc) dci[j] = a.dc[i];
                 else yb[j] = a.d[i] * yb[j];
@@ -252,8 +255,9 @@ __global__ __launch_bounds__(256) void k_gtc_interp(GtcArgs a) {
             for (int u = 0; u < 4; u++) acc = fma(v[u], w[u], acc);
         }
         const int64_t i = (int64_t)gz * fplane + (int64_t)gy * a.rx + gx;
-        if constexpr (MODE == SPMV_SET) a.y[i] = acc;
-        else a.y[i] = yb[j] + acc;  // ADD, ADD0
+        const double out = MODE == SPMV_SET ? acc : yb[j] + acc;  // ADD, ADD0: y + P v
+        if (NT) __builtin_nontemporal_store(out, a.y + i);
+        else a.y[i] = out;
     }
 }
 
@@ -332,6 +336,121 @@ __global__ __launch_bounds__(256) void k_gtc_restrict(GtcArgs a) {
         if constexpr (DF) {
             const double dd = a.dconst ? a.dk : a.dc ? sdt[dci[j]] : a.d[J[j]];
             a.y2[J[j]] = dd * acc;  // vec_mul(_coded)'s product
+        }
+    }
+}
+
+
+// Marching R (k_gtc_restrict_march): a workgroup takes a 32 x 8 tile of coarse
+// rows through a run of jper coarse planes.  Coarse plane Z reads fine planes
+// 2Z - 1 .. 2Z + 2, so consecutive planes share two: a ring of four fine-plane
+// windows (66 x 18 each) in LDS, ring slot = fine plane mod 4, and while plane Z
+// is summed the registers fetch fine planes 2Z + 3 and 2Z + 4, which then
+// replace 2Z - 1 and 2Z.  Each fine value is staged ~1.2 times (the x/y halo)
+// instead of ~1.8 (tiles of two coarse planes with their z halo).  Same
+// dictionary walk per row as k_gtc_restrict (bitwise the same sums).
+constexpr int GM_TX = 32, GM_TY = 8;
+constexpr int GM_WX = 2 * GM_TX + 2, GM_WY = 2 * GM_TY + 2, GM_PL = GM_WX * GM_WY;
+constexpr int GM_PF = (2 * GM_PL + 255) / 256;  // registers per lane for two fine planes
+
+__device__ __forceinline__ void gtc_march_fetch(const GtcArgs &a, int wx0, int wy0, int fz, double (&v)[GM_PF]) {
+    // fine local planes fz, fz + 1 of the tile's window
+    const int64_t fplane = (int64_t)a.kx * a.ky;
+#pragma unroll
+    for (int u = 0; u < GM_PF; u++) {
+        const int q = threadIdx.x + 256 * u;
+        const int pl = q >= GM_PL ? 1 : 0, qq = q - pl * GM_PL;
+        const int y = wy0 + qq / GM_WX, x = wx0 + qq % GM_WX, z = fz + pl;
+        const bool in = q < 2 * GM_PL && (unsigned)x < (unsigned)a.kx && (unsigned)y < (unsigned)a.ky &&
+                        z >= a.kz_lo && z < a.kz_hi;
+        const int64_t zb = (int64_t)z * fplane + (z < 0 ? a.add_lo : z >= a.kz ? a.add_hi : 0);
+        v[u] = in ? a.x[zb + (int64_t)y * a.kx + x] : 0.0;
+    }
+}
+
+// ring slot of fine plane 2 Z + dz: (2 Z + dz) & 3 (Z local coarse plane)
+__device__ __forceinline__ void gtc_march_store(double *ring, int Z, const double (&v)[GM_PF], int dz) {
+#pragma unroll
+    for (int u = 0; u < GM_PF; u++) {
+        const int q = threadIdx.x + 256 * u;
+        if (q < 2 * GM_PL) {
+            const int pl = q >= GM_PL ? 1 : 0, qq = q - pl * GM_PL;
+            ring[((2 * Z + dz + pl) & 3) * GM_PL + qq] = v[u];
+        }
+    }
+}
+
+template <bool DF>
+__global__ __launch_bounds__(256) void k_gtc_restrict_march(GtcArgs a) {
+    __shared__ double ring[4 * GM_PL];
+    extern __shared__ uint16_t sd[];
+    __shared__ double st[256];
+    __shared__ int16_t lut[2][64];  // [Z & 1][slot]: ring plane * GM_PL + dy * GM_WX + dx
+    __shared__ double sdt[DF ? 256 : 1];
+    const int tid = threadIdx.x;
+    const int t = xcd_remap(blockIdx.x, gridDim.x);
+    const int ntxy = a.ntx * a.nty;
+    const int chunk = t / ntxy, txy = t - chunk * ntxy;
+    const int X0 = (txy % a.ntx) * GM_TX, Y0 = (txy / a.ntx) * GM_TY;
+    const int Zb = a.mz0 + chunk * a.jper, Ze = min(Zb + a.jper, a.mz1);
+    const int wx0 = 2 * X0 - 1, wy0 = 2 * Y0 - 1;
+    const int lx = tid % GM_TX, ly = tid / GM_TX;
+    const int X = X0 + lx, Y = Y0 + ly;
+    const bool live = X < a.rx && Y < a.ry;
+    const int base = (2 * ly + 1) * GM_WX + 2 * lx + 1;
+    const int64_t cplane = (int64_t)a.rx * a.ry;
+    if (tid < 128) {
+        const int par = tid >> 6, s = tid & 63;
+        const int dz = s / 16 - 1, dy = (s / 4) % 4 - 1, dx = s % 4 - 1;
+        lut[par][s] = (int16_t)(((2 * par + dz) & 3) * GM_PL + dy * GM_WX + dx);
+    }
+    if constexpr (DF)
+        if (a.dc && !a.dconst) sdt[tid] = a.dt[tid];
+    // fine local plane of coarse local plane Z, offset dz
+    auto fzof = [&](int Z, int dz) { return 2 * (a.rz0 + Z) + dz - a.kz0; };
+    {
+        double v0[GM_PF], v1[GM_PF];
+        gtc_march_fetch(a, wx0, wy0, fzof(Zb, -1), v0);
+        gtc_march_fetch(a, wx0, wy0, fzof(Zb, 1), v1);
+        gtc_march_store(ring, Zb, v0, -1);
+        gtc_march_store(ring, Zb, v1, 1);
+    }
+    gtc_stage_dict<G_RMAX>(a, sd, st);
+    __syncthreads();
+    for (int Z = Zb; Z < Ze; Z++) {
+        const bool more = Z + 1 < Ze;
+        double v[GM_PF];
+        if (more) gtc_march_fetch(a, wx0, wy0, fzof(Z, 3), v);
+        const int64_t J = live ? (int64_t)Z * cplane + (int64_t)Y * a.rx + X : 0;
+        const int c = a.cls[J];
+        int dci = 0;
+        if constexpr (DF)
+            if (a.dc && !a.dconst) dci = a.dc[J];
+        if (live) {
+            const uint16_t *e = sd + c * a.ke;
+            const int16_t *lz = lut[Z & 1];
+            double acc = 0.0;
+            for (int k = 0; k < a.ke; k += 8) {
+                double cv[8], w[8];
+#pragma unroll
+                for (int u = 0; u < 8; u++) {
+                    const uint16_t q = e[k + u];
+                    cv[u] = st[q >> 8];
+                    w[u] = ring[base + lz[q & 255]];
+                }
+#pragma unroll
+                for (int u = 0; u < 8; u++) acc = fma(cv[u], w[u], acc);
+            }
+            a.y[J] = acc;
+            if constexpr (DF) {
+                const double dd = a.dconst ? a.dk : a.dc ? sdt[dci] : a.d[J];
+                a.y2[J] = dd * acc;  // vec_mul(_coded)'s product
+            }
+        }
+        if (more) {
+            __syncthreads();                  // plane Z's reads of 2Z - 1 and 2Z done
+            gtc_march_store(ring, Z, v, 3);   // 2Z + 3 -> slot of 2Z - 1, 2Z + 4 -> slot of 2Z
+            __syncthreads();
         }
     }
 }
@@ -447,6 +566,34 @@ static int gtc_rtz() {
     return v;
 }
 
+// workgroups of the marching R per CU with dyn bytes of dictionary (cached)
+static int gtc_march_occupancy(bool df, size_t dyn) {
+    static std::mutex mu;
+    static std::unordered_map<size_t, int> cache;
+    const size_t key = dyn * 2 + (df ? 1 : 0);
+    std::lock_guard<std::mutex> lk(mu);
+    auto it = cache.find(key);
+    if (it != cache.end()) return it->second;
+    int n = 0;
+    const hipError_t e = df ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_gtc_restrict_march<true>, 256, dyn)
+                            : hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_gtc_restrict_march<false>, 256, dyn);
+    if (e != hipSuccess || n < 1) {
+        (void)hipGetLastError();
+        n = 1;
+    }
+    cache[key] = n;
+    return n;
+}
+
+// FAMG_GTC_MARCH=0: R in tiles of two coarse planes instead of marching workgroups
+static bool gtc_march_r() {
+    static const bool on = [] {
+        const char *e = getenv("FAMG_GTC_MARCH");
+        return !(e && e[0] == '0');
+    }();
+    return on;
+}
+
 bool gtc_supports(const GpuCsr &m, SpmvMode mode) {
     return m.gtc_r ? (mode == SPMV_SET || mode == SPMV_SETDF) : (mode == SPMV_SET || mode == SPMV_ADD || mode == SPMV_ADD0);
 }
@@ -509,6 +656,31 @@ void spmv_gtc(const GpuCsr &m, const double *x, double *y, SpmvMode mode, const 
                      "SETDF needs y2 and d");
         a.ntx = (int)ceil_div(a.rx, GR_TX);
         a.nty = (int)ceil_div(a.ry, GR_TY);
+        if (gtc_march_r() && m.ctx) {
+            // marching R: z segments in single coarse planes
+            int ta = 0, tb = a.rz, z0, z1;
+            if (seg >= 0)
+                interior_tiles(a.rz, 4, a.kz, a.kz_lo, a.kz_hi, [&](int t) { return 2 * (a.rz0 + t) - 1 - a.kz0; }, ta, tb);
+            range(a.rz, ta, tb, z0, z1);
+            if (z1 <= z0) return;
+            a.ntx = (int)ceil_div(a.rx, GM_TX);
+            a.nty = (int)ceil_div(a.ry, GM_TY);
+            const int64_t ntxy = (int64_t)a.ntx * a.nty;
+            // exactly one round of workgroups: as many as fit the chip at once (a
+            // second, partial round left most CUs idle: 512 / 768 / 1024 / 1408
+            // workgroups on R_0 of the 256^3 cycle ran 68 / 54 / 70 / 63 us)
+            const size_t dyn = (size_t)a.nce * sizeof(uint16_t);
+            const int per_cu = gtc_march_occupancy(mode == SPMV_SETDF, dyn);
+            const int64_t want = (int64_t)per_cu * std::max(m.ctx->num_cus, 1);
+            a.jper = (int)std::max<int64_t>(1, ceil_div((int64_t)(z1 - z0) * ntxy, want));
+            a.mz0 = z0;
+            a.mz1 = z1;
+            const dim3 grid((unsigned)(ntxy * ceil_div(z1 - z0, a.jper)));
+            if (mode == SPMV_SETDF) k_gtc_restrict_march<true><<<grid, dim3(256), dyn, s>>>(a);
+            else k_gtc_restrict_march<false><<<grid, dim3(256), dyn, s>>>(a);
+            FAMG_CHECK_HIP(hipGetLastError());
+            return;
+        }
         const int rtz = gtc_rtz();  // coarse planes per tile
         const int ntz = (int)ceil_div(a.rz, rtz);
         int ta = 0, tb = ntz, z0, z1;
@@ -539,15 +711,22 @@ void spmv_gtc(const GpuCsr &m, const double *x, double *y, SpmvMode mode, const 
         if (z1 <= z0) return;
         a.tile0 = a.ntx * a.nty * z0;
         const dim3 grid((unsigned)((int64_t)a.ntx * a.nty * (z1 - z0))), block(256);
-#define FAMG_GTCI(TZ)                                                                              \
+#define FAMG_GTCI(TZ, NT)                                                                            \
     switch (mode) {                                                                                \
-    case SPMV_SET: k_gtc_interp<SPMV_SET, TZ><<<grid, block, 0, s>>>(a); break;                    \
-    case SPMV_ADD: k_gtc_interp<SPMV_ADD, TZ><<<grid, block, 0, s>>>(a); break;                    \
-    case SPMV_ADD0: k_gtc_interp<SPMV_ADD0, TZ><<<grid, block, 0, s>>>(a); break;                  \
+    case SPMV_SET: k_gtc_interp<SPMV_SET, TZ, NT><<<grid, block, 0, s>>>(a); break;                \
+    case SPMV_ADD: k_gtc_interp<SPMV_ADD, TZ, NT><<<grid, block, 0, s>>>(a); break;                \
+    case SPMV_ADD0: k_gtc_interp<SPMV_ADD0, TZ, NT><<<grid, block, 0, s>>>(a); break;              \
     default: fail(AMG_ERR_UNSUPPORTED, "grid-transfer P: unsupported SpMV epilogue");              \
     }
-        if (tz == 8) { FAMG_GTCI(8) }
-        else { FAMG_GTCI(4) }
+        // FAMG_GTC_NT=0: cached fine-vector streams (non-temporal: P_0 ADD0 75.3 -> 72.8 us)
+        static const bool nt = !(getenv("FAMG_GTC_NT") && getenv("FAMG_GTC_NT")[0] == '0');
+        if (nt) {
+            if (tz == 8) { FAMG_GTCI(8, true) }
+            else { FAMG_GTCI(4, true) }
+        } else {
+            if (tz == 8) { FAMG_GTCI(8, false) }
+            else { FAMG_GTCI(4, false) }
+        }
 #undef FAMG_GTCI
     }
     FAMG_CHECK_HIP(hipGetLastError());
