@@ -57,6 +57,8 @@ struct Sgs27Args {
     const double *cpy_src; // optional: the tile's rows of plane z + 1 copied from cpy_src to cpy_dst
     double *cpy_dst;
     int jper;    // march: planes of the parity per workgroup
+    int ext[8];  // march: colour s is computed on rows [y0 - ext[s], y1 + ext[s]) of its parity
+    int halo;    // march: own rows staged from y0 - halo (max ext + 1)
     float rnx2;  // march: 1 / (nx / 2), rounded (q / (nx / 2) as (q + 0.5) * rnx2: exact for q < 2^14)
 };
 
@@ -371,9 +373,9 @@ __global__ __launch_bounds__(64 * NW) void k_sgs27_march(Sgs27Args a) {
     const int j0 = chunk * a.jper, j1 = min(j0 + a.jper, nplanes);
     const int nx = a.nx, ny = a.ny, nx2 = nx / 2, rs = nx + 4;
     const int y0 = tile * a.ty, y1 = min(y0 + a.ty, ny);
-    const int r0 = max(y0 - a.nst, 0), r1 = min(y1 + a.nst, ny);
+    const int r0 = max(y0 - a.halo, 0), r1 = min(y1 + a.halo, ny);
     const int nown2 = (r1 - r0) * nx2, npl2 = (r1 - r0 + 2) * nx2;
-    const int srw = a.ty + 2 * a.nst + 2;  // rows per slot
+    const int srw = a.ty + 2 * a.halo + 2;  // rows per slot
     double *own = lds, *lo = lds + (int64_t)srw * rs, *hi = lo + (int64_t)srw * rs;
     sgs_dbl2_t *ow2 = reinterpret_cast<sgs_dbl2_t *>(own);
     // everything zero first: the pad columns and the own slot's rows r0 - 1 and r1
@@ -406,7 +408,7 @@ __global__ __launch_bounds__(64 * NW) void k_sgs27_march(Sgs27Args a) {
         sgs_dbl2_t vo[PFS], vp[PFO];
         if (more) sgs27m_fetch<NW, PFS, PFO>(a, z + 2, z + 3, r0, nown2, npl2, !a.own_zero, vo, vp);
         for (int s = 0; s < a.nst; s++) {
-            const int h = a.nst - 1 - s;
+            const int h = a.ext[s];
             const int ys0 = max(y0 - h, 0), ys1 = min(y1 + h, ny);
             const bool first_zero = a.own_zero && a.other_zero && s == 0;
             if (a.px[s] == 0) sgs27m_stage<0, NW>(a, own, lo, hi, z, r0, ys0, ys1, a.py[s], first_zero);
@@ -672,14 +674,35 @@ static void sgs27_phase(const SgsOp &S, int pz, int nst, const int *px, const in
                        (other_zero ? 0 : (int64_t)(m.nrows - rows) * 8) +
                        (cpy_src ? (int64_t)(m.nrows - rows) * 16 : 0));
     constexpr int MPFS = 3, MPFO = 4;  // march: pairs per thread of a tile's own rows / a plane's rows
-    if (ol && S.const27 && S.nx27 <= 256 && nst <= 4 && flag(FLAG_SGS27_MARCH) > 0 && !cpy_src &&
-        (int64_t)(a.ty + 2 * nst) * (S.nx27 / 2) <= MPFS * 1024 && (int64_t)(a.ty + 2 * nst + 2) * (S.nx27 / 2) <= MPFO * 1024 &&
-        (size_t)3 * (a.ty + 2 * nst + 2) * (S.nx27 + 4) * sizeof(double) <= 160 * 1024) {
+    // Exact halos: colour t at row y reads colour s < t at rows y +- 1 when their row
+    // parities differ and only at row y (the x neighbours) when they agree, so colour
+    // s is needed on ext[s] = max over t > s of ext[t] + (py[t] != py[s]) rows beyond the
+    // tile (forward: 1, 1, 0, 0) -- not nst - 1 - s (256^3 SGS step 285.8 -> 281.9 us).
+    // Tile height 16 where it fits: the per-plane step's fixed costs favour tall
+    // tiles over single-round colours (ty 12 / 14 / 16 / 20: 593 / 316 / 282 / 293 us).
+    int ext[8] = {0}, emax = 0;
+    for (int q = nst - 2; q >= 0; q--)
+        for (int t = q + 1; t < nst; t++) ext[q] = std::max(ext[q], ext[t] + (py[t] != py[q] ? 1 : 0));
+    for (int q = 0; q < nst; q++) emax = std::max(emax, ext[q]);
+    const int halo = emax + 1;
+    int tym = 0;
+    for (int ty = 16; ty >= 4 && !tym; ty--) {
+        if ((int64_t)(ty + 2 * halo) * (S.nx27 / 2) <= MPFS * 1024 &&
+            (int64_t)(ty + 2 * halo + 2) * (S.nx27 / 2) <= MPFO * 1024 &&
+            (size_t)3 * (ty + 2 * halo + 2) * (S.nx27 + 4) * sizeof(double) <= 160 * 1024)
+            tym = std::min(ty, S.ny27);
+    }
+
+    if (ol && S.const27 && S.nx27 <= 256 && nst <= 4 && flag(FLAG_SGS27_MARCH) > 0 && !cpy_src && tym > 0) {
+        for (int q = 0; q < 8; q++) a.ext[q] = ext[q];
+        a.halo = halo;
+        a.ty = tym;
+        a.ntiles = (int)ceil_div(S.ny27, a.ty);
         const int cus = std::max(S.ctx->num_cus, 1);
         a.rnx2 = 1.0f / (float)(S.nx27 / 2);
         a.jper = flag(FLAG_SGS27_MARCH) > 1 ? (int)flag(FLAG_SGS27_MARCH) : (int)std::max<int64_t>(1, ceil_div((int64_t)nplanes * a.ntiles, cus));
         const int64_t nchunks = ceil_div(nplanes, a.jper);
-        const size_t lds_m = (size_t)3 * (a.ty + 2 * nst + 2) * (S.nx27 + 4) * sizeof(double);
+        const size_t lds_m = (size_t)3 * (a.ty + 2 * halo + 2) * (S.nx27 + 4) * sizeof(double);
         k_sgs27_march<16, MPFS, MPFO><<<dim3((unsigned)(nchunks * a.ntiles)), dim3(1024), lds_m, s>>>(a);
         FAMG_CHECK_HIP(hipGetLastError());
         return;

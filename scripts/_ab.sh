@@ -1,7 +1,6 @@
 set -e
 export TMPDIR=/tmp
-R=$(pwd)
-timeout -k 10 500 rocprofv3 --kernel-trace --stats -d "$R/gpurun_out/benchprof" -o run --output-format csv -- python3 "$R/bench.py" > gpurun_out/benchprof.log 2>&1 || { tail -20 gpurun_out/benchprof.log; exit 1; }
-grep '^{' gpurun_out/benchprof.log | cut -c1-200
-bash scripts/prof_dist1.sh dist1r4
-grep '^{' gpurun_out/dist1r4.log | cut -c1-250
+timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_gpu_parity.py -m gpu -k "sgs" > gpurun_out/t_sgs.log 2>&1 || { tail -30 gpurun_out/t_sgs.log; exit 1; }
+tail -n 1 gpurun_out/t_sgs.log
+bash scripts/prof_c3.sh c3ex > /dev/null; grep -E "sgs27|per V-cycle" gpurun_out/c3ex.txt | head -2
+grep '^{' gpurun_out/c3ex.log | cut -c1-160
