@@ -1,6 +1,4 @@
 set -e
 export TMPDIR=/tmp
-timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_gpu_parity.py -m gpu -k "sgs" > gpurun_out/t_sgs.log 2>&1 || { tail -30 gpurun_out/t_sgs.log; exit 1; }
-tail -n 1 gpurun_out/t_sgs.log
-bash scripts/prof_c3.sh c3ex > /dev/null; grep -E "sgs27|per V-cycle" gpurun_out/c3ex.txt | head -2
-grep '^{' gpurun_out/c3ex.log | cut -c1-160
+FAMG_BSR_LATE=1 bash scripts/prof_c5.sh c5late > /dev/null; grep -E "bsr3|per V-cycle" gpurun_out/c5late.txt | head -8; grep -o '"value": [0-9.]*' gpurun_out/c5late.log | head -1
+FAMG_BSR_LATE=0 bash scripts/prof_c5.sh c5early > /dev/null; grep -E "bsr3|per V-cycle" gpurun_out/c5early.txt | head -8; grep -o '"value": [0-9.]*' gpurun_out/c5early.log | head -1
