@@ -193,7 +193,7 @@ amg_status amg_ctx_join_stream(amg_ctx *ctx, void *other, int32_t ctx_waits) {
 amg_status amg_set_alloc_policy(int32_t policy) {
     return guard([&] {
         FAMG_REQUIRE(policy == 0 || policy == 1, AMG_ERR_INVALID, "policy must be 0 or 1");
-        FAMG_REQUIRE(policy == 0, AMG_ERR_UNSUPPORTED,
+        FAMG_REQUIRE(policy == 0 || g_alloc_experiment > 0, AMG_ERR_UNSUPPORTED,
                      "contiguous allocations read stale data across kernels on gfx950 (DESIGN.md 3)");
         g_alloc_policy = policy;
     });

@@ -51,12 +51,19 @@ extern int g_alloc_policy;
 
 extern bool g_alloc_debug;  // FAMG_ALLOC_DEBUG=1: log large allocations to stderr
 
+// FAMG_ALLOC_EXPERIMENT (root-causing the contiguous-allocation stale reads,
+// DESIGN.md 3; never set in production): 1 = amg_set_alloc_policy(1) accepted,
+// 2 = that plus a device-wide sync after each contiguous allocation
+extern int g_alloc_experiment;
 inline void *dev_alloc(size_t bytes) {
     void *p = nullptr;
     const bool large = bytes >= (size_t(16) << 20);
     if (g_alloc_policy == 1 && large) {
         if (hipExtMallocWithFlags(&p, bytes, hipDeviceMallocContiguous) == hipSuccess && p) {
             if (g_alloc_debug) fprintf(stderr, "famg alloc contiguous %p %zu\n", p, bytes);
+            // root-cause experiment (scripts/alloc_coherence.py): 2 = device-wide
+            // sync right after the allocation, before any kernel touches it
+            if (g_alloc_experiment == 2) FAMG_CHECK_HIP(hipDeviceSynchronize());
             return p;
         }
         (void)hipGetLastError();

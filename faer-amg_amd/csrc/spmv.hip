@@ -36,6 +36,10 @@ typedef int32_t i32x4_t __attribute__((ext_vector_type(4)));
 int g_spmv_format_policy = 0;
 int g_value_codes = 1;
 int g_alloc_policy = 0;
+int g_alloc_experiment = [] {
+    const char *e = getenv("FAMG_ALLOC_EXPERIMENT");
+    return e ? atoi(e) : 0;
+}();
 bool g_alloc_debug = [] {
     const char *e = getenv("FAMG_ALLOC_DEBUG");
     return e && e[0] == '1';

@@ -1,7 +1,14 @@
 set -e
 export TMPDIR=/tmp
-timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_gpu_parity.py tests/test_gpu_dist.py -m gpu -k "gtc or grid_transfer or setdf or transfer or constant_diagonal or slab or one_rank or vcycle_256" > gpurun_out/t_gtc.log 2>&1 || { tail -30 gpurun_out/t_gtc.log; exit 1; }
-tail -n 1 gpurun_out/t_gtc.log
-bash scripts/prof_c2.sh c2xp2 > /dev/null; grep -E "gtc_interp|per V-cycle" gpurun_out/c2xp2.txt | head -3
-FAMG_GTC_XP=1 bash scripts/prof_c2.sh c2xp1 > /dev/null; grep -E "gtc_interp|per V-cycle" gpurun_out/c2xp1.txt | head -3
-bash scripts/prof_c3.sh c3xp2 > /dev/null; grep -E "gtc_interp|per V-cycle" gpurun_out/c3xp2.txt | head -3
+cat > /tmp/ac.py <<'PY'
+import os, sys
+import torch
+torch.zeros(1, device="cuda:0")
+sys.argv = ["x", os.environ.get("BUILDS", "4"), "0"]
+sys.path[:0] = ["faer-amg_amd", "oracle"]
+import faer_amg_amd as fa
+fa.set_alloc_policy(int(os.environ.get("POLICY", "1")))
+src = open("scripts/alloc_coherence.py").read().replace("dims = (64, 64, 64)", "dims = (%s,)" % os.environ.get("DIMS", "64, 64, 64"))
+exec(src)
+PY
+echo "== 128^3 contiguous"; DIMS="128, 128, 128" FAMG_ALLOC_DEBUG=1 FAMG_ALLOC_EXPERIMENT=1 FAMG_CHECK_STORAGE=1 timeout -k 10 400 python /tmp/ac.py > gpurun_out/ac1.log 2>&1 || true; echo "contiguous allocs: $(grep -c 'alloc contiguous' gpurun_out/ac1.log)"; grep -E "^build|mismatch|Error" gpurun_out/ac1.log | head -6
