@@ -47,6 +47,7 @@ struct SellpArgs {
     const double *d;
     const uint8_t *dc;
     const double *dt;
+    double *y2;  // SETDF: y2 = d * y (the next level's first Jacobi step from zero)
 };
 
 template <int MODE> __device__ __forceinline__ double sellp_x(const SellpArgs &a, int c) { return a.x[c]; }
@@ -111,6 +112,7 @@ __device__ __forceinline__ void sellp_slice(const SellpArgs &a, const double *st
             br = a.b[row];
             dr = a.dc ? a.dt[a.dc[row]] : a.d[row];
         }
+        if constexpr (MODE == SPMV_SETDF) dr = a.dc ? a.dt[a.dc[row]] : a.d[row];
     }
     const int2 pw = a.pat[s];
     const int32_t *off = a.offs + pw.x;
@@ -141,7 +143,10 @@ __device__ __forceinline__ void sellp_slice(const SellpArgs &a, const double *st
     for (int m = L / 2; m > 0; m >>= 1) acc += __shfl_xor(acc, m);
     if (live && q == 0) {
         if constexpr (MODE == SPMV_SET) a.y[row] = acc;
-        else if constexpr (MODE == SPMV_ADD || MODE == SPMV_ADD0) a.y[row] = yr + acc;
+        else if constexpr (MODE == SPMV_SETDF) {
+            a.y[row] = acc;
+            a.y2[row] = dr * acc;  // vec_mul(_coded)'s product
+        } else if constexpr (MODE == SPMV_ADD || MODE == SPMV_ADD0) a.y[row] = yr + acc;
         else if constexpr (MODE == SPMV_RESID) a.y[row] = br - acc;
         else a.y[row] = xr + dr * (br - acc);  // JACOBI
     }
@@ -372,7 +377,9 @@ void spmv_sellp(const GpuCsr &m, const double *x, double *y, SpmvMode mode, cons
     if (s1 <= s0) return;
     SellpArgs a{m.sellp_vals.get(), m.sellp_eoff.get(), m.sellp_row0.get(),
                 reinterpret_cast<const int2 *>(m.sellp_pat.get()), m.sellp_offs.get(), m.sellp_rbase.get(), m.sellp_vtab.get(), (int32_t)m.sellp_ntab,
-                (int32_t)s0, (int32_t)(s1 - s0), (int32_t)m.ncols, sellp_w2_enabled(), sellp_spw(), x, y, epi.b, epi.d, epi.dc, epi.dt};
+                (int32_t)s0, (int32_t)(s1 - s0), (int32_t)m.ncols, sellp_w2_enabled(), sellp_spw(), x, y, epi.b, epi.d, epi.dc, epi.dt,
+                epi.y2};
+    FAMG_REQUIRE(mode != SPMV_SETDF || (epi.y2 && (epi.d || epi.dc)), AMG_ERR_INVALID, "SETDF needs y2 and d");
     const dim3 grid((unsigned)ceil_div(s1 - s0, 4 * (int64_t)a.spw)), block(256);
 #define FAMG_SELLP(L, VB)                                                                          \
     switch (mode) {                                                                                \
@@ -381,6 +388,7 @@ void spmv_sellp(const GpuCsr &m, const double *x, double *y, SpmvMode mode, cons
     case SPMV_RESID: spmv_sellp_kernel<SPMV_RESID, L, VB><<<grid, block, 0, s>>>(a); break;        \
     case SPMV_JACOBI: spmv_sellp_kernel<SPMV_JACOBI, L, VB><<<grid, block, 0, s>>>(a); break;      \
     case SPMV_ADD0: spmv_sellp_kernel<SPMV_ADD0, L, VB><<<grid, block, 0, s>>>(a); break;          \
+    case SPMV_SETDF: spmv_sellp_kernel<SPMV_SETDF, L, VB><<<grid, block, 0, s>>>(a); break;        \
     default: fail(AMG_ERR_UNSUPPORTED, "pattern SELL: unsupported SpMV epilogue");                 \
     }
 #define FAMG_SELLP_VB(L)                                                                           \

@@ -2531,7 +2531,8 @@ void spmv(const GpuCsr &m, const double *x, double *y, SpmvMode mode, const Spmv
         spmv_gtc(m, x, y, mode, epi, s, seg);
         return;
     }
-    FAMG_REQUIRE(mode != SPMV_SETDF, AMG_ERR_UNSUPPORTED, "SETDF needs a grid-transfer restriction");
+    FAMG_REQUIRE(mode != SPMV_SETDF || m.kernel == SPMV_KERNEL_SELLP, AMG_ERR_UNSUPPORTED,
+                 "SETDF needs a grid-transfer or pattern-SELL restriction");
     if (m.kernel == SPMV_KERNEL_BSR) {
         FAMG_REQUIRE(mode != SPMV_SGS, AMG_ERR_UNSUPPORTED, "block storage has no SGS sweep");
         spmv_bsr(m, x, y, mode, epi, s, seg);
