@@ -551,7 +551,9 @@ bool fold_level(const CsrOp *A, const DiagOp *D, const CsrOp *P, bool fold_zero_
     const bool fold_xscs = flag(FLAG_FOLD_XSCS) != 0;
     const bool p_add0 = P && (P->m.kernel == SPMV_KERNEL_SELL || P->m.kernel == SPMV_KERNEL_SELLP ||
                               P->m.kernel == SPMV_KERNEL_STREAM || P->m.kernel == SPMV_KERNEL_VECTOR || P->m.gtc_on);
-    return fold_zero_guess && v_zero && steps == 1 && A && D && P &&
+    // every fold writes the correction d*f + P v_c with P's ADD0 epilogue (the 3x3-block
+    // kernel has none: a level with a block-stored P never folds)
+    return fold_zero_guess && v_zero && steps == 1 && A && D && P && p_add0 &&
                       ((A->m.kernel == SPMV_KERNEL_SELL && A->m.sell_vbits == 0 && gather_cheap) ||
                        A->m.kernel == SPMV_KERNEL_XS ||  // x-staged: d*x staged with x, no extra gather
                        (fold_xscs && A->m.kernel == SPMV_KERNEL_SCS && A->m.xscs && p_add0) ||
