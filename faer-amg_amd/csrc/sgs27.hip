@@ -526,6 +526,69 @@ __global__ void k_sgs27_const(const uint32_t *codes, int cw, Sgs27Const c, int n
     }
 }
 
+// A 27-point DIA operator (whole matrix, offsets of an nx x ny x nz grid, nx
+// even) whose every row is the interior row's code group with the entries
+// leaving the grid cleared to the +0.0 code (code 0): the SpMV can use the
+// interior coefficients and zero the x operands that leave the grid instead of
+// decoding each row's codes (spmv_dia_pat_kernel CST: the same products, the
+// cleared ones +-0.0 added to an accumulator that is never -0.0).
+bool dia27_constant(GpuCsr &m) {
+    m.dia_cst27 = false;
+    if (!m.has_dia() || m.dia_rowid || m.dia_r0 != 0 || m.dia_r1 != m.nrows || m.dia_k != 27 || m.nrows != m.ncols)
+        return false;
+    if (!((m.dia_vbits == 4 && m.dia_cw == 4) || (m.dia_vbits == 8 && m.dia_cw == 8))) return false;
+    const std::vector<int> &off = m.dia_off;
+    const int64_t nx = off[16], pl = off[22];
+    if (nx < 2 || (nx & 1) || pl <= 0 || pl % nx != 0 || m.nrows % pl != 0) return false;
+    const int64_t ny = pl / nx, nz = m.nrows / pl;
+    for (int k = 0; k < 27; k++) {
+        const int dx = k % 3 - 1, dy = (k / 3) % 3 - 1, dz = k / 9 - 1;
+        if (off[k] != dz * pl + dy * nx + dx) return false;
+    }
+    hipStream_t s = m.ctx->stream;
+    std::vector<double> tab(m.dia_ntab);
+    FAMG_CHECK_HIP(hipMemcpyAsync(tab.data(), m.dia_vtab.get(), tab.size() * 8, hipMemcpyDeviceToHost, s));
+    FAMG_CHECK_HIP(hipStreamSynchronize(s));
+    uint64_t bits0 = 1;
+    if (!tab.empty()) std::memcpy(&bits0, &tab[0], 8);
+    if (bits0 != 0) return false;  // code 0 must be +0.0
+    const int64_t ic = ((nz / 2) * ny + ny / 2) * nx + nx / 2;
+    std::vector<uint32_t> w(m.dia_cw);
+    FAMG_CHECK_HIP(hipMemcpyAsync(w.data(), m.dia_codes.get() + ic * m.dia_cw, m.dia_cw * 4, hipMemcpyDeviceToHost, s));
+    FAMG_CHECK_HIP(hipStreamSynchronize(s));
+    const uint32_t mask = (1u << m.dia_vbits) - 1;
+    Sgs27Const c;
+    for (int q = 0; q < 8; q++) c.icode[q] = q < m.dia_cw ? w[q] : 0xffffffffu;
+    for (int f = 0; f < 6; f++)
+        for (int q = 0; q < 8; q++) c.fmask[f][q] = 0;
+    for (int k = 0; k < 27; k++) {
+        const int dx = k % 3 - 1, dy = (k / 3) % 3 - 1, dz = k / 9 - 1;
+        const uint32_t b = mask << ((k * m.dia_vbits) & 31);
+        const int q = (k * m.dia_vbits) >> 5;
+        if (dx < 0) c.fmask[0][q] |= b;
+        if (dx > 0) c.fmask[1][q] |= b;
+        if (dy < 0) c.fmask[2][q] |= b;
+        if (dy > 0) c.fmask[3][q] |= b;
+        if (dz < 0) c.fmask[4][q] |= b;
+        if (dz > 0) c.fmask[5][q] |= b;
+    }
+    DevBuf<int> bad(1);
+    FAMG_CHECK_HIP(hipMemsetAsync(bad.get(), 0, sizeof(int), s));
+    hipLaunchKernelGGL(k_sgs27_const, dim3((unsigned)ceil_div(m.nrows, 256)), dim3(256), 0, s, m.dia_codes.get(),
+                       m.dia_cw, c, (int)nx, (int)ny, (int)nz, bad.get());
+    FAMG_CHECK_HIP(hipGetLastError());
+    int hb = 1;
+    FAMG_CHECK_HIP(hipMemcpyAsync(&hb, bad.get(), sizeof(int), hipMemcpyDeviceToHost, s));
+    FAMG_CHECK_HIP(hipStreamSynchronize(s));
+    if (hb) return false;
+    for (int k = 0; k < 27; k++) m.dia_cst[k] = tab[(w[(k * m.dia_vbits) >> 5] >> ((k * m.dia_vbits) & 31)) & mask];
+    m.dia_cst_n[0] = (int)nx;
+    m.dia_cst_n[1] = (int)ny;
+    m.dia_cst_n[2] = (int)nz;
+    m.dia_cst27 = true;
+    return true;
+}
+
 // Decide whether S's sweeps can run as fused plane-parity phases: A is stored
 // as DIA codes (whole matrix) with the 27 offsets of an nx x ny x nz grid, the
 // colouring is the parity colouring, and every entry that would leave the grid

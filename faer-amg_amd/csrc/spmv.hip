@@ -1017,6 +1017,8 @@ struct DiaArgs {
     int32_t band_bp;    // > 0: 512-row blocks per plane; XCD x walks band x of every plane
     int32_t off[DIA_MAX];
     Epi e;
+    int32_t gnx, gny, gnz;  // CST: the grid (nx even)
+    double cst[27];         // CST: the interior stencil
 };
 
 typedef int32_t i32x2u_t __attribute__((ext_vector_type(2), aligned(4)));
@@ -1345,7 +1347,11 @@ __device__ __forceinline__ void dia_pat_loads(const DiaArgs &a, int row, double 
     }
 }
 
-template <int MODE, int VB, int CW, int PAT>
+// CST (PAT 27, dia27_constant): no codes; the interior coefficients from the
+// arguments and the x operands of neighbours outside the grid taken as 0.0 (the
+// coded rows hold the +0.0 code there: the same products up to the sign of a
+// zero, added to an accumulator that is never -0.0 -- bitwise equal)
+template <int MODE, int VB, int CW, int PAT, bool CST = false>
 __global__ __launch_bounds__(256) void spmv_dia_pat_kernel(DiaArgs a) {
     constexpr bool DC = MODE == DIA_JACOBI_DC;
     constexpr int GM = DC ? SPMV_JACOBI : MODE;
@@ -1369,7 +1375,7 @@ __global__ __launch_bounds__(256) void spmv_dia_pat_kernel(DiaArgs a) {
     ep.load_codes(a.e, row, a.row_end);
     ep.load(a.e, row, a.row_end);
     uint32_t u[2 * CW];
-    {
+    if constexpr (!CST) {
         const uint32_t *cp = a.codes + (int64_t)(min(row, a.row_end - 1) - a.code_row0) * CW;
 #pragma unroll
         for (int q = 0; q < (2 * CW) / 4; q++) {
@@ -1399,7 +1405,25 @@ __global__ __launch_bounds__(256) void spmv_dia_pat_kernel(DiaArgs a) {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
     if (row >= a.row_end) return;
     double acc0 = 0.0, acc1 = 0.0;
-    {
+    if constexpr (CST) {
+        static_assert(PAT == 27, "constant stencils: the 27-point pattern");
+        const int q = row / a.gnx, gx = row - q * a.gnx;  // row even, nx even: the pair shares its grid row
+        const int gz = q / a.gny, gy = q - gz * a.gny;
+        const bool xlo = gx == 0, xhi = gx + 2 == a.gnx;
+#pragma unroll
+        for (int j = 0; j < 9; j++) {
+            const int dz = j / 3 - 1, dy = j % 3 - 1;
+            const bool ok = (unsigned)(gy + dy) < (unsigned)a.gny && (unsigned)(gz + dz) < (unsigned)a.gnz;
+#pragma unroll
+            for (int m = 0; m < 3; m++) {
+                const int k = 3 * j + m;
+                const double x0 = ok && !(m == 0 && xlo) ? xv[4 * j + m] : 0.0;
+                const double x1 = ok && !(m == 2 && xhi) ? xv[4 * j + m + 1] : 0.0;
+                acc0 = fma(a.cst[k], x0, acc0);
+                acc1 = fma(a.cst[k], x1, acc1);
+            }
+        }
+    } else {
         int kd = 0, vo = 0;
 #pragma unroll
         for (int j = 0; j < NRUN; j++) {
@@ -1414,6 +1438,15 @@ __global__ __launch_bounds__(256) void spmv_dia_pat_kernel(DiaArgs a) {
         }
     }
     ep.store(a.e, sdt, acc0, acc1);
+}
+
+// FAMG_DIA_CST=0: a constant 27-point stencil still reads its rows' codes
+static bool dia_cst_enabled() {
+    static const bool on = [] {
+        const char *e = getenv("FAMG_DIA_CST");
+        return !(e && e[0] == '0');
+    }();
+    return on;
 }
 
 // A/B switch FAMG_DIA_PAT=0: no DIA storage for more than 32 diagonals
@@ -2481,7 +2514,7 @@ static void log_spmv(const GpuCsr &m, SpmvMode mode, const SpmvEpi &epi, int64_t
     } else if (m.kernel == SPMV_KERNEL_DIA || (m.has_dia() && !m.dia_rowid && seg >= 0 && seg == m.dia_seg)) {
         kernel = SPMV_KERNEL_DIA;
         name = (m.dia_pat || (m.dia_k == 27 && dia_runs() && dia_pat27())) ? "dia_pat" : "dia";
-        mat = dia_bytes;
+        mat = (m.dia_cst27 && seg < 0 && dia_cst_enabled()) ? 27 * 8 : dia_bytes;  // CST: no codes read
     } else if (m.kernel == SPMV_KERNEL_SELL) {
         name = (m.sell_short && seg < 0 && mode != SPMV_SGS && mode != SPMV_RESID0 && sell_short_enabled())
                    ? "sell_short" : "sell";
@@ -2633,7 +2666,16 @@ void spmv(const GpuCsr &m, const double *x, double *y, SpmvMode mode, const Spmv
         const int runs9i = runs9 ? 9 : run7 ? -1 : 0;
         const int pat = m.dia_pat ? m.dia_pat : runs9 && dia_pat27() && (key == 4 * 16 + 4 || key == 8 * 16 + 8) ? 27 : 0;
         if (pat) {
-#define FAMG_DIAP2(M, VB, CW, P) spmv_dia_pat_kernel<M, VB, CW, P><<<grid, block, 0, s>>>(a);
+        const bool cst = pat == 27 && m.dia_cst27 && seg < 0 && dia_cst_enabled();
+        if (cst) {
+            a.gnx = m.dia_cst_n[0];
+            a.gny = m.dia_cst_n[1];
+            a.gnz = m.dia_cst_n[2];
+            for (int k = 0; k < 27; k++) a.cst[k] = m.dia_cst[k];
+        }
+#define FAMG_DIAP2(M, VB, CW, P)                                                                  \
+    if (cst) spmv_dia_pat_kernel<M, VB, CW, P, (P == 27)><<<grid, block, 0, s>>>(a);              \
+    else spmv_dia_pat_kernel<M, VB, CW, P><<<grid, block, 0, s>>>(a);
 #define FAMG_DIAP(VB, CW, P)                                                                        \
     switch (mode) {                                                                               \
     case SPMV_SET: FAMG_DIAP2(SPMV_SET, VB, CW, P) break;                                            \

@@ -1,3 +1,6 @@
 set -e
 export TMPDIR=/tmp
-for w in 64 40; do FAMG_BSR_MAXW=$w bash scripts/prof_c5.sh c5w$w > /dev/null; echo "== maxw $w"; sed -n '/per launch/,$p' gpurun_out/c5w$w.txt | head -20; grep -o '"value": [0-9.]*' gpurun_out/c5w$w.log | head -1; done
+timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_gpu_parity.py -m gpu -k "dia27 or 27pt or sgs27 or dia_codes or dia" > gpurun_out/t_cst.log 2>&1 || { tail -30 gpurun_out/t_cst.log; exit 1; }
+tail -n 1 gpurun_out/t_cst.log
+bash scripts/prof_c3.sh c3cst > /dev/null; grep -E "dia_pat|per V-cycle" gpurun_out/c3cst.txt | head -3
+FAMG_DIA_CST=0 bash scripts/prof_c3.sh c3nocst > /dev/null; grep -E "dia_pat|per V-cycle" gpurun_out/c3nocst.txt | head -3

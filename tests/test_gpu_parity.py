@@ -1178,6 +1178,18 @@ def _epilogues_bitwise(ctx, M, seed):
         assert np.array_equal(H(yd), ref), (mode, M.spmv_info())
 
 
+@pytest.mark.parametrize("dims", [(66, 40, 33), (48, 45, 41)])
+def test_dia27_constant_stencil_bitwise(ctx, dims):
+    """The 27-point constant stencil truncated at the grid faces (aniso27) on DIA
+    storage runs the pattern kernel without codes (spmv_dia_pat_kernel CST: the
+    interior coefficients, x operands outside the grid taken as 0.0): all four
+    epilogues bitwise equal to the oracle's row sums, odd y/z extents included."""
+    A = fa().SparseMatOp.aniso27(ctx, *dims, 1.0, 1.0, 0.01)
+    if A.spmv_info()["kernel"] != "dia":
+        pytest.skip("operator not stored as DIA codes")
+    _epilogues_bitwise(ctx, A, 77)
+
+
 def test_xstaged_stencil_classes(ctx):
     """x-staged stencil classes (scs.hip spmv_xscs_kernel): the coarse operators
     of box hierarchies on a grid (7-pt 128^3: A_2 = 32^3 with 13^3 classes and
