@@ -339,8 +339,8 @@ void csr_finalize(GpuCsr &m, const std::vector<int64_t> *segments) {
         m.sell_mode_slices[0] = m.sell_mode_slices[1] = m.sell_mode_slices[2] = 0;
     }
     choose_kernel(m);
-    m.dia_cst27 = false;
-    if (m.kernel == SPMV_KERNEL_DIA) dia27_constant(m);
+    m.dia_cst = false;
+    if (m.kernel == SPMV_KERNEL_DIA) dia_constant(m);
     if (storage_check_enabled()) storage_check(m);
 }
 

@@ -101,11 +101,11 @@ struct GpuCsr {
     int64_t dia_ntab = 0;
     int dia_k = 0, dia_cw = 0, dia_vbits = 0;
     int dia_pat = 0;  // > 32 diagonals: the run pattern (spmv_dia_pat_kernel)
-    // 27-point DIA operator whose every row is the interior stencil truncated at the
-    // grid faces (dia27_constant): the pattern kernel reads no codes
-    bool dia_cst27 = false;
+    // 7- or 27-point DIA operator whose every row is the interior stencil truncated
+    // at the grid faces (dia_constant): the kernels read no codes
+    bool dia_cst = false;
     int dia_cst_n[3] = {0, 0, 0};
-    double dia_cst[27] = {0};
+    double dia_cst_v[27] = {0};
     std::vector<int> dia_off;
     // DIA row range: the whole matrix (kernel == DIA) or one row segment
     // (dia_seg, e.g. the halo interior of a distributed level) beside SELL
@@ -199,7 +199,7 @@ struct GpuCsr {
     int64_t index_bytes() const { return 12 * nnz + 4 * (nrows + 1); }
     // matrix bytes one SpMV streams with the chosen kernel (data + metadata)
     int64_t stream_bytes() const {
-        if (kernel == 3) return 4 * dia_cw * nrows + 8 * dia_ntab;
+        if (kernel == 3) return dia_cst ? 8 * (int64_t)dia_k : 4 * dia_cw * nrows + 8 * dia_ntab;  // constant: no codes
         if (kernel == 4) return bsr_steps * (64 * 76) + 8 * (bsr_slices + 1);
         if (kernel == 5) return sellp_stream;
         if (kernel == 6) return scs_ib * nrows + 8 * scs_k * scs_nclass + 4 * scs_k;
@@ -522,9 +522,9 @@ struct MultigridOp : LinOp {
 };
 
 // the zero-guess fold decision of one level (RESID0 + ADD0 instead of v = d*f)
-// m's DIA codes are a constant 27-point stencil on an nx x ny x nz grid (nx even),
-// truncated at the faces: fills m.dia_cst* (sgs27.hip)
-bool dia27_constant(GpuCsr &m);
+// m's DIA codes are a constant 7- or 27-point stencil on an nx x ny x nz grid (nx
+// even), truncated at the faces: fills m.dia_cst* (sgs27.hip)
+bool dia_constant(GpuCsr &m);
 bool fold_level(const CsrOp *A, const DiagOp *D, const CsrOp *P, bool fold_zero_guess, bool v_zero, int64_t steps);
 // the restriction into a level writes that level's first Jacobi step from zero
 // (SPMV_SETDF) -- false with FAMG_SETDF=0

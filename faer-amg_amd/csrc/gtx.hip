@@ -325,12 +325,17 @@ int gtx_mode() {
     return v;
 }
 
-// flag FLAG_GTX_TIME (FAMG_GTX_TIME=0, amg_set_flag(3, 0)): keep the classes
-// without timing them against the storage underneath
-static bool gtx_time_enabled() { return flag(FLAG_GTX_TIME) != 0; }
-
+// flag FLAG_GTX_TIME (FAMG_GTX_TIME, amg_set_flag(3, v)): 0 = keep the classes
+// wherever they build; 1 = time them against the storage underneath; 2 (default)
+// = keep them on transfer operators of >= 2^18 rows (P: fine rows, R: coarse
+// rows), the levels where the timing chose them on the 256^3 cycles (P_1, R_1,
+// P_2) -- deterministic, so two builds of one hierarchy take the same storages
+// (the timing could flip on noise between a 2-lane pattern SELL and the classes,
+// whose row sums differ in rounding)
 static bool gtx_beats_storage(GpuCsr &m) {
-    if (!gtx_time_enabled() || gtx_mode() == 2) return true;
+    const int64_t how = flag(FLAG_GTX_TIME);
+    if (how == 0 || gtx_mode() == 2) return true;
+    if (how != 1) return m.nrows >= (int64_t(1) << 18);
     // R of the small levels (<= 65536 coarse rows of hundreds of entries) loses in the cycle
     // even where an isolated timing has it ahead (R_2 of the 256^3 cycle: 32.5 vs 21.9 + 4.6 us)
     if (m.gtx_r && m.nrows <= 65536) return false;

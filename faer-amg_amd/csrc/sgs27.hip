@@ -526,25 +526,36 @@ __global__ void k_sgs27_const(const uint32_t *codes, int cw, Sgs27Const c, int n
     }
 }
 
-// A 27-point DIA operator (whole matrix, offsets of an nx x ny x nz grid, nx
-// even) whose every row is the interior row's code group with the entries
+// A 7- or 27-point DIA operator (whole matrix, offsets of an nx x ny x nz grid,
+// nx even) whose every row is the interior row's code group with the entries
 // leaving the grid cleared to the +0.0 code (code 0): the SpMV can use the
 // interior coefficients and zero the x operands that leave the grid instead of
-// decoding each row's codes (spmv_dia_pat_kernel CST: the same products, the
+// decoding each row's codes (the CST DIA kernels: the same products, the
 // cleared ones +-0.0 added to an accumulator that is never -0.0).
-bool dia27_constant(GpuCsr &m) {
-    m.dia_cst27 = false;
-    if (!m.has_dia() || m.dia_rowid || m.dia_r0 != 0 || m.dia_r1 != m.nrows || m.dia_k != 27 || m.nrows != m.ncols)
+bool dia_constant(GpuCsr &m) {
+    m.dia_cst = false;
+    const int K = m.dia_k;
+    if (!m.has_dia() || m.dia_rowid || m.dia_r0 != 0 || m.dia_r1 != m.nrows || (K != 27 && K != 7) ||
+        m.nrows != m.ncols || m.dia_pat)
         return false;
-    if (!((m.dia_vbits == 4 && m.dia_cw == 4) || (m.dia_vbits == 8 && m.dia_cw == 8))) return false;
+    if (K == 27 && !((m.dia_vbits == 4 && m.dia_cw == 4) || (m.dia_vbits == 8 && m.dia_cw == 8))) return false;
+    if (K * m.dia_vbits > 32 * m.dia_cw || m.dia_cw > 8) return false;
+    // the grid steps of diagonal k
+    int st[27][3];
+    for (int k = 0; k < K; k++) {
+        if (K == 27) {
+            st[k][0] = k % 3 - 1; st[k][1] = (k / 3) % 3 - 1; st[k][2] = k / 9 - 1;
+        } else {
+            static const int s7[7][3] = {{0, 0, -1}, {0, -1, 0}, {-1, 0, 0}, {0, 0, 0}, {1, 0, 0}, {0, 1, 0}, {0, 0, 1}};
+            for (int q = 0; q < 3; q++) st[k][q] = s7[k][q];
+        }
+    }
     const std::vector<int> &off = m.dia_off;
-    const int64_t nx = off[16], pl = off[22];
+    const int64_t nx = K == 27 ? off[16] : off[5], pl = K == 27 ? off[22] : off[6];
     if (nx < 2 || (nx & 1) || pl <= 0 || pl % nx != 0 || m.nrows % pl != 0) return false;
     const int64_t ny = pl / nx, nz = m.nrows / pl;
-    for (int k = 0; k < 27; k++) {
-        const int dx = k % 3 - 1, dy = (k / 3) % 3 - 1, dz = k / 9 - 1;
-        if (off[k] != dz * pl + dy * nx + dx) return false;
-    }
+    for (int k = 0; k < K; k++)
+        if (off[k] != st[k][2] * pl + st[k][1] * nx + st[k][0]) return false;
     hipStream_t s = m.ctx->stream;
     std::vector<double> tab(m.dia_ntab);
     FAMG_CHECK_HIP(hipMemcpyAsync(tab.data(), m.dia_vtab.get(), tab.size() * 8, hipMemcpyDeviceToHost, s));
@@ -561,8 +572,8 @@ bool dia27_constant(GpuCsr &m) {
     for (int q = 0; q < 8; q++) c.icode[q] = q < m.dia_cw ? w[q] : 0xffffffffu;
     for (int f = 0; f < 6; f++)
         for (int q = 0; q < 8; q++) c.fmask[f][q] = 0;
-    for (int k = 0; k < 27; k++) {
-        const int dx = k % 3 - 1, dy = (k / 3) % 3 - 1, dz = k / 9 - 1;
+    for (int k = 0; k < K; k++) {
+        const int dx = st[k][0], dy = st[k][1], dz = st[k][2];
         const uint32_t b = mask << ((k * m.dia_vbits) & 31);
         const int q = (k * m.dia_vbits) >> 5;
         if (dx < 0) c.fmask[0][q] |= b;
@@ -572,6 +583,7 @@ bool dia27_constant(GpuCsr &m) {
         if (dz < 0) c.fmask[4][q] |= b;
         if (dz > 0) c.fmask[5][q] |= b;
     }
+    // code bits past the K diagonals must match too (they are the +0.0 padding)
     DevBuf<int> bad(1);
     FAMG_CHECK_HIP(hipMemsetAsync(bad.get(), 0, sizeof(int), s));
     hipLaunchKernelGGL(k_sgs27_const, dim3((unsigned)ceil_div(m.nrows, 256)), dim3(256), 0, s, m.dia_codes.get(),
@@ -581,11 +593,11 @@ bool dia27_constant(GpuCsr &m) {
     FAMG_CHECK_HIP(hipMemcpyAsync(&hb, bad.get(), sizeof(int), hipMemcpyDeviceToHost, s));
     FAMG_CHECK_HIP(hipStreamSynchronize(s));
     if (hb) return false;
-    for (int k = 0; k < 27; k++) m.dia_cst[k] = tab[(w[(k * m.dia_vbits) >> 5] >> ((k * m.dia_vbits) & 31)) & mask];
+    for (int k = 0; k < K; k++) m.dia_cst_v[k] = tab[(w[(k * m.dia_vbits) >> 5] >> ((k * m.dia_vbits) & 31)) & mask];
     m.dia_cst_n[0] = (int)nx;
     m.dia_cst_n[1] = (int)ny;
     m.dia_cst_n[2] = (int)nz;
-    m.dia_cst27 = true;
+    m.dia_cst = true;
     return true;
 }
 

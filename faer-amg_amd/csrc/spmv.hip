@@ -1183,7 +1183,10 @@ __device__ __forceinline__ void dia_gx4(const Epi &e, int c, int ncols, double (
 // consecutive values, two 16-B loads instead of three and 4 NR instead of 2 KMAX
 // registers.  NR = -1: the 7-point pattern (single, single, run of three,
 // single, single).  The row sums run over the same diagonals in the same order.
-template <int MODE, int VB, int CW, bool NT, int NR = 0>
+// CST (7-point run kernel, dia_constant): no codes, the interior coefficients
+// from the arguments, x operands of neighbours outside the grid taken as 0.0
+// (bitwise the coded sums, as spmv_dia_pat_kernel CST)
+template <int MODE, int VB, int CW, bool NT, int NR = 0, bool CST = false>
 __global__ __launch_bounds__(256) void spmv_dia_kernel(DiaArgs a) {
     constexpr bool DC = MODE == DIA_JACOBI_DC;
     constexpr bool RC = MODE == DIA_RESID0_DC && NR == -1;  // coded d gathered beside x
@@ -1218,7 +1221,8 @@ __global__ __launch_bounds__(256) void spmv_dia_kernel(DiaArgs a) {
     double x0[KX], x1[KX], xq[NRX][4];
     ep.load_codes(a.e, row, a.row_end);
     ep.load(a.e, row, a.row_end);
-    dia_codes2<CW>(a.codes + (int64_t)(min(row, a.row_end - 1) - a.code_row0) * CW, w0, w1);
+    static_assert(!CST || NR == -1, "constant stencils: the 7-point run kernel");
+    if constexpr (!CST) dia_codes2<CW>(a.codes + (int64_t)(min(row, a.row_end - 1) - a.code_row0) * CW, w0, w1);
     double xs7[4][2];  // NR == -1 (7-point): the four single diagonals
     uint32_t ks7[4][2], kq[4];  // RC: their codes of d
     if constexpr (RC) {
@@ -1265,7 +1269,22 @@ __global__ __launch_bounds__(256) void spmv_dia_kernel(DiaArgs a) {
     }
     if constexpr (JK) ep.dr = dbl2_t{dk, dk};
     double acc0 = 0.0, acc1 = 0.0;
-    if constexpr (NR == -1) {
+    if constexpr (NR == -1 && CST) {
+        // diagonals z-1, y-1, x-1, 0, x+1, y+1, z+1; the row pair shares its grid row
+        const int q = row / a.gnx, gx = row - q * a.gnx;
+        const int gz = q / a.gny, gy = q - gz * a.gny;
+        const bool zlo = gz > 0, ylo = gy > 0, yhi = gy < a.gny - 1, zhi = gz < a.gnz - 1;
+        const bool xlo = gx > 0, xhi = gx + 2 < a.gnx;
+#pragma unroll
+        for (int k = 0; k < 7; k++) {
+            const double y0 = k < 2 ? xs7[k][0] : k < 5 ? xq[0][k - 2] : xs7[k - 3][0];
+            const double y1 = k < 2 ? xs7[k][1] : k < 5 ? xq[0][k - 1] : xs7[k - 3][1];
+            const bool in = k == 0 ? zlo : k == 1 ? ylo : k == 5 ? yhi : k == 6 ? zhi : true;
+            const bool in0 = in && (k != 2 || xlo), in1 = in && (k != 4 || xhi);
+            acc0 = fma(a.cst[k], in0 ? y0 : 0.0, acc0);
+            acc1 = fma(a.cst[k], in1 ? y1 : 0.0, acc1);
+        }
+    } else if constexpr (NR == -1) {
 #pragma unroll
         for (int k = 0; k < 7; k++) {
             const double y0 = k < 2 ? xs7[k][0] : k < 5 ? xq[0][k - 2] : xs7[k - 3][0];
@@ -1347,7 +1366,7 @@ __device__ __forceinline__ void dia_pat_loads(const DiaArgs &a, int row, double 
     }
 }
 
-// CST (PAT 27, dia27_constant): no codes; the interior coefficients from the
+// CST (PAT 27, dia_constant): no codes; the interior coefficients from the
 // arguments and the x operands of neighbours outside the grid taken as 0.0 (the
 // coded rows hold the +0.0 code there: the same products up to the sign of a
 // zero, added to an accumulator that is never -0.0 -- bitwise equal)
@@ -2384,7 +2403,13 @@ void spmm(const GpuCsr &m, const double *x, int64_t ldx, double *y, int64_t ldy,
 }
 
 template <int M, int VB, int CW>
-static void launch_dia(int runs, bool nt, dim3 grid, dim3 block, hipStream_t s, const DiaArgs &a) {
+static void launch_dia(int runs, bool nt, dim3 grid, dim3 block, hipStream_t s, const DiaArgs &a, bool cst = false) {
+    if constexpr (CW * 32 / VB >= 7) {
+        if (runs == -1 && cst) {  // constant 7-point stencil: no codes
+            spmv_dia_kernel<M, VB, CW, false, -1, true><<<grid, block, 0, s>>>(a);
+            return;
+        }
+    }
     if constexpr (M == DIA_JACOBI_DK || M == DIA_RESID0_DK) {  // chosen only for the 7-point run kernel
         if constexpr (CW * 32 / VB >= 7) {
             if (runs == -1) {
@@ -2514,7 +2539,7 @@ static void log_spmv(const GpuCsr &m, SpmvMode mode, const SpmvEpi &epi, int64_t
     } else if (m.kernel == SPMV_KERNEL_DIA || (m.has_dia() && !m.dia_rowid && seg >= 0 && seg == m.dia_seg)) {
         kernel = SPMV_KERNEL_DIA;
         name = (m.dia_pat || (m.dia_k == 27 && dia_runs() && dia_pat27())) ? "dia_pat" : "dia";
-        mat = (m.dia_cst27 && seg < 0 && dia_cst_enabled()) ? 27 * 8 : dia_bytes;  // CST: no codes read
+        mat = (m.dia_cst && seg < 0) ? (int64_t)m.dia_k * 8 : dia_bytes;  // constant stencil: no codes read
     } else if (m.kernel == SPMV_KERNEL_SELL) {
         name = (m.sell_short && seg < 0 && mode != SPMV_SGS && mode != SPMV_RESID0 && sell_short_enabled())
                    ? "sell_short" : "sell";
@@ -2666,12 +2691,12 @@ void spmv(const GpuCsr &m, const double *x, double *y, SpmvMode mode, const Spmv
         const int runs9i = runs9 ? 9 : run7 ? -1 : 0;
         const int pat = m.dia_pat ? m.dia_pat : runs9 && dia_pat27() && (key == 4 * 16 + 4 || key == 8 * 16 + 8) ? 27 : 0;
         if (pat) {
-        const bool cst = pat == 27 && m.dia_cst27 && seg < 0 && dia_cst_enabled();
+        const bool cst = pat == 27 && m.dia_cst && seg < 0 && dia_cst_enabled();
         if (cst) {
             a.gnx = m.dia_cst_n[0];
             a.gny = m.dia_cst_n[1];
             a.gnz = m.dia_cst_n[2];
-            for (int k = 0; k < 27; k++) a.cst[k] = m.dia_cst[k];
+            for (int k = 0; k < 27; k++) a.cst[k] = m.dia_cst_v[k];
         }
 #define FAMG_DIAP2(M, VB, CW, P)                                                                  \
     if (cst) spmv_dia_pat_kernel<M, VB, CW, P, (P == 27)><<<grid, block, 0, s>>>(a);              \
@@ -2709,7 +2734,14 @@ void spmv(const GpuCsr &m, const double *x, double *y, SpmvMode mode, const Spmv
             FAMG_CHECK_HIP(hipGetLastError());
             return;
         }
-#define FAMG_DIA2(M, VB, CW) launch_dia<M, VB, CW>(runs9i, nt, grid, block, s, a);
+        const bool cst7 = runs9i == -1 && m.dia_cst && m.dia_k == 7 && seg < 0 && dia_cst_enabled();
+        if (cst7) {
+            a.gnx = m.dia_cst_n[0];
+            a.gny = m.dia_cst_n[1];
+            a.gnz = m.dia_cst_n[2];
+            for (int k = 0; k < 7; k++) a.cst[k] = m.dia_cst_v[k];
+        }
+#define FAMG_DIA2(M, VB, CW) launch_dia<M, VB, CW>(runs9i, nt, grid, block, s, a, cst7);
 #define FAMG_DIA(VB, CW)                                                                          \
     switch (mode) {                                                                               \
     case SPMV_SET: FAMG_DIA2(SPMV_SET, VB, CW) break;                                             \

@@ -116,9 +116,10 @@ amg_status amg_set_alloc_policy(int32_t policy);
  * levels (default 0, env FAMG_FOLD_XSCS), 1 = read a constant coded Jacobi
  * diagonal as one scalar (default 1, env FAMG_DIA_DK), 2 = waves per row of the
  * wave-per-row kernel (0 auto = chosen per matrix at finalize, 1/2/4; env
- * FAMG_VEC_WPR), 3 = time the wide grid-transfer classes (gtx.hip) against a
- * transfer operator's other storage at setup and keep them only where they win
- * (default 1, env FAMG_GTX_TIME; 0 keeps them wherever they build), 4 = marching
+ * FAMG_VEC_WPR), 3 = where the wide grid-transfer classes (gtx.hip) are kept:
+ * 0 wherever they build, 1 where they beat the transfer operator's other storage
+ * in a setup-time timing, 2 (default) on operators of >= 2^18 rows (env
+ * FAMG_GTX_TIME), 4 = marching
  * 27-point SGS phases (sgs27.hip): 0 = one workgroup per tile and plane, 1 = auto
  * (about one workgroup per CU), n >= 2 = n planes per workgroup (default 1, env
  * FAMG_SGS27_MARCH).  Setting one

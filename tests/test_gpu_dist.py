@@ -524,7 +524,7 @@ def slab_run(nranks, dims, coarsest, agglo, b, overlap=True):
     try:
         res = run_ranks(nranks, rank_fn)
     finally:
-        fa().set_flag("gtx_time", 1)
+        fa().set_flag("gtx_time", 2)
     z = np.zeros(len(b))
     for r in res:
         z[r[0]:r[1]] = r[2]

@@ -1178,13 +1178,17 @@ def _epilogues_bitwise(ctx, M, seed):
         assert np.array_equal(H(yd), ref), (mode, M.spmv_info())
 
 
+@pytest.mark.parametrize("gen", ["27pt", "7pt"])
 @pytest.mark.parametrize("dims", [(66, 40, 33), (48, 45, 41)])
-def test_dia27_constant_stencil_bitwise(ctx, dims):
-    """The 27-point constant stencil truncated at the grid faces (aniso27) on DIA
-    storage runs the pattern kernel without codes (spmv_dia_pat_kernel CST: the
-    interior coefficients, x operands outside the grid taken as 0.0): all four
-    epilogues bitwise equal to the oracle's row sums, odd y/z extents included."""
-    A = fa().SparseMatOp.aniso27(ctx, *dims, 1.0, 1.0, 0.01)
+def test_dia27_constant_stencil_bitwise(ctx, dims, gen):
+    """Constant stencils truncated at the grid faces (aniso27, the 7-point
+    Laplacian) on DIA storage run without codes (spmv_dia_pat_kernel /
+    spmv_dia_kernel CST: the interior coefficients, x operands outside the grid
+    taken as 0.0): all four epilogues bitwise equal to the oracle's row sums, odd
+    y/z extents included; the folded and constant-diagonal epilogues of the 7-point
+    kernel inside a V-cycle are covered by test_constant_diagonal_epilogues_bitwise."""
+    A = (fa().SparseMatOp.aniso27(ctx, *dims, 1.0, 1.0, 0.01) if gen == "27pt"
+         else fa().SparseMatOp.laplace3d_7pt(ctx, *dims))
     if A.spmv_info()["kernel"] != "dia":
         pytest.skip("operator not stored as DIA codes")
     _epilogues_bitwise(ctx, A, 77)
@@ -1383,7 +1387,7 @@ def test_wide_grid_transfer_classes(ctx, gen, dims):
     try:
         mg = fa().sa_build_box(A, dims, (2, 2, 2), coarsest_dim=60)
     finally:
-        fa().set_flag("gtx_time", 1)
+        fa().set_flag("gtx_time", 2)
     seen = set()
     rng = np.random.default_rng(4)
     for l in range(mg.levels() - 1):
