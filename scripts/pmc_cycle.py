@@ -5,6 +5,9 @@ Runs, on one GPU, in this order:
     per row + x read + y written, exactly known bytes through the same DIA
     kernel family -- calibrates FETCH_SIZE (gfx950: half the bytes of 16-B/lane
     streams, MI355X_MICROARCH.md) for these kernels;
+  * COPY: y.copy_(x) between k_trace_mark<<<3>>> and <<<4>>>: 8 n read, 8 n
+    written by torch's vectorised copy (16 B/lane), the access width the
+    guide's factor of 2 is stated for -- a second, independent calibration;
   * FINE: y = A_0 x (the bench's roofline kernel, DIA SET on the 7-pt 256^3);
   * k_trace_mark<<<1>>>, CYCLES eager V-cycles of the C2 hierarchy (the bench's),
     k_trace_mark<<<2>>>.
@@ -38,6 +41,11 @@ torch.cuda.synchronize()
 mg.apply(z, x)  # workspaces, Jacobi codes
 ctx.synchronize()
 plan = mg.cycle_plan()
+ctx.trace_mark(3)
+for _ in range(ITERS):  # COPY: torch's vectorised copy, 16-B/lane streams (the guide's calibrated width)
+    y.copy_(x)
+ctx.synchronize()
+ctx.trace_mark(4)
 for _ in range(ITERS):
     D.apply(y, x)
 ctx.synchronize()

@@ -31,11 +31,17 @@ def split(rows, iters, cycles, nplan):
     names = [r[0] for r in rows]
     marks = [i for i, nm in enumerate(names) if "k_trace_mark" in nm]
     assert len(marks) >= 2, "no trace marks"
-    dia = [i for i in range(marks[0]) if "spmv_dia_kernel" in names[i]]
+    cp, lo = [], 0
+    if len(marks) >= 4:  # marks 3, 4 bracket the torch copies, then 1, 2 the cycles
+        cp = list(range(marks[0] + 1, marks[1]))
+        lo, marks = marks[1] + 1, marks[2:]
+    # CAL and FINE sit between the copy marks and the cycle marks (the warm-up
+    # cycle before the copies also runs DIA kernels and must not be counted)
+    dia = [i for i in range(lo, marks[0]) if "spmv_dia_kernel" in names[i]]
     cal, fine = dia[:iters], dia[iters:2 * iters]
     cyc = list(range(marks[0] + 1, marks[1]))
     assert len(cyc) == cycles * nplan, (len(cyc), cycles, nplan)
-    return cal, fine, cyc
+    return cal, fine, cyc, cp
 
 
 def main(fetch_csv, write_csv, known_json, plan_json, out_json):
@@ -43,10 +49,19 @@ def main(fetch_csv, write_csv, known_json, plan_json, out_json):
     plan = json.load(open(plan_json))
     n, iters, cycles = known["n"], known["iters"], known["cycles"]
     F, W = load(fetch_csv, "FETCH_SIZE"), load(write_csv, "WRITE_SIZE")
-    cal, fine, cyc = split(F, iters, cycles, len(plan))
-    calw, finew, cycw = split(W, iters, cycles, len(plan))
+    cal, fine, cyc, cp = split(F, iters, cycles, len(plan))
+    calw, finew, cycw, cpw = split(W, iters, cycles, len(plan))
     cal_known = known["cal"]["stream_bytes"] + 8 * n
-    factor = cal_known / statistics.median(F[i][1] for i in cal)
+    dia_factor = cal_known / statistics.median(F[i][1] for i in cal)
+    copy = None
+    if cp:  # the 16-B/lane copy calibration is the one used when present
+        factor = 8 * n / statistics.median(F[i][1] for i in cp)
+        copy = {"kernel": F[cp[0]][0].split("(")[0][:80], "known_read_bytes": 8 * n,
+                "fetch_size_bytes": statistics.median(F[i][1] for i in cp),
+                "write_size_bytes": statistics.median(W[i][1] for i in cpw), "known_write_bytes": 8 * n,
+                "factor": round(factor, 4)}
+    else:
+        factor = dia_factor
     fine_alg = known["fine"]["stream_bytes"] + 16 * n
     fine_rd = statistics.median(F[i][1] for i in fine) * factor
     fine_wr = statistics.median(W[i][1] for i in finew)
@@ -63,7 +78,8 @@ def main(fetch_csv, write_csv, known_json, plan_json, out_json):
     out = {
         "workload": "C2 hierarchy (7-pt 256^3, SA 2^3 boxes), eager V-cycles; FETCH/WRITE passes separate",
         "fetch_correction_factor": round(factor, 4),
-        "calibration": {"kernel": "spmv_dia_kernel<SET> on a diagonal matrix (4-bit DIA codes)",
+        "copy_calibration": copy,
+        "calibration": {"factor": round(dia_factor, 4), "kernel": "spmv_dia_kernel<SET> on a diagonal matrix (4-bit DIA codes)",
                         "known_read_bytes": cal_known,
                         "fetch_size_bytes": statistics.median(F[i][1] for i in cal),
                         "write_size_bytes": statistics.median(W[i][1] for i in calw), "known_write_bytes": 8 * n},
