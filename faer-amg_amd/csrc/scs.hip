@@ -26,6 +26,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <mutex>
 #include <unordered_map>
 
 #include "famg.hpp"
@@ -212,7 +213,14 @@ struct XscsArgs {
     const double *d;
     const uint8_t *dc;
     const double *dt;
+    // float reciprocals of wx, wy, tx, ty: q / d as (int)((q + 0.5f) * r), exact for
+    // the q < 2^14, d <= 128 used here (checked on the host for every q of a launch);
+    // the runtime integer divisions of the staging loop were the kernel's largest
+    // VALU cost (PMC, profiles/r04/pmc_xscs_summary.json)
+    float rwx, rwy, rtx, rty;
 };
+
+__device__ __forceinline__ int xscs_div(int q, float r) { return (int)(((float)q + 0.5f) * r); }
 
 template <int MODE, int IB, int RL>
 __global__ __launch_bounds__(256) void spmv_xscs_kernel(XscsArgs a) {
@@ -234,7 +242,8 @@ __global__ __launch_bounds__(256) void spmv_xscs_kernel(XscsArgs a) {
 #pragma unroll
     for (int j = 0; j < RL; j++) {
         const int lt = tid + 256 * j;
-        const int lx = lt % a.tx, ly = (lt / a.tx) % a.ty, lz = lt / (a.tx * a.ty);
+        const int lq = xscs_div(lt, a.rtx), lz = xscs_div(lq, a.rty);
+        const int lx = lt - lq * a.tx, ly = lq - lz * a.ty;
         const int gx = x0 + lx, gy = y0 + ly, gz = z0 + lz;
         live[j] = lt < T && gx < a.nx && gy < a.ny && gz < a.nz;
         gi[j] = live[j] ? (int64_t)gz * plane + (int64_t)gy * a.nx + gx
@@ -264,8 +273,8 @@ __global__ __launch_bounds__(256) void spmv_xscs_kernel(XscsArgs a) {
 #pragma unroll
         for (int u = 0; u < PF; u++) {
             const int p = p0 + 256 * u;
-            const int px = p % a.wx, q = p / a.wx;
-            const int py = q % a.wy, pz = q / a.wy;
+            const int q = xscs_div(p, a.rwx), pz = xscs_div(q, a.rwy);
+            const int px = p - q * a.wx, py = q - pz * a.wy;
             const int gx = x0 - a.rx + px, gy = y0 - a.ry + py, gz = z0 - a.rz + pz;
             const bool in = p < W && (unsigned)gx < (unsigned)a.nx && (unsigned)gy < (unsigned)a.ny && gz >= a.zlo &&
                             gz < a.zhi;
@@ -742,6 +751,20 @@ bool build_scs(GpuCsr &m, const std::vector<int64_t> &rp, int64_t other_bytes) {
     return true;
 }
 
+// Every q < n divided by d through the float reciprocal r as the kernel does it
+// equals q / d (memoised: the tile set of a matrix is small).
+static bool xscs_div_exact(int n, int d, float r) {
+    static std::mutex mu;
+    static std::vector<std::array<int, 2>> ok;
+    std::lock_guard<std::mutex> g(mu);
+    for (const auto &e : ok)
+        if (e[0] >= n && e[1] == d) return true;
+    for (int q = 0; q < n; q++)
+        if ((int)(((float)q + 0.5f) * r) != q / d) return false;
+    ok.push_back({n, d});
+    return true;
+}
+
 static void spmv_xscs(const GpuCsr &m, const double *x, double *y, SpmvMode mode, const SpmvEpi &epi,
                       hipStream_t s, int64_t seg) {
     XscsArgs a{};
@@ -755,6 +778,11 @@ static void spmv_xscs(const GpuCsr &m, const double *x, double *y, SpmvMode mode
     a.wx = a.tx + 2 * a.rx; a.wy = a.ty + 2 * a.ry; a.wz = a.tz + 2 * a.rz;
     a.ntx = (int)ceil_div(a.nx, a.tx); a.nty = (int)ceil_div(a.ny, a.ty);
     const int ntz = (int)ceil_div(a.nz, a.tz);
+    a.rwx = 1.0f / (float)a.wx; a.rwy = 1.0f / (float)a.wy;
+    a.rtx = 1.0f / (float)a.tx; a.rty = 1.0f / (float)a.ty;
+    FAMG_REQUIRE(xscs_div_exact(a.wx * a.wy * a.wz, a.wx, a.rwx) && xscs_div_exact(a.wy * a.wz, a.wy, a.rwy) &&
+                     xscs_div_exact(1024, a.tx, a.rtx) && xscs_div_exact(1024 / a.tx + 1, a.ty, a.rty),
+                 AMG_ERR_UNSUPPORTED, "x-staged classes: window too large for the float divisions");
     a.zlo = 0; a.zhi = a.nz; a.add_lo = a.add_hi = 0;
     const SlabFrame &F = m.cframe;
     if (F.on()) {  // rank-local: the ghost planes below / above the owned ones
