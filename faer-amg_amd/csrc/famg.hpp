@@ -29,6 +29,23 @@ __device__ __forceinline__ int xcd_remap(int b, int nb) {
     return x * q + min(x, r) + idx;
 }
 
+// q / d for 0 <= q < 2^14 through a float reciprocal r = 1.0f / d: (q + 0.5) / d
+// lies at least 0.5 / d from an integer, far beyond the float error, for the
+// window and tile extents the staging loops divide by.  fdiv_exact checks every
+// q < n on the host before a kernel relies on it (memoised per (n, d)).
+__device__ __forceinline__ int fdiv_rcp(int q, float r) { return (int)(((float)q + 0.5f) * r); }
+inline bool fdiv_exact(int n, int d, float r) {
+    static std::mutex mu;
+    static std::vector<std::pair<int, int>> ok;
+    std::lock_guard<std::mutex> g(mu);
+    for (const auto &e : ok)
+        if (e.first >= n && e.second == d) return true;
+    for (int q = 0; q < n; q++)
+        if ((int)(((float)q + 0.5f) * r) != q / d) return false;
+    ok.push_back({n, d});
+    return true;
+}
+
 // ------------------------------------------------------------------ CSR data
 
 // Plane layout of a rank-local vector of a distributed grid level (dist.hip,

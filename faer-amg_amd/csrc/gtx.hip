@@ -59,6 +59,7 @@ struct GtxArgs {
     int dconst;
     double dk;
     double *y2;  // SETDF: y2 = d * y
+    float rwx, rwy, rtx, rty;  // 1 / wx, wy, tx, ty for fdiv_rcp (host-checked exact)
 };
 
 // stage the column window [w0, w0 + w) into LDS (0.0 outside the grid / the
@@ -74,7 +75,8 @@ __device__ __forceinline__ void gtx_stage(const GtxArgs &a, double *win, int wx0
 #pragma unroll
         for (int u = 0; u < PF; u++) {
             const int q = q0 + 256 * u;
-            const int X = wx0 + q % a.wx, Y = wy0 + (q / a.wx) % a.wy, Z = wz0 + q / (a.wx * a.wy);
+            const int q1 = fdiv_rcp(q, a.rwx), q2 = fdiv_rcp(q1, a.rwy);
+            const int X = wx0 + q - q1 * a.wx, Y = wy0 + q1 - q2 * a.wy, Z = wz0 + q2;
             const bool in = q < W && (unsigned)X < (unsigned)a.kx && (unsigned)Y < (unsigned)a.ky && Z >= a.kz_lo &&
                             Z < a.kz_hi;
             const int64_t zb = (int64_t)Z * cplane + (Z < 0 ? a.add_lo : Z >= a.kz ? a.add_hi : 0);
@@ -264,7 +266,8 @@ __global__ __launch_bounds__(256) void k_gtx_restrict(GtxArgs a) {
 #pragma unroll
     for (int j = 0; j < RL; j++) {
         const int lt = tid + 256 * j;
-        const int lx = lt % a.tx, ly = (lt / a.tx) % a.ty, lz = lt / (a.tx * a.ty);
+        const int lq = fdiv_rcp(lt, a.rtx), lz = fdiv_rcp(lq, a.rty);
+        const int lx = lt - lq * a.tx, ly = lq - lz * a.ty;
         const int X = X0 + lx, Y = Y0 + ly, Z = Z0 + lz;
         live[j] = lt < T && X < a.rx && Y < a.ry && Z < a.rz;
         J[j] = live[j] ? (int64_t)Z * cplane + (int64_t)Y * a.rx + X : 0;
@@ -595,6 +598,12 @@ void spmv_gtx(const GpuCsr &m, const double *x, double *y, SpmvMode mode, const 
     a.tx = m.gtx_tile[0]; a.ty = m.gtx_tile[1]; a.tz = m.gtx_tile[2];
     a.wx = m.gtx_win[0]; a.wy = m.gtx_win[1]; a.wz = m.gtx_win[2];
     a.lox = m.gtx_lo[0]; a.loy = m.gtx_lo[1]; a.loz = m.gtx_lo[2];
+    a.rwx = 1.0f / (float)a.wx; a.rwy = 1.0f / (float)a.wy;
+    a.rtx = 1.0f / (float)std::max(a.tx, 1); a.rty = 1.0f / (float)std::max(a.ty, 1);
+    FAMG_REQUIRE(fdiv_exact(a.wx * a.wy * a.wz + 256 * 8, a.wx, a.rwx) &&
+                     fdiv_exact((a.wx * a.wy * a.wz + 256 * 8) / a.wx + 1, a.wy, a.rwy) &&
+                     fdiv_exact(1024, std::max(a.tx, 1), a.rtx) && fdiv_exact(1024 / std::max(a.tx, 1) + 1, std::max(a.ty, 1), a.rty),
+                 AMG_ERR_UNSUPPORTED, "wide grid-transfer classes: window too large for the float divisions");
     a.kz_lo = 0; a.kz_hi = a.kz; a.rz0 = 0; a.kz0 = 0; a.add_lo = a.add_hi = 0;
     if (m.rframe.on()) {
         a.rz = (int)m.rframe.nz;

@@ -26,7 +26,6 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
-#include <mutex>
 #include <unordered_map>
 
 #include "famg.hpp"
@@ -220,8 +219,6 @@ struct XscsArgs {
     float rwx, rwy, rtx, rty;
 };
 
-__device__ __forceinline__ int xscs_div(int q, float r) { return (int)(((float)q + 0.5f) * r); }
-
 template <int MODE, int IB, int RL>
 __global__ __launch_bounds__(256) void spmv_xscs_kernel(XscsArgs a) {
     extern __shared__ double win[];
@@ -242,7 +239,7 @@ __global__ __launch_bounds__(256) void spmv_xscs_kernel(XscsArgs a) {
 #pragma unroll
     for (int j = 0; j < RL; j++) {
         const int lt = tid + 256 * j;
-        const int lq = xscs_div(lt, a.rtx), lz = xscs_div(lq, a.rty);
+        const int lq = fdiv_rcp(lt, a.rtx), lz = fdiv_rcp(lq, a.rty);
         const int lx = lt - lq * a.tx, ly = lq - lz * a.ty;
         const int gx = x0 + lx, gy = y0 + ly, gz = z0 + lz;
         live[j] = lt < T && gx < a.nx && gy < a.ny && gz < a.nz;
@@ -273,7 +270,7 @@ __global__ __launch_bounds__(256) void spmv_xscs_kernel(XscsArgs a) {
 #pragma unroll
         for (int u = 0; u < PF; u++) {
             const int p = p0 + 256 * u;
-            const int q = xscs_div(p, a.rwx), pz = xscs_div(q, a.rwy);
+            const int q = fdiv_rcp(p, a.rwx), pz = fdiv_rcp(q, a.rwy);
             const int px = p - q * a.wx, py = q - pz * a.wy;
             const int gx = x0 - a.rx + px, gy = y0 - a.ry + py, gz = z0 - a.rz + pz;
             const bool in = p < W && (unsigned)gx < (unsigned)a.nx && (unsigned)gy < (unsigned)a.ny && gz >= a.zlo &&
@@ -751,20 +748,6 @@ bool build_scs(GpuCsr &m, const std::vector<int64_t> &rp, int64_t other_bytes) {
     return true;
 }
 
-// Every q < n divided by d through the float reciprocal r as the kernel does it
-// equals q / d (memoised: the tile set of a matrix is small).
-static bool xscs_div_exact(int n, int d, float r) {
-    static std::mutex mu;
-    static std::vector<std::array<int, 2>> ok;
-    std::lock_guard<std::mutex> g(mu);
-    for (const auto &e : ok)
-        if (e[0] >= n && e[1] == d) return true;
-    for (int q = 0; q < n; q++)
-        if ((int)(((float)q + 0.5f) * r) != q / d) return false;
-    ok.push_back({n, d});
-    return true;
-}
-
 static void spmv_xscs(const GpuCsr &m, const double *x, double *y, SpmvMode mode, const SpmvEpi &epi,
                       hipStream_t s, int64_t seg) {
     XscsArgs a{};
@@ -780,8 +763,8 @@ static void spmv_xscs(const GpuCsr &m, const double *x, double *y, SpmvMode mode
     const int ntz = (int)ceil_div(a.nz, a.tz);
     a.rwx = 1.0f / (float)a.wx; a.rwy = 1.0f / (float)a.wy;
     a.rtx = 1.0f / (float)a.tx; a.rty = 1.0f / (float)a.ty;
-    FAMG_REQUIRE(xscs_div_exact(a.wx * a.wy * a.wz, a.wx, a.rwx) && xscs_div_exact(a.wy * a.wz, a.wy, a.rwy) &&
-                     xscs_div_exact(1024, a.tx, a.rtx) && xscs_div_exact(1024 / a.tx + 1, a.ty, a.rty),
+    FAMG_REQUIRE(fdiv_exact(a.wx * a.wy * a.wz, a.wx, a.rwx) && fdiv_exact(a.wy * a.wz, a.wy, a.rwy) &&
+                     fdiv_exact(1024, a.tx, a.rtx) && fdiv_exact(1024 / a.tx + 1, a.ty, a.rty),
                  AMG_ERR_UNSUPPORTED, "x-staged classes: window too large for the float divisions");
     a.zlo = 0; a.zhi = a.nz; a.add_lo = a.add_hi = 0;
     const SlabFrame &F = m.cframe;
