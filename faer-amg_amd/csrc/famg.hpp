@@ -160,6 +160,7 @@ struct GpuCsr {
     DevBuf<double> scs_dict;
     DevBuf<int32_t> scs_offs;
     int64_t scs_k = 0, scs_nclass = 0;
+    int64_t scs_kr = 0;  // offsets before the padding to a multiple of 8 (the x-staged walk stops there)
     int64_t scs_seg = -1;  // >= 0: only this row segment (a distributed level's halo interior) beside SELL
     int scs_ib = 0;
     bool scs_lanes = false;  // one row per wave (few long rows: spmv_scs_lanes_kernel)

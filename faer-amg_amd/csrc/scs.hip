@@ -199,7 +199,7 @@ struct XscsArgs {
     const void *cls;
     const double *dict;
     const int32_t *lo;
-    int32_t k;
+    int32_t k, kr;  // offsets per dictionary row (a multiple of 8) / before the padding
     int nx, ny, nz, tx, ty, tz, rx, ry, rz, wx, wy, wz, ntx, nty;
     // staged planes: local plane z is loadable for zlo <= z < zhi (else 0.0) and
     // starts at z * plane + (z < 0 ? add_lo : z >= nz ? add_hi : 0) -- a rank-local
@@ -318,10 +318,13 @@ __global__ __launch_bounds__(256) void spmv_xscs_kernel(XscsArgs a) {
 #pragma unroll
                 for (int u = 0; u < UG; u++) acc[j] = fma(v[j][u], xv[j][u], acc[j]);
         };
+        // the padding offsets (+0.0 at the row itself) are skipped: adding +0.0 x
+        // to a sum that started at +0.0 never changes it
         int k0 = 0;
         if (RL == 1)
-            for (; k0 + 16 <= a.k; k0 += 16) group(std::integral_constant<int, 16>{}, k0);
-        for (; k0 < a.k; k0 += SCS_U) group(std::integral_constant<int, SCS_U>{}, k0);
+            for (; k0 + 16 <= a.kr; k0 += 16) group(std::integral_constant<int, 16>{}, k0);
+        for (; k0 + SCS_U <= a.kr; k0 += SCS_U) group(std::integral_constant<int, SCS_U>{}, k0);
+        for (; k0 < a.kr; k0++) group(std::integral_constant<int, 1>{}, k0);
     } else {
         for (int k0 = 0; k0 < a.k; k0 += SCS_U) {
             int l[SCS_U];
@@ -381,6 +384,7 @@ void scs_release(GpuCsr &m) {
     m.scs_dict.release();
     m.scs_offs.release();
     m.scs_k = m.scs_nclass = m.scs_ib = 0;
+    m.scs_kr = 0;
     m.scs_seg = -1;
     m.scs_lanes = false;
     m.xscs = false;
@@ -740,6 +744,7 @@ bool build_scs(GpuCsr &m, const std::vector<int64_t> &rp, int64_t other_bytes) {
         FAMG_CHECK_HIP(hipStreamSynchronize(st));
     }
     m.scs_k = Kp;
+    m.scs_kr = K;
     m.scs_nclass = C;
     m.scs_ib = ib;
     m.scs_seg = seg;
@@ -755,6 +760,7 @@ static void spmv_xscs(const GpuCsr &m, const double *x, double *y, SpmvMode mode
     a.dict = m.scs_dict.get();
     a.lo = m.xscs_lo.get();
     a.k = (int32_t)m.scs_k;
+    a.kr = (int32_t)m.scs_kr;
     a.nx = (int)m.grid[0]; a.ny = (int)m.grid[1]; a.nz = (int)m.grid[2];
     a.tx = m.xscs_t[0]; a.ty = m.xscs_t[1]; a.tz = m.xscs_t[2];
     a.rx = m.xscs_r[0]; a.ry = m.xscs_r[1]; a.rz = m.xscs_r[2];
