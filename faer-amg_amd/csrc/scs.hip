@@ -201,6 +201,7 @@ struct XscsArgs {
     const int32_t *lo;
     int32_t k, kr;  // offsets per dictionary row (a multiple of 8) / before the padding
     int nx, ny, nz, tx, ty, tz, rx, ry, rz, wx, wy, wz, ntx, nty;
+    int ws;  // LDS row stride of the window (>= wx)
     // staged planes: local plane z is loadable for zlo <= z < zhi (else 0.0) and
     // starts at z * plane + (z < 0 ? add_lo : z >= nz ? add_hi : 0) -- a rank-local
     // matrix's ghost planes (SlabFrame); single GPU: 0, nz, 0, 0
@@ -245,8 +246,8 @@ __global__ __launch_bounds__(256) void spmv_xscs_kernel(XscsArgs a) {
         live[j] = lt < T && gx < a.nx && gy < a.ny && gz < a.nz;
         gi[j] = live[j] ? (int64_t)gz * plane + (int64_t)gy * a.nx + gx
                         : (int64_t)z0 * plane + (int64_t)y0 * a.nx + x0;  // the tile's first point
-        wb[j] = live[j] ? ((lz + a.rz) * a.wy + ly + a.ry) * a.wx + lx + a.rx
-                        : (a.rz * a.wy + a.ry) * a.wx + a.rx;
+        wb[j] = live[j] ? ((lz + a.rz) * a.wy + ly + a.ry) * a.ws + lx + a.rx
+                        : (a.rz * a.wy + a.ry) * a.ws + a.rx;
         c[j] = cls_of(gi[j]);
         br[j] = xr[j] = dr[j] = yr[j] = 0.0;
         if (live[j]) {
@@ -267,11 +268,13 @@ __global__ __launch_bounds__(256) void spmv_xscs_kernel(XscsArgs a) {
     constexpr int PF = 8;
     for (int p0 = tid; p0 < W; p0 += 256 * PF) {
         double v[PF];
+        int si[PF];
 #pragma unroll
         for (int u = 0; u < PF; u++) {
             const int p = p0 + 256 * u;
             const int q = fdiv_rcp(p, a.rwx), pz = fdiv_rcp(q, a.rwy);
             const int px = p - q * a.wx, py = q - pz * a.wy;
+            si[u] = q * a.ws + px;  // (pz wy + py) ws + px
             const int gx = x0 - a.rx + px, gy = y0 - a.ry + py, gz = z0 - a.rz + pz;
             const bool in = p < W && (unsigned)gx < (unsigned)a.nx && (unsigned)gy < (unsigned)a.ny && gz >= a.zlo &&
                             gz < a.zhi;
@@ -282,7 +285,7 @@ __global__ __launch_bounds__(256) void spmv_xscs_kernel(XscsArgs a) {
         }
 #pragma unroll
         for (int u = 0; u < PF; u++)
-            if (p0 + 256 * u < W) win[p0 + 256 * u] = v[u];
+            if (p0 + 256 * u < W) win[si[u]] = v[u];
     }
     __syncthreads();
     bool uni = true;
@@ -409,13 +412,44 @@ static bool grid_applies(const GpuCsr &m) {
 
 // Tile t for m's x-staged kernel: the window offset of every stencil offset,
 // relative to the row's own window position.
+// The window's LDS row stride for tile t: the stride in [wx, wx + 31] (window
+// <= 64 KB) whose first wave's ds_read_b64 lanes meet the fewest bank repeats
+// (lanes 0-31 and 32-63 each serviced together, bank = dword mod 64,
+// MI355X_MICROARCH.md LDS table); every stencil offset shifts all lanes alike,
+// so the row positions decide.  A_1 of the 7-point cycle on 8 x 8 x 8 tiles:
+// stride 12 put rows y and y + 3 on the same banks (PMC: 45 % of the LDS cycles
+// were bank conflicts).
+static int xscs_stride(const int *t, int wx, int wy, int wz) {
+    int best = wx, best_cost = 1 << 30;
+    for (int s = wx; s < wx + 32 && (int64_t)s * wy * wz * 8 <= 64 * 1024; s++) {
+        int cost = 0;
+        for (int g = 0; g < 2; g++) {
+            int cnt[64] = {0};
+            for (int lane = 32 * g; lane < 32 * g + 32; lane++) {
+                const int lx = lane % t[0], ly = (lane / t[0]) % t[1], lz = lane / (t[0] * t[1]);
+                const int a = (lz * wy + ly) * s + lx;
+                cnt[(2 * a) & 63]++;
+                cnt[(2 * a + 1) & 63]++;
+            }
+            cost += *std::max_element(cnt, cnt + 64);
+        }
+        if (cost < best_cost) {
+            best_cost = cost;
+            best = s;
+        }
+    }
+    return best;
+}
+
 static void xscs_set_tile(GpuCsr &m, const int *t) {
-    const int rx = m.xscs_r[0], ry = m.xscs_r[1];
+    const int rx = m.xscs_r[0], ry = m.xscs_r[1], rz = m.xscs_r[2];
     const int wx = t[0] + 2 * rx, wy = t[1] + 2 * ry;
+    const int ws = xscs_stride(t, wx, wy, t[2] + 2 * rz);
     const int Kp = (int)(m.xscs_steps.size() / 3);
     std::vector<int32_t> lo(Kp);
     for (int k = 0; k < Kp; k++)
-        lo[k] = (m.xscs_steps[3 * k + 2] * wy + m.xscs_steps[3 * k + 1]) * wx + m.xscs_steps[3 * k];
+        lo[k] = (m.xscs_steps[3 * k + 2] * wy + m.xscs_steps[3 * k + 1]) * ws + m.xscs_steps[3 * k];
+    m.xscs_ws = ws;
     m.xscs_lo.resize(Kp);
     FAMG_CHECK_HIP(hipMemcpyAsync(m.xscs_lo.get(), lo.data(), Kp * 4, hipMemcpyHostToDevice, m.ctx->stream));
     FAMG_CHECK_HIP(hipStreamSynchronize(m.ctx->stream));
@@ -765,6 +799,8 @@ static void spmv_xscs(const GpuCsr &m, const double *x, double *y, SpmvMode mode
     a.tx = m.xscs_t[0]; a.ty = m.xscs_t[1]; a.tz = m.xscs_t[2];
     a.rx = m.xscs_r[0]; a.ry = m.xscs_r[1]; a.rz = m.xscs_r[2];
     a.wx = a.tx + 2 * a.rx; a.wy = a.ty + 2 * a.ry; a.wz = a.tz + 2 * a.rz;
+    a.ws = m.xscs_ws;
+    FAMG_REQUIRE(a.ws >= a.wx, AMG_ERR_UNSUPPORTED, "x-staged classes: no window stride");
     a.ntx = (int)ceil_div(a.nx, a.tx); a.nty = (int)ceil_div(a.ny, a.ty);
     const int ntz = (int)ceil_div(a.nz, a.tz);
     a.rwx = 1.0f / (float)a.wx; a.rwy = 1.0f / (float)a.wy;
@@ -800,7 +836,7 @@ static void spmv_xscs(const GpuCsr &m, const double *x, double *y, SpmvMode mode
     a.x = x; a.y = y; a.b = epi.b; a.d = epi.d; a.dc = epi.dc; a.dt = epi.dt;
     const int T = a.tx * a.ty * a.tz;
     const int rl = T <= 256 ? 1 : T <= 512 ? 2 : 4;
-    const size_t lds = (size_t)a.wx * a.wy * a.wz * sizeof(double);
+    const size_t lds = (size_t)a.ws * a.wy * a.wz * sizeof(double);
     const dim3 grid((unsigned)((int64_t)a.ntx * a.nty * (tz1 - tz0))), block(256);
 #define FAMG_XS3(M, IB)                                                                            \
     if (rl == 1) spmv_xscs_kernel<M, IB, 1><<<grid, block, lds, s>>>(a);                           \
