@@ -170,7 +170,8 @@ def _time_cycles(omg, b, budget_s, max_cycles=60, min_cycles=3):
     return ts, out
 
 
-def cpu_side(mg, A, b_host, z_gpu, args):
+def cpu_side(mg, A, b_host, z_gpu, args, hist_gpu=None, rho_cycles=10, min_cycles=None, budget=None,
+             what_gpu="GPU"):
     """Everything the CPU restatement contributes to the bench line, on the SAME
     hierarchy (the GPU's A_l, R_l, P_l arrays):
       parity      -- ||z_gpu - z_oracle|| / ||z_oracle|| for one V-cycle (<= 1e-11,
@@ -201,15 +202,18 @@ def cpu_side(mg, A, b_host, z_gpu, args):
     # parity of one V-cycle (the bench's own z from the timed loop); >= 50 cycles
     # at 16 threads (median over >= 50 cycles)
     omg.set_parallel(t16)
-    ts16, zref = _time_cycles(omg, b_host, args.cpu_budget, min_cycles=args.cpu_min_cycles)
+    ts16, zref = _time_cycles(omg, b_host, args.cpu_budget if budget is None else budget,
+                              min_cycles=args.cpu_min_cycles if min_cycles is None else min_cycles)
     rel_err = float(np.linalg.norm(z_gpu - zref) / np.linalg.norm(zref))
-    # residual history of 10 stationary cycles (simple_geometric.rs:117-158)
-    K = 10
-    bd = torch.as_tensor(b_host, device="cuda:0")
-    xd = torch.zeros_like(bd)
-    _, hist_gpu = fa.stationary_solve(A, mg, bd, xd, max_iter=K + 1, rel_tol=1e-300)
+    # residual history of K stationary cycles (simple_geometric.rs:117-158)
+    K = rho_cycles
+    if hist_gpu is None:
+        bd = torch.as_tensor(b_host, device=torch.cuda.current_device())
+        xd = torch.zeros_like(bd)
+        _, hist_gpu = fa.stationary_solve(A, mg, bd, xd, max_iter=K + 1, rel_tol=1e-300)
+        torch.cuda.synchronize()
+    hist_gpu = np.asarray(hist_gpu, np.float64)[:K + 1]
     _, _, hist_cpu = O.stationary_solve(OA, omg, b_host, max_iter=K + 1, rel_tol=1e-300)
-    torch.cuda.synchronize()
     rho_rel = float(np.max(np.abs(hist_gpu - hist_cpu) / hist_cpu))
 
     # fine-level SpMV of the restated rayon path (ParSpmmOp), 16 threads
@@ -240,11 +244,11 @@ def cpu_side(mg, A, b_host, z_gpu, args):
                             "nproc": nproc, "cpu_quota": quota,
                             "sample": f"median of {len(tsa)} V-cycles at {all_threads} OpenMP threads"}
         omg.set_parallel(t16)
-    parity = {"vcycle_rel_err": rel_err, "tol": 1e-11, "ok": rel_err <= 1e-11,
+    parity = {"vcycle_rel_err": rel_err, "tol": 1e-11, "ok": rel_err <= 1e-11 and rho_rel <= 1e-8,
               "rho_k_gpu": [float(v) for v in hist_gpu], "rho_k_cpu": [float(v) for v in hist_cpu],
-              "rho_k_max_rel_diff": rho_rel,
-              "what": "one V-cycle z = M b and 10 stationary cycles (rho_k = ||b - A x_k||/||b||), "
-                      "GPU vs the oracle restatement on the same hierarchy"}
+              "rho_k_max_rel_diff": rho_rel, "rho_k_tol": 1e-8, "rho_k_cycles": K,
+              "what": f"one V-cycle z = M b and {K} stationary cycles (rho_k = ||b - A x_k||/||b||), "
+                      f"{what_gpu} vs the oracle restatement on the same hierarchy"}
     return res, parity
 
 
@@ -576,7 +580,7 @@ def run_dist(args, world, rank, local_rank):
         k = "xscs" if i["kernel"] == "classes" and i["xstaged"] else i["kernel"]
         return k + ("+gtc" if i["gtc"] != "none" else "")
     storages = [{w: kind(dm.level_matrix(l, w)) for w in ("A", "R", "P")} for l in range(La)]
-    n_glob = A.nrows
+    n_glob = A_rows_global = A.nrows
     del mg, A  # global fine levels are no longer needed on this rank
     torch.cuda.synchronize()
     setup_s = time.perf_counter() - t0
@@ -650,71 +654,112 @@ def run_dist(args, world, rank, local_rank):
     dist.barrier()
     halo_ms = time_kernel(lambda: Ad.apply(yl, b), 20, stream)
 
-    # residual after one cycle (global)
+    # rho_k of the distributed stationary loop (collective) and the timed z gathered
+    # on rank 0, for the parity checks below
+    K = args.parity_cycles if args.parity_cycles is not None else (10 if A_rows_global <= (1 << 25) else 5)
     x = torch.zeros_like(b)
-    it, hist = dm.stationary_solve(b, x, max_iter=2, rel_tol=1e-300)
+    it, hist = dm.stationary_solve(b, x, max_iter=K + 1, rel_tol=1e-300)
+    hist = np.asarray(hist, np.float64)
+    zparts = [None] * world if rank == 0 else None
+    dist.gather_object((r0, z.cpu().numpy()), zparts, dst=0)
     ga = torch.tensor([achieved], dtype=torch.float64)
     dist.all_reduce(ga, op=dist.ReduceOp.MIN)
     cycles_per_s = 1000.0 / ms_per_cycle
+    # rank 0, while the other ranks wait: the same global problem on this one GPU
+    # (the single-GPU cycle the distributed one must reproduce; at 512^3 also
+    # the base of the C4 strong-scaling ratio), then the oracle on that hierarchy
+    # (parity of the distributed z and rho_k, and the CPU baseline)
+    single, cpu, parity = None, None, None
+    if rank == 0 and not args.no_single_base:
+        del dm, Ad, Al
+        torch.cuda.synchronize()
+        try:
+            z_dist = np.empty(A_rows_global)
+            for (p0, zp) in zparts:
+                z_dist[p0:p0 + zp.shape[0]] = zp
+            single, cpu, parity = dist_single_side(fa, ctx, args, stream, dims, z_dist, hist)
+        except Exception as e:  # reported, never fatal to the distributed measurement
+            log(f"single-GPU base / parity failed: {e!r}")
+            single = {"error": repr(e)}
+    sb = torch.tensor([(single or {}).get("vcycles_per_s") or 0.0], dtype=torch.float64)
+    dist.broadcast(sb, src=0)
+    base = float(sb[0])
+    ratio = round(cycles_per_s / base, 3) if base > 0 else None
     c4 = None
-    if dims == (512, 512, 512) and args.problem == "7pt" and not args.no_c4_base:
-        # C4 strong-scaling ratio: the same 512^3 problem on one
-        # GPU, timed in this job by rank 0 while the other ranks wait
-        base = None
-        if rank == 0:
-            del dm, Ad, Al
-            torch.cuda.synchronize()
-            base = c4_single_gpu_rate(fa, ctx, args, stream)
-        tb = torch.tensor([base or 0.0], dtype=torch.float64)
-        dist.broadcast(tb, src=0)
-        base = float(tb[0])
+    if dims == (512, 512, 512) and args.problem == "7pt":
         c4 = {"global_vcycles_per_s": round(cycles_per_s, 3), "one_gpu_512_vcycles_per_s": round(base, 3),
-              "ratio_vs_1gpu": round(cycles_per_s / base, 3) if base > 0 else None, "gpus": world,
+              "ratio_vs_1gpu": ratio, "gpus": world,
               "what": "512^3 7-pt (C4): V-cycles/s of this row-split run / V-cycles/s of the same "
                       "hierarchy on one GPU (single-GPU path, measured in this job by rank 0)"}
+    out = dist_line(args, world, dims, strong, ms_per_cycle, cycles_per_s, ratio, c4, single, cpu, parity,
+                    extra={"levels": nl, "level_plan_rank0": infos, "setup_s": round(setup_s, 2),
+                           "fine_spmv_with_halo_ms": round(halo_ms, 4),
+                           "rel_residual_after_1_cycle": float(hist[1]) if len(hist) > 1 else None,
+                           "agglomerate_rows": args.agglomerate,
+                           "halo_overlap": not args.no_overlap,
+                           "dist_graph": graph,
+                           "local_storages_rank0": storages,
+                           "vcycle_plan_rank0": {"launches": plan["launches"],
+                                                 "source": "amg_dist_cycle_plan (the launches this rank makes)",
+                                                 "per_level_GB": [round(d["bytes"] / 1e9, 4)
+                                                                  for d in plan["per_level"]],
+                                                 "per_level_kernels": [d["kernels"] for d in plan["per_level"]]},
+                           "rccl": fa.rccl_library(),
+                           "rccl_ranks": comm.nranks},
+                    roofline={"bound": "hbm", "achieved": round(float(ga[0]), 1), "peak": HBM_PEAK_GBS,
+                              "unit": "GB/s", "frac": round(float(ga[0]) / HBM_PEAK_GBS, 4), "traffic": None,
+                              "kernel": f"{al_info['kernel']} SpMV (SET) on the rank-local A_0 (min over ranks)",
+                              "bytes_per_launch": bytes_spmv, "ms_per_launch": round(spmv_ms, 5)})
+    dist.destroy_process_group()
+    return out if rank == 0 else None
+
+
+DIST_LINE_KEYS = ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better",
+                  "scaling", "vs_baseline", "ratio_vs_1gpu", "ratio_vs_1gpu_what", "dtype", "data", "config",
+                  "fine_spmv_gbs", "roofline", "cpu_baseline", "parity")
+
+
+def dist_line(args, world, dims, strong, ms_per_cycle, cycles_per_s, ratio, c4, single, cpu, parity, extra,
+              roofline, transport="RCCL"):
+    """The JSON line of a distributed run (rank 0): value = global V-cycles/s (strong)
+    or x N (weak: 256^3-equivalent cycles/s of the whole job); ratio_vs_1gpu = the
+    global rate over the same global problem's one-GPU rate (at 512^3 the C4
+    strong-scaling ratio); cpu_baseline / parity from the oracle on rank 0."""
     out = {
         "metric": METRIC,
-        "value": round(cycles_per_s if strong else cycles_per_s * world, 3),
+        "value": None if cycles_per_s is None else round(cycles_per_s if strong else cycles_per_s * world, 3),
         "unit": "V-cycles/s",
-        "n_gpus": comm.nranks,
+        "n_gpus": world,
         "steps": args.steps,
         "warmup": args.warmup,
-        "ms_per_step": round(ms_per_cycle, 4),
+        "ms_per_step": None if ms_per_cycle is None else round(ms_per_cycle, 4),
         "higher_is_better": True,
         "scaling": "strong" if strong else ("weak" if world > 1 else "none"),
         "vs_baseline": None,
+        "ratio_vs_1gpu": ratio,
+        "ratio_vs_1gpu_what": (f"global V-cycles/s of this {world}-rank run / V-cycles/s of the same global "
+                               f"problem ({dims[0]}x{dims[1]}x{dims[2]}) on one GPU, measured by rank 0 in this "
+                               f"job" + (" = the C4 strong-scaling ratio (SURVEY.md 8(e), target >= 6 at 8 GPUs)"
+                                         if tuple(dims) == (512, 512, 512) else "")),
         "dtype": "f64",
         "data": "synthetic (device-generated operator, splitmix64 rhs seed 42)",
-        "config": {"workload": workload_name(args, dims) + (
-                       f"; C4 strong scaling: fixed 512^3 over {world} GPUs, value = global V-cycles/s"
-                       if strong else f"; weak scaling: {world} x {args.edge}^3 rows, "
-                                      f"value = global V-cycles/s x {world}"),
-                   "c4_strong": c4,
-                   "global_vcycles_per_s": round(cycles_per_s, 3),
-                   "levels": nl, "level_plan_rank0": infos, "setup_s": round(setup_s, 2),
-                   "fine_spmv_with_halo_ms": round(halo_ms, 4),
-                   "rel_residual_after_1_cycle": float(hist[1]) if len(hist) > 1 else None,
-                   "agglomerate_rows": args.agglomerate,
-                   "halo_overlap": not args.no_overlap,
-                   "dist_graph": graph,
-                   "local_storages_rank0": storages,
-                   "vcycle_plan_rank0": {"launches": plan["launches"],
-                                         "source": "amg_dist_cycle_plan (the launches this rank makes)",
-                                         "per_level_GB": [round(d["bytes"] / 1e9, 4) for d in plan["per_level"]],
-                                         "per_level_kernels": [d["kernels"] for d in plan["per_level"]]},
-                   "rccl": fa.rccl_library(),
-                   "rccl_ranks": comm.nranks,
-                   "parallelism": f"row-block {'z-slabs' if args.problem in ('7pt', '27pt') else 'row ranges'} "
-                                  f"x{world}, RCCL halo exchange"},
-        "fine_spmv_gbs": round(float(ga[0]), 1),
-        "roofline": {"bound": "hbm", "achieved": round(float(ga[0]), 1), "peak": HBM_PEAK_GBS,
-                     "unit": "GB/s", "frac": round(float(ga[0]) / HBM_PEAK_GBS, 4), "traffic": None,
-                     "kernel": f"{al_info['kernel']} SpMV (SET) on the rank-local A_0 (min over ranks)",
-                     "bytes_per_launch": bytes_spmv, "ms_per_launch": round(spmv_ms, 5)},
-        "cpu_baseline": None,
+        "config": dict({"workload": workload_name(args, dims) + (
+                            f"; C4 strong scaling: fixed 512^3 over {world} ranks, value = global V-cycles/s"
+                            if strong else f"; weak scaling: {world} x {args.edge}^3 rows, "
+                                           f"value = global V-cycles/s x {world}"),
+                        "c4_strong": c4,
+                        "single_gpu_same_problem": single,
+                        "global_vcycles_per_s": None if cycles_per_s is None else round(cycles_per_s, 3),
+                        "parallelism": f"row-block "
+                                       f"{'z-slabs' if args.problem in ('7pt', '27pt') else 'row ranges'} "
+                                       f"x{world}, {transport} halo exchange"}, **extra),
+        "fine_spmv_gbs": roofline.get("achieved"),
+        "roofline": roofline,
+        "cpu_baseline": cpu,
+        "parity": parity,
     }
-    dist.destroy_process_group()
-    return out if rank == 0 else None
+    assert tuple(out) == DIST_LINE_KEYS
+    return out
 
 
 def general_roofline(fa, ctx, dims, stream, x, y):
@@ -754,21 +799,147 @@ def general_roofline(fa, ctx, dims, stream, x, y):
     return out
 
 
-def c4_single_gpu_rate(fa, ctx, args, stream, cycles=10):
-    """V-cycles/s of the 512^3 hierarchy on this one GPU (the C4 base rate)."""
-    import torch
-    dims = (512, 512, 512)
+def dist_single_side(fa, ctx, args, stream, dims, z_dist, hist_dist, cycles=10):
+    """Rank 0 of a distributed run, after its timing: the same global problem on
+    this one GPU -- its V-cycles/s (at 512^3 the C4 base rate), its z against the
+    distributed z (the row split keeps every row's arithmetic: <= 1e-13), then the
+    oracle on that hierarchy: one cycle against the distributed z (<= 1e-11),
+    rho_k of the distributed stationary loop against the oracle's (<= 1e-8), and
+    the CPU baseline from the oracle's cycles (budgeted: at 512^3 one cycle of the
+    restated rayon path takes seconds)."""
     A, mg = build_problem(fa, ctx, args, dims)
+    out = single_side(fa, args, stream, A, mg, dims, z_dist, hist_dist, cycles)
+    del mg, A
+    import torch
+    torch.cuda.synchronize()
+    return out
+
+
+def single_side(fa, args, stream, A, mg, dims, z_dist, hist_dist, cycles=10, what="the distributed GPU run"):
+    """One-GPU rate of the global hierarchy (A, mg), its z against the distributed
+    z, and the oracle's parity / CPU baseline on that hierarchy (dist_single_side)."""
+    import numpy as np
+    import torch
     n = A.nrows
-    b = torch.as_tensor(splitmix_uniform(n, 42), device=torch.cuda.current_device())
+    b_host = splitmix_uniform(n, 42)
+    b = torch.as_tensor(b_host, device=torch.cuda.current_device())
     z = torch.empty_like(b)
     for _ in range(2):
         mg.apply(z, b)
     ms = time_kernel(lambda: mg.apply(z, b), cycles, stream)
-    del mg, A
     torch.cuda.synchronize()
-    log(f"C4 base: 512^3 on one GPU {1000.0 / ms:.2f} V-cycles/s")
-    return 1000.0 / ms
+    zs = z.cpu().numpy()
+    rel = float(np.linalg.norm(z_dist - zs) / np.linalg.norm(zs))
+    single = {"vcycles_per_s": round(1000.0 / ms, 3), "ms_per_step": round(ms, 4), "cycles": cycles,
+              "z_rel_diff_vs_distributed": rel, "tol": 1e-13, "ok": rel <= 1e-13,
+              "what": "the global problem's hierarchy on one GPU (single-GPU path) timed by rank 0 in this job; "
+                      "its z = M b against the distributed run's timed z"}
+    log(f"single-GPU base: {dims} {single['vcycles_per_s']:.2f} V-cycles/s, z rel diff vs distributed {rel:.2e}")
+    cpu, parity = None, None
+    if not args.no_cpu_baseline:
+        K = len(hist_dist) - 1
+        cpu, parity = cpu_side(mg, A, b_host, z_dist, args, hist_gpu=hist_dist, rho_cycles=K, min_cycles=1,
+                               budget=args.cpu_budget / 2, what_gpu=what + " (z gathered on rank 0)")
+        cpu["sample"] += f"; global problem {dims[0]}x{dims[1]}x{dims[2]}, rank 0's host"
+        log(f"parity (distributed vs oracle): V-cycle rel err {parity['vcycle_rel_err']:.3e}, "
+            f"rho_k max rel diff {parity['rho_k_max_rel_diff']:.3e} over {K} cycles")
+    return single, cpu, parity
+
+
+def run_loopback(args):
+    """--loopback N: the distributed cycle with N virtual ranks on this one GPU
+    (threads of this process over the library's loopback transport: the same
+    row-block split, halo plans, slab frames and agglomeration as N RCCL ranks,
+    with device copies instead of xGMI).  A rehearsal of the N-GPU line on a
+    1-GPU box -- the same fields (parity against the oracle, CPU baseline,
+    ratio to the one-GPU rate) -- whose rate measures N ranks time-sharing one
+    GPU, not scaling."""
+    import threading
+
+    import numpy as np
+    import torch
+
+    import faer_amg_amd as fa
+
+    N = args.loopback
+    torch.cuda.set_device(0)
+    stream = torch.cuda.Stream()
+    torch.cuda.set_stream(stream)
+    ctx = fa.Context(0, stream=stream.cuda_stream)
+    strong = args.workload == "c4"
+    dims = (512, 512, 512) if strong else weak_dims(args.edge, N)
+    t0 = time.perf_counter()
+    A, mg = build_problem(fa, ctx, args, dims)
+    n = A.nrows
+    b_host = splitmix_uniform(n, 42)
+    b = torch.as_tensor(b_host, device="cuda:0")
+    zg = torch.empty_like(b)
+    mg.apply(zg, b)  # codes the Jacobi diagonals before the ranks share the levels
+    torch.cuda.synchronize()
+    nl = mg.levels()
+    splits = fa.slab_splits(fa.box_level_dims(dims, (args.box,) * 3, nl), N)
+    hub = fa.LoopbackHub(N)
+    comms, dms = [None] * N, [None] * N
+
+    def ranks(fn):
+        out, errs = [None] * N, []
+
+        def body(r):
+            try:
+                out[r] = fn(r)
+            except BaseException as e:  # noqa: BLE001
+                errs.append(e)
+        th = [threading.Thread(target=body, args=(r,)) for r in range(N)]
+        for t in th:
+            t.start()
+        for t in th:
+            t.join()
+        if errs:
+            raise errs[0]
+        return out
+
+    def build(r):
+        comms[r] = fa.Comm(ctx, hub=hub, rank=r)
+        dms[r] = fa.DistMultigrid(comms[r], mg, splits, agglomerate_rows=args.agglomerate)
+        return dms[r].local_rows()
+    rows = ranks(build)
+    setup_s = time.perf_counter() - t0
+    infos = [dms[0].level_info(l) for l in range(nl)]
+    bs = [b[r0:r1] for (r0, r1) in rows]
+    zs = [torch.empty_like(bb) for bb in bs]
+    for _ in range(args.warmup):
+        ranks(lambda r: dms[r].apply(zs[r], bs[r]))
+    torch.cuda.synchronize()
+
+    def timed(r):
+        for _ in range(args.steps):
+            dms[r].apply(zs[r], bs[r])
+    tw = time.perf_counter()
+    ranks(timed)
+    torch.cuda.synchronize()
+    ms = 1000.0 * (time.perf_counter() - tw) / args.steps
+    K = args.parity_cycles if args.parity_cycles is not None else (10 if n <= (1 << 25) else 5)
+    xs = [torch.zeros_like(bb) for bb in bs]
+    hists = ranks(lambda r: dms[r].stationary_solve(bs[r], xs[r], max_iter=K + 1, rel_tol=1e-300)[1])
+    z_dist = torch.cat(zs).cpu().numpy()
+    del dms, comms
+    torch.cuda.synchronize()
+    single, cpu, parity = single_side(fa, args, stream, A, mg, dims, z_dist, np.asarray(hists[0]), 10,
+                                      what=f"the {N}-rank loopback run")
+    cps = 1000.0 / ms
+    ratio = round(cps / single["vcycles_per_s"], 3)
+    c4 = None
+    if dims == (512, 512, 512) and args.problem == "7pt":
+        c4 = {"global_vcycles_per_s": round(cps, 3), "one_gpu_512_vcycles_per_s": single["vcycles_per_s"],
+              "ratio_vs_1gpu": ratio, "gpus": 1, "virtual_ranks": N,
+              "what": "loopback rehearsal: N virtual ranks time-share one GPU (not a scaling figure)"}
+    return dist_line(args, N, dims, strong, ms, cps, ratio, c4, single, cpu, parity,
+                     extra={"levels": nl, "level_plan_rank0": infos, "setup_s": round(setup_s, 2),
+                            "rel_residual_after_1_cycle": float(hists[0][1]) if len(hists[0]) > 1 else None,
+                            "agglomerate_rows": args.agglomerate, "physical_gpus": 1,
+                            "note": f"{N} virtual ranks on one GPU (loopback transport): value is not a "
+                                    f"multi-GPU rate; the line rehearses the N-GPU line's fields"},
+                     roofline={}, transport="loopback (device copies)")
 
 
 def visible_gpus():
@@ -852,8 +1023,11 @@ def launch_check(world, rank):
     dist.init_process_group("gloo")
     t = torch.tensor([1.0], dtype=torch.float64)
     dist.all_reduce(t)
-    out = {"metric": METRIC, "value": None, "n_gpus": dist.get_world_size(), "ranks_counted": int(t[0]),
-           "launch_check": True}
+    args = argparse.Namespace(steps=0, warmup=0, problem="7pt", edge=256, box=2, smoother="jacobi")
+    world = dist.get_world_size()
+    dims = weak_dims(256, world)
+    out = dist_line(args, world, dims, False, None, None, None, None, None, None, None, {}, {})
+    out.update({"ranks_counted": int(t[0]), "launch_check": True})
     dist.destroy_process_group()
     return out if rank == 0 else None
 
@@ -905,15 +1079,21 @@ def main():
     ap.add_argument("--workload", default="weak", choices=["weak", "c4"],
                     help="N > 1: weak (N x edge^3 rows; at N = 8 the grid is 512^3 = C4 and the line "
                          "carries the C4 strong-scaling ratio) or c4 (512^3 fixed at every N, strong)")
-    ap.add_argument("--no-c4-base", action="store_true",
-                    help="skip the one-GPU 512^3 measurement behind the C4 ratio")
+    ap.add_argument("--no-single-base", "--no-c4-base", action="store_true",
+                    help="distributed: skip rank 0's one-GPU run of the same global problem (the base of "
+                         "ratio_vs_1gpu, at 512^3 the C4 ratio) and the parity / CPU baseline drawn from it")
+    ap.add_argument("--parity-cycles", type=int, default=None,
+                    help="distributed: stationary cycles compared with the oracle (default 10; 5 above 2^25 rows)")
     ap.add_argument("--plan-out", default=None,
                     help="write the V-cycle launch plan (JSON) here, for scripts/prof_summary.py --plan")
+    ap.add_argument("--loopback", type=int, default=0,
+                    help="N virtual ranks of the distributed cycle on this one GPU (loopback transport): "
+                         "rehearses the N-GPU line's parity / CPU-baseline / ratio fields")
     ap.add_argument("--dist", action="store_true",
                     help="distributed path even at world size 1 (1-rank RCCL; a check of run_dist)")
     args = ap.parse_args()
     if args.agglomerate is None:
-        args.agglomerate = 16384 * max(1, int(os.environ.get("WORLD_SIZE", "1")))
+        args.agglomerate = 16384 * max(1, args.loopback, int(os.environ.get("WORLD_SIZE", "1")))
     if args.smoother is None:
         args.smoother = {"7pt": "jacobi", "27pt": "sgs"}.get(args.problem, "l1")
     if args.problem == "mtx" and not args.mtx:
@@ -935,7 +1115,9 @@ def main():
         return
     if args.workload == "c4" and world == 1 and not args.dist:
         args.edge = 512  # C4 on one GPU: the base of the strong-scaling curve
-    if world > 1 or args.dist:
+    if args.loopback > 0:
+        out = run_loopback(args)
+    elif world > 1 or args.dist:
         out = run_dist(args, world, rank, local_rank)
     else:
         out = run_single(args)

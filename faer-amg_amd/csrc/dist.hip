@@ -1099,6 +1099,8 @@ static std::shared_ptr<DistMultigridOp> build_dist(amg_comm *comm, const Multigr
         const GpuCsr &Ag = dynamic_cast<CsrOp *>(g.levels[d->La].A.get())->m;
         set_frames(D.P->m, D.sp.frame, owned_frame(Ag, 0, Ag.nrows), false);
         csr_finalize(D.P->m);
+        // the same waves per row as the global P (finalize chose from the local rows)
+        D.P->m.vec_wpr = dynamic_cast<CsrOp *>(g.levels[d->La - 1].P.get())->m.vec_wpr;
     }
     // R_l / P_l of a 2x2x2-box level as grid-transfer classes through the slab
     // frames (the classes of their global rows; every entry checked)
@@ -1137,6 +1139,7 @@ static std::shared_ptr<DistMultigridOp> build_dist(amg_comm *comm, const Multigr
     d->tail->steps = g.steps;
     d->tail->fold_zero_guess = g.fold_zero_guess;
     d->tail->sgs_residual_form = g.sgs_residual_form;
+    d->tail->restrict_df = g.restrict_df;  // DistMultigridOp::restrict_df reads it
     for (int64_t l = d->La; l < d->nlevels; l++) d->tail->levels.push_back(MgLevel{g.levels[l].A, g.levels[l].S, g.levels[l].R, g.levels[l].P});
     d->tail->nrows = d->tail->ncols = g.levels[d->La].A->nrows;
     // the tail is cycled redundantly on every rank: under the auto policy,

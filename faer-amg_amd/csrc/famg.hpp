@@ -32,12 +32,12 @@ __device__ __forceinline__ int xcd_remap(int b, int nb) {
 // q / d for 0 <= q < 2^14 through a float reciprocal r = 1.0f / d: (q + 0.5) / d
 // lies at least 0.5 / d from an integer, far beyond the float error, for the
 // window and tile extents the staging loops divide by.  fdiv_exact checks every
-// q < n on the host before a kernel relies on it (memoised per (n, d)).
+// q < n on the host before a kernel relies on it (memoised per (n, d) in a
+// per-thread table: the eager launch paths of the loopback ranks call it
+// without a lock).
 __device__ __forceinline__ int fdiv_rcp(int q, float r) { return (int)(((float)q + 0.5f) * r); }
 inline bool fdiv_exact(int n, int d, float r) {
-    static std::mutex mu;
-    static std::vector<std::pair<int, int>> ok;
-    std::lock_guard<std::mutex> g(mu);
+    thread_local std::vector<std::pair<int, int>> ok;
     for (const auto &e : ok)
         if (e.first >= n && e.second == d) return true;
     for (int q = 0; q < n; q++)

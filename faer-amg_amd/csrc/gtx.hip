@@ -338,7 +338,11 @@ int gtx_mode() {
 static bool gtx_beats_storage(GpuCsr &m) {
     const int64_t how = flag(FLAG_GTX_TIME);
     if (how == 0 || gtx_mode() == 2) return true;
-    if (how != 1) return m.nrows >= (int64_t(1) << 18);
+    // a rank-local matrix of a distributed level (rframe on) is sized by its global
+    // operator's rows, so every rank keeps the storage -- and the rounding -- of
+    // the single-GPU cycle
+    const int64_t rows = m.rframe.on() ? m.rframe.nx * m.rframe.ny * m.rframe.gz : m.nrows;
+    if (how != 1) return rows >= (int64_t(1) << 18);
     // R of the small levels (<= 65536 coarse rows of hundreds of entries) loses in the cycle
     // even where an isolated timing has it ahead (R_2 of the 256^3 cycle: 32.5 vs 21.9 + 4.6 us)
     if (m.gtx_r && m.nrows <= 65536) return false;

@@ -775,6 +775,8 @@ static void sgs27_phase(const SgsOp &S, int pz, int nst, const int *px, const in
         a.ntiles = (int)ceil_div(S.ny27, a.ty);
         const int cus = std::max(S.ctx->num_cus, 1);
         a.rnx2 = 1.0f / (float)(S.nx27 / 2);
+        FAMG_REQUIRE(fdiv_exact((a.ty + 2 * halo + 2) * (S.nx27 / 2) + 1024, S.nx27 / 2, a.rnx2), AMG_ERR_UNSUPPORTED,
+                     "sgs27 march: float reciprocal division not exact for this plane width");
         a.jper = flag(FLAG_SGS27_MARCH) > 1 ? (int)flag(FLAG_SGS27_MARCH) : (int)std::max<int64_t>(1, ceil_div((int64_t)nplanes * a.ntiles, cus));
         const int64_t nchunks = ceil_div(nplanes, a.jper);
         const size_t lds_m = (size_t)3 * (a.ty + 2 * halo + 2) * (S.nx27 + 4) * sizeof(double);

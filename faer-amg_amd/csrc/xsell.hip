@@ -153,6 +153,187 @@ __global__ __launch_bounds__(XS_BS) void spmv_xs_kernel(XsArgs a) {
     }
 }
 
+// ---------------------------------------------------------------- pipelined form
+// The kernel above pays two dependent memory round trips per staging trip (the
+// chunk id, then its x entries: ten trips of a 1024-thread workgroup for 320
+// chunks) and one round trip per slice walk with nothing else in flight.  Here
+// (default; FLAG_XS_PIPE = 0 selects the kernel above):
+//  * every wave issues the value/index loads of its first 8-step batch and its
+//    first slice's epilogue operands before the staging starts, so the matrix
+//    stream runs under the staging;
+//  * the staging loads all its chunk ids at once, then all its x pairs, then
+//    writes LDS (two round trips per workgroup instead of twenty);
+//  * the walk is software pipelined over a wave's batches (8 steps of one slice):
+//    batch k + 1's loads are issued before batch k's LDS gathers and fmas.  A
+//    batch past the slice's width loads its last step again (clamped, never
+//    summed), the batch after the wave's last one reloads that one: no branch
+//    around a load, so the compiler counts the loads in flight exactly.
+// Per row the same stored entries are summed in the same order: bitwise the
+// kernel above.
+constexpr int XS_B = 8;                      // steps per batch
+constexpr int XS_STAGE = (XS_MAXCH * XS_CH / 2 + XS_BS - 1) / XS_BS;  // 16-B staging loads per thread
+
+struct XsBatch {
+    double v[XS_B];
+    int32_t ix[XS_B];
+};
+
+// operands the epilogue of one row needs (loaded with the slice's first batch)
+struct XsEpi {
+    double x, b, d, y;
+};
+
+// a batch's loads: steps t0..t0+7 clamped to the slice's last step (no branch
+// around a load: on a control-flow join the compiler's wait counting turns
+// conservative).  Escape slices are read the same way (their 32-bit column
+// block read as 16-bit halves: in bounds, never summed -- see below).
+__device__ __forceinline__ void xs_issue(XsBatch &B, const char *blk, int w, int t0, int lane) {
+    const double *vp = reinterpret_cast<const double *>(blk) + lane;
+    const uint16_t *ip = reinterpret_cast<const uint16_t *>(blk + (int64_t)w * 512) + lane;
+    const int tl = w - 1;  // every slice has >= 1 step
+#pragma unroll
+    for (int u = 0; u < XS_B; u++) B.v[u] = __builtin_nontemporal_load(vp + (int64_t)min(t0 + u, tl) * 64);
+#pragma unroll
+    for (int u = 0; u < XS_B; u++) B.ix[u] = __builtin_nontemporal_load(ip + (int64_t)min(t0 + u, tl) * 64);
+}
+
+template <int MODE>
+__device__ __forceinline__ XsEpi xs_epi_load(const XsArgs &a, int row) {
+    XsEpi e{0.0, 0.0, 0.0, 0.0};
+    const int r = min(row, a.nrows - 1);  // padding lanes: any row, never stored
+    if constexpr (MODE == SPMV_JACOBI) {
+        e.x = a.x[r];
+        e.d = a.dc ? a.dt[a.dc[r]] : a.d[r];
+    }
+    if constexpr (MODE == SPMV_JACOBI || MODE == SPMV_RESID || MODE == SPMV_RESID0) e.b = a.b[r];
+    if constexpr (MODE == SPMV_ADD) e.y = a.y[r];
+    if constexpr (MODE == SPMV_ADD0) e.y = (a.dc ? a.dt[a.dc[r]] : a.d[r]) * a.b[r];
+    return e;
+}
+
+// LDS gathers (indices clamped into the window: an escape slice's are not LDS
+// indices) and the fmas of the batch's first cnt steps
+__device__ __forceinline__ double xs_consume(const XsBatch &B, int cnt, const double *sx, double acc) {
+    double xv[XS_B];
+#pragma unroll
+    for (int u = 0; u < XS_B; u++) xv[u] = sx[min(B.ix[u], XS_MAXCH * XS_CH - 1)];
+#pragma unroll
+    for (int u = 0; u < XS_B; u++)
+        if (u < cnt) acc = fma(B.v[u], xv[u], acc);
+    return acc;
+}
+
+template <int MODE>
+__global__ __launch_bounds__(XS_BS) void spmv_xs_pipe_kernel(XsArgs a) {
+    __shared__ double sx[XS_MAXCH * XS_CH];
+    const int g = xcd_remap(blockIdx.x, gridDim.x);
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int s_end = min((g + 1) * XS_SLICES, (a.nrows + 63) / 64);
+    const int s_last = s_end - 1;
+
+    // the wave's first batch and epilogue operands, in flight during the staging
+    int s = g * XS_SLICES + wave;
+    int sc = min(s, s_last);
+    int w = a.soff[sc + 1] - a.soff[sc];
+    uint32_t dsc = a.desc[sc];
+    XsBatch cur;
+    xs_issue(cur, a.data + (int64_t)(dsc & 0x3fffffffu) * 128, w, 0, lane);
+    XsEpi epi = xs_epi_load<MODE>(a, sc * 64 + lane);
+
+    // staging: all chunk ids, then all x pairs, then the LDS writes
+    {
+        const int c0 = a.coff[g], nch = a.coff[g + 1] - c0, tot = nch * (XS_CH / 2);
+        int32_t ch[XS_STAGE];
+#pragma unroll
+        for (int k = 0; k < XS_STAGE; k++) {
+            const int i = min((int)threadIdx.x + k * XS_BS, tot - 1);
+            ch[k] = a.chunks[c0 + i / (XS_CH / 2)];
+        }
+        xs_dbl2_t v[XS_STAGE];
+        const int64_t nc = a.ncols;
+#pragma unroll
+        for (int k = 0; k < XS_STAGE; k++) {
+            const int i = min((int)threadIdx.x + k * XS_BS, tot - 1);
+            const int64_t e = (int64_t)ch[k] * XS_CH + 2 * (i % (XS_CH / 2));  // even
+            const int64_t ea = min(e, nc - 2);                                   // ncols >= 2: a pair in range
+            xs_dbl2_t xv = *reinterpret_cast<const xs_dbl2_t *>(a.x + ea);
+            if constexpr (MODE == SPMV_RESID0) xv = *reinterpret_cast<const xs_dbl2_t *>(a.d + ea) * xv;
+            // e = nc - 1 (odd nc): the pair loaded is (nc - 2, nc - 1); e >= nc: zeros
+            const double lo = e == ea ? xv.x : (e == nc - 1 ? xv.y : 0.0);
+            const double hi = e == ea ? xv.y : 0.0;
+            v[k] = xs_dbl2_t{lo, hi};
+        }
+#pragma unroll
+        for (int k = 0; k < XS_STAGE; k++) {
+            const int i = (int)threadIdx.x + k * XS_BS;
+            if (i < tot) *reinterpret_cast<xs_dbl2_t *>(sx + 2 * i) = v[k];
+        }
+    }
+    __syncthreads();
+
+    double acc = 0.0;
+    int t0 = 0;
+    bool done = s >= s_end;
+    // one pipeline step: consume cur, with nxt's loads in flight (two buffers
+    // alternate roles, so no register copy waits for the loads)
+    // a finished row's y is stored at the start of the next step, before that
+    // step's loads: on gfx950 stores count in vmcnt, so a store issued after the
+    // loads would make the next register reuse wait for all of them
+    int prow = -1;
+    double pval = 0.0;
+    auto step = [&](const XsBatch &cur, XsBatch &nxt) {
+        if (prow >= 0 && prow < a.nrows) a.y[prow] = pval;
+        prow = -1;
+        const bool last = t0 + XS_B >= w;
+        const int sn = last ? s + XS_BS / 64 : s, tn = last ? 0 : t0 + XS_B;
+        // the next batch (the wave's last batch again past its end)
+        const bool more = sn < s_end;
+        const int snc = min(sn, s_last);
+        const int wn = more ? a.soff[snc + 1] - a.soff[snc] : w;
+        const uint32_t dn = more ? a.desc[snc] : dsc;
+        xs_issue(nxt, a.data + (int64_t)(dn & 0x3fffffffu) * 128, wn, more ? tn : t0, lane);
+        const XsEpi en = xs_epi_load<MODE>(a, snc * 64 + lane);
+        acc = xs_consume(cur, min(XS_B, w - t0), sx, acc);
+        if (last) {
+            prow = (dsc >> 30) == 1 ? s * 64 + lane : -1;  // escape slices: below
+            if constexpr (MODE == SPMV_SET) pval = acc;
+            else if constexpr (MODE == SPMV_ADD || MODE == SPMV_ADD0) pval = epi.y + acc;
+            else if constexpr (MODE == SPMV_RESID || MODE == SPMV_RESID0) pval = epi.b - acc;
+            else pval = epi.x + epi.d * (epi.b - acc);  // JACOBI
+            acc = 0.0;
+            epi = en;
+        }
+        s = sn;
+        t0 = tn;
+        w = wn;
+        dsc = dn;
+        done = !more;
+    };
+    XsBatch alt;
+    while (!done) {
+        step(cur, alt);
+        if (done) break;
+        step(alt, cur);
+    }
+    if (prow >= 0 && prow < a.nrows) a.y[prow] = pval;
+    // escape slices (32-bit global columns, at most 1/16 of the slices) gather x
+    // through the caches, one slice at a time as in the kernel above
+    for (int e = g * XS_SLICES + wave; e < s_end; e += XS_BS / 64) {
+        const uint32_t d = a.desc[e];
+        if ((d >> 30) == 1) continue;
+        const int row = e * 64 + lane;
+        const XsEpi ep = xs_epi_load<MODE>(a, row);
+        const double acc2 = xs_walk<2, MODE>(a.data + (int64_t)(d & 0x3fffffffu) * 128, a.soff[e + 1] - a.soff[e], lane, sx, a);
+        if (row < a.nrows) {
+            if constexpr (MODE == SPMV_SET) a.y[row] = acc2;
+            else if constexpr (MODE == SPMV_ADD || MODE == SPMV_ADD0) a.y[row] = ep.y + acc2;
+            else if constexpr (MODE == SPMV_RESID || MODE == SPMV_RESID0) a.y[row] = ep.b - acc2;
+            else a.y[row] = ep.x + ep.d * (ep.b - acc2);  // JACOBI
+        }
+    }
+}
+
 // one thread per row: values and indices of its lane in its slice
 __global__ __launch_bounds__(256) void k_xs_fill(const int64_t *rp, const int32_t *col, const double *val,
                                                  int64_t n, int64_t ns, const uint32_t *desc, const int32_t *soff,
@@ -256,7 +437,7 @@ bool build_xs(GpuCsr &m, const std::vector<int64_t> &rp) {
                     esc = !std::binary_search(keep.begin(), keep.end(), col[e] / XS_CH);
             }
             if (ws > XS_MAX_W) too_wide = true;
-            w[s] = ws;
+            w[s] = std::max<int32_t>(ws, 1);  // an all-empty slice: one padding step (0.0 at index 0)
             mode[s] = esc ? 2 : 1;
         }
         if (keep.empty()) keep.push_back(0);
@@ -279,7 +460,7 @@ bool build_xs(GpuCsr &m, const std::vector<int64_t> &rp) {
         chunks.insert(chunks.end(), gch[g].begin(), gch[g].end());
         coff[g + 1] = (int32_t)chunks.size();
     }
-    m.xs_data.resize(std::max<int64_t>(128, bytes));
+    m.xs_data.resize(std::max<int64_t>(128, bytes));  // every slice has >= 1 step: no load leaves it
     m.xs_desc.resize(ns);
     m.xs_soff.resize(ns + 1);
     m.xs_coff.resize(ng + 1);
@@ -307,15 +488,19 @@ void spmv_xs(const GpuCsr &m, const double *x, double *y, SpmvMode mode, const S
     XsArgs a{m.xs_data.get(), m.xs_desc.get(), m.xs_soff.get(), m.xs_coff.get(), m.xs_chunks.get(),
              (int32_t)m.nrows, (int32_t)m.ncols, (int32_t)m.xs_groups, x, y, epi.b, epi.d, epi.dc, epi.dt};
     const dim3 grid((unsigned)m.xs_groups), block(XS_BS);
-    switch (mode) {
-    case SPMV_SET: spmv_xs_kernel<SPMV_SET><<<grid, block, 0, s>>>(a); break;
-    case SPMV_ADD: spmv_xs_kernel<SPMV_ADD><<<grid, block, 0, s>>>(a); break;
-    case SPMV_RESID: spmv_xs_kernel<SPMV_RESID><<<grid, block, 0, s>>>(a); break;
-    case SPMV_JACOBI: spmv_xs_kernel<SPMV_JACOBI><<<grid, block, 0, s>>>(a); break;
-    case SPMV_RESID0: spmv_xs_kernel<SPMV_RESID0><<<grid, block, 0, s>>>(a); break;
-    case SPMV_ADD0: spmv_xs_kernel<SPMV_ADD0><<<grid, block, 0, s>>>(a); break;
-    default: fail(AMG_ERR_UNSUPPORTED, "x-staged SELL: unsupported SpMV epilogue");
+#define FAMG_XS_LAUNCH(K)                                                             \
+    switch (mode) {                                                                   \
+    case SPMV_SET: K<SPMV_SET><<<grid, block, 0, s>>>(a); break;                      \
+    case SPMV_ADD: K<SPMV_ADD><<<grid, block, 0, s>>>(a); break;                      \
+    case SPMV_RESID: K<SPMV_RESID><<<grid, block, 0, s>>>(a); break;                  \
+    case SPMV_JACOBI: K<SPMV_JACOBI><<<grid, block, 0, s>>>(a); break;                \
+    case SPMV_RESID0: K<SPMV_RESID0><<<grid, block, 0, s>>>(a); break;                \
+    case SPMV_ADD0: K<SPMV_ADD0><<<grid, block, 0, s>>>(a); break;                    \
+    default: fail(AMG_ERR_UNSUPPORTED, "x-staged SELL: unsupported SpMV epilogue"); \
     }
+    if (flag(FLAG_XS_PIPE) != 0) FAMG_XS_LAUNCH(spmv_xs_pipe_kernel)
+    else FAMG_XS_LAUNCH(spmv_xs_kernel)
+#undef FAMG_XS_LAUNCH
     FAMG_CHECK_HIP(hipGetLastError());
 }
 

@@ -32,6 +32,14 @@ def test_launcher_spawns_n_ranks_and_forwards_one_line(n):
     d = json.loads(lines[0])
     assert d["launch_check"] is True
     assert d["n_gpus"] == n and d["ranks_counted"] == n
+    # a distributed line carries the one-GPU ratio, the CPU baseline and the
+    # parity block beside the metric keys (bench.dist_line, verdict r04 item 2)
+    import bench
+    for k in bench.DIST_LINE_KEYS:
+        assert k in d, k
+    for k in ("ratio_vs_1gpu", "cpu_baseline", "parity", "roofline"):
+        assert k in d
+    assert d["scaling"] == "weak" and "single_gpu_same_problem" in d["config"]
     assert "torch.distributed.run" in p.stderr  # the launcher logged its child command
 
 

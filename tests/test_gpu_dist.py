@@ -483,7 +483,7 @@ def _kinds(info):
     return k + ("+gtc" if info.get("gtc", "none") != "none" else "")
 
 
-def slab_run(nranks, dims, coarsest, agglo, b, overlap=True):
+def slab_run(nranks, dims, coarsest, agglo, b, overlap=True, gtx_time=0):
     """Distributed cycle on z-slabs of a 7-pt box hierarchy: per rank its part of
     z, the storage of its local A_l / R_l / P_l, its cycle plan; plus the same
     for the single-GPU multigrid (built once per rank: the loopback ranks are
@@ -520,7 +520,7 @@ def slab_run(nranks, dims, coarsest, agglo, b, overlap=True):
     # wide grid-transfer classes wherever they build: the setup-time timing that
     # keeps them only where they win would decide per matrix (global vs local, per
     # rank) on noise, and these tests compare storages
-    fa().set_flag("gtx_time", 0)
+    fa().set_flag("gtx_time", gtx_time)
     try:
         res = run_ranks(nranks, rank_fn)
     finally:
@@ -588,6 +588,30 @@ def test_dist_slab_levels_use_grid_storages(nranks, overlap):
                 assert P.endswith("+gtc"), (l, local, glob)
         names = {p["name"] for p in plan if p["level"] < La}
         assert "xscs" in names and "gtc" in names, names
+
+
+def test_dist_slab_default_gtx_rule_matches_single_gpu():
+    """At the default keep rule of the wide grid-transfer classes (gtx_time = 2:
+    transfer operators of >= 2^18 rows), a rank-local R/P is sized by its global
+    operator: 128^3 on 4 ranks, where P_1 has 2^18 fine rows
+    globally but 2^16 per rank, keeps the classes on every rank exactly where
+    the single-GPU hierarchy does, and the cycle stays within 1e-13."""
+    import os
+    dims = (128, 128, 128)
+    b = np.random.default_rng(41).uniform(-1, 1, int(np.prod(dims)))
+    os.environ["FAMG_XSCS_VS_DIA"] = "1"
+    try:
+        z, res = slab_run(4, dims, 100, 4096, b, True, gtx_time=2)
+    finally:
+        del os.environ["FAMG_XSCS_VS_DIA"]
+    zg = res[0][7]
+    assert np.linalg.norm(z - zg) <= 1e-13 * np.linalg.norm(zg)
+    for r0, r1, _, local, glob, plan, gplan, _, La in res:
+        assert La >= 3
+        assert glob[1][2].endswith("+gtc"), glob  # P_1 keeps the classes on one GPU
+        for l in range(La):
+            for w in (1, 2):
+                assert local[l][w].endswith("+gtc") == glob[l][w].endswith("+gtc"), (l, w, local, glob)
 
 
 @pytest.mark.timeout(900)

@@ -1024,6 +1024,62 @@ def test_xsell_general_operator(ctx):
     assert Rw.spmv_info()["kernel"] == "sell"
 
 
+def test_xsell_pipelined_kernel_bitwise(ctx):
+    """The pipelined x-staged SELL kernel (flag xs_pipe = 1, the default) against
+    the round-4 kernel (xs_pipe = 0) and the oracle: every epilogue bitwise, on
+    an operator with escape slices (a few rows given one far column each: their
+    slices keep 32-bit global columns) and an all-empty slice (64 empty rows:
+    one padding step)."""
+    import scipy.sparse as sp
+    dims = (128, 128, 128)
+    A0 = fa().SparseMatOp.random7(ctx, *dims, seed=11, window=4096)
+    n = A0.nrows
+    rp, ci, va = A0.arrays()
+    R = sp.csr_matrix((va, ci, rp), shape=(n, n)).tolil()
+    rng = np.random.default_rng(12)
+    # 40 slices in 40 groups escape (< 1/16 of 32768): 32 far columns each, in 32
+    # distinct x chunks, push the group past the 320 staged chunks (its own
+    # footprint is ~300) and the least referenced (these) stay out
+    far = rng.choice(n // 4096, size=40, replace=False) * 4096 + 64 * rng.integers(0, 64, 40)
+    for r in far:
+        for j in range(32):
+            R[r + j, (r + n // 2 + 64 * j) % n] = 0.25
+    R = R.tocsr()
+    e0 = 64 * 1000  # slice 1000: 64 empty rows
+    Rl = R.tolil()
+    for r in range(e0, e0 + 64):
+        Rl.rows[r] = []
+        Rl.data[r] = []
+    R = Rl.tocsr()
+    A = fa().SparseMatOp.from_scipy(ctx, R)
+    info = A.spmv_info()
+    assert info["kernel"] == "xsell" and info["slices_i32"] > 0, info
+    x = rng.standard_normal(n)
+    b = rng.standard_normal(n)
+    d = rng.uniform(0.1, 0.2, n)
+    OA = O.Csr.from_scipy(R)
+    xd, bd, dd = T(x), T(b), T(d)
+    outs = {}
+    try:
+        for pipe in (0, 1):
+            fa().set_flag("xs_pipe", pipe)
+            for mode in ("set", "add", "resid", "jacobi"):
+                y = T(np.linspace(-1, 1, n))
+                A.spmv_epilogue(mode, xd, y, bd, dd)
+                ctx.synchronize()
+                outs[(pipe, mode)] = H(y)
+    finally:
+        fa().set_flag("xs_pipe", 1)
+    for mode in ("set", "add", "resid", "jacobi"):
+        assert np.array_equal(outs[(0, mode)].view(np.int64), outs[(1, mode)].view(np.int64)), mode
+    ax = OA.spmv(x)
+    assert np.array_equal(outs[(1, "set")].view(np.int64), ax.view(np.int64))
+    assert np.all(outs[(1, "set")][e0:e0 + 64] == 0.0)
+    assert np.array_equal(outs[(1, "resid")], b - ax)
+    assert np.array_equal(outs[(1, "add")], np.linspace(-1, 1, n) + ax)
+    assert np.array_equal(outs[(1, "jacobi")], x + d * (b - ax))
+
+
 def test_sgs_dia_sweeps(ctx):
     """Color sweeps of a constant-stencil operator run on DIA codes of the
     color-permuted copy (diagonals taken against the original row): the same
