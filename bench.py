@@ -49,6 +49,17 @@ def splitmix_uniform(n, seed=42):
     return 2.0 * u - 1.0
 
 
+def csr_traffic():
+    """HBM bytes per launch of roofline.csr's SpMV from the latest committed PMC
+    passes (scripts/pmc_csr.sh -> profiles/rNN/csr_spmv_traffic.json), or None."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "csr_spmv_traffic.json")))
+    if not files:
+        return None, None
+    d = json.load(open(files[-1]))
+    return d["hbm_bytes_per_launch"], os.path.relpath(files[-1], ROOT)
+
+
 def measured_traffic(edge, problem):
     """HBM bytes per fine-SpMV launch from the committed rocprofv3 PMC passes
     (scripts/pmc_fine_spmv.py + scripts/pmc_summary.py; FETCH_SIZE calibrated on
@@ -442,10 +453,11 @@ def run_single(args):
                    "storage": A64.spmv_info()}
     del A64
 
-    general = None
+    general, csr_block = None, None
     if args.problem == "7pt" and not args.no_general:
         general = general_roofline(fa, ctx, dims, stream, x, y)
         log("roofline.general: " + json.dumps(general))
+        csr_block = csr_roofline(general)
 
     if args.ab:
         ops = {}
@@ -533,6 +545,7 @@ def run_single(args):
                      "csr_bytes_per_launch": bytes_csr,
                      "csr_equivalent_GBs": round(bytes_csr / (spmv_ms * 1e-3) / 1e9, 1),
                      "fp64_values": fp64_values,
+                     "csr": csr_block,
                      "general": general},
         "cpu_baseline": cpu,
         "parity": parity,
@@ -760,6 +773,30 @@ def dist_line(args, world, dims, strong, ms_per_cycle, cycles_per_s, ratio, c4, 
     }
     assert tuple(out) == DIST_LINE_KEYS
     return out
+
+
+def csr_roofline(general):
+    """roofline.csr (verdict r04 item 1): the fine-level SpMV of a general CSR
+    operator -- the 7-pt 256^3 graph with random coefficients (fp64 values, no
+    value codes, no stencil structure) and rows shuffled within windows of 4096 --
+    in the storage the auto policy gives it (x-staged SELL), priced on the bytes
+    that storage moves per launch (format + x read once + y written) and on
+    SURVEY.md 8(d)'s 32-bit CSR bytes; traffic = calibrated PMC HBM bytes of the
+    same kernel (scripts/pmc_csr.sh)."""
+    res = general["window4096"]
+    kern = next(iter(res))  # the auto policy's storage (first entry)
+    r = res[kern]
+    moved, csr_b, ms = r["format_bytes_per_launch"], r["csr_bytes_per_launch"], r["ms_per_launch"]
+    achieved = moved / (ms * 1e-3) / 1e9
+    traffic, src = csr_traffic()
+    return {"bound": "hbm", "kernel": f"{kern} SpMV (SET) on the random-coefficient 7-pt 256^3 operator, "
+                                      f"rows shuffled within windows of 4096",
+            "storage": kern, "ms_per_launch": ms,
+            "bytes_per_launch": moved, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 4),
+            "csr_bytes_per_launch": csr_b, "csr_equivalent_GBs": r["achieved_csr_GBs"], "frac_csr": r["frac_csr"],
+            "traffic": traffic, "traffic_source": src,
+            "traffic_ratio": None if not traffic else round(traffic / moved, 4)}
 
 
 def general_roofline(fa, ctx, dims, stream, x, y):

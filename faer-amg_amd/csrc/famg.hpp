@@ -207,6 +207,7 @@ struct GpuCsr {
     DevBuf<uint32_t> xs_desc;
     DevBuf<int32_t> xs_soff, xs_coff, xs_chunks;
     int64_t xs_groups = 0, xs_bytes = 0, xs_steps = 0, xs_chunk_total = 0, xs_escape_slices = 0;
+    int64_t xs_maxw = 0;  // widest slice (the burst kernel's batch: 7 or 8 steps)
     int kernel = 0;  // SpmvKernel chosen at finalize
     bool spmv_ready() const { return rp32.get() != nullptr && sched.get() != nullptr; }
     bool has_sell() const { return sell_desc.get() != nullptr; }

@@ -173,9 +173,10 @@ __global__ __launch_bounds__(XS_BS) void spmv_xs_kernel(XsArgs a) {
 constexpr int XS_B = 8;                      // steps per batch
 constexpr int XS_STAGE = (XS_MAXCH * XS_CH / 2 + XS_BS - 1) / XS_BS;  // 16-B staging loads per thread
 
+template <int NB = XS_B>
 struct XsBatch {
-    double v[XS_B];
-    int32_t ix[XS_B];
+    double v[NB];
+    int32_t ix[NB];
 };
 
 // operands the epilogue of one row needs (loaded with the slice's first batch)
@@ -187,14 +188,15 @@ struct XsEpi {
 // around a load: on a control-flow join the compiler's wait counting turns
 // conservative).  Escape slices are read the same way (their 32-bit column
 // block read as 16-bit halves: in bounds, never summed -- see below).
-__device__ __forceinline__ void xs_issue(XsBatch &B, const char *blk, int w, int t0, int lane) {
+template <int NB>
+__device__ __forceinline__ void xs_issue(XsBatch<NB> &B, const char *blk, int w, int t0, int lane) {
     const double *vp = reinterpret_cast<const double *>(blk) + lane;
     const uint16_t *ip = reinterpret_cast<const uint16_t *>(blk + (int64_t)w * 512) + lane;
     const int tl = w - 1;  // every slice has >= 1 step
 #pragma unroll
-    for (int u = 0; u < XS_B; u++) B.v[u] = __builtin_nontemporal_load(vp + (int64_t)min(t0 + u, tl) * 64);
+    for (int u = 0; u < NB; u++) B.v[u] = __builtin_nontemporal_load(vp + (int64_t)min(t0 + u, tl) * 64);
 #pragma unroll
-    for (int u = 0; u < XS_B; u++) B.ix[u] = __builtin_nontemporal_load(ip + (int64_t)min(t0 + u, tl) * 64);
+    for (int u = 0; u < NB; u++) B.ix[u] = __builtin_nontemporal_load(ip + (int64_t)min(t0 + u, tl) * 64);
 }
 
 template <int MODE>
@@ -213,12 +215,13 @@ __device__ __forceinline__ XsEpi xs_epi_load(const XsArgs &a, int row) {
 
 // LDS gathers (indices clamped into the window: an escape slice's are not LDS
 // indices) and the fmas of the batch's first cnt steps
-__device__ __forceinline__ double xs_consume(const XsBatch &B, int cnt, const double *sx, double acc) {
-    double xv[XS_B];
+template <int NB>
+__device__ __forceinline__ double xs_consume(const XsBatch<NB> &B, int cnt, const double *sx, double acc) {
+    double xv[NB];
 #pragma unroll
-    for (int u = 0; u < XS_B; u++) xv[u] = sx[min(B.ix[u], XS_MAXCH * XS_CH - 1)];
+    for (int u = 0; u < NB; u++) xv[u] = sx[min(B.ix[u], XS_MAXCH * XS_CH - 1)];
 #pragma unroll
-    for (int u = 0; u < XS_B; u++)
+    for (int u = 0; u < NB; u++)
         if (u < cnt) acc = fma(B.v[u], xv[u], acc);
     return acc;
 }
@@ -237,7 +240,7 @@ __global__ __launch_bounds__(XS_BS) void spmv_xs_pipe_kernel(XsArgs a) {
     int sc = min(s, s_last);
     int w = a.soff[sc + 1] - a.soff[sc];
     uint32_t dsc = a.desc[sc];
-    XsBatch cur;
+    XsBatch<> cur;
     xs_issue(cur, a.data + (int64_t)(dsc & 0x3fffffffu) * 128, w, 0, lane);
     XsEpi epi = xs_epi_load<MODE>(a, sc * 64 + lane);
 
@@ -282,7 +285,7 @@ __global__ __launch_bounds__(XS_BS) void spmv_xs_pipe_kernel(XsArgs a) {
     // loads would make the next register reuse wait for all of them
     int prow = -1;
     double pval = 0.0;
-    auto step = [&](const XsBatch &cur, XsBatch &nxt) {
+    auto step = [&](const XsBatch<> &cur, XsBatch<> &nxt) {
         if (prow >= 0 && prow < a.nrows) a.y[prow] = pval;
         prow = -1;
         const bool last = t0 + XS_B >= w;
@@ -310,7 +313,7 @@ __global__ __launch_bounds__(XS_BS) void spmv_xs_pipe_kernel(XsArgs a) {
         dsc = dn;
         done = !more;
     };
-    XsBatch alt;
+    XsBatch<> alt;
     while (!done) {
         step(cur, alt);
         if (done) break;
@@ -320,6 +323,126 @@ __global__ __launch_bounds__(XS_BS) void spmv_xs_pipe_kernel(XsArgs a) {
     // escape slices (32-bit global columns, at most 1/16 of the slices) gather x
     // through the caches, one slice at a time as in the kernel above
     for (int e = g * XS_SLICES + wave; e < s_end; e += XS_BS / 64) {
+        const uint32_t d = a.desc[e];
+        if ((d >> 30) == 1) continue;
+        const int row = e * 64 + lane;
+        const XsEpi ep = xs_epi_load<MODE>(a, row);
+        const double acc2 = xs_walk<2, MODE>(a.data + (int64_t)(d & 0x3fffffffu) * 128, a.soff[e + 1] - a.soff[e], lane, sx, a);
+        if (row < a.nrows) {
+            if constexpr (MODE == SPMV_SET) a.y[row] = acc2;
+            else if constexpr (MODE == SPMV_ADD || MODE == SPMV_ADD0) a.y[row] = ep.y + acc2;
+            else if constexpr (MODE == SPMV_RESID || MODE == SPMV_RESID0) a.y[row] = ep.b - acc2;
+            else a.y[row] = ep.x + ep.d * (ep.b - acc2);  // JACOBI
+        }
+    }
+}
+
+// ---------------------------------------------------------------- burst form
+// One round trip per group for everything the group reads from HBM (flag
+// FLAG_XS_PIPE = 2, the default): every wave first loads the chunk ids of its
+// staging share, then issues the first NB-step batch of all four of its slices
+// (values + LDS indices: 4 x 3 NB VGPRs) and its epilogue operands, and stages
+// its chunk pairs with LDS-DMA (global_load_lds_dwordx4: one wave instruction
+// copies two 512-B chunks straight into LDS, no registers), so the group's
+// 290 KB of matrix and 160 KB of x window are in flight at once; one barrier,
+// then the four slices are summed from registers and LDS.  Slices wider than NB
+// steps load their further batches one at a time.  The folded zero-guess
+// residual (RESID0) stages d*x, a product, through registers instead.
+// Bitwise the kernels above: the same stored entries per row, in order.
+constexpr int XS_NS = XS_SLICES / (XS_BS / 64);    // slices per wave (4)
+constexpr int XS_PPW = XS_MAXCH / 2 / (XS_BS / 64);  // LDS-DMA chunk pairs per wave (10)
+
+template <int MODE, int NB>
+__global__ __launch_bounds__(XS_BS) void spmv_xs_burst_kernel(XsArgs a) {
+    __shared__ double sx[XS_MAXCH * XS_CH];
+    const int g = xcd_remap(blockIdx.x, gridDim.x);
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int s0 = g * XS_SLICES + wave;
+    const int s_end = min((g + 1) * XS_SLICES, (a.nrows + 63) / 64);
+    const int s_last = s_end - 1;
+    const int c0 = a.coff[g], nch = a.coff[g + 1] - c0;
+    const int64_t nc = a.ncols;
+
+    XsBatch<NB> B[XS_NS];
+    int W[XS_NS];
+#pragma unroll
+    for (int j = 0; j < XS_NS; j++) {
+        const int sc = min(s0 + 16 * j, s_last);
+        W[j] = a.soff[sc + 1] - a.soff[sc];
+        xs_issue(B[j], a.data + (int64_t)(a.desc[sc] & 0x3fffffffu) * 128, W[j], 0, lane);
+    }
+    if constexpr (MODE != SPMV_RESID0) {
+        // the chunk ids of the wave's pairs by scalar loads, all before the first
+        // LDS-DMA (a scalar load may not follow a write the compiler cannot rule
+        // out); counted on lgkmcnt, so the matrix loads in flight are not waited for
+        int32_t clo[XS_PPW], chi[XS_PPW];
+#pragma unroll
+        for (int j = 0; j < XS_PPW; j++) {
+            const int p = min(wave + 16 * j, (nch - 1) / 2);
+            clo[j] = a.chunks[c0 + 2 * p];
+            chi[j] = a.chunks[c0 + min(2 * p + 1, nch - 1)];
+        }
+#pragma unroll
+        for (int j = 0; j < XS_PPW; j++) {
+            const int p = wave + 16 * j;
+            if (2 * p < nch) {  // wave-uniform: the pair's first chunk exists
+                const int slot = 2 * p + (lane >> 5);
+                const int64_t e = (int64_t)(lane >> 5 ? chi[j] : clo[j]) * XS_CH + 2 * (lane & 31);
+                if (slot < nch && e + 1 < nc)
+                    __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void *)(a.x + e),
+                                                     (__attribute__((address_space(3))) void *)(sx + 2 * p * XS_CH), 16, 0, 0);
+                else if (slot < nch && e < nc)
+                    sx[slot * XS_CH + 2 * (lane & 31)] = a.x[e];  // odd ncols: the last entry alone
+            }
+        }
+    } else {
+        const int tot = nch * (XS_CH / 2);
+        for (int i = threadIdx.x; i < tot; i += XS_BS) {
+            const int64_t e = (int64_t)a.chunks[c0 + i / (XS_CH / 2)] * XS_CH + 2 * (i % (XS_CH / 2));
+            xs_dbl2_t v = {0.0, 0.0};
+            if (e + 1 < nc) v = *reinterpret_cast<const xs_dbl2_t *>(a.d + e) * *reinterpret_cast<const xs_dbl2_t *>(a.x + e);
+            else if (e < nc) v.x = a.d[e] * a.x[e];
+            *reinterpret_cast<xs_dbl2_t *>(sx + 2 * i) = v;
+        }
+    }
+    // epilogue operands: with the burst where registers allow; else (JACOBI's
+    // three, or 8-step batches) each slice's right after its batch is summed
+    constexpr bool epi_late = MODE == SPMV_JACOBI || (NB > 7 && MODE != SPMV_SET);
+    XsEpi E[XS_NS];
+    if constexpr (!epi_late) {
+#pragma unroll
+        for (int j = 0; j < XS_NS; j++) E[j] = xs_epi_load<MODE>(a, min(s0 + 16 * j, s_last) * 64 + lane);
+    }
+    __syncthreads();
+    double acc[XS_NS];
+#pragma unroll
+    for (int j = 0; j < XS_NS; j++) {
+        const int s = min(s0 + 16 * j, s_last);
+        const uint32_t dsc = a.desc[s];
+        const char *blk = a.data + (int64_t)(dsc & 0x3fffffffu) * 128;
+        acc[j] = xs_consume(B[j], min(NB, W[j]), sx, 0.0);
+        if constexpr (epi_late) E[j] = xs_epi_load<MODE>(a, s * 64 + lane);
+        for (int t0 = NB; t0 < W[j]; t0 += NB) {
+            XsBatch<NB> X;
+            xs_issue(X, blk, W[j], t0, lane);
+            acc[j] = xs_consume(X, min(NB, W[j] - t0), sx, acc[j]);
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < XS_NS; j++) {
+        const int s = s0 + 16 * j;
+        if (s >= s_end) break;
+        if ((a.desc[s] >> 30) != 1) continue;  // escape slice: below
+        const int row = s * 64 + lane;
+        if (row < a.nrows) {
+            if constexpr (MODE == SPMV_SET) a.y[row] = acc[j];
+            else if constexpr (MODE == SPMV_ADD || MODE == SPMV_ADD0) a.y[row] = E[j].y + acc[j];
+            else if constexpr (MODE == SPMV_RESID || MODE == SPMV_RESID0) a.y[row] = E[j].b - acc[j];
+            else a.y[row] = E[j].x + E[j].d * (E[j].b - acc[j]);  // JACOBI
+        }
+    }
+    for (int e = s0; e < s_end; e += XS_BS / 64) {
         const uint32_t d = a.desc[e];
         if ((d >> 30) == 1) continue;
         const int row = e * 64 + lane;
@@ -382,7 +505,7 @@ void xs_release(GpuCsr &m) {
     m.xs_soff.release();
     m.xs_coff.release();
     m.xs_chunks.release();
-    m.xs_groups = m.xs_bytes = m.xs_steps = m.xs_chunk_total = m.xs_escape_slices = 0;
+    m.xs_groups = m.xs_bytes = m.xs_steps = m.xs_chunk_total = m.xs_escape_slices = m.xs_maxw = 0;
 }
 
 // Built for a single-segment matrix of >= XS_MIN_GROUPS groups (one workgroup
@@ -479,28 +602,35 @@ bool build_xs(GpuCsr &m, const std::vector<int64_t> &rp) {
     m.xs_steps = soff[ns];
     m.xs_chunk_total = (int64_t)chunks.size();
     m.xs_escape_slices = esc;
+    m.xs_maxw = *std::max_element(w.begin(), w.end());
     return true;
 }
 
 bool xs_supports(SpmvMode mode) { return mode != SPMV_SGS; }
 
+#define FAMG_COMMA ,
 void spmv_xs(const GpuCsr &m, const double *x, double *y, SpmvMode mode, const SpmvEpi &epi, hipStream_t s) {
     XsArgs a{m.xs_data.get(), m.xs_desc.get(), m.xs_soff.get(), m.xs_coff.get(), m.xs_chunks.get(),
              (int32_t)m.nrows, (int32_t)m.ncols, (int32_t)m.xs_groups, x, y, epi.b, epi.d, epi.dc, epi.dt};
     const dim3 grid((unsigned)m.xs_groups), block(XS_BS);
-#define FAMG_XS_LAUNCH(K)                                                             \
+// T: the template arguments after the mode (empty, or ", NB")
+#define FAMG_XS_LAUNCH(K, T)                                                          \
     switch (mode) {                                                                   \
-    case SPMV_SET: K<SPMV_SET><<<grid, block, 0, s>>>(a); break;                      \
-    case SPMV_ADD: K<SPMV_ADD><<<grid, block, 0, s>>>(a); break;                      \
-    case SPMV_RESID: K<SPMV_RESID><<<grid, block, 0, s>>>(a); break;                  \
-    case SPMV_JACOBI: K<SPMV_JACOBI><<<grid, block, 0, s>>>(a); break;                \
-    case SPMV_RESID0: K<SPMV_RESID0><<<grid, block, 0, s>>>(a); break;                \
-    case SPMV_ADD0: K<SPMV_ADD0><<<grid, block, 0, s>>>(a); break;                    \
+    case SPMV_SET: K<SPMV_SET T><<<grid, block, 0, s>>>(a); break;                    \
+    case SPMV_ADD: K<SPMV_ADD T><<<grid, block, 0, s>>>(a); break;                    \
+    case SPMV_RESID: K<SPMV_RESID T><<<grid, block, 0, s>>>(a); break;                \
+    case SPMV_JACOBI: K<SPMV_JACOBI T><<<grid, block, 0, s>>>(a); break;              \
+    case SPMV_RESID0: K<SPMV_RESID0 T><<<grid, block, 0, s>>>(a); break;              \
+    case SPMV_ADD0: K<SPMV_ADD0 T><<<grid, block, 0, s>>>(a); break;                  \
     default: fail(AMG_ERR_UNSUPPORTED, "x-staged SELL: unsupported SpMV epilogue"); \
     }
-    if (flag(FLAG_XS_PIPE) != 0) FAMG_XS_LAUNCH(spmv_xs_pipe_kernel)
-    else FAMG_XS_LAUNCH(spmv_xs_kernel)
+    const int64_t how = flag(FLAG_XS_PIPE);
+    if (how >= 2 && m.xs_maxw <= 7) FAMG_XS_LAUNCH(spmv_xs_burst_kernel, FAMG_COMMA 7)
+    else if (how >= 2) FAMG_XS_LAUNCH(spmv_xs_burst_kernel, FAMG_COMMA 8)
+    else if (how == 1) FAMG_XS_LAUNCH(spmv_xs_pipe_kernel, )
+    else FAMG_XS_LAUNCH(spmv_xs_kernel, )
 #undef FAMG_XS_LAUNCH
+#undef FAMG_COMMA
     FAMG_CHECK_HIP(hipGetLastError());
 }
 

@@ -122,8 +122,9 @@ amg_status amg_set_alloc_policy(int32_t policy);
  * FAMG_GTX_TIME), 4 = marching
  * 27-point SGS phases (sgs27.hip): 0 = one workgroup per tile and plane, 1 = auto
  * (about one workgroup per CU), n >= 2 = n planes per workgroup (default 1, env
- * FAMG_SGS27_MARCH), 5 = x-staged SELL (xsell.hip): 1 = the pipelined kernel
- * (default), 0 = the round-4 kernel (env FAMG_XS_PIPE).  Setting one
+ * FAMG_SGS27_MARCH), 5 = x-staged SELL kernel (xsell.hip): 2 = one burst of
+ * loads per row group with LDS-DMA staging (default), 1 = software-pipelined
+ * batches, 0 = the round-4 kernel (env FAMG_XS_PIPE).  Setting one
  * makes every multigrid re-capture its hipGraph at its next apply.  amg_get_flag
  * reads the current value. */
 amg_status amg_set_flag(int32_t which, int64_t value);

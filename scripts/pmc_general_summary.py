@@ -27,7 +27,7 @@ def values(path, counter, kernel):
 def main(fetch_csv, write_csv, known_json, out_json):
     known = json.load(open(known_json))
     n, nnz = known["n"], known["nnz"]
-    kern = {"xsell": "spmv_xs_kernel", "sell": "spmv_sell_kernel"}[known["gen"]["kernel"]]
+    kern = {"xsell": known.get("xs_kernel", "spmv_xs_burst_kernel"), "sell": "spmv_sell_kernel"}[known["gen"]["kernel"]]
     cal_f, gen_f = values(fetch_csv, "FETCH_SIZE", kern)
     cal_w, gen_w = values(write_csv, "WRITE_SIZE", kern)
     cal_read = known["cal"]["stream_bytes"] + 8 * n

@@ -1025,8 +1025,9 @@ def test_xsell_general_operator(ctx):
 
 
 def test_xsell_pipelined_kernel_bitwise(ctx):
-    """The pipelined x-staged SELL kernel (flag xs_pipe = 1, the default) against
-    the round-4 kernel (xs_pipe = 0) and the oracle: every epilogue bitwise, on
+    """The burst x-staged SELL kernel (flag xs_pipe = 2, the default: LDS-DMA
+    staging) and the pipelined one (1) against the round-4 kernel (0) and the
+    oracle: every epilogue bitwise, on
     an operator with escape slices (a few rows given one far column each: their
     slices keep 32-bit global columns) and an all-empty slice (64 empty rows:
     one padding step)."""
@@ -1061,7 +1062,7 @@ def test_xsell_pipelined_kernel_bitwise(ctx):
     xd, bd, dd = T(x), T(b), T(d)
     outs = {}
     try:
-        for pipe in (0, 1):
+        for pipe in (0, 1, 2):
             fa().set_flag("xs_pipe", pipe)
             for mode in ("set", "add", "resid", "jacobi"):
                 y = T(np.linspace(-1, 1, n))
@@ -1069,15 +1070,16 @@ def test_xsell_pipelined_kernel_bitwise(ctx):
                 ctx.synchronize()
                 outs[(pipe, mode)] = H(y)
     finally:
-        fa().set_flag("xs_pipe", 1)
+        fa().set_flag("xs_pipe", 2)
     for mode in ("set", "add", "resid", "jacobi"):
-        assert np.array_equal(outs[(0, mode)].view(np.int64), outs[(1, mode)].view(np.int64)), mode
+        for pipe in (1, 2):
+            assert np.array_equal(outs[(0, mode)].view(np.int64), outs[(pipe, mode)].view(np.int64)), (mode, pipe)
     ax = OA.spmv(x)
-    assert np.array_equal(outs[(1, "set")].view(np.int64), ax.view(np.int64))
-    assert np.all(outs[(1, "set")][e0:e0 + 64] == 0.0)
-    assert np.array_equal(outs[(1, "resid")], b - ax)
-    assert np.array_equal(outs[(1, "add")], np.linspace(-1, 1, n) + ax)
-    assert np.array_equal(outs[(1, "jacobi")], x + d * (b - ax))
+    assert np.array_equal(outs[(2, "set")].view(np.int64), ax.view(np.int64))
+    assert np.all(outs[(2, "set")][e0:e0 + 64] == 0.0)
+    assert np.array_equal(outs[(2, "resid")], b - ax)
+    assert np.array_equal(outs[(2, "add")], np.linspace(-1, 1, n) + ax)
+    assert np.array_equal(outs[(2, "jacobi")], x + d * (b - ax))
 
 
 def test_sgs_dia_sweeps(ctx):
