@@ -137,6 +137,112 @@ __global__ __launch_bounds__(256) void spmv_bsr3_kernel(BsrArgs a) {
     }
 }
 
+// ------------------------------------------------------------ columns-first form
+// The kernel above waits two dependent round trips per group of block steps (the
+// node columns, then the x operands they address).  Here (FLAG_BSR_KERNEL >= 1,
+// slices of <= BSR_PCOL steps) a wave first loads the node columns of all its
+// slice's steps (one round trip; a step past the slice's width reloads the last
+// one), then walks U-step batches whose value and x loads are independent of
+// each other -- one round trip per batch -- and with PIPE issues batch b + 1
+// before summing batch b.  Same fma order per dof row: bitwise the kernel above.
+constexpr int BSR_PCOL = 32;
+
+template <int U>
+__device__ __forceinline__ void bsr_issue(const char *__restrict__ st, int lane, const double *__restrict__ x,
+                                          const int32_t *J, int b, int tl, double (&v)[U][9], double (&xx)[U][3]) {
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+        const char *p = st + (int64_t)min(b * U + u, tl) * BSR_STEP;
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            const bsr_dbl2_t w = __builtin_nontemporal_load(reinterpret_cast<const bsr_dbl2_t *>(p + q * 1024) + lane);
+            v[u][2 * q] = w.x;
+            v[u][2 * q + 1] = w.y;
+        }
+        v[u][8] = __builtin_nontemporal_load(reinterpret_cast<const double *>(p + BSR_K8) + lane);
+        const double *xp = x + 3 * (int64_t)J[b * U + u];
+        xx[u][0] = xp[0];
+        xx[u][1] = xp[1];
+        xx[u][2] = xp[2];
+    }
+}
+
+template <int U>
+__device__ __forceinline__ void bsr_sum(const double (&v)[U][9], const double (&xx)[U][3], int b, int w, double &a0,
+                                        double &a1, double &a2) {
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+        if (b * U + u >= w) break;  // clamped steps past the slice's width: loaded, never summed
+        a0 = fma(v[u][0], xx[u][0], a0);
+        a0 = fma(v[u][1], xx[u][1], a0);
+        a0 = fma(v[u][2], xx[u][2], a0);
+        a1 = fma(v[u][3], xx[u][0], a1);
+        a1 = fma(v[u][4], xx[u][1], a1);
+        a1 = fma(v[u][5], xx[u][2], a1);
+        a2 = fma(v[u][6], xx[u][0], a2);
+        a2 = fma(v[u][7], xx[u][1], a2);
+        a2 = fma(v[u][8], xx[u][2], a2);
+    }
+}
+
+template <int MODE, int U, bool PIPE>
+__global__ __launch_bounds__(256) void spmv_bsr3p_kernel(BsrArgs a) {
+    const int blk = xcd_remap(blockIdx.x, gridDim.x);
+    const int sl = __builtin_amdgcn_readfirstlane(blk * 4 + (int)(threadIdx.x >> 6));
+    if (sl >= a.nslices) return;
+    const int s = a.slice0 + sl;
+    const int lane = threadIdx.x & 63;
+    const int I = a.row0[s] + lane;
+    const bool live = I < a.row0[s + 1];
+    const int t0 = a.soff[s], w = a.soff[s + 1] - t0;
+    const char *st = a.data + (int64_t)t0 * BSR_STEP;
+    double a0 = 0.0, a1 = 0.0, a2 = 0.0;
+    BsrRow<MODE> r0, r1, r2;
+    if (w > 0) {
+        const int tl = w - 1;
+        int32_t J[BSR_PCOL];
+#pragma unroll
+        for (int t = 0; t < BSR_PCOL; t++)
+            J[t] = __builtin_nontemporal_load(reinterpret_cast<const int32_t *>(st + (int64_t)min(t, tl) * BSR_STEP + BSR_COL) + lane);
+        if (live) {
+            r0.load(a.e, 3 * I);
+            r1.load(a.e, 3 * I + 1);
+            r2.load(a.e, 3 * I + 2);
+        }
+        constexpr int NB = BSR_PCOL / U;
+        if constexpr (PIPE) {
+            double v0[U][9], x0[U][3], v1[U][9], x1[U][3];
+            bsr_issue<U>(st, lane, a.e.x, J, 0, tl, v0, x0);
+#pragma unroll
+            for (int b = 0; b < NB; b += 2) {
+                if (b * U >= w) break;
+                if ((b + 1) * U < w) bsr_issue<U>(st, lane, a.e.x, J, b + 1, tl, v1, x1);
+                bsr_sum<U>(v0, x0, b, w, a0, a1, a2);
+                if ((b + 1) * U >= w) break;
+                if ((b + 2) * U < w && b + 2 < NB) bsr_issue<U>(st, lane, a.e.x, J, b + 2, tl, v0, x0);
+                bsr_sum<U>(v1, x1, b + 1, w, a0, a1, a2);
+            }
+        } else {
+#pragma unroll
+            for (int b = 0; b < NB; b++) {
+                if (b * U >= w) break;
+                double v[U][9], xx[U][3];
+                bsr_issue<U>(st, lane, a.e.x, J, b, tl, v, xx);
+                bsr_sum<U>(v, xx, b, w, a0, a1, a2);
+            }
+        }
+    } else if (live) {
+        r0.load(a.e, 3 * I);
+        r1.load(a.e, 3 * I + 1);
+        r2.load(a.e, 3 * I + 2);
+    }
+    if (live) {
+        r0.store(a.e, 3 * I, a0);
+        r1.store(a.e, 3 * I + 1, a1);
+        r2.store(a.e, 3 * I + 2, a2);
+    }
+}
+
 static bool bsr_disabled() {
     static const bool off = [] {
         const char *e = getenv("FAMG_NO_BSR");
@@ -266,6 +372,8 @@ bool build_bsr(GpuCsr &m, const std::vector<int64_t> &rp, int64_t other_bytes) {
     FAMG_CHECK_HIP(hipStreamSynchronize(s));
     m.bsr_slices = ns;
     m.bsr_steps = steps;
+    m.bsr_maxw = 0;
+    for (int64_t k = 0; k < ns; k++) m.bsr_maxw = std::max<int64_t>(m.bsr_maxw, soff[k + 1] - soff[k]);
     m.bsr_seg_slc = seg_slc;
     return true;
 }
@@ -278,13 +386,23 @@ void spmv_bsr(const GpuCsr &m, const double *x, double *y, SpmvMode mode, const 
     BsrArgs a{m.bsr_data.get(), m.bsr_row0.get(), m.bsr_soff.get(), (int32_t)s0, (int32_t)(s1 - s0),
               BsrEpi{x, y, epi.b, epi.d, epi.dc, epi.dt}};
     const dim3 grid((unsigned)ceil_div(s1 - s0, 4)), block(256);
-    switch (mode) {
-    case SPMV_SET: spmv_bsr3_kernel<SPMV_SET><<<grid, block, 0, s>>>(a); break;
-    case SPMV_ADD: spmv_bsr3_kernel<SPMV_ADD><<<grid, block, 0, s>>>(a); break;
-    case SPMV_RESID: spmv_bsr3_kernel<SPMV_RESID><<<grid, block, 0, s>>>(a); break;
-    case SPMV_JACOBI: spmv_bsr3_kernel<SPMV_JACOBI><<<grid, block, 0, s>>>(a); break;
-    default: fail(AMG_ERR_UNSUPPORTED, "block storage: unsupported SpMV epilogue");
+    // T: the template arguments after the mode
+#define FAMG_BSR_LAUNCH(K, T)                                                      \
+    switch (mode) {                                                                \
+    case SPMV_SET: K<SPMV_SET T><<<grid, block, 0, s>>>(a); break;                 \
+    case SPMV_ADD: K<SPMV_ADD T><<<grid, block, 0, s>>>(a); break;                 \
+    case SPMV_RESID: K<SPMV_RESID T><<<grid, block, 0, s>>>(a); break;             \
+    case SPMV_JACOBI: K<SPMV_JACOBI T><<<grid, block, 0, s>>>(a); break;           \
+    default: fail(AMG_ERR_UNSUPPORTED, "block storage: unsupported SpMV epilogue"); \
     }
+#define FAMG_C ,
+    const int64_t how = m.bsr_maxw <= BSR_PCOL ? flag(FLAG_BSR_KERNEL) : 0;
+    if (how == 1) FAMG_BSR_LAUNCH(spmv_bsr3p_kernel, FAMG_C 4 FAMG_C false)
+    else if (how == 2) FAMG_BSR_LAUNCH(spmv_bsr3p_kernel, FAMG_C 2 FAMG_C true)
+    else if (how == 3) FAMG_BSR_LAUNCH(spmv_bsr3p_kernel, FAMG_C 4 FAMG_C true)
+    else FAMG_BSR_LAUNCH(spmv_bsr3_kernel, )
+#undef FAMG_BSR_LAUNCH
+#undef FAMG_C
     FAMG_CHECK_HIP(hipGetLastError());
 }
 

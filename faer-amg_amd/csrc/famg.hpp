@@ -140,7 +140,7 @@ struct GpuCsr {
     // 3x3 block storage (bsr.hip): node-row slices, one 4864-B unit per block step
     DevBuf<char> bsr_data;
     DevBuf<int32_t> bsr_row0, bsr_soff;
-    int64_t bsr_slices = 0, bsr_steps = 0;
+    int64_t bsr_slices = 0, bsr_steps = 0, bsr_maxw = 0;
     std::vector<int64_t> bsr_seg_slc;
     bool no_bsr = false;  // e.g. a color-permuted SGS copy
     // pattern SELL with L lanes per row (sellp.hip): values / codes only, columns

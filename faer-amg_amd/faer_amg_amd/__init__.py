@@ -481,7 +481,7 @@ class SparseMatOp(LinOp):
         return sp.csr_matrix((va, ci, rp), shape=self.dims())
 
 
-FLAGS = {"fold_xscs": 0, "dia_dk": 1, "vec_wpr": 2, "gtx_time": 3, "sgs27_march": 4, "xs_pipe": 5}
+FLAGS = {"fold_xscs": 0, "dia_dk": 1, "vec_wpr": 2, "gtx_time": 3, "sgs27_march": 4, "xs_pipe": 5, "bsr_kernel": 6}
 
 
 def set_flag(name, value):

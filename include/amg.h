@@ -124,7 +124,10 @@ amg_status amg_set_alloc_policy(int32_t policy);
  * (about one workgroup per CU), n >= 2 = n planes per workgroup (default 1, env
  * FAMG_SGS27_MARCH), 5 = x-staged SELL kernel (xsell.hip): 2 = one burst of
  * loads per row group with LDS-DMA staging (default), 1 = software-pipelined
- * batches, 0 = the round-4 kernel (env FAMG_XS_PIPE).  Setting one
+ * batches, 0 = the round-4 kernel (env FAMG_XS_PIPE), 6 = 3x3-block SpMV kernel
+ * (bsr.hip): 0 = the round-2 kernel (default), 1 = node columns first, 4-step
+ * batches, 2 = columns first, 2-step batches pipelined, 3 = 4-step pipelined
+ * (env FAMG_BSR_KERNEL).  Setting one
  * makes every multigrid re-capture its hipGraph at its next apply.  amg_get_flag
  * reads the current value. */
 amg_status amg_set_flag(int32_t which, int64_t value);

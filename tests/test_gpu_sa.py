@@ -239,6 +239,22 @@ def test_bsr_storage_bitwise(ctx, gap):
     A.apply(yd, xd)
     ctx.synchronize()
     assert np.array_equal(yd.cpu().numpy(), OA.spmv(x))
+    # every 3x3-block kernel (flag bsr_kernel: round-2 kernel, columns first
+    # with 4-step batches, 2- / 4-step pipelined) and epilogue: bitwise
+    ax = OA.spmv(x)
+    b0 = np.random.default_rng(8).standard_normal(S.shape[0])
+    d0 = np.random.default_rng(9).uniform(0.1, 0.2, S.shape[0])
+    bd, dd = torch.as_tensor(b0, device="cuda:0"), torch.as_tensor(d0, device="cuda:0")
+    try:
+        for k in (0, 1, 2, 3):
+            fa().set_flag("bsr_kernel", k)
+            for mode, ref in (("set", ax), ("add", 0.5 + ax), ("resid", b0 - ax), ("jacobi", x + d0 * (b0 - ax))):
+                yk = torch.full_like(xd, 0.5)
+                A.spmv_epilogue(mode, xd, yk, bd, dd)
+                ctx.synchronize()
+                assert np.array_equal(yk.cpu().numpy().view(np.int64), ref.view(np.int64)), (k, mode)
+    finally:
+        fa().set_flag("bsr_kernel", 0)
     nn = fa().constant_candidates(S.shape[0], 3)
     w = weights(S, nn)
     mg = fa().smoothed_aggregation(A, nn, weights=w, block_size=3, candidate_dimension=3, coarsest_dim=150,
