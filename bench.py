@@ -319,6 +319,26 @@ def plan_summary(plan):
             "per_level": [dict(level=l, **lv[l]) for l in sorted(lv)]}
 
 
+def level_storages(mg):
+    """Per level the storage of A_l, R_l, P_l (kernel, x-staged tile and how it
+    was chosen: the frozen per-shape table of tuning.cpp or a setup-time timing),
+    so two runs of one configuration can be compared decision by decision."""
+    out = []
+    for l in range(mg.levels()):
+        Al, _, Rl, Pl = mg.level(l)
+        d = {}
+        for name, M in (("A", Al), ("R", Rl), ("P", Pl)):
+            if M is None:
+                continue
+            i = M.spmv_info()
+            e = {"kernel": i["kernel"], "gtc": i["gtc_kind"]}
+            if i.get("xstaged"):
+                e["tile"], e["tile_source"] = list(i["tile"]), i["tile_source"]
+            d[name] = e
+        out.append(d)
+    return out
+
+
 def abi_ingest(fa, ctx, mg, b, z_ref, stream, args):
     """The drop-in path's rate (what a Rust caller of INTEGRATION.md does): the
     hierarchy's arrays downloaded to the host and handed back level by level
@@ -489,6 +509,7 @@ def run_single(args):
     rho1 = float(torch.linalg.norm(b - r) / torch.linalg.norm(b))
     plan = mg.cycle_plan()
     psum = plan_summary(plan)
+    storage_plan = level_storages(mg)
     vbytes, vbytes_csr = psum["bytes"], psum["csr_bytes"]
     if args.plan_out:
         with open(args.plan_out, "w") as fh:
@@ -531,7 +552,8 @@ def run_single(args):
                                    "source": "amg_multigrid_cycle_plan (the launches the library makes)",
                                    "per_level_GB": [round(d["bytes"] / 1e9, 4) for d in psum["per_level"]],
                                    "per_level_launches": [d["launches"] for d in psum["per_level"]],
-                                   "per_level_kernels": [d["kernels"] for d in psum["per_level"]]},
+                                   "per_level_kernels": [d["kernels"] for d in psum["per_level"]],
+                                   "per_level_storage": storage_plan},
                    "rel_residual_after_1_cycle": rho1,
                    "abi_ingest": abi,
                    "parallelism": "single GPU"},

@@ -387,9 +387,10 @@ amg_status amg_csr_grid_info(const amg_linop *op, int64_t *info12) {
     return guard([&] {
         FAMG_REQUIRE(info12, AMG_ERR_INVALID, "null argument");
         const GpuCsr &m = need_csr(op)->m;
-        for (int q = 0; q < 12; q++) info12[q] = 0;
+        for (int q = 0; q < 13; q++) info12[q] = 0;
         for (int q = 0; q < 3; q++) info12[q] = m.grid[q];
         info12[10] = m.grid_src;
+        info12[12] = m.xscs ? m.xscs_tile_src : 0;
         info12[11] = m.gtx_on ? (m.gtx_r ? 4 : 3) : m.gtc_on ? (m.gtc_r ? 2 : 1) : 0;
         const bool on = m.has_scs() && m.xscs;
         info12[3] = on ? 1 : 0;

@@ -91,11 +91,18 @@ static void storage_check(GpuCsr &m) {
             (long)m.ncols, (long)m.nnz, (int)k, (long)bad, (long)first);
 }
 
-// Time y = A x (SET) on scratch vectors with m's DIA codes and with its x-staged
-// stencil classes (3 launches each after one warm-up); true if the classes win.
-// Both sum every row in the same order: the choice changes no result.
+// DIA run pattern or x-staged stencil classes for a long-stencil grid operator
+// (A_1 of the 7-point box hierarchy): the classes, by rule -- they won the
+// setup-time timing in every round-4 bench run (29.6 / 34.1 against 34.6 / 35.5
+// us on C2's A_1), but the timing flipped to DIA under counter collection, so
+// the plan depended on the run (verdict r04 item 6).  FAMG_XSCS_VS_DIA = 0 / 1
+// forces DIA / the classes, = t times them as round 4 did (3 launches each after
+// one warm-up; true if the classes win).  Both sum every row in the same order:
+// the choice changes no result.
 static bool xscs_beats_dia(GpuCsr &m) {
-    if (const char *e = getenv("FAMG_XSCS_VS_DIA")) return e[0] == '1';
+    const char *e = getenv("FAMG_XSCS_VS_DIA");
+    if (!e || !e[0]) return true;
+    if (e[0] != 't') return e[0] == '1';
     hipStream_t s = m.ctx->stream;
     DevBuf<double> x(m.ncols), y(m.nrows);
     FAMG_CHECK_HIP(hipMemsetAsync(x.get(), 0, m.ncols * sizeof(double), s));

@@ -170,6 +170,7 @@ struct GpuCsr {
     bool xscs = false;
     int xscs_t[3] = {0, 0, 0}, xscs_r[3] = {0, 0, 0};
     int xscs_ws = 0;  // LDS row stride of the window (>= wx; padded against bank conflicts)
+    int xscs_tile_src = 0;  // how the tile was chosen: TuneSource (tuning.hpp)
     DevBuf<int32_t> xscs_lo;
     std::vector<int> xscs_steps;  // (dx, dy, dz) of each of the scs_k offsets
     // grid-transfer classes (gtc.hip) for R/P of a 2x2x2-box hierarchy: an overlay

@@ -29,6 +29,7 @@
 #include <unordered_map>
 
 #include "famg.hpp"
+#include "tuning.hpp"
 
 namespace famg {
 
@@ -391,6 +392,7 @@ void scs_release(GpuCsr &m) {
     m.scs_seg = -1;
     m.scs_lanes = false;
     m.xscs = false;
+    m.xscs_tile_src = 0;
     m.xscs_lo.release();
 }
 
@@ -606,9 +608,23 @@ static void spmv_xscs(const GpuCsr &m, const double *x, double *y, SpmvMode mode
 // classes reads the dictionary per lane (profiles/r03/ab_xscs_*.log).  The
 // tile changes no result (same sums in the same order).
 static void xscs_autotune(GpuCsr &m) {
-    if (getenv("FAMG_XSCS_TILE")) return;
+    if (getenv("FAMG_XSCS_TILE")) {
+        m.xscs_tile_src = TUNE_ENV;
+        return;
+    }
     const int64_t nx = m.grid[0], ny = m.grid[1], nz = m.grid[2], n = m.nrows;
     const int rx = m.xscs_r[0], ry = m.xscs_r[1], rz = m.xscs_r[2];
+    // a shape of the frozen table (tuning.cpp) takes its tile without timing
+    const TileKey key{nx, ny, nz, rx, ry, rz, (int)m.scs_kr, m.scs_nclass, m.rframe.on()};
+    {
+        int t[3];
+        if (getenv("FAMG_TUNE_RETIME") == nullptr && tune_tile_lookup(key, t)) {
+            xscs_set_tile(m, t);
+            m.xscs_tile_src = TUNE_TABLE;
+            tune_tile_record(key, t, TUNE_TABLE);
+            return;
+        }
+    }
     std::vector<std::array<int, 3>> cands;
     for (int tx : {4, 8, 16, 32, 64})
         for (int ty : {1, 2, 4, 8, 16})
@@ -647,6 +663,8 @@ static void xscs_autotune(GpuCsr &m) {
     (void)hipEventDestroy(e0);
     (void)hipEventDestroy(e1);
     xscs_set_tile(m, best);
+    m.xscs_tile_src = TUNE_TIMED;
+    tune_tile_record(key, best, TUNE_TIMED);
 }
 
 bool build_scs(GpuCsr &m, const std::vector<int64_t> &rp, int64_t other_bytes) {

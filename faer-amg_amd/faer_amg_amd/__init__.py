@@ -443,7 +443,7 @@ class SparseMatOp(LinOp):
         ci = np.zeros(4, np.int64)
         _ck(_lib.amg_csr_class_info(self.h, ci.ctypes.data_as(vp)))
         d["classes"], d["class_offsets"], d["class_id_bits"] = int(ci[0]), int(ci[1]), int(ci[2])
-        g = np.zeros(12, np.int64)
+        g = np.zeros(13, np.int64)
         _ck(_lib.amg_csr_grid_info(self.h, g.ctypes.data_as(vp)))
         d["grid"] = tuple(int(v) for v in g[:3])
         d["grid_source"] = ("none", "given", "inferred")[int(g[10])]
@@ -452,6 +452,7 @@ class SparseMatOp(LinOp):
         d["xstaged"] = bool(g[3])
         if d["xstaged"]:
             d["tile"], d["halo"] = tuple(int(v) for v in g[4:7]), tuple(int(v) for v in g[7:10])
+            d["tile_source"] = ("none", "table", "timed", "env", "rule")[int(g[12])]
         return d
 
     def spmv_epilogue(self, mode, x, y, b=None, d=None):

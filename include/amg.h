@@ -162,9 +162,11 @@ amg_status amg_grid_from_offsets(const int64_t *offs, int64_t k, int64_t n, int6
  * scaled inverse diagonal).  x != y. */
 amg_status amg_csr_spmv_epilogue(const amg_linop *op, int32_t mode, const double *x, double *y,
                                  const double *b, const double *d);
-/* info12 = {nx, ny, nz (0: no hint), x-staged (0/1), tile tx, ty, tz, halo
- * rx, ry, rz, hint source (0 none, 1 given, 2 inferred), grid-transfer classes
- * (0 none, 1 as P, 2 as R: 8-bit gtc.hip; 3 as P, 4 as R: 16-bit gtx.hip)}. */
+/* info12 (13 entries) = {nx, ny, nz (0: no hint), x-staged (0/1), tile tx, ty,
+ * tz, halo rx, ry, rz, hint source (0 none, 1 given, 2 inferred), grid-transfer
+ * classes (0 none, 1 as P, 2 as R: 8-bit gtc.hip; 3 as P, 4 as R: 16-bit
+ * gtx.hip), how the x-staged tile was chosen (1 the frozen per-shape table of
+ * tuning.cpp, 2 timed at setup, 3 FAMG_XSCS_TILE)}. */
 amg_status amg_csr_grid_info(const amg_linop *op, int64_t *info12);
 
 /* Copy a host CSR with usize-compatible (int64) row pointers and column indices
