@@ -306,16 +306,25 @@ def workload_name(args, dims):
 def plan_summary(plan):
     """Per-level and whole-cycle algorithmic bytes from the library's own launch
     plan of one V-cycle (amg_multigrid_cycle_plan: every launch the cycle makes,
-    with the bytes its storage streams and the vectors it moves)."""
+    with the bytes its storage streams and the vectors it moves).  Halo
+    exchange records of a distributed plan (kernel -2) are summed apart
+    (halo_bytes: what this rank sends + receives)."""
     lv = {}
+    kern = [r for r in plan if r["kernel"] != -2]
     for r in plan:
-        d = lv.setdefault(r["level"], {"launches": 0, "bytes": 0, "csr_bytes": 0, "kernels": []})
+        d = lv.setdefault(r["level"], {"launches": 0, "bytes": 0, "csr_bytes": 0, "halo_bytes": 0,
+                                       "exchanges": 0, "kernels": []})
+        if r["kernel"] == -2:
+            d["halo_bytes"] += r["bytes"]
+            d["exchanges"] += 1
+            continue
         d["launches"] += 1
         d["bytes"] += r["bytes"]
         d["csr_bytes"] += r["csr_bytes"]
         d["kernels"].append(f"{r['role']}:{r['name']}:{r['mode']}")
-    return {"launches": len(plan), "bytes": sum(r["bytes"] for r in plan),
-            "csr_bytes": sum(r["csr_bytes"] for r in plan),
+    return {"launches": len(kern), "bytes": sum(r["bytes"] for r in kern),
+            "csr_bytes": sum(r["csr_bytes"] for r in kern),
+            "halo_bytes": sum(r["bytes"] for r in plan if r["kernel"] == -2),
             "per_level": [dict(level=l, **lv[l]) for l in sorted(lv)]}
 
 
@@ -736,6 +745,9 @@ def run_dist(args, world, rank, local_rank):
                            "local_storages_rank0": storages,
                            "vcycle_plan_rank0": {"launches": plan["launches"],
                                                  "source": "amg_dist_cycle_plan (the launches this rank makes)",
+                                                 "halo_bytes": plan["halo_bytes"],
+                                                 "per_level_halo_bytes": [d["halo_bytes"] for d in plan["per_level"]],
+                                                 "per_level_exchanges": [d["exchanges"] for d in plan["per_level"]],
                                                  "per_level_GB": [round(d["bytes"] / 1e9, 4)
                                                                   for d in plan["per_level"]],
                                                  "per_level_kernels": [d["kernels"] for d in plan["per_level"]]},

@@ -345,7 +345,27 @@ struct Space {
     DevBuf<double> sendbuf;
     std::vector<Peer> peers;              // rebuilt per vector (rbuf differs)
     int64_t nsend = 0;
+    // Sweep-position halo lists of a level smoothed by multicolor SGS (sgs_sweep;
+    // ADVICE r03 / verdict r04 item 7).  An SGS step sweeps the colours in the
+    // order seq = 0, 1, ..., C-1, C-2, ..., 0 (positions 0 .. 2C-2); the exchange
+    // before position p >= 1 carries the ghost entries of colour seq[p-1] -- just
+    // updated -- that a row of the reading rank reads at a later position before
+    // that colour is updated again, and the exchange before position 0 (x not
+    // zero: after an interpolation) the entries read before their first update.
+    // Which rows read an entry is known on both sides (the reader's colours per
+    // ghost entry, sent to the owner once at setup), so sender and receiver build
+    // the same lists.  Slots ordered (position, peer, global id).
+    int64_t ncol = 0;
+    std::vector<int64_t> cs_off, cr_off;  // [p * npeer + k] .. +1: slot ranges, ((2C-1) * npeer + 1) entries
+    DevBuf<int32_t> cs_idx, cr_idx;       // owned local index to send / ghost local index to fill
+    DevBuf<double> cs_buf, cr_buf;
 };
+
+// x[idx[k]] = in[k]: a colour's received ghost entries into their slots
+__global__ void k_scatter_idx(double *x, const int32_t *idx, int64_t n, const double *in) {
+    const int64_t k = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (k < n) x[idx[k]] = in[k];
+}
 
 // Local copy of rows [r0, r1) of M with global column ids.
 static void extract_rows(const GpuCsr &M, int64_t r0, int64_t r1, GpuCsr &out, Ctx *ctx) {
@@ -523,11 +543,118 @@ static void halo_exchange(Space &sp, double *x, Transport &tr, hipStream_t s) {
     tr.exchange(sp.peers, s);
 }
 
+// the plan record of a halo exchange (kernel -2: bytes this rank sends + receives)
+static void log_halo(const char *name, int64_t entries_sent, int64_t entries_recv) {
+    log_launch(name, -2, -1, entries_recv, 8 * (entries_sent + entries_recv));
+}
+
 // refresh the ghost region of x (x has n_own + n_ghost entries)
 static void halo(Space &sp, double *x, Transport &tr, hipStream_t s) {
     if (sp.redundant || sp.nbr.empty()) return;
     halo_pack(sp, x, s);
     halo_exchange(sp, x, tr, s);
+    log_halo("halo", sp.nsend, sp.n_ghost);
+}
+
+// the exchange before sweep position p of an SGS level (its position lists)
+static void halo_position(Space &sp, double *x, int64_t p, Transport &tr, hipStream_t s) {
+    if (sp.redundant || sp.nbr.empty()) return;
+    const int64_t np = (int64_t)sp.nbr.size();
+    const int64_t s0 = sp.cs_off[p * np], s1 = sp.cs_off[(p + 1) * np];
+    const int64_t q0 = sp.cr_off[p * np], q1 = sp.cr_off[(p + 1) * np];
+    if (s1 > s0)
+        hipLaunchKernelGGL(k_gather_idx, dim3(g1(s1 - s0)), dim3(256), 0, s, x, sp.cs_idx.get() + s0, s1 - s0,
+                           sp.cs_buf.get() + s0);
+    FAMG_CHECK_HIP(hipGetLastError());
+    sp.peers.clear();
+    for (int64_t k = 0; k < np; k++) {
+        const int64_t a = sp.cs_off[p * np + k], b = sp.cs_off[p * np + k + 1];
+        const int64_t ra = sp.cr_off[p * np + k], rb = sp.cr_off[p * np + k + 1];
+        if (b == a && rb == ra) continue;  // the peer's mirrored counts are zero too
+        sp.peers.push_back({sp.nbr[k], sp.cs_buf.get() + a, (b - a) * 8, sp.cr_buf.get() + ra, (rb - ra) * 8});
+    }
+    tr.exchange(sp.peers, s);
+    if (q1 > q0)
+        hipLaunchKernelGGL(k_scatter_idx, dim3(g1(q1 - q0)), dim3(256), 0, s, x, sp.cr_idx.get() + q0, q1 - q0,
+                           sp.cr_buf.get() + q0);
+    FAMG_CHECK_HIP(hipGetLastError());
+    log_halo("halo_sgs", s1 - s0, q1 - q0);
+}
+
+// Does the exchange before position p carry an entry of colour c whose reading
+// rows (on the receiving rank) have the colours in `readers`?  (Space comment)
+static bool sgs_needed(int64_t p, int64_t c, uint32_t readers, int64_t C) {
+    auto first = [&](int64_t col) { return col; };                            // forward position
+    auto second = [&](int64_t col) { return col <= C - 2 ? 2 * C - 2 - col : INT64_MAX; };  // backward
+    int64_t lo, hi;  // a reader at a position in [lo, hi) needs the value this exchange carries
+    if (p == 0) {
+        lo = 0;
+        hi = first(c);
+    } else {
+        const int64_t t = p - 1, ct = t < C ? t : 2 * C - 2 - t;  // colour swept at t
+        if (ct != c) return false;
+        lo = p;
+        hi = t == first(c) ? second(c) : INT64_MAX;
+    }
+    for (int64_t r = 0; r < C; r++) {
+        if (!((readers >> r) & 1u)) continue;
+        const int64_t q1 = first(r), q2 = second(r);
+        if ((q1 >= lo && q1 < hi) || (q2 != INT64_MAX && q2 >= lo && q2 < hi)) return true;
+    }
+    return false;
+}
+
+// Position lists of an SGS level from its plan, the local A (owned rows, columns
+// [owned | ghost]) and the global colouring (every rank holds it).  The reading
+// colours of every ghost entry go to its owner once (a reversed halo exchange).
+static void space_sgs_lists(Space &sp, const GpuCsr &A, const std::vector<int32_t> &colors, int64_t C, Transport &tr,
+                            Ctx *ctx) {
+    const int64_t np = (int64_t)sp.nbr.size(), P = 2 * C - 1;
+    sp.ncol = C;
+    sp.cs_off.assign(P * np + 1, 0);
+    sp.cr_off.assign(P * np + 1, 0);
+    if (sp.redundant || np == 0 || C > 32) return;
+    hipStream_t s = ctx->stream;
+    const HaloPlan &pl = sp.plan;
+    // the colours of my rows reading each ghost entry
+    std::vector<int64_t> rp(A.nrows + 1);
+    std::vector<int32_t> col(std::max<int64_t>(1, A.nnz));
+    FAMG_CHECK_HIP(hipMemcpyAsync(rp.data(), A.rp64.get(), (A.nrows + 1) * 8, hipMemcpyDeviceToHost, s));
+    if (A.nnz) FAMG_CHECK_HIP(hipMemcpyAsync(col.data(), A.col.get(), A.nnz * 4, hipMemcpyDeviceToHost, s));
+    FAMG_CHECK_HIP(hipStreamSynchronize(s));
+    std::vector<uint32_t> rmask(sp.n_ghost, 0);
+    for (int64_t i = 0; i < A.nrows; i++)
+        for (int64_t e = rp[i]; e < rp[i + 1]; e++)
+            if (col[e] >= sp.n_own) rmask[col[e] - sp.n_own] |= 1u << colors[sp.r0 + i];
+    // ... to the owners: my receive range of peer k -> its send range to me
+    DevBuf<uint32_t> dr(std::max<int64_t>(1, sp.n_ghost)), ds(std::max<int64_t>(1, sp.nsend));
+    if (sp.n_ghost) FAMG_CHECK_HIP(hipMemcpyAsync(dr.get(), rmask.data(), sp.n_ghost * 4, hipMemcpyHostToDevice, s));
+    std::vector<Peer> rev;
+    for (int64_t k = 0; k < np; k++)
+        rev.push_back({sp.nbr[k], dr.get() + sp.roff[k], sp.rcnt[k] * 4, ds.get() + sp.soff[k], sp.scnt[k] * 4});
+    tr.exchange(rev, s);
+    std::vector<uint32_t> smask(sp.nsend, 0);
+    if (sp.nsend) FAMG_CHECK_HIP(hipMemcpyAsync(smask.data(), ds.get(), sp.nsend * 4, hipMemcpyDeviceToHost, s));
+    FAMG_CHECK_HIP(hipStreamSynchronize(s));
+    std::vector<int32_t> si, ri;
+    for (int64_t p = 0; p < P; p++)
+        for (int64_t k = 0; k < np; k++) {
+            for (int64_t i = sp.soff[k]; i < sp.soff[k] + sp.scnt[k]; i++) {
+                const int32_t li = pl.send_idx[i];
+                if (sgs_needed(p, colors[sp.r0 + li], smask[i], C)) si.push_back(li);
+            }
+            for (int64_t j = sp.roff[k]; j < sp.roff[k] + sp.rcnt[k]; j++)
+                if (sgs_needed(p, colors[pl.ghost_ids[j]], rmask[j], C)) ri.push_back((int32_t)(sp.n_own + j));
+            sp.cs_off[p * np + k + 1] = (int64_t)si.size();
+            sp.cr_off[p * np + k + 1] = (int64_t)ri.size();
+        }
+    sp.cs_idx.resize(std::max<size_t>(1, si.size()));
+    sp.cr_idx.resize(std::max<size_t>(1, ri.size()));
+    sp.cs_buf.resize(std::max<size_t>(1, si.size()));
+    sp.cr_buf.resize(std::max<size_t>(1, ri.size()));
+    if (!si.empty()) FAMG_CHECK_HIP(hipMemcpyAsync(sp.cs_idx.get(), si.data(), si.size() * 4, hipMemcpyHostToDevice, s));
+    if (!ri.empty()) FAMG_CHECK_HIP(hipMemcpyAsync(sp.cr_idx.get(), ri.data(), ri.size() * 4, hipMemcpyHostToDevice, s));
+    FAMG_CHECK_HIP(hipStreamSynchronize(s));
 }
 
 // ---------------------------------------------------------- multigrid
@@ -554,6 +681,8 @@ struct DistMultigridOp : LinOp {
     // halo/interior overlap: the exchange runs on comm_stream while the
     // interior rows run on the context stream
     bool overlap = true;
+    // SGS levels exchange, before each colour, only what later colours read (option 2)
+    bool per_colour_halo = true;
     hipStream_t comm_stream = nullptr;
     hipEvent_t ev_pack = nullptr, ev_halo = nullptr;
     // hipGraph replay of the cycle (option 1, off by default): RCCL transport only
@@ -622,12 +751,18 @@ struct DistMultigridOp : LinOp {
             if (D.sp.n_own) G.first_color(x, b);
             c0 = 1;
         }
+        // ghosts before each colour: the position lists (only what a later colour
+        // reads; none before colour 0 from zero: the ghosts are zero), else the
+        // whole halo before every colour as in round 3
+        const bool pl = per_colour_halo && D.sp.ncol == C && C <= 32;
         for (int64_t c = c0; c < C; c++) {
-            halo(D.sp, x, *tr, s);
+            if (!pl) halo(D.sp, x, *tr, s);
+            else if (c > 0 || !zero) halo_position(D.sp, x, c, *tr, s);
             if (D.sp.n_own) spmv(G.Ap, x, x, SPMV_SGS, epi, s, c);
         }
         for (int64_t c = C - 2; c >= 0; c--) {
-            halo(D.sp, x, *tr, s);
+            if (pl) halo_position(D.sp, x, 2 * C - 2 - c, *tr, s);
+            else halo(D.sp, x, *tr, s);
             if (D.sp.n_own) spmv(G.Ap, x, x, SPMV_SGS, epi, s, c);
         }
     }
@@ -1092,6 +1227,7 @@ static std::shared_ptr<DistMultigridOp> build_dist(amg_comm *comm, const Multigr
         FAMG_REQUIRE((int64_t)G->host_colors.size() == D.sp.n_glob, AMG_ERR_INVALID, "sgs: coloring size");
         auto *Ag = dynamic_cast<CsrOp *>(g.levels[l].A.get());
         D.G = make_sgs_slice(D.A, G->host_colors.data() + D.sp.r0, G->ncolors, Ag->diagonal() + D.sp.r0);
+        space_sgs_lists(D.sp, D.A->m, G->host_colors, G->ncolors, *d->tr, ctx);
     }
     // the last distributed level's P references the replicated level La by global id
     if (d->La > 0) {
@@ -1379,6 +1515,7 @@ amg_status amg_dist_set_option(amg_linop *dist, int32_t option, int64_t value) {
         switch (option) {
         case 0: d->overlap = value != 0; d->drop_graphs(); break;
         case 1: d->use_graph = value != 0; d->drop_graphs(); break;
+        case 2: d->per_colour_halo = value != 0; d->drop_graphs(); break;
         default: fail(AMG_ERR_INVALID, "unknown distributed multigrid option");
         }
     });

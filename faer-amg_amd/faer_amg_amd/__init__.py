@@ -1025,6 +1025,11 @@ class DistMultigrid(LinOp):
         _ck(_lib.amg_dist_set_option(self.h, 1, 1 if on else 0))
         return self
 
+    def set_per_colour_halo(self, on=True):
+        """SGS levels: exchange only the colour swept last before each colour (default on)."""
+        _ck(_lib.amg_dist_set_option(self.h, 2, 1 if on else 0))
+        return self
+
     def pcg_solve(self, b, x, max_iter=1000, rel_tol=1e-8, abs_tol=0.0, precondition=True):
         """Distributed PCG (dots all-reduced), one distributed V-cycle per iteration."""
         hist = np.zeros(max(max_iter, 1))

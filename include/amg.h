@@ -532,7 +532,12 @@ amg_status amg_dist_level_matrix(const amg_linop *dist, int64_t level, int32_t w
 /* Options of a distributed multigrid: 0 = overlap each halo exchange with the
  * interior rows of the SpMV that consumes it (default 1; 0 exchanges first);
  * 1 = replay apply() as a captured hipGraph per (out, rhs) pair (default 0;
- * RCCL communicators only -- the loopback transport always runs eagerly). */
+ * RCCL communicators only -- the loopback transport always runs eagerly);
+ * 2 = multicolor SGS levels exchange, before each colour, only the ghost
+ * entries of the colour swept just before it (per-colour halo lists; default
+ * 1; 0 refreshes the whole halo before every colour).  The plans of
+ * amg_dist_cycle_plan carry the exchanges as records of kernel -2 (bytes this
+ * rank sends + receives). */
 amg_status amg_dist_set_option(amg_linop *dist, int32_t option, int64_t value);
 /* Distributed stationary solve (dots all-reduced over ranks): local vectors. */
 amg_status amg_dist_stationary_solve(amg_linop *dist_mg, const double *b, double *x,

@@ -64,7 +64,7 @@ def global_reference(dims, coarsest, b, problem="7pt", smoother="jacobi", steps=
 
 
 def dist_apply(nranks, dims, coarsest, b, agglo, split_kind="slab", problem="7pt", overlap=True, storage_level=0,
-               smoother="jacobi", steps=1, resid_form=False):
+               smoother="jacobi", steps=1, resid_form=False, per_colour=True, plan=False):
     import torch
     hub = fa().LoopbackHub(nranks)
 
@@ -85,18 +85,20 @@ def dist_apply(nranks, dims, coarsest, b, agglo, split_kind="slab", problem="7pt
                 splits.append([(p * n) // nranks for p in range(nranks + 1)])
         comm = fa().Comm(ctx, hub=hub, rank=r)
         dm = fa().DistMultigrid(comm, mg, splits, agglomerate_rows=agglo).set_overlap(overlap)
+        dm.set_per_colour_halo(per_colour)
         r0, r1 = dm.local_rows()
         bl = torch.as_tensor(np.ascontiguousarray(b[r0:r1]), device="cuda:0")
         zl = torch.empty_like(bl)
         dm.apply(zl, bl)
         ctx.synchronize()
         infos = [dm.level_info(l) for l in range(nl)]
+        cplan = dm.cycle_plan() if plan else None
         # distributed stationary solve (3 cycles) as well
         x = torch.zeros_like(bl)
         it, hist = dm.stationary_solve(bl, x, max_iter=4, rel_tol=1e-300)
         storage = (dm.level_matrix(storage_level, "A").spmv_info()
                    if infos[storage_level]["redundant"] == 0 else None)
-        return r0, r1, zl.cpu().numpy(), infos, hist, storage
+        return r0, r1, zl.cpu().numpy(), infos, hist, storage, cplan
 
     res = run_ranks(nranks, rank_fn)
     z = np.zeros(len(b))
@@ -179,6 +181,32 @@ def test_dist_sgs_27pt(nranks, split_kind, steps, resid_form):
         finally:
             fa().set_spmv_format("auto")
         assert np.array_equal(z2.view(np.int64), zg2.view(np.int64))
+
+
+@pytest.mark.parametrize("nranks,split_kind", [(2, "slab"), (3, "equal")])
+def test_dist_sgs_position_halo_lists(nranks, split_kind):
+    """Distributed SGS with the sweep-position halo lists (verdict r04 item 7):
+    before each colour only the ghost entries that a later colour of the reading
+    rank reads (the reading colours per entry are exchanged once at setup) -- the
+    cycle bitwise equal to the round-3 exchange of the whole halo before every
+    colour, and the halo bytes of the SGS level's smoothing (pre-smoothing from
+    zero + post-smoothing) at most 2x those of two Jacobi steps (one whole-halo
+    refresh each), as the distributed cycle plan records them."""
+    dims = (14, 12, 16)
+    b = np.random.default_rng(23 + nranks).uniform(-1, 1, int(np.prod(dims)))
+    kw = dict(problem="27pt", smoother="sgs", steps=1, plan=True)
+    z_on, r_on = dist_apply(nranks, dims, 60, b, 100, split_kind, per_colour=True, **kw)
+    z_off, r_off = dist_apply(nranks, dims, 60, b, 100, split_kind, per_colour=False, **kw)
+    assert np.array_equal(z_on.view(np.int64), z_off.view(np.int64))
+    for rank in range(nranks):
+        on = [p for p in r_on[rank][6] if p["level"] == 0 and p["kernel"] == -2 and p["role"] == "smooth"]
+        off = [p for p in r_off[rank][6] if p["level"] == 0 and p["kernel"] == -2 and p["role"] == "smooth"]
+        full = {p["bytes"] for p in off}
+        assert len(full) == 1, full  # every round-3 exchange is the whole halo
+        full = full.pop()
+        assert len(off) == 7 + 7 + 8 + 7  # from zero: 2C - 2 exchanges; after the interpolation: 2C - 1
+        assert all(p["name"] == "halo_sgs" for p in on)
+        assert sum(p["bytes"] for p in on) <= 2 * (2 * full), (rank, sum(p["bytes"] for p in on), full)
 
 
 def test_rccl_single_rank():
@@ -499,12 +527,14 @@ def slab_run(nranks, dims, coarsest, agglo, b, overlap=True, gtx_time=0):
         splits = fa().slab_splits(fa().box_level_dims(dims, (2, 2, 2), nl), nranks)
         comm = fa().Comm(ctx, hub=hub, rank=r)
         dm = fa().DistMultigrid(comm, mg, splits, agglomerate_rows=agglo).set_overlap(overlap)
+        dm.set_per_colour_halo(per_colour)
         r0, r1 = dm.local_rows()
         bl = torch.as_tensor(np.ascontiguousarray(b[r0:r1]), device="cuda:0")
         zl = torch.empty_like(bl)
         dm.apply(zl, bl)
         ctx.synchronize()
         infos = [dm.level_info(l) for l in range(nl)]
+        cplan = dm.cycle_plan() if plan else None
         La = sum(1 for i in infos if i["redundant"] == 0)
         local = [tuple(_kinds(dm.level_matrix(l, w).spmv_info()) for w in ("A", "R", "P")) for l in range(La)]
         glob = [tuple(_kinds(M.spmv_info()) if M is not None else None for M in (lv[0], lv[2], lv[3]))
