@@ -33,6 +33,37 @@ if not os.path.exists(LIB_PATH):
 
 _lib = C.CDLL(LIB_PATH)
 
+
+def source_hash(root=None):
+    """sha256[:16] over the library's sources in the Makefile's order (SRCFILES)."""
+    import glob
+    import hashlib
+    root = root or os.path.dirname(_PKG_DIR)
+    src = os.path.join(root, "csrc")
+    files = []
+    for pat in ("*.hip", "*.cpp", "*.hpp", "*.inc"):
+        files += sorted(glob.glob(os.path.join(src, pat)))
+    files.append(os.path.join(root, "..", "include", "amg.h"))
+    h = hashlib.sha256()
+    for f in files:
+        with open(f, "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()[:16]
+
+
+def library_hash():
+    f = _lib.amg_source_hash
+    f.restype = C.c_char_p
+    return f().decode()
+
+
+# a prebuilt library must match the sources beside it (it travels with the tree
+# to the GPU box): a stale one is refused instead of silently running old kernels
+if not os.environ.get("FAMG_LIB") and os.path.isdir(os.path.join(os.path.dirname(_PKG_DIR), "csrc")):
+    if library_hash() != source_hash():
+        raise ImportError(f"{LIB_PATH} was built from other sources (library {library_hash()}, tree "
+                          f"{source_hash()}): rebuild with make -C faer-amg_amd")
+
 i32, i64, dbl, vp = C.c_int32, C.c_int64, C.c_double, C.c_void_p
 P = C.POINTER
 
@@ -66,6 +97,7 @@ SIGNATURES = {
     "amg_csr_grid_info": (i32, [vp, vp]),
     "amg_grid_from_offsets": (i32, [vp, i64, i64, vp, P(i32)]),
     "amg_set_flag": (i32, [i32, i64]),
+    "amg_source_hash": (C.c_char_p, []),
     "amg_get_flag": (i32, [i32, P(i64)]),
     "amg_gen_laplace3d_7pt": (i32, [vp, i64, i64, i64, P(vp)]),
     "amg_gen_aniso27": (i32, [vp, i64, i64, i64, dbl, dbl, dbl, P(vp)]),

@@ -353,6 +353,11 @@ amg_status amg_multigrid_cycle_plan(amg_linop *mg, amg_launch_rec *recs, int64_t
  * level = global level index (the redundant tail's levels after the
  * distributed ones), rows = this rank's rows. */
 amg_status amg_dist_cycle_plan(amg_linop *dist, amg_launch_rec *recs, int64_t cap, int64_t *count);
+/* The first 16 hex digits of sha256 over the library's sources (csrc/*.hip,
+ * *.cpp, *.hpp, *.inc in sorted order, then this header) it was built from: the
+ * Python package and __graft_entry__.build() compare it with the tree and
+ * refuse / rebuild a stale prebuilt library. */
+const char *amg_source_hash(void);
 /* Launch the marker kernel k_trace_mark(tag) on the context stream: brackets a
  * region of a rocprofv3 kernel trace (bench.py marks its timed V-cycles, and
  * scripts/prof_summary.py keeps the dispatches between the marks). */
