@@ -271,8 +271,8 @@ def make_operator(fa, ctx, args, dims):
         return fa.SparseMatOp.aniso27(ctx, *dims, 1.0, 1.0, 0.01)
     if args.problem == "elast":  # in-tree C5 stand-in (Flan_1565 cannot be fetched)
         e = args.elements
-        return fa.elasticity_q1((e, e, e), contrast=1.0, nu=0.3, seed=42,
-                                permute=True if args.permute == 0 else args.permute).upload(ctx)
+        perm = False if args.permute < 0 else True if args.permute == 0 else args.permute
+        return fa.elasticity_q1((e, e, e), contrast=1.0, nu=0.3, seed=42, permute=perm).upload(ctx)
     if args.problem == "mtx":  # a Matrix Market file placed on the box (e.g. Flan_1565.mtx)
         return fa.read_mtx(args.mtx).upload(ctx)
     raise ValueError(args.problem)
@@ -294,7 +294,7 @@ def workload_name(args, dims):
     if args.problem in ("7pt", "27pt"):
         return (f"SA V-cycle, 3D {args.problem} {dims[0]}x{dims[1]}x{dims[2]}, box {args.box}^3, "
                 f"{args.smoother} s=1 mu=1, Cholesky coarsest")
-    perm = "all nodes" if args.permute == 0 else f"windows of {args.permute} nodes"
+    perm = "all nodes" if args.permute == 0 else "no nodes" if args.permute < 0 else f"windows of {args.permute} nodes"
     src = (f"Q1 elasticity {args.elements}^3 elements (C5 stand-in: random E, node numbering shuffled "
            f"within {perm})"
            if args.problem == "elast" else f"Matrix Market {os.path.basename(args.mtx)}")
@@ -1118,7 +1118,8 @@ def main():
     ap.add_argument("--mtx", default=None, help="mtx: path of a Matrix Market file")
     ap.add_argument("--permute", type=int, default=4096,
                     help="elast: node numbering shuffled within windows of this many nodes (the locality "
-                         "of a mesh numbering without stencil structure); 0 = over all nodes")
+                         "of a mesh numbering without stencil structure); 0 = over all nodes; -1 = none "
+                         "(the generator's lexicographic numbering)")
     ap.add_argument("--block-size", type=int, default=3, help="elast/mtx: dofs per node")
     ap.add_argument("--strength-depth", type=int, default=1,
                     help="elast/mtx: BFS depth of the strength graph (the reference hard-codes 3, "

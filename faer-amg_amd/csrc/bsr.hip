@@ -48,6 +48,7 @@ struct BsrArgs {
     const int32_t *soff;  // step offset per slice (+1)
     int32_t slice0, nslices;
     BsrEpi e;
+    int32_t jmask;  // node column mask: -1; 0 = measurement only (FAMG_BSR_DIAG=1: every x gather at node 0)
 };
 
 template <int MODE> struct BsrRow {
@@ -72,7 +73,7 @@ template <int MODE> struct BsrRow {
 // U block steps: every load of the group is issued before the fmas
 template <int U>
 __device__ __forceinline__ void bsr_steps(const char *__restrict__ st, int lane, const double *__restrict__ x,
-                                          double &a0, double &a1, double &a2) {
+                                          double &a0, double &a1, double &a2, int jmask) {
     double v[U][9], xx[U][3];
 #pragma unroll
     for (int u = 0; u < U; u++) {
@@ -84,7 +85,7 @@ __device__ __forceinline__ void bsr_steps(const char *__restrict__ st, int lane,
             v[u][2 * q + 1] = w.y;
         }
         v[u][8] = __builtin_nontemporal_load(reinterpret_cast<const double *>(p + BSR_K8) + lane);
-        const int J = __builtin_nontemporal_load(reinterpret_cast<const int32_t *>(p + BSR_COL) + lane);
+        const int J = __builtin_nontemporal_load(reinterpret_cast<const int32_t *>(p + BSR_COL) + lane) & jmask;
         const double *xp = x + 3 * (int64_t)J;
         xx[u][0] = xp[0];
         xx[u][1] = xp[1];
@@ -123,11 +124,11 @@ __global__ __launch_bounds__(256) void spmv_bsr3_kernel(BsrArgs a) {
     const char *st = a.data + (int64_t)t0 * BSR_STEP;
     double a0 = 0.0, a1 = 0.0, a2 = 0.0;
     int t = 0;
-    for (; t + 4 <= w; t += 4) bsr_steps<4>(st + (int64_t)t * BSR_STEP, lane, a.e.x, a0, a1, a2);
+    for (; t + 4 <= w; t += 4) bsr_steps<4>(st + (int64_t)t * BSR_STEP, lane, a.e.x, a0, a1, a2, a.jmask);
     switch (w - t) {
-    case 1: bsr_steps<1>(st + (int64_t)t * BSR_STEP, lane, a.e.x, a0, a1, a2); break;
-    case 2: bsr_steps<2>(st + (int64_t)t * BSR_STEP, lane, a.e.x, a0, a1, a2); break;
-    case 3: bsr_steps<3>(st + (int64_t)t * BSR_STEP, lane, a.e.x, a0, a1, a2); break;
+    case 1: bsr_steps<1>(st + (int64_t)t * BSR_STEP, lane, a.e.x, a0, a1, a2, a.jmask); break;
+    case 2: bsr_steps<2>(st + (int64_t)t * BSR_STEP, lane, a.e.x, a0, a1, a2, a.jmask); break;
+    case 3: bsr_steps<3>(st + (int64_t)t * BSR_STEP, lane, a.e.x, a0, a1, a2, a.jmask); break;
     default: break;
     }
     if (live) {
@@ -383,8 +384,12 @@ void spmv_bsr(const GpuCsr &m, const double *x, double *y, SpmvMode mode, const 
     const int64_t s0 = seg < 0 ? 0 : m.bsr_seg_slc[seg];
     const int64_t s1 = seg < 0 ? m.bsr_slices : m.bsr_seg_slc[seg + 1];
     if (s1 <= s0) return;
+    static const int32_t jmask = [] {
+        const char *e = getenv("FAMG_BSR_DIAG");
+        return (e && e[0] == '1') ? 0 : -1;
+    }();
     BsrArgs a{m.bsr_data.get(), m.bsr_row0.get(), m.bsr_soff.get(), (int32_t)s0, (int32_t)(s1 - s0),
-              BsrEpi{x, y, epi.b, epi.d, epi.dc, epi.dt}};
+              BsrEpi{x, y, epi.b, epi.d, epi.dc, epi.dt}, jmask};
     const dim3 grid((unsigned)ceil_div(s1 - s0, 4)), block(256);
     // T: the template arguments after the mode
 #define FAMG_BSR_LAUNCH(K, T)                                                      \
