@@ -244,6 +244,84 @@ __global__ __launch_bounds__(256) void spmv_bsr3p_kernel(BsrArgs a) {
     }
 }
 
+// ------------------------------------------------------------ long-row form
+// A matrix of few, long node rows (R_0 and A_1 of C5: 625 slices of ~128 block
+// steps) is bound by each wave's chain of dependent round trips (node columns,
+// then the x operands they address, per group of steps), not by HBM.  Here
+// (FLAG_BSR_LONG: slices averaging at least that many steps) a wave walks
+// 8-step groups and loads the next group's node columns while the current
+// group's values and x operands are in flight: one round trip per 8 steps.
+// Two column buffers alternate (no loop-carried copies).  Same fma order per
+// dof row: bitwise the kernels above.
+constexpr int BSR_LU = 8;
+
+__device__ __forceinline__ void bsr_long_cols(const char *__restrict__ st, int lane, int g, int tl, int (&J)[BSR_LU]) {
+#pragma unroll
+    for (int u = 0; u < BSR_LU; u++)  // (the mask is applied at use: no wait on these loads here)
+        J[u] = __builtin_nontemporal_load(
+            reinterpret_cast<const int32_t *>(st + (int64_t)min(g * BSR_LU + u, tl) * BSR_STEP + BSR_COL) + lane);
+}
+
+__device__ __forceinline__ void bsr_long_issue(const char *__restrict__ st, int lane, const double *__restrict__ x,
+                                               const int (&J)[BSR_LU], int jmask, int g, int tl,
+                                               double (&v)[BSR_LU][9], double (&xx)[BSR_LU][3]) {
+#pragma unroll
+    for (int u = 0; u < BSR_LU; u++) {
+        const char *p = st + (int64_t)min(g * BSR_LU + u, tl) * BSR_STEP;
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            const bsr_dbl2_t w = __builtin_nontemporal_load(reinterpret_cast<const bsr_dbl2_t *>(p + q * 1024) + lane);
+            v[u][2 * q] = w.x;
+            v[u][2 * q + 1] = w.y;
+        }
+        v[u][8] = __builtin_nontemporal_load(reinterpret_cast<const double *>(p + BSR_K8) + lane);
+        const double *xp = x + 3 * (int64_t)(J[u] & jmask);
+        xx[u][0] = xp[0];
+        xx[u][1] = xp[1];
+        xx[u][2] = xp[2];
+    }
+}
+
+template <int MODE>
+__global__ __launch_bounds__(256) void spmv_bsr3l_kernel(BsrArgs a) {
+    const int blk = xcd_remap(blockIdx.x, gridDim.x);
+    const int sl = __builtin_amdgcn_readfirstlane(blk * 4 + (int)(threadIdx.x >> 6));
+    if (sl >= a.nslices) return;
+    const int s = a.slice0 + sl;
+    const int lane = threadIdx.x & 63;
+    const int I = a.row0[s] + lane;
+    const bool live = I < a.row0[s + 1];
+    const int t0 = a.soff[s], w = a.soff[s + 1] - t0;
+    const char *st = a.data + (int64_t)t0 * BSR_STEP;
+    double a0 = 0.0, a1 = 0.0, a2 = 0.0;
+    BsrRow<MODE> r0, r1, r2;
+    if (live) {
+        r0.load(a.e, 3 * I);
+        r1.load(a.e, 3 * I + 1);
+        r2.load(a.e, 3 * I + 2);
+    }
+    if (w > 0) {
+        const int tl = w - 1;
+        int JA[BSR_LU], JB[BSR_LU];
+        bsr_long_cols(st, lane, 0, tl, JA);
+        for (int g = 0; g * BSR_LU < w; g += 2) {
+            double v[BSR_LU][9], xx[BSR_LU][3];
+            bsr_long_issue(st, lane, a.e.x, JA, a.jmask, g, tl, v, xx);
+            if ((g + 1) * BSR_LU < w) bsr_long_cols(st, lane, g + 1, tl, JB);
+            bsr_sum<BSR_LU>(v, xx, g, w, a0, a1, a2);
+            if ((g + 1) * BSR_LU >= w) break;
+            bsr_long_issue(st, lane, a.e.x, JB, a.jmask, g + 1, tl, v, xx);
+            if ((g + 2) * BSR_LU < w) bsr_long_cols(st, lane, g + 2, tl, JA);
+            bsr_sum<BSR_LU>(v, xx, g + 1, w, a0, a1, a2);
+        }
+    }
+    if (live) {
+        r0.store(a.e, 3 * I, a0);
+        r1.store(a.e, 3 * I + 1, a1);
+        r2.store(a.e, 3 * I + 2, a2);
+    }
+}
+
 static bool bsr_disabled() {
     static const bool off = [] {
         const char *e = getenv("FAMG_NO_BSR");
@@ -267,7 +345,7 @@ bool build_bsr(GpuCsr &m, const std::vector<int64_t> &rp, int64_t other_bytes) {
         if (b % BSR_B) return false;
     const int64_t N = m.nrows / BSR_B;
     hipStream_t s = m.ctx->stream;
-    {  // cheap pre-check on the first node rows: blocked at all?
+    if (!m.bsr_pin) {  // cheap pre-check on the first node rows: blocked at all?
         const int64_t Ns = std::min<int64_t>(N, 2048), ne = rp[3 * Ns];
         std::vector<int32_t> c(ne);
         if (ne) FAMG_CHECK_HIP(hipMemcpyAsync(c.data(), m.col.get(), ne * sizeof(int32_t), hipMemcpyDeviceToHost, s));
@@ -284,6 +362,11 @@ bool build_bsr(GpuCsr &m, const std::vector<int64_t> &rp, int64_t other_bytes) {
     std::vector<int32_t> col(m.nnz);
     FAMG_CHECK_HIP(hipMemcpyAsync(col.data(), m.col.get(), m.nnz * sizeof(int32_t), hipMemcpyDeviceToHost, s));
     FAMG_CHECK_HIP(hipStreamSynchronize(s));
+    // a renumbered copy (reorder.hip: nodes renumbered, each row in its original
+    // order) merges a node's rows by original column: key(c) -- blocks keep their
+    // original ascending-column order, stored under the new node column c / 3
+    const std::vector<int32_t> &co = m.col_orig;
+    auto key = [&](int32_t c) -> int64_t { return co.empty() ? c : co[c]; };
     // node columns per node row: the union of its three rows' (ascending) col / 3
     std::vector<int64_t> nb(N + 1, 0);
     bool sorted = true;
@@ -295,10 +378,10 @@ bool build_bsr(GpuCsr &m, const std::vector<int64_t> &rp, int64_t other_bytes) {
         for (;;) {
             int64_t best = INT64_MAX;
             for (int r = 0; r < 3; r++)
-                if (p[r] < e[r]) best = std::min<int64_t>(best, col[p[r]] / 3);
+                if (p[r] < e[r]) best = std::min<int64_t>(best, key(col[p[r]]) / 3);
             if (best == INT64_MAX) break;
             for (int r = 0; r < 3; r++)
-                while (p[r] < e[r] && col[p[r]] / 3 == best) p[r]++;
+                while (p[r] < e[r] && key(col[p[r]]) / 3 == best) p[r]++;
             if (best <= last) sorted = false;
             last = best;
             cnt++;
@@ -327,7 +410,7 @@ bool build_bsr(GpuCsr &m, const std::vector<int64_t> &rp, int64_t other_bytes) {
     }
     const int64_t steps = soff[ns];
     const int64_t bytes = steps * BSR_STEP + 4 * (2 * ns + 2);
-    if (bytes >= other_bytes) return false;
+    if (bytes >= other_bytes && !m.bsr_pin) return false;
     std::vector<double> val(m.nnz);
     FAMG_CHECK_HIP(hipMemcpyAsync(val.data(), m.val.get(), m.nnz * sizeof(double), hipMemcpyDeviceToHost, s));
     FAMG_CHECK_HIP(hipStreamSynchronize(s));
@@ -345,18 +428,20 @@ bool build_bsr(GpuCsr &m, const std::vector<int64_t> &rp, int64_t other_bytes) {
             for (;; t++) {
                 int64_t J = INT64_MAX;
                 for (int r = 0; r < 3; r++)
-                    if (p[r] < e[r]) J = std::min<int64_t>(J, col[p[r]] / 3);
+                    if (p[r] < e[r]) J = std::min<int64_t>(J, key(col[p[r]]) / 3);
                 if (J == INT64_MAX) break;
                 char *st = blk + t * BSR_STEP;
+                int32_t Jstore = -1;
                 for (int r = 0; r < 3; r++)
-                    for (; p[r] < e[r] && col[p[r]] / 3 == J; p[r]++) {
+                    for (; p[r] < e[r] && key(col[p[r]]) / 3 == J; p[r]++) {
+                        Jstore = col[p[r]] / 3;
                         const int kk = 3 * r + col[p[r]] % 3;
                         double *dst = kk < 8 ? reinterpret_cast<double *>(st + (kk / 2) * 1024) + 2 * lane + (kk & 1)
                                              : reinterpret_cast<double *>(st + BSR_K8) + lane;
                         *dst = val[p[r]];
                     }
-                reinterpret_cast<int32_t *>(st + BSR_COL)[lane] = (int32_t)J;
-                lastJ = (int32_t)J;
+                reinterpret_cast<int32_t *>(st + BSR_COL)[lane] = Jstore;  // the (new) node column
+                lastJ = Jstore;
             }
             for (; t < w; t++)  // padding blocks: zeros at the row's last node column
                 reinterpret_cast<int32_t *>(blk + t * BSR_STEP + BSR_COL)[lane] = lastJ;
@@ -402,7 +487,9 @@ void spmv_bsr(const GpuCsr &m, const double *x, double *y, SpmvMode mode, const 
     }
 #define FAMG_C ,
     const int64_t how = m.bsr_maxw <= BSR_PCOL ? flag(FLAG_BSR_KERNEL) : 0;
-    if (how == 1) FAMG_BSR_LAUNCH(spmv_bsr3p_kernel, FAMG_C 4 FAMG_C false)
+    const int64_t lg = flag(FLAG_BSR_LONG);
+    if (lg >= 0 && m.bsr_steps >= lg * m.bsr_slices) FAMG_BSR_LAUNCH(spmv_bsr3l_kernel, )
+    else if (how == 1) FAMG_BSR_LAUNCH(spmv_bsr3p_kernel, FAMG_C 4 FAMG_C false)
     else if (how == 2) FAMG_BSR_LAUNCH(spmv_bsr3p_kernel, FAMG_C 2 FAMG_C true)
     else if (how == 3) FAMG_BSR_LAUNCH(spmv_bsr3p_kernel, FAMG_C 4 FAMG_C true)
     else FAMG_BSR_LAUNCH(spmv_bsr3_kernel, )

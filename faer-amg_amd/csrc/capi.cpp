@@ -109,7 +109,8 @@ static std::atomic<int64_t> g_flag_val[FLAG_COUNT] = {
     {[] { const char *e = getenv("FAMG_GTX_TIME"); return (int64_t)(e ? atoi(e) : 2); }()},
     {[] { const char *e = getenv("FAMG_SGS27_MARCH"); return (int64_t)(e ? atoi(e) : 1); }()},
     {[] { const char *e = getenv("FAMG_XS_PIPE"); return (int64_t)(e ? atoi(e) : 2); }()},
-    {[] { const char *e = getenv("FAMG_BSR_KERNEL"); return (int64_t)(e ? atoi(e) : 0); }()}};
+    {[] { const char *e = getenv("FAMG_BSR_KERNEL"); return (int64_t)(e ? atoi(e) : 0); }()},
+    {[] { const char *e = getenv("FAMG_BSR_LONG"); return (int64_t)(e ? atoll(e) : 16); }()}};
 static std::atomic<uint64_t> g_flag_gen{0};
 int64_t flag(FlagId f) { return g_flag_val[f].load(std::memory_order_relaxed); }
 void set_flag(FlagId f, int64_t v) {
@@ -734,6 +735,11 @@ amg_status amg_multigrid_set_option(amg_linop *mg, int32_t option, int64_t value
         case 2: m->fold_zero_guess = value != 0; break;
         case 3: m->fuse_transfers = value != 0; m->invalidate_graphs(); m->fuse_reset(); break;
         case 4: m->restrict_df = value != 0; break;
+        case 5:
+            FAMG_REQUIRE(value >= 0 && value <= 2, AMG_ERR_INVALID, "reorder: 0, 1 or 2");
+            m->undo_reorder();
+            m->reorder = (int)value;
+            break;
         default: fail(AMG_ERR_INVALID, "unknown multigrid option");
         }
         m->invalidate_graphs();
@@ -794,11 +800,22 @@ amg_status amg_multigrid_get_level(const amg_linop *mg, int64_t level, amg_linop
     return guard([&] {
         auto m = need_mg(mg);
         FAMG_REQUIRE(level >= 0 && level < (int64_t)m->levels.size(), AMG_ERR_INVALID, "level out of range");
-        const MgLevel &L = m->levels[level];
-        if (A) *A = box(L.A);
-        if (S) *S = box(L.S);
-        if (R) *R = L.R ? box(L.R) : nullptr;
-        if (P) *P = L.P ? box(L.P) : nullptr;
+        const MgLevel &L = m->levels[level];  // the caller's operators (not a renumbered copy)
+        if (A) *A = box(L.origA());
+        if (S) *S = box(L.origS());
+        if (R) *R = L.origR() ? box(L.origR()) : nullptr;
+        if (P) *P = L.origP() ? box(L.origP()) : nullptr;
+    });
+}
+
+amg_status amg_multigrid_level_reordered(amg_linop *mg, int64_t level, int32_t *reordered) {
+    return guard([&] {
+        auto m = need_mg(mg);
+        FAMG_REQUIRE(reordered, AMG_ERR_INVALID, "null output");
+        std::lock_guard<std::mutex> lk(m->mtx);
+        FAMG_REQUIRE(level >= 0 && level < (int64_t)m->levels.size(), AMG_ERR_INVALID, "level out of range");
+        m->ensure_workspace();  // the renumbering is decided with the workspaces
+        *reordered = m->levels[level].permuted ? 1 : 0;
     });
 }
 

@@ -284,7 +284,7 @@ void csr_finalize(GpuCsr &m, const std::vector<int64_t> *segments) {
     FAMG_CHECK_HIP(hipMemcpyAsync(m.sched.get(), sched.data(), sched.size() * sizeof(int32_t),
                                   hipMemcpyHostToDevice, ctx.stream));
     FAMG_CHECK_HIP(hipStreamSynchronize(ctx.stream));
-    infer_grid(m, rp);
+    if (!m.order_fixed) infer_grid(m, rp);  // a renumbered copy keeps no grid (reorder.hip)
     scs_release(m);
     sellp_release(m);
     gtc_release(m);
@@ -307,7 +307,7 @@ void csr_finalize(GpuCsr &m, const std::vector<int64_t> *segments) {
     // long DIA run patterns (> 27 diagonals: A_1 of the 7-point box hierarchy) on a
     // grid may run faster as x-staged stencil classes: both are built and timed
     const bool dia_vs_xscs = dia_all && m.dia_k > 27 && m.grid[0] > 0;
-    const bool scs = (!dia_all || dia_vs_xscs) && !m.has_bsr() && build_scs(m, rp, other_b);
+    const bool scs = (!dia_all || dia_vs_xscs) && !m.has_bsr() && !m.order_fixed && build_scs(m, rp, other_b);
     if (dia_vs_xscs && scs) {
         if (m.xscs && xscs_beats_dia(m)) {
             m.dia_codes.release();
@@ -329,7 +329,7 @@ void csr_finalize(GpuCsr &m, const std::vector<int64_t> *segments) {
         m.dia_r0 = m.dia_r1 = m.dia_seg = 0;
         m.dia_off.clear();
     }
-    if (!dia_all && !m.has_bsr() && (scs_all || (!scs && build_sellp(m, rp, other_b)))) {
+    if (!dia_all && !m.has_bsr() && (scs_all || (!scs && !m.order_fixed && build_sellp(m, rp, other_b)))) {
         m.sell_row0.release(); m.sell_soff.release(); m.sell_desc.release(); m.sell_base.release();
         m.sell_data.release(); m.sell_vtab.release();
         m.nslices = m.sell_steps = m.sell_bytes = m.sell_ntab = 0;

@@ -1100,8 +1100,12 @@ static void set_frames(GpuCsr &m, const SlabFrame &rf, const SlabFrame &cf, bool
     }
 }
 
-static std::shared_ptr<DistMultigridOp> build_dist(amg_comm *comm, const MultigridOp &g,
+static std::shared_ptr<DistMultigridOp> build_dist(amg_comm *comm, MultigridOp &g_in,
                                                    const int64_t *splits, int64_t agglo) {
+    // the caller's operators (a multigrid that ran may hold renumbered copies of
+    // some levels, reorder.hip): the splits refer to their rows
+    const std::shared_ptr<MultigridOp> gview = g_in.original_view();
+    const MultigridOp &g = *gview;
     Ctx *ctx = comm->ctx;
     Transport &tr = *comm->tr;
     const int P = tr.nranks, me = tr.rank;
@@ -1276,6 +1280,7 @@ static std::shared_ptr<DistMultigridOp> build_dist(amg_comm *comm, const Multigr
     d->tail->fold_zero_guess = g.fold_zero_guess;
     d->tail->sgs_residual_form = g.sgs_residual_form;
     d->tail->restrict_df = g.restrict_df;  // DistMultigridOp::restrict_df reads it
+    d->tail->reorder = 0;  // the distributed cycle drives the tail's levels directly, in their numbering
     for (int64_t l = d->La; l < d->nlevels; l++) d->tail->levels.push_back(MgLevel{g.levels[l].A, g.levels[l].S, g.levels[l].R, g.levels[l].P});
     d->tail->nrows = d->tail->ncols = g.levels[d->La].A->nrows;
     // the tail is cycled redundantly on every rank: under the auto policy,

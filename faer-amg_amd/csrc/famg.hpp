@@ -143,6 +143,8 @@ struct GpuCsr {
     int64_t bsr_slices = 0, bsr_steps = 0, bsr_maxw = 0;
     std::vector<int64_t> bsr_seg_slc;
     bool no_bsr = false;  // e.g. a color-permuted SGS copy
+    bool bsr_pin = false;  // a renumbered copy of a 3x3-block matrix: take the block storage whenever it builds
+    int8_t kind_pin = -1;  // a renumbered copy: 0 one-lane storages (SELL / x-staged) whenever they build, 1 wave-per-row, 2 CSR-stream
     // pattern SELL with L lanes per row (sellp.hip): values / codes only, columns
     // from per-slice offset patterns
     DevBuf<char> sellp_vals;
@@ -209,6 +211,13 @@ struct GpuCsr {
     DevBuf<int32_t> xs_soff, xs_coff, xs_chunks;
     int64_t xs_groups = 0, xs_bytes = 0, xs_steps = 0, xs_chunk_total = 0, xs_escape_slices = 0;
     int64_t xs_maxw = 0;  // widest slice (the burst kernel's batch: 7 or 8 steps)
+    // a renumbered copy (reorder.hip): rows in a new order, each row's entries in
+    // the original's stored order with renamed columns -- storages that reorder a
+    // row's entries (DIA, stencil / grid-transfer classes, pattern and aligned SELL)
+    // are not built, so every row sum stays the original's; col_orig = new column ->
+    // original column (the 3x3-block build merges a node's rows by original column)
+    bool order_fixed = false;
+    std::vector<int32_t> col_orig;
     int kernel = 0;  // SpmvKernel chosen at finalize
     bool spmv_ready() const { return rp32.get() != nullptr && sched.get() != nullptr; }
     bool has_sell() const { return sell_desc.get() != nullptr; }
@@ -492,6 +501,15 @@ struct TransferFuse;  // fuse.hip
 extern int g_fuse_transfers;
 struct MgLevel {
     LinOpPtr A, S, R, P;  // R, P: transfer to the next-coarser level (null on the coarsest)
+    // locality reordering (reorder.hip): the operators the caller added when A/S/R/P
+    // above are renumbered copies; perm = the level's numbering (new -> original)
+    LinOpPtr oA, oS, oR, oP;
+    DevBuf<int32_t> perm;
+    bool permuted = false;
+    const LinOpPtr &origA() const { return oA ? oA : A; }
+    const LinOpPtr &origS() const { return oS ? oS : S; }
+    const LinOpPtr &origR() const { return oR ? oR : R; }
+    const LinOpPtr &origP() const { return oP ? oP : P; }
     // device workspaces (allocated lazily at first apply)
     DevBuf<double> v, f, t, r;
     // fused residual->restriction and interpolation->Jacobi launches (fuse.hip)
@@ -512,6 +530,9 @@ struct MultigridOp : LinOp {
     // R on wide grid-transfer classes writes the next level's first Jacobi step
     // from zero beside f_c (SPMV_SETDF) instead of a separate d*f pass
     bool restrict_df = true;
+    // locality reordering of general levels (reorder.hip): 0 off, 1 where RCM at
+    // least halves the x lines an SpMV slice touches (default), 2 every eligible level
+    int reorder = 1;
     std::mutex mtx;
     Kind kind() const override { return Kind::Multigrid; }
     bool is_precond() const override { return true; }
@@ -529,6 +550,11 @@ struct MultigridOp : LinOp {
     void smooth(int64_t l, double *&v, double *&t, const double *f, bool v_zero, bool pre_df = false);
     // launch records of one V-cycle (eager, recorder on)
     std::vector<LaunchRec> cycle_plan();
+    // renumber eligible levels (first ensure_workspace) / restore the caller's operators
+    void reorder_levels();
+    void undo_reorder();
+    // the same multigrid over the caller's operators (no renumbering)
+    std::shared_ptr<MultigridOp> original_view();
 
   private:
     struct GraphEntry {
@@ -540,7 +566,12 @@ struct MultigridOp : LinOp {
     uint64_t flags_gen_ = 0;  // flags_generation() the graphs were captured under
     bool workspace_ready_ = false;
     bool fuse_ready_ = false;
+    bool reorder_done_ = false;
+    DevBuf<double> perm_f0_, perm_v0_;  // the fine level's rhs / result in its numbering
 };
+// y = x[p] / y[p] = x over n entries (reorder.hip; launch-plan records)
+void perm_gather(double *out, const double *in, const int32_t *p, int64_t n, hipStream_t s);
+void perm_scatter(double *out, const double *in, const int32_t *p, int64_t n, hipStream_t s);
 
 // the zero-guess fold decision of one level (RESID0 + ADD0 instead of v = d*f)
 // m's DIA codes are a constant 7- or 27-point stencil on an nx x ny x nz grid (nx

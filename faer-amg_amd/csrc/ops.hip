@@ -407,6 +407,7 @@ void MultigridOp::invalidate_graphs() {
 
 void MultigridOp::add_level(LinOpPtr A, LinOpPtr S, LinOpPtr R, LinOpPtr P) {
     FAMG_REQUIRE(!levels.empty(), AMG_ERR_INVALID, "add_level on an empty multigrid");
+    undo_reorder();  // renumbered again at the next apply, over every level
     FAMG_REQUIRE(A && S && R && P, AMG_ERR_INVALID, "add_level: null operator");
     const int64_t nf = levels.back().A->nrows, nc = A->nrows;
     FAMG_REQUIRE(A->nrows == A->ncols, AMG_ERR_DIM, "add_level: op must be square");
@@ -444,6 +445,7 @@ void MultigridOp::ensure_workspace() {
         }
         return;
     }
+    if (!reorder_done_) reorder_levels();
     for (size_t l = 0; l < levels.size(); l++) {
         const int64_t n = levels[l].A->nrows;
         MgLevel &L = levels[l];
@@ -711,7 +713,16 @@ void MultigridOp::apply(double *out, const double *rhs) {
         flags_gen_ = flags_generation();
     }
     hipStream_t s = ctx->stream;
-    auto run = [&]() { cycle(0, out, rhs, true, out); };
+    auto run = [&]() {
+        if (levels[0].permuted) {  // the fine level runs in its numbering: rhs in, result out
+            const int64_t n = levels[0].A->nrows;
+            perm_gather(perm_f0_.get(), rhs, levels[0].perm.get(), n, s);
+            cycle(0, perm_v0_.get(), perm_f0_.get(), true, perm_v0_.get());
+            perm_scatter(out, perm_v0_.get(), levels[0].perm.get(), n, s);
+        } else {
+            cycle(0, out, rhs, true, out);
+        }
+    };
     if (!use_graph || s == nullptr) {
         run();
         return;
@@ -754,7 +765,13 @@ std::vector<LaunchRec> MultigridOp::cycle_plan() {
     LaunchLog log;
     g_launch_log = &log;
     try {
-        cycle(0, z.get(), b.get(), true, z.get());
+        if (levels[0].permuted) {
+            perm_gather(perm_f0_.get(), b.get(), levels[0].perm.get(), n, ctx->stream);
+            cycle(0, perm_v0_.get(), perm_f0_.get(), true, perm_v0_.get());
+            perm_scatter(z.get(), perm_v0_.get(), levels[0].perm.get(), n, ctx->stream);
+        } else {
+            cycle(0, z.get(), b.get(), true, z.get());
+        }
     } catch (...) {
         g_launch_log = nullptr;
         throw;

@@ -1,0 +1,437 @@
+// reorder.hip -- locality reordering of general multigrid levels, bitwise neutral.
+//
+// A general operator whose numbering has no locality (the C5 stand-in: mesh
+// nodes shuffled within windows of 4096; a user's matrix in any order) makes
+// every x gather of its SpMV a distinct cache line: the fine 3x3-block SpMV of
+// the C5 stand-in ran 261 / 276 us (RESID / JACOBI), 177 / 180 us with its x
+// gathers pointed at one node (a measurement-only build) and 193 / 187 us on the
+// generator's lexicographic numbering (profiles/r05/c5_locality.txt).
+//
+// The cycle can run a level in another numbering without changing one bit:
+// rows of A_l', R_l', P_l' are the original rows in the new order, each row's
+// entries keep their stored (original ascending-column) order with the column
+// ids renamed, so every row sum is the same fma chain over the same values and
+// the same x entries (found at their new positions).  The smoother's diagonal
+// is permuted alike; the vectors of a permuted level live in its numbering
+// throughout the cycle, so only the fine level's rhs and result cross it (one
+// gather, one scatter per apply).  The numbering: reverse Cuthill-McKee on the
+// node graph (block size 3 for 3x3-blocked operators, so blocks stay intact),
+// kept for a level when it at least halves the x cache lines its 64-row slices
+// touch.  Storages that rely on column order (DIA, stencil and grid-transfer
+// classes, pattern SELL, aligned SELL slices) are not built for a permuted
+// matrix (GpuCsr::order_fixed); the 3x3-block storage merges a node's rows by
+// original column (GpuCsr::col_orig).
+#include <algorithm>
+#include <numeric>
+#include <queue>
+
+#include "famg.hpp"
+
+namespace famg {
+
+// RCM node order (new -> old) of the node graph of an n x n CSR (bs dofs per node)
+static std::vector<int32_t> rcm_order(const std::vector<int64_t> &rp, const std::vector<int32_t> &col, int64_t n,
+                                      int bs) {
+    const int64_t N = n / bs;
+    std::vector<int64_t> ap(N + 1, 0);
+    std::vector<std::vector<int32_t>> nb(N);
+#pragma omp parallel for schedule(dynamic, 1024)
+    for (int64_t I = 0; I < N; I++) {
+        auto &v = nb[I];
+        for (int64_t r = bs * I; r < bs * I + bs; r++)
+            for (int64_t e = rp[r]; e < rp[r + 1]; e++)
+                if (col[e] / bs != I) v.push_back(col[e] / bs);
+        std::sort(v.begin(), v.end());
+        v.erase(std::unique(v.begin(), v.end()), v.end());
+    }
+    std::vector<int32_t> deg(N);
+    for (int64_t I = 0; I < N; I++) deg[I] = (int32_t)nb[I].size();
+    std::vector<int32_t> order;
+    order.reserve(N);
+    std::vector<uint8_t> seen(N, 0);
+    std::vector<int32_t> lvl(N, -1);
+    auto bfs = [&](int32_t s, std::vector<int32_t> &out, bool mark) {
+        // breadth-first from s, neighbours by ascending degree (Cuthill-McKee)
+        std::vector<int32_t> q{s};
+        std::vector<uint8_t> *vis = &seen;
+        std::vector<uint8_t> tmp;
+        if (!mark) {
+            tmp.assign(N, 0);
+            vis = &tmp;
+        }
+        (*vis)[s] = 1;
+        lvl[s] = 0;
+        for (size_t h = 0; h < q.size(); h++) {
+            const int32_t u = q[h];
+            std::vector<int32_t> c;
+            for (int32_t w : nb[u])
+                if (!(*vis)[w]) {
+                    (*vis)[w] = 1;
+                    lvl[w] = lvl[u] + 1;
+                    c.push_back(w);
+                }
+            std::stable_sort(c.begin(), c.end(), [&](int32_t a, int32_t b) { return deg[a] < deg[b]; });
+            q.insert(q.end(), c.begin(), c.end());
+        }
+        out = std::move(q);
+    };
+    for (int64_t s0 = 0; s0 < N; s0++) {
+        if (seen[s0]) continue;
+        // a pseudo-peripheral start: twice the lowest-degree node of the last BFS level
+        int32_t s = (int32_t)s0;
+        for (int it = 0; it < 2; it++) {
+            std::vector<int32_t> q;
+            bfs(s, q, false);
+            const int32_t L = lvl[q.back()];
+            int32_t best = q.back();
+            for (auto it2 = q.rbegin(); it2 != q.rend() && lvl[*it2] == L; ++it2)
+                if (deg[*it2] < deg[best]) best = *it2;
+            s = best;
+        }
+        std::vector<int32_t> q;
+        bfs(s, q, true);
+        order.insert(order.end(), q.begin(), q.end());
+    }
+    std::reverse(order.begin(), order.end());
+    return order;
+}
+
+// Nodes grouped by their aggregate, aggregates in the coarse level's order
+// (new -> old node order): the aggregate of fine node I is the coarse node of
+// the largest |entry| of its first row of P (the tentative prolongation's entry,
+// which smoothing leaves dominant).  A 64-row slice then holds a few compact
+// aggregates, and consecutive rows of R (coarse rows) and P (fine rows) read
+// neighbouring x entries.
+static std::vector<int32_t> induced_order(const GpuCsr &P, int bs, int bsc, const std::vector<int32_t> &qc) {
+    const int64_t n = P.nrows, N = n / bs;
+    std::vector<int64_t> rp(n + 1);
+    std::vector<int32_t> col(std::max<int64_t>(1, P.nnz));
+    std::vector<double> val(std::max<int64_t>(1, P.nnz));
+    hipStream_t s = P.ctx->stream;
+    FAMG_CHECK_HIP(hipMemcpyAsync(rp.data(), P.rp64.get(), (n + 1) * 8, hipMemcpyDeviceToHost, s));
+    if (P.nnz) {
+        FAMG_CHECK_HIP(hipMemcpyAsync(col.data(), P.col.get(), P.nnz * 4, hipMemcpyDeviceToHost, s));
+        FAMG_CHECK_HIP(hipMemcpyAsync(val.data(), P.val.get(), P.nnz * 8, hipMemcpyDeviceToHost, s));
+    }
+    FAMG_CHECK_HIP(hipStreamSynchronize(s));
+    std::vector<int64_t> key(N);
+#pragma omp parallel for schedule(static)
+    for (int64_t I = 0; I < N; I++) {
+        const int64_t r = bs * I;
+        int64_t best = -1;
+        double bv = -1.0;
+        for (int64_t e = rp[r]; e < rp[r + 1]; e++)
+            if (std::abs(val[e]) > bv) {
+                bv = std::abs(val[e]);
+                best = col[e];
+            }
+        // rank of the aggregate in the coarse order (qc: coarse dof old -> new)
+        key[I] = best < 0 ? INT64_MAX : (int64_t)(qc.empty() ? best : qc[best]) / bsc;
+    }
+    std::vector<int32_t> order(N);
+    std::iota(order.begin(), order.end(), 0);
+    std::stable_sort(order.begin(), order.end(), [&](int32_t a, int32_t b) { return key[a] < key[b]; });
+    return order;
+}
+
+// x cache lines (16 entries) summed over 64-row slices, rows in the order
+// row_n2o (new -> old; null: as stored) and columns renamed by col_o2n
+static int64_t slice_lines(const std::vector<int64_t> &rp, const std::vector<int32_t> &col, int64_t n,
+                           const int32_t *row_n2o, const int32_t *col_o2n) {
+    const int64_t ns = (n + 63) / 64;
+    int64_t total = 0;
+#pragma omp parallel for schedule(dynamic, 256) reduction(+ : total)
+    for (int64_t s = 0; s < ns; s++) {
+        std::vector<int32_t> v;
+        for (int64_t i = 64 * s; i < std::min(n, 64 * s + 64); i++) {
+            const int64_t r = row_n2o ? row_n2o[i] : i;
+            for (int64_t e = rp[r]; e < rp[r + 1]; e++) v.push_back((col_o2n ? col_o2n[col[e]] : col[e]) >> 4);
+        }
+        std::sort(v.begin(), v.end());
+        total += std::unique(v.begin(), v.end()) - v.begin();
+    }
+    return total;
+}
+
+__global__ void k_perm_len(const int64_t *rp, const int32_t *rows, int64_t n, int64_t *len) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i < n) len[i] = rp[rows[i] + 1] - rp[rows[i]];
+}
+
+// one thread per new row: the original row's entries in their stored order,
+// columns renamed (col_o2n null: unchanged)
+__global__ void k_perm_copy(const int64_t *rp, const int32_t *col, const double *val, const int32_t *rows,
+                            const int32_t *col_o2n, const int64_t *rpn, int64_t n, int32_t *coln, double *valn) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    const int64_t r = rows[i], e0 = rp[r], e1 = rp[r + 1], o = rpn[i] - e0;
+    for (int64_t e = e0; e < e1; e++) {
+        coln[o + e] = col_o2n ? col_o2n[col[e]] : col[e];
+        valn[o + e] = val[e];
+    }
+}
+
+__global__ void k_gather_perm(double *out, const double *in, const int32_t *p, int64_t n) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i < n) out[i] = in[p[i]];
+}
+__global__ void k_scatter_perm(double *out, const double *in, const int32_t *p, int64_t n) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i < n) out[p[i]] = in[i];
+}
+
+void perm_gather(double *out, const double *in, const int32_t *p, int64_t n, hipStream_t s) {
+    if (n <= 0) return;
+    hipLaunchKernelGGL(k_gather_perm, dim3((unsigned)ceil_div(n, 256)), dim3(256), 0, s, out, in, p, n);
+    FAMG_CHECK_HIP(hipGetLastError());
+    log_launch("perm_gather", -1, -1, n, 20 * n);
+}
+void perm_scatter(double *out, const double *in, const int32_t *p, int64_t n, hipStream_t s) {
+    if (n <= 0) return;
+    hipLaunchKernelGGL(k_scatter_perm, dim3((unsigned)ceil_div(n, 256)), dim3(256), 0, s, out, in, p, n);
+    FAMG_CHECK_HIP(hipGetLastError());
+    log_launch("perm_scatter", -1, -1, n, 20 * n);
+}
+
+// How a storage sums a row: 0 one lane in stored order (3x3 blocks, SELL,
+// x-staged SELL), 1 a wave per row with a fixed lane split (wave-per-row), 2
+// depends on the row's neighbours (CSR-stream: the lanes per row follow the rows
+// its block holds).  A copy of the same kind sums bitwise like its original in
+// classes 0 and 1 whatever the row order, in class 2 with its rows in their
+// original order (only columns renamed: the same blocks).
+static int sum_class(const GpuCsr &m) {
+    switch (m.kernel) {
+    case SPMV_KERNEL_BSR:
+    case SPMV_KERNEL_SELL:
+    case SPMV_KERNEL_XS: return 0;
+    case SPMV_KERNEL_VECTOR: return 1;
+    default: return 2;
+    }
+}
+
+// rows in the order rows_n2o (empty: as stored), columns renamed col_o2n (empty:
+// unchanged); col_n2o = the inverse (empty: identity) for order keys
+// allow_bsr: rows and columns renumbered node by node (block size 3) or kept
+static CsrPtr csr_permuted(const CsrOp &A, const std::vector<int32_t> &rows_n2o, const std::vector<int32_t> &col_o2n,
+                           const std::vector<int32_t> &col_n2o, bool allow_bsr) {
+    Ctx *ctx = A.ctx;
+    hipStream_t s = ctx->stream;
+    const GpuCsr &m = A.m;
+    const int64_t n = m.nrows;
+    DevBuf<int32_t> drows(std::max<int64_t>(1, n)), dmap(std::max<int64_t>(1, m.ncols));
+    std::vector<int32_t> ident;
+    const std::vector<int32_t> *rows = &rows_n2o;
+    if (rows_n2o.empty()) {
+        ident.resize(n);
+        std::iota(ident.begin(), ident.end(), 0);
+        rows = &ident;
+    }
+    FAMG_CHECK_HIP(hipMemcpyAsync(drows.get(), rows->data(), n * 4, hipMemcpyHostToDevice, s));
+    if (!col_o2n.empty()) FAMG_CHECK_HIP(hipMemcpyAsync(dmap.get(), col_o2n.data(), m.ncols * 4, hipMemcpyHostToDevice, s));
+    auto P = make_csr(ctx);
+    csr_alloc(P->m, ctx, n, m.ncols, m.nnz);
+    DevBuf<int64_t> len(std::max<int64_t>(1, n));
+    if (n) hipLaunchKernelGGL(k_perm_len, dim3((unsigned)ceil_div(n, 256)), dim3(256), 0, s, m.rp64.get(), drows.get(), n, len.get());
+    FAMG_CHECK_HIP(hipGetLastError());
+    scan_counts(len.get(), P->m.rp64.get(), n, *ctx);
+    if (n)
+        hipLaunchKernelGGL(k_perm_copy, dim3((unsigned)ceil_div(n, 256)), dim3(256), 0, s, m.rp64.get(), m.col.get(),
+                           m.val.get(), drows.get(), col_o2n.empty() ? nullptr : dmap.get(), P->m.rp64.get(), n,
+                           P->m.col.get(), P->m.val.get());
+    FAMG_CHECK_HIP(hipGetLastError());
+    FAMG_CHECK_HIP(hipStreamSynchronize(s));
+    P->m.order_fixed = true;
+    P->m.col_orig = col_n2o;
+    // the copy keeps the original's kind of storage (the heuristics that chose it
+    // see other rows or other slices), so every row sums in the same order
+    P->m.no_bsr = m.no_bsr || !allow_bsr || !m.has_bsr();
+    P->m.bsr_pin = !P->m.no_bsr;
+    P->m.kind_pin = (int8_t)sum_class(m);
+    csr_finalize(P->m);
+    P->nrows = n;
+    P->ncols = m.ncols;
+    return P;
+}
+
+static std::shared_ptr<DiagOp> diag_permuted(const DiagOp &D, const std::vector<int32_t> &p) {
+    auto S = std::make_shared<DiagOp>();
+    S->ctx = D.ctx;
+    S->nrows = S->ncols = D.nrows;
+    S->d.resize(std::max<int64_t>(1, D.nrows));
+    DevBuf<int32_t> dp(std::max<int64_t>(1, D.nrows));
+    FAMG_CHECK_HIP(hipMemcpyAsync(dp.get(), p.data(), D.nrows * 4, hipMemcpyHostToDevice, D.ctx->stream));
+    if (D.nrows)
+        hipLaunchKernelGGL(k_gather_perm, dim3((unsigned)ceil_div(D.nrows, 256)), dim3(256), 0, D.ctx->stream,
+                           S->d.get(), D.d.get(), dp.get(), D.nrows);
+    FAMG_CHECK_HIP(hipGetLastError());
+    FAMG_CHECK_HIP(hipStreamSynchronize(D.ctx->stream));
+    return S;
+}
+
+// a level whose operator gathers x (no grid storage) and whose transfers carry no
+// grid-transfer overlay may be renumbered
+static bool level_reorderable(const MgLevel &L, const MgLevel *prev) {
+    auto *A = dynamic_cast<CsrOp *>(L.A.get());
+    if (!A || !dynamic_cast<DiagOp *>(L.S.get()) || A->m.nrows < 65536 || A->m.grid_src != 0 || A->m.order_fixed)
+        return false;
+    const int k = A->m.kernel;
+    if (k != SPMV_KERNEL_SELL && k != SPMV_KERNEL_BSR && k != SPMV_KERNEL_XS && k != SPMV_KERNEL_STREAM &&
+        k != SPMV_KERNEL_VECTOR)
+        return false;
+    for (const LinOp *op : {L.R.get(), L.P.get(), prev ? prev->R.get() : nullptr, prev ? prev->P.get() : nullptr}) {
+        if (!op) continue;
+        auto *c = dynamic_cast<const CsrOp *>(op);
+        if (!c || c->m.gtc_on || c->m.gtx_on || c->m.kernel == SPMV_KERNEL_SELLP) return false;
+    }
+    return true;
+}
+
+// the operators whose ROWS a renumbering of level l permutes (A_l, P_l, R_{l-1})
+// sum every row independently of its neighbours (sum_class 0 / 1); those it
+// only renames columns of (R_l, P_{l-1}) keep their rows: the renumbered cycle
+// is bitwise the original
+static bool level_bitwise(const MgLevel &L, const MgLevel *prev) {
+    for (const LinOp *op : {L.A.get(), L.P.get(), prev ? prev->R.get() : nullptr}) {
+        if (!op) continue;
+        auto *c = dynamic_cast<const CsrOp *>(op);
+        if (!c || sum_class(c->m) > 1) return false;
+    }
+    return true;
+}
+
+void MultigridOp::undo_reorder() {
+    for (auto &L : levels) {
+        if (L.oA) L.A = L.oA;
+        if (L.oS) L.S = L.oS;
+        if (L.oR) L.R = L.oR;
+        if (L.oP) L.P = L.oP;
+        L.oA = L.oS = L.oR = L.oP = nullptr;
+        L.perm.release();
+        L.permuted = false;
+    }
+    reorder_done_ = false;
+    workspace_ready_ = false;  // decided again with the workspaces
+    invalidate_graphs();
+}
+
+void MultigridOp::reorder_levels() {
+    reorder_done_ = true;
+    if (reorder == 0 || levels.size() < 2) return;
+    const size_t NL = levels.size();
+    std::vector<std::vector<int32_t>> p(NL), q(NL);  // dof new -> old, old -> new (empty: identity)
+    std::vector<int> bsl(NL, 0);                       // node size of a level's renumbering (0: none)
+    hipStream_t s = ctx->stream;
+    // coarse to fine: a level whose coarser neighbour is renumbered may take the
+    // order its aggregates induce, else reverse Cuthill-McKee -- whichever touches
+    // fewer x lines per SpMV slice
+    for (size_t l = NL - 1; l-- > 0;) {
+        if (!level_reorderable(levels[l], l > 0 ? &levels[l - 1] : nullptr)) continue;
+        // auto: only where the result stays bitwise
+        if (reorder == 1 && !level_bitwise(levels[l], l > 0 ? &levels[l - 1] : nullptr)) continue;
+        const GpuCsr &m = dynamic_cast<CsrOp *>(levels[l].A.get())->m;
+        const int64_t n = m.nrows;
+        const int bs = m.has_bsr() ? 3 : 1;
+        std::vector<int64_t> rp(n + 1);
+        std::vector<int32_t> col(std::max<int64_t>(1, m.nnz));
+        FAMG_CHECK_HIP(hipMemcpyAsync(rp.data(), m.rp64.get(), (n + 1) * 8, hipMemcpyDeviceToHost, s));
+        if (m.nnz) FAMG_CHECK_HIP(hipMemcpyAsync(col.data(), m.col.get(), m.nnz * 4, hipMemcpyDeviceToHost, s));
+        FAMG_CHECK_HIP(hipStreamSynchronize(s));
+        auto expand = [&](const std::vector<int32_t> &nodes, std::vector<int32_t> &pn, std::vector<int32_t> &qn) {
+            pn.assign(n, 0);
+            qn.assign(n, 0);
+            for (int64_t I = 0; I < (int64_t)nodes.size(); I++)
+                for (int d = 0; d < bs; d++) pn[bs * I + d] = bs * nodes[I] + d;
+            for (int64_t i = 0; i < n; i++) qn[pn[i]] = (int32_t)i;
+        };
+        std::vector<int32_t> pn, qn;
+        expand(rcm_order(rp, col, n, bs), pn, qn);
+        int64_t best = slice_lines(rp, col, n, pn.data(), qn.data());
+        auto *Pc = dynamic_cast<CsrOp *>(levels[l].P.get());
+        if (!p[l + 1].empty() && Pc && n % bs == 0) {
+            const int bsc = bsl[l + 1] > 0 ? bsl[l + 1] : 1;
+            std::vector<int32_t> pi, qi;
+            expand(induced_order(Pc->m, bs, bsc, q[l + 1]), pi, qi);
+            const int64_t li = slice_lines(rp, col, n, pi.data(), qi.data());
+            if (li < best) {
+                best = li;
+                pn.swap(pi);
+                qn.swap(qi);
+            }
+        }
+        if (reorder == 1 && 2 * best > slice_lines(rp, col, n, nullptr, nullptr)) continue;  // at least halve them
+        p[l] = std::move(pn);
+        q[l] = std::move(qn);
+        bsl[l] = bs;
+    }
+    bool any = false;
+    for (auto &v : p) any = any || !v.empty();
+    if (!any) return;
+    for (size_t l = 0; l < NL; l++) {
+        MgLevel &L = levels[l];
+        const bool pl = !p[l].empty(), pc = l + 1 < NL && !p[l + 1].empty();
+        if (pl) {
+            L.oA = L.A;
+            L.oS = L.S;
+            L.A = csr_permuted(*dynamic_cast<CsrOp *>(L.oA.get()), p[l], q[l], p[l], bsl[l] != 1);
+            L.S = diag_permuted(*dynamic_cast<DiagOp *>(L.oS.get()), p[l]);
+            L.permuted = true;
+            L.perm.resize(std::max<size_t>(1, p[l].size()));
+            FAMG_CHECK_HIP(hipMemcpyAsync(L.perm.get(), p[l].data(), p[l].size() * 4, hipMemcpyHostToDevice, s));
+        }
+        if (l + 1 < NL && (pl || pc)) {
+            L.oR = L.R;
+            L.oP = L.P;
+            // R_l: coarse rows in level l + 1's order, fine columns renamed; P_l the converse
+            const bool blk = bsl[l] != 1 && bsl[l + 1] != 1;
+            L.R = csr_permuted(*dynamic_cast<CsrOp *>(L.oR.get()), p[l + 1], q[l], p[l], blk);
+            L.P = csr_permuted(*dynamic_cast<CsrOp *>(L.oP.get()), p[l], q[l + 1], p[l + 1], blk);
+        }
+    }
+    FAMG_CHECK_HIP(hipStreamSynchronize(s));
+    if (reorder == 1) {  // a copy whose storage did not follow its original's: back out
+        bool same = true;
+        for (auto &L : levels)
+            for (auto pr : {std::make_pair(L.oA, L.A), std::make_pair(L.oR, L.R), std::make_pair(L.oP, L.P)}) {
+                if (!pr.first) continue;
+                same = same && sum_class(dynamic_cast<CsrOp *>(pr.first.get())->m) ==
+                                   sum_class(dynamic_cast<CsrOp *>(pr.second.get())->m);
+            }
+        if (!same) {
+            undo_reorder();
+            reorder_done_ = true;  // (ensure_workspace goes on to build the workspaces)
+            return;
+        }
+    }
+    if (levels[0].permuted) {
+        const int64_t n = levels[0].A->nrows;
+        perm_f0_.resize(std::max<int64_t>(1, n));
+        perm_v0_.resize(std::max<int64_t>(1, n));
+    }
+}
+
+// a view with the operators the caller added (the distributed build partitions those)
+std::shared_ptr<MultigridOp> MultigridOp::original_view() {
+    auto v = std::make_shared<MultigridOp>();
+    v->ctx = ctx;
+    v->nrows = nrows;
+    v->ncols = ncols;
+    v->mu = mu;
+    v->steps = steps;
+    v->use_graph = use_graph;
+    v->sgs_residual_form = sgs_residual_form;
+    v->fold_zero_guess = fold_zero_guess;
+    v->fuse_transfers = fuse_transfers;
+    v->restrict_df = restrict_df;
+    v->reorder = reorder;
+    for (auto &L : levels) {
+        MgLevel M;
+        M.A = L.oA ? L.oA : L.A;
+        M.S = L.oS ? L.oS : L.S;
+        M.R = L.oR ? L.oR : L.R;
+        M.P = L.oP ? L.oP : L.P;
+        v->levels.push_back(std::move(M));
+    }
+    return v;
+}
+
+}  // namespace famg

@@ -2155,7 +2155,7 @@ void build_sell(GpuCsr &m, const std::vector<int64_t> &rp) {
     m.sell_short = false;
     m.seg_slc.clear();
     const int pol = g_spmv_format_policy;
-    if (pol == 1 || pol == 3 || m.nrows == 0 || m.nnz == 0) return;
+    if (pol == 1 || pol == 3 || m.kind_pin >= 1 || m.nrows == 0 || m.nnz == 0) return;
     // slices never straddle a segment
     std::vector<int32_t> row0;
     std::vector<int64_t> seg_slc{0};
@@ -2176,7 +2176,8 @@ void build_sell(GpuCsr &m, const std::vector<int64_t> &rp) {
     int64_t dseg = 0;
     for (size_t g = 1; g + 1 < m.seg_rows.size(); g++)
         if (m.seg_rows[g + 1] - m.seg_rows[g] > m.seg_rows[dseg + 1] - m.seg_rows[dseg]) dseg = (int64_t)g;
-    if (build_dia(m, vb, tab, rp, m.seg_rows[dseg], m.seg_rows[dseg + 1])) {
+    // (a renumbered copy, reorder.hip, keeps its rows' stored order: no DIA, no aligned slices)
+    if (!m.order_fixed && build_dia(m, vb, tab, rp, m.seg_rows[dseg], m.seg_rows[dseg + 1])) {
         m.dia_seg = dseg;
         if (m.dia_r0 == 0 && m.dia_r1 == m.nrows) return;
     }
@@ -2197,7 +2198,7 @@ void build_sell(GpuCsr &m, const std::vector<int64_t> &rp) {
     int64_t bytes = 0, steps = 0, cnt[3] = {0, 0, 0};
     for (int64_t k = 0; k < ns; k++) {
         const int wa = plan[4 * k], ma = plan[4 * k + 1], wp = plan[4 * k + 2], mp = plan[4 * k + 3];
-        const bool al = wa >= 0 && sell_slice_bytes(wa, ma, vb) <= sell_slice_bytes(wp, mp, vb);
+        const bool al = !m.order_fixed && wa >= 0 && sell_slice_bytes(wa, ma, vb) <= sell_slice_bytes(wp, mp, vb);
         const int w = al ? wa : wp, md = al ? ma : mp;
         aligned[k] = al;
         if (bytes / 128 >= (int64_t(1) << 30) || steps + w >= (int64_t(1) << 31)) return;
@@ -2210,7 +2211,7 @@ void build_sell(GpuCsr &m, const std::vector<int64_t> &rp) {
     // auto: SELL pays when there are enough slices to fill the chip (>= 1024
     // slices = 64K rows) and it streams no more than 1.25x the CSR bytes;
     // measured on the 256^3 hierarchy (scripts/ab_levels.py).
-    const bool ok = pol == 2 || (bytes * 100 <= 12 * m.nnz * 125 && (m.nrows >= SELL_MIN_ROWS || maxlen <= 16) &&
+    const bool ok = pol == 2 || m.kind_pin == 0 || (bytes * 100 <= 12 * m.nnz * 125 && (m.nrows >= SELL_MIN_ROWS || maxlen <= 16) &&
                                  (vec_min_avg() >= VECTOR_MIN_AVG || m.nnz < vec_min_avg() * m.nrows));
     if (!ok) return;
     m.sell_row0 = std::move(drow0);
@@ -2328,6 +2329,12 @@ static int vec_waves_per_row(int64_t rows, int64_t nnz);
 void choose_kernel(GpuCsr &m) {
     if (m.has_dia() && !m.dia_rowid && m.dia_r0 == 0 && m.dia_r1 == m.nrows) m.kernel = SPMV_KERNEL_DIA;
     else if (m.has_bsr()) m.kernel = SPMV_KERNEL_BSR;
+    else if (m.kind_pin == 1) {  // a renumbered copy of a wave-per-row matrix (reorder.hip)
+        m.kernel = SPMV_KERNEL_VECTOR;
+        m.vec_wpr = vec_waves_per_row(m.nrows, m.nnz);
+        build_vec_codes(m);
+    }
+    else if (m.kind_pin == 2) m.kernel = SPMV_KERNEL_STREAM;
     else if (m.has_scs() && m.scs_seg < 0) m.kernel = SPMV_KERNEL_SCS;
     else if (m.has_sellp()) m.kernel = SPMV_KERNEL_SELLP;
     else if (m.has_xs()) m.kernel = SPMV_KERNEL_XS;

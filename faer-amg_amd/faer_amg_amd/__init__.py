@@ -98,6 +98,7 @@ SIGNATURES = {
     "amg_grid_from_offsets": (i32, [vp, i64, i64, vp, P(i32)]),
     "amg_set_flag": (i32, [i32, i64]),
     "amg_source_hash": (C.c_char_p, []),
+    "amg_multigrid_level_reordered": (i32, [vp, i64, P(i32)]),
     "amg_get_flag": (i32, [i32, P(i64)]),
     "amg_gen_laplace3d_7pt": (i32, [vp, i64, i64, i64, P(vp)]),
     "amg_gen_aniso27": (i32, [vp, i64, i64, i64, dbl, dbl, dbl, P(vp)]),
@@ -492,7 +493,8 @@ class SparseMatOp(LinOp):
         "resid" y = b - A x, "jacobi" y = x + d (b - A x)."""
         m = {"set": 0, "add": 1, "resid": 2, "jacobi": 3}[mode]
         ptr = lambda t: None if t is None else vp(t.data_ptr())  # noqa: E731
-        _ck(_lib.amg_csr_spmv_epilogue(self.h, m, ptr(x), ptr(y), ptr(b), ptr(d)))
+        with _ordered(self.ctx, AMG_MEM_DEVICE):  # y / b / d written on torch's stream
+            _ck(_lib.amg_csr_spmv_epilogue(self.h, m, ptr(x), ptr(y), ptr(b), ptr(d)))
 
     def set_grid(self, nx, ny, nz):
         """Grid hint (amg_csr_set_grid): the rows are an nx x ny x nz grid; re-finalizes the storage."""
@@ -514,7 +516,8 @@ class SparseMatOp(LinOp):
         return sp.csr_matrix((va, ci, rp), shape=self.dims())
 
 
-FLAGS = {"fold_xscs": 0, "dia_dk": 1, "vec_wpr": 2, "gtx_time": 3, "sgs27_march": 4, "xs_pipe": 5, "bsr_kernel": 6}
+FLAGS = {"fold_xscs": 0, "dia_dk": 1, "vec_wpr": 2, "gtx_time": 3, "sgs27_march": 4, "xs_pipe": 5, "bsr_kernel": 6,
+         "bsr_long": 7}
 
 
 def set_flag(name, value):
@@ -649,6 +652,16 @@ class Multigrid(LinOp):
     def set_graph(self, enable):
         _ck(_lib.amg_multigrid_set_graph(self.h, 1 if enable else 0))
 
+    def set_reorder(self, mode):
+        """Locality reordering of general levels (multigrid option 5): 0 off, 1 auto, 2 force."""
+        _ck(_lib.amg_multigrid_set_option(self.h, 5, int(mode)))
+
+    def reordered(self, l):
+        """Whether level l runs in a renumbered (reverse Cuthill-McKee) numbering."""
+        v = i32()
+        _ck(_lib.amg_multigrid_level_reordered(self.h, l, C.byref(v)))
+        return bool(v.value)
+
     def set_sgs_residual_form(self, enable):
         """Literal smooth() order for SGS (residual SpMV + SGS(r)) instead of the fused sweep."""
         _ck(_lib.amg_multigrid_set_option(self.h, 1, 1 if enable else 0))
@@ -663,8 +676,9 @@ class Multigrid(LinOp):
         Returns False when the level has no such fused launch."""
         ptr = lambda t: None if t is None else vp(t.data_ptr())  # noqa: E731
         ok = i32()
-        _ck(_lib.amg_multigrid_fused_transfer(self.h, level, {"restrict": 0, "interp": 1}[which], ptr(a), ptr(b),
-                                              ptr(x), ptr(out), C.byref(ok)))
+        with _ordered(self.ctx, AMG_MEM_DEVICE):
+            _ck(_lib.amg_multigrid_fused_transfer(self.h, level, {"restrict": 0, "interp": 1}[which], ptr(a),
+                                                  ptr(b), ptr(x), ptr(out), C.byref(ok)))
         return bool(ok.value)
 
     def set_restrict_df(self, enable):

@@ -127,7 +127,10 @@ amg_status amg_set_alloc_policy(int32_t policy);
  * batches, 0 = the round-4 kernel (env FAMG_XS_PIPE), 6 = 3x3-block SpMV kernel
  * (bsr.hip): 0 = the round-2 kernel (default), 1 = node columns first, 4-step
  * batches, 2 = columns first, 2-step batches pipelined, 3 = 4-step pipelined
- * (env FAMG_BSR_KERNEL).  Setting one
+ * (env FAMG_BSR_KERNEL), 7 = 3x3-block matrices whose slices (64 node rows)
+ * average at least this many block steps take the long-row kernel that loads
+ * the next 8 steps' node columns ahead (default 16, env FAMG_BSR_LONG; -1
+ * never).  Setting one
  * makes every multigrid re-capture its hipGraph at its next apply.  amg_get_flag
  * reads the current value. */
 amg_status amg_set_flag(int32_t which, int64_t value);
@@ -312,6 +315,16 @@ amg_status amg_multigrid_set_graph(amg_linop *mg, int32_t enable);
  * next level's first Jacobi step from zero, d_c f_c, beside f_c (SPMV_SETDF)
  * instead of a separate pass (default 1; bitwise identical). */
 amg_status amg_multigrid_set_option(amg_linop *mg, int32_t option, int64_t value);
+/* Multigrid option 5 -- locality reordering (reorder.hip; no reference
+ * counterpart, results bitwise unchanged): the cycle runs a level of a general
+ * operator (no grid storage, a diagonal smoother, >= 65536 rows) in a reverse
+ * Cuthill-McKee numbering of its node graph -- renumbered copies of A_l, its
+ * diagonal, R_l and P_l whose rows keep their stored entry order -- with one
+ * gather of rhs and one scatter of the result per apply when the fine level is
+ * renumbered.  0 off, 1 (default) where it at least halves the x cache lines an
+ * SpMV slice of 64 rows touches, 2 every eligible level.  amg_multigrid_get_level
+ * returns the caller's operators; *reordered = 1 when level runs renumbered. */
+amg_status amg_multigrid_level_reordered(amg_linop *mg, int64_t level, int32_t *reordered);
 /* One fused grid transfer of level l on device vectors (test hook; *applied = 0
  * when the level has none): which 0 -- out (coarse) = R (a - A x), x = the
  * iterate, or NULL for the folded zero-guess iterate d*a; which 1 -- out (fine)
@@ -353,8 +366,8 @@ amg_status amg_multigrid_cycle_plan(amg_linop *mg, amg_launch_rec *recs, int64_t
  * level = global level index (the redundant tail's levels after the
  * distributed ones), rows = this rank's rows. */
 amg_status amg_dist_cycle_plan(amg_linop *dist, amg_launch_rec *recs, int64_t cap, int64_t *count);
-/* The first 16 hex digits of sha256 over the library's sources (csrc/*.hip,
- * *.cpp, *.hpp, *.inc in sorted order, then this header) it was built from: the
+/* The first 16 hex digits of sha256 over the library's sources (the .hip,
+ * .cpp, .hpp and .inc files of csrc in sorted order, then this header) it was built from: the
  * Python package and __graft_entry__.build() compare it with the tree and
  * refuse / rebuild a stale prebuilt library. */
 const char *amg_source_hash(void);

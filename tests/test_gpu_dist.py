@@ -527,14 +527,12 @@ def slab_run(nranks, dims, coarsest, agglo, b, overlap=True, gtx_time=0):
         splits = fa().slab_splits(fa().box_level_dims(dims, (2, 2, 2), nl), nranks)
         comm = fa().Comm(ctx, hub=hub, rank=r)
         dm = fa().DistMultigrid(comm, mg, splits, agglomerate_rows=agglo).set_overlap(overlap)
-        dm.set_per_colour_halo(per_colour)
         r0, r1 = dm.local_rows()
         bl = torch.as_tensor(np.ascontiguousarray(b[r0:r1]), device="cuda:0")
         zl = torch.empty_like(bl)
         dm.apply(zl, bl)
         ctx.synchronize()
         infos = [dm.level_info(l) for l in range(nl)]
-        cplan = dm.cycle_plan() if plan else None
         La = sum(1 for i in infos if i["redundant"] == 0)
         local = [tuple(_kinds(dm.level_matrix(l, w).spmv_info()) for w in ("A", "R", "P")) for l in range(La)]
         glob = [tuple(_kinds(M.spmv_info()) if M is not None else None for M in (lv[0], lv[2], lv[3]))

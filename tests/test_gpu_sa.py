@@ -245,16 +245,20 @@ def test_bsr_storage_bitwise(ctx, gap):
     b0 = np.random.default_rng(8).standard_normal(S.shape[0])
     d0 = np.random.default_rng(9).uniform(0.1, 0.2, S.shape[0])
     bd, dd = torch.as_tensor(b0, device="cuda:0"), torch.as_tensor(d0, device="cuda:0")
+    # (bsr_long: the prefetching long-row kernel for slices averaging at least that
+    # many block steps -- 0 always, -1 never)
     try:
-        for k in (0, 1, 2, 3):
+        for k, split in ((0, -1), (1, -1), (2, -1), (3, -1), (0, 0)):
             fa().set_flag("bsr_kernel", k)
+            fa().set_flag("bsr_long", split)
             for mode, ref in (("set", ax), ("add", 0.5 + ax), ("resid", b0 - ax), ("jacobi", x + d0 * (b0 - ax))):
                 yk = torch.full_like(xd, 0.5)
                 A.spmv_epilogue(mode, xd, yk, bd, dd)
                 ctx.synchronize()
-                assert np.array_equal(yk.cpu().numpy().view(np.int64), ref.view(np.int64)), (k, mode)
+                assert np.array_equal(yk.cpu().numpy().view(np.int64), ref.view(np.int64)), (k, split, mode)
     finally:
         fa().set_flag("bsr_kernel", 0)
+        fa().set_flag("bsr_long", 16)
     nn = fa().constant_candidates(S.shape[0], 3)
     w = weights(S, nn)
     mg = fa().smoothed_aggregation(A, nn, weights=w, block_size=3, candidate_dimension=3, coarsest_dim=150,
@@ -311,3 +315,72 @@ def test_strength_depth3_block3_and_vcycle(ctx):
     mg.apply(z, bd)
     ctx.synchronize()
     assert np.linalg.norm(z.cpu().numpy() - zref) <= 1e-11 * np.linalg.norm(zref)
+
+
+def _reorder_runs(ctx, e, modes):
+    """elasticity stand-in with shuffled nodes, e^3 elements: z = M b and an
+    11-cycle stationary history per reorder mode"""
+    import torch
+    H = fa().elasticity_q1((e, e, e), seed=3, permute=True)
+    A, S = H.upload(ctx), H.to_scipy()
+    nn = fa().constant_candidates(S.shape[0], 3)
+    mg = fa().smoothed_aggregation(A, nn, weights=weights(S, nn), block_size=3, candidate_dimension=3,
+                                   coarsest_dim=150, smoother="l1")
+    b = torch.as_tensor(np.random.default_rng(31).uniform(-1, 1, S.shape[0]), device="cuda:0")
+    out = {}
+    for mode in modes:
+        mg.set_reorder(mode)
+        z = torch.empty_like(b)
+        mg.apply(z, b)
+        x = torch.zeros_like(b)
+        _, hist = fa().stationary_solve(A, mg, b, x, max_iter=11, rel_tol=1e-300)
+        ctx.synchronize()
+        out[mode] = {"z": z.cpu().numpy(), "hist": np.asarray(hist), "plan": mg.cycle_plan(),
+                     "reordered": [mg.reordered(l) for l in range(mg.levels())]}
+    return mg, b, out
+
+
+def _renumbered_plan_ok(plan, n, mg):
+    names = [p["name"] for p in plan]
+    assert names[0] == "perm_gather" and names[-1] == "perm_scatter", names
+    assert any(p["name"] == "bsr3" and p["level"] == 0 for p in plan), names
+    assert mg.level(0)[0].nrows == n and mg.level(0)[0].spmv_info()["kernel"] == "bsr"
+
+
+def test_locality_reordering_bitwise(ctx):
+    """Locality reordering (multigrid option 5, reorder.hip): a general operator
+    with its nodes shuffled (elasticity stand-in, 3x3 blocks) runs its eligible
+    levels in a locality numbering (reverse Cuthill-McKee, or nodes grouped by
+    aggregate in the coarse level's order) -- renumbered copies of A_l, the L1
+    diagonal, R_l, P_l with every row's entries in their original order and the
+    original's kind of storage, one gather of rhs and one scatter of z per apply.
+    56^3 elements (546K rows; A_0, P_0 3x3-block): the auto rule renumbers the
+    fine level and the cycle and 10 stationary cycles are bitwise those of the
+    unrenumbered cycle.  30^3 (89K rows): P_0 takes CSR-stream, whose lanes per
+    row follow the rows of its block, so auto leaves the level alone (bitwise by
+    doing nothing), while the forced mode renumbers it and agrees to rounding.
+    The operators the multigrid hands back are the caller's (oracle parity).  A
+    grid operator's levels (C2-like) are never renumbered."""
+    mg, b, out = _reorder_runs(ctx, 56, (0, 1))
+    assert not any(out[0]["reordered"]) and out[1]["reordered"][0]
+    _renumbered_plan_ok(out[1]["plan"], b.numel(), mg)
+    assert np.array_equal(out[1]["z"].view(np.int64), out[0]["z"].view(np.int64))
+    assert np.array_equal(out[1]["hist"], out[0]["hist"])
+    del mg, out
+    mg, b, out = _reorder_runs(ctx, 30, (0, 2, 1))
+    assert not any(out[0]["reordered"]) and not any(out[1]["reordered"]) and out[2]["reordered"][0]
+    assert [p["name"] for p in out[0]["plan"] if p["level"] == 0 and p["role"] == "interp"] == ["csr-stream"]
+    _renumbered_plan_ok(out[2]["plan"], b.numel(), mg)
+    assert np.array_equal(out[1]["z"].view(np.int64), out[0]["z"].view(np.int64))
+    z0 = out[0]["z"]
+    assert np.linalg.norm(out[2]["z"] - z0) <= 1e-14 * np.linalg.norm(z0)
+    assert np.allclose(out[2]["hist"], out[0]["hist"], rtol=1e-10, atol=0)
+    # the handed-back operators are the caller's: the oracle on them matches
+    levels = oracle_levels(mg, "l1")
+    zref = O.Multigrid(levels).apply(b.cpu().numpy())
+    assert np.linalg.norm(out[2]["z"] - zref) <= 1e-11 * np.linalg.norm(zref)
+    # a grid operator: nothing to renumber
+    dims = (64, 64, 64)
+    G = fa().SparseMatOp.laplace3d_7pt(ctx, *dims)
+    mgg = fa().sa_build_box(G, dims, (2, 2, 2), coarsest_dim=500)
+    assert not any(mgg.reordered(l) for l in range(mgg.levels()))
