@@ -110,7 +110,8 @@ static std::atomic<int64_t> g_flag_val[FLAG_COUNT] = {
     {[] { const char *e = getenv("FAMG_SGS27_MARCH"); return (int64_t)(e ? atoi(e) : 1); }()},
     {[] { const char *e = getenv("FAMG_XS_PIPE"); return (int64_t)(e ? atoi(e) : 2); }()},
     {[] { const char *e = getenv("FAMG_BSR_KERNEL"); return (int64_t)(e ? atoi(e) : 0); }()},
-    {[] { const char *e = getenv("FAMG_BSR_LONG"); return (int64_t)(e ? atoll(e) : 16); }()}};
+    {[] { const char *e = getenv("FAMG_BSR_LONG"); return (int64_t)(e ? atoll(e) : 16); }()},
+    {[] { const char *e = getenv("FAMG_DIA7_RP"); return (int64_t)(e ? atoi(e) : 0); }()}};
 static std::atomic<uint64_t> g_flag_gen{0};
 int64_t flag(FlagId f) { return g_flag_val[f].load(std::memory_order_relaxed); }
 void set_flag(FlagId f, int64_t v) {
@@ -361,6 +362,9 @@ amg_status amg_csr_set_grid(amg_linop *op, int64_t nx, int64_t ny, int64_t nz) {
 amg_status amg_set_flag(int32_t which, int64_t value) {
     return guard([&] {
         FAMG_REQUIRE(which >= 0 && which < FLAG_COUNT, AMG_ERR_INVALID, "unknown flag");
+        if (which == FLAG_DIA7_RP)
+            FAMG_REQUIRE(value == 0 || value == 1 || value == 2 || value == 4, AMG_ERR_INVALID,
+                         "row pairs per lane must be 0 (auto), 1, 2 or 4");
         if (which == FLAG_VEC_WPR)
             FAMG_REQUIRE(value == 0 || value == 1 || value == 2 || value == 4, AMG_ERR_INVALID,
                          "waves per row must be 0 (auto), 1, 2 or 4");
@@ -805,6 +809,21 @@ amg_status amg_multigrid_get_level(const amg_linop *mg, int64_t level, amg_linop
         if (S) *S = box(L.origS());
         if (R) *R = L.origR() ? box(L.origR()) : nullptr;
         if (P) *P = L.origP() ? box(L.origP()) : nullptr;
+    });
+}
+
+amg_status amg_multigrid_get_run_level(amg_linop *mg, int64_t level, amg_linop **A, amg_linop **S, amg_linop **R,
+                                       amg_linop **P) {
+    return guard([&] {
+        auto m = need_mg(mg);
+        std::lock_guard<std::mutex> lk(m->mtx);
+        FAMG_REQUIRE(level >= 0 && level < (int64_t)m->levels.size(), AMG_ERR_INVALID, "level out of range");
+        m->ensure_workspace();  // the renumbering is decided with the workspaces
+        const MgLevel &L = m->levels[level];
+        if (A) *A = box(L.A);
+        if (S) *S = box(L.S);
+        if (R) *R = L.R ? box(L.R) : nullptr;
+        if (P) *P = L.P ? box(L.P) : nullptr;
     });
 }
 

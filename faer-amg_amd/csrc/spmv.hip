@@ -1310,6 +1310,66 @@ __global__ __launch_bounds__(256) void spmv_dia_kernel(DiaArgs a) {
     ep.store(a.e, sdt, acc0, acc1);
 }
 
+// The constant 7-point kernel (CST above) with RP row pairs per lane (FLAG_DIA7_RP:
+// 0 auto = 2 for SET, or 2 / 4): a workgroup covers RP adjacent 512-row blocks and issues every load
+// of all its row pairs before the first sum -- RP times the bytes in flight per
+// wave, fewer and longer-lived workgroups.  Same sums and epilogues, bitwise.
+// (Coded-diagonal epilogues, which stage a table in LDS, stay on the kernel above.)
+template <int MODE, int RP>
+__global__ __launch_bounds__(256) void spmv_dia7c_kernel(DiaArgs a) {
+    constexpr bool JK = MODE == DIA_JACOBI_DK, RK = MODE == DIA_RESID0_DK;
+    constexpr int GM = JK ? SPMV_JACOBI : RK ? SPMV_SET : MODE;
+    int blk;
+    if (a.band_bp > 0) {  // the 2.5-D band order in units of RP blocks
+        const int bp = a.band_bp / RP, bb = bp >> 3, x = blockIdx.x & 7, i = blockIdx.x >> 3;
+        blk = (i / bb) * bp + x * bb + (i % bb);
+    } else {
+        blk = xcd_remap(blockIdx.x, gridDim.x);
+    }
+    DiaEpi<MODE, false> ep[RP];
+    double xs7[RP][4][2], xq[RP][4];
+    int row[RP];
+#pragma unroll
+    for (int p = 0; p < RP; p++) {
+        row[p] = a.row_begin + 512 * (RP * blk + p) + 2 * (int)threadIdx.x;
+        ep[p].load(a.e, row[p], a.row_end);
+        dia_gx2<GM>(a.e, row[p] + a.off[0], a.ncols, xs7[p][0][0], xs7[p][0][1]);
+        dia_gx2<GM>(a.e, row[p] + a.off[1], a.ncols, xs7[p][1][0], xs7[p][1][1]);
+        dia_gx4<GM>(a.e, row[p] + a.off[2], a.ncols, xq[p]);
+        dia_gx2<GM>(a.e, row[p] + a.off[5], a.ncols, xs7[p][2][0], xs7[p][2][1]);
+        dia_gx2<GM>(a.e, row[p] + a.off[6], a.ncols, xs7[p][3][0], xs7[p][3][1]);
+    }
+#pragma unroll
+    for (int p = 0; p < RP; p++) {
+        if (row[p] >= a.row_end) break;  // the row pairs ascend
+        if constexpr (RK) {
+            const double dk = a.e.dk;
+#pragma unroll
+            for (int i = 0; i < 4; i++)
+#pragma unroll
+                for (int j = 0; j < 2; j++) xs7[p][i][j] = dk * xs7[p][i][j];
+#pragma unroll
+            for (int j = 0; j < 4; j++) xq[p][j] = dk * xq[p][j];
+        }
+        if constexpr (JK) ep[p].dr = dbl2_t{a.e.dk, a.e.dk};
+        const int q = row[p] / a.gnx, gx = row[p] - q * a.gnx;
+        const int gz = q / a.gny, gy = q - gz * a.gny;
+        const bool zlo = gz > 0, ylo = gy > 0, yhi = gy < a.gny - 1, zhi = gz < a.gnz - 1;
+        const bool xlo = gx > 0, xhi = gx + 2 < a.gnx;
+        double acc0 = 0.0, acc1 = 0.0;
+#pragma unroll
+        for (int k = 0; k < 7; k++) {
+            const double y0 = k < 2 ? xs7[p][k][0] : k < 5 ? xq[p][k - 2] : xs7[p][k - 3][0];
+            const double y1 = k < 2 ? xs7[p][k][1] : k < 5 ? xq[p][k - 1] : xs7[p][k - 3][1];
+            const bool in = k == 0 ? zlo : k == 1 ? ylo : k == 5 ? yhi : k == 6 ? zhi : true;
+            const bool in0 = in && (k != 2 || xlo), in1 = in && (k != 4 || xhi);
+            acc0 = fma(a.cst[k], in0 ? y0 : 0.0, acc0);
+            acc1 = fma(a.cst[k], in1 ? y1 : 0.0, acc1);
+        }
+        ep[p].store(a.e, nullptr, acc0, acc1);
+    }
+}
+
 // Run patterns of longer stencils (more than 32 diagonals): the lengths of the
 // runs of consecutive offsets, ascending.  PAT 33: the Galerkin operator of
 // smoothed aggregation on 2^3 boxes of the 7-point operator (A_1 of the C2
@@ -2413,6 +2473,19 @@ template <int M, int VB, int CW>
 static void launch_dia(int runs, bool nt, dim3 grid, dim3 block, hipStream_t s, const DiaArgs &a, bool cst = false) {
     if constexpr (CW * 32 / VB >= 7) {
         if (runs == -1 && cst) {  // constant 7-point stencil: no codes
+            if constexpr (M != DIA_JACOBI_DC && M != DIA_RESID0_DC) {
+                // auto (0): two pairs for SET (the solve loops' operator apply: 52.3 -> 49.0 us on
+                // 256^3), one for the cycle's RESID0 / JACOBI (in-cycle 65.9 -> 74.3 and
+                // 84.6 -> 89.4 us with two: profiles/r05/ab_dia7_rp.txt)
+                int rp = (int)flag(FLAG_DIA7_RP);
+                if (rp == 0) rp = M == SPMV_SET ? 2 : 1;
+                if (rp > 1 && (a.band_bp == 0 || a.band_bp % (8 * rp) == 0)) {
+                    const dim3 g((unsigned)ceil_div((int64_t)grid.x, rp));
+                    if (rp == 2) spmv_dia7c_kernel<M, 2><<<g, block, 0, s>>>(a);
+                    else spmv_dia7c_kernel<M, 4><<<g, block, 0, s>>>(a);
+                    return;
+                }
+            }
             spmv_dia_kernel<M, VB, CW, false, -1, true><<<grid, block, 0, s>>>(a);
             return;
         }

@@ -99,6 +99,7 @@ SIGNATURES = {
     "amg_set_flag": (i32, [i32, i64]),
     "amg_source_hash": (C.c_char_p, []),
     "amg_multigrid_level_reordered": (i32, [vp, i64, P(i32)]),
+    "amg_multigrid_get_run_level": (i32, [vp, i64, P(vp), P(vp), P(vp), P(vp)]),
     "amg_get_flag": (i32, [i32, P(i64)]),
     "amg_gen_laplace3d_7pt": (i32, [vp, i64, i64, i64, P(vp)]),
     "amg_gen_aniso27": (i32, [vp, i64, i64, i64, dbl, dbl, dbl, P(vp)]),
@@ -517,7 +518,8 @@ class SparseMatOp(LinOp):
 
 
 FLAGS = {"fold_xscs": 0, "dia_dk": 1, "vec_wpr": 2, "gtx_time": 3, "sgs27_march": 4, "xs_pipe": 5, "bsr_kernel": 6,
-         "bsr_long": 7}
+         "bsr_long": 7,
+         "dia7_rp": 8}
 
 
 def set_flag(name, value):
@@ -656,8 +658,16 @@ class Multigrid(LinOp):
         """Locality reordering of general levels (multigrid option 5): 0 off, 1 auto, 2 force."""
         _ck(_lib.amg_multigrid_set_option(self.h, 5, int(mode)))
 
+    def run_level(self, l):
+        """(A, S, R, P) the cycle runs on level l: the renumbered copies of a renumbered level."""
+        a, s, r, p = vp(), vp(), vp(), vp()
+        _ck(_lib.amg_multigrid_get_run_level(self.h, l, C.byref(a), C.byref(s), C.byref(r), C.byref(p)))
+        return (SparseMatOp(a, self.ctx), LinOp(s, self.ctx),
+                SparseMatOp(r, self.ctx) if r.value else None,
+                SparseMatOp(p, self.ctx) if p.value else None)
+
     def reordered(self, l):
-        """Whether level l runs in a renumbered (reverse Cuthill-McKee) numbering."""
+        """Whether level l runs in a renumbered (locality) numbering."""
         v = i32()
         _ck(_lib.amg_multigrid_level_reordered(self.h, l, C.byref(v)))
         return bool(v.value)

@@ -130,7 +130,9 @@ amg_status amg_set_alloc_policy(int32_t policy);
  * (env FAMG_BSR_KERNEL), 7 = 3x3-block matrices whose slices (64 node rows)
  * average at least this many block steps take the long-row kernel that loads
  * the next 8 steps' node columns ahead (default 16, env FAMG_BSR_LONG; -1
- * never).  Setting one
+ * never), 8 = row pairs per lane of the constant 7-point DIA kernel: 0 auto
+ * (default: 2 for SET, 1 for the cycle's epilogues), 1, 2 or 4 adjacent 512-row
+ * blocks per workgroup (env FAMG_DIA7_RP).  Setting one
  * makes every multigrid re-capture its hipGraph at its next apply.  amg_get_flag
  * reads the current value. */
 amg_status amg_set_flag(int32_t which, int64_t value);
@@ -316,15 +318,22 @@ amg_status amg_multigrid_set_graph(amg_linop *mg, int32_t enable);
  * instead of a separate pass (default 1; bitwise identical). */
 amg_status amg_multigrid_set_option(amg_linop *mg, int32_t option, int64_t value);
 /* Multigrid option 5 -- locality reordering (reorder.hip; no reference
- * counterpart, results bitwise unchanged): the cycle runs a level of a general
- * operator (no grid storage, a diagonal smoother, >= 65536 rows) in a reverse
- * Cuthill-McKee numbering of its node graph -- renumbered copies of A_l, its
- * diagonal, R_l and P_l whose rows keep their stored entry order -- with one
- * gather of rhs and one scatter of the result per apply when the fine level is
- * renumbered.  0 off, 1 (default) where it at least halves the x cache lines an
- * SpMV slice of 64 rows touches, 2 every eligible level.  amg_multigrid_get_level
- * returns the caller's operators; *reordered = 1 when level runs renumbered. */
+ * counterpart): the cycle runs a level of a general operator (no grid storage,
+ * a diagonal smoother, >= 65536 rows) in a locality numbering of its node graph
+ * (its nodes grouped by aggregate in the renumbered coarse level's order, or
+ * reverse Cuthill-McKee, whichever touches fewer x cache lines) -- renumbered
+ * copies of A_l, its diagonal, R_l and P_l whose rows keep their stored entry
+ * order and their original's kind of storage -- with one gather of rhs and one
+ * scatter of the result per apply when the fine level is renumbered.  0 off,
+ * 1 (default) where the result stays bitwise (every operator whose rows move
+ * sums a row independently of its neighbours) and it at least halves the x
+ * cache lines an SpMV slice of 64 rows touches, 2 every eligible level (equal
+ * to rounding).  amg_multigrid_get_level returns the caller's operators,
+ * amg_multigrid_get_run_level the ones the cycle runs (the renumbered copies of
+ * a renumbered level); *reordered = 1 when level runs renumbered. */
 amg_status amg_multigrid_level_reordered(amg_linop *mg, int64_t level, int32_t *reordered);
+amg_status amg_multigrid_get_run_level(amg_linop *mg, int64_t level, amg_linop **A, amg_linop **S,
+                                       amg_linop **R, amg_linop **P);
 /* One fused grid transfer of level l on device vectors (test hook; *applied = 0
  * when the level has none): which 0 -- out (coarse) = R (a - A x), x = the
  * iterate, or NULL for the folded zero-guess iterate d*a; which 1 -- out (fine)

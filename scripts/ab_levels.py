@@ -1,4 +1,5 @@
-"""A/B of the SpMV kernels on every operator of the 256^3 SA hierarchy.
+"""A/B of the SpMV kernels on every operator of the 256^3 SA hierarchy (and the
+storage the cycle runs, "cycle").
 
 For each level l >= 1 (and the fine P/R), the operator is re-uploaded under each
 storage policy (csr-stream / vector / sell) and y = M x is timed with HIP
@@ -49,6 +50,7 @@ for l in range(mg.levels() - 1):
             ops[fmt] = fa.SparseMatOp.from_arrays(ctx, m, n, *arrs)
         fa.set_spmv_format("auto")
         ops["auto"] = fa.SparseMatOp.from_arrays(ctx, m, n, *arrs)
+        ops["cycle"] = M  # the storage the cycle runs (grid classes / transfer classes)
         x = torch.rand(n, dtype=torch.float64, device="cuda:0")
         y = torch.empty(m, dtype=torch.float64, device="cuda:0")
         res = {k: [] for k in ops}
@@ -56,7 +58,7 @@ for l in range(mg.levels() - 1):
             for k, op in ops.items():
                 res[k].append(timeit(op, x, y))
         byts = 12 * nnz + 4 * (m + 1) + 8 * n + 8 * m
-        line = f"L{l} {name} {m}x{n} nnz/row {nnz / max(m, 1):7.1f}: "
+        line = f"L{l} {name} {m}x{n} nnz/row {nnz / max(m, 1):7.1f} [{M.spmv_info()['kernel']}]: "
         line += "  ".join(f"{k} {min(v) * 1e3:8.1f}us {byts / (min(v) * 1e-3) / 1e9:6.0f}GB/s"
                           for k, v in res.items())
         print(line, flush=True)

@@ -1734,3 +1734,40 @@ def test_spmm_compressed_storages(ctx):
         _spmm_vs_spmv(ctx, M, ks=(1, 3, 8, 32) if M.nrows < 2_000_000 else (3, 8))
     kinds = {k for k, _ in seen}
     assert {"dia", "bsr"} <= kinds, seen
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dims", [(64, 64, 64), (70, 62, 50), (256, 128, 8)])
+def test_dia7_row_pairs_bitwise(ctx, dims):
+    """Constant 7-point DIA kernel with 2 / 4 row pairs per lane (flag dia7_rp,
+    spmv_dia7c_kernel): every epilogue and the folded V-cycle (RESID0 / JACOBI
+    with the one-value diagonal) bitwise the one-pair kernel's -- a ragged row
+    count (70 x 62 x 50) and the 2.5-D band order (256 x 128 planes) included."""
+    import torch
+    n = int(np.prod(dims))
+    rng = np.random.default_rng(5)
+    x, b = T(rng.uniform(-1, 1, n)), T(rng.uniform(-1, 1, n))
+    d = T(rng.uniform(0.1, 0.2, n))
+    A = fa().SparseMatOp.laplace3d_7pt(ctx, *dims)
+    assert A.spmv_info()["kernel"] == "dia"
+    mg = fa().sa_build_box(A, dims, (2, 2, 2), coarsest_dim=100)
+    outs = {}
+    try:
+        for rp in (1, 2, 4, 0):
+            fa().set_flag("dia7_rp", rp)
+            res = []
+            for mode in ("set", "add", "resid", "jacobi"):
+                y = torch.full_like(x, 0.5)
+                A.spmv_epilogue(mode, x, y, b, d)
+                ctx.synchronize()
+                res.append(H(y))
+            z = torch.empty_like(b)
+            mg.apply(z, b)
+            ctx.synchronize()
+            res.append(H(z))
+            outs[rp] = res
+    finally:
+        fa().set_flag("dia7_rp", 0)
+    for rp in (2, 4, 0):
+        for u, v in zip(outs[rp], outs[1]):
+            assert np.array_equal(u.view(np.int64), v.view(np.int64)), rp

@@ -345,6 +345,8 @@ def _renumbered_plan_ok(plan, n, mg):
     assert names[0] == "perm_gather" and names[-1] == "perm_scatter", names
     assert any(p["name"] == "bsr3" and p["level"] == 0 for p in plan), names
     assert mg.level(0)[0].nrows == n and mg.level(0)[0].spmv_info()["kernel"] == "bsr"
+    Ar = mg.run_level(0)[0]  # the renumbered copy the cycle runs
+    assert Ar.nrows == n and Ar.nnz == mg.level(0)[0].nnz and Ar.spmv_info()["kernel"] == "bsr"
 
 
 def test_locality_reordering_bitwise(ctx):
