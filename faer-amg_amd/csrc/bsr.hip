@@ -105,10 +105,13 @@ __device__ __forceinline__ void bsr_steps(const char *__restrict__ st, int lane,
     }
 }
 
-template <int MODE>
+// WPB waves (slices) per workgroup: 4, or 1 for a matrix of few slices, so that
+// its few hundred waves spread over every CU (625 slices in 4-wave workgroups
+// left 99 of the 256 CUs idle: C5's R_0 / A_1)
+template <int MODE, int WPB>
 __global__ __launch_bounds__(256) void spmv_bsr3_kernel(BsrArgs a) {
     const int blk = xcd_remap(blockIdx.x, gridDim.x);
-    const int sl = __builtin_amdgcn_readfirstlane(blk * 4 + (int)(threadIdx.x >> 6));
+    const int sl = __builtin_amdgcn_readfirstlane(blk * WPB + (int)(threadIdx.x >> 6));
     if (sl >= a.nslices) return;
     const int s = a.slice0 + sl;
     const int lane = threadIdx.x & 63;
@@ -254,6 +257,7 @@ __global__ __launch_bounds__(256) void spmv_bsr3p_kernel(BsrArgs a) {
 // Two column buffers alternate (no loop-carried copies).  Same fma order per
 // dof row: bitwise the kernels above.
 constexpr int BSR_LU = 8;
+constexpr int64_t BSR_ONE_WAVE_SLICES = 4096;
 
 __device__ __forceinline__ void bsr_long_cols(const char *__restrict__ st, int lane, int g, int tl, int (&J)[BSR_LU]) {
 #pragma unroll
@@ -282,10 +286,10 @@ __device__ __forceinline__ void bsr_long_issue(const char *__restrict__ st, int 
     }
 }
 
-template <int MODE>
+template <int MODE, int WPB>
 __global__ __launch_bounds__(256) void spmv_bsr3l_kernel(BsrArgs a) {
     const int blk = xcd_remap(blockIdx.x, gridDim.x);
-    const int sl = __builtin_amdgcn_readfirstlane(blk * 4 + (int)(threadIdx.x >> 6));
+    const int sl = __builtin_amdgcn_readfirstlane(blk * WPB + (int)(threadIdx.x >> 6));
     if (sl >= a.nslices) return;
     const int s = a.slice0 + sl;
     const int lane = threadIdx.x & 63;
@@ -488,11 +492,25 @@ void spmv_bsr(const GpuCsr &m, const double *x, double *y, SpmvMode mode, const 
 #define FAMG_C ,
     const int64_t how = m.bsr_maxw <= BSR_PCOL ? flag(FLAG_BSR_KERNEL) : 0;
     const int64_t lg = flag(FLAG_BSR_LONG);
-    if (lg >= 0 && m.bsr_steps >= lg * m.bsr_slices) FAMG_BSR_LAUNCH(spmv_bsr3l_kernel, )
+    // one-wave workgroups below 4096 slices (C5: 1097 -> 1165 V-cycles/s,
+    // profiles/r05/ab_bsr_one_wave.txt)
+    const bool one = s1 - s0 < BSR_ONE_WAVE_SLICES;
+    const dim3 grid1((unsigned)(s1 - s0)), block1(64);
+    if (lg >= 0 && m.bsr_steps >= lg * m.bsr_slices) {
+        if (one) {
+            const dim3 grid = grid1, block = block1;
+            FAMG_BSR_LAUNCH(spmv_bsr3l_kernel, FAMG_C 1)
+        } else {
+            FAMG_BSR_LAUNCH(spmv_bsr3l_kernel, FAMG_C 4)
+        }
+    }
     else if (how == 1) FAMG_BSR_LAUNCH(spmv_bsr3p_kernel, FAMG_C 4 FAMG_C false)
     else if (how == 2) FAMG_BSR_LAUNCH(spmv_bsr3p_kernel, FAMG_C 2 FAMG_C true)
     else if (how == 3) FAMG_BSR_LAUNCH(spmv_bsr3p_kernel, FAMG_C 4 FAMG_C true)
-    else FAMG_BSR_LAUNCH(spmv_bsr3_kernel, )
+    else if (one) {
+        const dim3 grid = grid1, block = block1;
+        FAMG_BSR_LAUNCH(spmv_bsr3_kernel, FAMG_C 1)
+    } else FAMG_BSR_LAUNCH(spmv_bsr3_kernel, FAMG_C 4)
 #undef FAMG_BSR_LAUNCH
 #undef FAMG_C
     FAMG_CHECK_HIP(hipGetLastError());

@@ -37,7 +37,7 @@ def split(rows, iters, cycles, nplan):
         lo, marks = marks[1] + 1, marks[2:]
     # CAL and FINE sit between the copy marks and the cycle marks (the warm-up
     # cycle before the copies also runs DIA kernels and must not be counted)
-    dia = [i for i in range(lo, marks[0]) if "spmv_dia_kernel" in names[i]]
+    dia = [i for i in range(lo, marks[0]) if "spmv_dia_kernel" in names[i] or "spmv_dia7c_kernel" in names[i]]
     cal, fine = dia[:iters], dia[iters:2 * iters]
     cyc = list(range(marks[0] + 1, marks[1]))
     assert len(cyc) == cycles * nplan, (len(cyc), cycles, nplan)
@@ -83,7 +83,8 @@ def main(fetch_csv, write_csv, known_json, plan_json, out_json):
                         "known_read_bytes": cal_known,
                         "fetch_size_bytes": statistics.median(F[i][1] for i in cal),
                         "write_size_bytes": statistics.median(W[i][1] for i in calw), "known_write_bytes": 8 * n},
-        "fine_set": {"kernel": "spmv_dia_kernel<SET> on A_0 (7-pt 256^3)", "algorithmic_bytes_per_launch": fine_alg,
+        "fine_set": {"kernel": F[fine[0]][0].split("(")[0].replace("void ", "").replace("famg::", "") + " on A_0 (7-pt 256^3)",
+                     "algorithmic_bytes_per_launch": fine_alg,
                      "read_bytes_per_launch": round(fine_rd), "write_bytes_per_launch": round(fine_wr),
                      "hbm_bytes_per_launch": round(fine_rd + fine_wr),
                      "ratio": round((fine_rd + fine_wr) / fine_alg, 4)},
