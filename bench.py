@@ -287,6 +287,7 @@ def build_problem(fa, ctx, args, dims):
         nn = fa.constant_candidates(A.nrows, bs)
         mg = fa.smoothed_aggregation(A, nn, block_size=bs, candidate_dimension=bs, coarsest_dim=1000,
                                      smoother=args.smoother, strength_depth=args.strength_depth)
+    mg.set_reorder(args.reorder)
     return A, mg
 
 
@@ -568,6 +569,7 @@ def run_single(args):
                                    "per_level_kernels": [d["kernels"] for d in psum["per_level"]],
                                    "per_level_storage": storage_plan},
                    "rel_residual_after_1_cycle": rho1,
+                   "locality_renumbered_levels": [l for l in range(mg.levels()) if mg.reordered(l)],
                    "abi_ingest": abi,
                    "parallelism": "single GPU"},
         "fine_spmv_gbs": round(achieved, 1),
@@ -1133,6 +1135,9 @@ def main():
                     help="elast: node numbering shuffled within windows of this many nodes (the locality "
                          "of a mesh numbering without stencil structure); 0 = over all nodes; -1 = none "
                          "(the generator's lexicographic numbering)")
+    ap.add_argument("--reorder", type=int, default=1, choices=[0, 1, 2],
+                    help="locality renumbering of general levels (multigrid option 5): 0 off, 1 auto "
+                         "(bitwise), 2 every eligible level")
     ap.add_argument("--block-size", type=int, default=3, help="elast/mtx: dofs per node")
     ap.add_argument("--strength-depth", type=int, default=1,
                     help="elast/mtx: BFS depth of the strength graph (the reference hard-codes 3, "
