@@ -737,7 +737,7 @@ amg_status amg_multigrid_set_option(amg_linop *mg, int32_t option, int64_t value
         case 0: m->use_graph = value != 0; break;
         case 1: m->sgs_residual_form = value != 0; break;
         case 2: m->fold_zero_guess = value != 0; break;
-        case 3: m->fuse_transfers = value != 0; m->invalidate_graphs(); m->fuse_reset(); break;
+        case 3: FAMG_REQUIRE(value == 0, AMG_ERR_UNSUPPORTED, "fused grid transfers were removed (DESIGN.md 3)"); break;
         case 4: m->restrict_df = value != 0; break;
         case 5:
             FAMG_REQUIRE(value >= 0 && value <= 2, AMG_ERR_INVALID, "reorder: 0, 1 or 2");
@@ -747,29 +747,6 @@ amg_status amg_multigrid_set_option(amg_linop *mg, int32_t option, int64_t value
         default: fail(AMG_ERR_INVALID, "unknown multigrid option");
         }
         m->invalidate_graphs();
-    });
-}
-
-amg_status amg_multigrid_fused_transfer(amg_linop *mg, int64_t level, int32_t which, const double *a,
-                                       const double *b, const double *x, double *out, int32_t *applied) {
-    return guard([&] {
-        auto m = need_mg(mg);
-        FAMG_REQUIRE(applied, AMG_ERR_INVALID, "null output");
-        std::lock_guard<std::mutex> lk(m->mtx);
-        FAMG_REQUIRE(level >= 0 && level + 1 < (int64_t)m->levels.size(), AMG_ERR_INVALID, "level out of range");
-        m->ensure_workspace();
-        MgLevel &L = m->levels[level];
-        auto *A = dynamic_cast<CsrOp *>(L.A.get());
-        auto *D = dynamic_cast<DiagOp *>(L.S.get());
-        *applied = 0;
-        if (which == 0 && fuse_has_pre(L)) {
-            FAMG_REQUIRE(x || D, AMG_ERR_INVALID, "folded restriction needs a diagonal smoother");
-            fuse_resid_restrict(*L.fuse, A->m, a, x, D, out, m->ctx->stream);
-            *applied = 1;
-        } else if (which == 1 && fuse_has_post(L) && D) {
-            fuse_interp_jacobi(*L.fuse, A->m, a, b, x, *D, out, m->ctx->stream);
-            *applied = 1;
-        }
     });
 }
 

@@ -496,9 +496,6 @@ struct CoarseCholOp : LinOp {
     void apply(double *out, const double *rhs) override;
 };
 
-struct TransferFuse;  // fuse.hip
-// default of MultigridOp::fuse_transfers (FAMG_FUSE=1: on)
-extern int g_fuse_transfers;
 struct MgLevel {
     LinOpPtr A, S, R, P;  // R, P: transfer to the next-coarser level (null on the coarsest)
     // locality reordering (reorder.hip): the operators the caller added when A/S/R/P
@@ -512,8 +509,6 @@ struct MgLevel {
     const LinOpPtr &origP() const { return oP ? oP : P; }
     // device workspaces (allocated lazily at first apply)
     DevBuf<double> v, f, t, r;
-    // fused residual->restriction and interpolation->Jacobi launches (fuse.hip)
-    std::shared_ptr<TransferFuse> fuse;
 };
 
 struct MultigridOp : LinOp {
@@ -524,14 +519,12 @@ struct MultigridOp : LinOp {
     // s = 1 Jacobi levels: fold the first smoothing step from v = 0 (v = d*f)
     // into the residual (RESID0) and the correction (ADD0) instead of storing it
     bool fold_zero_guess = true;
-    // grid levels: residual + restriction and interpolation + post-smoothing
-    // Jacobi as one launch each (fuse.hip)
-    bool fuse_transfers = g_fuse_transfers != 0;
     // R on wide grid-transfer classes writes the next level's first Jacobi step
     // from zero beside f_c (SPMV_SETDF) instead of a separate d*f pass
     bool restrict_df = true;
-    // locality reordering of general levels (reorder.hip): 0 off, 1 where RCM at
-    // least halves the x lines an SpMV slice touches (default), 2 every eligible level
+    // locality renumbering of general levels (reorder.hip): 0 off, 1 where it stays
+    // bitwise and at least halves the x lines an SpMV slice touches (default), 2 every
+    // eligible level
     int reorder = 1;
     std::mutex mtx;
     Kind kind() const override { return Kind::Multigrid; }
@@ -540,7 +533,6 @@ struct MultigridOp : LinOp {
     void add_level(LinOpPtr A, LinOpPtr S, LinOpPtr R, LinOpPtr P);
     void ensure_workspace();
     void invalidate_graphs();
-    void fuse_reset() { fuse_ready_ = false; }  // fused transfers re-decided at the next apply
     ~MultigridOp() override;
 
     // V-cycle building blocks (also used by the distributed multigrid)
@@ -565,7 +557,6 @@ struct MultigridOp : LinOp {
     std::vector<GraphEntry> graphs_;
     uint64_t flags_gen_ = 0;  // flags_generation() the graphs were captured under
     bool workspace_ready_ = false;
-    bool fuse_ready_ = false;
     bool reorder_done_ = false;
     DevBuf<double> perm_f0_, perm_v0_;  // the fine level's rhs / result in its numbering
 };
@@ -585,15 +576,6 @@ bool setdf_enabled();
 inline bool r_has_setdf(const CsrOp *R) {
     return R && ((R->m.gtx_on && R->m.gtx_r) || (R->m.gtc_on && R->m.gtc_r) || R->m.kernel == SPMV_KERNEL_SELLP);
 }
-
-// fused grid transfers (fuse.hip)
-void fuse_setup(MultigridOp &mg, size_t l);
-bool fuse_has_pre(const MgLevel &L);
-bool fuse_has_post(const MgLevel &L);
-void fuse_resid_restrict(const TransferFuse &F, const GpuCsr &m, const double *f, const double *x,
-                         const DiagOp *D, double *fc, hipStream_t s);
-void fuse_interp_jacobi(const TransferFuse &F, const GpuCsr &m, const double *vc, const double *f, const double *x,
-                        const DiagOp &D, double *out, hipStream_t s);
 
 // ---------------------------------------------------------------- factories
 

@@ -435,16 +435,7 @@ void MultigridOp::add_level(LinOpPtr A, LinOpPtr S, LinOpPtr R, LinOpPtr P) {
 }
 
 void MultigridOp::ensure_workspace() {
-    if (workspace_ready_) {
-        if (!fuse_ready_) {
-            for (size_t l = 0; l + 1 < levels.size(); l++) {
-                if (fuse_transfers) fuse_setup(*this, l);
-                else levels[l].fuse.reset();
-            }
-            fuse_ready_ = true;
-        }
-        return;
-    }
+    if (workspace_ready_) return;
     if (!reorder_done_) reorder_levels();
     for (size_t l = 0; l < levels.size(); l++) {
         const int64_t n = levels[l].A->nrows;
@@ -461,11 +452,6 @@ void MultigridOp::ensure_workspace() {
             D->codes_tried = true;
         }
     }
-    for (size_t l = 0; l + 1 < levels.size(); l++) {
-        if (fuse_transfers) fuse_setup(*this, l);
-        else levels[l].fuse.reset();
-    }
-    fuse_ready_ = true;
     workspace_ready_ = true;
 }
 
@@ -609,27 +595,19 @@ void MultigridOp::cycle(int64_t l, double *v, const double *f, bool v_zero, doub
     // than the pass it saves (Q1 elasticity 1.57M rows: 640 vs 388 + 15 us).
     const bool fold = fold_level(A, D, P, fold_zero_guess, v_zero, steps);
     MgLevel &C = levels[l + 1];
-    // grid levels: residual and restriction in one launch (fuse.hip), r never stored
-    const bool fuse_pre = fuse_transfers && A && fuse_has_pre(L) && (!fold || D);
     if (fold) {
         log_at(l, AMG_ROLE_RESID);
-        if (fuse_pre) {
-            fuse_resid_restrict(*L.fuse, A->m, f, nullptr, D, C.f.get(), s);  // f_c = R (f - A (d f))
-        } else {
-            SpmvEpi epi;
-            epi.b = f;
-            epi.d = D->d.get();
-            epi.dc = D->dcode.get();  // DIA: 1-B codes of d gathered instead of d
-            epi.dt = D->dtab.get();
-            epi.dk = D->dconst;
-            spmv(A->m, f, L.r.get(), SPMV_RESID0, epi, s);  // work = f - A (d f)
-        }
+        SpmvEpi epi;
+        epi.b = f;
+        epi.d = D->d.get();
+        epi.dc = D->dcode.get();  // DIA: 1-B codes of d gathered instead of d
+        epi.dt = D->dtab.get();
+        epi.dk = D->dconst;
+        spmv(A->m, f, L.r.get(), SPMV_RESID0, epi, s);  // work = f - A (d f)
     } else {
         smooth(l, v, t, f, v_zero, pre_df);
         log_at(l, AMG_ROLE_RESID);
-        if (fuse_pre) {
-            fuse_resid_restrict(*L.fuse, A->m, f, v, nullptr, C.f.get(), s);  // f_c = R (f - A v)
-        } else if (A) {
+        if (A) {
             SpmvEpi epi;
             epi.b = f;
             spmv(A->m, v, L.r.get(), SPMV_RESID, epi, s);  // work = f - A v (:341-342)
@@ -642,7 +620,7 @@ void MultigridOp::cycle(int64_t l, double *v, const double *f, bool v_zero, doub
     // step from zero (d_c * f_c, what smooth() would compute first) into the
     // buffer that step writes: one launch and 24 n_c bytes fewer, same values
     bool df = false;
-    if (!fuse_pre && l + 2 < (int64_t)levels.size() && restrict_df && setdf_enabled()) {
+    if (l + 2 < (int64_t)levels.size() && restrict_df && setdf_enabled()) {
         auto *Rc = dynamic_cast<CsrOp *>(L.R.get());
         auto *Ac = dynamic_cast<CsrOp *>(C.A.get());
         auto *Dc = dynamic_cast<DiagOp *>(C.S.get());
@@ -660,25 +638,12 @@ void MultigridOp::cycle(int64_t l, double *v, const double *f, bool v_zero, doub
             spmv(Rc->m, L.r.get(), C.f.get(), SPMV_SETDF, epi, s);
         }
     }
-    if (!fuse_pre && !df) {
+    if (!df) {
         log_at(l, AMG_ROLE_RESTRICT);
         L.R->apply(C.f.get(), L.r.get());  // f_c = R work (:343)
     }
     for (int64_t k = 0; k < mu; k++) cycle(l + 1, C.v.get(), C.f.get(), k == 0, nullptr, df && k == 0);
     log_at(l, AMG_ROLE_INTERP);
-    // grid levels with one post-smoothing Jacobi step: interpolation and that
-    // step in one launch (fuse.hip), the corrected v never stored
-    if (fuse_transfers && A && D && steps == 1 && fuse_has_post(L)) {
-        // folded: v = d f + P v_c is not read from memory, so the result can
-        // go to v0 directly; else the corrected iterate is read around every
-        // point and must not be overwritten in the same launch
-        double *o = (fold || v != v0) ? v0 : t;
-        fuse_interp_jacobi(*L.fuse, A->m, C.v.get(), f, fold ? nullptr : v, *D, o, s);
-        v = o;
-        log_at(l, AMG_ROLE_OTHER);
-        if (v != v0) vec_copy(v0, v, n, s);
-        return;
-    }
     if (fold) {
         SpmvEpi epi;
         epi.b = f;

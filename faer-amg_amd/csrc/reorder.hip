@@ -420,7 +420,6 @@ std::shared_ptr<MultigridOp> MultigridOp::original_view() {
     v->use_graph = use_graph;
     v->sgs_residual_form = sgs_residual_form;
     v->fold_zero_guess = fold_zero_guess;
-    v->fuse_transfers = fuse_transfers;
     v->restrict_df = restrict_df;
     v->reorder = reorder;
     for (auto &L : levels) {

@@ -92,7 +92,6 @@ SIGNATURES = {
     "amg_csr_dia_range": (i32, [vp, vp]),
     "amg_csr_class_info": (i32, [vp, vp]),
     "amg_csr_set_grid": (i32, [vp, i64, i64, i64]),
-    "amg_multigrid_fused_transfer": (i32, [vp, i64, i32, vp, vp, vp, vp, P(i32)]),
     "amg_csr_spmv_epilogue": (i32, [vp, i32, vp, vp, vp, vp]),
     "amg_csr_grid_info": (i32, [vp, vp]),
     "amg_grid_from_offsets": (i32, [vp, i64, i64, vp, P(i32)]),
@@ -680,26 +679,10 @@ class Multigrid(LinOp):
         """Fold the zero-guess Jacobi step into the residual/correction SpMVs (default on)."""
         _ck(_lib.amg_multigrid_set_option(self.h, 2, 1 if enable else 0))
 
-    def fused_transfer(self, level, which, a, b, x, out):
-        """amg_multigrid_fused_transfer on device tensors (test hook): which "restrict"
-        out = R (a - A x) (x None: d*a), "interp" out = Jacobi step from (x or d*b) + P a.
-        Returns False when the level has no such fused launch."""
-        ptr = lambda t: None if t is None else vp(t.data_ptr())  # noqa: E731
-        ok = i32()
-        with _ordered(self.ctx, AMG_MEM_DEVICE):
-            _ck(_lib.amg_multigrid_fused_transfer(self.h, level, {"restrict": 0, "interp": 1}[which], ptr(a),
-                                                  ptr(b), ptr(x), ptr(out), C.byref(ok)))
-        return bool(ok.value)
-
     def set_restrict_df(self, enable):
         """R on wide grid-transfer classes also writes the next level's first Jacobi step
         from zero (SPMV_SETDF; default on; bitwise the separate d*f pass)."""
         _ck(_lib.amg_multigrid_set_option(self.h, 4, 1 if enable else 0))
-
-    def set_fuse_transfers(self, enable):
-        """Grid levels: residual + restriction and interpolation + post-smoothing Jacobi
-        as one launch each (fuse.hip; default off, FAMG_FUSE=1 turns it on for new multigrids)."""
-        _ck(_lib.amg_multigrid_set_option(self.h, 3, 1 if enable else 0))
 
     def levels(self):
         v = i64()

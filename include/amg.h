@@ -306,13 +306,8 @@ amg_status amg_multigrid_set_graph(amg_linop *mg, int32_t enable);
  * and correction SpMVs instead of storing it (default 1; bitwise identical), on
  * levels whose operator is fp64 SELL with mostly short columns, x-staged SELL,
  * or DIA codes whose P runs the short-slice kernel; amg_multigrid_cycle_plan
- * reports which levels fold (RESID0 / ADD0 launches); 3 = fused grid transfers
- * (default 0; FAMG_FUSE=1 sets 1 for multigrids created afterwards): on a level whose operator is
- * DIA codes on a grid (amg_csr_set_grid) with steps in {-1,0,1}^3 and whose
- * next level is its 2x2x2-box grid, the residual and the restriction run as
- * one launch (fuse_resid_restrict), and the interpolation with one Jacobi
- * post-smoothing step as another (fuse_interp_jacobi); R and P are read as
- * grid-transfer classes (8-bit class per row).  Bitwise identical.  4 = a
+ * reports which levels fold (RESID0 / ADD0 launches); 3 = fused grid transfers:
+ * removed in round 5 (measured slower twice); only 0 is accepted.  4 = a
  * restriction stored as wide grid-transfer classes (gtx.hip) also writes the
  * next level's first Jacobi step from zero, d_c f_c, beside f_c (SPMV_SETDF)
  * instead of a separate pass (default 1; bitwise identical). */
@@ -334,12 +329,6 @@ amg_status amg_multigrid_set_option(amg_linop *mg, int32_t option, int64_t value
 amg_status amg_multigrid_level_reordered(amg_linop *mg, int64_t level, int32_t *reordered);
 amg_status amg_multigrid_get_run_level(amg_linop *mg, int64_t level, amg_linop **A, amg_linop **S,
                                        amg_linop **R, amg_linop **P);
-/* One fused grid transfer of level l on device vectors (test hook; *applied = 0
- * when the level has none): which 0 -- out (coarse) = R (a - A x), x = the
- * iterate, or NULL for the folded zero-guess iterate d*a; which 1 -- out (fine)
- * = one Jacobi step from v = (x, or NULL: d*b) + P a on A v = b. */
-amg_status amg_multigrid_fused_transfer(amg_linop *mg, int64_t level, int32_t which, const double *a,
-                                       const double *b, const double *x, double *out, int32_t *applied);
 /* Multigrid::apply == amg_linop_apply on a multigrid handle. */
 amg_status amg_multigrid_apply(amg_linop *mg, double *out, int64_t ld_out, const double *rhs,
                                int64_t ld_rhs, int64_t k, amg_mem mem);
