@@ -444,7 +444,16 @@ bool gtx_attach(GpuCsr &m, const int64_t *fg, const int64_t *cg, int which) {
     // tiles whose fine window fits 64 KB of LDS
     int tile[3] = {0, 0, 0}, wdim[3] = {0, 0, 0};
     if (!is_r) {
-        for (int tzc : {4, 2}) {
+        // four fine planes per lane, or two where that leaves fewer than 1024 tiles
+        // (P_2 of the 256^3 cycle: 256 workgroups of 4 planes cover the chip once and
+        // leave its cold misses exposed; FAMG_GTX_PTZ=4 / 2 forces)
+        static const int ptz = [] {
+            const char *e = getenv("FAMG_GTX_PTZ");
+            return e ? atoi(e) : 0;
+        }();
+        const int64_t tiles4 = ((rx + 31) / 32) * ((ry + 7) / 8) * ((n / (rx * ry) + 3) / 4);
+        const int first = ptz == 2 || (ptz == 0 && tiles4 < 1024) ? 2 : 4;
+        for (int tzc : {first, 2}) {
             const int w0 = 16 + hi[0] - lo[0], w1 = 4 + hi[1] - lo[1], w2 = tzc / 2 + hi[2] - lo[2];
             if ((int64_t)w0 * w1 * w2 * 8 <= 64 * 1024) {
                 tile[0] = 32; tile[1] = 8; tile[2] = tzc;
