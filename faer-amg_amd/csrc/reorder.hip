@@ -175,20 +175,35 @@ __global__ void k_gather_perm(double *out, const double *in, const int32_t *p, i
     const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
     if (i < n) out[i] = in[p[i]];
 }
-__global__ void k_scatter_perm(double *out, const double *in, const int32_t *p, int64_t n) {
-    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    if (i < n) out[p[i]] = in[i];
+// the apply's rhs gather / result scatter: PG elements per thread, all index
+// loads, then all value loads issued before the stores (PG gathers in flight)
+constexpr int PG = 4;
+template <bool SCATTER>
+__global__ __launch_bounds__(256) void k_perm_apply(double *out, const double *in, const int32_t *p, int64_t n) {
+    const int64_t i0 = (int64_t)blockIdx.x * (256 * PG) + threadIdx.x;
+    int32_t q[PG];
+    double v[PG];
+#pragma unroll
+    for (int u = 0; u < PG; u++) q[u] = p[min(i0 + 256 * u, n - 1)];
+#pragma unroll
+    for (int u = 0; u < PG; u++) v[u] = SCATTER ? in[min(i0 + 256 * u, n - 1)] : in[q[u]];
+#pragma unroll
+    for (int u = 0; u < PG; u++)
+        if (i0 + 256 * u < n) {
+            if (SCATTER) out[q[u]] = v[u];
+            else out[i0 + 256 * u] = v[u];
+        }
 }
 
 void perm_gather(double *out, const double *in, const int32_t *p, int64_t n, hipStream_t s) {
     if (n <= 0) return;
-    hipLaunchKernelGGL(k_gather_perm, dim3((unsigned)ceil_div(n, 256)), dim3(256), 0, s, out, in, p, n);
+    hipLaunchKernelGGL(k_perm_apply<false>, dim3((unsigned)ceil_div(n, 256 * PG)), dim3(256), 0, s, out, in, p, n);
     FAMG_CHECK_HIP(hipGetLastError());
     log_launch("perm_gather", -1, -1, n, 20 * n);
 }
 void perm_scatter(double *out, const double *in, const int32_t *p, int64_t n, hipStream_t s) {
     if (n <= 0) return;
-    hipLaunchKernelGGL(k_scatter_perm, dim3((unsigned)ceil_div(n, 256)), dim3(256), 0, s, out, in, p, n);
+    hipLaunchKernelGGL(k_perm_apply<true>, dim3((unsigned)ceil_div(n, 256 * PG)), dim3(256), 0, s, out, in, p, n);
     FAMG_CHECK_HIP(hipGetLastError());
     log_launch("perm_scatter", -1, -1, n, 20 * n);
 }
@@ -344,8 +359,10 @@ void MultigridOp::reorder_levels() {
             for (int64_t i = 0; i < n; i++) qn[pn[i]] = (int32_t)i;
         };
         std::vector<int32_t> pn, qn;
-        expand(rcm_order(rp, col, n, bs), pn, qn);
+        const std::vector<int32_t> rcm = rcm_order(rp, col, n, bs);
+        expand(rcm, pn, qn);
         int64_t best = slice_lines(rp, col, n, pn.data(), qn.data());
+        const int64_t rcm_lines = best;
         auto *Pc = dynamic_cast<CsrOp *>(levels[l].P.get());
         if (!p[l + 1].empty() && Pc && n % bs == 0) {
             const int bsc = bsl[l + 1] > 0 ? bsl[l + 1] : 1;
@@ -358,7 +375,11 @@ void MultigridOp::reorder_levels() {
                 qn.swap(qi);
             }
         }
-        if (reorder == 1 && 2 * best > slice_lines(rp, col, n, nullptr, nullptr)) continue;  // at least halve them
+        const int64_t orig_lines = slice_lines(rp, col, n, nullptr, nullptr);
+        if (getenv("FAMG_REORDER_LOG"))
+            fprintf(stderr, "reorder level %zu: x lines per SpMV (64-row slices) stored %lld, rcm %lld, chosen %lld\n", l,
+                    (long long)orig_lines, (long long)rcm_lines, (long long)best);
+        if (reorder == 1 && 2 * best > orig_lines) continue;  // at least halve them
         p[l] = std::move(pn);
         q[l] = std::move(qn);
         bsl[l] = bs;
