@@ -60,7 +60,6 @@ struct Sgs27Args {
     int ext[8];  // march: colour s is computed on rows [y0 - ext[s], y1 + ext[s]) of its parity
     int halo;    // march: own rows staged from y0 - halo (max ext + 1)
     float rnx2;  // march: 1 / (nx / 2), rounded (q / (nx / 2) as (q + 0.5) * rnx2: exact for q < 2^14)
-    int pair;    // march: a row parity's two colours in one pass (FLAG_SGS27_PAIR)
 };
 
 
@@ -356,65 +355,6 @@ __device__ __forceinline__ void sgs27m_stage(const Sgs27Args &a, double *own, co
     }
 }
 
-// Two colours of one row parity in one pass (FLAG_SGS27_PAIR): colour B (x parity
-// 1 - PXA) reads colour A only at its x neighbours in the same row, so one wave
-// takes a whole row -- colour A on every segment, then colour B -- and the barrier
-// between the two colour stages disappears (LDS operations of a wave complete in
-// order, so B's reads see A's writes).  The row's b values of both colours are
-// loaded first.  Per point the arithmetic is sgs27m_stage's (bitwise).
-template <int PX>
-__device__ __forceinline__ void sgs27m_point(const Sgs27Args &a, double *own, const double *const (&planes)[3], int y,
-                                             int r0, int rs, int nk, int sg, double br, bool first_zero) {
-    const int lane = threadIdx.x & 63;
-    const int k = (sg << 6) + lane;
-    const bool live = k < nk;
-    const int x = PX + 2 * min(k, nk - 1);
-    const int o16 = 2 + x - PX, o8 = PX == 0 ? 1 + x : 3 + x;
-    double w[9][3];
-#pragma unroll
-    for (int j = 0; j < 9; j++) {
-        const double *row = planes[j / 3] + (y + j % 3 - r0) * rs;
-        const sgs_dbl2_t p = *reinterpret_cast<const sgs_dbl2_t *>(row + o16);
-        const double v = row[o8];
-        w[j][0] = PX == 0 ? v : p.x;
-        w[j][1] = PX == 0 ? p.x : p.y;
-        w[j][2] = PX == 0 ? p.y : v;
-    }
-    double acc = 0.0;
-#pragma unroll
-    for (int q = 0; q < 27; q++) acc = fma(a.icoef[q], w[q / 3][q % 3], acc);
-    const double xr = w[4][1];
-    if (live) own[(y - r0 + 1) * rs + 2 + x] = first_zero ? a.idinv * br : xr + a.idinv * (br - acc);
-}
-
-template <int PXA, int NW>
-__device__ __forceinline__ void sgs27m_stage2(const Sgs27Args &a, double *own, const double *lo, const double *hi,
-                                              int z, int r0, int ys0, int ys1, int py, bool first_zero) {
-    const int nx = a.nx, ny = a.ny, rs = nx + 4;
-    const int yfirst = ys0 + ((ys0 & 1) != py ? 1 : 0);
-    const int nrow = yfirst < ys1 ? (ys1 - yfirst + 1) / 2 : 0;
-    const int nk = nx / 2;
-    const int nseg = (nk + 63) >> 6;  // 1 or 2 (nx <= 256)
-    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int lane = threadIdx.x & 63;
-    const double *const planes[3] = {lo, own, hi};
-    for (int yr = wave; yr < nrow; yr += NW) {
-        const int y = yfirst + 2 * yr;
-        const double *brow = a.b + ((int64_t)z * ny + y) * nx;
-        double bA[2], bB[2];
-#pragma unroll
-        for (int sg = 0; sg < 2; sg++) {
-            const int kk = min((sg << 6) + lane, nk - 1);
-            bA[sg] = brow[PXA + 2 * kk];
-            bB[sg] = brow[1 - PXA + 2 * kk];
-        }
-        sgs27m_point<PXA>(a, own, planes, y, r0, rs, nk, 0, bA[0], first_zero);
-        if (nseg > 1) sgs27m_point<PXA>(a, own, planes, y, r0, rs, nk, 1, bA[1], first_zero);
-        sgs27m_point<1 - PXA>(a, own, planes, y, r0, rs, nk, 0, bB[0], false);
-        if (nseg > 1) sgs27m_point<1 - PXA>(a, own, planes, y, r0, rs, nk, 1, bB[1], false);
-    }
-}
-
 // pairs q of a row set (nx / 2 per row) -> LDS pair index in slot rows of nx + 4
 __device__ __forceinline__ int sgs27m_lpair(int q, int nx2, float rnx2) {
     const int pr = (int)(((float)q + 0.5f) * rnx2);
@@ -467,20 +407,12 @@ __global__ __launch_bounds__(64 * NW) void k_sgs27_march(Sgs27Args a) {
         const bool more = j + 1 < j1;
         sgs_dbl2_t vo[PFS], vp[PFO];
         if (more) sgs27m_fetch<NW, PFS, PFO>(a, z + 2, z + 3, r0, nown2, npl2, !a.own_zero, vo, vp);
-        for (int s = 0; s < a.nst;) {
+        for (int s = 0; s < a.nst; s++) {
             const int h = a.ext[s];
             const int ys0 = max(y0 - h, 0), ys1 = min(y1 + h, ny);
             const bool first_zero = a.own_zero && a.other_zero && s == 0;
-            // (a pair's colours share their row parity, hence their halo: ext[s] == ext[s + 1])
-            if (a.pair && s + 1 < a.nst && a.py[s + 1] == a.py[s] && a.px[s + 1] != a.px[s]) {
-                if (a.px[s] == 0) sgs27m_stage2<0, NW>(a, own, lo, hi, z, r0, ys0, ys1, a.py[s], first_zero);
-                else sgs27m_stage2<1, NW>(a, own, lo, hi, z, r0, ys0, ys1, a.py[s], first_zero);
-                s += 2;
-            } else {
-                if (a.px[s] == 0) sgs27m_stage<0, NW>(a, own, lo, hi, z, r0, ys0, ys1, a.py[s], first_zero);
-                else sgs27m_stage<1, NW>(a, own, lo, hi, z, r0, ys0, ys1, a.py[s], first_zero);
-                s += 1;
-            }
+            if (a.px[s] == 0) sgs27m_stage<0, NW>(a, own, lo, hi, z, r0, ys0, ys1, a.py[s], first_zero);
+            else sgs27m_stage<1, NW>(a, own, lo, hi, z, r0, ys0, ys1, a.py[s], first_zero);
             __syncthreads();
         }
         sgs_dbl2_t *dst = reinterpret_cast<sgs_dbl2_t *>(a.T + ((int64_t)z * ny + y0) * nx);
@@ -845,7 +777,6 @@ static void sgs27_phase(const SgsOp &S, int pz, int nst, const int *px, const in
         a.rnx2 = 1.0f / (float)(S.nx27 / 2);
         FAMG_REQUIRE(fdiv_exact((a.ty + 2 * halo + 2) * (S.nx27 / 2) + 1024, S.nx27 / 2, a.rnx2), AMG_ERR_UNSUPPORTED,
                      "sgs27 march: float reciprocal division not exact for this plane width");
-        a.pair = flag(FLAG_SGS27_PAIR) != 0;
         a.jper = flag(FLAG_SGS27_MARCH) > 1 ? (int)flag(FLAG_SGS27_MARCH) : (int)std::max<int64_t>(1, ceil_div((int64_t)nplanes * a.ntiles, cus));
         const int64_t nchunks = ceil_div(nplanes, a.jper);
         const size_t lds_m = (size_t)3 * (a.ty + 2 * halo + 2) * (S.nx27 + 4) * sizeof(double);

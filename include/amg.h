@@ -132,9 +132,7 @@ amg_status amg_set_alloc_policy(int32_t policy);
  * the next 8 steps' node columns ahead (default 16, env FAMG_BSR_LONG; -1
  * never), 8 = row pairs per lane of the constant 7-point DIA kernel: 0 auto
  * (default: 2 for SET, 1 for the cycle's epilogues), 1, 2 or 4 adjacent 512-row
- * blocks per workgroup (env FAMG_DIA7_RP), 9 = marching SGS phases run a row
- * parity's two colours in one pass, one wave per grid row (1, default) or as two
- * colour stages (0; env FAMG_SGS27_PAIR).  Setting one
+ * blocks per workgroup (env FAMG_DIA7_RP).  Setting one
  * makes every multigrid re-capture its hipGraph at its next apply.  amg_get_flag
  * reads the current value. */
 amg_status amg_set_flag(int32_t which, int64_t value);

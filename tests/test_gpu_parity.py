@@ -1622,16 +1622,13 @@ def test_sgs27_marching_phases_bitwise(ctx, dims):
     S1 = fa().SymGaussSeidel(A)
     mg1 = fa().sa_build_box(A, dims, (2, 2, 2), coarsest_dim=500, smoother="sgs")
     assert fa().sgs_fused(S1)
-    # sgs27_pair: a row parity's two colours in one pass (one wave per row)
     try:
-        for v, pair in ((0, 0), (2, 0), (3, 0), (5, 0), (1, 0), (1, 1), (3, 1), (0, 1)):
+        for v in (0, 2, 3, 5, 1):
             fa().set_flag("sgs27_march", v)
-            fa().set_flag("sgs27_pair", pair)
-            assert np.array_equal(apply_dev(ctx, S1, r, n), e0), (v, pair)
-            assert np.array_equal(apply_dev(ctx, mg1, b, n), z0), (v, pair)
+            assert np.array_equal(apply_dev(ctx, S1, r, n), e0), v
+            assert np.array_equal(apply_dev(ctx, mg1, b, n), z0), v
     finally:
         fa().set_flag("sgs27_march", 1)
-        fa().set_flag("sgs27_pair", 1)
 
 
 def _spmm_vs_spmv(ctx, A, ks=(1, 3, 8, 32), seed=0):
