@@ -540,6 +540,9 @@ struct MultigridOp : LinOp {
     // step from zero (d*f, SPMV_SETDF) into the level's t buffer
     void cycle(int64_t l, double *v, const double *f, bool v_zero, double *out_final, bool pre_df = false);
     void smooth(int64_t l, double *&v, double *&t, const double *f, bool v_zero, bool pre_df = false);
+    // the renumbered fine level's rhs gather, with its first Jacobi step from zero
+    // written beside it where the level takes that step unfolded
+    void gather_fine(const double *rhs, hipStream_t s);
     // launch records of one V-cycle (eager, recorder on)
     std::vector<LaunchRec> cycle_plan();
     // renumber eligible levels (first ensure_workspace) / restore the caller's operators
@@ -563,6 +566,9 @@ struct MultigridOp : LinOp {
 // y = x[p] / y[p] = x over n entries (reorder.hip; launch-plan records)
 void perm_gather(double *out, const double *in, const int32_t *p, int64_t n, hipStream_t s);
 void perm_scatter(double *out, const double *in, const int32_t *p, int64_t n, hipStream_t s);
+// the gather and the first Jacobi step from zero in one pass: f0 = in[p], t = d * f0
+void perm_gather_df(double *f0, double *t, const double *in, const int32_t *p, const DiagOp &D, int64_t n,
+                    hipStream_t s);
 
 // the zero-guess fold decision of one level (RESID0 + ADD0 instead of v = d*f)
 // m's DIA codes are a constant 7- or 27-point stencil on an nx x ny x nz grid (nx

@@ -565,6 +565,25 @@ bool setdf_enabled() {
     return on;
 }
 
+// gather rhs into the renumbered fine level's order and run the cycle there; where
+// level 0 takes its first Jacobi step from zero unfolded (smooth(): t = d*f), the
+// gather writes that step too (one pass, one launch fewer: the t buffer cycle(0)
+// smooths into, as SPMV_SETDF does for coarser levels)
+void MultigridOp::gather_fine(const double *rhs, hipStream_t s) {
+    MgLevel &L = levels[0];
+    const int64_t n = L.A->nrows;
+    auto *A = dynamic_cast<CsrOp *>(L.A.get());
+    auto *D = dynamic_cast<DiagOp *>(L.S.get());
+    auto *P = dynamic_cast<CsrOp *>(L.P.get());
+    const bool df = levels.size() > 1 && A && D && steps >= 1 && !fold_level(A, D, P, fold_zero_guess, true, steps);
+    if (df) {
+        perm_gather_df(perm_f0_.get(), L.t.get(), rhs, L.perm.get(), *D, n, s);
+    } else {
+        perm_gather(perm_f0_.get(), rhs, L.perm.get(), n, s);
+    }
+    cycle(0, perm_v0_.get(), perm_f0_.get(), true, perm_v0_.get(), df);
+}
+
 void MultigridOp::cycle(int64_t l, double *v, const double *f, bool v_zero, double *, bool pre_df) {
     MgLevel &L = levels[l];
     hipStream_t s = ctx->stream;
@@ -681,8 +700,7 @@ void MultigridOp::apply(double *out, const double *rhs) {
     auto run = [&]() {
         if (levels[0].permuted) {  // the fine level runs in its numbering: rhs in, result out
             const int64_t n = levels[0].A->nrows;
-            perm_gather(perm_f0_.get(), rhs, levels[0].perm.get(), n, s);
-            cycle(0, perm_v0_.get(), perm_f0_.get(), true, perm_v0_.get());
+            gather_fine(rhs, s);
             perm_scatter(out, perm_v0_.get(), levels[0].perm.get(), n, s);
         } else {
             cycle(0, out, rhs, true, out);
@@ -731,8 +749,7 @@ std::vector<LaunchRec> MultigridOp::cycle_plan() {
     g_launch_log = &log;
     try {
         if (levels[0].permuted) {
-            perm_gather(perm_f0_.get(), b.get(), levels[0].perm.get(), n, ctx->stream);
-            cycle(0, perm_v0_.get(), perm_f0_.get(), true, perm_v0_.get());
+            gather_fine(b.get(), ctx->stream);
             perm_scatter(z.get(), perm_v0_.get(), levels[0].perm.get(), n, ctx->stream);
         } else {
             cycle(0, z.get(), b.get(), true, z.get());

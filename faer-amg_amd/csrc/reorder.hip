@@ -195,6 +195,44 @@ __global__ __launch_bounds__(256) void k_perm_apply(double *out, const double *i
         }
 }
 
+// the gather fused with the fine level's first Jacobi step from zero: f0 = in[p],
+// t = d * f0 (vec_mul's product, the coded diagonal's dt[dc] where it has codes)
+template <bool CODED>
+__global__ __launch_bounds__(256) void k_perm_gather_df(double *f0, double *t, const double *in, const int32_t *p,
+                                                       const double *d, const uint8_t *dc, const double *dt,
+                                                       int64_t n) {
+    const int64_t i0 = (int64_t)blockIdx.x * (256 * PG) + threadIdx.x;
+    int32_t q[PG];
+    double v[PG], dd[PG];
+#pragma unroll
+    for (int u = 0; u < PG; u++) {
+        const int64_t i = min(i0 + 256 * u, n - 1);
+        q[u] = p[i];
+        dd[u] = CODED ? dt[dc[i]] : d[i];
+    }
+#pragma unroll
+    for (int u = 0; u < PG; u++) v[u] = in[q[u]];
+#pragma unroll
+    for (int u = 0; u < PG; u++)
+        if (i0 + 256 * u < n) {
+            f0[i0 + 256 * u] = v[u];
+            t[i0 + 256 * u] = dd[u] * v[u];
+        }
+}
+
+void perm_gather_df(double *f0, double *t, const double *in, const int32_t *p, const DiagOp &D, int64_t n,
+                    hipStream_t s) {
+    if (n <= 0) return;
+    const dim3 grid((unsigned)ceil_div(n, 256 * PG));
+    if (D.dcode.get())
+        hipLaunchKernelGGL(k_perm_gather_df<true>, grid, dim3(256), 0, s, f0, t, in, p, nullptr, D.dcode.get(),
+                           D.dtab.get(), n);
+    else
+        hipLaunchKernelGGL(k_perm_gather_df<false>, grid, dim3(256), 0, s, f0, t, in, p, D.d.get(), nullptr, nullptr, n);
+    FAMG_CHECK_HIP(hipGetLastError());
+    log_launch("perm_gather_df", -1, -1, n, (D.dcode.get() ? 29 : 36) * n);
+}
+
 void perm_gather(double *out, const double *in, const int32_t *p, int64_t n, hipStream_t s) {
     if (n <= 0) return;
     hipLaunchKernelGGL(k_perm_apply<false>, dim3((unsigned)ceil_div(n, 256 * PG)), dim3(256), 0, s, out, in, p, n);

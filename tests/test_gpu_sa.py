@@ -342,7 +342,8 @@ def _reorder_runs(ctx, e, modes):
 
 def _renumbered_plan_ok(plan, n, mg):
     names = [p["name"] for p in plan]
-    assert names[0] == "perm_gather" and names[-1] == "perm_scatter", names
+    # (perm_gather_df: the gather writes the fine level's first Jacobi step from zero too)
+    assert names[0] in ("perm_gather", "perm_gather_df") and names[-1] == "perm_scatter", names
     assert any(p["name"] == "bsr3" and p["level"] == 0 for p in plan), names
     assert mg.level(0)[0].nrows == n and mg.level(0)[0].spmv_info()["kernel"] == "bsr"
     Ar = mg.run_level(0)[0]  # the renumbered copy the cycle runs
