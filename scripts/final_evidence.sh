@@ -8,9 +8,14 @@ export TMPDIR=/tmp
 R=$(pwd)
 O=$R/gpurun_out/final
 mkdir -p "$O"
-timeout -k 10 400 python3 bench.py > "$O/bench_stdout.log" 2> "$O/bench_stderr.log" || exit 1
+# heartbeat: the CPU baseline / parity legs of the C3 / C5 lines run minutes without output
+( while sleep 50; do date >> "$O/heartbeat.log"; done ) &
+HB=$!
+trap 'kill $HB 2>/dev/null' EXIT
+SKIP=${SKIP:-}
+[[ $SKIP == *bench* ]] || timeout -k 10 400 python3 bench.py > "$O/bench_stdout.log" 2> "$O/bench_stderr.log" || exit 1
 echo "bench: $(tail -1 "$O/bench_stdout.log" | cut -c1-160)"
-timeout -k 10 500 rocprofv3 --kernel-trace --stats -d "$O/prof" -o run --output-format csv \
+[[ $SKIP == *prof* ]] || timeout -k 10 500 rocprofv3 --kernel-trace --stats -d "$O/prof" -o run --output-format csv \
     -- python3 "$R/bench.py" > "$O/bench_prof_stdout.log" 2> "$O/bench_prof_stderr.log" || exit 1
 echo "bench under rocprofv3: $(tail -1 "$O/bench_prof_stdout.log" | cut -c1-160)"
 timeout -k 10 500 python3 bench.py --problem 27pt > "$O/c3_stdout.log" 2> "$O/c3_stderr.log" || exit 1
