@@ -494,7 +494,7 @@ void spmv_bsr(const GpuCsr &m, const double *x, double *y, SpmvMode mode, const 
     const int64_t lg = flag(FLAG_BSR_LONG);
     // one-wave workgroups below 4096 slices (C5: 1097 -> 1165 V-cycles/s,
     // profiles/r05/ab_bsr_one_wave.txt)
-    const bool one = s1 - s0 < BSR_ONE_WAVE_SLICES;
+    const bool one = s1 - s0 < BSR_ONE_WAVE_SLICES;  // (everywhere: neutral on C5's A_0)
     const dim3 grid1((unsigned)(s1 - s0)), block1(64);
     if (lg >= 0 && m.bsr_steps >= lg * m.bsr_slices) {
         if (one) {

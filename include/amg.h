@@ -129,7 +129,7 @@ amg_status amg_set_alloc_policy(int32_t policy);
  * batches, 2 = columns first, 2-step batches pipelined, 3 = 4-step pipelined
  * (env FAMG_BSR_KERNEL), 7 = 3x3-block matrices whose slices (64 node rows)
  * average at least this many block steps take the long-row kernel that loads
- * the next 8 steps' node columns ahead (default 16, env FAMG_BSR_LONG; -1
+ * the next 8 steps' node columns ahead (default 48, env FAMG_BSR_LONG; -1
  * never), 8 = row pairs per lane of the constant 7-point DIA kernel: 0 auto
  * (default: 2 for SET, 1 for the cycle's epilogues), 1, 2 or 4 adjacent 512-row
  * blocks per workgroup (env FAMG_DIA7_RP).  Setting one

@@ -258,7 +258,7 @@ def test_bsr_storage_bitwise(ctx, gap):
                 assert np.array_equal(yk.cpu().numpy().view(np.int64), ref.view(np.int64)), (k, split, mode)
     finally:
         fa().set_flag("bsr_kernel", 0)
-        fa().set_flag("bsr_long", 16)
+        fa().set_flag("bsr_long", 48)
     nn = fa().constant_candidates(S.shape[0], 3)
     w = weights(S, nn)
     mg = fa().smoothed_aggregation(A, nn, weights=w, block_size=3, candidate_dimension=3, coarsest_dim=150,
