@@ -40,6 +40,7 @@ struct BsrEpi {
     const double *d;
     const uint8_t *dc;
     const double *dt;
+    double *y2;  // SETDF: d * y beside y (the next level's first Jacobi step from zero)
 };
 
 struct BsrArgs {
@@ -61,10 +62,14 @@ template <int MODE> struct BsrRow {
         }
         if constexpr (MODE == SPMV_RESID) br = a.b[i];
         if constexpr (MODE == SPMV_ADD) yr = a.y[i];
+        if constexpr (MODE == SPMV_SETDF) dr = a.dc ? a.dt[a.dc[i]] : a.d[i];
     }
     __device__ __forceinline__ void store(const BsrEpi &a, int i, double acc) const {
         if constexpr (MODE == SPMV_SET) a.y[i] = acc;
-        else if constexpr (MODE == SPMV_ADD) a.y[i] = yr + acc;
+        else if constexpr (MODE == SPMV_SETDF) {
+            a.y[i] = acc;
+            a.y2[i] = dr * acc;  // vec_mul(_coded)'s product
+        } else if constexpr (MODE == SPMV_ADD) a.y[i] = yr + acc;
         else if constexpr (MODE == SPMV_RESID) a.y[i] = br - acc;
         else a.y[i] = xr + dr * (br - acc);  // JACOBI
     }
@@ -478,7 +483,7 @@ void spmv_bsr(const GpuCsr &m, const double *x, double *y, SpmvMode mode, const 
         return (e && e[0] == '1') ? 0 : -1;
     }();
     BsrArgs a{m.bsr_data.get(), m.bsr_row0.get(), m.bsr_soff.get(), (int32_t)s0, (int32_t)(s1 - s0),
-              BsrEpi{x, y, epi.b, epi.d, epi.dc, epi.dt}, jmask};
+              BsrEpi{x, y, epi.b, epi.d, epi.dc, epi.dt, epi.y2}, jmask};
     const dim3 grid((unsigned)ceil_div(s1 - s0, 4)), block(256);
     // T: the template arguments after the mode
 #define FAMG_BSR_LAUNCH(K, T)                                                      \
@@ -487,6 +492,7 @@ void spmv_bsr(const GpuCsr &m, const double *x, double *y, SpmvMode mode, const 
     case SPMV_ADD: K<SPMV_ADD T><<<grid, block, 0, s>>>(a); break;                 \
     case SPMV_RESID: K<SPMV_RESID T><<<grid, block, 0, s>>>(a); break;             \
     case SPMV_JACOBI: K<SPMV_JACOBI T><<<grid, block, 0, s>>>(a); break;           \
+    case SPMV_SETDF: K<SPMV_SETDF T><<<grid, block, 0, s>>>(a); break;             \
     default: fail(AMG_ERR_UNSUPPORTED, "block storage: unsupported SpMV epilogue"); \
     }
 #define FAMG_C ,

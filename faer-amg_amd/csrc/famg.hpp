@@ -578,9 +578,10 @@ bool fold_level(const CsrOp *A, const DiagOp *D, const CsrOp *P, bool fold_zero_
 // the restriction into a level writes that level's first Jacobi step from zero
 // (SPMV_SETDF) -- false with FAMG_SETDF=0
 bool setdf_enabled();
-// R serves SPMV_SETDF (a grid-transfer overlay of either width, or pattern SELL)
+// R serves SPMV_SETDF (a grid-transfer overlay of either width, pattern SELL or 3x3 blocks)
 inline bool r_has_setdf(const CsrOp *R) {
-    return R && ((R->m.gtx_on && R->m.gtx_r) || (R->m.gtc_on && R->m.gtc_r) || R->m.kernel == SPMV_KERNEL_SELLP);
+    return R && ((R->m.gtx_on && R->m.gtx_r) || (R->m.gtc_on && R->m.gtc_r) || R->m.kernel == SPMV_KERNEL_SELLP ||
+                 R->m.kernel == SPMV_KERNEL_BSR);
 }
 
 // ---------------------------------------------------------------- factories

@@ -2669,8 +2669,8 @@ void spmv(const GpuCsr &m, const double *x, double *y, SpmvMode mode, const Spmv
         spmv_gtc(m, x, y, mode, epi, s, seg);
         return;
     }
-    FAMG_REQUIRE(mode != SPMV_SETDF || m.kernel == SPMV_KERNEL_SELLP, AMG_ERR_UNSUPPORTED,
-                 "SETDF needs a grid-transfer or pattern-SELL restriction");
+    FAMG_REQUIRE(mode != SPMV_SETDF || m.kernel == SPMV_KERNEL_SELLP || m.kernel == SPMV_KERNEL_BSR,
+                 AMG_ERR_UNSUPPORTED, "SETDF needs a grid-transfer, pattern-SELL or 3x3-block restriction");
     if (m.kernel == SPMV_KERNEL_BSR) {
         FAMG_REQUIRE(mode != SPMV_SGS, AMG_ERR_UNSUPPORTED, "block storage has no SGS sweep");
         spmv_bsr(m, x, y, mode, epi, s, seg);
