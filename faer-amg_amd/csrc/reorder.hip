@@ -15,9 +15,12 @@
 // is permuted alike; the vectors of a permuted level live in its numbering
 // throughout the cycle, so only the fine level's rhs and result cross it (one
 // gather, one scatter per apply).  The numbering: reverse Cuthill-McKee on the
-// node graph (block size 3 for 3x3-blocked operators, so blocks stay intact),
-// kept for a level when it at least halves the x cache lines its 64-row slices
-// touch.  Storages that rely on column order (DIA, stencil and grid-transfer
+// node graph (block size 3 for 3x3-blocked operators, so blocks stay intact), or
+// the nodes grouped by aggregate in the renumbered coarse level's order, whichever
+// touches fewer x cache lines per 64-row slice, kept for a level when it at least
+// halves them.  The copies keep their original's kind of storage (a CSR-stream
+// operator, whose lanes per row follow its block's rows, only has its columns
+// renamed), so the auto mode is bitwise.  Storages that rely on column order (DIA, stencil and grid-transfer
 // classes, pattern SELL, aligned SELL slices) are not built for a permuted
 // matrix (GpuCsr::order_fixed); the 3x3-block storage merges a node's rows by
 // original column (GpuCsr::col_orig).
