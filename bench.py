@@ -65,9 +65,15 @@ def measured_traffic(edge, problem):
     (scripts/pmc_fine_spmv.py + scripts/pmc_summary.py; FETCH_SIZE calibrated on
     a diagonal matrix through the same kernel).  None if not measured for this
     workload."""
+    import glob
+    if problem == "elast" and edge == 80:  # the C5 stand-in's renumbered fine SpMV (scripts/pmc_bsr_renum.sh)
+        files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "c5_renum_spmv_traffic.json")))
+        if not files:
+            return None, None
+        d = json.load(open(files[-1]))
+        return d["hbm_bytes_per_launch"], os.path.relpath(files[-1], ROOT)
     if edge != 256 or problem != "7pt":
         return None, None
-    import glob
     # the latest round's cycle-wide passes (scripts/pmc_cycle.sh: the roofline
     # kernel -- DIA SET on A_0 -- and every launch of the cycle), else the
     # older fine-SpMV-only passes
@@ -539,7 +545,9 @@ def run_single(args):
             log(f"cpu baseline / parity failed: {e!r}")
 
     cycles_per_s = 1000.0 / ms_per_cycle
-    traffic, traffic_src = measured_traffic(args.edge, args.problem)
+    # (C5 stand-in: the counter file covers 80^3 elements, windows of 4096, renumbering on)
+    c5_default = args.problem == "elast" and args.permute == 4096 and args.reorder == 1
+    traffic, traffic_src = measured_traffic(args.elements if c5_default else args.edge, args.problem)
     return {
         "metric": METRIC,
         "value": round(cycles_per_s, 3),
