@@ -20,10 +20,10 @@
 // touches fewer x cache lines per 64-row slice, kept for a level when it at least
 // halves them.  The copies keep their original's kind of storage (a CSR-stream
 // operator, whose lanes per row follow its block's rows, only has its columns
-// renamed), so the auto mode is bitwise.  Storages that rely on column order (DIA, stencil and grid-transfer
-// classes, pattern SELL, aligned SELL slices) are not built for a permuted
-// matrix (GpuCsr::order_fixed); the 3x3-block storage merges a node's rows by
-// original column (GpuCsr::col_orig).
+// renamed), so the auto mode is bitwise.  Storages that rely on column order
+// (DIA, stencil and grid-transfer classes, pattern SELL, aligned SELL slices)
+// are not built for a permuted matrix (GpuCsr::order_fixed); the 3x3-block
+// storage merges a node's rows by original column (GpuCsr::col_orig).
 #include <algorithm>
 #include <numeric>
 #include <queue>
@@ -231,7 +231,8 @@ void perm_gather_df(double *f0, double *t, const double *in, const int32_t *p, c
         hipLaunchKernelGGL(k_perm_gather_df<true>, grid, dim3(256), 0, s, f0, t, in, p, nullptr, D.dcode.get(),
                            D.dtab.get(), n);
     else
-        hipLaunchKernelGGL(k_perm_gather_df<false>, grid, dim3(256), 0, s, f0, t, in, p, D.d.get(), nullptr, nullptr, n);
+        hipLaunchKernelGGL(k_perm_gather_df<false>, grid, dim3(256), 0, s, f0, t, in, p, D.d.get(), nullptr, nullptr,
+                           n);
     FAMG_CHECK_HIP(hipGetLastError());
     log_launch("perm_gather_df", -1, -1, n, (D.dcode.get() ? 29 : 36) * n);
 }
@@ -283,11 +284,14 @@ static CsrPtr csr_permuted(const CsrOp &A, const std::vector<int32_t> &rows_n2o,
         rows = &ident;
     }
     FAMG_CHECK_HIP(hipMemcpyAsync(drows.get(), rows->data(), n * 4, hipMemcpyHostToDevice, s));
-    if (!col_o2n.empty()) FAMG_CHECK_HIP(hipMemcpyAsync(dmap.get(), col_o2n.data(), m.ncols * 4, hipMemcpyHostToDevice, s));
+    if (!col_o2n.empty())
+        FAMG_CHECK_HIP(hipMemcpyAsync(dmap.get(), col_o2n.data(), m.ncols * 4, hipMemcpyHostToDevice, s));
     auto P = make_csr(ctx);
     csr_alloc(P->m, ctx, n, m.ncols, m.nnz);
     DevBuf<int64_t> len(std::max<int64_t>(1, n));
-    if (n) hipLaunchKernelGGL(k_perm_len, dim3((unsigned)ceil_div(n, 256)), dim3(256), 0, s, m.rp64.get(), drows.get(), n, len.get());
+    if (n)
+        hipLaunchKernelGGL(k_perm_len, dim3((unsigned)ceil_div(n, 256)), dim3(256), 0, s, m.rp64.get(), drows.get(), n,
+                           len.get());
     FAMG_CHECK_HIP(hipGetLastError());
     scan_counts(len.get(), P->m.rp64.get(), n, *ctx);
     if (n)
@@ -418,7 +422,8 @@ void MultigridOp::reorder_levels() {
         }
         const int64_t orig_lines = slice_lines(rp, col, n, nullptr, nullptr);
         if (getenv("FAMG_REORDER_LOG"))
-            fprintf(stderr, "reorder level %zu: x lines per SpMV (64-row slices) stored %lld, rcm %lld, chosen %lld\n", l,
+            fprintf(stderr, "reorder level %zu: x lines per SpMV (64-row slices) stored %lld, rcm %lld, chosen %lld\n",
+                    l,
                     (long long)orig_lines, (long long)rcm_lines, (long long)best);
         if (reorder == 1 && 2 * best > orig_lines) continue;  // at least halve them
         p[l] = std::move(pn);
