@@ -420,6 +420,136 @@ def abi_ingest(fa, ctx, mg, b, z_ref, stream, args):
                     "(no grid hints: inferred), same timed cycle as the headline"}
 
 
+FUSED_NAMES = {0: ("fine-rr", "k_fine_resid_restrict",
+                    "folded fine residual r = f - A (d f) + restriction f_c = R r, d_c f_c (r kept in LDS)"),
+               1: ("fine-pj", "k_fine_interp_jacobi",
+                   "folded correction v = d f + P v_c + post-smoothing Jacobi step (v kept in LDS)")}
+
+
+def fused_launches(mg, plan, b, z, stream, reps=20):
+    """The cycle's fused fine-level launches (fine.hip) timed on their own with HIP
+    events on the library stream: each exactly as the V-cycle makes it, on the
+    cycle's own workspace (amg_multigrid_fine_launch), priced on the algorithmic
+    bytes of its plan record.  warm: the same rhs / out every launch (the x and y
+    of consecutive launches partly resident in the 256 MB MALL); cold: rhs / out
+    rotating over three pairs (a 1.6 GB working set, nothing MALL-resident)."""
+    import torch
+    out = {}
+    recs = {p["name"]: p for p in plan if p["level"] == 0}
+    for which, (pname, kname, what) in FUSED_NAMES.items():
+        if pname not in recs or not mg.fine_launch(which, z, b):
+            continue
+        bytes_ = recs[pname]["bytes"]
+        for _ in range(3):
+            mg.fine_launch(which, z, b)
+        warm = time_kernel(lambda: mg.fine_launch(which, z, b), reps, stream)
+        pairs = [(b.clone(), torch.empty_like(z)) for _ in range(3)]
+        it = [0]
+
+        def rot():
+            bb, zz = pairs[it[0] % 3]
+            it[0] += 1
+            mg.fine_launch(which, zz, bb)
+        for _ in range(3):
+            rot()
+        cold = time_kernel(rot, 3 * reps, stream)
+        del pairs
+        torch.cuda.synchronize()
+        out[pname] = {"kernel": kname, "what": what, "bytes_per_launch": bytes_,
+                      "csr_bytes_per_launch": recs[pname]["csr_bytes"],
+                      "ms_per_launch": round(warm, 5), "achieved": round(bytes_ / (warm * 1e-3) / 1e9, 1),
+                      "frac": round(bytes_ / (warm * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                      "cold": {"ms_per_launch": round(cold, 5),
+                               "achieved": round(bytes_ / (cold * 1e-3) / 1e9, 1),
+                               "frac": round(bytes_ / (cold * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                               "what": "rhs / out rotating over three pairs (1.6 GB > the 256 MB MALL)"}}
+    return out
+
+
+def fused_traffic(pname):
+    """Calibrated PMC HBM bytes per launch of a fused fine-level kernel
+    (scripts/pmc_cycle.sh -> profiles/rNN/c2_cycle_traffic.json, per plan
+    position), or (None, None)."""
+    import glob
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "c2_cycle_traffic.json")), reverse=True):
+        d = json.load(open(f))
+        for r in d.get("launches", []):
+            if r.get("storage") == pname and r.get("hbm_bytes"):
+                return r["hbm_bytes"], os.path.relpath(f, ROOT)
+    return None, None
+
+
+SECONDARY = (("c3_27pt_sgs", {"problem": "27pt", "smoother": "sgs"},
+              "C3: 3D 27-point anisotropic 256^3, SA 2^3 boxes, multicolour SGS s=1, Cholesky coarsest"),
+             ("c5_standin_shuffled", {"problem": "elast", "smoother": "l1", "permute": 4096},
+              "C5 stand-in: Q1 elasticity 80^3 elements (1.57M rows), nodes shuffled within windows of 4096, "
+              "general SA block 3, L1-Jacobi"),
+             ("c5_standin_natural", {"problem": "elast", "smoother": "l1", "permute": -1},
+              "C5 stand-in, the generator's lexicographic node numbering (no shuffle)"))
+
+
+def secondary_one(fa, ctx, stream, a):
+    """One secondary configuration on this GPU: setup, V-cycles/s of hipGraph
+    replays (events on the library stream), the launch plan's bytes, and one
+    V-cycle against the oracle on the same hierarchy."""
+    import numpy as np
+    import torch
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as O
+    dims = (a.edge,) * 3
+    t0 = time.perf_counter()
+    A, mg = build_problem(fa, ctx, a, dims)
+    mg.set_graph(True)
+    torch.cuda.synchronize()
+    setup_s = time.perf_counter() - t0
+    n = A.nrows
+    b_host = splitmix_uniform(n, 42)
+    b = torch.as_tensor(b_host, device="cuda:0")
+    z = torch.empty_like(b)
+    for _ in range(3):
+        mg.apply(z, b)
+    ms = time_kernel(lambda: mg.apply(z, b), 20, stream)
+    psum = plan_summary(mg.cycle_plan())
+    t1 = time.perf_counter()
+    omg = O.Multigrid(oracle_levels(mg, a.smoother))
+    omg.set_parallel(a.cpu_threads)
+    zref = omg.apply(b_host)
+    rel = float(np.linalg.norm(z.cpu().numpy() - zref) / np.linalg.norm(zref))
+    del omg
+    res = {"vcycles_per_s": round(1000.0 / ms, 3), "ms_per_step": round(ms, 4), "steps": 20,
+           "setup_s": round(setup_s, 2), "levels": mg.levels(), "fine_rows": n, "fine_nnz": A.nnz,
+           "vcycle_launches": psum["launches"], "vcycle_algorithmic_GB": round(psum["bytes"] / 1e9, 3),
+           "vcycle_GBs": round(psum["bytes"] / (ms * 1e-3) / 1e9, 1),
+           "locality_renumbered_levels": [l for l in range(mg.levels()) if mg.reordered(l)],
+           "parity": {"vcycle_rel_err": rel, "tol": 1e-11, "ok": rel <= 1e-11,
+                      "oracle_s": round(time.perf_counter() - t1, 1),
+                      "what": "one V-cycle z = M b (b = splitmix64 seed 42) against the oracle on the same hierarchy"}}
+    del mg, A, b, z
+    torch.cuda.synchronize()
+    return res
+
+
+def secondary_configs(fa, ctx, stream, args):
+    """config.secondary: C3 and the C5 stand-in (both numberings) under the same
+    clock as the headline, each with its own one-cycle oracle parity."""
+    out = {}
+    t_all = time.perf_counter()
+    for name, over, what in SECONDARY:
+        a = argparse.Namespace(**vars(args))
+        for k, v in over.items():
+            setattr(a, k, v)
+        a.edge = 256
+        t0 = time.perf_counter()
+        try:
+            out[name] = dict(secondary_one(fa, ctx, stream, a), workload=what)
+        except Exception as e:  # reported, never fatal to the headline
+            out[name] = {"error": repr(e), "workload": what}
+        out[name]["wall_s"] = round(time.perf_counter() - t0, 1)
+        log(f"secondary {name}: " + json.dumps({k: v for k, v in out[name].items() if k != "workload"}))
+    out["wall_s"] = round(time.perf_counter() - t_all, 1)
+    return out
+
+
 def run_single(args):
     import numpy as np
     import torch
@@ -535,6 +665,15 @@ def run_single(args):
         with open(args.plan_out, "w") as fh:
             json.dump({"steps": args.steps, "plan": plan}, fh)
 
+    # the cycle's fused fine-level launches timed on their own (roofline: the
+    # dominant one -- the launch the V-cycle spends most time in)
+    fused = {}
+    if args.problem == "7pt" and not renumbered:
+        zz = torch.empty_like(b)
+        fused = fused_launches(mg, plan, b, zz, stream)
+        del zz
+        log("fused fine launches: " + json.dumps(fused))
+
     cpu, parity = None, None
     if not args.no_cpu_baseline:
         try:
@@ -544,10 +683,43 @@ def run_single(args):
         except Exception as e:  # the baseline must not kill the GPU measurement
             log(f"cpu baseline / parity failed: {e!r}")
 
+    secondary = None
+    if args.problem == "7pt" and args.edge == 256 and not args.no_secondary:
+        secondary = secondary_configs(fa, ctx, stream, args)
+
     cycles_per_s = 1000.0 / ms_per_cycle
     # (C5 stand-in: the counter file covers 80^3 elements, windows of 4096, renumbering on)
     c5_default = args.problem == "elast" and args.permute == 4096 and args.reorder == 1
     traffic, traffic_src = measured_traffic(args.elements if c5_default else args.edge, args.problem)
+    # A_0's SET SpMV (the solve loops' operator apply); its CSR-equivalent rate
+    # only where it stays below the HBM peak (a matrix-free stencil moves far
+    # fewer bytes than CSR, so a CSR-priced rate above peak says nothing)
+    csr_eq = bytes_csr / (spmv_ms * 1e-3) / 1e9
+    a0_set = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+              "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "traffic_source": traffic_src,
+              "kernel": roofline_kernel_name(fa, info, args) + " on A_0"
+                        + (" (locality-renumbered copy the cycle runs)" if renumbered else ""),
+              "storage": info, "bytes_per_launch": bytes_spmv, "ms_per_launch": round(spmv_ms, 5),
+              "csr_bytes_per_launch": bytes_csr}
+    if csr_eq <= HBM_PEAK_GBS:
+        a0_set["csr_equivalent_GBs"] = round(csr_eq, 1)
+    else:
+        a0_set["csr_equivalent_note"] = (f"CSR-priced rate {csr_eq / HBM_PEAK_GBS:.1f}x the HBM peak: the "
+                                         f"storage streams {bytes_csr / bytes_spmv:.1f}x fewer bytes than CSR")
+    if fused:
+        # headline roofline: the cycle's dominant fused launch (most bytes, most time)
+        dom = max(fused, key=lambda k: fused[k]["bytes_per_launch"])
+        f = fused[dom]
+        ftraffic, fsrc = fused_traffic(dom)
+        roofline = {"bound": "hbm", "achieved": f["achieved"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                    "frac": f["frac"], "traffic": ftraffic, "traffic_source": fsrc,
+                    "kernel": f"{f['kernel']} ({f['what']}) on level 0 -- the V-cycle's dominant launch",
+                    "in_cycle": True, "bytes_per_launch": f["bytes_per_launch"],
+                    "ms_per_launch": f["ms_per_launch"], "cold": f["cold"],
+                    "fused": fused, "a0_set": a0_set, "fp64_values": fp64_values,
+                    "csr": csr_block, "general": general}
+    else:
+        roofline = dict(a0_set, fp64_values=fp64_values, csr=csr_block, general=general)
     return {
         "metric": METRIC,
         "value": round(cycles_per_s, 3),
@@ -579,20 +751,10 @@ def run_single(args):
                    "rel_residual_after_1_cycle": rho1,
                    "locality_renumbered_levels": [l for l in range(mg.levels()) if mg.reordered(l)],
                    "abi_ingest": abi,
+                   "secondary": secondary,
                    "parallelism": "single GPU"},
         "fine_spmv_gbs": round(achieved, 1),
-        "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
-                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                     "traffic_source": traffic_src,
-                     "kernel": roofline_kernel_name(fa, info, args) + " on A_0"
-                               + (" (locality-renumbered copy the cycle runs)" if renumbered else ""),
-                     "storage": info,
-                     "bytes_per_launch": bytes_spmv, "ms_per_launch": round(spmv_ms, 5),
-                     "csr_bytes_per_launch": bytes_csr,
-                     "csr_equivalent_GBs": round(bytes_csr / (spmv_ms * 1e-3) / 1e9, 1),
-                     "fp64_values": fp64_values,
-                     "csr": csr_block,
-                     "general": general},
+        "roofline": roofline,
         "cpu_baseline": cpu,
         "parity": parity,
     }
@@ -1170,6 +1332,8 @@ def main():
                     help="distributed: exchange halos before the SpMV instead of under its interior rows")
     ap.add_argument("--ab", action="store_true", help="A/B the SpMV storage formats (stderr)")
     ap.add_argument("--no-general", action="store_true", help="skip roofline.general (random 7-pt)")
+    ap.add_argument("--no-secondary", action="store_true",
+                    help="skip config.secondary (C3 and the C5 stand-in, both numberings, under the same clock)")
     ap.add_argument("--no-abi", action="store_true",
                     help="skip config.abi_ingest (the hierarchy re-ingested through the C ABI, timed)")
     ap.add_argument("--no-fold", action="store_true",

@@ -111,7 +111,8 @@ static std::atomic<int64_t> g_flag_val[FLAG_COUNT] = {
     {[] { const char *e = getenv("FAMG_XS_PIPE"); return (int64_t)(e ? atoi(e) : 2); }()},
     {[] { const char *e = getenv("FAMG_BSR_KERNEL"); return (int64_t)(e ? atoi(e) : 0); }()},
     {[] { const char *e = getenv("FAMG_BSR_LONG"); return (int64_t)(e ? atoll(e) : 48); }()},
-    {[] { const char *e = getenv("FAMG_DIA7_RP"); return (int64_t)(e ? atoi(e) : 0); }()}};
+    {[] { const char *e = getenv("FAMG_DIA7_RP"); return (int64_t)(e ? atoi(e) : 0); }()},
+    {[] { const char *e = getenv("FAMG_FINE_FUSE"); return (int64_t)(e ? atoi(e) : 1); }()}};
 static std::atomic<uint64_t> g_flag_gen{0};
 int64_t flag(FlagId f) { return g_flag_val[f].load(std::memory_order_relaxed); }
 void set_flag(FlagId f, int64_t v) {
@@ -741,6 +742,7 @@ amg_status amg_multigrid_set_option(amg_linop *mg, int32_t option, int64_t value
         case 4: m->restrict_df = value != 0; break;
         case 5:
             FAMG_REQUIRE(value >= 0 && value <= 2, AMG_ERR_INVALID, "reorder: 0, 1 or 2");
+            if (m->reorder == (int)value) return;  // unchanged: keep the copies and the graphs
             m->undo_reorder();
             m->reorder = (int)value;
             break;
@@ -765,6 +767,16 @@ amg_status amg_multigrid_cycle_plan(amg_linop *mg, amg_launch_rec *recs, int64_t
         FAMG_REQUIRE(count && cap >= 0, AMG_ERR_INVALID, "bad argument");
         m->ctx->set_device();
         export_plan(m->cycle_plan(), recs, cap, count);
+    });
+}
+
+amg_status amg_multigrid_fine_launch(amg_linop *mg, int32_t which, double *out, const double *rhs) {
+    return guard([&] {
+        auto m = need_mg(mg);
+        FAMG_REQUIRE((which == 0 || which == 1) && rhs && (out || which == 0), AMG_ERR_INVALID, "bad argument");
+        m->ctx->set_device();
+        FAMG_REQUIRE(m->fine_launch(which, out, rhs), AMG_ERR_UNSUPPORTED,
+                     "the cycle takes no fused fine-level launch of this kind");
     });
 }
 

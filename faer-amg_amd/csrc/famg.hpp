@@ -173,6 +173,7 @@ struct GpuCsr {
     int xscs_t[3] = {0, 0, 0}, xscs_r[3] = {0, 0, 0};
     int xscs_ws = 0;  // LDS row stride of the window (>= wx; padded against bank conflicts)
     int xscs_tile_src = 0;  // how the tile was chosen: TuneSource (tuning.hpp)
+    bool xscs_fdiv = false;  // the tile's float-reciprocal divisions checked exact (xscs_set_tile)
     DevBuf<int32_t> xscs_lo;
     std::vector<int> xscs_steps;  // (dx, dy, dz) of each of the scs_k offsets
     // grid-transfer classes (gtc.hip) for R/P of a 2x2x2-box hierarchy: an overlay
@@ -182,7 +183,10 @@ struct GpuCsr {
     DevBuf<uint8_t> gtc_cls;
     DevBuf<uint16_t> gtc_dict;  // nclass x ke entries: value index << 8 | step slot
     DevBuf<double> gtc_vtab;    // the distinct values (<= 256)
-    int gtc_ke = 0, gtc_nce = 0, gtc_ntab = 0;
+    int gtc_ke = 0, gtc_nce = 0, gtc_ntab = 0, gtc_nclass = 0;
+    // R: per class the first entry of each fine-plane group dz = -1, 0, 1, 2 and the
+    // real entry count (5 bytes; the marching fused restriction of fine.hip)
+    DevBuf<uint8_t> gtc_kdz;
     int64_t gtc_fg[3] = {0, 0, 0}, gtc_cg[3] = {0, 0, 0};
     // wide grid-transfer classes (gtx.hip): 16-bit class per row, dictionary of
     // (window offset, fp64 value) entries in global memory -- every box level
@@ -193,6 +197,7 @@ struct GpuCsr {
     int64_t gtx_nclass = 0, gtx_nent = 0;
     int gtx_tile[3] = {0, 0, 0}, gtx_win[3] = {0, 0, 0}, gtx_lo[3] = {0, 0, 0};
     int64_t gtx_fg[3] = {0, 0, 0}, gtx_cg[3] = {0, 0, 0};
+    bool gtx_fdiv = false;  // the window's float-reciprocal divisions checked exact (at build)
     // grid hint: the rows are the points of an nx x ny x nz grid, x fastest (0 = none);
     // set by the stencil generators, the box hierarchy and amg_csr_set_grid
     // (grid_src 1), else inferred at finalize from the stencil offsets (grid_src 2)
@@ -342,6 +347,19 @@ void spmv_bsr(const GpuCsr &m, const double *x, double *y, SpmvMode mode, const 
 void spmv_scs(const GpuCsr &m, const double *x, double *y, SpmvMode mode, const SpmvEpi &epi, hipStream_t s,
               int64_t seg);
 bool xs_supports(SpmvMode mode);
+// the constant 7-point DIA kernel with a one-value Jacobi diagonal takes m's
+// JACOBI / RESID0 launches (spmv.hip: no codes read, d = epi.dk)
+bool dia7_cst_dk(const GpuCsr &m, const SpmvEpi &epi);
+// fine.hip: the folded correction v = d f + P v_c and one Jacobi step on a
+// constant 7-point fine level as one marching kernel (out = the Jacobi result)
+bool fine_interp_jacobi_ok(const GpuCsr &A, const GpuCsr &P, const SpmvEpi &epi);
+void fine_interp_jacobi(const GpuCsr &A, const GpuCsr &P, const double *vc, const double *f, double dk, double *out,
+                        hipStream_t s);
+// the folded residual r = f - A (d f) and f_c = R r, d_c f_c (SETDF) as one marching kernel
+// (epic: the coarse level's d and y2 = d_c f_c, as spmv's SETDF epilogue takes them)
+bool fine_resid_restrict_ok(const GpuCsr &A, const GpuCsr &R, const SpmvEpi &epi, const SpmvEpi &epic);
+void fine_resid_restrict(const GpuCsr &A, const GpuCsr &R, const double *f, double dk, double *fc,
+                         const SpmvEpi &epic, hipStream_t s);
 bool gtc_supports(const GpuCsr &m, SpmvMode mode);
 // wide grid-transfer classes (gtx.hip); which as gtc_attach
 bool gtx_attach(GpuCsr &m, const int64_t *fg, const int64_t *cg, int which = -1);
@@ -384,6 +402,8 @@ void trace_mark(Ctx &ctx, int32_t tag);
 
 // dense row-major GEMV: out = M * x (M n x n)
 void dense_gemv(const double *M, const double *x, double *out, int64_t n, hipStream_t s);
+// RCM node order (new -> old) of the node graph of an n x n CSR, bs dofs per node (reorder.hip)
+std::vector<int32_t> rcm_order(const std::vector<int64_t> &rp, const std::vector<int32_t> &col, int64_t n, int bs);
 
 // exclusive scan of int64 counts (n entries) into out (n+1 entries); returns total
 int64_t scan_counts(const int64_t *counts, int64_t *out, int64_t n, Ctx &ctx);
@@ -490,7 +510,14 @@ struct SgsOp : LinOp {
 };
 
 struct CoarseCholOp : LinOp {
-    DevBuf<double> inv;  // dense A^{-1}, row-major
+    DevBuf<double> inv;  // dense A^{-1}, row-major (n <= 8192)
+    // above 8192 rows (chol.hip): the envelope Cholesky factor of the RCM-ordered
+    // matrix in 64-row blocks -- off-diagonal slabs, inverses of the diagonal blocks
+    int64_t nb = 0, env_bytes = 0;
+    DevBuf<double> slab, mc, mr;
+    DevBuf<int64_t> soff;
+    DevBuf<int32_t> cmin, perm;
+    mutable DevBuf<double> z;
     Kind kind() const override { return Kind::Coarse; }
     bool is_precond() const override { return true; }
     void apply(double *out, const double *rhs) override;
@@ -545,6 +572,11 @@ struct MultigridOp : LinOp {
     void gather_fine(const double *rhs, hipStream_t s);
     // launch records of one V-cycle (eager, recorder on)
     std::vector<LaunchRec> cycle_plan();
+    // one of the fine level's fused launches exactly as the cycle makes it, on the
+    // cycle's workspace (which 0: folded residual + restriction into level 1's f
+    // and t; 1: interpolation + post-smoothing from level 1's v into out); false
+    // where the cycle does not take it (amg_multigrid_fine_launch: bench timing)
+    bool fine_launch(int which, double *out, const double *rhs);
     // renumber eligible levels (first ensure_workspace) / restore the caller's operators
     void reorder_levels();
     void undo_reorder();

@@ -461,7 +461,8 @@ void gtc_release(GpuCsr &m) {
     m.gtc_cls.release();
     m.gtc_dict.release();
     m.gtc_vtab.release();
-    m.gtc_ke = m.gtc_nce = m.gtc_ntab = 0;
+    m.gtc_kdz.release();
+    m.gtc_ke = m.gtc_nce = m.gtc_ntab = m.gtc_nclass = 0;
     m.gtc_r = m.gtc_on = false;
 }
 
@@ -523,7 +524,21 @@ bool gtc_attach(GpuCsr &m, const int64_t *fg, const int64_t *cg, int which) {
     FAMG_CHECK_HIP(hipMemcpyAsync(m.gtc_cls.get(), cls.data(), cls.size(), hipMemcpyHostToDevice, s));
     FAMG_CHECK_HIP(hipMemcpyAsync(m.gtc_dict.get(), hd.data(), hd.size() * 2, hipMemcpyHostToDevice, s));
     FAMG_CHECK_HIP(hipMemcpyAsync(m.gtc_vtab.get(), vt.data(), vt.size() * 8, hipMemcpyHostToDevice, s));
+    if (is_r && ke <= 255) {  // per class: where each fine plane's entries start (slots ascend in dz)
+        std::vector<uint8_t> kdz(dict.size() * 5);
+        for (size_t c = 0; c < dict.size(); c++) {
+            int k = 0;
+            for (int g = 0; g < 4; g++) {
+                kdz[c * 5 + g] = (uint8_t)k;
+                while (k < (int)dict[c].size() && dict[c][k].first / 16 == g) k++;
+            }
+            kdz[c * 5 + 4] = (uint8_t)dict[c].size();
+        }
+        m.gtc_kdz.resize(kdz.size());
+        FAMG_CHECK_HIP(hipMemcpyAsync(m.gtc_kdz.get(), kdz.data(), kdz.size(), hipMemcpyHostToDevice, s));
+    }
     FAMG_CHECK_HIP(hipStreamSynchronize(s));
+    m.gtc_nclass = (int)dict.size();
     m.gtc_ke = (int)ke;
     m.gtc_nce = (int)(dict.size() * ke);
     m.gtc_ntab = (int)vt.size();

@@ -564,6 +564,12 @@ bool gtx_attach(GpuCsr &m, const int64_t *fg, const int64_t *cg, int which) {
         m.gtx_cg[q] = cg[q];
     }
     m.gtx_r = is_r;
+    {  // the staging loops' float-reciprocal divisions, checked once at build
+        const int wx = wdim[0], wy = wdim[1], wz = wdim[2], tx = std::max(tile[0], 1), ty = std::max(tile[1], 1);
+        m.gtx_fdiv = fdiv_exact(wx * wy * wz + 256 * 8, wx, 1.0f / (float)wx) &&
+                     fdiv_exact((wx * wy * wz + 256 * 8) / wx + 1, wy, 1.0f / (float)wy) &&
+                     fdiv_exact(1024, tx, 1.0f / (float)tx) && fdiv_exact(1024 / tx + 1, ty, 1.0f / (float)ty);
+    }
     m.gtx_on = true;
     // keep the classes only where they beat the storage underneath (timed on
     // scratch vectors; R is charged with the d*f pass its SETDF epilogue saves):
@@ -613,10 +619,7 @@ void spmv_gtx(const GpuCsr &m, const double *x, double *y, SpmvMode mode, const 
     a.lox = m.gtx_lo[0]; a.loy = m.gtx_lo[1]; a.loz = m.gtx_lo[2];
     a.rwx = 1.0f / (float)a.wx; a.rwy = 1.0f / (float)a.wy;
     a.rtx = 1.0f / (float)std::max(a.tx, 1); a.rty = 1.0f / (float)std::max(a.ty, 1);
-    FAMG_REQUIRE(fdiv_exact(a.wx * a.wy * a.wz + 256 * 8, a.wx, a.rwx) &&
-                     fdiv_exact((a.wx * a.wy * a.wz + 256 * 8) / a.wx + 1, a.wy, a.rwy) &&
-                     fdiv_exact(1024, std::max(a.tx, 1), a.rtx) && fdiv_exact(1024 / std::max(a.tx, 1) + 1, std::max(a.ty, 1), a.rty),
-                 AMG_ERR_UNSUPPORTED, "wide grid-transfer classes: window too large for the float divisions");
+    FAMG_REQUIRE(m.gtx_fdiv, AMG_ERR_UNSUPPORTED, "wide grid-transfer classes: window too large for the float divisions");
     a.kz_lo = 0; a.kz_hi = a.kz; a.rz0 = 0; a.kz0 = 0; a.add_lo = a.add_hi = 0;
     if (m.rframe.on()) {
         a.rz = (int)m.rframe.nz;

@@ -338,11 +338,25 @@ void SgsOp::apply_in_place(double *rhs) {
 // ------------------------------------------------------------ coarse solve
 
 // Dense Cholesky on the host (setup) and the explicit inverse; the solve on the
-// device is one GEMV (8 n^2 bytes, L2/MALL resident for n <= ~2000).
+// device is one GEMV (8 n^2 bytes, L2/MALL resident for n <= ~2000).  Larger
+// coarsest levels (FAMG_COARSE_DENSE_MAX, default 8192 rows) take chol.hip's
+// envelope factor.
+static int64_t coarse_dense_max() {
+    static const int64_t v = [] {
+        const char *e = getenv("FAMG_COARSE_DENSE_MAX");
+        return e ? std::max<int64_t>(0, atoll(e)) : (int64_t)8192;
+    }();
+    return v;
+}
+
+std::shared_ptr<CoarseCholOp> make_coarse_chol_env(CsrOp &A);  // chol.hip
+void chol_env_apply(const CoarseCholOp &op, double *out, const double *rhs, hipStream_t s);
+
 std::shared_ptr<CoarseCholOp> make_coarse_chol(CsrOp &A) {
     FAMG_REQUIRE(A.nrows == A.ncols, AMG_ERR_DIM, "coarse solve: matrix must be square");
     const int64_t n = A.nrows;
-    FAMG_REQUIRE(n <= 8192, AMG_ERR_UNSUPPORTED, "coarse Cholesky limited to 8192 rows (dense)");
+    // above 8192 rows: the envelope Cholesky factor, block triangular solves (chol.hip)
+    if (n > coarse_dense_max()) return make_coarse_chol_env(A);
     std::vector<int64_t> rp(n + 1), col(A.m.nnz);
     std::vector<double> val(A.m.nnz);
     csr_to_host(A.m, rp.data(), col.data(), val.data());
@@ -393,7 +407,8 @@ std::shared_ptr<CoarseCholOp> make_coarse_chol(CsrOp &A) {
 
 void CoarseCholOp::apply(double *out, const double *rhs) {
     if (out == rhs) { LinOp::apply_in_place(out); return; }
-    dense_gemv(inv.get(), rhs, out, nrows, ctx->stream);
+    if (nb > 0) chol_env_apply(*this, out, rhs, ctx->stream);
+    else dense_gemv(inv.get(), rhs, out, nrows, ctx->stream);
 }
 
 // --------------------------------------------------------------- multigrid
@@ -614,52 +629,58 @@ void MultigridOp::cycle(int64_t l, double *v, const double *f, bool v_zero, doub
     // than the pass it saves (Q1 elasticity 1.57M rows: 640 vs 388 + 15 us).
     const bool fold = fold_level(A, D, P, fold_zero_guess, v_zero, steps);
     MgLevel &C = levels[l + 1];
-    if (fold) {
-        log_at(l, AMG_ROLE_RESID);
-        SpmvEpi epi;
-        epi.b = f;
-        epi.d = D->d.get();
-        epi.dc = D->dcode.get();  // DIA: 1-B codes of d gathered instead of d
-        epi.dt = D->dtab.get();
-        epi.dk = D->dconst;
-        spmv(A->m, f, L.r.get(), SPMV_RESID0, epi, s);  // work = f - A (d f)
-    } else {
-        smooth(l, v, t, f, v_zero, pre_df);
-        log_at(l, AMG_ROLE_RESID);
-        if (A) {
-            SpmvEpi epi;
-            epi.b = f;
-            spmv(A->m, v, L.r.get(), SPMV_RESID, epi, s);  // work = f - A v (:341-342)
-        } else {
-            L.A->apply(L.r.get(), v);
-            vec_sub(L.r.get(), f, L.r.get(), n, s);
-        }
-    }
     // R on grid-transfer classes (either width) also writes the next level's first Jacobi
     // step from zero (d_c * f_c, what smooth() would compute first) into the
     // buffer that step writes: one launch and 24 n_c bytes fewer, same values
     bool df = false;
+    auto *Rc = dynamic_cast<CsrOp *>(L.R.get());
+    SpmvEpi epic;  // the SETDF epilogue: level l + 1's d, y2 = d_c f_c
     if (l + 2 < (int64_t)levels.size() && restrict_df && setdf_enabled()) {
-        auto *Rc = dynamic_cast<CsrOp *>(L.R.get());
         auto *Ac = dynamic_cast<CsrOp *>(C.A.get());
         auto *Dc = dynamic_cast<DiagOp *>(C.S.get());
         auto *Pc = dynamic_cast<CsrOp *>(C.P.get());
         df = r_has_setdf(Rc) && Ac && Dc && steps >= 1 &&
              !fold_level(Ac, Dc, Pc, fold_zero_guess, true, steps);
         if (df) {
-            log_at(l, AMG_ROLE_RESTRICT);
-            SpmvEpi epi;
-            epi.d = Dc->d.get();
-            epi.dc = Dc->dcode.get();
-            epi.dt = Dc->dtab.get();
-            epi.dk = Dc->dconst;
-            epi.y2 = C.t.get();  // cycle(l + 1, C.v, ...) smooths into C.t first
-            spmv(Rc->m, L.r.get(), C.f.get(), SPMV_SETDF, epi, s);
+            epic.d = Dc->d.get();
+            epic.dc = Dc->dcode.get();
+            epic.dt = Dc->dtab.get();
+            epic.dk = Dc->dconst;
+            epic.y2 = C.t.get();  // cycle(l + 1, C.v, ...) smooths into C.t first
         }
     }
-    if (!df) {
+    SpmvEpi epi0;  // the folded residual's epilogue
+    if (fold) {
+        epi0.b = f;
+        epi0.d = D->d.get();
+        epi0.dc = D->dcode.get();  // DIA: 1-B codes of d gathered instead of d
+        epi0.dt = D->dtab.get();
+        epi0.dk = D->dconst;
+    }
+    if (fold && df && fine_resid_restrict_ok(A->m, Rc->m, epi0, epic)) {
+        // the folded residual and the restriction in one marching launch
+        // (fine.hip): r stays in LDS, f_c and d_c f_c land where SETDF writes them
+        log_at(l, AMG_ROLE_RESID);
+        fine_resid_restrict(A->m, Rc->m, f, D->dconst, C.f.get(), epic, s);
+    } else {
+        if (fold) {
+            log_at(l, AMG_ROLE_RESID);
+            spmv(A->m, f, L.r.get(), SPMV_RESID0, epi0, s);  // work = f - A (d f)
+        } else {
+            smooth(l, v, t, f, v_zero, pre_df);
+            log_at(l, AMG_ROLE_RESID);
+            if (A) {
+                SpmvEpi epi;
+                epi.b = f;
+                spmv(A->m, v, L.r.get(), SPMV_RESID, epi, s);  // work = f - A v (:341-342)
+            } else {
+                L.A->apply(L.r.get(), v);
+                vec_sub(L.r.get(), f, L.r.get(), n, s);
+            }
+        }
         log_at(l, AMG_ROLE_RESTRICT);
-        L.R->apply(C.f.get(), L.r.get());  // f_c = R work (:343)
+        if (df) spmv(Rc->m, L.r.get(), C.f.get(), SPMV_SETDF, epic, s);
+        else L.R->apply(C.f.get(), L.r.get());  // f_c = R work (:343)
     }
     for (int64_t k = 0; k < mu; k++) cycle(l + 1, C.v.get(), C.f.get(), k == 0, nullptr, df && k == 0);
     log_at(l, AMG_ROLE_INTERP);
@@ -670,6 +691,12 @@ void MultigridOp::cycle(int64_t l, double *v, const double *f, bool v_zero, doub
         epi.dc = D->dcode.get();
         epi.dt = D->dtab.get();
         epi.dk = D->dconst;
+        if (steps == 1 && fine_interp_jacobi_ok(A->m, P->m, epi)) {
+            // v = d f + P v_c and the post-smoothing step in one marching launch
+            // (fine.hip): v stays in LDS, the result lands in v0
+            fine_interp_jacobi(A->m, P->m, C.v.get(), f, D->dconst, v0, s);
+            return;
+        }
         spmv(P->m, C.v.get(), t, SPMV_ADD0, epi, s);  // v = d f + P v_c
         std::swap(v, t);                               // (where smooth() would have left v)
     } else if (P) {
@@ -681,6 +708,45 @@ void MultigridOp::cycle(int64_t l, double *v, const double *f, bool v_zero, doub
     smooth(l, v, t, f, false);  // post-smoothing (:361-369)
     log_at(l, AMG_ROLE_OTHER);
     if (v != v0) vec_copy(v0, v, n, s);
+}
+
+bool MultigridOp::fine_launch(int which, double *out, const double *rhs) {
+    std::lock_guard<std::mutex> lk(mtx);
+    ensure_workspace();
+    if (levels.size() < 3 || levels[0].permuted) return false;
+    MgLevel &L = levels[0], &C = levels[1];
+    auto *A = dynamic_cast<CsrOp *>(L.A.get());
+    auto *D = dynamic_cast<DiagOp *>(L.S.get());
+    auto *P = dynamic_cast<CsrOp *>(L.P.get());
+    auto *Rc = dynamic_cast<CsrOp *>(L.R.get());
+    if (!A || !D || !P || !Rc || !fold_level(A, D, P, fold_zero_guess, true, steps) || steps != 1) return false;
+    SpmvEpi epi0;
+    epi0.b = rhs;
+    epi0.d = D->d.get();
+    epi0.dc = D->dcode.get();
+    epi0.dt = D->dtab.get();
+    epi0.dk = D->dconst;
+    hipStream_t s = ctx->stream;
+    if (which == 1) {
+        if (!fine_interp_jacobi_ok(A->m, P->m, epi0)) return false;
+        fine_interp_jacobi(A->m, P->m, C.v.get(), rhs, D->dconst, out, s);
+        return true;
+    }
+    auto *Ac = dynamic_cast<CsrOp *>(C.A.get());
+    auto *Dc = dynamic_cast<DiagOp *>(C.S.get());
+    auto *Pc = dynamic_cast<CsrOp *>(C.P.get());
+    if (!(restrict_df && setdf_enabled() && r_has_setdf(Rc) && Ac && Dc &&
+          !fold_level(Ac, Dc, Pc, fold_zero_guess, true, steps)))
+        return false;
+    SpmvEpi epic;
+    epic.d = Dc->d.get();
+    epic.dc = Dc->dcode.get();
+    epic.dt = Dc->dtab.get();
+    epic.dk = Dc->dconst;
+    epic.y2 = C.t.get();
+    if (!fine_resid_restrict_ok(A->m, Rc->m, epi0, epic)) return false;
+    fine_resid_restrict(A->m, Rc->m, rhs, D->dconst, C.f.get(), epic, s);
+    return true;
 }
 
 // LinOp::apply for Multigrid (multigrid.rs:469-473 / init_cycle :251-267):

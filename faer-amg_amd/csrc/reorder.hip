@@ -33,8 +33,7 @@
 namespace famg {
 
 // RCM node order (new -> old) of the node graph of an n x n CSR (bs dofs per node)
-static std::vector<int32_t> rcm_order(const std::vector<int64_t> &rp, const std::vector<int32_t> &col, int64_t n,
-                                      int bs) {
+std::vector<int32_t> rcm_order(const std::vector<int64_t> &rp, const std::vector<int32_t> &col, int64_t n, int bs) {
     const int64_t N = n / bs;
     std::vector<int64_t> ap(N + 1, 0);
     std::vector<std::vector<int32_t>> nb(N);
@@ -53,23 +52,27 @@ static std::vector<int32_t> rcm_order(const std::vector<int64_t> &rp, const std:
     order.reserve(N);
     std::vector<uint8_t> seen(N, 0);
     std::vector<int32_t> lvl(N, -1);
+    // the start-node searches mark visits with a per-search epoch (one array for
+    // every search: O(component) per search, not O(N))
+    std::vector<int32_t> stamp(N, 0);
+    int32_t epoch = 0;
     auto bfs = [&](int32_t s, std::vector<int32_t> &out, bool mark) {
         // breadth-first from s, neighbours by ascending degree (Cuthill-McKee)
         std::vector<int32_t> q{s};
-        std::vector<uint8_t> *vis = &seen;
-        std::vector<uint8_t> tmp;
-        if (!mark) {
-            tmp.assign(N, 0);
-            vis = &tmp;
-        }
-        (*vis)[s] = 1;
+        ++epoch;
+        auto visited = [&](int32_t w) { return mark ? seen[w] != 0 : stamp[w] == epoch; };
+        auto visit = [&](int32_t w) {
+            if (mark) seen[w] = 1;
+            else stamp[w] = epoch;
+        };
+        visit(s);
         lvl[s] = 0;
         for (size_t h = 0; h < q.size(); h++) {
             const int32_t u = q[h];
             std::vector<int32_t> c;
             for (int32_t w : nb[u])
-                if (!(*vis)[w]) {
-                    (*vis)[w] = 1;
+                if (!visited(w)) {
+                    visit(w);
                     lvl[w] = lvl[u] + 1;
                     c.push_back(w);
                 }
@@ -80,6 +83,11 @@ static std::vector<int32_t> rcm_order(const std::vector<int64_t> &rp, const std:
     };
     for (int64_t s0 = 0; s0 < N; s0++) {
         if (seen[s0]) continue;
+        if (nb[s0].empty()) {  // an isolated node is its own component
+            seen[s0] = 1;
+            order.push_back((int32_t)s0);
+            continue;
+        }
         // a pseudo-peripheral start: twice the lowest-degree node of the last BFS level
         int32_t s = (int32_t)s0;
         for (int it = 0; it < 2; it++) {
@@ -253,16 +261,19 @@ void perm_scatter(double *out, const double *in, const int32_t *p, int64_t n, hi
 // How a storage sums a row: 0 one lane in stored order (3x3 blocks, SELL,
 // x-staged SELL), 1 a wave per row with a fixed lane split (wave-per-row), 2
 // depends on the row's neighbours (CSR-stream: the lanes per row follow the rows
-// its block holds).  A copy of the same kind sums bitwise like its original in
-// classes 0 and 1 whatever the row order, in class 2 with its rows in their
-// original order (only columns renamed: the same blocks).
+// its block holds), 3 a storage a renumbered copy cannot have (DIA, stencil or
+// grid-transfer classes, pattern SELL: they rely on the column order).  A copy of
+// the same kind sums bitwise like its original in classes 0 and 1 whatever the
+// row order, in class 2 with its rows in their original order (only columns
+// renamed: the same blocks), never in class 3.
 static int sum_class(const GpuCsr &m) {
     switch (m.kernel) {
     case SPMV_KERNEL_BSR:
     case SPMV_KERNEL_SELL:
     case SPMV_KERNEL_XS: return 0;
     case SPMV_KERNEL_VECTOR: return 1;
-    default: return 2;
+    case SPMV_KERNEL_STREAM: return 2;
+    default: return 3;
     }
 }
 
@@ -306,7 +317,7 @@ static CsrPtr csr_permuted(const CsrOp &A, const std::vector<int32_t> &rows_n2o,
     // see other rows or other slices), so every row sums in the same order
     P->m.no_bsr = m.no_bsr || !allow_bsr || !m.has_bsr();
     P->m.bsr_pin = !P->m.no_bsr;
-    P->m.kind_pin = (int8_t)sum_class(m);
+    P->m.kind_pin = (int8_t)std::min(sum_class(m), 2);  // (class 3 only in mode 2: CSR-stream)
     csr_finalize(P->m);
     P->nrows = n;
     P->ncols = m.ncols;
@@ -355,6 +366,11 @@ static bool level_bitwise(const MgLevel &L, const MgLevel *prev) {
         if (!op) continue;
         auto *c = dynamic_cast<const CsrOp *>(op);
         if (!c || sum_class(c->m) > 1) return false;
+    }
+    for (const LinOp *op : {L.R.get(), prev ? prev->P.get() : nullptr}) {
+        if (!op) continue;
+        auto *c = dynamic_cast<const CsrOp *>(op);
+        if (!c || sum_class(c->m) > 2) return false;
     }
     return true;
 }
@@ -455,13 +471,16 @@ void MultigridOp::reorder_levels() {
         }
     }
     FAMG_CHECK_HIP(hipStreamSynchronize(s));
-    if (reorder == 1) {  // a copy whose storage did not follow its original's: back out
+    if (reorder == 1) {  // a copy whose kernel did not follow its original's: back out
+        // (the exact kernel: a 3x3-block original rebuilt as SELL sums its
+        // zero-filled block slots differently, so the same class is not enough)
         bool same = true;
         for (auto &L : levels)
             for (auto pr : {std::make_pair(L.oA, L.A), std::make_pair(L.oR, L.R), std::make_pair(L.oP, L.P)}) {
                 if (!pr.first) continue;
-                same = same && sum_class(dynamic_cast<CsrOp *>(pr.first.get())->m) ==
-                                   sum_class(dynamic_cast<CsrOp *>(pr.second.get())->m);
+                const GpuCsr &a = dynamic_cast<CsrOp *>(pr.first.get())->m;
+                const GpuCsr &b = dynamic_cast<CsrOp *>(pr.second.get())->m;
+                same = same && a.kernel == b.kernel && a.has_bsr() == b.has_bsr() && sum_class(a) <= 2;
             }
         if (!same) {
             undo_reorder();

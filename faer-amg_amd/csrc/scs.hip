@@ -456,6 +456,11 @@ static void xscs_set_tile(GpuCsr &m, const int *t) {
     FAMG_CHECK_HIP(hipMemcpyAsync(m.xscs_lo.get(), lo.data(), Kp * 4, hipMemcpyHostToDevice, m.ctx->stream));
     FAMG_CHECK_HIP(hipStreamSynchronize(m.ctx->stream));
     for (int q = 0; q < 3; q++) m.xscs_t[q] = t[q];
+    // the staging loops divide by the window and tile extents through float
+    // reciprocals: checked once here, at storage build, not per launch
+    const int wz = t[2] + 2 * rz;
+    m.xscs_fdiv = fdiv_exact(wx * wy * wz, wx, 1.0f / (float)wx) && fdiv_exact(wy * wz, wy, 1.0f / (float)wy) &&
+                  fdiv_exact(1024, t[0], 1.0f / (float)t[0]) && fdiv_exact(1024 / t[0] + 1, t[1], 1.0f / (float)t[1]);
 }
 
 // Decompose the offsets into grid steps (dx, dy, dz) (centred residues), check
@@ -823,9 +828,7 @@ static void spmv_xscs(const GpuCsr &m, const double *x, double *y, SpmvMode mode
     const int ntz = (int)ceil_div(a.nz, a.tz);
     a.rwx = 1.0f / (float)a.wx; a.rwy = 1.0f / (float)a.wy;
     a.rtx = 1.0f / (float)a.tx; a.rty = 1.0f / (float)a.ty;
-    FAMG_REQUIRE(fdiv_exact(a.wx * a.wy * a.wz, a.wx, a.rwx) && fdiv_exact(a.wy * a.wz, a.wy, a.rwy) &&
-                     fdiv_exact(1024, a.tx, a.rtx) && fdiv_exact(1024 / a.tx + 1, a.ty, a.rty),
-                 AMG_ERR_UNSUPPORTED, "x-staged classes: window too large for the float divisions");
+    FAMG_REQUIRE(m.xscs_fdiv, AMG_ERR_UNSUPPORTED, "x-staged classes: window too large for the float divisions");
     a.zlo = 0; a.zhi = a.nz; a.add_lo = a.add_hi = 0;
     const SlabFrame &F = m.cframe;
     if (F.on()) {  // rank-local: the ghost planes below / above the owned ones

@@ -2575,6 +2575,12 @@ static bool dia_dk(const GpuCsr &m, const SpmvEpi &epi) {
     return epi.dc && epi.dk != 0.0 && dia_dk_enabled() && !m.dia_pat && dia_run7(m);
 }
 
+bool dia7_cst_dk(const GpuCsr &m, const SpmvEpi &epi) {
+    return m.kernel == SPMV_KERNEL_DIA && m.dia_cst && m.dia_k == 7 && dia_cst_enabled() && dia_dk(m, epi) &&
+           m.dia_vbits > 0 && m.dia_cw * 32 / m.dia_vbits >= 7 &&
+           m.nrows == (int64_t)m.dia_cst_n[0] * m.dia_cst_n[1] * m.dia_cst_n[2];
+}
+
 thread_local LaunchLog *g_launch_log = nullptr;
 
 // Launch-plan record of one spmv() call (amg_multigrid_cycle_plan): the storage

@@ -183,6 +183,7 @@ SIGNATURES = {
     "amg_gen_elasticity_q1": (i32, [i64, i64, i64, dbl, dbl, C.c_uint64, i32, P(vp)]),
     "amg_dist_pcg_solve": (i32, [vp, i32, vp, vp, i64, dbl, dbl, vp, P(i64)]),
     "amg_multigrid_cycle_plan": (i32, [vp, vp, i64, P(i64)]),
+    "amg_multigrid_fine_launch": (i32, [vp, i32, vp, vp]),
     "amg_dist_cycle_plan": (i32, [vp, vp, i64, P(i64)]),
     "amg_set_sgs_fused": (i32, [i32]),
     "amg_sgs_fused": (i32, [vp, P(i32)]),
@@ -518,7 +519,7 @@ class SparseMatOp(LinOp):
 
 FLAGS = {"fold_xscs": 0, "dia_dk": 1, "vec_wpr": 2, "gtx_time": 3, "sgs27_march": 4, "xs_pipe": 5, "bsr_kernel": 6,
          "bsr_long": 7,
-         "dia7_rp": 8}
+         "dia7_rp": 8, "fine_fuse": 9}
 
 
 def set_flag(name, value):
@@ -664,6 +665,24 @@ class Multigrid(LinOp):
         return (SparseMatOp(a, self.ctx), LinOp(s, self.ctx),
                 SparseMatOp(r, self.ctx) if r.value else None,
                 SparseMatOp(p, self.ctx) if p.value else None)
+
+    def fine_launch(self, which, out, rhs):
+        """One fused fine-level launch as the cycle makes it (amg_multigrid_fine_launch):
+        which 0 = residual + restriction, 1 = interpolation + post-smoothing; device
+        tensors, asynchronous on the context stream.  False where the cycle has none."""
+        import torch
+        n = self.nrows
+        for t in (rhs,) if out is None else (rhs, out):
+            if not (isinstance(t, torch.Tensor) and t.is_cuda and t.dtype == torch.float64 and t.is_contiguous()
+                    and t.numel() == n):
+                raise ValueError("fine_launch: contiguous float64 device vectors of the fine level's size")
+        st = _lib.amg_multigrid_fine_launch(self.h, int(which), None if out is None else C.c_void_p(out.data_ptr()),
+                                            C.c_void_p(rhs.data_ptr()))
+        if st == 0:
+            return True
+        if st == 3:  # AMG_ERR_UNSUPPORTED
+            return False
+        _ck(st)
 
     def reordered(self, l):
         """Whether level l runs in a renumbered (locality) numbering."""

@@ -132,7 +132,9 @@ amg_status amg_set_alloc_policy(int32_t policy);
  * the next 8 steps' node columns ahead (default 48, env FAMG_BSR_LONG; -1
  * never), 8 = row pairs per lane of the constant 7-point DIA kernel: 0 auto
  * (default: 2 for SET, 1 for the cycle's epilogues), 1, 2 or 4 adjacent 512-row
- * blocks per workgroup (env FAMG_DIA7_RP).  Setting one
+ * blocks per workgroup (env FAMG_DIA7_RP), 9 = the fine level of a constant
+ * 7-point box hierarchy as marching fused kernels (fine.hip): 0 = off, 1 = on
+ * (default), n >= 2 = n planes per workgroup (env FAMG_FINE_FUSE).  Setting one
  * makes every multigrid re-capture its hipGraph at its next apply.  amg_get_flag
  * reads the current value. */
 amg_status amg_set_flag(int32_t which, int64_t value);
@@ -359,6 +361,16 @@ typedef struct amg_launch_rec {
     char name[32];                     /* storage kernel ("dia", "sell_short", "dia_sgs", "vec_mul" ...) */
 } amg_launch_rec;
 amg_status amg_multigrid_cycle_plan(amg_linop *mg, amg_launch_rec *recs, int64_t cap, int64_t *count);
+/* One of the fine level's fused launches (no reference counterpart: the fused
+ * forms of multigrid.rs:341-343 and 349-369 on a constant 7-point box
+ * hierarchy, fine.hip), exactly as amg_multigrid_apply makes it, on the cycle's
+ * own workspace, asynchronous on the context stream: which 0 = the folded
+ * residual + restriction (rhs in; level 1's f and first Jacobi step written),
+ * 1 = interpolation + post-smoothing (rhs and level 1's v in; out written).
+ * Device pointers, n = the fine level's rows.  AMG_ERR_UNSUPPORTED where the
+ * cycle does not take that launch.  For timing the cycle's dominant kernels
+ * on their own (bench.py roofline). */
+amg_status amg_multigrid_fine_launch(amg_linop *mg, int32_t which, double *out, const double *rhs);
 /* The same for a distributed multigrid: one eager cycle (halo exchanges
  * included: collective, every rank calls it) on this rank's scratch vectors;
  * level = global level index (the redundant tail's levels after the

@@ -692,9 +692,69 @@ typedef struct {
     double *d;         /* diag smoother */
     int64_t *color;    /* sgs */
     int64_t ncolors;
-    double *L;         /* dense Cholesky factor */
+    double *L;         /* dense Cholesky factor (or the envelope factor's values) */
+    int64_t *ep, *fc;  /* envelope factor: row i holds columns fc[i] .. i at L + ep[i] */
     const orc_csr *M;  /* explicit smoother matrix (borrowed) */
 } orc_smoother;
+
+/* Envelope (profile) Cholesky A = L L^T for coarse levels above 4096 rows, in
+ * the given numbering: row i of L spans columns fc[i] .. i, fc[i] = its first
+ * nonzero of A (fill stays inside the envelope).  The reference's
+ * SparseCholeskySolve (coarse_solvers.rs:164-206) factors any size with faer's
+ * sparse LLt; a dense n^3 / 3 factor stops scaling at a few thousand rows. */
+static int orc_env_factor(const orc_csr *A, double **Lp, int64_t **epp, int64_t **fcp) {
+    const int64_t n = A->nrows;
+    int64_t *fc = (int64_t *)xmalloc((size_t)n * sizeof(int64_t));
+    int64_t *ep = (int64_t *)xmalloc((size_t)(n + 1) * sizeof(int64_t));
+    ep[0] = 0;
+    for (int64_t i = 0; i < n; i++) {
+        int64_t f = i;
+        for (int64_t e = A->rowptr[i]; e < A->rowptr[i + 1]; e++)
+            if (A->col[e] < f) f = A->col[e];
+        fc[i] = f;
+        ep[i + 1] = ep[i] + (i - f + 1);
+    }
+    double *L = (double *)xcalloc((size_t)ep[n], sizeof(double));
+    for (int64_t i = 0; i < n; i++)
+        for (int64_t e = A->rowptr[i]; e < A->rowptr[i + 1]; e++)
+            if (A->col[e] <= i) L[ep[i] + A->col[e] - fc[i]] += A->val[e];
+    for (int64_t i = 0; i < n; i++) {
+        double *li = L + ep[i] - fc[i];  /* li[j] = L_ij */
+        for (int64_t j = fc[i]; j < i; j++) {
+            const double *lj = L + ep[j] - fc[j];
+            const int64_t k0 = fc[i] > fc[j] ? fc[i] : fc[j];
+            double t = li[j];
+            for (int64_t k = k0; k < j; k++) t -= li[k] * lj[k];
+            li[j] = t / lj[j];
+        }
+        double d = li[i];
+        for (int64_t k = fc[i]; k < i; k++) d -= li[k] * li[k];
+        if (!(d > 0.0)) {
+            free(L); free(ep); free(fc);
+            return 1;
+        }
+        li[i] = sqrt(d);
+    }
+    *Lp = L;
+    *epp = ep;
+    *fcp = fc;
+    return 0;
+}
+
+static void orc_env_solve(int64_t n, const double *L, const int64_t *ep, const int64_t *fc, double *b) {
+    for (int64_t i = 0; i < n; i++) {
+        const double *li = L + ep[i] - fc[i];
+        double t = b[i];
+        for (int64_t k = fc[i]; k < i; k++) t -= li[k] * b[k];
+        b[i] = t / li[i];
+    }
+    for (int64_t i = n - 1; i >= 0; i--) {
+        const double *li = L + ep[i] - fc[i];
+        b[i] /= li[i];
+        const double x = b[i];
+        for (int64_t k = fc[i]; k < i; k++) b[k] -= li[k] * x;
+    }
+}
 
 struct orc_mg {
     int64_t nlevels, mu, steps;
@@ -723,6 +783,8 @@ static void free_smoother(orc_smoother *s) {
     free(s->d);
     free(s->color);
     free(s->L);
+    free(s->ep);
+    free(s->fc);
     memset(s, 0, sizeof(*s));
 }
 
@@ -771,6 +833,8 @@ int orc_mg_set_chol(orc_mg *mg, int64_t level) {
     free_smoother(s);
     const orc_csr *A = mg->A[level];
     int64_t n = A->nrows;
+    s->kind = ORC_SM_CHOL;
+    if (n > 4096) return orc_env_factor(A, &s->L, &s->ep, &s->fc);
     double *dense = (double *)xmalloc((size_t)(n * n) * sizeof(double));
     orc_csr_to_dense(A, dense);
     s->kind = ORC_SM_CHOL;
@@ -830,7 +894,8 @@ static void smoother_in_place(const orc_mg *mg, int64_t level, double *r) {
         orc_sgs_apply_in_place(mg->A[level], s->color, s->ncolors, r);
         break;
     case ORC_SM_CHOL:
-        orc_chol_solve(n, s->L, r);
+        if (s->ep) orc_env_solve(n, s->L, s->ep, s->fc, r);
+        else orc_chol_solve(n, s->L, r);
         break;
     case ORC_SM_CSR: {
         double *t = (double *)xmalloc((size_t)n * sizeof(double));

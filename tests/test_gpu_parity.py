@@ -291,6 +291,36 @@ def test_coarse_cholesky(ctx):
     assert ei.value.status == 4
 
 
+@pytest.mark.parametrize("dims", [(42, 42, 42), (21, 23, 25)])
+def test_coarse_cholesky_any_size(ctx, dims):
+    """The coarsest solve above 8192 rows (SparseCholeskySolve takes any size,
+    coarse_solvers.rs:164-206): the envelope Cholesky factor of the RCM-ordered
+    matrix in 64-row blocks (chol.hip).  42^3: a 2-level hierarchy whose
+    coarsest level has 9261 rows -- the V-cycle within 1e-11 of the oracle
+    (whose envelope factor keeps the natural order), the plan's coarse launch
+    the block solve.  21 x 23 x 25: the solve on the 7-point operator itself
+    (12075 rows, a ragged last block), A x = b to 1e-11."""
+    import torch
+    n = int(np.prod(dims))
+    if dims == (42, 42, 42):
+        A = fa().SparseMatOp.laplace3d_7pt(ctx, *dims)
+        mg = fa().sa_build_box(A, dims, (2, 2, 2), coarsest_dim=20000)
+        assert mg.levels() == 2 and mg.level(1)[0].nrows > 8192
+        b = np.random.default_rng(3).uniform(-1, 1, n)
+        z = torch.empty(n, dtype=torch.float64, device="cuda:0")
+        mg.apply(z, T(b))
+        ctx.synchronize()
+        zref = O.Multigrid(oracle_levels_from_gpu(mg, "jacobi")).apply(b)
+        assert np.linalg.norm(H(z) - zref) <= 1e-11 * np.linalg.norm(zref)
+        assert [p["name"] for p in mg.cycle_plan() if p["role"] == "coarse"] == ["chol-env"]
+        return
+    OA = O.laplace3d_7pt(*dims)
+    C = fa().CoarseCholesky(gpu_csr(ctx, OA))
+    b = np.random.default_rng(8).standard_normal(n)
+    x = apply_dev(ctx, C, b, n)
+    assert np.linalg.norm(OA.to_scipy() @ x - b) <= 1e-11 * np.linalg.norm(b)
+
+
 # ------------------------------------------------------------------- setup
 
 def csr_equal(G, Oc, exact=True, rtol=0.0):
@@ -1471,6 +1501,8 @@ def test_constant_diagonal_epilogues_bitwise(ctx):
             fa().set_flag("dia_dk", 1)
     assert np.array_equal(outs["1"].view(np.int64), outs["0"].view(np.int64))
     n = int(np.prod(dims))
+    if any(p["name"].startswith("fine-") for p in plans["1"]):
+        return  # the one-value d runs the fused fine-level kernels (test_fine_fused_bitwise)
     by = {p["mode"]: p["bytes"] for p in plans["1"]}
     by0 = {p["mode"]: p["bytes"] for p in plans["0"]}
     if "RESID0" in by and A.spmv_info()["kernel"] == "dia":
@@ -1502,7 +1534,14 @@ def test_cycle_plan_accounts_for_every_launch(ctx):
     n = A.nrows
     # the restriction is SETDF where it also writes level 1's first step d_1 f_1
     rmode = "SETDF" if any(p["mode"] == "SETDF" for p in f0) else "SET"
-    if "RESID0" in modes0:
+    names0 = [p["name"] for p in f0]
+    if "fine-pj" in names0:
+        # folded, with d f + P v_c and the post-smoothing Jacobi step as one
+        # marching launch (fine.hip): f, v_c and z cross HBM once
+        assert modes0[-1] == "-" and names0[-1] == "fine-pj", f0
+        assert f0[-1]["bytes"] == 17 * n + 8 * mg.level(1)[0].nrows, f0[-1]
+        assert modes0[:-1] in (["RESID0", rmode], ["-"]), f0
+    elif "RESID0" in modes0:
         # folded: RESID0 (f - A d f), R, ADD0 (d f + P v_c), post-smoothing Jacobi
         assert modes0 == ["RESID0", rmode, "ADD0", "JACOBI"], f0
         if info["kernel"] == "dia":  # 16 n: f read, r written; d = 6/omega everywhere is one scalar
@@ -1706,3 +1745,38 @@ def test_dia7_row_pairs_bitwise(ctx, dims):
     for rp in (2, 4, 0):
         for u, v in zip(outs[rp], outs[1]):
             assert np.array_equal(u.view(np.int64), v.view(np.int64)), rp
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dims", [(64, 64, 64), (66, 62, 50), (32, 48, 96), (256, 128, 8)])
+def test_fine_fused_bitwise(ctx, dims):
+    """The fine level of the constant 7-point box hierarchy as marching fused
+    kernels (fine.hip, flag fine_fuse): the folded residual r = f - A d f with
+    f_c = R r, d_c f_c in one launch (r in LDS), v = d f + P v_c with the
+    post-smoothing Jacobi step in another (v in LDS).  The V-cycle is bitwise
+    the four-launch cycle's (constant 7-point DIA RESID0, k_gtc_restrict_march
+    SETDF, k_gtc_interp ADD0, the constant 7-point DIA JACOBI) for
+    every run length of planes per workgroup -- ragged x/y tiles (66 x 62), odd
+    coarse plane counts (50 -> 25) and chunk ends included -- and within 1e-11
+    of the oracle."""
+    import torch
+    n = int(np.prod(dims))
+    b = T(np.random.default_rng(11).uniform(-1, 1, n))
+    A = fa().SparseMatOp.laplace3d_7pt(ctx, *dims)
+    mg = fa().sa_build_box(A, dims, (2, 2, 2), coarsest_dim=100)
+    outs = {}
+    try:
+        for ff in (0, 1, 2, 6, 1000):
+            fa().set_flag("fine_fuse", ff)
+            z = torch.full_like(b, np.nan)
+            mg.apply(z, b)
+            ctx.synchronize()
+            outs[ff] = H(z)
+            names = [p["name"] for p in mg.cycle_plan() if p["level"] == 0]
+            assert ("fine-pj" in names) == (ff != 0) and ("fine-rr" in names) == (ff != 0), (ff, names)
+    finally:
+        fa().set_flag("fine_fuse", 1)
+    for ff in (1, 2, 6, 1000):
+        assert np.array_equal(outs[ff].view(np.int64), outs[0].view(np.int64)), ff
+    zref = O.Multigrid(oracle_levels_from_gpu(mg, "jacobi")).apply(H(b))
+    assert np.linalg.norm(outs[1] - zref) <= 1e-11 * np.linalg.norm(zref)

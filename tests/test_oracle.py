@@ -330,3 +330,18 @@ def test_splitmix_stream():
     assert np.array_equal(splitmix_uniform(50, 42), seq(42, 50))
     u = splitmix_uniform(100000, 42)
     assert -1 <= u.min() < -0.99 and 0.99 < u.max() < 1 and abs(u.mean()) < 0.01
+
+
+def test_oracle_envelope_cholesky_large():
+    """The oracle's coarsest solve above 4096 rows: the envelope (profile)
+    Cholesky factor in the natural order (coarse_solvers.rs:164-206 takes any
+    size; a dense n^3/3 factor does not scale) -- A x = b to 1e-12 against
+    scipy's sparse direct solve, and the dense path below the threshold."""
+    import scipy.sparse.linalg as spla
+    for dims in ((17, 19, 21), (10, 10, 10)):
+        A = O.laplace3d_7pt(*dims)
+        S = A.to_scipy().tocsc()
+        b = np.random.default_rng(5).standard_normal(A.nrows)
+        x = O.Multigrid([{"A": A, "smoother": "chol"}]).apply(b)
+        xs = spla.spsolve(S, b)
+        assert np.linalg.norm(x - xs) <= 1e-12 * np.linalg.norm(xs), dims
