@@ -919,7 +919,8 @@ def run_dist(args, world, rank, local_rank):
         c4 = {"global_vcycles_per_s": round(cycles_per_s, 3), "one_gpu_512_vcycles_per_s": round(base, 3),
               "ratio_vs_1gpu": ratio, "gpus": world,
               "what": "512^3 7-pt (C4): V-cycles/s of this row-split run / V-cycles/s of the same "
-                      "hierarchy on one GPU (single-GPU path, measured in this job by rank 0)"}
+                      "hierarchy on one GPU (single-GPU path, measured in this job by rank 0)",
+              "mall_caveat": C4_MALL_CAVEAT}
     out = dist_line(args, world, dims, strong, ms_per_cycle, cycles_per_s, ratio, c4, single, cpu, parity,
                     extra={"levels": nl, "level_plan_rank0": infos, "setup_s": round(setup_s, 2),
                            "fine_spmv_with_halo_ms": round(halo_ms, 4),
@@ -946,6 +947,12 @@ def run_dist(args, world, rank, local_rank):
     return out if rank == 0 else None
 
 
+C4_MALL_CAVEAT = ("the one-GPU 512^3 base streams 1.07 GB vectors through a 256 MB MALL (cold), while each "
+                  "rank of an N-GPU run holds a 256^3-sized slab whose vectors largely stay MALL-resident: "
+                  "ratio_vs_1gpu can exceed N from cache alone; per_rank_vs_256cubed_single compares against "
+                  "the MALL-warm 256^3 single-GPU rate instead")
+
+
 DIST_LINE_KEYS = ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better",
                   "scaling", "vs_baseline", "ratio_vs_1gpu", "ratio_vs_1gpu_what", "dtype", "data", "config",
                   "fine_spmv_gbs", "roofline", "cpu_baseline", "parity")
@@ -957,6 +964,13 @@ def dist_line(args, world, dims, strong, ms_per_cycle, cycles_per_s, ratio, c4, 
     or x N (weak: 256^3-equivalent cycles/s of the whole job); ratio_vs_1gpu = the
     global rate over the same global problem's one-GPU rate (at 512^3 the C4
     strong-scaling ratio); cpu_baseline / parity from the oracle on rank 0."""
+    base256 = None
+    if single:
+        base256 = single.get("single_256_vcycles_per_s")
+        if base256 is None and tuple(dims) == (256, 256, 256):
+            base256 = single.get("vcycles_per_s")
+    per_rank = (round(cycles_per_s * world / base256, 4)
+                if cycles_per_s is not None and base256 and world > 1 else None)
     out = {
         "metric": METRIC,
         "value": None if cycles_per_s is None else round(cycles_per_s if strong else cycles_per_s * world, 3),
@@ -980,6 +994,12 @@ def dist_line(args, world, dims, strong, ms_per_cycle, cycles_per_s, ratio, c4, 
                             if strong else f"; weak scaling: {world} x {args.edge}^3 rows, "
                                            f"value = global V-cycles/s x {world}"),
                         "c4_strong": c4,
+                        "per_rank_vs_256cubed_single": per_rank,
+                        "per_rank_vs_256cubed_single_what": (
+                            f"global V-cycles/s x {world} / V-cycles/s of the 256^3 problem on one GPU "
+                            f"({base256}, rank 0 in this job): per-GPU efficiency against a single GPU running "
+                            f"the same 256^3-sized workload each rank holds -- the fair read of the weak "
+                            f"series (both MALL-warm)"),
                         "single_gpu_same_problem": single,
                         "global_vcycles_per_s": None if cycles_per_s is None else round(cycles_per_s, 3),
                         "parallelism": f"row-block "
@@ -1068,7 +1088,35 @@ def dist_single_side(fa, ctx, args, stream, dims, z_dist, hist_dist, cycles=10):
     del mg, A
     import torch
     torch.cuda.synchronize()
+    base256 = single_256_base(fa, ctx, args, stream, dims)
+    if base256 and out[0] is not None and "error" not in out[0]:
+        out[0]["single_256_vcycles_per_s"] = base256
     return out
+
+
+def single_256_base(fa, ctx, args, stream, dims):
+    """V-cycles/s of the 256^3 problem on this one GPU (the per-GPU workload of
+    the weak series): the base of per_rank_vs_256cubed_single.  Skipped when the
+    global problem is 256^3 itself (its single-GPU rate is that base)."""
+    import torch
+    if args.problem != "7pt" or tuple(dims) == (256, 256, 256):
+        return None
+    try:
+        a = argparse.Namespace(**vars(args))
+        a.edge = 256
+        A, mg = build_problem(fa, ctx, a, (256, 256, 256))
+        b = torch.as_tensor(splitmix_uniform(A.nrows, 42), device=torch.cuda.current_device())
+        z = torch.empty_like(b)
+        for _ in range(3):
+            mg.apply(z, b)
+        ms = time_kernel(lambda: mg.apply(z, b), 20, stream)
+        del mg, A, b, z
+        torch.cuda.synchronize()
+        log(f"single-GPU 256^3 base: {1000.0 / ms:.1f} V-cycles/s")
+        return round(1000.0 / ms, 3)
+    except Exception as e:  # reported as missing, never fatal
+        log(f"single-GPU 256^3 base failed: {e!r}")
+        return None
 
 
 def single_side(fa, args, stream, A, mg, dims, z_dist, hist_dist, cycles=10, what="the distributed GPU run"):
@@ -1182,13 +1230,19 @@ def run_loopback(args):
     torch.cuda.synchronize()
     single, cpu, parity = single_side(fa, args, stream, A, mg, dims, z_dist, np.asarray(hists[0]), 10,
                                       what=f"the {N}-rank loopback run")
+    del mg, A
+    torch.cuda.synchronize()
+    base256 = single_256_base(fa, ctx, args, stream, dims)
+    if base256:
+        single["single_256_vcycles_per_s"] = base256
     cps = 1000.0 / ms
     ratio = round(cps / single["vcycles_per_s"], 3)
     c4 = None
     if dims == (512, 512, 512) and args.problem == "7pt":
         c4 = {"global_vcycles_per_s": round(cps, 3), "one_gpu_512_vcycles_per_s": single["vcycles_per_s"],
               "ratio_vs_1gpu": ratio, "gpus": 1, "virtual_ranks": N,
-              "what": "loopback rehearsal: N virtual ranks time-share one GPU (not a scaling figure)"}
+              "what": "loopback rehearsal: N virtual ranks time-share one GPU (not a scaling figure)",
+              "mall_caveat": C4_MALL_CAVEAT}
     return dist_line(args, N, dims, strong, ms, cps, ratio, c4, single, cpu, parity,
                      extra={"levels": nl, "level_plan_rank0": infos, "setup_s": round(setup_s, 2),
                             "rel_residual_after_1_cycle": float(hists[0][1]) if len(hists[0]) > 1 else None,

@@ -12,6 +12,7 @@
 // row class kernel with the same lane split and butterfly), so every column is
 // bitwise the single-vector SpMV.  Column-major X, Y with leading dimensions.
 #include <algorithm>
+#include <type_traits>
 
 #include "famg.hpp"
 
@@ -198,6 +199,126 @@ __global__ __launch_bounds__(256) void spmm_bsr3_kernel(SpmmBsrArgs a) {
     }
 }
 
+// ------------------------------------------------------------ x-staged SELL
+
+struct SpmmXsArgs {
+    const char *data;       // per slice: values (w x 64 fp64) then indices (w x 64 u16 / i32)
+    const uint32_t *desc;   // per slice: byte offset / 128 | mode << 30 (1: LDS index, 2: global column)
+    const int32_t *soff;    // per slice: first step (+1 sentinel)
+    const int32_t *coff;    // per group: first staged chunk (+1 sentinel)
+    const int32_t *chunks;  // staged chunk ids
+    int32_t nrows, nslices;
+    const double *x;
+    int64_t ldx;
+    double *y;
+    int64_t ldy;
+};
+
+// one row per lane (xs_walk's order: the row's stored steps ascending, fma from
+// 0.0); the 16-bit LDS index of a staged slice is turned back into its global
+// column (chunk id * 64 + index % 64) and the k columns' x gathered through the
+// caches -- the matrix streams once per 8 columns.  A wave per slice, 16 per group.
+template <int KB>
+__global__ __launch_bounds__(256) void spmm_xs_kernel(SpmmXsArgs a) {
+    const int sl = __builtin_amdgcn_readfirstlane(xcd_remap(blockIdx.x, gridDim.x) * 4 + (int)(threadIdx.x >> 6));
+    if (sl >= a.nslices) return;
+    const int lane = threadIdx.x & 63, row = sl * 64 + lane;
+    const uint32_t dsc = a.desc[sl];
+    const int mode = (int)(dsc >> 30);
+    const char *blk = a.data + (int64_t)(dsc & 0x3fffffffu) * 128;
+    const int t0 = a.soff[sl], w = a.soff[sl + 1] - t0;
+    const int32_t *ch = a.chunks + a.coff[sl / 64];
+    double acc[KB];
+#pragma unroll
+    for (int c = 0; c < KB; c++) acc[c] = 0.0;
+    for (int t = 0; t < w; t++) {
+        const double v = __builtin_nontemporal_load(reinterpret_cast<const double *>(blk) + (int64_t)t * 64 + lane);
+        int64_t col;
+        if (mode == 1) {
+            const int ix = reinterpret_cast<const uint16_t *>(blk + (int64_t)w * 512)[(int64_t)t * 64 + lane];
+            col = (int64_t)ch[ix >> 6] * 64 + (ix & 63);
+        } else {
+            col = reinterpret_cast<const int32_t *>(blk + (int64_t)w * 512)[(int64_t)t * 64 + lane];
+        }
+#pragma unroll
+        for (int c = 0; c < KB; c++) acc[c] = fma(v, a.x[col + c * a.ldx], acc[c]);
+    }
+    if (row < a.nrows) {
+#pragma unroll
+        for (int c = 0; c < KB; c++) a.y[row + c * a.ldy] = acc[c];
+    }
+}
+
+// ------------------------------------------------------------- pattern SELL
+
+struct SpmmSellpArgs {
+    const char *vals;
+    const int64_t *eoff;
+    const int32_t *row0;
+    const int2 *pat;
+    const int32_t *offs;
+    const int32_t *rbase;
+    const double *vtab;
+    int32_t ntab, nslices, ncols;
+    const double *x;
+    int64_t ldx;
+    double *y;
+    int64_t ldy;
+};
+
+// spmv_sellp_kernel's sums per column: lane q of a row walks its steps t = s L + q
+// ascending with fma (fp64 values or 4/8-bit codes from the LDS table), padding
+// steps +0.0 at a clamped column, then the same xor butterfly over the L lanes.
+// A wave per slice.
+template <int L, int VB, int KB>
+__global__ __launch_bounds__(256) void spmm_sellp_kernel(SpmmSellpArgs a) {
+    __shared__ double stab[VB ? 256 : 1];
+    if constexpr (VB != 0) {
+        for (int i = threadIdx.x; i < a.ntab; i += 256) stab[i] = a.vtab[i];
+        __syncthreads();
+    }
+    const int s = __builtin_amdgcn_readfirstlane(xcd_remap(blockIdx.x, gridDim.x) * 4 + (int)(threadIdx.x >> 6));
+    if (s >= a.nslices) return;
+    const int lane = threadIdx.x & 63, r = lane / L, q = lane % L;
+    const int row = a.row0[s] + r;
+    const bool live = row < a.row0[s + 1];
+    const int rowc = live ? row : a.row0[s];
+    const int base = a.rbase ? a.rbase[rowc] : rowc;
+    const int2 pw = a.pat[s];
+    const int32_t *off = a.offs + pw.x;
+    const int w = pw.y, S = (w + L - 1) / L;
+    const int64_t e0 = a.eoff[s];
+    double acc[KB];
+#pragma unroll
+    for (int c = 0; c < KB; c++) acc[c] = 0.0;
+    // codes: whole words of K lane-steps, as spmv_sellp_kernel walks them
+    const int send = VB == 0 ? S : (S + 32 / (VB ? VB : 1) - 1) / (32 / (VB ? VB : 1)) * (32 / (VB ? VB : 1));
+    for (int st = 0; st < send; st++) {
+        const int t = st * L + q;
+        const bool in = t < w;
+        const int64_t col = min(max(base + off[in ? t : 0], 0), a.ncols - 1);
+        double v;
+        if constexpr (VB == 0) {
+            v = __builtin_nontemporal_load(reinterpret_cast<const double *>(a.vals) + e0 + (int64_t)st * 64 + lane);
+        } else {
+            constexpr int K = 32 / VB;
+            const uint32_t wd = reinterpret_cast<const uint32_t *>(a.vals)[e0 + (int64_t)(st / K) * 64 + lane];
+            v = stab[(wd >> ((st % K) * VB)) & ((1u << VB) - 1)];
+        }
+        v = in ? v : 0.0;
+#pragma unroll
+        for (int c = 0; c < KB; c++) acc[c] = fma(v, (L > 1 || VB == 0 || in) ? a.x[col + c * a.ldx] : 0.0, acc[c]);
+    }
+#pragma unroll
+    for (int c = 0; c < KB; c++)
+#pragma unroll
+        for (int m = L / 2; m > 0; m >>= 1) acc[c] += __shfl_xor(acc[c], m);
+    if (live && q == 0) {
+#pragma unroll
+        for (int c = 0; c < KB; c++) a.y[row + c * a.ldy] = acc[c];
+    }
+}
+
 // ------------------------------------------------------------------ dispatch
 
 #define FAMG_SPMM_KB(KB_EXPR, LAUNCH)                                                              \
@@ -219,7 +340,12 @@ bool spmm_compressed(const GpuCsr &m, const double *x, int64_t ldx, double *y, i
                      m.dia_r1 == m.nrows && m.dia_k <= 64;
     const bool scs = m.kernel == SPMV_KERNEL_SCS && m.has_scs() && m.scs_seg < 0;
     const bool bsr = m.kernel == SPMV_KERNEL_BSR && m.has_bsr();
-    if (!dia && !scs && !bsr) return false;
+    const bool xs = m.kernel == SPMV_KERNEL_XS && m.has_xs();
+    const int sL = m.sellp_L, sV = m.sellp_vbits;
+    const bool sellp = m.kernel == SPMV_KERNEL_SELLP && m.has_sellp() && m.sellp_seg_slc.size() <= 2 &&
+                       (sL == 1 || sL == 2 || sL == 4 || sL == 8 || sL == 16 || sL == 32 || sL == 64) &&
+                       (sV == 0 || sV == 4 || sV == 8);
+    if (!dia && !scs && !bsr && !xs && !sellp) return false;
     if (m.nrows == 0 || k == 0) return true;
     for (int64_t c0 = 0; c0 < k; c0 += SPMM_COLS) {
         const int kb = (int)std::min<int64_t>(SPMM_COLS, k - c0);
@@ -276,6 +402,48 @@ bool spmm_compressed(const GpuCsr &m, const double *x, int64_t ldx, double *y, i
                 if (m.scs_ib == 1) { FAMG_SPMM_KB(kb, FAMG_S1) }
                 else { FAMG_SPMM_KB(kb, FAMG_S2) }
             }
+        } else if (xs) {
+            const int32_t ns = (int32_t)ceil_div(m.nrows, 64);
+            SpmmXsArgs a{m.xs_data.get(), m.xs_desc.get(), m.xs_soff.get(), m.xs_coff.get(), m.xs_chunks.get(),
+                         (int32_t)m.nrows, ns, xc, ldx, yc, ldy};
+            const dim3 grid((unsigned)ceil_div(ns, 4)), block(256);
+#define FAMG_X(KB) spmm_xs_kernel<KB><<<grid, block, 0, s>>>(a)
+            FAMG_SPMM_KB(kb, FAMG_X)
+        } else if (sellp) {
+            SpmmSellpArgs a{m.sellp_vals.get(), m.sellp_eoff.get(), m.sellp_row0.get(),
+                            reinterpret_cast<const int2 *>(m.sellp_pat.get()), m.sellp_offs.get(), m.sellp_rbase.get(),
+                            m.sellp_vtab.get(), (int32_t)m.sellp_ntab, (int32_t)m.sellp_slices, (int32_t)m.ncols,
+                            xc, ldx, yc, ldy};
+            const dim3 grid((unsigned)ceil_div(m.sellp_slices, 4)), block(256);
+#define FAMG_P(L, VB, KB) spmm_sellp_kernel<L, VB, KB><<<grid, block, 0, s>>>(a)
+#define FAMG_PL(L, VB)                                                                              \
+    {                                                                                               \
+        auto go = [&](auto kbc) { FAMG_P(L, VB, decltype(kbc)::value); };                           \
+        switch (kb) {                                                                               \
+        case 1: go(std::integral_constant<int, 1>{}); break;                                        \
+        case 2: go(std::integral_constant<int, 2>{}); break;                                        \
+        case 3: go(std::integral_constant<int, 3>{}); break;                                        \
+        case 4: go(std::integral_constant<int, 4>{}); break;                                        \
+        case 5: go(std::integral_constant<int, 5>{}); break;                                        \
+        case 6: go(std::integral_constant<int, 6>{}); break;                                        \
+        case 7: go(std::integral_constant<int, 7>{}); break;                                        \
+        default: go(std::integral_constant<int, 8>{}); break;                                       \
+        }                                                                                           \
+    }
+#define FAMG_PV(L)                                                                                  \
+    if (sV == 0) FAMG_PL(L, 0) else if (sV == 4) FAMG_PL(L, 4) else FAMG_PL(L, 8)
+            switch (sL) {
+            case 1: FAMG_PV(1) break;
+            case 2: FAMG_PV(2) break;
+            case 4: FAMG_PV(4) break;
+            case 8: FAMG_PV(8) break;
+            case 16: FAMG_PV(16) break;
+            case 32: FAMG_PV(32) break;
+            default: FAMG_PV(64) break;
+            }
+#undef FAMG_PV
+#undef FAMG_PL
+#undef FAMG_P
         } else {
             SpmmBsrArgs a{m.bsr_data.get(), m.bsr_row0.get(), m.bsr_soff.get(), (int32_t)m.bsr_slices,
                           xc, ldx, yc, ldy};

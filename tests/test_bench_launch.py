@@ -40,6 +40,7 @@ def test_launcher_spawns_n_ranks_and_forwards_one_line(n):
     for k in ("ratio_vs_1gpu", "cpu_baseline", "parity", "roofline"):
         assert k in d
     assert d["scaling"] == "weak" and "single_gpu_same_problem" in d["config"]
+    assert "per_rank_vs_256cubed_single" in d["config"]
     assert "torch.distributed.run" in p.stderr  # the launcher logged its child command
 
 
@@ -63,3 +64,20 @@ def test_launcher_counts_gpus_without_torch():
     import bench
     src = __import__("inspect").getsource(bench.visible_gpus)
     assert "torch" not in src.split('"""')[2]
+
+
+def test_dist_line_per_rank_vs_256cubed_single():
+    """The N > 1 line's per-GPU efficiency against the MALL-warm 256^3 single-GPU
+    rate (verdict r05 item 7): global V-cycles/s x N / the 256^3 one-GPU rate
+    rank 0 measures; and the C4 block's MALL caveat text exists."""
+    import argparse
+    import bench
+    args = argparse.Namespace(steps=5, warmup=1, problem="7pt", edge=256, box=2, smoother="jacobi")
+    single = {"vcycles_per_s": 150.0, "single_256_vcycles_per_s": 1500.0}
+    d = bench.dist_line(args, 8, (512, 512, 512), False, 5.0, 200.0, 1.33, None, single, None, None, {}, {})
+    assert d["value"] == 1600.0
+    assert abs(d["config"]["per_rank_vs_256cubed_single"] - 200.0 * 8 / 1500.0) < 1e-3
+    assert "MALL" in bench.C4_MALL_CAVEAT
+    d1 = bench.dist_line(args, 2, (256, 256, 512), False, 5.0, 700.0, 1.9, None, {"vcycles_per_s": 760.0},
+                         None, None, {}, {})
+    assert d1["config"]["per_rank_vs_256cubed_single"] is None  # no 256^3 base measured

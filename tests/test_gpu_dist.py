@@ -575,10 +575,15 @@ def test_dist_one_rank_runs_the_single_gpu_kernels():
     dims = (64, 64, 64)
     b = np.random.default_rng(17).uniform(-1, 1, int(np.prod(dims)))
     os.environ["FAMG_XSCS_VS_DIA"] = "1"  # A_1: no timed DIA-vs-classes choice (noise could flip it)
+    # the single-GPU cycle's fused fine-level kernels (fine.hip) have no
+    # distributed form: compare against the unfused single-GPU plan (bitwise the
+    # fused one, test_fine_fused_bitwise)
+    fa().set_flag("fine_fuse", 0)
     try:
         z, res = slab_run(1, dims, 100, 1000, b)
     finally:
         del os.environ["FAMG_XSCS_VS_DIA"]
+        fa().set_flag("fine_fuse", 1)
     _, _, _, local, glob, plan, gplan, zg, La = res[0]
     assert La >= 3
     assert local == [g for g in glob[:La]], (local, glob)

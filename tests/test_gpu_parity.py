@@ -1454,20 +1454,27 @@ def test_gtc_restrict_setdf(ctx, gen, dims, smoother):
     launch.  The cycle is bitwise the one with the separate d*f pass (coded,
     constant and fp64 diagonals of the level-1 smoother), one launch shorter per
     such level, and within 1e-11 of the oracle's cycle."""
-    A = (fa().SparseMatOp.laplace3d_7pt(ctx, *dims) if gen == "7pt"
-         else fa().SparseMatOp.aniso27(ctx, *dims, 1.0, 1.0, 0.01))
-    mg = fa().sa_build_box(A, dims, (2, 2, 2), coarsest_dim=60, smoother=smoother)
-    assert mg.level(0)[2].spmv_info()["gtc_kind"] == "gtc"
-    plan = mg.cycle_plan()
-    assert any(p["mode"] == "SETDF" and p["level"] == 0 for p in plan), [(p["level"], p["name"], p["mode"]) for p in plan]
-    b = np.random.default_rng(44).uniform(-1, 1, A.nrows)
-    z = apply_dev(ctx, mg, b, A.nrows)
-    mg.set_restrict_df(False)
+    # (the 7-point fine level otherwise runs fused with its residual, fine.hip:
+    # test_fine_fused_bitwise; here the grid-transfer restriction itself)
+    fa().set_flag("fine_fuse", 0)
     try:
-        z0 = apply_dev(ctx, mg, b, A.nrows)
-        plan0 = mg.cycle_plan()
+        A = (fa().SparseMatOp.laplace3d_7pt(ctx, *dims) if gen == "7pt"
+             else fa().SparseMatOp.aniso27(ctx, *dims, 1.0, 1.0, 0.01))
+        mg = fa().sa_build_box(A, dims, (2, 2, 2), coarsest_dim=60, smoother=smoother)
+        assert mg.level(0)[2].spmv_info()["gtc_kind"] == "gtc"
+        plan = mg.cycle_plan()
+        assert any(p["mode"] == "SETDF" and p["level"] == 0 for p in plan), [(p["level"], p["name"], p["mode"])
+                                                                           for p in plan]
+        b = np.random.default_rng(44).uniform(-1, 1, A.nrows)
+        z = apply_dev(ctx, mg, b, A.nrows)
+        mg.set_restrict_df(False)
+        try:
+            z0 = apply_dev(ctx, mg, b, A.nrows)
+            plan0 = mg.cycle_plan()
+        finally:
+            mg.set_restrict_df(True)
     finally:
-        mg.set_restrict_df(True)
+        fa().set_flag("fine_fuse", 1)
     assert not any(p["mode"] == "SETDF" for p in plan0)
     assert len(plan0) > len(plan)
     assert np.array_equal(z.view(np.int64), z0.view(np.int64))
@@ -1780,3 +1787,29 @@ def test_fine_fused_bitwise(ctx, dims):
         assert np.array_equal(outs[ff].view(np.int64), outs[0].view(np.int64)), ff
     zref = O.Multigrid(oracle_levels_from_gpu(mg, "jacobi")).apply(H(b))
     assert np.linalg.norm(outs[1] - zref) <= 1e-11 * np.linalg.norm(zref)
+
+
+def test_spmm_xsell_and_pattern_sell(ctx):
+    """f2 on the two storages that applied per column before (verdict r05 item
+    8): x-staged SELL (the random-coefficient 7-point operator, rows shuffled in
+    windows of 4096) and pattern SELL (R / P / A of the box hierarchy's coarse
+    levels: fp64 values with 8-64 lanes per row, 4/8-bit codes with one) -- one
+    matrix stream per 8 columns, every column bitwise the single-vector kernel
+    for k in {1, 3, 8, 32}."""
+    seen = set()
+    # (x-staged SELL is built from 512 row groups of 4096 up: >= 2.1M rows)
+    mats = [fa().SparseMatOp.random7(ctx, 128, 128, 128, seed=3, window=4096),
+            fa().SparseMatOp.random7(ctx, 136, 128, 124, seed=4, window=4096)]
+    dims = (128, 128, 128)
+    A = fa().SparseMatOp.laplace3d_7pt(ctx, *dims)
+    mg = fa().sa_build_box(A, dims, (2, 2, 2), coarsest_dim=500)
+    for l in range(mg.levels()):
+        Al, _, Rl, Pl = mg.level(l)
+        mats += [M for M in (Al, Rl, Pl) if M is not None and M.spmv_info()["kernel"] in ("xsell", "sellp")]
+    for M in mats:
+        info = M.spmv_info()
+        if info["kernel"] not in ("xsell", "sellp"):
+            continue
+        seen.add(info["kernel"])
+        _spmm_vs_spmv(ctx, M, ks=(1, 3, 8, 32))
+    assert {"xsell", "sellp"} <= seen, seen
