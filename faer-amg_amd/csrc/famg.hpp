@@ -347,6 +347,8 @@ void spmv_bsr(const GpuCsr &m, const double *x, double *y, SpmvMode mode, const 
 void spmv_scs(const GpuCsr &m, const double *x, double *y, SpmvMode mode, const SpmvEpi &epi, hipStream_t s,
               int64_t seg);
 bool xs_supports(SpmvMode mode);
+// Y = A X over k columns on x-staged SELL (xsell.hip); false for other storages
+bool spmm_xs(const GpuCsr &m, const double *x, int64_t ldx, double *y, int64_t ldy, int64_t k, hipStream_t s);
 // the constant 7-point DIA kernel with a one-value Jacobi diagonal takes m's
 // JACOBI / RESID0 launches (spmv.hip: no codes read, d = epi.dk)
 bool dia7_cst_dk(const GpuCsr &m, const SpmvEpi &epi);

@@ -30,6 +30,15 @@
 
 namespace famg {
 
+// A workgroup barrier that orders LDS only: __syncthreads() also waits for every
+// outstanding global load, which would drain the next planes' register prefetch
+// at each plane step
+__device__ __forceinline__ void lds_barrier() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+
 typedef double dbl2_t __attribute__((ext_vector_type(2)));
 typedef double dbl2u_t __attribute__((ext_vector_type(2), aligned(8)));  // 8-B aligned 16-B loads
 
@@ -38,7 +47,6 @@ constexpr int FP_VX = FP_TX + 2, FP_VY = FP_TY + 2, FP_VPL = FP_VX * FP_VY;     
 constexpr int FP_CX = FP_TX / 2 + 4, FP_CY = FP_TY / 2 + 4, FP_CPL = FP_CX * FP_CY;  // coarse window 36 x 12
 constexpr int FP_PF = (FP_VPL + 255) / 256;                                      // window points per lane (5)
 constexpr int FP_CPF = (FP_CPL + 255) / 256;                                     // coarse points per lane (2)
-constexpr int FP_DMAX = 2048;                                                    // P dictionary entries in LDS
 
 struct FinePjArgs {
     const uint8_t *cls;    // P's class id per fine row (gtc.hip)
@@ -64,15 +72,20 @@ __device__ __forceinline__ void fp_coarse_fetch(const FinePjArgs &a, int cwx0, i
         const int X = cwx0 + p % FP_CX, Y = cwy0 + p / FP_CX;
         const bool in = p < FP_CPL && (unsigned)X < (unsigned)a.cx && (unsigned)Y < (unsigned)a.cy &&
                         (unsigned)Z < (unsigned)a.cz;
-        v[u] = in ? a.vc[(int64_t)Z * cpl + (int64_t)Y * a.cx + X] : 0.0;
+        v[u] = a.vc[in ? (int64_t)Z * cpl + (int64_t)Y * a.cx + X : 0];  // raw: the store selects
     }
 }
 
-__device__ __forceinline__ void fp_coarse_store(double *cring, int Z, const double (&v)[FP_CPF]) {
+// (the 0.0 outside the coarse grid is selected here, where the load is consumed:
+// a select next to the load would make every later wait include it)
+__device__ __forceinline__ void fp_coarse_store(const FinePjArgs &a, double *cring, int cwx0, int cwy0, int Z,
+                                                const double (&v)[FP_CPF]) {
 #pragma unroll
     for (int u = 0; u < FP_CPF; u++) {
         const int p = threadIdx.x + 256 * u;
-        if (p < FP_CPL) cring[(Z & 3) * FP_CPL + p] = v[u];
+        const int X = cwx0 + p % FP_CX, Y = cwy0 + p / FP_CX;
+        const bool in = (unsigned)X < (unsigned)a.cx && (unsigned)Y < (unsigned)a.cy && (unsigned)Z < (unsigned)a.cz;
+        if (p < FP_CPL) cring[(Z & 3) * FP_CPL + p] = in ? v[u] : 0.0;
     }
 }
 
@@ -82,12 +95,15 @@ struct FpSet {
     int C[FP_PF];
 };
 
+template <int KE>
 __global__ __launch_bounds__(256) void k_fine_interp_jacobi(FinePjArgs a) {
     __shared__ double vring[4 * FP_VPL];
     __shared__ double cring[4 * FP_CPL];
-    __shared__ uint16_t sd[FP_DMAX];
     __shared__ double st[256];
-    __shared__ int16_t lut[4][27];  // [Zc & 3][slot]: coarse ring offset of step (dx, dy, dz)
+    // P's dictionary decoded for the four coarse-ring phases: dec[r][e] = value
+    // index << 16 | (int16) coarse-window offset of entry e when the row's coarse
+    // plane sits in ring slot r (so a term is two LDS reads and no arithmetic)
+    extern __shared__ uint32_t dec[];
     const int tid = threadIdx.x;
     const int t = xcd_remap(blockIdx.x, gridDim.x);
     const int ntxy = a.ntx * a.nty;
@@ -97,8 +113,9 @@ __global__ __launch_bounds__(256) void k_fine_interp_jacobi(FinePjArgs a) {
     const int cwx0 = (x0 >> 1) - 2, cwy0 = (y0 >> 1) - 2;
     const int64_t fpl = (int64_t)a.nx * a.ny;
 
-    // the lane's window points q = tid + 256 u: (gx, gy) = (x0 - 1 + q % 66, y0 - 1 + q / 66)
-    int gxq[FP_PF], gyq[FP_PF], cb[FP_PF];
+    // the lane's window points q = tid + 256 u: (gx, gy) = (x0 - 1 + q % 66, y0 - 1 + q / 66);
+    // po = its offset in a plane (32-bit; an in-grid point for points outside the grid)
+    int cb[FP_PF], po[FP_PF], gxq[FP_PF], gyq[FP_PF];
     bool inq[FP_PF], jac[FP_PF];
 #pragma unroll
     for (int u = 0; u < FP_PF; u++) {
@@ -107,60 +124,73 @@ __global__ __launch_bounds__(256) void k_fine_interp_jacobi(FinePjArgs a) {
         gyq[u] = y0 - 1 + wy;
         inq[u] = q < FP_VPL && (unsigned)gxq[u] < (unsigned)a.nx && (unsigned)gyq[u] < (unsigned)a.ny;
         jac[u] = inq[u] && wx >= 1 && wx <= FP_TX && wy >= 1 && wy <= FP_TY;
-        cb[u] = inq[u] ? ((gyq[u] >> 1) - cwy0) * FP_CX + (gxq[u] >> 1) - cwx0 : 0;
+        // (in-range coarse-window reads for points outside the grid)
+        cb[u] = inq[u] ? ((gyq[u] >> 1) - cwy0) * FP_CX + (gxq[u] >> 1) - cwx0 : FP_CX + 1;
+        po[u] = inq[u] ? gyq[u] * a.nx + gxq[u] : 0;
     }
-    // f and the class ids of fine plane z at the lane's window points (0 outside the grid)
+    // f and the class ids of fine plane z at the lane's window points: one uniform
+    // plane pointer (clamped plane) and 32-bit offsets; unconditional loads, no
+    // select -- interp() zeroes v outside the grid, the Jacobi sum reads f at grid points
     auto fetch = [&](int z, double (&F)[FP_PF], int (&C)[FP_PF]) {
+        const int zc = min(max(z, 0), a.nz - 1);
+        const double *fz = a.f + (int64_t)zc * fpl;
+        const uint8_t *cz = a.cls + (int64_t)zc * fpl;
 #pragma unroll
         for (int u = 0; u < FP_PF; u++) {
-            const bool in = inq[u] && (unsigned)z < (unsigned)a.nz;
-            const int64_t i = in ? (int64_t)z * fpl + (int64_t)gyq[u] * a.nx + gxq[u] : 0;
-            F[u] = in ? a.f[i] : 0.0;
-            C[u] = in ? (int)a.cls[i] : 0;
+            F[u] = fz[po[u]];
+            C[u] = (int)cz[po[u]];
         }
     };
-    // v = d f + P v_c of fine plane z at the window points (k_gtc_interp's ADD0 sum)
+    // v = d f + P v_c of fine plane z at the window points (k_gtc_interp's ADD0
+    // sum); KE (the dictionary width) compile-time, all FP_PF x KE terms in flight
     auto interp = [&](int z, const double (&F)[FP_PF], const int (&C)[FP_PF], double (&V)[FP_PF]) {
         const bool zin = (unsigned)z < (unsigned)a.nz;
-        const int16_t *lz = lut[(z >> 1) & 3];
+        const uint32_t *dz = dec + ((z >> 1) & 3) * a.nce;
+        uint32_t e[FP_PF][KE];
+#pragma unroll
+        for (int u = 0; u < FP_PF; u++)
+#pragma unroll
+            for (int j = 0; j < KE; j += 4) {
+                const uint4 q = *reinterpret_cast<const uint4 *>(dz + C[u] * KE + j);
+                e[u][j] = q.x;
+                e[u][j + 1] = q.y;
+                e[u][j + 2] = q.z;
+                e[u][j + 3] = q.w;
+            }
+        double cv[FP_PF][KE], w[FP_PF][KE];
+#pragma unroll
+        for (int u = 0; u < FP_PF; u++)
+#pragma unroll
+            for (int j = 0; j < KE; j++) {
+                cv[u][j] = st[e[u][j] >> 16];
+                w[u][j] = cring[cb[u] + (int)(int16_t)(e[u][j] & 0xffffu)];
+            }
 #pragma unroll
         for (int u = 0; u < FP_PF; u++) {
-            double v = 0.0;
-            if (zin && inq[u]) {
-                const uint16_t *e = sd + C[u] * a.ke;
-                double acc = 0.0;
-                for (int k = 0; k < a.ke; k += 4) {
-                    double cv[4], w[4];
+            double acc = 0.0;
 #pragma unroll
-                    for (int j = 0; j < 4; j++) {
-                        const uint16_t c = e[k + j];
-                        cv[j] = st[c >> 8];
-                        w[j] = cring[cb[u] + lz[c & 255]];
-                    }
-#pragma unroll
-                    for (int j = 0; j < 4; j++) acc = fma(cv[j], w[j], acc);
-                }
-                v = a.dk * F[u] + acc;  // d*b (vec_mul's product) + P v_c
-            }
+            for (int j = 0; j < KE; j++) acc = fma(cv[u][j], w[u][j], acc);
+            const double v = (zin && inq[u]) ? a.dk * F[u] + acc : 0.0;  // d*b (vec_mul's product) + P v_c
             V[u] = v;
             if (tid + 256 * u < FP_VPL) vring[(z & 3) * FP_VPL + tid + 256 * u] = v;
         }
     };
 
-    // the dictionary, value table and ring lookup
-    for (int b = tid; b < a.nce; b += 256) sd[b] = a.dict[b];
-    if (tid < a.ntab) st[tid] = a.vtab[tid];
-    if (tid < 4 * 27) {
-        const int r = tid / 27, s = tid % 27;
-        const int dz = s / 9 - 1, dy = (s / 3) % 3 - 1, dx = s % 3 - 1;
-        lut[r][s] = (int16_t)(((r + dz) & 3) * FP_CPL + dy * FP_CX + dx);
+    // the decoded dictionary and the value table
+    for (int b = tid; b < 4 * a.nce; b += 256) {
+        const int r = b / a.nce, e = b - r * a.nce;
+        const uint32_t c = a.dict[e], sl = c & 255u;
+        const int dzs = (int)(sl / 9u) - 1, dys = (int)((sl / 3u) % 3u) - 1, dxs = (int)(sl % 3u) - 1;
+        const int off = ((r + dzs) & 3) * FP_CPL + dys * FP_CX + dxs;
+        dec[b] = (c >> 8) << 16 | ((uint32_t)off & 0xffffu);
     }
+    if (tid < a.ntab) st[tid] = a.vtab[tid];
     // coarse planes zb/2 - 2 .. zb/2 + 1 (those of v(zb - 1) .. v(zb + 1); zb is even)
     const int Zb = zb >> 1;
     for (int Z = Zb - 2; Z <= Zb + 1; Z++) {
         double cv[FP_CPF];
         fp_coarse_fetch(a, cwx0, cwy0, Z, cv);
-        fp_coarse_store(cring, Z, cv);
+        fp_coarse_store(a, cring, cwx0, cwy0, Z, cv);
     }
     // register sets of four consecutive planes (set = plane mod 4, renamed by
     // unrolling): at plane z the Jacobi sum reads set z, v(z + 1) is computed
@@ -172,48 +202,53 @@ __global__ __launch_bounds__(256) void k_fine_interp_jacobi(FinePjArgs a) {
     __syncthreads();
     interp(zb - 1, S3.F, S3.C, S3.V);  // plane zb - 1: only its ring slot is read
     interp(zb, S0.F, S0.C, S0.V);      // plane zb: ring slot and (registers) the row's own v
-    fetch(zb + 1, S1.F, S1.C);
-    fetch(zb + 2, S2.F, S2.C);
-    // the coarse plane v(zb + 2) adds, stored at the first step (its slot held zb/2 - 2)
+    // the coarse plane v(zb + 2) adds, stored at the first step (its slot held
+    // zb/2 - 2); issued before f as in every step, so the loop's waits match
     int cmax = Zb + 2;
-    bool cpend = true;
     double cp[FP_CPF];
     fp_coarse_fetch(a, cwx0, cwy0, cmax, cp);
+    fetch(zb + 1, S1.F, S1.C);
+    fetch(zb + 2, S2.F, S2.C);
     __syncthreads();  // the prologue's reads of plane zb/2 - 2 before its slot is reused
 
+    // every step of the unrolled loop runs unconditionally (a step past ze only
+    // skips its stores): a conditional step would join its loads' registers and
+    // drain the prefetch at the join
     auto step = [&](int z, FpSet &sz, FpSet &s1, FpSet &s3) {
         interp(z + 1, s1.F, s1.C, s1.V);  // v(z + 1)
-        if (cpend) fp_coarse_store(cring, cmax, cp);  // the plane v(z + 2) adds (slot of cmax - 4: unread)
-        cpend = false;
-        // issued now: f / classes of plane z + 3, the coarse plane v(z + 3) adds
-        if (z + 3 <= ze) fetch(z + 3, s3.F, s3.C);
-        if (((z + 3) >> 1) + 1 > cmax) {
-            cmax++;
-            fp_coarse_fetch(a, cwx0, cwy0, cmax, cp);
-            cpend = true;
-        }
-        __syncthreads();  // v(z + 1) in the ring
+        fp_coarse_store(a, cring, cwx0, cwy0, cmax, cp);  // the plane v(z + 2) adds (slot of cmax - 4: unread;
+                                                          // or cmax again: the same values)
+        // issued now: the coarse plane v(z + 3) adds (first: it is stored one
+        // plane later, and a wait for it then must not wait for the f below),
+        // f / classes of plane z + 3
+        // (both unconditional: a load under a branch is drained at the join)
+        cmax = ((z + 3) >> 1) + 1;
+        fp_coarse_fetch(a, cwx0, cwy0, cmax, cp);
+        fetch(min(z + 3, ze), s3.F, s3.C);
+        lds_barrier();  // v(z + 1) in the ring (the prefetches stay in flight)
         // z(z) = v + d (f - A v): spmv_dia_kernel's constant 7-point JACOBI sum
         const double *vm = vring + ((z - 1) & 3) * FP_VPL, *v0 = vring + (z & 3) * FP_VPL,
                      *vp = vring + ((z + 1) & 3) * FP_VPL;
-        const bool zlo = z > 0, zhi = z < a.nz - 1;
+        // (a neighbour outside the grid -- x, y or a plane past either end -- holds
+        // the +0.0 interp() wrote: the constant kernel's `in ? x : 0.0` without selects)
+        const bool zon = z < ze;
+        double *oz = a.out + (int64_t)min(z, a.nz - 1) * fpl;
 #pragma unroll
         for (int u = 0; u < FP_PF; u++) {
-            if (!jac[u]) continue;
-            const int q = tid + 256 * u, gx = gxq[u], gy = gyq[u];
+            if (!jac[u] || !zon) continue;
+            const int q = tid + 256 * u;
             const double y[7] = {vm[q], v0[q - FP_VX], v0[q - 1], sz.V[u], v0[q + 1], v0[q + FP_VX], vp[q]};
-            const bool in[7] = {zlo, gy > 0, gx > 0, true, gx + 1 < a.nx, gy < a.ny - 1, zhi};
             double acc = 0.0;
 #pragma unroll
-            for (int k = 0; k < 7; k++) acc = fma(a.cst[k], in[k] ? y[k] : 0.0, acc);
-            a.out[(int64_t)z * fpl + (int64_t)gy * a.nx + gx] = sz.V[u] + a.dk * (sz.F[u] - acc);
+            for (int k = 0; k < 7; k++) acc = fma(a.cst[k], y[k], acc);
+            oz[po[u]] = sz.V[u] + a.dk * (sz.F[u] - acc);
         }
     };
     for (int z = zb; z < ze; z += 4) {
         step(z, S0, S1, S3);
-        if (z + 1 < ze) step(z + 1, S1, S2, S0);
-        if (z + 2 < ze) step(z + 2, S2, S3, S1);
-        if (z + 3 < ze) step(z + 3, S3, S0, S2);
+        step(z + 1, S1, S2, S0);
+        step(z + 2, S2, S3, S1);
+        step(z + 3, S3, S0, S2);
     }
 }
 
@@ -221,11 +256,14 @@ __global__ __launch_bounds__(256) void k_fine_interp_jacobi(FinePjArgs a) {
 // k_fine_resid_restrict: the fine residual from the zero guess (RESID0,
 // multigrid.rs:341-342 with the first Jacobi step folded: r = f - A (d f)) and
 // the restriction f_c = R r with the next level's first step d_c f_c (SETDF) in
-// one marching launch -- r never reaches HBM (f in, f_c and d_c f_c out: 168 MB
+// one marching launch -- r never reaches HBM (f in, f_c and d_c f_c out: 172 MB
 // instead of 440 MB at 256^3).  A workgroup takes a 32 x 8 coarse tile through a
 // run of jper coarse planes, walking the fine planes p = 2 Zb - 1 .. 2 Ze once:
-//   r(p) on the 68 x 18 fine window (row pairs, f gathered as
-//   spmv_dia_kernel's constant 7-point RESID0 does) into one of two LDS slots;
+//   f of each fine plane (72 x 20 window) reaches an LDS ring of four planes
+//     through registers, loaded two planes ahead (16-B loads);
+//   r(p) on the 68 x 18 window from the ring (row pairs, the constant 7-point
+//     RESID0 sum of spmv_dia_kernel: d f at the seven neighbours, +0.0 where a
+//     neighbour leaves the grid) into one of two LDS slots;
 //   barrier;
 //   every coarse row adds the entries of its R row that lie in plane p to the
 //   fma chain of the coarse plane they belong to (p = 2Z - 1, 2Z, 2Z + 1,
@@ -234,9 +272,12 @@ __global__ __launch_bounds__(256) void k_fine_interp_jacobi(FinePjArgs a) {
 // R's entries ascend in (dz, dy, dx), so the chain is k_gtc_restrict_march's, term
 // for term: f_c and d_c f_c are bitwise the two-launch result.
 constexpr int FR_TX = 32, FR_TY = 8;                                  // coarse tile
-constexpr int FR_WX = 2 * FR_TX + 4, FR_WY = 2 * FR_TY + 2;           // r window 68 x 18 (pairs aligned)
+constexpr int FR_WX = 2 * FR_TX + 4, FR_WY = 2 * FR_TY + 2;           // r window 68 x 18 (x from 2 X0 - 2)
 constexpr int FR_WPL = FR_WX * FR_WY, FR_NP = FR_WPL / 2;             // 612 row pairs per plane
 constexpr int FR_PP = (FR_NP + 255) / 256;                            // pairs per lane (3)
+constexpr int FF_WX = FR_WX + 4, FF_WY = FR_WY + 2;                   // f window 72 x 20 (x from 2 X0 - 4)
+constexpr int FF_PL = FF_WX * FF_WY, FF_NU = FF_PL / 2;               // 720 16-B units per plane
+constexpr int FF_PU = (FF_NU + 255) / 256;                            // units per lane (3)
 constexpr int FR_DMAX = 4096;
 
 struct FineRrArgs {
@@ -257,110 +298,130 @@ struct FineRrArgs {
     double cst[7];
 };
 
-// x operands of rows (r, r + 1) at column c (dia_gx2) and the x run x[c .. c + 3] (dia_gx4)
-__device__ __forceinline__ void fr_gx2(const double *x, int64_t c, int64_t n, double &x0, double &x1) {
-    const int64_t cc = min(max(c, (int64_t)0), n - 2);
-    const dbl2_t v = *reinterpret_cast<const dbl2u_t *>(x + cc);
-    x0 = c > n - 2 ? v.y : v.x;
-    x1 = c < 0 ? v.x : v.y;
-}
-__device__ __forceinline__ void fr_gx4(const double *x, int64_t c, int64_t n, double (&v)[4]) {
-    const int64_t p0 = min(max(c, (int64_t)0), n - 2), p1 = min(max(c + 2, (int64_t)0), n - 2);
-    const dbl2_t q0 = *reinterpret_cast<const dbl2u_t *>(x + p0);
-    const dbl2_t q1 = *reinterpret_cast<const dbl2u_t *>(x + p1);
+// f of fine plane p at the lane's 16-B units of the window (0.0 outside the grid)
+__device__ __forceinline__ void fr_fetch(const FineRrArgs &a, int gx0, int gy0, int p, dbl2_t (&v)[FF_PU]) {
+    const int64_t fpl = (int64_t)a.nx * a.ny;
 #pragma unroll
-    for (int j = 0; j < 4; j++) {
-        const int64_t t = c + j;
-        v[j] = t == p0 ? q0.x : t == p0 + 1 ? q0.y : t == p1 ? q1.x : q1.y;
+    for (int u = 0; u < FF_PU; u++) {
+        const int q = threadIdx.x + 256 * u;
+        const int gx = gx0 + 2 * (q % (FF_WX / 2)), gy = gy0 + q / (FF_WX / 2);
+        const bool in = q < FF_NU && (unsigned)gx < (unsigned)a.nx && (unsigned)gy < (unsigned)a.ny &&
+                        (unsigned)p < (unsigned)a.nz;
+        // an unconditional load at a clamped address, no select here: a select (or
+        // a branch) next to the load makes the compiler drain every load in flight
+        v[u] = *reinterpret_cast<const dbl2_t *>(a.f + (in ? (int64_t)p * fpl + (int64_t)gy * a.nx + gx : 0));
+    }
+}
+
+// the 0.0 outside the grid selected where the prefetched plane is consumed
+__device__ __forceinline__ void fr_store(const FineRrArgs &a, int gx0, int gy0, double *fring, int p,
+                                         const dbl2_t (&v)[FF_PU]) {
+#pragma unroll
+    for (int u = 0; u < FF_PU; u++) {
+        const int q = threadIdx.x + 256 * u;
+        const int gx = gx0 + 2 * (q % (FF_WX / 2)), gy = gy0 + q / (FF_WX / 2);
+        const bool in = (unsigned)gx < (unsigned)a.nx && (unsigned)gy < (unsigned)a.ny && (unsigned)p < (unsigned)a.nz;
+        if (q < FF_NU) *reinterpret_cast<dbl2_t *>(fring + (p & 3) * FF_PL + 2 * q) = in ? v[u] : dbl2_t{0.0, 0.0};
     }
 }
 
 __global__ __launch_bounds__(256) void k_fine_resid_restrict(FineRrArgs a) {
+    __shared__ __attribute__((aligned(16))) double fring[4 * FF_PL];
     __shared__ __attribute__((aligned(16))) double rs[2 * FR_WPL];
-    __shared__ uint16_t sd[FR_DMAX];
     __shared__ double st[256];
     __shared__ double sdt[256];
-    __shared__ int16_t lut[16];
-    extern __shared__ uint8_t skdz[];  // nclass x 5
+    // nce dictionary entries, nclass x 5 plane-group starts, then the class ids and
+    // (coded d_c) diagonal codes of the run's coarse rows (256 per plane, jper planes):
+    // no global load in the plane loop waits behind the f prefetch
+    extern __shared__ uint16_t sdyn[];
+    uint16_t *sd = sdyn;
+    uint8_t *skdz = reinterpret_cast<uint8_t *>(sdyn + ((a.nce + 7) & ~7));
+    uint8_t *scl = skdz + ((5 * a.nclass + 15) & ~15);
+    uint8_t *sdc = scl + 256 * a.jper;
     const int tid = threadIdx.x;
     const int t = xcd_remap(blockIdx.x, gridDim.x);
     const int ntxy = a.ntx * a.nty;
     const int chunk = t / ntxy, txy = t - chunk * ntxy;
     const int X0 = (txy % a.ntx) * FR_TX, Y0 = (txy / a.ntx) * FR_TY;
     const int Zb = chunk * a.jper, Ze = min(Zb + a.jper, a.cz);
-    const int64_t fpl = (int64_t)a.nx * a.ny, n = fpl * a.nz, cpl = (int64_t)a.cx * a.cy;
-    const int wx0 = 2 * X0 - 2, wy0 = 2 * Y0 - 1;  // fine window origin (x even: row pairs aligned)
+    const int64_t cpl = (int64_t)a.cx * a.cy;
+    const int wx0 = 2 * X0 - 2, wy0 = 2 * Y0 - 1;  // r window origin (x even: row pairs aligned)
     for (int b = tid; b < a.nce; b += 256) sd[b] = a.dict[b];
     for (int b = tid; b < 5 * a.nclass; b += 256) skdz[b] = a.kdz[b];
     if (tid < a.ntab) st[tid] = a.vtab[tid];
     if (a.dmode == 1) sdt[tid] = a.dtc[tid];
-    if (tid < 16) lut[tid] = (int16_t)(((tid >> 2) - 1) * FR_WX + (tid & 3) - 1);
-    // the lane's row pairs of the window: pair q -> (wx, wy) = (2 (q % 34), q / 34)
-    int gxp[FR_PP], gyp[FR_PP];
+    // the lane's row pairs of the r window: pair q -> (wx, wy) = (2 (q % 34), q / 34)
+    int gxp[FR_PP], gyp[FR_PP], fo[FR_PP];
     bool inp[FR_PP];
 #pragma unroll
     for (int u = 0; u < FR_PP; u++) {
         const int q = tid + 256 * u;
-        gxp[u] = wx0 + 2 * (q % (FR_WX / 2));
-        gyp[u] = wy0 + q / (FR_WX / 2);
+        const int wx = 2 * (q % (FR_WX / 2)), wy = q / (FR_WX / 2);
+        gxp[u] = wx0 + wx;
+        gyp[u] = wy0 + wy;
         inp[u] = q < FR_NP && (unsigned)gxp[u] < (unsigned)a.nx && (unsigned)gyp[u] < (unsigned)a.ny;
+        fo[u] = q < FR_NP ? (wy + 1) * FF_WX + wx + 2 : FF_WX + 2;  // its position in the f window
     }
     // the lane's coarse row
     const int lx = tid % FR_TX, ly = tid / FR_TX, X = X0 + lx, Y = Y0 + ly;
     const bool live = X < a.cx && Y < a.cy;
+    for (int Z = Zb; Z < Ze; Z++) {
+        const int64_t J = live ? (int64_t)Z * cpl + (int64_t)Y * a.cx + X : 0;
+        const uint8_t c = a.cls[J];
+        scl[(Z - Zb) * 256 + tid] = c;
+        if (a.dmode == 1) sdc[(Z - Zb) * 256 + tid] = a.dcc[J];
+    }
     const int base = (2 * ly + 1) * FR_WX + 2 * lx + 2;  // window position of the anchor (2X, 2Y)
     double acc[2] = {0.0, 0.0}, ra[2] = {0.0, 0.0};
     int cl[2] = {0, 0};
-    __syncthreads();
-    for (int p = 2 * Zb - 1; p <= 2 * Ze; p++) {
-        // r(p) = f - A (d f) on the window's row pairs: spmv_dia_kernel<DIA_RESID0_DK, CST>
-        double rr[FR_PP][2];
-        {
-            double xs[FR_PP][4][2], xq[FR_PP][4];
-            const bool pin = (unsigned)p < (unsigned)a.nz;
-#pragma unroll
-            for (int u = 0; u < FR_PP; u++) {
-                const int64_t i = (pin && inp[u]) ? (int64_t)p * fpl + (int64_t)gyp[u] * a.nx + gxp[u] : 0;
-                fr_gx2(a.f, i - fpl, n, xs[u][0][0], xs[u][0][1]);
-                fr_gx2(a.f, i - a.nx, n, xs[u][1][0], xs[u][1][1]);
-                fr_gx4(a.f, i - 1, n, xq[u]);
-                fr_gx2(a.f, i + a.nx, n, xs[u][2][0], xs[u][2][1]);
-                fr_gx2(a.f, i + fpl, n, xs[u][3][0], xs[u][3][1]);
-            }
-            const bool zlo = p > 0, zhi = p < a.nz - 1;
-#pragma unroll
-            for (int u = 0; u < FR_PP; u++) {
-                const double b0 = xq[u][1], b1 = xq[u][2];  // f of the pair (the epilogue's b)
-#pragma unroll
-                for (int i = 0; i < 4; i++)
-#pragma unroll
-                    for (int j = 0; j < 2; j++) xs[u][i][j] = a.dk * xs[u][i][j];
-#pragma unroll
-                for (int j = 0; j < 4; j++) xq[u][j] = a.dk * xq[u][j];
-                const int gx = gxp[u], gy = gyp[u];
-                const bool ylo = gy > 0, yhi = gy < a.ny - 1, xlo = gx > 0, xhi = gx + 2 < a.nx;
-                double acc0 = 0.0, acc1 = 0.0;
-#pragma unroll
-                for (int k = 0; k < 7; k++) {
-                    const double y0 = k < 2 ? xs[u][k][0] : k < 5 ? xq[u][k - 2] : xs[u][k - 3][0];
-                    const double y1 = k < 2 ? xs[u][k][1] : k < 5 ? xq[u][k - 1] : xs[u][k - 3][1];
-                    const bool in = k == 0 ? zlo : k == 1 ? ylo : k == 5 ? yhi : k == 6 ? zhi : true;
-                    const bool in0 = in && (k != 2 || xlo), in1 = in && (k != 4 || xhi);
-                    acc0 = fma(a.cst[k], in0 ? y0 : 0.0, acc0);
-                    acc1 = fma(a.cst[k], in1 ? y1 : 0.0, acc1);
-                }
-                const bool ok = pin && inp[u];
-                rr[u][0] = ok ? b0 - acc0 : 0.0;
-                rr[u][1] = ok ? b1 - acc1 : 0.0;
-            }
+    const int p0 = 2 * Zb - 1, p1 = 2 * Ze;
+    const int fgx0 = 2 * X0 - 4, fgy0 = 2 * Y0 - 2;
+    {
+        dbl2_t v[FF_PU];
+        for (int p = p0 - 1; p <= p0 + 1; p++) {
+            fr_fetch(a, fgx0, fgy0, p, v);
+            fr_store(a, fgx0, fgy0, fring, p, v);
         }
+    }
+    dbl2_t pa[FF_PU], pb[FF_PU];  // f of planes p + 2 (even p: pa) and p + 3 in flight
+    fr_fetch(a, fgx0, fgy0, p0 + 2, (p0 & 1) ? pb : pa);
+    fr_fetch(a, fgx0, fgy0, p0 + 3, (p0 & 1) ? pa : pb);
+    __syncthreads();
+
+    auto step = [&](int p, dbl2_t (&pn)[FF_PU]) {
+        // r(p) = f - A (d f) on the window's row pairs: spmv_dia_kernel<DIA_RESID0_DK, CST>
+        const double *fm = fring + ((p - 1) & 3) * FF_PL, *f0 = fring + (p & 3) * FF_PL,
+                     *fp = fring + ((p + 1) & 3) * FF_PL;
+        const bool pin = (unsigned)p < (unsigned)a.nz;
         double *rp = rs + (p & 1) * FR_WPL;
 #pragma unroll
         for (int u = 0; u < FR_PP; u++) {
+            const int o = fo[u];
+            const dbl2_t zm = *reinterpret_cast<const dbl2_t *>(fm + o), ym = *reinterpret_cast<const dbl2_t *>(f0 + o - FF_WX);
+            const dbl2_t xc = *reinterpret_cast<const dbl2_t *>(f0 + o), yp = *reinterpret_cast<const dbl2_t *>(f0 + o + FF_WX);
+            const dbl2_t zp = *reinterpret_cast<const dbl2_t *>(fp + o);
+            const double xl = f0[o - 1], xr = f0[o + 2];
+            const double b0 = xc.x, b1 = xc.y;  // f of the pair (the epilogue's b)
+            const double dk = a.dk;
+            // every neighbour outside the grid (x, y, or a plane past either end) is
+            // +0.0 in the ring: dk * 0.0 is a zero whose term leaves the sum as the
+            // constant kernel's `in ? d x : 0.0` does (an accumulator that starts at
+            // +0.0 never becomes -0.0), so no selects
+            const double y0[7] = {dk * zm.x, dk * ym.x, dk * xl, dk * xc.x, dk * xc.y, dk * yp.x, dk * zp.x};
+            const double y1[7] = {dk * zm.y, dk * ym.y, dk * xc.x, dk * xc.y, dk * xr, dk * yp.y, dk * zp.y};
+            double acc0 = 0.0, acc1 = 0.0;
+#pragma unroll
+            for (int k = 0; k < 7; k++) {
+                acc0 = fma(a.cst[k], y0[k], acc0);
+                acc1 = fma(a.cst[k], y1[k], acc1);
+            }
+            const bool ok = pin && inp[u];
             const int q = tid + 256 * u;
-            if (q < FR_NP) *reinterpret_cast<dbl2_t *>(rp + 2 * q) = dbl2_t{rr[u][0], rr[u][1]};
+            if (q < FR_NP) *reinterpret_cast<dbl2_t *>(rp + 2 * q) = dbl2_t{ok ? b0 - acc0 : 0.0, ok ? b1 - acc1 : 0.0};
         }
-        __syncthreads();
+        fr_store(a, fgx0, fgy0, fring, p + 2, pn);            // f(p + 2): the slot of p - 2 (unread now)
+        fr_fetch(a, fgx0, fgy0, min(p + 4, p1 + 1), pn);      // in flight two planes (unconditional)
+        lds_barrier();
         // the plane's terms of the two coarse chains it belongs to
         if (live) {
             // p odd: Z = (p + 1) / 2 starts (dz = -1), Z - 1 continues (dz = +1);
@@ -370,30 +431,46 @@ __global__ __launch_bounds__(256) void k_fine_resid_restrict(FineRrArgs a) {
             for (int w = 0; w < 2; w++) {
                 const int Z = w == 0 ? Zn : Zo, g = w == 0 ? gn : go;
                 if (Z < Zb || Z >= Ze) continue;
-                const int s = Z & 1;
+                const int sl = Z & 1;
                 if (g == 0) {
-                    cl[s] = a.cls[(int64_t)Z * cpl + (int64_t)Y * a.cx + X];
-                    acc[s] = 0.0;
+                    cl[sl] = scl[(Z - Zb) * 256 + tid];
+                    acc[sl] = 0.0;
                 }
-                const uint8_t *kz = skdz + 5 * cl[s];
-                const uint16_t *e = sd + cl[s] * a.ke;
-                double ac = acc[s];
-                for (int k = kz[g]; k < kz[g + 1]; k++) {
-                    const uint16_t c = e[k];
-                    ac = fma(st[c >> 8], rp[base + lut[c & 15]], ac);
+                const uint8_t *kz = skdz + 5 * cl[sl];
+                const uint16_t *e = sd + cl[sl] * a.ke;
+                double ac = acc[sl];
+                const int k1 = kz[g + 1];
+                for (int k0 = kz[g]; k0 < k1; k0 += 8) {  // 8 terms' reads in flight, then the fmas in order
+                    double cv[8], w[8];
+#pragma unroll
+                    for (int j = 0; j < 8; j++) {
+                        const uint32_t c = e[min(k0 + j, a.ke - 1)], s4 = c & 15u;
+                        cv[j] = st[c >> 8];
+                        w[j] = rp[base + ((int)(s4 >> 2) - 1) * FR_WX + (int)(s4 & 3u) - 1];
+                    }
+#pragma unroll
+                    for (int j = 0; j < 8; j++) ac = k0 + j < k1 ? fma(cv[j], w[j], ac) : ac;
                 }
-                if (g == 1) ra[s] = rp[base];  // r at the anchor: the padding entries' operand
+                if (g == 1) ra[sl] = rp[base];  // r at the anchor: the padding entries' operand
                 if (g == 3) {
-                    for (int k = kz[4]; k < a.ke; k++) ac = fma(st[e[k] >> 8], ra[s], ac);
+                    for (int k = kz[4]; k < a.ke; k++) ac = fma(st[e[k] >> 8], ra[sl], ac);
                     const int64_t J = (int64_t)Z * cpl + (int64_t)Y * a.cx + X;
                     a.fc[J] = ac;
-                    const double dd = a.dmode == 0 ? a.dkc : a.dmode == 1 ? sdt[a.dcc[J]] : a.dpc[J];
+                    const double dd = a.dmode == 0 ? a.dkc : sdt[sdc[(Z - Zb) * 256 + tid]];
                     a.dfc[J] = dd * ac;  // vec_mul(_coded)'s product
                 }
-                acc[s] = ac;
+                acc[sl] = ac;
             }
         }
+    };
+    // planes p (odd p0 first): f(p + 2) in pa for even p, pb for odd p
+    int p = p0;
+    if (p & 1) step(p++, pb);
+    for (; p + 1 <= p1; p += 2) {
+        step(p, pa);
+        step(p + 1, pb);
     }
+    if (p <= p1) step(p, pa);
 }
 
 // ------------------------------------------------------------ host side
@@ -404,7 +481,8 @@ static int fine_pj_occupancy() {
     static int n = 1;
     std::call_once(once, [] {
         int v = 0;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&v, k_fine_interp_jacobi, 256, 0) == hipSuccess && v >= 1)
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&v, k_fine_interp_jacobi<4>, 256, 16 * 512) == hipSuccess &&
+            v >= 1)
             n = v;
         else
             (void)hipGetLastError();
@@ -433,7 +511,8 @@ bool fine_resid_restrict_ok(const GpuCsr &A, const GpuCsr &R, const SpmvEpi &epi
     if (!R.gtc_on || !R.gtc_r || R.rframe.on() || R.cframe.on() || R.gtc_nce > FR_DMAX || R.gtc_ntab > 256 ||
         !R.gtc_kdz.get() || R.gtc_ke % 8 != 0)
         return false;
-    if (!epic.y2 || !(epic.dk != 0.0 || epic.dc || epic.d)) return false;
+    // the coarse level's d coded (8-bit) or one value: no global load in the plane loop
+    if (!epic.y2 || !epic.dc) return false;
     for (int q = 0; q < 3; q++)
         if (R.gtc_fg[q] != A.dia_cst_n[q] || R.gtc_cg[q] != (R.gtc_fg[q] + 1) / 2) return false;
     return A.nrows == R.ncols && R.nrows == R.gtc_cg[0] * R.gtc_cg[1] * R.gtc_cg[2];
@@ -461,34 +540,36 @@ void fine_resid_restrict(const GpuCsr &A, const GpuCsr &R, const double *f, doub
     if (epic.dc && epic.dk != 0.0 && flag(FLAG_DIA_DK) != 0) {
         a.dmode = 0;
         a.dkc = epic.dk;
-    } else if (epic.dc) {
+    } else {
         a.dmode = 1;
         a.dcc = epic.dc;
         a.dtc = epic.dt;
-    } else {
-        a.dmode = 2;
-        a.dpc = epic.d;
     }
     a.dk = dk;
     for (int k = 0; k < 7; k++) a.cst[k] = A.dia_cst_v[k];
-    const size_t dyn = (size_t)5 * a.nclass;
     const int64_t ntxy = (int64_t)a.ntx * a.nty;
-    const int64_t want = (int64_t)fine_rr_occupancy(dyn) * std::max(A.ctx ? A.ctx->num_cus : 256, 1);
+    // occupancy with the dictionary part of the dynamic LDS (the per-plane class
+    // bytes are small), then the run length, then the exact dynamic size
+    const size_t dyn0 = (size_t)((a.nce + 7) & ~7) * 2 + (size_t)((5 * a.nclass + 15) & ~15);
+    const int64_t want = (int64_t)fine_rr_occupancy(dyn0 + 2 * 256 * 16) * std::max(A.ctx ? A.ctx->num_cus : 256, 1);
     a.jper = (int)std::max<int64_t>(1, ceil_div((int64_t)a.cz * ntxy, want));
     if (flag(FLAG_FINE_FUSE) > 1) a.jper = (int)std::max<int64_t>(1, flag(FLAG_FINE_FUSE) / 2);
+    a.jper = std::min(a.jper, 64);  // (the class bytes of a run: 512 per plane)
+    const size_t dyn = dyn0 + (size_t)2 * 256 * a.jper;
     const dim3 grid((unsigned)(ntxy * ceil_div(a.cz, a.jper)));
     k_fine_resid_restrict<<<grid, dim3(256), dyn, s>>>(a);
     FAMG_CHECK_HIP(hipGetLastError());
     const int64_t n = A.nrows, nc = R.nrows;
     // f in once, f_c and d_c f_c out, R's class ids (1 B per coarse row; a coded d_c: 1 B more);
     // CSR-equivalent: A's RESID0 (x, b = f; r out; d gathered) + R's SETDF
-    log_launch("fine-rr", SPMV_KERNEL_DIA, -1, n, 8 * n + 16 * nc + nc + (a.dmode == 1 ? nc : a.dmode == 2 ? 8 * nc : 0),
+    log_launch("fine-rr", SPMV_KERNEL_DIA, -1, n, 8 * n + 16 * nc + nc + (a.dmode == 1 ? nc : 0),
                (12 * A.nnz + 4 * (n + 1) + 32 * n) + (12 * R.nnz + 4 * (nc + 1) + 8 * n + 16 * nc));
 }
 
 bool fine_interp_jacobi_ok(const GpuCsr &A, const GpuCsr &P, const SpmvEpi &epi) {
     if (flag(FLAG_FINE_FUSE) == 0 || !dia7_cst_dk(A, epi)) return false;
-    if (!P.gtc_on || P.gtc_r || P.rframe.on() || P.cframe.on() || P.gtc_nce > FP_DMAX || P.gtc_ke % 4 != 0 ||
+    if (!P.gtc_on || P.gtc_r || P.rframe.on() || P.cframe.on() || P.gtc_nce > 512 ||
+        (P.gtc_ke != 4 && P.gtc_ke != 8) ||
         P.gtc_ntab > 256)
         return false;
     for (int q = 0; q < 3; q++)
@@ -521,7 +602,9 @@ void fine_interp_jacobi(const GpuCsr &A, const GpuCsr &P, const double *vc, cons
     if (flag(FLAG_FINE_FUSE) > 1) jper = (int)flag(FLAG_FINE_FUSE);
     a.jper = jper + (jper & 1);
     const dim3 grid((unsigned)(ntxy * ceil_div(a.nz, a.jper)));
-    k_fine_interp_jacobi<<<grid, dim3(256), 0, s>>>(a);
+    const size_t dyn = (size_t)16 * a.nce;  // the decoded dictionary, four ring phases
+    if (a.ke == 4) k_fine_interp_jacobi<4><<<grid, dim3(256), dyn, s>>>(a);
+    else k_fine_interp_jacobi<8><<<grid, dim3(256), dyn, s>>>(a);
     FAMG_CHECK_HIP(hipGetLastError());
     const int64_t n = A.nrows;
     // f and z once, v_c once, the class ids (1 B per row); CSR-equivalent: P's ADD0 + A's JACOBI

@@ -199,56 +199,6 @@ __global__ __launch_bounds__(256) void spmm_bsr3_kernel(SpmmBsrArgs a) {
     }
 }
 
-// ------------------------------------------------------------ x-staged SELL
-
-struct SpmmXsArgs {
-    const char *data;       // per slice: values (w x 64 fp64) then indices (w x 64 u16 / i32)
-    const uint32_t *desc;   // per slice: byte offset / 128 | mode << 30 (1: LDS index, 2: global column)
-    const int32_t *soff;    // per slice: first step (+1 sentinel)
-    const int32_t *coff;    // per group: first staged chunk (+1 sentinel)
-    const int32_t *chunks;  // staged chunk ids
-    int32_t nrows, nslices;
-    const double *x;
-    int64_t ldx;
-    double *y;
-    int64_t ldy;
-};
-
-// one row per lane (xs_walk's order: the row's stored steps ascending, fma from
-// 0.0); the 16-bit LDS index of a staged slice is turned back into its global
-// column (chunk id * 64 + index % 64) and the k columns' x gathered through the
-// caches -- the matrix streams once per 8 columns.  A wave per slice, 16 per group.
-template <int KB>
-__global__ __launch_bounds__(256) void spmm_xs_kernel(SpmmXsArgs a) {
-    const int sl = __builtin_amdgcn_readfirstlane(xcd_remap(blockIdx.x, gridDim.x) * 4 + (int)(threadIdx.x >> 6));
-    if (sl >= a.nslices) return;
-    const int lane = threadIdx.x & 63, row = sl * 64 + lane;
-    const uint32_t dsc = a.desc[sl];
-    const int mode = (int)(dsc >> 30);
-    const char *blk = a.data + (int64_t)(dsc & 0x3fffffffu) * 128;
-    const int t0 = a.soff[sl], w = a.soff[sl + 1] - t0;
-    const int32_t *ch = a.chunks + a.coff[sl / 64];
-    double acc[KB];
-#pragma unroll
-    for (int c = 0; c < KB; c++) acc[c] = 0.0;
-    for (int t = 0; t < w; t++) {
-        const double v = __builtin_nontemporal_load(reinterpret_cast<const double *>(blk) + (int64_t)t * 64 + lane);
-        int64_t col;
-        if (mode == 1) {
-            const int ix = reinterpret_cast<const uint16_t *>(blk + (int64_t)w * 512)[(int64_t)t * 64 + lane];
-            col = (int64_t)ch[ix >> 6] * 64 + (ix & 63);
-        } else {
-            col = reinterpret_cast<const int32_t *>(blk + (int64_t)w * 512)[(int64_t)t * 64 + lane];
-        }
-#pragma unroll
-        for (int c = 0; c < KB; c++) acc[c] = fma(v, a.x[col + c * a.ldx], acc[c]);
-    }
-    if (row < a.nrows) {
-#pragma unroll
-        for (int c = 0; c < KB; c++) a.y[row + c * a.ldy] = acc[c];
-    }
-}
-
 // ------------------------------------------------------------- pattern SELL
 
 struct SpmmSellpArgs {
@@ -345,7 +295,8 @@ bool spmm_compressed(const GpuCsr &m, const double *x, int64_t ldx, double *y, i
     const bool sellp = m.kernel == SPMV_KERNEL_SELLP && m.has_sellp() && m.sellp_seg_slc.size() <= 2 &&
                        (sL == 1 || sL == 2 || sL == 4 || sL == 8 || sL == 16 || sL == 32 || sL == 64) &&
                        (sV == 0 || sV == 4 || sV == 8);
-    if (!dia && !scs && !bsr && !xs && !sellp) return false;
+    if (xs) return spmm_xs(m, x, ldx, y, ldy, k, s);  // xsell.hip: per column with its x chunks in LDS
+    if (!dia && !scs && !bsr && !sellp) return false;
     if (m.nrows == 0 || k == 0) return true;
     for (int64_t c0 = 0; c0 < k; c0 += SPMM_COLS) {
         const int kb = (int)std::min<int64_t>(SPMM_COLS, k - c0);
@@ -402,13 +353,6 @@ bool spmm_compressed(const GpuCsr &m, const double *x, int64_t ldx, double *y, i
                 if (m.scs_ib == 1) { FAMG_SPMM_KB(kb, FAMG_S1) }
                 else { FAMG_SPMM_KB(kb, FAMG_S2) }
             }
-        } else if (xs) {
-            const int32_t ns = (int32_t)ceil_div(m.nrows, 64);
-            SpmmXsArgs a{m.xs_data.get(), m.xs_desc.get(), m.xs_soff.get(), m.xs_coff.get(), m.xs_chunks.get(),
-                         (int32_t)m.nrows, ns, xc, ldx, yc, ldy};
-            const dim3 grid((unsigned)ceil_div(ns, 4)), block(256);
-#define FAMG_X(KB) spmm_xs_kernel<KB><<<grid, block, 0, s>>>(a)
-            FAMG_SPMM_KB(kb, FAMG_X)
         } else if (sellp) {
             SpmmSellpArgs a{m.sellp_vals.get(), m.sellp_eoff.get(), m.sellp_row0.get(),
                             reinterpret_cast<const int2 *>(m.sellp_pat.get()), m.sellp_offs.get(), m.sellp_rbase.get(),

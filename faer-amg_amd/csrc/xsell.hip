@@ -153,6 +153,66 @@ __global__ __launch_bounds__(XS_BS) void spmv_xs_kernel(XsArgs a) {
     }
 }
 
+// ---------------------------------------------------------------- multi-column
+// Y = A X for k columns (f2, adaptivity.rs:168-244): one workgroup per group
+// walks its slices once per column with that column's chunks staged in LDS --
+// exactly the single-vector kernel's sums (bitwise per column), the group's
+// matrix read from HBM once and re-read from L2 / MALL for the other columns
+// (one x window fits the LDS, eight do not).
+__global__ __launch_bounds__(XS_BS) void spmm_xs_group_kernel(XsArgs a, int kb, int64_t ldx, int64_t ldy) {
+    __shared__ double sx[XS_MAXCH * XS_CH];
+    const int g = xcd_remap(blockIdx.x, gridDim.x);
+    const int c0 = a.coff[g], nch = a.coff[g + 1] - c0;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int s_end = min((g + 1) * XS_SLICES, (a.nrows + 63) / 64);
+    const double *x0 = a.x;
+    double *y0 = a.y;
+    for (int c = 0; c < kb; c++) {
+        a.x = x0 + c * ldx;
+        a.y = y0 + c * ldy;
+        if (c) __syncthreads();  // the previous column's walk is done with sx
+        for (int i = threadIdx.x; i < nch * (XS_CH / 2); i += XS_BS) {
+            const int64_t e = (int64_t)a.chunks[c0 + i / (XS_CH / 2)] * XS_CH + 2 * (i % (XS_CH / 2));
+            xs_dbl2_t v = {0.0, 0.0};
+            if (e + 1 < a.ncols) v = *reinterpret_cast<const xs_dbl2_t *>(a.x + e);
+            else if (e < a.ncols) v.x = a.x[e];
+            *reinterpret_cast<xs_dbl2_t *>(sx + 2 * i) = v;
+        }
+        __syncthreads();
+        for (int s = g * XS_SLICES + wave; s < s_end; s += XS_BS / 64) {
+            const int row = s * 64 + lane;
+            const int w = a.soff[s + 1] - a.soff[s];
+            const uint32_t d = a.desc[s];
+            const char *blk = a.data + (int64_t)(d & 0x3fffffffu) * 128;
+            const double acc = (d >> 30) == 1 ? xs_walk<1, SPMV_SET>(blk, w, lane, sx, a)
+                                              : xs_walk<2, SPMV_SET>(blk, w, lane, sx, a);
+            if (row < a.nrows) a.y[row] = acc;
+        }
+    }
+}
+
+bool spmm_xs(const GpuCsr &m, const double *x, int64_t ldx, double *y, int64_t ldy, int64_t k, hipStream_t s) {
+    if (m.kernel != SPMV_KERNEL_XS || !m.has_xs()) return false;
+    if (m.nrows == 0 || k == 0) return true;
+    XsArgs a{};
+    a.data = m.xs_data.get();
+    a.desc = m.xs_desc.get();
+    a.soff = m.xs_soff.get();
+    a.coff = m.xs_coff.get();
+    a.chunks = m.xs_chunks.get();
+    a.nrows = (int32_t)m.nrows;
+    a.ncols = (int32_t)m.ncols;
+    a.ngroups = (int32_t)m.xs_groups;
+    for (int64_t c0 = 0; c0 < k; c0 += 8) {
+        a.x = x + c0 * ldx;
+        a.y = y + c0 * ldy;
+        spmm_xs_group_kernel<<<dim3((unsigned)m.xs_groups), dim3(XS_BS), 0, s>>>(a, (int)std::min<int64_t>(8, k - c0),
+                                                                               ldx, ldy);
+        FAMG_CHECK_HIP(hipGetLastError());
+    }
+    return true;
+}
+
 // ---------------------------------------------------------------- pipelined form
 // The kernel above pays two dependent memory round trips per staging trip (the
 // chunk id, then its x entries: ten trips of a 1024-thread workgroup for 320

@@ -29,6 +29,7 @@ for s in "$@"; do
         loop8) step r6_loop8 900 python bench.py --loopback 8 --steps 5 --warmup 1 ;;
         one512) step r6_one512 600 python bench.py --workload c4 --steps 10 --warmup 2 --no-cpu-baseline ;;
         spmm) step r6_spmm 300 python scripts/time_spmm.py ;;
+        pmcfused) step r6_pmcfused 600 bash scripts/pmc_fused.sh ;;
         smoke) step r6_smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     esac
 done
