@@ -24,6 +24,7 @@
 // result (test_fine_fused_bitwise).
 #include <algorithm>
 #include <mutex>
+#include <type_traits>
 #include <unordered_map>
 
 #include "famg.hpp"
@@ -296,6 +297,7 @@ struct FineRrArgs {
     int dmode;             // 0 one value, 1 codes, 2 plain
     double dk;             // the fine level's one-value d
     double cst[7];
+    int dbg;               // timing experiments only (FAMG_FINE_DBG): 1 skips the R sums, 2 the residual
 };
 
 // f of fine plane p at the lane's 16-B units of the window (0.0 outside the grid)
@@ -325,18 +327,27 @@ __device__ __forceinline__ void fr_store(const FineRrArgs &a, int gx0, int gy0, 
     }
 }
 
+// one coarse row's fma chain and its class's position tables (registers)
+struct RrChain {
+    uint4 iw[4];   // per plane group: the 16 positions' value indices (bytes)
+    uint2 mk;      // per plane group: 16-bit position masks
+    double ac, ra;
+    int npad, c;
+};
+
 __global__ __launch_bounds__(256) void k_fine_resid_restrict(FineRrArgs a) {
     __shared__ __attribute__((aligned(16))) double fring[4 * FF_PL];
     __shared__ __attribute__((aligned(16))) double rs[2 * FR_WPL];
     __shared__ double st[256];
     __shared__ double sdt[256];
-    // nce dictionary entries, nclass x 5 plane-group starts, then the class ids and
+    // nclass x 5 plane-group starts, the position tables, then the class ids and
     // (coded d_c) diagonal codes of the run's coarse rows (256 per plane, jper planes):
     // no global load in the plane loop waits behind the f prefetch
-    extern __shared__ uint16_t sdyn[];
-    uint16_t *sd = sdyn;
-    uint8_t *skdz = reinterpret_cast<uint8_t *>(sdyn + ((a.nce + 7) & ~7));
-    uint8_t *scl = skdz + ((5 * a.nclass + 15) & ~15);
+    extern __shared__ __attribute__((aligned(16))) uint8_t sdyn[];
+    uint8_t *skdz = sdyn;
+    uint8_t *stab = skdz + ((5 * a.nclass + 15) & ~15);      // 64 B per class (16-B aligned)
+    uint16_t *smk = reinterpret_cast<uint16_t *>(stab + 64 * a.nclass);
+    uint8_t *scl = reinterpret_cast<uint8_t *>(smk + 4 * a.nclass);
     uint8_t *sdc = scl + 256 * a.jper;
     const int tid = threadIdx.x;
     const int t = xcd_remap(blockIdx.x, gridDim.x);
@@ -346,8 +357,22 @@ __global__ __launch_bounds__(256) void k_fine_resid_restrict(FineRrArgs a) {
     const int Zb = chunk * a.jper, Ze = min(Zb + a.jper, a.cz);
     const int64_t cpl = (int64_t)a.cx * a.cy;
     const int wx0 = 2 * X0 - 2, wy0 = 2 * Y0 - 1;  // r window origin (x even: row pairs aligned)
-    for (int b = tid; b < a.nce; b += 256) sd[b] = a.dict[b];
     for (int b = tid; b < 5 * a.nclass; b += 256) skdz[b] = a.kdz[b];
+    // per class and plane group: the value index of each of the 16 in-plane
+    // positions (bytes) and which positions hold an entry (16-bit masks)
+    for (int b = tid; b < 16 * a.nclass; b += 256) reinterpret_cast<uint32_t *>(stab)[b] = 0u;
+    for (int b = tid; b < 4 * a.nclass; b += 256) smk[b] = 0;
+    __syncthreads();
+    for (int b = tid; b < 4 * a.nclass; b += 256) {
+        const int c = b >> 2, g = b & 3;
+        uint32_t m = 0;
+        for (int k = a.kdz[5 * c + g]; k < a.kdz[5 * c + g + 1]; k++) {
+            const uint32_t e = a.dict[c * a.ke + k], pos = e & 15u;
+            stab[64 * c + 16 * g + pos] = (uint8_t)(e >> 8);
+            m |= 1u << pos;
+        }
+        smk[b] = (uint16_t)m;
+    }
     if (tid < a.ntab) st[tid] = a.vtab[tid];
     if (a.dmode == 1) sdt[tid] = a.dtc[tid];
     // the lane's row pairs of the r window: pair q -> (wx, wy) = (2 (q % 34), q / 34)
@@ -372,8 +397,6 @@ __global__ __launch_bounds__(256) void k_fine_resid_restrict(FineRrArgs a) {
         if (a.dmode == 1) sdc[(Z - Zb) * 256 + tid] = a.dcc[J];
     }
     const int base = (2 * ly + 1) * FR_WX + 2 * lx + 2;  // window position of the anchor (2X, 2Y)
-    double acc[2] = {0.0, 0.0}, ra[2] = {0.0, 0.0};
-    int cl[2] = {0, 0};
     const int p0 = 2 * Zb - 1, p1 = 2 * Ze;
     const int fgx0 = 2 * X0 - 4, fgy0 = 2 * Y0 - 2;
     {
@@ -388,7 +411,8 @@ __global__ __launch_bounds__(256) void k_fine_resid_restrict(FineRrArgs a) {
     fr_fetch(a, fgx0, fgy0, p0 + 3, (p0 & 1) ? pa : pb);
     __syncthreads();
 
-    auto step = [&](int p, dbl2_t (&pn)[FF_PU]) {
+    RrChain ch[2];
+    auto step = [&](int p, dbl2_t (&pn)[FF_PU], auto ph) {
         // r(p) = f - A (d f) on the window's row pairs: spmv_dia_kernel<DIA_RESID0_DK, CST>
         const double *fm = fring + ((p - 1) & 3) * FF_PL, *f0 = fring + (p & 3) * FF_PL,
                      *fp = fring + ((p + 1) & 3) * FF_PL;
@@ -396,6 +420,7 @@ __global__ __launch_bounds__(256) void k_fine_resid_restrict(FineRrArgs a) {
         double *rp = rs + (p & 1) * FR_WPL;
 #pragma unroll
         for (int u = 0; u < FR_PP; u++) {
+            if (a.dbg & 2) break;
             const int o = fo[u];
             const dbl2_t zm = *reinterpret_cast<const dbl2_t *>(fm + o), ym = *reinterpret_cast<const dbl2_t *>(f0 + o - FF_WX);
             const dbl2_t xc = *reinterpret_cast<const dbl2_t *>(f0 + o), yp = *reinterpret_cast<const dbl2_t *>(f0 + o + FF_WX);
@@ -422,55 +447,81 @@ __global__ __launch_bounds__(256) void k_fine_resid_restrict(FineRrArgs a) {
         fr_store(a, fgx0, fgy0, fring, p + 2, pn);            // f(p + 2): the slot of p - 2 (unread now)
         fr_fetch(a, fgx0, fgy0, min(p + 4, p1 + 1), pn);      // in flight two planes (unconditional)
         lds_barrier();
-        // the plane's terms of the two coarse chains it belongs to
-        if (live) {
-            // p odd: Z = (p + 1) / 2 starts (dz = -1), Z - 1 continues (dz = +1);
-            // p even: Z = p / 2 continues (dz = 0), Z - 1 ends (dz = +2, then the padding)
-            const int Zn = (p + 1) >> 1, Zo = Zn - 1;
-            const int gn = (p & 1) ? 0 : 1, go = (p & 1) ? 2 : 3;
-            for (int w = 0; w < 2; w++) {
-                const int Z = w == 0 ? Zn : Zo, g = w == 0 ? gn : go;
-                if (Z < Zb || Z >= Ze) continue;
-                const int sl = Z & 1;
-                if (g == 0) {
-                    cl[sl] = scl[(Z - Zb) * 256 + tid];
-                    acc[sl] = 0.0;
-                }
-                const uint8_t *kz = skdz + 5 * cl[sl];
-                const uint16_t *e = sd + cl[sl] * a.ke;
-                double ac = acc[sl];
-                const int k1 = kz[g + 1];
-                for (int k0 = kz[g]; k0 < k1; k0 += 8) {  // 8 terms' reads in flight, then the fmas in order
-                    double cv[8], w[8];
+        if (!live || (a.dbg & 1)) return;
+        // the plane's terms of the two coarse chains it belongs to: chain n (coarse
+        // plane Zn = (p + 1) / 2: dz = -1 at odd p, 0 at even p) and chain o (Zn - 1:
+        // dz = +1, then +2 and the padding); PH = (p - p0) % 4 fixes each chain's
+        // register slot and group at compile time
+        constexpr int PH = decltype(ph)::value;
+        constexpr int sn = (PH >> 1) & 1, so = sn ^ 1, gn = PH & 1, go = 2 + (PH & 1);
+        const int Zn = (p + 1) >> 1, Zo = Zn - 1;
+        const bool nl = Zn < Ze, ol = Zo >= Zb;
+        if (gn == 0 && nl) {  // chain n starts: its class's position tables into registers
+            const int c = scl[(Zn - Zb) * 256 + tid];
+            const uint4 *tw = reinterpret_cast<const uint4 *>(stab) + 4 * c;
 #pragma unroll
-                    for (int j = 0; j < 8; j++) {
-                        const uint32_t c = e[min(k0 + j, a.ke - 1)], s4 = c & 15u;
-                        cv[j] = st[c >> 8];
-                        w[j] = rp[base + ((int)(s4 >> 2) - 1) * FR_WX + (int)(s4 & 3u) - 1];
-                    }
+            for (int g = 0; g < 4; g++) ch[sn].iw[g] = tw[g];
+            ch[sn].mk = *reinterpret_cast<const uint2 *>(smk + 4 * c);
+            ch[sn].npad = a.ke - skdz[5 * c + 4];
+            ch[sn].c = c;
+            ch[sn].ac = 0.0;
+        }
+        // r(p) at the 4 x 4 in-plane positions (dy, dx) in -1..2 of the row's anchor,
+        // shared by both chains; a position's values through its class's byte index
+        double w[16];
 #pragma unroll
-                    for (int j = 0; j < 8; j++) ac = k0 + j < k1 ? fma(cv[j], w[j], ac) : ac;
-                }
-                if (g == 1) ra[sl] = rp[base];  // r at the anchor: the padding entries' operand
-                if (g == 3) {
-                    for (int k = kz[4]; k < a.ke; k++) ac = fma(st[e[k] >> 8], ra[sl], ac);
-                    const int64_t J = (int64_t)Z * cpl + (int64_t)Y * a.cx + X;
-                    a.fc[J] = ac;
-                    const double dd = a.dmode == 0 ? a.dkc : sdt[sdc[(Z - Zb) * 256 + tid]];
-                    a.dfc[J] = dd * ac;  // vec_mul(_coded)'s product
-                }
-                acc[sl] = ac;
+        for (int dy = 0; dy < 4; dy++) {
+            const double *rr = rp + base + (dy - 1) * FR_WX;
+            const dbl2_t m = *reinterpret_cast<const dbl2_t *>(rr);
+            w[4 * dy + 0] = rr[-1];
+            w[4 * dy + 1] = m.x;
+            w[4 * dy + 2] = m.y;
+            w[4 * dy + 3] = rr[2];
+        }
+        auto terms = [&](RrChain &c, int g) {
+            const uint4 iw = c.iw[g];
+            const uint32_t mk = ((g < 2 ? c.mk.x : c.mk.y) >> (16 * (g & 1))) & 0xffffu;
+            const uint32_t wd[4] = {iw.x, iw.y, iw.z, iw.w};
+            double v[16];
+#pragma unroll
+            for (int j = 0; j < 16; j++) v[j] = st[(wd[j >> 2] >> (8 * (j & 3))) & 255u];
+            double ac = c.ac;
+#pragma unroll
+            for (int j = 0; j < 16; j++) ac = (mk >> j) & 1u ? fma(v[j], w[j], ac) : ac;
+            c.ac = ac;
+        };
+        if (nl) {
+            terms(ch[sn], gn);
+            if (gn == 1) ch[sn].ra = w[5];  // r at the anchor: the padding entries' operand
+        }
+        if (ol) {
+            terms(ch[so], go);
+            if (go == 3) {
+                double ac = ch[so].ac;
+                for (int k = 0; k < ch[so].npad; k++) ac = fma(0.0, ch[so].ra, ac);  // +0.0 padding
+                const int64_t J = (int64_t)Zo * cpl + (int64_t)Y * a.cx + X;
+                a.fc[J] = ac;
+                const double dd = a.dmode == 0 ? a.dkc : sdt[sdc[(Zo - Zb) * 256 + tid]];
+                a.dfc[J] = dd * ac;  // vec_mul(_coded)'s product
             }
         }
     };
-    // planes p (odd p0 first): f(p + 2) in pa for even p, pb for odd p
+    // planes p0 .. p1 (p0 = 2 Zb - 1 odd, an even count): f(p + 2) in pb for odd p, pa for even p
+    using P0 = std::integral_constant<int, 0>;
+    using P1 = std::integral_constant<int, 1>;
+    using P2 = std::integral_constant<int, 2>;
+    using P3 = std::integral_constant<int, 3>;
     int p = p0;
-    if (p & 1) step(p++, pb);
-    for (; p + 1 <= p1; p += 2) {
-        step(p, pa);
-        step(p + 1, pb);
+    for (; p + 3 <= p1; p += 4) {
+        step(p, pb, P0{});
+        step(p + 1, pa, P1{});
+        step(p + 2, pb, P2{});
+        step(p + 3, pa, P3{});
     }
-    if (p <= p1) step(p, pa);
+    if (p < p1) {
+        step(p, pb, P0{});
+        step(p + 1, pa, P1{});
+    }
 }
 
 // ------------------------------------------------------------ host side
@@ -547,10 +598,14 @@ void fine_resid_restrict(const GpuCsr &A, const GpuCsr &R, const double *f, doub
     }
     a.dk = dk;
     for (int k = 0; k < 7; k++) a.cst[k] = A.dia_cst_v[k];
+    {
+        const char *e = getenv("FAMG_FINE_DBG");  // timing experiments only (results wrong)
+        a.dbg = e ? atoi(e) : 0;
+    }
     const int64_t ntxy = (int64_t)a.ntx * a.nty;
     // occupancy with the dictionary part of the dynamic LDS (the per-plane class
     // bytes are small), then the run length, then the exact dynamic size
-    const size_t dyn0 = (size_t)((a.nce + 7) & ~7) * 2 + (size_t)((5 * a.nclass + 15) & ~15);
+    const size_t dyn0 = (size_t)((5 * a.nclass + 15) & ~15) + 72 * (size_t)a.nclass;
     const int64_t want = (int64_t)fine_rr_occupancy(dyn0 + 2 * 256 * 16) * std::max(A.ctx ? A.ctx->num_cus : 256, 1);
     a.jper = (int)std::max<int64_t>(1, ceil_div((int64_t)a.cz * ntxy, want));
     if (flag(FLAG_FINE_FUSE) > 1) a.jper = (int)std::max<int64_t>(1, flag(FLAG_FINE_FUSE) / 2);

@@ -30,6 +30,8 @@ for s in "$@"; do
         one512) step r6_one512 600 python bench.py --workload c4 --steps 10 --warmup 2 --no-cpu-baseline ;;
         spmm) step r6_spmm 300 python scripts/time_spmm.py ;;
         pmcfused) step r6_pmcfused 600 bash scripts/pmc_fused.sh ;;
+        timefused) step r6_timefused 300 python scripts/time_fused.py 0 1 2 3 ;;
+        timefused0) step r6_timefused 300 python scripts/time_fused.py 0 ;;
         smoke) step r6_smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     esac
 done
