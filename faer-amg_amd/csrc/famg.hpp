@@ -187,6 +187,9 @@ struct GpuCsr {
     // R: per class the first entry of each fine-plane group dz = -1, 0, 1, 2 and the
     // real entry count (5 bytes; the marching fused restriction of fine.hip)
     DevBuf<uint8_t> gtc_kdz;
+    // R: per class its value at each of the 64 slots (dz, dy, dx) of the 4 x 4 x 4
+    // fine neighbourhood, +0.0 where the class has no entry (fine.hip's scalar terms)
+    DevBuf<double> gtc_wt;
     int64_t gtc_fg[3] = {0, 0, 0}, gtc_cg[3] = {0, 0, 0};
     // wide grid-transfer classes (gtx.hip): 16-bit class per row, dictionary of
     // (window offset, fp64 value) entries in global memory -- every box level

@@ -524,6 +524,245 @@ __global__ __launch_bounds__(256) void k_fine_resid_restrict(FineRrArgs a) {
     }
 }
 
+// k_fine_rr: the same launch (r = f - A (d f), f_c = R r, d_c f_c) with the
+// work per fine plane cut where the counters put it (round 6: 100.7 us of which
+// the R sums ~44 us, the residual ~23 us):
+//   R's terms with scalar weights: per class the 64 slot values (dz, dy, dx) of
+//     the 4 x 4 x 4 neighbourhood in global memory (gtc_wt, +0.0 where the class
+//     has no entry), read by uniform (scalar) loads of the wave's class and fed
+//     to v_fma_f64 as SGPR operands -- a wave whose rows take several classes
+//     (grid edges) walks them one at a time (exec-masked); no value-table
+//     lookups, no masks: an absent slot adds fma(+0.0, r, acc) = acc (r finite,
+//     the accumulator never -0.0), so every chain is the class's entries in
+//     ascending (dz, dy, dx) order, bitwise k_gtc_restrict_march's;
+//   g = d f once per point, when a plane arrives (the seven-point sum is
+//     spmv_dia_kernel's fma chain over d x_j): the z neighbours and the centre
+//     from the lane's registers (every lane keeps the same 16-B units of the
+//     window through the march), only the plane itself in LDS (two slots);
+//   windows start at an odd x (2 X0 - 3 for f, 2 X0 - 1 for r), so a coarse
+//     row's four r values per (dz, dy) are two aligned 16-B LDS reads.
+// LDS 49 KB (three workgroups per CU).  Even nx: a unit (x, x + 1) with x odd
+// straddles the grid only at x = -1 and x = nx - 1, loaded from the clamped
+// pair and shifted.
+constexpr int R2_TX = 32, R2_TY = 8;                        // coarse tile
+constexpr int R2_UX = R2_TX + 3, R2_UY = 2 * R2_TY + 4;     // f/g window: 35 units x 20 rows (x from 2 X0 - 3, y from 2 Y0 - 2)
+constexpr int R2_NU = R2_UX * R2_UY, R2_PU = (R2_NU + 255) / 256;  // 700 units, 3 per lane
+constexpr int R2_RX = R2_TX + 1, R2_RY = 2 * R2_TY + 2;     // r window: 33 units x 18 rows (x from 2 X0 - 1, y from 2 Y0 - 1)
+constexpr int R2_NR = R2_RX * R2_RY;                        // 594
+
+struct FineRr2Args {
+    const uint8_t *cls;  // R's class per coarse row
+    const double *wt;    // nclass x 64 slot values
+    int nx, ny, nz, cx, cy, cz;
+    int ntx, nty, jper;
+    const double *f;
+    double *fc, *dfc;
+    const uint8_t *dcc;  // the coarse level's d: codes into dtc, or one value dkc
+    const double *dtc;
+    double dkc;
+    int dmode;  // 0 one value, 1 codes
+    double dk;  // the fine level's one-value d
+    double cst[7];
+    int dbg;  // timing experiments only (FAMG_FINE_DBG): 1 skips the R sums, 2 the residual
+};
+
+struct Rr2Set {
+    dbl2_t F[R2_PU], G[R2_PU];  // f (shifted, 0.0 outside the grid) and d f of one plane at the lane's units
+};
+
+typedef const __attribute__((address_space(4))) double cdbl_t;
+
+__global__ __launch_bounds__(256) void k_fine_rr(FineRr2Args a) {
+    __shared__ __attribute__((aligned(16))) double gs[2 * 2 * R2_NU];   // d f of planes p, p + 1
+    __shared__ __attribute__((aligned(16))) double rs2[2 * 2 * R2_NR];  // r of planes p, p - 1
+    __shared__ double sdt[256];
+    extern __shared__ __attribute__((aligned(16))) uint8_t sdyn[];  // class ids (+ d_c codes) of the run's coarse rows
+    uint8_t *scl = sdyn, *sdc = sdyn + 256 * a.jper;
+    const int tid = threadIdx.x;
+    const int t = xcd_remap(blockIdx.x, gridDim.x);
+    const int ntxy = a.ntx * a.nty;
+    const int chunk = t / ntxy, txy = t - chunk * ntxy;
+    const int X0 = (txy % a.ntx) * R2_TX, Y0 = (txy / a.ntx) * R2_TY;
+    const int Zb = chunk * a.jper, Ze = min(Zb + a.jper, a.cz);
+    const int64_t cpl = (int64_t)a.cx * a.cy, fpl = (int64_t)a.nx * a.ny;
+    // the lane's units: load offset in a plane (32-bit), shift code, residual slot
+    int off[R2_PU], ri[R2_PU];
+    bool sa[R2_PU], sb[R2_PU], sc[R2_PU], rin[R2_PU], v0[R2_PU], v1[R2_PU];
+#pragma unroll
+    for (int u = 0; u < R2_PU; u++) {
+        const int q = tid + 256 * u, ux = q % R2_UX, uy = q / R2_UX;
+        const int x = 2 * X0 - 3 + 2 * ux, y = 2 * Y0 - 2 + uy;
+        const bool yin = q < R2_NU && (unsigned)y < (unsigned)a.ny;
+        const bool any = yin && x >= -1 && x <= a.nx - 1;
+        sa[u] = any && x >= 0 && x + 1 < a.nx;  // both points: (f[x], f[x + 1])
+        sb[u] = any && x == a.nx - 1;           // loaded (nx - 2, nx - 1): (.y, 0)
+        sc[u] = any && x == -1;                 // loaded (0, 1): (0, .x)
+        off[u] = any ? y * a.nx + min(max(x, 0), a.nx - 2) : 0;
+        rin[u] = q < R2_NU && ux >= 1 && ux <= R2_RX && uy >= 1 && uy <= R2_RY;
+        ri[u] = rin[u] ? (uy - 1) * R2_RX + ux - 1 : 0;
+        v0[u] = yin && x >= 0 && x < a.nx;
+        v1[u] = yin && x + 1 >= 0 && x + 1 < a.nx;
+    }
+    // the lane's coarse row
+    const int lx = tid % R2_TX, ly = tid / R2_TX, X = X0 + lx, Y = Y0 + ly;
+    const bool live = X < a.cx && Y < a.cy;
+    for (int Z = Zb; Z < Ze; Z++) {
+        const int64_t J = live ? (int64_t)Z * cpl + (int64_t)Y * a.cx + X : 0;
+        scl[(Z - Zb) * 256 + tid] = a.cls[J];
+        if (a.dmode == 1) sdc[(Z - Zb) * 256 + tid] = a.dcc[J];
+    }
+    if (a.dmode == 1) sdt[tid] = a.dtc[tid];
+    const int p0 = 2 * Zb - 1, p1 = 2 * Ze;
+    // the stencil in VGPRs (SGPRs go to the chains' weights)
+    double cst[7];
+#pragma unroll
+    for (int k = 0; k < 7; k++) {
+        cst[k] = a.cst[k];
+        asm volatile("" : "+v"(cst[k]));
+    }
+    auto fetch = [&](int p, Rr2Set &S) {
+        const double *fz = a.f + (int64_t)min(max(p, 0), a.nz - 1) * fpl;
+#pragma unroll
+        for (int u = 0; u < R2_PU; u++) S.F[u] = *reinterpret_cast<const dbl2u_t *>(fz + off[u]);
+    };
+    // the arrived plane: shift / zero in place, d f beside it
+    auto settle = [&](int p, Rr2Set &S) {
+        const bool pin = (unsigned)p < (unsigned)a.nz;
+#pragma unroll
+        for (int u = 0; u < R2_PU; u++) {
+            const dbl2_t v = S.F[u];
+            const double x0 = sa[u] ? v.x : sb[u] ? v.y : 0.0;
+            const double x1 = sa[u] ? v.y : sc[u] ? v.x : 0.0;
+            S.F[u] = pin ? dbl2_t{x0, x1} : dbl2_t{0.0, 0.0};
+            S.G[u] = a.dk * S.F[u];
+        }
+    };
+    auto publish = [&](int p, const Rr2Set &S) {
+        double *g = gs + (p & 1) * 2 * R2_NU;
+#pragma unroll
+        for (int u = 0; u < R2_PU; u++) {
+            const int q = tid + 256 * u;
+            if (q < R2_NU) *reinterpret_cast<dbl2_t *>(g + 2 * q) = S.G[u];
+        }
+    };
+    Rr2Set S0, S1, S2, S3;  // plane p0 + k in set k mod 4
+    fetch(p0 - 1, S3);
+    fetch(p0, S0);
+    fetch(p0 + 1, S1);
+    settle(p0 - 1, S3);
+    settle(p0, S0);
+    publish(p0, S0);
+    fetch(p0 + 2, S2);
+    __syncthreads();
+
+    double acc[2] = {0.0, 0.0};
+    int cc[2] = {0, 0};
+    cdbl_t *wt = (cdbl_t *)a.wt;
+    // one chain's 16 terms of plane group g, the wave's classes one at a time
+    auto terms = [&](int sl, int g, const double (&w)[16]) {
+        const int c = cc[sl];
+        // a uniform loop over the classes of the wave's active lanes: the weights
+        // loaded outside the divergent branch (inside it the optimiser would use
+        // the lane's own c for the address: vector loads)
+        uint64_t todo = __ballot(1);
+        while (todo) {
+            const int cu = __builtin_amdgcn_readlane(c, (int)__builtin_ctzll(todo));
+            cdbl_t *wp = wt + (cu * 4 + g) * 16;
+            double wv[16];
+#pragma unroll
+            for (int j = 0; j < 16; j++) wv[j] = wp[j];
+            // held in SGPRs here (not sunk into the branch), one wait for all 16
+            asm volatile("" : "+s"(wv[0]), "+s"(wv[1]), "+s"(wv[2]), "+s"(wv[3]), "+s"(wv[4]), "+s"(wv[5]),
+                         "+s"(wv[6]), "+s"(wv[7]), "+s"(wv[8]), "+s"(wv[9]), "+s"(wv[10]), "+s"(wv[11]),
+                         "+s"(wv[12]), "+s"(wv[13]), "+s"(wv[14]), "+s"(wv[15]));
+            const bool mine = c == cu;
+            if (mine) {
+                double ac = acc[sl];
+#pragma unroll
+                for (int j = 0; j < 16; j++) ac = fma(wv[j], w[j], ac);
+                acc[sl] = ac;
+            }
+            todo &= ~__ballot(mine);
+        }
+    };
+    // step p: Sm = plane p - 1 (its G), S0 = p, S1 = p + 1 (arrived), S3 = p + 3 (issued here; the set of p - 1)
+    auto step = [&](int p, Rr2Set &Sm, Rr2Set &Sp, Rr2Set &S1p, Rr2Set &S3p, auto ph) {
+        settle(p + 1, S1p);
+        publish(p + 1, S1p);  // the slot of p - 1: its in-plane reads ended before the last barrier
+        const double *g0 = gs + (p & 1) * 2 * R2_NU;
+        double *rp = rs2 + (p & 1) * 2 * R2_NR;
+        const bool pin = (unsigned)p < (unsigned)a.nz;
+#pragma unroll
+        for (int u = 0; u < R2_PU; u++) {
+            if (!rin[u] || (a.dbg & 2)) continue;
+            const int q = tid + 256 * u;
+            const dbl2_t ym = *reinterpret_cast<const dbl2_t *>(g0 + 2 * (q - R2_UX));
+            const dbl2_t yp = *reinterpret_cast<const dbl2_t *>(g0 + 2 * (q + R2_UX));
+            const double xl = g0[2 * q - 1], xr = g0[2 * q + 2];
+            const dbl2_t gm = Sm.G[u], gc = Sp.G[u], gp = S1p.G[u];
+            const double y0[7] = {gm.x, ym.x, xl, gc.x, gc.y, yp.x, gp.x};
+            const double y1[7] = {gm.y, ym.y, gc.x, gc.y, xr, yp.y, gp.y};
+            double acc0 = 0.0, acc1 = 0.0;
+#pragma unroll
+            for (int k = 0; k < 7; k++) {
+                acc0 = fma(cst[k], y0[k], acc0);
+                acc1 = fma(cst[k], y1[k], acc1);
+            }
+            const dbl2_t b = Sp.F[u];
+            *reinterpret_cast<dbl2_t *>(rp + 2 * ri[u]) =
+                dbl2_t{pin && v0[u] ? b.x - acc0 : 0.0, pin && v1[u] ? b.y - acc1 : 0.0};
+        }
+        fetch(min(p + 3, p1 + 1), S3p);  // in flight two planes
+        lds_barrier();
+        if (!live || (a.dbg & 1)) return;
+        constexpr int PH = decltype(ph)::value;
+        constexpr int sn = (PH >> 1) & 1, so = sn ^ 1, gn = PH & 1, go = 2 + (PH & 1);
+        const int Zn = (p + 1) >> 1, Zo = Zn - 1;
+        const bool nl = Zn < Ze, ol = Zo >= Zb;
+        if (gn == 0 && nl) {
+            cc[sn] = scl[(Zn - Zb) * 256 + tid];
+            acc[sn] = 0.0;
+        }
+        // r(p) at the 4 x 4 positions (dy, dx) in -1..2 of the anchor (2X, 2Y): units lx, lx + 1 of rows 2 ly + dy
+        double w[16];
+#pragma unroll
+        for (int dy = 0; dy < 4; dy++) {
+            const double *rr = rp + 2 * ((2 * ly + dy) * R2_RX + lx);
+            const dbl2_t m0 = *reinterpret_cast<const dbl2_t *>(rr);
+            const dbl2_t m1 = *reinterpret_cast<const dbl2_t *>(rr + 2);
+            w[4 * dy + 0] = m0.x;
+            w[4 * dy + 1] = m0.y;
+            w[4 * dy + 2] = m1.x;
+            w[4 * dy + 3] = m1.y;
+        }
+        if (nl) terms(sn, gn, w);
+        if (ol) {
+            terms(so, go, w);
+            if (go == 3) {
+                const int64_t J = (int64_t)Zo * cpl + (int64_t)Y * a.cx + X;
+                a.fc[J] = acc[so];
+                const double dd = a.dmode == 0 ? a.dkc : sdt[sdc[(Zo - Zb) * 256 + tid]];
+                a.dfc[J] = dd * acc[so];  // vec_mul(_coded)'s product
+            }
+        }
+    };
+    using P0 = std::integral_constant<int, 0>;
+    using P1 = std::integral_constant<int, 1>;
+    using P2 = std::integral_constant<int, 2>;
+    using P3 = std::integral_constant<int, 3>;
+    int p = p0;
+    for (; p + 3 <= p1; p += 4) {
+        step(p, S3, S0, S1, S3, P0{});
+        step(p + 1, S0, S1, S2, S0, P1{});
+        step(p + 2, S1, S2, S3, S1, P2{});
+        step(p + 3, S2, S3, S0, S2, P3{});
+    }
+    if (p < p1) {
+        step(p, S3, S0, S1, S3, P0{});
+        step(p + 1, S0, S1, S2, S0, P1{});
+    }
+}
+
 // ------------------------------------------------------------ host side
 
 // workgroups of k_fine_interp_jacobi per CU (cached)
@@ -566,11 +805,84 @@ bool fine_resid_restrict_ok(const GpuCsr &A, const GpuCsr &R, const SpmvEpi &epi
     if (!epic.y2 || !epic.dc) return false;
     for (int q = 0; q < 3; q++)
         if (R.gtc_fg[q] != A.dia_cst_n[q] || R.gtc_cg[q] != (R.gtc_fg[q] + 1) / 2) return false;
+    // even nx: the 16-B units of a window row never straddle the end of a grid row
+    // except where the kernels shift them (an odd nx runs the unfused launches)
+    if (R.gtc_fg[0] % 2 != 0) return false;
     return A.nrows == R.ncols && R.nrows == R.gtc_cg[0] * R.gtc_cg[1] * R.gtc_cg[2];
+}
+
+// workgroups of k_fine_rr per CU with dyn bytes of class ids (cached)
+static int fine_rr2_occupancy(size_t dyn) {
+    static std::mutex mu;
+    static std::unordered_map<size_t, int> cache;
+    std::lock_guard<std::mutex> lk(mu);
+    auto it = cache.find(dyn);
+    if (it != cache.end()) return it->second;
+    int v = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&v, k_fine_rr, 256, dyn) != hipSuccess || v < 1) {
+        (void)hipGetLastError();
+        v = 1;
+    }
+    cache[dyn] = v;
+    return v;
+}
+
+// FAMG_FINE_RR=1: the round-5 resid+restrict kernel (A/B timing)
+static bool fine_rr_v1() {
+    static const bool on = [] {
+        const char *e = getenv("FAMG_FINE_RR");
+        return e && e[0] == '1';
+    }();
+    return on;
+}
+
+static void fine_rr2(const GpuCsr &A, const GpuCsr &R, const double *f, double dk, double *fc, const SpmvEpi &epic,
+                     hipStream_t s) {
+    FineRr2Args a{};
+    a.cls = R.gtc_cls.get();
+    a.wt = R.gtc_wt.get();
+    a.nx = (int)R.gtc_fg[0]; a.ny = (int)R.gtc_fg[1]; a.nz = (int)R.gtc_fg[2];
+    a.cx = (int)R.gtc_cg[0]; a.cy = (int)R.gtc_cg[1]; a.cz = (int)R.gtc_cg[2];
+    a.ntx = (int)ceil_div(a.cx, R2_TX);
+    a.nty = (int)ceil_div(a.cy, R2_TY);
+    a.f = f;
+    a.fc = fc;
+    a.dfc = epic.y2;
+    if (epic.dc && epic.dk != 0.0 && flag(FLAG_DIA_DK) != 0) {
+        a.dmode = 0;
+        a.dkc = epic.dk;
+    } else {
+        a.dmode = 1;
+        a.dcc = epic.dc;
+        a.dtc = epic.dt;
+    }
+    a.dk = dk;
+    for (int k = 0; k < 7; k++) a.cst[k] = A.dia_cst_v[k];
+    {
+        const char *e = getenv("FAMG_FINE_DBG");  // timing experiments only (results wrong)
+        a.dbg = e ? atoi(e) : 0;
+    }
+    const int64_t ntxy = (int64_t)a.ntx * a.nty;
+    // occupancy at a typical run length, then the run length for one round of workgroups
+    const int64_t want = (int64_t)fine_rr2_occupancy(2 * 256 * 12) * std::max(A.ctx ? A.ctx->num_cus : 256, 1);
+    a.jper = (int)std::max<int64_t>(1, ceil_div((int64_t)a.cz * ntxy, want));
+    if (flag(FLAG_FINE_FUSE) > 1) a.jper = (int)std::max<int64_t>(1, flag(FLAG_FINE_FUSE) / 2);
+    a.jper = std::min(a.jper, 64);
+    const size_t dyn = (size_t)2 * 256 * a.jper;
+    const dim3 grid((unsigned)(ntxy * ceil_div(a.cz, a.jper)));
+    k_fine_rr<<<grid, dim3(256), dyn, s>>>(a);
+    FAMG_CHECK_HIP(hipGetLastError());
 }
 
 void fine_resid_restrict(const GpuCsr &A, const GpuCsr &R, const double *f, double dk, double *fc,
                          const SpmvEpi &epic, hipStream_t s) {
+    if (!fine_rr_v1() && R.gtc_wt.get() && R.gtc_fg[0] * R.gtc_fg[1] < (int64_t(1) << 31)) {
+        fine_rr2(A, R, f, dk, fc, epic, s);
+        const int64_t n = A.nrows, nc = R.nrows;
+        log_launch("fine-rr", SPMV_KERNEL_DIA, -1, n, 8 * n + 16 * nc + nc + (epic.dc && !(epic.dk != 0.0 && flag(FLAG_DIA_DK) != 0) ? nc : 0),
+                   (12 * A.nnz + 4 * (n + 1) + 32 * n) + (12 * R.nnz + 4 * (nc + 1) + 8 * n + 16 * nc));
+        return;
+    }
     FineRrArgs a{};
     a.cls = R.gtc_cls.get();
     a.dict = R.gtc_dict.get();

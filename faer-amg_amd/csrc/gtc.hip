@@ -462,6 +462,7 @@ void gtc_release(GpuCsr &m) {
     m.gtc_dict.release();
     m.gtc_vtab.release();
     m.gtc_kdz.release();
+    m.gtc_wt.release();
     m.gtc_ke = m.gtc_nce = m.gtc_ntab = m.gtc_nclass = 0;
     m.gtc_r = m.gtc_on = false;
 }
@@ -536,6 +537,12 @@ bool gtc_attach(GpuCsr &m, const int64_t *fg, const int64_t *cg, int which) {
         }
         m.gtc_kdz.resize(kdz.size());
         FAMG_CHECK_HIP(hipMemcpyAsync(m.gtc_kdz.get(), kdz.data(), kdz.size(), hipMemcpyHostToDevice, s));
+        // the slot-indexed values (a slot holds at most one entry: one column)
+        std::vector<double> wt(dict.size() * 64, 0.0);
+        for (size_t c = 0; c < dict.size(); c++)
+            for (const auto &e : dict[c]) wt[c * 64 + e.first] = e.second;
+        m.gtc_wt.resize(wt.size());
+        FAMG_CHECK_HIP(hipMemcpyAsync(m.gtc_wt.get(), wt.data(), wt.size() * 8, hipMemcpyHostToDevice, s));
     }
     FAMG_CHECK_HIP(hipStreamSynchronize(s));
     m.gtc_nclass = (int)dict.size();
