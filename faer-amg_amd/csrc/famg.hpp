@@ -187,8 +187,9 @@ struct GpuCsr {
     // R: per class the first entry of each fine-plane group dz = -1, 0, 1, 2 and the
     // real entry count (5 bytes; the marching fused restriction of fine.hip)
     DevBuf<uint8_t> gtc_kdz;
-    // R: per class its value at each of the 64 slots (dz, dy, dx) of the 4 x 4 x 4
-    // fine neighbourhood, +0.0 where the class has no entry (fine.hip's scalar terms)
+    // R: per class its value at each of the 32 slots (dz, dy, dx) a 2 x 2 x 2 box
+    // smoothed by the 7-point stencil reaches, +0.0 where the class has no entry
+    // (fine.hip k_fine_rr); empty when some class has an entry outside them
     DevBuf<double> gtc_wt;
     int64_t gtc_fg[3] = {0, 0, 0}, gtc_cg[3] = {0, 0, 0};
     // wide grid-transfer classes (gtx.hip): 16-bit class per row, dictionary of

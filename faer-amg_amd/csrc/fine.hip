@@ -527,32 +527,36 @@ __global__ __launch_bounds__(256) void k_fine_resid_restrict(FineRrArgs a) {
 // k_fine_rr: the same launch (r = f - A (d f), f_c = R r, d_c f_c) with the
 // work per fine plane cut where the counters put it (round 6: 100.7 us of which
 // the R sums ~44 us, the residual ~23 us):
-//   R's terms with scalar weights: per class the 64 slot values (dz, dy, dx) of
-//     the 4 x 4 x 4 neighbourhood in global memory (gtc_wt, +0.0 where the class
-//     has no entry), read by uniform (scalar) loads of the wave's class and fed
-//     to v_fma_f64 as SGPR operands -- a wave whose rows take several classes
-//     (grid edges) walks them one at a time (exec-masked); no value-table
-//     lookups, no masks: an absent slot adds fma(+0.0, r, acc) = acc (r finite,
-//     the accumulator never -0.0), so every chain is the class's entries in
-//     ascending (dz, dy, dx) order, bitwise k_gtc_restrict_march's;
+//   R's terms without value-table lookups or masks: every class's entries lie in
+//     the 32 slots (dz, dy, dx) a 2 x 2 x 2 box smoothed by the 7-point stencil
+//     reaches (4 at dz = -1, 12 at dz = 0, 12 at dz = 1, 4 at dz = 2), so each
+//     class is 32 fp64 weights in LDS (gtc_wt, +0.0 where the class has no
+//     entry) and a plane adds 4 or 12 fma terms per chain: an absent slot adds
+//     fma(+0.0, r, acc) = acc (r finite, the accumulator never -0.0), so every
+//     chain is the class's entries in ascending (dz, dy, dx) order, bitwise
+//     k_gtc_restrict_march's; the two chains of a plane interleave;
 //   g = d f once per point, when a plane arrives (the seven-point sum is
 //     spmv_dia_kernel's fma chain over d x_j): the z neighbours and the centre
 //     from the lane's registers (every lane keeps the same 16-B units of the
 //     window through the march), only the plane itself in LDS (two slots);
 //   windows start at an odd x (2 X0 - 3 for f, 2 X0 - 1 for r), so a coarse
-//     row's four r values per (dz, dy) are two aligned 16-B LDS reads.
-// LDS 49 KB (three workgroups per CU).  Even nx: a unit (x, x + 1) with x odd
-// straddles the grid only at x = -1 and x = nx - 1, loaded from the clamped
-// pair and shifted.
+//     row's four r values per (dz, dy) are two aligned 16-B LDS reads;
+//   the class ids and d_c codes of the next coarse plane load with the f plane
+//     two steps ahead (no LDS staging, no wait of their own).
+// Three workgroups per CU.  Even nx: a unit (x, x + 1) with x odd straddles the
+// grid only at x = -1 and x = nx - 1, loaded from the clamped pair and shifted.
 constexpr int R2_TX = 32, R2_TY = 8;                        // coarse tile
 constexpr int R2_UX = R2_TX + 3, R2_UY = 2 * R2_TY + 4;     // f/g window: 35 units x 20 rows (x from 2 X0 - 3, y from 2 Y0 - 2)
 constexpr int R2_NU = R2_UX * R2_UY, R2_PU = (R2_NU + 255) / 256;  // 700 units, 3 per lane
 constexpr int R2_RX = R2_TX + 1, R2_RY = 2 * R2_TY + 2;     // r window: 33 units x 18 rows (x from 2 X0 - 1, y from 2 Y0 - 1)
 constexpr int R2_NR = R2_RX * R2_RY;                        // 594
+constexpr int R2_WS = 34;                                   // LDS doubles per class (32 weights, padded against bank repeats)
+constexpr int R2_CMAX = 32;                                 // classes (LDS: 8.7 KB)
 
 struct FineRr2Args {
     const uint8_t *cls;  // R's class per coarse row
-    const double *wt;    // nclass x 64 slot values
+    const double *wt;    // nclass x 32 weights (the 32-slot pattern)
+    int nclass;
     int nx, ny, nz, cx, cy, cz;
     int ntx, nty, jper;
     const double *f;
@@ -570,14 +574,11 @@ struct Rr2Set {
     dbl2_t F[R2_PU], G[R2_PU];  // f (shifted, 0.0 outside the grid) and d f of one plane at the lane's units
 };
 
-typedef const __attribute__((address_space(4))) double cdbl_t;
-
-__global__ __launch_bounds__(256) void k_fine_rr(FineRr2Args a) {
+__global__ __launch_bounds__(256, 3) void k_fine_rr(FineRr2Args a) {
     __shared__ __attribute__((aligned(16))) double gs[2 * 2 * R2_NU];   // d f of planes p, p + 1
     __shared__ __attribute__((aligned(16))) double rs2[2 * 2 * R2_NR];  // r of planes p, p - 1
     __shared__ double sdt[256];
-    extern __shared__ __attribute__((aligned(16))) uint8_t sdyn[];  // class ids (+ d_c codes) of the run's coarse rows
-    uint8_t *scl = sdyn, *sdc = sdyn + 256 * a.jper;
+    extern __shared__ __attribute__((aligned(16))) double sw[];  // the classes' weights, R2_WS per class
     const int tid = threadIdx.x;
     const int t = xcd_remap(blockIdx.x, gridDim.x);
     const int ntxy = a.ntx * a.nty;
@@ -585,6 +586,8 @@ __global__ __launch_bounds__(256) void k_fine_rr(FineRr2Args a) {
     const int X0 = (txy % a.ntx) * R2_TX, Y0 = (txy / a.ntx) * R2_TY;
     const int Zb = chunk * a.jper, Ze = min(Zb + a.jper, a.cz);
     const int64_t cpl = (int64_t)a.cx * a.cy, fpl = (int64_t)a.nx * a.ny;
+    for (int b = tid; b < a.nclass * 32; b += 256) sw[(b >> 5) * R2_WS + (b & 31)] = a.wt[b];
+    if (a.dmode == 1) sdt[tid] = a.dtc[tid];
     // the lane's units: load offset in a plane (32-bit), shift code, residual slot
     int off[R2_PU], ri[R2_PU];
     bool sa[R2_PU], sb[R2_PU], sc[R2_PU], rin[R2_PU], v0[R2_PU], v1[R2_PU];
@@ -606,24 +609,19 @@ __global__ __launch_bounds__(256) void k_fine_rr(FineRr2Args a) {
     // the lane's coarse row
     const int lx = tid % R2_TX, ly = tid / R2_TX, X = X0 + lx, Y = Y0 + ly;
     const bool live = X < a.cx && Y < a.cy;
-    for (int Z = Zb; Z < Ze; Z++) {
-        const int64_t J = live ? (int64_t)Z * cpl + (int64_t)Y * a.cx + X : 0;
-        scl[(Z - Zb) * 256 + tid] = a.cls[J];
-        if (a.dmode == 1) sdc[(Z - Zb) * 256 + tid] = a.dcc[J];
-    }
-    if (a.dmode == 1) sdt[tid] = a.dtc[tid];
+    const int64_t Jxy = live ? (int64_t)Y * a.cx + X : 0;
     const int p0 = 2 * Zb - 1, p1 = 2 * Ze;
-    // the stencil in VGPRs (SGPRs go to the chains' weights)
-    double cst[7];
-#pragma unroll
-    for (int k = 0; k < 7; k++) {
-        cst[k] = a.cst[k];
-        asm volatile("" : "+v"(cst[k]));
-    }
     auto fetch = [&](int p, Rr2Set &S) {
         const double *fz = a.f + (int64_t)min(max(p, 0), a.nz - 1) * fpl;
 #pragma unroll
         for (int u = 0; u < R2_PU; u++) S.F[u] = *reinterpret_cast<const dbl2u_t *>(fz + off[u]);
+    };
+    // class id and d_c code of coarse plane Z (clamped: a plane past the run is never used)
+    int ncls = 0, ndc = 0;
+    auto fetch_cls = [&](int Z) {
+        const int64_t J = (int64_t)min(Z, a.cz - 1) * cpl + Jxy;
+        ncls = a.cls[J];
+        if (a.dmode == 1) ndc = a.dcc[J];
     };
     // the arrived plane: shift / zero in place, d f beside it
     auto settle = [&](int p, Rr2Set &S) {
@@ -649,6 +647,7 @@ __global__ __launch_bounds__(256) void k_fine_rr(FineRr2Args a) {
     fetch(p0 - 1, S3);
     fetch(p0, S0);
     fetch(p0 + 1, S1);
+    fetch_cls(Zb);
     settle(p0 - 1, S3);
     settle(p0, S0);
     publish(p0, S0);
@@ -656,37 +655,11 @@ __global__ __launch_bounds__(256) void k_fine_rr(FineRr2Args a) {
     __syncthreads();
 
     double acc[2] = {0.0, 0.0};
-    int cc[2] = {0, 0};
-    cdbl_t *wt = (cdbl_t *)a.wt;
-    // one chain's 16 terms of plane group g, the wave's classes one at a time
-    auto terms = [&](int sl, int g, const double (&w)[16]) {
-        const int c = cc[sl];
-        // a uniform loop over the classes of the wave's active lanes: the weights
-        // loaded outside the divergent branch (inside it the optimiser would use
-        // the lane's own c for the address: vector loads)
-        uint64_t todo = __ballot(1);
-        while (todo) {
-            const int cu = __builtin_amdgcn_readlane(c, (int)__builtin_ctzll(todo));
-            cdbl_t *wp = wt + (cu * 4 + g) * 16;
-            double wv[16];
-#pragma unroll
-            for (int j = 0; j < 16; j++) wv[j] = wp[j];
-            // held in SGPRs here (not sunk into the branch), one wait for all 16
-            asm volatile("" : "+s"(wv[0]), "+s"(wv[1]), "+s"(wv[2]), "+s"(wv[3]), "+s"(wv[4]), "+s"(wv[5]),
-                         "+s"(wv[6]), "+s"(wv[7]), "+s"(wv[8]), "+s"(wv[9]), "+s"(wv[10]), "+s"(wv[11]),
-                         "+s"(wv[12]), "+s"(wv[13]), "+s"(wv[14]), "+s"(wv[15]));
-            const bool mine = c == cu;
-            if (mine) {
-                double ac = acc[sl];
-#pragma unroll
-                for (int j = 0; j < 16; j++) ac = fma(wv[j], w[j], ac);
-                acc[sl] = ac;
-            }
-            todo &= ~__ballot(mine);
-        }
-    };
+    int cb[2] = {0, 0}, dq[2] = {0, 0};  // per chain: its class's weights in sw, its d_c code
     // step p: Sm = plane p - 1 (its G), S0 = p, S1 = p + 1 (arrived), S3 = p + 3 (issued here; the set of p - 1)
     auto step = [&](int p, Rr2Set &Sm, Rr2Set &Sp, Rr2Set &S1p, Rr2Set &S3p, auto ph) {
+        constexpr int PH = decltype(ph)::value;
+        constexpr int sn = (PH >> 1) & 1, so = sn ^ 1, gn = PH & 1, go = 2 + (PH & 1);
         settle(p + 1, S1p);
         publish(p + 1, S1p);  // the slot of p - 1: its in-plane reads ended before the last barrier
         const double *g0 = gs + (p & 1) * 2 * R2_NU;
@@ -705,24 +678,24 @@ __global__ __launch_bounds__(256) void k_fine_rr(FineRr2Args a) {
             double acc0 = 0.0, acc1 = 0.0;
 #pragma unroll
             for (int k = 0; k < 7; k++) {
-                acc0 = fma(cst[k], y0[k], acc0);
-                acc1 = fma(cst[k], y1[k], acc1);
+                acc0 = fma(a.cst[k], y0[k], acc0);
+                acc1 = fma(a.cst[k], y1[k], acc1);
             }
             const dbl2_t b = Sp.F[u];
             *reinterpret_cast<dbl2_t *>(rp + 2 * ri[u]) =
                 dbl2_t{pin && v0[u] ? b.x - acc0 : 0.0, pin && v1[u] ? b.y - acc1 : 0.0};
         }
         fetch(min(p + 3, p1 + 1), S3p);  // in flight two planes
-        lds_barrier();
-        if (!live || (a.dbg & 1)) return;
-        constexpr int PH = decltype(ph)::value;
-        constexpr int sn = (PH >> 1) & 1, so = sn ^ 1, gn = PH & 1, go = 2 + (PH & 1);
         const int Zn = (p + 1) >> 1, Zo = Zn - 1;
         const bool nl = Zn < Ze, ol = Zo >= Zb;
-        if (gn == 0 && nl) {
-            cc[sn] = scl[(Zn - Zb) * 256 + tid];
+        if (gn == 0 && nl) {  // chain n starts: its class (loaded two steps ago); the next one's load
+            cb[sn] = ncls * R2_WS;
+            dq[sn] = ndc;
             acc[sn] = 0.0;
+            fetch_cls(Zn + 1);
         }
+        lds_barrier();
+        if (!live || (a.dbg & 1)) return;
         // r(p) at the 4 x 4 positions (dy, dx) in -1..2 of the anchor (2X, 2Y): units lx, lx + 1 of rows 2 ly + dy
         double w[16];
 #pragma unroll
@@ -735,15 +708,41 @@ __global__ __launch_bounds__(256) void k_fine_rr(FineRr2Args a) {
             w[4 * dy + 2] = m1.x;
             w[4 * dy + 3] = m1.y;
         }
-        if (nl) terms(sn, gn, w);
-        if (ol) {
-            terms(so, go, w);
-            if (go == 3) {
-                const int64_t J = (int64_t)Zo * cpl + (int64_t)Y * a.cx + X;
-                a.fc[J] = acc[so];
-                const double dd = a.dmode == 0 ? a.dkc : sdt[sdc[(Zo - Zb) * 256 + tid]];
-                a.dfc[J] = dd * acc[so];  // vec_mul(_coded)'s product
+        // the slots of a plane group: 4 (dz = -1, 2) or 12 (dz = 0, 1), as w indices
+        constexpr int P4[4] = {5, 6, 9, 10};
+        constexpr int P12[12] = {1, 2, 4, 5, 6, 7, 8, 9, 10, 11, 13, 14};
+        constexpr int NN = (gn == 0) ? 4 : 12, NO = (go == 3) ? 4 : 12;
+        constexpr int ON = (gn == 0) ? 0 : 4, OO = (go == 2) ? 16 : 28;
+        double wn[NN], wo[NO];
+        if (nl) {
+#pragma unroll
+            for (int k = 0; k < NN; k += 2) {
+                const dbl2_t v = *reinterpret_cast<const dbl2_t *>(sw + cb[sn] + ON + k);
+                wn[k] = v.x;
+                wn[k + 1] = v.y;
             }
+        }
+        if (ol) {
+#pragma unroll
+            for (int k = 0; k < NO; k += 2) {
+                const dbl2_t v = *reinterpret_cast<const dbl2_t *>(sw + cb[so] + OO + k);
+                wo[k] = v.x;
+                wo[k + 1] = v.y;
+            }
+        }
+        double an = acc[sn], ao = acc[so];
+#pragma unroll
+        for (int k = 0; k < 12; k++) {
+            if (nl && k < NN) an = fma(wn[k], w[NN == 4 ? P4[k % 4] : P12[k]], an);
+            if (ol && k < NO) ao = fma(wo[k], w[NO == 4 ? P4[k % 4] : P12[k]], ao);
+        }
+        acc[sn] = an;
+        acc[so] = ao;
+        if (go == 3 && ol) {
+            const int64_t J = (int64_t)Zo * cpl + Jxy;
+            a.fc[J] = ao;
+            const double dd = a.dmode == 0 ? a.dkc : sdt[dq[so]];
+            a.dfc[J] = dd * ao;  // vec_mul(_coded)'s product
         }
     };
     using P0 = std::integral_constant<int, 0>;
@@ -811,7 +810,7 @@ bool fine_resid_restrict_ok(const GpuCsr &A, const GpuCsr &R, const SpmvEpi &epi
     return A.nrows == R.ncols && R.nrows == R.gtc_cg[0] * R.gtc_cg[1] * R.gtc_cg[2];
 }
 
-// workgroups of k_fine_rr per CU with dyn bytes of class ids (cached)
+// workgroups of k_fine_rr per CU (cached)
 static int fine_rr2_occupancy(size_t dyn) {
     static std::mutex mu;
     static std::unordered_map<size_t, int> cache;
@@ -841,6 +840,7 @@ static void fine_rr2(const GpuCsr &A, const GpuCsr &R, const double *f, double d
     FineRr2Args a{};
     a.cls = R.gtc_cls.get();
     a.wt = R.gtc_wt.get();
+    a.nclass = R.gtc_nclass;
     a.nx = (int)R.gtc_fg[0]; a.ny = (int)R.gtc_fg[1]; a.nz = (int)R.gtc_fg[2];
     a.cx = (int)R.gtc_cg[0]; a.cy = (int)R.gtc_cg[1]; a.cz = (int)R.gtc_cg[2];
     a.ntx = (int)ceil_div(a.cx, R2_TX);
@@ -864,11 +864,10 @@ static void fine_rr2(const GpuCsr &A, const GpuCsr &R, const double *f, double d
     }
     const int64_t ntxy = (int64_t)a.ntx * a.nty;
     // occupancy at a typical run length, then the run length for one round of workgroups
-    const int64_t want = (int64_t)fine_rr2_occupancy(2 * 256 * 12) * std::max(A.ctx ? A.ctx->num_cus : 256, 1);
+    const size_t dyn = (size_t)8 * R2_WS * a.nclass;
+    const int64_t want = (int64_t)fine_rr2_occupancy(dyn) * std::max(A.ctx ? A.ctx->num_cus : 256, 1);
     a.jper = (int)std::max<int64_t>(1, ceil_div((int64_t)a.cz * ntxy, want));
     if (flag(FLAG_FINE_FUSE) > 1) a.jper = (int)std::max<int64_t>(1, flag(FLAG_FINE_FUSE) / 2);
-    a.jper = std::min(a.jper, 64);
-    const size_t dyn = (size_t)2 * 256 * a.jper;
     const dim3 grid((unsigned)(ntxy * ceil_div(a.cz, a.jper)));
     k_fine_rr<<<grid, dim3(256), dyn, s>>>(a);
     FAMG_CHECK_HIP(hipGetLastError());
@@ -876,7 +875,7 @@ static void fine_rr2(const GpuCsr &A, const GpuCsr &R, const double *f, double d
 
 void fine_resid_restrict(const GpuCsr &A, const GpuCsr &R, const double *f, double dk, double *fc,
                          const SpmvEpi &epic, hipStream_t s) {
-    if (!fine_rr_v1() && R.gtc_wt.get() && R.gtc_fg[0] * R.gtc_fg[1] < (int64_t(1) << 31)) {
+    if (!fine_rr_v1() && R.gtc_wt.get() && R.gtc_nclass <= R2_CMAX && R.gtc_fg[0] * R.gtc_fg[1] < (int64_t(1) << 31)) {
         fine_rr2(A, R, f, dk, fc, epic, s);
         const int64_t n = A.nrows, nc = R.nrows;
         log_launch("fine-rr", SPMV_KERNEL_DIA, -1, n, 8 * n + 16 * nc + nc + (epic.dc && !(epic.dk != 0.0 && flag(FLAG_DIA_DK) != 0) ? nc : 0),

@@ -537,12 +537,31 @@ bool gtc_attach(GpuCsr &m, const int64_t *fg, const int64_t *cg, int which) {
         }
         m.gtc_kdz.resize(kdz.size());
         FAMG_CHECK_HIP(hipMemcpyAsync(m.gtc_kdz.get(), kdz.data(), kdz.size(), hipMemcpyHostToDevice, s));
-        // the slot-indexed values (a slot holds at most one entry: one column)
-        std::vector<double> wt(dict.size() * 64, 0.0);
-        for (size_t c = 0; c < dict.size(); c++)
-            for (const auto &e : dict[c]) wt[c * 64 + e.first] = e.second;
-        m.gtc_wt.resize(wt.size());
-        FAMG_CHECK_HIP(hipMemcpyAsync(m.gtc_wt.get(), wt.data(), wt.size() * 8, hipMemcpyHostToDevice, s));
+        // the 32-slot weights (fine.hip k_fine_rr): every entry in the slots a
+        // 2 x 2 x 2 box smoothed by the 7-point stencil reaches, else none
+        static const int8_t pat[64] = {
+            // dz = -1: (dy, dx) in {1, 2}^2
+            -1, -1, -1, -1, -1, 0, 1, -1, -1, 2, 3, -1, -1, -1, -1, -1,
+            // dz = 0: the 2 x 2 centre and its x / y face neighbours
+            -1, 4, 5, -1, 6, 7, 8, 9, 10, 11, 12, 13, -1, 14, 15, -1,
+            // dz = 1
+            -1, 16, 17, -1, 18, 19, 20, 21, 22, 23, 24, 25, -1, 26, 27, -1,
+            // dz = 2
+            -1, -1, -1, -1, -1, 28, 29, -1, -1, 30, 31, -1, -1, -1, -1, -1};
+        std::vector<double> wt(dict.size() * 32, 0.0);
+        bool fits = true;
+        for (size_t c = 0; c < dict.size() && fits; c++)
+            for (const auto &e : dict[c]) {
+                if (e.first >= 64 || pat[e.first] < 0) {
+                    fits = false;
+                    break;
+                }
+                wt[c * 32 + pat[e.first]] = e.second;
+            }
+        if (fits) {
+            m.gtc_wt.resize(wt.size());
+            FAMG_CHECK_HIP(hipMemcpyAsync(m.gtc_wt.get(), wt.data(), wt.size() * 8, hipMemcpyHostToDevice, s));
+        }
     }
     FAMG_CHECK_HIP(hipStreamSynchronize(s));
     m.gtc_nclass = (int)dict.size();
