@@ -762,6 +762,217 @@ __global__ __launch_bounds__(256, 3) void k_fine_rr(FineRr2Args a) {
     }
 }
 
+// k_fine_pj: the same launch as k_fine_interp_jacobi (v = d f + P v_c, then
+// z = v + d (f - A v)) on 16-B units -- two x-adjacent fine points, x even, in
+// one box, so one coarse window anchor -- the way k_fine_rr cut its plane work:
+//   per lane three units of the 68 x 18 v window (x from x0 - 2, y from y0 - 1):
+//     f and the two class bytes of a unit in one load each (16 B, 2 B);
+//   v of planes z - 1, z, z + 1 stay in the lane's registers (the Jacobi sum's
+//     z neighbours and centre), only plane z in LDS for the in-plane neighbours
+//     (two slots);
+//   P's dictionary decoded per class: its KE = 4 fp64 weights (two 16-B LDS
+//     reads) and, per coarse-ring phase, its four coarse-window offsets (one
+//     8-B read) -- the fma chain over the KE entries in dictionary order, padding
+//     +0.0 terms included, is k_gtc_interp's ADD0 sum;
+//   the output tile's 512 units as 16-B stores.
+// Bitwise k_fine_interp_jacobi (test_fine_fused_bitwise).  Even nx.
+constexpr int J2_NT = 1024;                                 // threads per workgroup
+constexpr int J2_TX = 256, J2_TY = 16;                      // fine tile (x, y): whole grid rows at 256^3
+constexpr int J2_UX = J2_TX / 2 + 2, J2_UY = J2_TY + 2;     // v window: 130 units x 18 rows
+constexpr int J2_NU = J2_UX * J2_UY, J2_PU = (J2_NU + J2_NT - 1) / J2_NT;  // 2340 units, 3 per lane
+constexpr int J2_CX = J2_TX / 2 + 4, J2_CY = J2_TY / 2 + 4, J2_CPL = J2_CX * J2_CY;  // coarse window 132 x 12
+constexpr int J2_CPF = (J2_CPL + J2_NT - 1) / J2_NT;        // coarse points per lane (2)
+constexpr int J2_CMAX = 128;                                // classes
+
+struct FinePj2Args {
+    const uint8_t *cls;    // P's class id per fine row
+    const uint16_t *dict;  // nclass x 4 entries: value index << 8 | slot
+    const double *vtab;
+    int nclass;
+    int nx, ny, nz, cx, cy, cz;
+    int ntx, nty, jper;
+    const double *vc;  // coarse correction v_c
+    const double *f;   // fine rhs
+    double *out;       // z
+    double dk;
+    double cst[7];
+    int dbg;  // timing experiments only (FAMG_FINE_DBG): 1 no stores, 2 no P sums, 4 no Jacobi sums
+};
+
+struct Pj2Set {
+    dbl2_t F[J2_PU], V[J2_PU];
+    int C[J2_PU];  // the unit's two class bytes (x even: low byte)
+};
+
+__global__ __launch_bounds__(J2_NT) void k_fine_pj(FinePj2Args a) {
+    __shared__ __attribute__((aligned(16))) double vr[2 * 2 * J2_NU];  // v of planes z, z + 1
+    __shared__ double cring[4 * J2_CPL];
+    __shared__ __attribute__((aligned(16))) double pw[J2_CMAX * 4];    // per class its 4 weights
+    __shared__ __attribute__((aligned(8))) int16_t po[4 * J2_CMAX * 4];  // per ring phase and class: 4 offsets
+    const int tid = threadIdx.x;
+    const int t = xcd_remap(blockIdx.x, gridDim.x);
+    const int ntxy = a.ntx * a.nty;
+    const int chunk = t / ntxy, txy = t - chunk * ntxy;
+    const int x0 = (txy % a.ntx) * J2_TX, y0 = (txy / a.ntx) * J2_TY;
+    const int zb = chunk * a.jper, ze = min(zb + a.jper, a.nz);
+    const int cwx0 = (x0 >> 1) - 2, cwy0 = (y0 >> 1) - 2;
+    const int64_t fpl = (int64_t)a.nx * a.ny;
+    for (int b = tid; b < 4 * a.nclass; b += J2_NT) {
+        const uint32_t e = a.dict[b], sl = e & 255u;
+        pw[b] = a.vtab[e >> 8];
+        const int dzs = (int)(sl / 9u) - 1, dys = (int)((sl / 3u) % 3u) - 1, dxs = (int)(sl % 3u) - 1;
+#pragma unroll
+        for (int r = 0; r < 4; r++) po[r * 4 * a.nclass + b] = (int16_t)(((r + dzs) & 3) * J2_CPL + dys * J2_CX + dxs);
+    }
+    // the lane's units: plane offset (32-bit, an in-grid unit for units outside),
+    // coarse anchor, whether in the grid / in the output tile
+    int off[J2_PU], cb[J2_PU];
+    bool inq[J2_PU], jac[J2_PU];
+#pragma unroll
+    for (int u = 0; u < J2_PU; u++) {
+        const int q = tid + J2_NT * u, ux = q % J2_UX, uy = q / J2_UX;
+        const int x = x0 - 2 + 2 * ux, y = y0 - 1 + uy;
+        inq[u] = q < J2_NU && (unsigned)x < (unsigned)a.nx && (unsigned)y < (unsigned)a.ny;
+        jac[u] = inq[u] && ux >= 1 && ux <= J2_TX / 2 && uy >= 1 && uy <= J2_TY;
+        off[u] = inq[u] ? y * a.nx + x : 0;
+        cb[u] = inq[u] ? ((y >> 1) - cwy0) * J2_CX + (x >> 1) - cwx0 : J2_CX + 1;
+    }
+    auto fetch = [&](int z, Pj2Set &S) {
+        const int zc = min(max(z, 0), a.nz - 1);
+        const double *fz = a.f + (int64_t)zc * fpl;
+        const uint8_t *cz = a.cls + (int64_t)zc * fpl;
+#pragma unroll
+        for (int u = 0; u < J2_PU; u++) {
+            S.F[u] = *reinterpret_cast<const dbl2_t *>(fz + off[u]);
+            S.C[u] = (int)*reinterpret_cast<const uint16_t *>(cz + off[u]);
+        }
+    };
+    auto cfetch = [&](int Z, double (&v)[J2_CPF]) {
+        const int64_t cpl = (int64_t)a.cx * a.cy;
+#pragma unroll
+        for (int u = 0; u < J2_CPF; u++) {
+            const int p = tid + J2_NT * u;
+            const int X = cwx0 + p % J2_CX, Y = cwy0 + p / J2_CX;
+            const bool in = p < J2_CPL && (unsigned)X < (unsigned)a.cx && (unsigned)Y < (unsigned)a.cy &&
+                            (unsigned)Z < (unsigned)a.cz;
+            v[u] = a.vc[in ? (int64_t)Z * cpl + (int64_t)Y * a.cx + X : 0];
+        }
+    };
+    auto cstore = [&](int Z, const double (&v)[J2_CPF]) {
+#pragma unroll
+        for (int u = 0; u < J2_CPF; u++) {
+            const int p = tid + J2_NT * u;
+            const int X = cwx0 + p % J2_CX, Y = cwy0 + p / J2_CX;
+            const bool in = (unsigned)X < (unsigned)a.cx && (unsigned)Y < (unsigned)a.cy && (unsigned)Z < (unsigned)a.cz;
+            if (p < J2_CPL) cring[(Z & 3) * J2_CPL + p] = in ? v[u] : 0.0;
+        }
+    };
+    // v = d f + P v_c of plane z at the lane's units (0.0 outside the grid)
+    auto interp = [&](int z, Pj2Set &S) {
+        const bool zin = (unsigned)z < (unsigned)a.nz;
+        const int16_t *pz = po + ((z >> 1) & 3) * 4 * a.nclass;
+#pragma unroll
+        for (int u = 0; u < J2_PU; u++) {
+            double vv[2];
+#pragma unroll
+            for (int h = 0; h < 2; h++) {
+                const int c = (S.C[u] >> (8 * h)) & 255;
+                const dbl2_t w01 = *reinterpret_cast<const dbl2_t *>(pw + 4 * c);
+                const dbl2_t w23 = *reinterpret_cast<const dbl2_t *>(pw + 4 * c + 2);
+                const uint2 oo = *reinterpret_cast<const uint2 *>(pz + 4 * c);
+                const int o0 = (int)(int16_t)(oo.x & 0xffffu), o1 = (int)(int16_t)(oo.x >> 16);
+                const int o2 = (int)(int16_t)(oo.y & 0xffffu), o3 = (int)(int16_t)(oo.y >> 16);
+                double acc = 0.0;
+                if (!(a.dbg & 2)) {
+                    acc = fma(w01.x, cring[cb[u] + o0], acc);
+                    acc = fma(w01.y, cring[cb[u] + o1], acc);
+                    acc = fma(w23.x, cring[cb[u] + o2], acc);
+                    acc = fma(w23.y, cring[cb[u] + o3], acc);
+                }
+                const double fv = h ? S.F[u].y : S.F[u].x;
+                vv[h] = (zin && inq[u]) ? a.dk * fv + acc : 0.0;  // d*b (vec_mul's product) + P v_c
+            }
+            S.V[u] = dbl2_t{vv[0], vv[1]};
+        }
+    };
+    auto publish = [&](int z, const Pj2Set &S) {
+        double *g = vr + (z & 1) * 2 * J2_NU;
+#pragma unroll
+        for (int u = 0; u < J2_PU; u++) {
+            const int q = tid + J2_NT * u;
+            if (q < J2_NU) *reinterpret_cast<dbl2_t *>(g + 2 * q) = S.V[u];
+        }
+    };
+    // coarse planes zb/2 - 2 .. zb/2 + 1 (those of v(zb - 1) .. v(zb + 1); zb is even)
+    const int Zb = zb >> 1;
+    {
+        double cv[J2_CPF];
+        for (int Z = Zb - 2; Z <= Zb + 1; Z++) {
+            cfetch(Z, cv);
+            cstore(Z, cv);
+        }
+    }
+    Pj2Set S0, S1, S2, S3;  // plane zb + k in set k mod 4
+    fetch(zb - 1, S3);
+    fetch(zb, S0);
+    fetch(zb + 1, S1);
+    __syncthreads();
+    interp(zb - 1, S3);
+    interp(zb, S0);
+    publish(zb, S0);
+    int cmax = Zb + 2;
+    double cp[J2_CPF];
+    cfetch(cmax, cp);
+    fetch(zb + 2, S2);
+    __syncthreads();
+
+    // step z: Sm = z - 1 (its V), Sz = z, S1 = z + 1 (f arrived: its v now), S3 = z + 3 (issued; the set of z - 1)
+    auto step = [&](int z, Pj2Set &Sm, Pj2Set &Sz, Pj2Set &S1, Pj2Set &S3) {
+        interp(z + 1, S1);
+        publish(z + 1, S1);  // the slot of z - 1: its in-plane reads ended before the last barrier
+        // z(z) = v + d (f - A v): spmv_dia_kernel's constant 7-point JACOBI sum
+        const double *v0 = vr + (z & 1) * 2 * J2_NU;
+        const bool zon = z < ze;
+        double *oz = a.out + (int64_t)min(z, a.nz - 1) * fpl;
+#pragma unroll
+        for (int u = 0; u < J2_PU; u++) {
+            if (!jac[u] || !zon || (a.dbg & 1)) continue;
+            const int q = tid + J2_NT * u;
+            if (a.dbg & 4) {
+                *reinterpret_cast<dbl2_t *>(oz + off[u]) = Sz.V[u];
+                continue;
+            }
+            const dbl2_t ym = *reinterpret_cast<const dbl2_t *>(v0 + 2 * (q - J2_UX));
+            const dbl2_t yp = *reinterpret_cast<const dbl2_t *>(v0 + 2 * (q + J2_UX));
+            const double xl = v0[2 * q - 1], xr = v0[2 * q + 2];
+            const dbl2_t vm = Sm.V[u], vc = Sz.V[u], vp = S1.V[u];
+            const double y0[7] = {vm.x, ym.x, xl, vc.x, vc.y, yp.x, vp.x};
+            const double y1[7] = {vm.y, ym.y, vc.x, vc.y, xr, yp.y, vp.y};
+            double acc0 = 0.0, acc1 = 0.0;
+#pragma unroll
+            for (int k = 0; k < 7; k++) {
+                acc0 = fma(a.cst[k], y0[k], acc0);
+                acc1 = fma(a.cst[k], y1[k], acc1);
+            }
+            const dbl2_t fz = Sz.F[u];
+            // streamed out (nontemporal: z is read by the next solve step, not by this cycle)
+            __builtin_nontemporal_store(dbl2_t{vc.x + a.dk * (fz.x - acc0), vc.y + a.dk * (fz.y - acc1)},
+                                        reinterpret_cast<dbl2_t *>(oz + off[u]));
+        }
+        cstore(cmax, cp);  // the coarse plane v(z + 2) adds (slot of cmax - 4: unread)
+        cmax = ((z + 3) >> 1) + 1;
+        cfetch(cmax, cp);
+        fetch(min(z + 3, ze), S3);
+        lds_barrier();
+    };
+    for (int z = zb; z < ze; z += 4) {
+        step(z, S3, S0, S1, S3);
+        step(z + 1, S0, S1, S2, S0);
+        step(z + 2, S1, S2, S3, S1);
+        step(z + 3, S2, S3, S0, S2);
+    }
+}
+
 // ------------------------------------------------------------ host side
 
 // workgroups of k_fine_interp_jacobi per CU (cached)
@@ -940,11 +1151,72 @@ bool fine_interp_jacobi_ok(const GpuCsr &A, const GpuCsr &P, const SpmvEpi &epi)
         return false;
     for (int q = 0; q < 3; q++)
         if (P.gtc_fg[q] != A.dia_cst_n[q] || P.gtc_cg[q] != (P.gtc_fg[q] + 1) / 2) return false;
+    if (P.gtc_fg[0] % 2 != 0) return false;  // even nx (16-B units of two points in one box)
     return A.nrows == P.nrows && P.ncols == P.gtc_cg[0] * P.gtc_cg[1] * P.gtc_cg[2];
+}
+
+// workgroups of k_fine_pj per CU (cached)
+static int fine_pj2_occupancy() {
+    static std::once_flag once;
+    static int n = 1;
+    std::call_once(once, [] {
+        int v = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&v, k_fine_pj, J2_NT, 0) == hipSuccess && v >= 1)
+            n = v;
+        else
+            (void)hipGetLastError();
+    });
+    return n;
+}
+
+// FAMG_FINE_PJ=1: the round-5 interp+Jacobi kernel (A/B timing)
+static bool fine_pj_v1() {
+    static const bool on = [] {
+        const char *e = getenv("FAMG_FINE_PJ");
+        return e && e[0] == '1';
+    }();
+    return on;
+}
+
+static void fine_pj2(const GpuCsr &A, const GpuCsr &P, const double *vc, const double *f, double dk, double *out,
+                     hipStream_t s) {
+    FinePj2Args a{};
+    a.cls = P.gtc_cls.get();
+    a.dict = P.gtc_dict.get();
+    a.vtab = P.gtc_vtab.get();
+    a.nclass = P.gtc_nclass;
+    a.nx = (int)P.gtc_fg[0]; a.ny = (int)P.gtc_fg[1]; a.nz = (int)P.gtc_fg[2];
+    a.cx = (int)P.gtc_cg[0]; a.cy = (int)P.gtc_cg[1]; a.cz = (int)P.gtc_cg[2];
+    a.ntx = (int)ceil_div(a.nx, J2_TX);
+    a.nty = (int)ceil_div(a.ny, J2_TY);
+    a.vc = vc;
+    a.f = f;
+    a.out = out;
+    a.dk = dk;
+    for (int k = 0; k < 7; k++) a.cst[k] = A.dia_cst_v[k];
+    {
+        const char *e = getenv("FAMG_FINE_DBG");  // timing experiments only (results wrong)
+        a.dbg = e ? atoi(e) : 0;
+    }
+    const int64_t ntxy = (int64_t)a.ntx * a.nty;
+    const int64_t want = (int64_t)fine_pj2_occupancy() * std::max(A.ctx ? A.ctx->num_cus : 256, 1);
+    int jper = (int)std::max<int64_t>(2, ceil_div((int64_t)a.nz * ntxy, want));
+    if (flag(FLAG_FINE_FUSE) > 1) jper = (int)flag(FLAG_FINE_FUSE);
+    a.jper = jper + (jper & 1);
+    const dim3 grid((unsigned)(ntxy * ceil_div(a.nz, a.jper)));
+    k_fine_pj<<<grid, dim3(J2_NT), 0, s>>>(a);
+    FAMG_CHECK_HIP(hipGetLastError());
 }
 
 void fine_interp_jacobi(const GpuCsr &A, const GpuCsr &P, const double *vc, const double *f, double dk, double *out,
                         hipStream_t s) {
+    if (!fine_pj_v1() && P.gtc_ke == 4 && P.gtc_nclass <= J2_CMAX && P.gtc_fg[0] * P.gtc_fg[1] < (int64_t(1) << 31)) {
+        fine_pj2(A, P, vc, f, dk, out, s);
+        const int64_t n = A.nrows;
+        log_launch("fine-pj", SPMV_KERNEL_DIA, -1, n, 8 * n + 8 * P.ncols + 8 * n + n,
+                   (12 * P.nnz + 4 * (n + 1) + 8 * P.ncols + 16 * n) + (12 * A.nnz + 4 * (n + 1) + 32 * n));
+        return;
+    }
     FinePjArgs a{};
     a.cls = P.gtc_cls.get();
     a.dict = P.gtc_dict.get();
