@@ -126,12 +126,13 @@ __global__ __launch_bounds__(256) void spmv_scs_kernel(ScsArgs a) {
 }
 
 // Few long rows (A_3 of the 256^3 cycle: 32768 rows of 638 entries, 15625
-// classes): one row per wave, lane q takes offsets q, q + 64, ... (the class's
-// dictionary row and the x operands both coalesced), then a fixed butterfly --
-// the pattern SELL's lanes-per-row order (deterministic; rounding-level
-// differences from the oracle's sequential order, covered by the V-cycle
-// tolerance).  Interior rows share their class, so the dictionary streams about
-// half of the fp64 values the pattern SELL reads.
+// classes -- nearly every row its own): one row per wave, lane q takes the
+// offset pairs 2q, 2q + 1 of every 128-offset block (16-B dictionary and 8-B
+// offset loads, both coalesced), then a fixed butterfly -- deterministic;
+// rounding-level differences from the oracle's sequential order, covered by
+// the V-cycle tolerance.  Two dependent round trips per row: the class id and
+// ALL the row's offsets first (the offsets do not depend on the class), then
+// the dictionary row and every x operand at once.
 template <int MODE, int IB>
 __global__ __launch_bounds__(256) void spmv_scs_lanes_kernel(ScsArgs a) {
     const int blk = xcd_remap(blockIdx.x, gridDim.x);
@@ -139,8 +140,16 @@ __global__ __launch_bounds__(256) void spmv_scs_lanes_kernel(ScsArgs a) {
     if (row >= a.row_end) return;
     const int lane = threadIdx.x & 63;
     const int c = IB == 1 ? (int)static_cast<const uint8_t *>(a.cls)[row] : (int)static_cast<const uint16_t *>(a.cls)[row];
+    constexpr int NB = SCS_KMAX / 128;  // 128-offset blocks (K <= 1024, a multiple of 8)
+    const int nb = (a.k + 127) >> 7;
+    int2 of[NB];
+#pragma unroll
+    for (int j = 0; j < NB; j++) {
+        const int kk = 128 * j + 2 * lane;
+        of[j] = (j < nb && kk < a.k) ? *reinterpret_cast<const int2 *>(a.offs + kk) : int2{0, 0};
+    }
     double br = 0.0, xr = 0.0, dr = 0.0, yr = 0.0;
-    if (lane == 0) {  // epilogue operands first
+    if (lane == 0) {  // epilogue operands
         if constexpr (MODE == SPMV_RESID) br = a.b[row];
         if constexpr (MODE == SPMV_ADD) yr = a.y[row];
         if constexpr (MODE == SPMV_JACOBI) {
@@ -149,31 +158,28 @@ __global__ __launch_bounds__(256) void spmv_scs_lanes_kernel(ScsArgs a) {
             dr = a.dc ? a.dt[a.dc[row]] : a.d[row];
         }
     }
-    const double *dct = a.dict + (int64_t)c * a.k;
-    double acc = 0.0;
-    int k0 = 0;
-    for (; k0 + 8 * 64 <= a.k; k0 += 8 * 64) {
-        double v[8], xv[8];
+    double x0[NB], x1[NB];
 #pragma unroll
-        for (int u = 0; u < 8; u++) {
-            const int k = k0 + 64 * u + lane;
-            v[u] = dct[k];
-            xv[u] = a.x[min(max(row + a.offs[k], 0), a.ncols - 1)];
+    for (int j = 0; j < NB; j++) {
+        if (j < nb) {
+            x0[j] = a.x[min(max(row + of[j].x, 0), a.ncols - 1)];
+            x1[j] = a.x[min(max(row + of[j].y, 0), a.ncols - 1)];
         }
-#pragma unroll
-        for (int u = 0; u < 8; u++) acc = fma(v[u], xv[u], acc);
     }
-    {  // the last < 512 offsets (K is a multiple of 8): clamped loads, +0.0 terms past K
-        double v[8], xv[8];
+    const double *dct = a.dict + (int64_t)c * a.k;
+    scs_dbl2a_t v[NB];
 #pragma unroll
-        for (int u = 0; u < 8; u++) {
-            const int k = k0 + 64 * u + lane;
-            const int kc = min(k, a.k - 1);
-            v[u] = k < a.k ? dct[kc] : 0.0;
-            xv[u] = a.x[min(max(row + a.offs[kc], 0), a.ncols - 1)];
+    for (int j = 0; j < NB; j++) {
+        const int kk = 128 * j + 2 * lane;
+        if (j < nb) v[j] = kk < a.k ? *reinterpret_cast<const scs_dbl2a_t *>(dct + kk) : scs_dbl2a_t{0.0, 0.0};
+    }
+    double acc = 0.0;
+#pragma unroll
+    for (int j = 0; j < NB; j++) {
+        if (j < nb) {
+            acc = fma(v[j].x, x0[j], acc);
+            acc = fma(v[j].y, x1[j], acc);
         }
-#pragma unroll
-        for (int u = 0; u < 8; u++) acc = fma(v[u], xv[u], acc);
     }
 #pragma unroll
     for (int m = 32; m > 0; m >>= 1) acc += __shfl_xor(acc, m);
@@ -371,6 +377,14 @@ static bool scs_lanes_enabled() {
     static const bool on = [] {
         const char *e = getenv("FAMG_SCS_LANES");
         return !(e && e[0] == '0');
+    }();
+    return on;
+}
+
+static bool scs_rows_pref() {
+    static const bool on = [] {
+        const char *e = getenv("FAMG_SCS_ROWS");
+        return e && e[0] == '1';
     }();
     return on;
 }
@@ -768,7 +782,10 @@ bool build_scs(GpuCsr &m, const std::vector<int64_t> &rp, int64_t other_bytes) {
     const int64_t dict_bytes = (int64_t)Kp * C * 8;
     const int64_t stream = ib * (r1 - r0) + dict_bytes + 4 * Kp;
     // x staged per grid tile when the offsets are grid steps within the grid
-    const bool xs3 = on_grid && dict_bytes <= (int64_t(256) << 20) &&
+    // FAMG_SCS_ROWS=1: few long rows take the lanes-per-row kernel even where the
+    // x-staged one applies (A/B)
+    const bool rows_pref = scs_rows_pref() && r1 - r0 < SCS_LANES_ROWS && Kp >= 256 && !framed;
+    const bool xs3 = !rows_pref && on_grid && dict_bytes <= (int64_t(256) << 20) &&
                      (framed || (double)stream <= 0.5 * (double)other_bytes) && xscs_setup(m, offs, Kp, rp, col, val);
     if (!xs3 && (K < SCS_KMIN || small_table || framed)) return false;
     // few long rows: one row per wave, the dictionary streamed (up to 256 MiB)

@@ -32,6 +32,8 @@ for s in "$@"; do
         pmcfused) step r6_pmcfused 600 bash scripts/pmc_fused.sh ;;
         timefused) step r6_timefused 300 python scripts/time_fused.py 0 1 2 3 ;;
         timefused0) step r6_timefused 300 python scripts/time_fused.py 0 ;;
+        pmcsq) step r6_pmcsq 400 bash scripts/pmc_cycle_sq.sh ;;
+        abrows) step r6_abrows 400 bash scripts/r06_ab_rows.sh ;;
         smoke) step r6_smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     esac
 done
