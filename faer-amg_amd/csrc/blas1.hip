@@ -185,10 +185,70 @@ __global__ __launch_bounds__(256) void k_gemv(const double *M, const double *x, 
     if (lane == 0) out[row] = acc;
 }
 
+// The same for even n: 16-B loads of M and x, eight of them in flight per lane
+// before the first fma (the dense tail's 4096 x 4096 M streams 134 MB per cycle)
+typedef double gemv_dbl2_t __attribute__((ext_vector_type(2)));
+__global__ __launch_bounds__(256) void k_gemv2(const double *M, const double *x, double *out, int64_t n) {
+    const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    if (row >= n) return;
+    const double *mr = M + row * n;
+    double a0 = 0.0, a1 = 0.0;
+    constexpr int U = 8;
+    for (int64_t j0 = 2 * lane; j0 < n; j0 += 128 * U) {
+        gemv_dbl2_t m[U], xx[U];
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            const int64_t j = min(j0 + 128 * u, n - 2);
+            m[u] = __builtin_nontemporal_load(reinterpret_cast<const gemv_dbl2_t *>(mr + j));
+            xx[u] = *reinterpret_cast<const gemv_dbl2_t *>(x + j);
+        }
+#pragma unroll
+        for (int u = 0; u < U; u++)
+            if (j0 + 128 * u < n) {
+                a0 = fma(m[u].x, xx[u].x, a0);
+                a1 = fma(m[u].y, xx[u].y, a1);
+            }
+    }
+    double acc = a0 + a1;
+    for (int off = 32; off > 0; off >>= 1) acc += __shfl_xor(acc, off);
+    if (lane == 0) out[row] = acc;
+}
+
 void dense_gemv(const double *M, const double *x, double *out, int64_t n, hipStream_t s) {
     if (n <= 0) return;
     log_launch("gemv", -1, -1, n, 8 * n * n + 16 * n);
-    hipLaunchKernelGGL(k_gemv, dim3((unsigned)ceil_div(n, 4)), dim3(256), 0, s, M, x, out, n);
+    if (n % 2 == 0 && n >= 2) hipLaunchKernelGGL(k_gemv2, dim3((unsigned)ceil_div(n, 4)), dim3(256), 0, s, M, x, out, n);
+    else hipLaunchKernelGGL(k_gemv, dim3((unsigned)ceil_div(n, 4)), dim3(256), 0, s, M, x, out, n);
+    FAMG_CHECK_HIP(hipGetLastError());
+}
+
+__global__ __launch_bounds__(256) void k_transpose(const double *in, double *out, int64_t n) {
+    __shared__ double t[32][33];
+    const int64_t bx = (int64_t)blockIdx.x * 32, by = (int64_t)blockIdx.y * 32;
+    const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;  // 32 x 8
+    for (int k = ty; k < 32; k += 8)
+        if (by + k < n && bx + tx < n) t[k][tx] = in[(by + k) * n + bx + tx];
+    __syncthreads();
+    for (int k = ty; k < 32; k += 8)
+        if (bx + k < n && by + tx < n) out[(bx + k) * n + by + tx] = t[tx][k];
+}
+
+void dense_transpose(const double *in, double *out, int64_t n, hipStream_t s) {
+    if (n <= 0) return;
+    const dim3 grid((unsigned)ceil_div(n, 32), (unsigned)ceil_div(n, 32));
+    hipLaunchKernelGGL(k_transpose, grid, dim3(256), 0, s, in, out, n);
+    FAMG_CHECK_HIP(hipGetLastError());
+}
+
+__global__ void k_unit(double *v, int64_t n, int64_t j) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) v[i] = i == j ? 1.0 : 0.0;
+}
+
+void unit_vector(double *v, int64_t n, int64_t j, hipStream_t s) {
+    if (n <= 0) return;
+    hipLaunchKernelGGL(k_unit, dim3((unsigned)ceil_div(n, 256)), dim3(256), 0, s, v, n, j);
     FAMG_CHECK_HIP(hipGetLastError());
 }
 

@@ -112,7 +112,8 @@ static std::atomic<int64_t> g_flag_val[FLAG_COUNT] = {
     {[] { const char *e = getenv("FAMG_BSR_KERNEL"); return (int64_t)(e ? atoi(e) : 0); }()},
     {[] { const char *e = getenv("FAMG_BSR_LONG"); return (int64_t)(e ? atoll(e) : 48); }()},
     {[] { const char *e = getenv("FAMG_DIA7_RP"); return (int64_t)(e ? atoi(e) : 0); }()},
-    {[] { const char *e = getenv("FAMG_FINE_FUSE"); return (int64_t)(e ? atoi(e) : 1); }()}};
+    {[] { const char *e = getenv("FAMG_FINE_FUSE"); return (int64_t)(e ? atoi(e) : 1); }()},
+    {[] { const char *e = getenv("FAMG_DENSE_TAIL"); return (int64_t)(e ? atoll(e) : 4096); }()}};
 static std::atomic<uint64_t> g_flag_gen{0};
 int64_t flag(FlagId f) { return g_flag_val[f].load(std::memory_order_relaxed); }
 void set_flag(FlagId f, int64_t v) {

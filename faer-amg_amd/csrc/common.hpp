@@ -132,7 +132,7 @@ inline int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
 // the old value (a graph replays the launches it recorded).
 enum FlagId : int { FLAG_FOLD_XSCS = 0, FLAG_DIA_DK = 1, FLAG_VEC_WPR = 2, FLAG_GTX_TIME = 3, FLAG_SGS27_MARCH = 4, FLAG_XS_PIPE = 5,
               FLAG_BSR_KERNEL = 6, FLAG_BSR_LONG = 7,
-              FLAG_DIA7_RP = 8, FLAG_FINE_FUSE = 9, FLAG_COUNT = 10 };
+              FLAG_DIA7_RP = 8, FLAG_FINE_FUSE = 9, FLAG_DENSE_TAIL = 10, FLAG_COUNT = 11 };
 int64_t flag(FlagId f);
 void set_flag(FlagId f, int64_t v);
 uint64_t flags_generation();

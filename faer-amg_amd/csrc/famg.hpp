@@ -588,6 +588,15 @@ struct MultigridOp : LinOp {
     void undo_reorder();
     // the same multigrid over the caller's operators (no renumbering)
     std::shared_ptr<MultigridOp> original_view();
+    // the dense tail: with mu = 1 every level l >= tail_level is entered with v = 0,
+    // so the part of the cycle from tail_level down (smoothing, residual,
+    // restriction, the coarser levels, the coarsest solve, correction, post-
+    // smoothing) maps that level's f to its v linearly: v = M f.  M (n x n,
+    // row-major) is built once by running that part of the cycle on the n unit
+    // vectors; the cycle then takes one GEMV there instead of its launches.
+    // The first level 1 <= l < L - 1 with n_l <= flag dense_tail (0: off).
+    int64_t tail_level = -1;
+    void ensure_tail();
 
   private:
     struct GraphEntry {
@@ -600,7 +609,13 @@ struct MultigridOp : LinOp {
     bool workspace_ready_ = false;
     bool reorder_done_ = false;
     DevBuf<double> perm_f0_, perm_v0_;  // the fine level's rhs / result in its numbering
+    DevBuf<double> tail_M_;
+    uint64_t tail_key_ = ~uint64_t(0);
 };
+// out (n x n, row-major) = in^T
+void dense_transpose(const double *in, double *out, int64_t n, hipStream_t s);
+// v = e_j: zeros with a one at j
+void unit_vector(double *v, int64_t n, int64_t j, hipStream_t s);
 // y = x[p] / y[p] = x over n entries (reorder.hip; launch-plan records)
 void perm_gather(double *out, const double *in, const int32_t *p, int64_t n, hipStream_t s);
 void perm_scatter(double *out, const double *in, const int32_t *p, int64_t n, hipStream_t s);

@@ -418,6 +418,7 @@ MultigridOp::~MultigridOp() { invalidate_graphs(); }
 void MultigridOp::invalidate_graphs() {
     for (auto &g : graphs_) (void)hipGraphExecDestroy(g.exec);
     graphs_.clear();
+    tail_key_ = ~uint64_t(0);  // operators, options or switches changed: the dense tail is rebuilt
 }
 
 void MultigridOp::add_level(LinOpPtr A, LinOpPtr S, LinOpPtr R, LinOpPtr P) {
@@ -599,10 +600,48 @@ void MultigridOp::gather_fine(const double *rhs, hipStream_t s) {
     cycle(0, perm_v0_.get(), perm_f0_.get(), true, perm_v0_.get(), df);
 }
 
+void MultigridOp::ensure_tail() {
+    const int64_t lim = flag(FLAG_DENSE_TAIL);
+    const uint64_t key = ((uint64_t)mu << 48) ^ ((uint64_t)steps << 40) ^ ((uint64_t)levels.size() << 32) ^
+                         (uint64_t)std::max<int64_t>(lim, 0);
+    if (key == tail_key_) return;
+    tail_key_ = key;
+    tail_level = -1;
+    tail_M_.release();
+    if (lim <= 0 || mu != 1 || levels.size() < 3) return;
+    int64_t l0 = -1;
+    for (int64_t l = 1; l + 1 < (int64_t)levels.size(); l++)
+        if (levels[l].A->nrows <= lim) {
+            l0 = l;
+            break;
+        }
+    if (l0 < 0) return;
+    const int64_t n = levels[l0].A->nrows;
+    hipStream_t s = ctx->stream;
+    // column j of M = the tail's v for f = e_j (eager launches, before any capture)
+    DevBuf<double> Mt(n * n), e(n);
+    LaunchLog *saved = g_launch_log;
+    g_launch_log = nullptr;
+    for (int64_t j = 0; j < n; j++) {
+        unit_vector(e.get(), n, j, s);
+        cycle(l0, Mt.get() + j * n, e.get(), true, nullptr, false);
+    }
+    g_launch_log = saved;
+    tail_M_.resize(n * n);
+    dense_transpose(Mt.get(), tail_M_.get(), n, s);
+    FAMG_CHECK_HIP(hipStreamSynchronize(s));
+    tail_level = l0;
+}
+
 void MultigridOp::cycle(int64_t l, double *v, const double *f, bool v_zero, double *, bool pre_df) {
     MgLevel &L = levels[l];
     hipStream_t s = ctx->stream;
     const int64_t n = L.A->nrows;
+    if (l == tail_level && v_zero) {  // the dense tail: this level and every coarser one as v = M f
+        log_at(l, AMG_ROLE_COARSE);
+        dense_gemv(tail_M_.get(), f, v, n, s);
+        return;
+    }
     if (l == (int64_t)levels.size() - 1) {
         log_at(l, AMG_ROLE_COARSE);
         L.S->apply(v, f);  // smoother.apply(v, f) (:291)
@@ -635,7 +674,7 @@ void MultigridOp::cycle(int64_t l, double *v, const double *f, bool v_zero, doub
     bool df = false;
     auto *Rc = dynamic_cast<CsrOp *>(L.R.get());
     SpmvEpi epic;  // the SETDF epilogue: level l + 1's d, y2 = d_c f_c
-    if (l + 2 < (int64_t)levels.size() && restrict_df && setdf_enabled()) {
+    if (l + 2 < (int64_t)levels.size() && l + 1 != tail_level && restrict_df && setdf_enabled()) {
         auto *Ac = dynamic_cast<CsrOp *>(C.A.get());
         auto *Dc = dynamic_cast<DiagOp *>(C.S.get());
         auto *Pc = dynamic_cast<CsrOp *>(C.P.get());
@@ -762,6 +801,7 @@ void MultigridOp::apply(double *out, const double *rhs) {
         invalidate_graphs();
         flags_gen_ = flags_generation();
     }
+    ensure_tail();
     hipStream_t s = ctx->stream;
     auto run = [&]() {
         if (levels[0].permuted) {  // the fine level runs in its numbering: rhs in, result out
@@ -808,6 +848,7 @@ std::vector<LaunchRec> MultigridOp::cycle_plan() {
     std::lock_guard<std::mutex> lk(mtx);
     FAMG_REQUIRE(!levels.empty(), AMG_ERR_INVALID, "empty multigrid");
     ensure_workspace();
+    ensure_tail();
     const int64_t n = levels[0].A->nrows;
     DevBuf<double> b(std::max<int64_t>(1, n)), z(std::max<int64_t>(1, n));
     vec_fill(b.get(), 1.0, n, ctx->stream);

@@ -519,7 +519,7 @@ class SparseMatOp(LinOp):
 
 FLAGS = {"fold_xscs": 0, "dia_dk": 1, "vec_wpr": 2, "gtx_time": 3, "sgs27_march": 4, "xs_pipe": 5, "bsr_kernel": 6,
          "bsr_long": 7,
-         "dia7_rp": 8, "fine_fuse": 9}
+         "dia7_rp": 8, "fine_fuse": 9, "dense_tail": 10}
 
 
 def set_flag(name, value):

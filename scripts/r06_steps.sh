@@ -21,6 +21,8 @@ for s in "$@"; do
         fusetests) step r6_pytest_fuse 600 python -u -m pytest tests/test_gpu_parity.py -x -v --timeout 300 \
                    --timeout-method thread -k "fine_fused or cycle_plan_accounts or constant_diagonal or dia7_row or storage_mix or setdf or gtc or coarse_cholesky or spmm" ;;
         gputests) step r6_pytest_gpu 1000 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread ;;
+        gputestsall) step r6_pytest_gpu 1000 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread ;;
+        tailtests) step r6_pytest_tail 600 python -u -m pytest tests/test_gpu_parity.py -v --timeout 300 --timeout-method thread -k "dense_tail or cycle_plan or wide_grid or fold_zero" ;;
         profc2) step r6_profc2 400 bash scripts/prof_c2.sh r6_c2f ;;
         profc3) step r6_profc3 500 bash scripts/prof_c3.sh r6_c3f ;;
         profc5) step r6_profc5 500 bash scripts/prof_c5.sh r6_c5f ;;

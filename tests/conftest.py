@@ -32,3 +32,13 @@ def ctx():
 def dev():
     import torch
     return torch.device("cuda:0")
+
+
+@pytest.fixture
+def no_tail():
+    """The cycle without its dense tail (flag dense_tail = 0, ops.hip
+    ensure_tail): for tests about the launches of the coarse levels it replaces."""
+    import faer_amg_amd as fa
+    fa.set_flag("dense_tail", 0)
+    yield
+    fa.set_flag("dense_tail", 4096)

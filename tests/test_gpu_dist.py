@@ -18,6 +18,19 @@ def fa():
     return faer_amg_amd
 
 
+@pytest.fixture(autouse=True)
+def _no_dense_tail():
+    """The distributed cycle runs every level (no dense tail, ops.hip
+    ensure_tail): the single-GPU references these tests compare with bitwise
+    run without it too."""
+    import torch
+    if not torch.cuda.is_available():  # torch first, as the ctx fixture (conftest.py)
+        pytest.skip("no GPU")
+    fa().set_flag("dense_tail", 0)
+    yield
+    fa().set_flag("dense_tail", 4096)
+
+
 def run_ranks(nranks, fn):
     """Run fn(rank) in nranks threads; re-raise the first failure."""
     out, errs = [None] * nranks, []

@@ -1325,7 +1325,7 @@ def test_xstaged_stencil_classes(ctx):
     assert A1.spmv_info()["grid"] == (0, 0, 0) and not A1.spmv_info()["xstaged"]
 
 
-def test_xstaged_classes_fold_zero_guess(ctx):
+def test_xstaged_classes_fold_zero_guess(ctx, no_tail):
     """The zero-guess smoothing step folded on x-staged stencil-class levels
     (RESID0 stages d*f with the x window, ADD0 writes d*f + P v_c): the plan
     shows RESID0/ADD0 and no d*f pass on those levels, the V-cycle is bitwise
@@ -1399,7 +1399,7 @@ def test_grid_transfer_classes(ctx, gen, dims):
 
 
 @pytest.mark.parametrize("gen,dims", [("7pt", (64, 48, 40)), ("27pt", (40, 36, 33)), ("7pt", (45, 37, 29))])
-def test_wide_grid_transfer_classes(ctx, gen, dims):
+def test_wide_grid_transfer_classes(ctx, gen, dims, no_tail):
     """gtx.hip: R and P of the box levels the 8-bit classes cannot take (levels
     >= 1: thousands of classes, steps up to {-5,..,6}^3) as 16-bit classes over a
     global dictionary of (window offset, value) entries: y = P v_c, y += P v_c
@@ -1529,9 +1529,13 @@ def test_cycle_plan_accounts_for_every_launch(ctx):
     mg = fa().sa_build_box(A, dims, (2, 2, 2), coarsest_dim=100)
     plan = mg.cycle_plan()
     nl = mg.levels()
-    assert {p["level"] for p in plan} == set(range(nl))
+    # the last level in the plan is the coarsest or the dense tail (the first level
+    # l >= 1 of <= 4096 rows above it: one GEMV of 8 n_l^2 + 16 n_l bytes for l..L-1)
+    lt = max(p["level"] for p in plan)
+    assert lt == nl - 1 or (lt >= 1 and mg.level(lt)[0].nrows <= 4096 < mg.level(lt - 1)[0].nrows), lt
+    assert {p["level"] for p in plan} == set(range(lt + 1))
     coarse = [p for p in plan if p["role"] == "coarse"]
-    n_c = mg.level(nl - 1)[0].nrows
+    n_c = mg.level(lt)[0].nrows
     assert len(coarse) == 1 and coarse[0]["name"] == "gemv" and coarse[0]["bytes"] == 8 * n_c * n_c + 16 * n_c
     for p in plan:
         assert p["bytes"] > 0 and p["csr_bytes"] >= p["bytes"] or p["kernel"] in (-1, 4, 7)
@@ -1787,6 +1791,54 @@ def test_fine_fused_bitwise(ctx, dims):
         assert np.array_equal(outs[ff].view(np.int64), outs[0].view(np.int64)), ff
     zref = O.Multigrid(oracle_levels_from_gpu(mg, "jacobi")).apply(H(b))
     assert np.linalg.norm(outs[1] - zref) <= 1e-11 * np.linalg.norm(zref)
+
+
+@pytest.mark.parametrize("dims,smoother", [((64, 64, 64), "jacobi"), ((48, 40, 36), "sgs")])
+def test_dense_tail(ctx, dims, smoother):
+    """The dense tail (ops.hip ensure_tail): with mu = 1 the part of the V-cycle
+    from the first level of <= 4096 rows down maps that level's f to its v
+    linearly, so the cycle takes one GEMV with the matrix of that map (built by
+    running that part on the unit vectors) instead of its launches.  The cycle
+    agrees with the one that runs every level to rounding (1e-13) and with the
+    oracle (1e-11); the plan ends in one GEMV of 8 n^2 + 16 n bytes at that
+    level, whose restriction then writes no d f; mu = 2 and the flag at 0 run
+    every level."""
+    import torch
+    A = (fa().SparseMatOp.laplace3d_7pt(ctx, *dims) if smoother == "jacobi"
+         else fa().SparseMatOp.aniso27(ctx, *dims, 1.0, 1.0, 0.01))
+    mg = fa().sa_build_box(A, dims, (2, 2, 2), coarsest_dim=100, smoother=smoother)
+    nl = mg.levels()
+    ns = [mg.level(l)[0].nrows for l in range(nl)]
+    lt = next(l for l in range(1, nl - 1) if ns[l] <= 4096)
+    b = np.random.default_rng(61).uniform(-1, 1, A.nrows)
+    plan = mg.cycle_plan()
+    assert max(p["level"] for p in plan) == lt
+    tail = [p for p in plan if p["level"] == lt]
+    assert len(tail) == 1 and tail[0]["name"] == "gemv" and tail[0]["bytes"] == 8 * ns[lt] ** 2 + 16 * ns[lt]
+    assert all(p["mode"] != "SETDF" for p in plan if p["level"] == lt - 1)
+    z = apply_dev(ctx, mg, b, A.nrows)
+    fa().set_flag("dense_tail", 0)
+    try:
+        z0 = apply_dev(ctx, mg, b, A.nrows)
+        assert max(p["level"] for p in mg.cycle_plan()) == nl - 1
+    finally:
+        fa().set_flag("dense_tail", 4096)
+    assert np.linalg.norm(z - z0) <= 1e-13 * np.linalg.norm(z0)
+    zref = O.Multigrid(oracle_levels_from_gpu(mg, smoother)).apply(b)
+    assert np.linalg.norm(z - zref) <= 1e-11 * np.linalg.norm(zref)
+    # graph replay equals the eager cycle
+    mg.set_graph(True)
+    zg = torch.empty(A.nrows, dtype=torch.float64, device="cuda:0")
+    for _ in range(2):
+        mg.apply(zg, T(b))
+    ctx.synchronize()
+    assert np.array_equal(H(zg).view(np.int64), z.view(np.int64))
+    # a W-cycle enters the tail level twice, the second time from v != 0: no tail
+    mg.with_cycle_type(2)
+    try:
+        assert max(p["level"] for p in mg.cycle_plan()) == nl - 1
+    finally:
+        mg.with_cycle_type(1)
 
 
 def test_spmm_xsell_and_pattern_sell(ctx):
