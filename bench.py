@@ -420,9 +420,9 @@ def abi_ingest(fa, ctx, mg, b, z_ref, stream, args):
                     "(no grid hints: inferred), same timed cycle as the headline"}
 
 
-FUSED_NAMES = {0: ("fine-rr", "k_fine_resid_restrict",
+FUSED_NAMES = {0: ("fine-rr", "k_fine_rr",
                     "folded fine residual r = f - A (d f) + restriction f_c = R r, d_c f_c (r kept in LDS)"),
-               1: ("fine-pj", "k_fine_interp_jacobi",
+               1: ("fine-pj", "k_fine_pj",
                    "folded correction v = d f + P v_c + post-smoothing Jacobi step (v kept in LDS)")}
 
 

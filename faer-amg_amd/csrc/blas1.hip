@@ -120,7 +120,7 @@ void vec_nn_step(double *x, const double *d, const double *r, int64_t n, hipStre
 
 // ---------------------------------------------------------------- reductions
 
-constexpr int RED_GRID = 1024;
+constexpr int RED_GRID = VEC_DOT_PARTIALS;
 
 __device__ __forceinline__ double block_sum(double v, double *sh) {
     for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
@@ -152,13 +152,16 @@ __global__ __launch_bounds__(256) void k_dot_final(const double *partials, doubl
     if (threadIdx.x == 0) *res = t;
 }
 
+void vec_dot_dev(const double *x, const double *y, int64_t n, double *res, double *partials, hipStream_t s) {
+    log_launch("vec_dot", -1, -1, n, 16 * n);
+    hipLaunchKernelGGL(k_dot_partial, dim3(RED_GRID), dim3(256), 0, s, x, y, n, partials);
+    hipLaunchKernelGGL(k_dot_final, dim3(1), dim3(256), 0, s, partials, res);
+    FAMG_CHECK_HIP(hipGetLastError());
+}
+
 void vec_dot_dev(const double *x, const double *y, int64_t n, double *res, Ctx &ctx) {
     if (ctx.red_partials.size() < (size_t)RED_GRID) ctx.red_partials.resize(RED_GRID);
-    log_launch("vec_dot", -1, -1, n, 16 * n);
-    hipLaunchKernelGGL(k_dot_partial, dim3(RED_GRID), dim3(256), 0, ctx.stream, x, y, n,
-                       ctx.red_partials.get());
-    hipLaunchKernelGGL(k_dot_final, dim3(1), dim3(256), 0, ctx.stream, ctx.red_partials.get(), res);
-    FAMG_CHECK_HIP(hipGetLastError());
+    vec_dot_dev(x, y, n, res, ctx.red_partials.get(), ctx.stream);
 }
 
 double vec_dot(const double *x, const double *y, int64_t n, Ctx &ctx) {

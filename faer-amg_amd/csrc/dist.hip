@@ -1542,11 +1542,14 @@ static SolveOps dist_ops(const std::shared_ptr<DistMultigridOp> &d, bool precond
         dm->residual0(b, x, r);
     };
     if (precondition) o.M = [dm](double *out, const double *r) { dm->apply(out, r); };
-    auto red = std::make_shared<DevBuf<double>>(1);
+    // the result and its partial sums in a buffer of this solve's own: loopback ranks
+    // share one context, and the context's reduction scratch raced between them
+    // (the bench's 8-rank rehearsal: rho_0 = 1.0000122)
+    auto red = std::make_shared<DevBuf<double>>(1 + VEC_DOT_PARTIALS);
     o.dot = [dm, red](const double *u, const double *w) {
         Ctx &ctx = *dm->ctx;
         hipStream_t s = ctx.stream;
-        vec_dot_dev(u, w, dm->nrows, red->get(), ctx);
+        vec_dot_dev(u, w, dm->nrows, red->get(), red->get() + 1, s);
         dm->tr->allreduce(red->get(), 1, false, s);
         double h = 0;
         FAMG_CHECK_HIP(hipMemcpyAsync(&h, red->get(), 8, hipMemcpyDeviceToHost, s));

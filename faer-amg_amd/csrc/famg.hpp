@@ -401,6 +401,10 @@ void vec_scale(double *x, double alpha, int64_t n, hipStream_t s);              
 void vec_nn_step(double *x, const double *d, const double *r, int64_t n, hipStream_t s);
 // Deterministic dot product; result left on device in *res (fixed reduction tree).
 void vec_dot_dev(const double *x, const double *y, int64_t n, double *res, Ctx &ctx);
+// the same with the caller's partial sums (VEC_DOT_PARTIALS doubles): callers that share
+// a context across threads (loopback ranks) must not share the context's scratch
+constexpr int VEC_DOT_PARTIALS = 1024;
+void vec_dot_dev(const double *x, const double *y, int64_t n, double *res, double *partials, hipStream_t s);
 double vec_dot(const double *x, const double *y, int64_t n, Ctx &ctx);  // syncs
 
 // marker kernel for rocprofv3 traces (amg_trace_mark)

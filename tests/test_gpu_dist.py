@@ -750,3 +750,34 @@ def test_dist_c4_partition_512_eight_ranks():
     say(f"rho_k dist {hist['dist']} single {hist['single']}")
     assert np.all(np.abs(hist["dist"] - hist["single"]) <= 1e-8 * hist["single"])
     assert hist["dist"][-1] < 0.1 * hist["dist"][0]
+
+
+@pytest.mark.parametrize("dims,nranks", [((16, 12, 24), 2), ((64, 64, 64), 4)])
+def test_dist_stationary_history_shared_context(dims, nranks):
+    """Loopback ranks that share one context (as the bench's --loopback
+    rehearsal does): the distributed stationary solve's residual history equals
+    the single-GPU one (rho_0 exactly 1).  Its dot products once used the
+    context's reduction scratch, which the rank threads raced on (the 8-rank
+    rehearsal reported rho_0 = 1.0000122, profiles/r06)."""
+    import torch
+    ctx = fa().Context(0)
+    A = fa().SparseMatOp.laplace3d_7pt(ctx, *dims)
+    mg = fa().sa_build_box(A, dims, (2, 2, 2), coarsest_dim=1000)
+    b = torch.as_tensor(np.random.default_rng(7).uniform(-1, 1, A.nrows), device="cuda:0")
+    z = torch.empty_like(b)
+    mg.apply(z, b)
+    x = torch.zeros_like(b)
+    _, hs = fa().stationary_solve(A, mg, b, x, max_iter=5, rel_tol=1e-300)
+    splits = fa().slab_splits(fa().box_level_dims(dims, (2, 2, 2), mg.levels()), nranks)
+    hub = fa().LoopbackHub(nranks)
+
+    def body(r):
+        comm = fa().Comm(ctx, hub=hub, rank=r)
+        dm = fa().DistMultigrid(comm, mg, splits, agglomerate_rows=1000)
+        r0, r1 = dm.local_rows()
+        xl = torch.zeros_like(b[r0:r1])
+        return dm.stationary_solve(b[r0:r1], xl, max_iter=5, rel_tol=1e-300)[1]
+    hist = run_ranks(nranks, body)
+    for h in hist:
+        assert h[0] == 1.0
+        assert np.all(np.abs(h - hs) <= 1e-12 * hs), (h, hs)
