@@ -781,6 +781,28 @@ amg_status amg_multigrid_fine_launch(amg_linop *mg, int32_t which, double *out, 
     });
 }
 
+amg_status amg_multigrid_set_fine_timer(amg_linop *mg, int32_t which) {
+    return guard([&] {
+        auto m = need_mg(mg);
+        FAMG_REQUIRE(which >= -1 && which <= 1, AMG_ERR_INVALID, "bad argument");
+        std::lock_guard<std::mutex> lk(m->mtx);
+        m->ctx->set_device();
+        for (auto &e : m->fine_ev)
+            if (!e) FAMG_CHECK_HIP(hipEventCreate(&e));
+        m->fine_timer = which;
+        m->invalidate_graphs();
+    });
+}
+
+amg_status amg_multigrid_fine_timer_ms(amg_linop *mg, float *ms) {
+    return guard([&] {
+        auto m = need_mg(mg);
+        FAMG_REQUIRE(ms && m->fine_timer >= 0, AMG_ERR_INVALID, "no fine-level timer set");
+        FAMG_CHECK_HIP(hipEventSynchronize(m->fine_ev[1]));
+        FAMG_CHECK_HIP(hipEventElapsedTime(ms, m->fine_ev[0], m->fine_ev[1]));
+    });
+}
+
 amg_status amg_trace_mark(amg_ctx *ctx, int32_t tag) {
     return guard([&] {
         FAMG_REQUIRE(ctx, AMG_ERR_INVALID, "null context");

@@ -601,6 +601,9 @@ struct MultigridOp : LinOp {
     // The first level 1 <= l < L - 1 with n_l <= flag dense_tail (0: off).
     int64_t tail_level = -1;
     void ensure_tail();
+    // in-cycle timing of one fused fine-level launch (amg_multigrid_set_fine_timer)
+    int fine_timer = -1;
+    hipEvent_t fine_ev[2] = {nullptr, nullptr};
 
   private:
     struct GraphEntry {

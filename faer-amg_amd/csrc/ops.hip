@@ -413,7 +413,11 @@ void CoarseCholOp::apply(double *out, const double *rhs) {
 
 // --------------------------------------------------------------- multigrid
 
-MultigridOp::~MultigridOp() { invalidate_graphs(); }
+MultigridOp::~MultigridOp() {
+    invalidate_graphs();
+    for (auto &e : fine_ev)
+        if (e) (void)hipEventDestroy(e);
+}
 
 void MultigridOp::invalidate_graphs() {
     for (auto &g : graphs_) (void)hipGraphExecDestroy(g.exec);
@@ -700,7 +704,9 @@ void MultigridOp::cycle(int64_t l, double *v, const double *f, bool v_zero, doub
         // the folded residual and the restriction in one marching launch
         // (fine.hip): r stays in LDS, f_c and d_c f_c land where SETDF writes them
         log_at(l, AMG_ROLE_RESID);
+        if (fine_timer == 0) FAMG_CHECK_HIP(hipEventRecord(fine_ev[0], s));
         fine_resid_restrict(A->m, Rc->m, f, D->dconst, C.f.get(), epic, s);
+        if (fine_timer == 0) FAMG_CHECK_HIP(hipEventRecord(fine_ev[1], s));
     } else {
         if (fold) {
             log_at(l, AMG_ROLE_RESID);
@@ -733,7 +739,9 @@ void MultigridOp::cycle(int64_t l, double *v, const double *f, bool v_zero, doub
         if (steps == 1 && fine_interp_jacobi_ok(A->m, P->m, epi)) {
             // v = d f + P v_c and the post-smoothing step in one marching launch
             // (fine.hip): v stays in LDS, the result lands in v0
+            if (fine_timer == 1) FAMG_CHECK_HIP(hipEventRecord(fine_ev[0], s));
             fine_interp_jacobi(A->m, P->m, C.v.get(), f, D->dconst, v0, s);
+            if (fine_timer == 1) FAMG_CHECK_HIP(hipEventRecord(fine_ev[1], s));
             return;
         }
         spmv(P->m, C.v.get(), t, SPMV_ADD0, epi, s);  // v = d f + P v_c
@@ -812,7 +820,9 @@ void MultigridOp::apply(double *out, const double *rhs) {
             cycle(0, out, rhs, true, out);
         }
     };
-    if (!use_graph || s == nullptr) {
+    // (the in-cycle launch timer runs the cycle eagerly: events recorded by graph
+    // nodes cannot be read back with hipEventElapsedTime)
+    if (!use_graph || s == nullptr || fine_timer >= 0) {
         run();
         return;
     }

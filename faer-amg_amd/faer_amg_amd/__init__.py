@@ -184,6 +184,8 @@ SIGNATURES = {
     "amg_dist_pcg_solve": (i32, [vp, i32, vp, vp, i64, dbl, dbl, vp, P(i64)]),
     "amg_multigrid_cycle_plan": (i32, [vp, vp, i64, P(i64)]),
     "amg_multigrid_fine_launch": (i32, [vp, i32, vp, vp]),
+    "amg_multigrid_set_fine_timer": (i32, [vp, i32]),
+    "amg_multigrid_fine_timer_ms": (i32, [vp, vp]),
     "amg_dist_cycle_plan": (i32, [vp, vp, i64, P(i64)]),
     "amg_set_sgs_fused": (i32, [i32]),
     "amg_sgs_fused": (i32, [vp, P(i32)]),
@@ -665,6 +667,17 @@ class Multigrid(LinOp):
         return (SparseMatOp(a, self.ctx), LinOp(s, self.ctx),
                 SparseMatOp(r, self.ctx) if r.value else None,
                 SparseMatOp(p, self.ctx) if p.value else None)
+
+    def set_fine_timer(self, which):
+        """In-cycle timing of fused fine-level launch `which` (0 / 1; -1 off):
+        every cycle records HIP events around it (amg_multigrid_set_fine_timer)."""
+        _ck(_lib.amg_multigrid_set_fine_timer(self.h, int(which)))
+
+    def fine_timer_ms(self):
+        """Milliseconds of the timed launch in the last completed cycle."""
+        v = C.c_float()
+        _ck(_lib.amg_multigrid_fine_timer_ms(self.h, C.byref(v)))
+        return float(v.value)
 
     def fine_launch(self, which, out, rhs):
         """One fused fine-level launch as the cycle makes it (amg_multigrid_fine_launch):

@@ -371,6 +371,14 @@ amg_status amg_multigrid_cycle_plan(amg_linop *mg, amg_launch_rec *recs, int64_t
  * cycle does not take that launch.  For timing the cycle's dominant kernels
  * on their own (bench.py roofline). */
 amg_status amg_multigrid_fine_launch(amg_linop *mg, int32_t which, double *out, const double *rhs);
+/* In-cycle timing of one fused fine-level launch (no reference counterpart:
+ * measurement): which 0 / 1 as amg_multigrid_fine_launch, -1 off.  While on,
+ * every cycle records a pair of HIP events around that launch on the context
+ * stream (the cycle then runs its launches eagerly, not as its hipGraph: HIP
+ * cannot time events recorded by graph nodes); *ms = the time between the pair
+ * of the last completed cycle.  Setting it drops the captured graphs. */
+amg_status amg_multigrid_set_fine_timer(amg_linop *mg, int32_t which);
+amg_status amg_multigrid_fine_timer_ms(amg_linop *mg, float *ms);
 /* The same for a distributed multigrid: one eager cycle (halo exchanges
  * included: collective, every rank calls it) on this rank's scratch vectors;
  * level = global level index (the redundant tail's levels after the

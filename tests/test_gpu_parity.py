@@ -1793,6 +1793,32 @@ def test_fine_fused_bitwise(ctx, dims):
     assert np.linalg.norm(outs[1] - zref) <= 1e-11 * np.linalg.norm(zref)
 
 
+def test_fine_timer_in_cycle(ctx):
+    """amg_multigrid_set_fine_timer: HIP events around one fused fine-level launch
+    inside the cycle (run eagerly while timed) -- a positive time per cycle, and
+    the cycle's result bitwise the graph-replayed one."""
+    import torch
+    dims = (64, 64, 64)
+    A = fa().SparseMatOp.laplace3d_7pt(ctx, *dims)
+    mg = fa().sa_build_box(A, dims, (2, 2, 2), coarsest_dim=100)
+    mg.set_graph(True)
+    b = T(np.random.default_rng(5).uniform(-1, 1, A.nrows))
+    z0, z1 = torch.empty_like(b), torch.empty_like(b)
+    mg.apply(z0, b)
+    ctx.synchronize()
+    for which in (0, 1):
+        mg.set_fine_timer(which)
+        try:
+            for _ in range(3):
+                mg.apply(z1, b)
+                ms = mg.fine_timer_ms()
+                assert 0.0 < ms < 100.0, ms
+        finally:
+            mg.set_fine_timer(-1)
+        ctx.synchronize()
+        assert torch.equal(z0, z1)
+
+
 @pytest.mark.parametrize("dims,smoother", [((64, 64, 64), "jacobi"), ((48, 40, 36), "sgs")])
 def test_dense_tail(ctx, dims, smoother):
     """The dense tail (ops.hip ensure_tail): with mu = 1 the part of the V-cycle
