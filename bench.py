@@ -774,12 +774,28 @@ def run_single(args):
                    "locality_renumbered_levels": [l for l in range(mg.levels()) if mg.reordered(l)],
                    "abi_ingest": abi,
                    "secondary": secondary,
+                   "dense_tail": dense_tail_info(plan, levels),
                    "parallelism": "single GPU"},
         "fine_spmv_gbs": round(achieved, 1),
         "roofline": roofline,
         "cpu_baseline": cpu,
         "parity": parity,
     }
+
+
+def dense_tail_info(plan, levels):
+    """The dense tail as the cycle ran it (ops.hip ensure_tail): the level whose
+    launches down to the coarsest solve are one GEMV with the precomputed matrix
+    of that part of the cycle, or None (every level launched)."""
+    lt = max(p["level"] for p in plan)
+    if lt >= len(levels) - 1:
+        return None
+    n = levels[lt]["n"]
+    return {"level": lt, "rows": n, "matrix_bytes": 8 * n * n,
+            "what": (f"levels {lt}..{len(levels) - 1} entered with v = 0 (mu = 1): that part of the cycle maps "
+                     f"f_{lt} to v_{lt} linearly, so the cycle applies its {n} x {n} matrix (built once at the "
+                     f"first apply by running it on the unit vectors) with one GEMV instead of its launches; "
+                     f"the parity block compares against the oracle running every level")}
 
 
 def roofline_kernel_name(fa, info, args):
