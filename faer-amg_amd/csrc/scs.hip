@@ -260,8 +260,7 @@ __global__ __launch_bounds__(256) void spmv_xscs_kernel(XscsArgs a) {
         if (live[j]) {
             if constexpr (MODE == SPMV_RESID || MODE == SPMV_RESID0) br[j] = a.b[gi[j]];
             if constexpr (MODE == SPMV_ADD) yr[j] = a.y[gi[j]];
-            if constexpr (MODE == SPMV_JACOBI) {
-                xr[j] = a.x[gi[j]];
+            if constexpr (MODE == SPMV_JACOBI) {  // (x at the row itself: from the staged window below)
                 br[j] = a.b[gi[j]];
                 dr[j] = a.dc ? a.dt[a.dc[gi[j]]] : a.d[gi[j]];
             }
@@ -295,6 +294,10 @@ __global__ __launch_bounds__(256) void spmv_xscs_kernel(XscsArgs a) {
             if (p0 + 256 * u < W) win[si[u]] = v[u];
     }
     __syncthreads();
+    if constexpr (MODE == SPMV_JACOBI) {
+#pragma unroll
+        for (int j = 0; j < RL; j++) xr[j] = win[wb[j]];  // the staged x_i (the window holds x itself)
+    }
     bool uni = true;
     int cu[RL];
 #pragma unroll
