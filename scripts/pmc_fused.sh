@@ -4,6 +4,8 @@
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 R=$(pwd)
+# (the dense tail's one-time build under counter collection crashed rocprofv3: scripts/pmc_cycle.sh)
+export FAMG_DENSE_TAIL=0
 mkdir -p gpurun_out
 i=0
 for pmc in "SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_LDS SQ_BUSY_CYCLES SQ_WAVES" \
